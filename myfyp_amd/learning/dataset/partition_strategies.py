@@ -1,0 +1,192 @@
+"""Partition strategies (parity: ``p2pfl/learning/dataset/partition_strategies.py:29-436``).
+
+* ``RandomIIDPartitionStrategy`` — seeded shuffle, near-equal contiguous split (first ``remainder``
+  partitions get one extra sample), same index semantics as the reference.
+* ``DirichletPartitionStrategy`` — per-class Dirichlet(α) proportions with optional self-balancing
+  and a minimum partition size (retry up to ``max_tries``).
+* ``LabelSkewedPartitionStrategy`` and ``PercentageBasedNonIIDPartitionStrategy`` — left as
+  ``NotImplementedError`` in the reference; implemented here (sort-by-label shards / per-node
+  dominant-class percentage).
+
+Strategies operate on label arrays (numpy), not on row-by-row Python loops, so partitioning a
+60k-sample dataset is a few milliseconds.
+"""
+
+from __future__ import annotations
+
+import random
+from abc import ABC, abstractmethod
+from typing import Any, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+
+def _labels(data: Any, label_tag: str) -> np.ndarray:
+    if isinstance(data, dict):
+        return np.asarray(data[label_tag])
+    return np.asarray(data[label_tag])
+
+
+class DataPartitionStrategy(ABC):
+    """Returns ``(train_partition_indices, test_partition_indices)``."""
+
+    @staticmethod
+    @abstractmethod
+    def generate_partitions(train_data: Any, test_data: Any, num_partitions: int, seed: int = 666, **kwargs) -> Tuple[List[List[int]], List[List[int]]]: ...
+
+
+class RandomIIDPartitionStrategy(DataPartitionStrategy):
+    """IID random split."""
+
+    @staticmethod
+    def generate_partitions(train_data: Any, test_data: Any, num_partitions: int, seed: int = 666, **kwargs) -> Tuple[List[List[int]], List[List[int]]]:
+        return (
+            RandomIIDPartitionStrategy.partition_data(len(train_data), seed, num_partitions),
+            RandomIIDPartitionStrategy.partition_data(len(test_data), seed, num_partitions),
+        )
+
+    @staticmethod
+    def partition_data(n: int, seed: int, num_partitions: int) -> List[List[int]]:
+        indices = list(range(n))
+        random.Random(seed).shuffle(indices)
+        per, rem = divmod(n, num_partitions)
+        return [indices[i * per + min(i, rem) : (i + 1) * per + min(i + 1, rem)] for i in range(num_partitions)]
+
+
+class LabelSkewedPartitionStrategy(DataPartitionStrategy):
+    """Sort by label, cut into ``shards_per_partition·num_partitions`` shards, deal shards randomly
+    (McMahan et al. pathological non-IID)."""
+
+    @staticmethod
+    def generate_partitions(
+        train_data: Any, test_data: Any, num_partitions: int, seed: int = 666, label_tag: str = "label", shards_per_partition: int = 2, **kwargs
+    ) -> Tuple[List[List[int]], List[List[int]]]:
+        rng = np.random.default_rng(seed)
+
+        def split(data: Any) -> List[List[int]]:
+            y = _labels(data, label_tag)
+            order = np.argsort(y, kind="stable")
+            shards = np.array_split(order, num_partitions * shards_per_partition)
+            perm = rng.permutation(len(shards))
+            return [sorted(np.concatenate([shards[j] for j in perm[i::num_partitions]]).tolist()) for i in range(num_partitions)]
+
+        return split(train_data), split(test_data)
+
+
+class PercentageBasedNonIIDPartitionStrategy(DataPartitionStrategy):
+    """Each partition draws ``percentage`` of its samples from one dominant class and the rest IID."""
+
+    @staticmethod
+    def generate_partitions(
+        train_data: Any, test_data: Any, num_partitions: int, seed: int = 666, label_tag: str = "label", percentage: float = 0.8, **kwargs
+    ) -> Tuple[List[List[int]], List[List[int]]]:
+        rng = np.random.default_rng(seed)
+
+        def split(data: Any) -> List[List[int]]:
+            y = _labels(data, label_tag)
+            classes = np.unique(y)
+            pools = {c: list(rng.permutation(np.nonzero(y == c)[0])) for c in classes}
+            size = len(y) // num_partitions
+            out: List[List[int]] = []
+            for i in range(num_partitions):
+                dom = classes[i % len(classes)]
+                take = min(int(size * percentage), len(pools[dom]))
+                part = [pools[dom].pop() for _ in range(take)]
+                rest = [idx for c in classes for idx in pools[c]]
+                rng.shuffle(rest)
+                need = size - len(part)
+                chosen = set(rest[:need])
+                for c in classes:
+                    pools[c] = [j for j in pools[c] if j not in chosen]
+                out.append(sorted(part + list(chosen)))
+            return out
+
+        return split(train_data), split(test_data)
+
+
+class DirichletPartitionStrategy(DataPartitionStrategy):
+    """Per-class Dirichlet(α) proportions (flwr-style, reference ``partition_strategies.py:161-430``)."""
+
+    @staticmethod
+    def _preprocess_alpha(alpha: Union[int, float, List[float]], num_partitions: int) -> List[float]:
+        if isinstance(alpha, (int, float)):
+            alpha = [float(alpha)] * num_partitions
+        elif isinstance(alpha, list):
+            if len(alpha) != num_partitions:
+                raise ValueError("If passing alpha as a List, it needs to be of length of equal to num_partitions.")
+            alpha = [float(a) for a in alpha]
+        else:
+            raise ValueError("The given alpha format is not supported.")
+        if not all(a > 0 for a in alpha):
+            raise ValueError(f"Alpha values should be strictly greater than zero: {alpha}")
+        return alpha
+
+    @staticmethod
+    def _generate_proportions(
+        num_partitions: int,
+        class_props: np.ndarray,
+        min_partition_proportion: float,
+        alpha: Sequence[float],
+        rng: np.random.Generator,
+        balancing: bool,
+        max_tries: int = 10,
+    ) -> np.ndarray:
+        """``[num_classes, num_partitions]`` division proportions (rows sum to 1)."""
+        if not np.isclose(class_props.sum(), 1.0):
+            raise ValueError("The sum of the class proportions must be 1")
+        for _ in range(max_tries):
+            result = np.zeros((len(class_props), num_partitions))
+            active = np.ones(num_partitions, dtype=bool)
+            for ci in range(len(class_props)):
+                props = rng.dirichlet(alpha)
+                if balancing:
+                    props = props * active
+                    props = props / props.sum() if props.sum() > 0 else np.full(num_partitions, 1.0 / num_partitions)
+                result[ci] = props
+                if balancing:
+                    assigned = (class_props[:, None] * result).sum(0)
+                    active = assigned < 1.0 / num_partitions
+            assigned = (class_props[:, None] * result).sum(0)
+            if assigned.min() >= min_partition_proportion:
+                return result
+        raise ValueError("Could not find a valid partitioning after max_tries. Try with other parameters.")
+
+    @classmethod
+    def _partition_data(
+        cls, data: Any, label_tag: str, num_partitions: int, min_partition_size: int, alpha: Sequence[float], rng: np.random.Generator, balancing: bool
+    ) -> List[List[int]]:
+        y = _labels(data, label_tag)
+        classes, counts = np.unique(y, return_counts=True)
+        props = cls._generate_proportions(num_partitions, counts / counts.sum(), min_partition_size / len(y), alpha, rng, balancing)
+        result: List[List[int]] = [[] for _ in range(num_partitions)]
+        for ci, c in enumerate(classes):
+            idx = np.nonzero(y == c)[0]
+            rng.shuffle(idx)
+            cuts = np.round(np.cumsum(props[ci]) * len(idx)).astype(int)
+            start = 0
+            for p, end in enumerate(cuts):
+                result[p].extend(idx[start:end].tolist())
+                start = end
+        return result
+
+    @classmethod
+    def generate_partitions(
+        cls,
+        train_data: Any,
+        test_data: Any,
+        num_partitions: int,
+        seed: int = 666,
+        label_tag: str = "label",
+        alpha: Union[int, float, List[float]] = 1,
+        min_partition_size: int = 2,
+        self_balancing: bool = False,
+        **kwargs,
+    ) -> Tuple[List[List[int]], List[List[int]]]:
+        alpha = cls._preprocess_alpha(alpha, num_partitions)
+        if num_partitions > min(len(train_data), len(test_data)):
+            raise ValueError("More partitions than samples")
+        rng = np.random.default_rng(seed=seed)
+        return (
+            cls._partition_data(train_data, label_tag, num_partitions, min_partition_size, alpha, rng, self_balancing),
+            cls._partition_data(test_data, label_tag, num_partitions, min_partition_size, alpha, rng, self_balancing),
+        )

@@ -1,0 +1,138 @@
+"""Framework-neutral model wrapper and the wire/checkpoint format.
+
+Parity: ``p2pfl/learning/frameworks/p2pfl_model.py:30-195``. The serialized format is unchanged:
+``pickle.dumps({"params": List[np.ndarray] (state_dict order), "additional_info": {...}})`` so peers
+and checkpoints interoperate with the reference. Decoding uses a restricted unpickler that only
+materialises numpy arrays and plain containers (no arbitrary code execution from the network).
+"""
+
+from __future__ import annotations
+
+import copy
+import io
+import pickle
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from myfyp_amd.learning.frameworks.exceptions import DecodingParamsError
+
+_SAFE_GLOBALS = {
+    ("numpy", "ndarray"),
+    ("numpy", "dtype"),
+    ("numpy.core.multiarray", "_reconstruct"),
+    ("numpy._core.multiarray", "_reconstruct"),
+    ("numpy.core.multiarray", "scalar"),
+    ("numpy._core.multiarray", "scalar"),
+    ("numpy.core.numeric", "_frombuffer"),
+    ("numpy._core.numeric", "_frombuffer"),
+    ("builtins", "complex"),
+    ("builtins", "bytearray"),
+    ("collections", "OrderedDict"),
+}
+
+
+class _SafeUnpickler(pickle.Unpickler):
+    def find_class(self, module: str, name: str) -> Any:
+        if (module, name) in _SAFE_GLOBALS or (module.startswith("numpy") and name.endswith("DType")):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"Refusing to unpickle {module}.{name}")
+
+
+def safe_loads(data: bytes) -> Any:
+    """Unpickle model payloads allowing only numpy arrays and builtin containers."""
+    return _SafeUnpickler(io.BytesIO(data)).load()
+
+
+class P2PFLModel:
+    """Holds parameters (as numpy on the wire), contributors, sample count and callback info."""
+
+    def __init__(
+        self,
+        model: Any,
+        params: Optional[Union[List[np.ndarray], bytes]] = None,
+        num_samples: Optional[int] = None,
+        contributors: Optional[List[str]] = None,
+        additional_info: Optional[Dict[str, Any]] = None,
+    ) -> None:
+        self.model = model
+        self.contributors: List[str] = list(contributors) if contributors is not None else []
+        self.num_samples: int = num_samples if num_samples is not None else 0
+        self.additional_info: Dict[str, Any] = additional_info if additional_info is not None else {}
+        if params is not None:
+            self.set_parameters(params)
+
+    def get_model(self) -> Any:
+        return self.model
+
+    # ------------------------------------------------------------------ wire format
+    def encode_parameters(self, params: Optional[List[np.ndarray]] = None) -> bytes:
+        if params is None:
+            params = self.get_parameters()
+        return pickle.dumps({"params": params, "additional_info": self.additional_info})
+
+    def decode_parameters(self, data: bytes) -> Tuple[List[np.ndarray], Dict[str, Any]]:
+        try:
+            loaded = safe_loads(data)
+            return loaded["params"], loaded["additional_info"]
+        except Exception as e:
+            raise DecodingParamsError("Error decoding parameters") from e
+
+    # ------------------------------------------------------------------ parameters
+    def get_parameters(self) -> List[np.ndarray]:
+        raise NotImplementedError
+
+    def set_parameters(self, params: Union[List[np.ndarray], bytes]) -> None:
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ info / contribution
+    def add_info(self, callback: str, info: Any) -> None:
+        self.additional_info[callback] = info
+
+    def get_info(self, callback: Optional[str] = None) -> Any:
+        if callback is None:
+            return self.additional_info
+        return self.additional_info[callback]
+
+    def set_contribution(self, contributors: List[str], num_samples: int) -> None:
+        self.contributors = list(contributors)
+        self.num_samples = num_samples
+
+    def get_contributors(self) -> List[str]:
+        if not self.contributors:
+            raise ValueError("Contributors are empty")
+        return self.contributors
+
+    def get_num_samples(self) -> int:
+        if self.num_samples == 0:
+            raise ValueError("Number of samples required")
+        return self.num_samples
+
+    def build_copy(self, **kwargs) -> "P2PFLModel":
+        return self.__class__(copy.deepcopy(self.model), **kwargs)
+
+    def get_framework(self) -> str:
+        raise NotImplementedError
+
+
+class NumpyModel(P2PFLModel):
+    """Parameter-only model (aggregation math, interop with non-PyTorch peers, tests)."""
+
+    def __init__(self, model: Any = None, params=None, **kwargs) -> None:
+        self._params: List[np.ndarray] = []
+        super().__init__(model, params=params, **kwargs)
+
+    def get_parameters(self) -> List[np.ndarray]:
+        return self._params
+
+    def set_parameters(self, params: Union[List[np.ndarray], bytes]) -> None:
+        if isinstance(params, bytes):
+            params, info = self.decode_parameters(params)
+            self.additional_info.update(info)
+        self._params = [np.asarray(p) for p in params]
+
+    def build_copy(self, **kwargs) -> "P2PFLModel":
+        return NumpyModel(None, **kwargs)
+
+    def get_framework(self) -> str:
+        return "numpy"

@@ -1,0 +1,98 @@
+"""Aggregator-required client callbacks for the PyTorch-ROCm learners.
+
+Both work on the learner's flat parameter buffer and hand the optimizer kernel extra read streams
+instead of editing gradients in Python:
+
+* ``SCAFFOLDCallback`` (parity target: ``pytorch/callbacks/scaffold_callback.py:32-150``). The
+  reference adds ``lr·(c_i − c)`` to ``param.grad`` of *detached state_dict copies*, so its
+  correction is a no-op. Here the optimizer really uses ``g − c_i + c`` and the
+  control variate follows SCAFFOLD option II: ``c_i⁺ = c_i − c + (x − y)/(K·η)``.
+* ``FedProxCallback``: proximal term ``μ(w − w_global)`` with ``w_global`` snapshotted at fit start.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from myfyp_amd.learning.frameworks.callback import P2PFLCallback
+from myfyp_amd.learning.frameworks.callback_factory import CallbackFactory
+
+
+class TorchCallback(P2PFLCallback):
+    """Hook points used by the torch learners."""
+
+    def on_train_start(self, learner) -> None: ...
+
+    def grad_correction(self) -> Dict[str, Any]:
+        return {}
+
+    def on_train_end(self, learner, steps: int, lr: float) -> None: ...
+
+
+def _flat_to_list(flat: torch.Tensor, learner) -> list:
+    return [v.detach().cpu().numpy().copy() for v in learner.split_flat(flat)]
+
+
+def _list_to_flat(arrs, like: torch.Tensor) -> torch.Tensor:
+    return torch.cat([torch.as_tensor(np.asarray(a), dtype=torch.float32).reshape(-1) for a in arrs]).to(like.device)
+
+
+class SCAFFOLDCallback(TorchCallback):
+    """Client side of SCAFFOLD."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.c_i: Optional[torch.Tensor] = None
+        self.c: Optional[torch.Tensor] = None
+        self.x0: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def get_name() -> str:
+        return "scaffold"
+
+    def on_train_start(self, learner) -> None:
+        flat = learner.flat_params()
+        if self.c_i is None or self.c_i.numel() != flat.numel():
+            self.c_i = torch.zeros_like(flat)
+        g = self.additional_info.get("global_c")
+        self.c = _list_to_flat(g, flat) if g is not None else torch.zeros_like(flat)
+        self.x0 = flat.detach().clone()
+
+    def grad_correction(self) -> Dict[str, Any]:
+        return {"c_global": self.c, "c_local": self.c_i}
+
+    def on_train_end(self, learner, steps: int, lr: float) -> None:
+        assert self.x0 is not None and self.c_i is not None and self.c is not None
+        y = learner.flat_params().detach()
+        k = max(1, steps)
+        c_new = self.c_i - self.c + (self.x0 - y) / (k * lr)
+        delta_c = c_new - self.c_i
+        self.c_i = c_new
+        self.additional_info["delta_y_i"] = _flat_to_list(y - self.x0, learner)
+        self.additional_info["delta_c_i"] = _flat_to_list(delta_c, learner)
+
+
+class FedProxCallback(TorchCallback):
+    """Client side of FedProx."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.anchor: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def get_name() -> str:
+        return "fedprox"
+
+    def on_train_start(self, learner) -> None:
+        self.anchor = learner.flat_params().detach().clone()
+
+    def grad_correction(self) -> Dict[str, Any]:
+        return {"anchor": self.anchor, "mu": float(self.additional_info.get("mu", 0.01))}
+
+
+for _fw in ("pytorch", "rocm"):
+    CallbackFactory.register_callback(_fw, SCAFFOLDCallback)
+    CallbackFactory.register_callback(_fw, FedProxCallback)

@@ -1,0 +1,225 @@
+"""Fused device ops (HIP, gfx950) with PyTorch reference implementations for CPU hosts.
+
+Every op takes/returns torch tensors. Device tensors go to the hand-written kernels in
+``csrc/kernels`` (through :mod:`myfyp_amd.ops._native`); CPU tensors use the reference math below,
+which is also the numerics oracle in ``tests/test_kernels_gpu.py``.
+
+Ops
+---
+* ``weighted_average``  — FedAvg reduction over K models (multi-tensor, one launch per layer list)
+* ``stacked_weighted_sum`` / ``broadcast_rows`` — reductions over a ``[P, N]`` stacked flat buffer
+  (co-located peers) feeding / consuming the RCCL all-reduce
+* ``coordinate_median`` — FedMedian (register sorting network, K ≤ 16)
+* ``adam_step`` / ``sgd_step`` — fused optimizers over a flat buffer, optionally with the FedProx
+  proximal term and the SCAFFOLD control-variate correction fused in (K5, K8, K13)
+* ``scale_add_noise`` — attack injection (sign flip / Gaussian noise, K14)
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from myfyp_amd.ops import _native
+
+__all__ = [
+    "weighted_average",
+    "stacked_weighted_sum",
+    "broadcast_rows",
+    "coordinate_median",
+    "adam_step",
+    "sgd_step",
+    "scale_add_noise",
+    "native_available",
+]
+
+
+def native_available() -> bool:
+    return _native.available()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _lib():
+    return _native.load(required=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# aggregation
+# ---------------------------------------------------------------------------------------------
+def weighted_average(param_lists: Sequence[Sequence[torch.Tensor]], norm_weights: Sequence[float]) -> List[torch.Tensor]:
+    """``out[l] = Σ_k w_k · params[k][l]`` (weights already normalised)."""
+    k = len(param_lists)
+    out: List[torch.Tensor] = []
+    dev = param_lists[0][0].device
+    if dev.type != "cuda":
+        for layer in range(len(param_lists[0])):
+            acc = torch.zeros_like(param_lists[0][layer], dtype=torch.float64)
+            for p, w in zip(param_lists, norm_weights):
+                acc += p[layer].double() * w
+            out.append(acc.to(param_lists[0][layer].dtype))
+        return out
+    lib = _lib()
+    w = torch.tensor(list(norm_weights), dtype=torch.float32, device=dev)
+    for layer in range(len(param_lists[0])):
+        srcs = [p[layer].contiguous().float() for p in param_lists]
+        dst = torch.empty_like(srcs[0])
+        ptrs = torch.tensor([s.data_ptr() for s in srcs], dtype=torch.int64, device=dev)
+        _native.check(lib.myfyp_weighted_sum(dst.data_ptr(), ptrs.data_ptr(), w.data_ptr(), k, dst.numel(), _stream()), "weighted_sum")
+        out.append(dst.to(param_lists[0][layer].dtype))
+    return out
+
+
+def stacked_weighted_sum(stacked: torch.Tensor, weights: torch.Tensor, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """``out[n] = scale · Σ_p weights[p] · stacked[p, n]`` for a ``[P, N]`` fp32 buffer."""
+    if stacked.device.type != "cuda":
+        out.copy_((weights.view(-1, 1).to(stacked.dtype) * stacked).sum(0) * scale)
+        return out
+    lib = _lib()
+    p, n = stacked.shape
+    _native.check(
+        lib.myfyp_stacked_weighted_sum(out.data_ptr(), stacked.data_ptr(), p, n, stacked.stride(0), weights.data_ptr(), float(scale), _stream()),
+        "stacked_weighted_sum",
+    )
+    return out
+
+
+def broadcast_rows(src: torch.Tensor, stacked: torch.Tensor, mask: Optional[torch.Tensor] = None, shadow: Optional[torch.Tensor] = None) -> None:
+    """``stacked[p, :] = src`` for every row p with ``mask[p] != 0`` (and the bf16 shadow copy)."""
+    if stacked.device.type != "cuda":
+        rows = range(stacked.shape[0]) if mask is None else [i for i in range(stacked.shape[0]) if float(mask[i]) != 0]
+        for r in rows:
+            stacked[r].copy_(src)
+            if shadow is not None:
+                shadow[r].copy_(src.to(shadow.dtype))
+        return
+    lib = _lib()
+    p, n = stacked.shape
+    _native.check(lib.myfyp_broadcast_rows(stacked.data_ptr(), src.data_ptr(), p, n, stacked.stride(0), _ptr(mask), _stream()), "broadcast_rows")
+    if shadow is not None:
+        shadow.copy_(stacked.to(shadow.dtype))
+
+
+def coordinate_median(param_lists: Sequence[Sequence[torch.Tensor]]) -> List[torch.Tensor]:
+    k = len(param_lists)
+    out: List[torch.Tensor] = []
+    dev = param_lists[0][0].device
+    if dev.type != "cuda" or k > 16:
+        for layer in range(len(param_lists[0])):
+            st = torch.stack([p[layer].float() for p in param_lists])
+            s, _ = torch.sort(st, dim=0)
+            med = s[(k - 1) // 2] if k % 2 else 0.5 * (s[k // 2 - 1] + s[k // 2])
+            out.append(med.to(param_lists[0][layer].dtype))
+        return out
+    lib = _lib()
+    for layer in range(len(param_lists[0])):
+        srcs = [p[layer].contiguous().float() for p in param_lists]
+        dst = torch.empty_like(srcs[0])
+        ptrs = torch.tensor([s.data_ptr() for s in srcs], dtype=torch.int64, device=dev)
+        _native.check(lib.myfyp_coordinate_median(dst.data_ptr(), ptrs.data_ptr(), k, dst.numel(), _stream()), "coordinate_median")
+        out.append(dst.to(param_lists[0][layer].dtype))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# optimizers (flat fp32 buffers)
+# ---------------------------------------------------------------------------------------------
+def _corrected_grad(param, grad, anchor, c_global, c_local, mu):
+    g = grad
+    if anchor is not None and mu != 0.0:
+        g = g + mu * (param - anchor)
+    if c_global is not None and c_local is not None:
+        g = g + (c_global - c_local)
+    return g
+
+
+def adam_step(
+    param: torch.Tensor,
+    grad: torch.Tensor,
+    exp_avg: torch.Tensor,
+    exp_avg_sq: torch.Tensor,
+    step: int,
+    lr: float = 1e-3,
+    beta1: float = 0.9,
+    beta2: float = 0.999,
+    eps: float = 1e-8,
+    weight_decay: float = 0.0,
+    shadow: Optional[torch.Tensor] = None,
+    anchor: Optional[torch.Tensor] = None,
+    c_global: Optional[torch.Tensor] = None,
+    c_local: Optional[torch.Tensor] = None,
+    mu: float = 0.0,
+) -> None:
+    """One Adam step (torch.optim.Adam semantics, L2 ``weight_decay``), in place, step ≥ 1."""
+    if param.device.type != "cuda":
+        g = _corrected_grad(param, grad, anchor, c_global, c_local, mu)
+        if weight_decay:
+            g = g + weight_decay * param
+        exp_avg.mul_(beta1).add_(g, alpha=1 - beta1)
+        exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        bc1 = 1 - beta1**step
+        bc2 = 1 - beta2**step
+        denom = (exp_avg_sq / bc2).sqrt_().add_(eps)
+        param.addcdiv_(exp_avg, denom, value=-lr / bc1)
+        if shadow is not None:
+            shadow.copy_(param.to(shadow.dtype))
+        return
+    lib = _lib()
+    _native.check(
+        lib.myfyp_adam_step(
+            param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), _ptr(shadow), param.numel(),
+            lr, beta1, beta2, eps, weight_decay, int(step), _ptr(anchor), _ptr(c_global), _ptr(c_local), float(mu), _stream(),
+        ),
+        "adam_step",
+    )
+
+
+def sgd_step(
+    param: torch.Tensor,
+    grad: torch.Tensor,
+    momentum_buf: Optional[torch.Tensor],
+    lr: float,
+    momentum: float = 0.0,
+    weight_decay: float = 0.0,
+    nesterov: bool = False,
+    anchor: Optional[torch.Tensor] = None,
+    c_global: Optional[torch.Tensor] = None,
+    c_local: Optional[torch.Tensor] = None,
+    mu: float = 0.0,
+) -> None:
+    """One SGD(+momentum, +nesterov) step (torch.optim.SGD semantics; buffer starts at 0)."""
+    if param.device.type != "cuda":
+        g = _corrected_grad(param, grad, anchor, c_global, c_local, mu)
+        if weight_decay:
+            g = g + weight_decay * param
+        if momentum != 0.0 and momentum_buf is not None:
+            momentum_buf.mul_(momentum).add_(g)
+            g = g + momentum * momentum_buf if nesterov else momentum_buf
+        param.add_(g, alpha=-lr)
+        return
+    lib = _lib()
+    _native.check(
+        lib.myfyp_sgd_step(
+            param.data_ptr(), grad.data_ptr(), _ptr(momentum_buf), param.numel(), lr, momentum, weight_decay, int(nesterov),
+            _ptr(anchor), _ptr(c_global), _ptr(c_local), float(mu), _stream(),
+        ),
+        "sgd_step",
+    )
+
+
+def scale_add_noise(t: torch.Tensor, scale: float, sigma: float, seed: int = 0) -> None:
+    """``t = scale·t + σ·N(0,1)`` in place (sign flip: scale=-1, σ=0)."""
+    if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        noise = torch.randn(t.shape, generator=g, dtype=torch.float32).to(t.device, t.dtype) if sigma else 0.0
+        t.mul_(scale).add_(noise * sigma if sigma else 0.0)
+        return
+    lib = _lib()
+    _native.check(lib.myfyp_scale_add_noise(t.data_ptr(), t.numel(), float(scale), float(sigma), int(seed), _stream()), "scale_add_noise")

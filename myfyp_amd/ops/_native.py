@@ -1,0 +1,101 @@
+"""Loader for the in-tree native library ``myfyp_amd/_native/libmyfyp_hip.so``.
+
+The library is plain C ABI (HIP kernels + the C++ runtime: grouped MLP engine, hipGraph capture),
+called through ``ctypes`` with raw device pointers and the caller's HIP stream — no PyTorch C++
+ABI coupling, no hipify. ``build()`` in ``__graft_entry__.py`` / ``python -m myfyp_amd.ops.build``
+compiles it for gfx950.
+
+Policy: on a machine with a GPU the native library is REQUIRED for device tensors (ops raise if it
+is missing — a silent eager fallback would hide a broken build); on CPU-only hosts the PyTorch
+reference implementations in :mod:`myfyp_amd.ops` run instead.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_LIB: Optional[ctypes.CDLL] = None
+_LOCK = threading.Lock()
+_ERR: Optional[str] = None
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+LIB_PATH = os.path.join(LIB_DIR, "libmyfyp_hip.so")
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "myfyp_version": (c_int, []),
+    "myfyp_last_error": (ctypes.c_char_p, []),
+    # aggregation
+    "myfyp_weighted_sum": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "myfyp_stacked_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_float, c_void_p]),
+    "myfyp_broadcast_rows": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "myfyp_coordinate_median": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    # optimizers over flat buffers
+    "myfyp_adam_step": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+    ),
+    "myfyp_sgd_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
+    # attacks / elementwise
+    "myfyp_scale_add_noise": (c_int, [c_void_p, c_int64, c_float, c_float, ctypes.c_uint64, c_void_p]),
+    # grouped MLP engine
+    "mlp_engine_create": (c_void_p, [c_int, c_int, c_void_p, c_int, c_int]),
+    "mlp_engine_destroy": (None, [c_void_p]),
+    "mlp_engine_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64]),
+    "mlp_engine_set_optimizer": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float, c_float, c_float]),
+    "mlp_engine_set_extras": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float]),
+    "mlp_engine_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "mlp_engine_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_forward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "mlp_engine_reset_graphs": (None, [c_void_p]),
+}
+
+
+def load(required: bool = False) -> Optional[ctypes.CDLL]:
+    """Return the native library (loading it once). ``required`` raises if unavailable."""
+    global _LIB, _ERR
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is None and _ERR is None:
+            if not os.path.exists(LIB_PATH):
+                _ERR = f"native library not built: {LIB_PATH} (run python -m myfyp_amd.ops.build)"
+            else:
+                try:
+                    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+                    for name, (res, args) in _SIGNATURES.items():
+                        fn = getattr(lib, name, None)
+                        if fn is None:
+                            continue
+                        fn.restype = res
+                        fn.argtypes = args
+                    _LIB = lib
+                except OSError as e:
+                    _ERR = f"failed to load {LIB_PATH}: {e}"
+    if _LIB is None and required:
+        raise RuntimeError(_ERR or "native library unavailable")
+    return _LIB
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def error() -> Optional[str]:
+    load()
+    return _ERR
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _LIB.myfyp_last_error().decode() if _LIB is not None else "?"
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")

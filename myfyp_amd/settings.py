@@ -1,0 +1,197 @@
+"""Global, mutable framework settings.
+
+Parity with the reference ``Settings`` class (``p2pfl/settings.py:28-153``): every flat
+attribute keeps its name and default so existing experiment scripts keep working.
+
+Additions (MI355X-first):
+
+* nested groups (``Settings.general.SEED``, ``Settings.training.BATCH_SIZE`` ...) that alias the
+  flat names — the FYP scripts use the nested API (``exp_SAVE3.txt:74``);
+* device/engine knobs for the GPU data plane (batch size, compute dtype, grouped peers);
+* a YAML/JSON experiment loader (``Settings.from_yaml``) — the reference has none.
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Any, Dict
+
+_CERT_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "certificates")
+
+
+class _Group:
+    """A nested settings group whose attributes alias flat ``Settings`` attributes."""
+
+    def __init__(self, mapping: Dict[str, str]) -> None:
+        object.__setattr__(self, "_mapping", mapping)
+
+    def __getattr__(self, name: str) -> Any:
+        mapping = object.__getattribute__(self, "_mapping")
+        if name in mapping:
+            return getattr(Settings, mapping[name])
+        raise AttributeError(name)
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        mapping = object.__getattribute__(self, "_mapping")
+        if name not in mapping:
+            raise AttributeError(f"Unknown setting {name!r}")
+        setattr(Settings, mapping[name], value)
+
+    def __dir__(self):  # pragma: no cover - convenience
+        return list(object.__getattribute__(self, "_mapping"))
+
+
+class Settings:
+    """Class-level global settings (mutated at runtime, like the reference)."""
+
+    # ---------------- GENERAL (p2pfl/settings.py:34-50)
+    GRPC_TIMEOUT: float = 10
+    LOG_LEVEL: str = "INFO"
+    LOG_DIR: str = "logs"
+    EXCLUDE_BEAT_LOGS: bool = True
+    DISABLE_RAY: bool = True  # Ray is replaced by the device pool; kept for API compatibility.
+    SEED: int | None = None
+
+    # ---------------- HEARTBEAT (p2pfl/settings.py:58-62)
+    HEARTBEAT_PERIOD: float = 2
+    HEARTBEAT_TIMEOUT: float = 5
+
+    # ---------------- GOSSIP (p2pfl/settings.py:70-94)
+    GOSSIP_PERIOD: float = 0.1
+    TTL: int = 10
+    GOSSIP_MESSAGES_PER_PERIOD: int = 100
+    AMOUNT_LAST_MESSAGES_SAVED: int = 100
+    GOSSIP_MODELS_PERIOD: float = 1
+    GOSSIP_MODELS_PER_ROUND: int = 2
+    GOSSIP_EXIT_ON_X_EQUAL_ROUNDS: int = 10
+
+    # ---------------- SSL (p2pfl/settings.py:102-125)
+    USE_SSL: bool = False
+    CA_CRT: str = f"{_CERT_DIR}/ca.crt"
+    SERVER_CRT: str = f"{_CERT_DIR}/server.crt"
+    CLIENT_CRT: str = f"{_CERT_DIR}/client.crt"
+    SERVER_KEY: str = f"{_CERT_DIR}/server.key"
+    CLIENT_KEY: str = f"{_CERT_DIR}/client.key"
+
+    # ---------------- TRAINING (p2pfl/settings.py:130-142)
+    TRAIN_SET_SIZE: int = 4
+    VOTE_TIMEOUT: float = 60
+    AGGREGATION_TIMEOUT: float = 300
+    WAIT_HEARTBEATS_CONVERGENCE: float = 0.2 * HEARTBEAT_TIMEOUT
+
+    # ---------------- WEB (p2pfl/settings.py:150)
+    RESOURCE_MONITOR_PERIOD: float = 1
+
+    # ---------------- DEVICE / ENGINE (new: MI355X data plane)
+    DEVICE: str = "auto"  # "auto" -> cuda if available else cpu
+    BATCH_SIZE: int = 1  # reference default (lightning_dataset.py:81); benchmarks override it
+    COMPUTE_DTYPE: str = "bf16"  # GEMM operand dtype on the GPU (fp32 master weights)
+    USE_FUSED_KERNELS: bool = True  # hand-written HIP path when the extension is present
+    GROUP_PEERS: bool = True  # train co-located peers in one grouped launch
+    GANG_WINDOW: float = 0.05  # seconds a grouped fit waits for expected co-located peers
+    COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
+    BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
+
+    # nested aliases (FYP scripts: Settings.general.SEED)
+    general = _Group(
+        {
+            "SEED": "SEED",
+            "GRPC_TIMEOUT": "GRPC_TIMEOUT",
+            "LOG_LEVEL": "LOG_LEVEL",
+            "LOG_DIR": "LOG_DIR",
+            "EXCLUDE_BEAT_LOGS": "EXCLUDE_BEAT_LOGS",
+            "DISABLE_RAY": "DISABLE_RAY",
+        }
+    )
+    heartbeat = _Group({"PERIOD": "HEARTBEAT_PERIOD", "TIMEOUT": "HEARTBEAT_TIMEOUT", "WAIT_CONVERGENCE": "WAIT_HEARTBEATS_CONVERGENCE"})
+    gossip = _Group(
+        {
+            "PERIOD": "GOSSIP_PERIOD",
+            "TTL": "TTL",
+            "MESSAGES_PER_PERIOD": "GOSSIP_MESSAGES_PER_PERIOD",
+            "AMOUNT_LAST_MESSAGES_SAVED": "AMOUNT_LAST_MESSAGES_SAVED",
+            "MODELS_PERIOD": "GOSSIP_MODELS_PERIOD",
+            "MODELS_PER_ROUND": "GOSSIP_MODELS_PER_ROUND",
+            "EXIT_ON_X_EQUAL_ROUNDS": "GOSSIP_EXIT_ON_X_EQUAL_ROUNDS",
+        }
+    )
+    ssl = _Group(
+        {
+            "USE_SSL": "USE_SSL",
+            "CA_CRT": "CA_CRT",
+            "SERVER_CRT": "SERVER_CRT",
+            "CLIENT_CRT": "CLIENT_CRT",
+            "SERVER_KEY": "SERVER_KEY",
+            "CLIENT_KEY": "CLIENT_KEY",
+        }
+    )
+    training = _Group(
+        {
+            "TRAIN_SET_SIZE": "TRAIN_SET_SIZE",
+            "VOTE_TIMEOUT": "VOTE_TIMEOUT",
+            "AGGREGATION_TIMEOUT": "AGGREGATION_TIMEOUT",
+            "BATCH_SIZE": "BATCH_SIZE",
+        }
+    )
+    device = _Group(
+        {
+            "DEVICE": "DEVICE",
+            "COMPUTE_DTYPE": "COMPUTE_DTYPE",
+            "USE_FUSED_KERNELS": "USE_FUSED_KERNELS",
+            "GROUP_PEERS": "GROUP_PEERS",
+            "GANG_WINDOW": "GANG_WINDOW",
+            "COLLECTIVE_TIMEOUT": "COLLECTIVE_TIMEOUT",
+            "BUCKET_BYTES": "BUCKET_BYTES",
+        }
+    )
+
+    # ------------------------------------------------------------------ helpers
+    @classmethod
+    def snapshot(cls) -> Dict[str, Any]:
+        """Return all flat settings as a plain dict (checkpoint sidecars, logging)."""
+        out: Dict[str, Any] = {}
+        for k in dir(cls):
+            if k.isupper():
+                v = getattr(cls, k)
+                if isinstance(v, (int, float, str, bool)) or v is None:
+                    out[k] = v
+        return out
+
+    @classmethod
+    def update(cls, values: Dict[str, Any]) -> None:
+        """Apply a dict of settings. Keys may be flat (``HEARTBEAT_PERIOD``) or nested dicts
+        (``{"general": {"SEED": 1}}``)."""
+        for k, v in values.items():
+            group = getattr(cls, k.lower(), None) if isinstance(v, dict) else None
+            if isinstance(group, _Group):
+                for gk, gv in v.items():
+                    setattr(group, gk.upper(), gv)
+                continue
+            key = k.upper()
+            if not hasattr(cls, key):
+                raise KeyError(f"Unknown setting {k!r}")
+            setattr(cls, key, v)
+
+    @classmethod
+    def from_yaml(cls, path: str) -> Dict[str, Any]:
+        """Load an experiment file. The ``settings`` section is applied to ``Settings``; the
+        whole parsed document is returned so callers (CLI) can read the experiment section."""
+        import yaml
+
+        with open(path) as f:
+            doc = yaml.safe_load(f) or {}
+        if "settings" in doc:
+            cls.update(doc["settings"])
+        return doc
+
+
+def resolve_device() -> str:
+    """Resolve ``Settings.DEVICE`` ("auto" → ``cuda`` when a GPU is visible)."""
+    if Settings.DEVICE != "auto":
+        return Settings.DEVICE
+    try:
+        import torch
+
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    except Exception:  # pragma: no cover
+        return "cpu"
