@@ -1,0 +1,203 @@
+"""Headline benchmark: rounds/sec (+ wall-clock to target accuracy) of MNIST-MLP FedAvg with 8 peers.
+
+Metric/config come from BASELINE.json: "rounds/sec + wall-clock-to-target-acc, MNIST MLP FedAvg 8 peers
+at 1/2/4/8 MI355X". One process per GPU (``torchrun``); the 8 peers are split evenly over the N
+ranks (8/N co-located peers per GPU, grouped into each fused launch) — total work is fixed, so the
+scaling mode is "strong". Every timed round is a full federated round through the public Node API
+and the collective stage workflow:
+
+    vote (all-gather) → evaluate (fused fwd) → local epoch (fused fwd+bwd+Adam, hipGraph replay)
+    → FedAvg (weighted local reduction + RCCL all-reduce over xGMI + broadcast) → round bookkeeping
+
+Data: synthetic MNIST-shaped uint8 (60k train / 10k test, IID split, no network), random-init
+weights of the reference MLP (784-256-128-10, Adam lr 1e-3, 1 local epoch). Local batch 64
+(the reference's batch-1 default is a Lightning export default; see BASELINE.md / README).
+
+    python bench.py --gpus 1 --steps 20 --warmup 3
+    torchrun --nproc-per-node 8 bench.py --gpus 8 --steps 20 --warmup 3
+
+Rank 0 prints ONE JSON line. Timing: barrier + device synchronize on both sides of exactly K rounds
+(inside the round-end hook that every rank's gang leader runs after aggregation), MAX over ranks.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rounds/sec + wall-clock-to-target-acc, MNIST MLP FedAvg 8 peers at 1/2/4/8 MI355X"
+# the reference publishes no throughput; its gossip pacing caps it at <= 0.5 rounds/s
+# (gossiper.py:238 sleep sign bug + >=2 model-gossip loops per round). Used as the comparison point.
+BASELINE_ROUNDS_PER_SEC = 0.5
+
+
+def parse() -> argparse.Namespace:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed federated rounds")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed rounds (graph capture, caches)")
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--n-train", type=int, default=60000)
+    ap.add_argument("--n-test", type=int, default=10000)
+    ap.add_argument("--target-acc", type=float, default=0.9)
+    ap.add_argument("--no-fused", action="store_true", help="autograd path instead of the fused HIP engine")
+    ap.add_argument("--eager", action="store_true", help="fused kernels without hipGraph (A/B)")
+    return ap.parse_args()
+
+
+def main() -> None:
+    args = parse()
+    import numpy as np
+    import torch
+
+    from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
+    from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
+    from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
+    from myfyp_amd.learning.frameworks.torch import TorchModel
+    from myfyp_amd.management.logger import logger
+    from myfyp_amd.models import MLP
+    from myfyp_amd.node import Node
+    from myfyp_amd.parallel.federation import Federation
+    from myfyp_amd.settings import Settings
+    from myfyp_amd.utils.seed import set_seed
+    from myfyp_amd.utils.utils import wait_to_finish
+
+    set_seed(1234)
+    Settings.LOG_LEVEL = "WARNING"
+    logger.set_level("WARNING")
+    Settings.HEARTBEAT_PERIOD = 5
+    Settings.HEARTBEAT_TIMEOUT = 600
+    Settings.GOSSIP_PERIOD = 0
+    Settings.TRAIN_SET_SIZE = args.peers  # FedAvg over all 8 peers every round
+    Settings.VOTE_TIMEOUT = 600
+    Settings.AGGREGATION_TIMEOUT = 600
+    Settings.BATCH_SIZE = args.batch_size
+    Settings.USE_FUSED_KERNELS = not args.no_fused
+    Settings.GANG_WINDOW = 5.0
+
+    fed = Federation.init()
+    world, rank = fed.world, fed.rank
+    if args.peers % world:
+        raise SystemExit(f"--peers {args.peers} must be divisible by the number of ranks {world}")
+    ppr = args.peers // world
+    data = synthetic_mnist(args.n_train, args.n_test, seed=2024)
+    parts = data.generate_partitions(args.peers, RandomIIDPartitionStrategy)
+    gids = [rank * ppr + j for j in range(ppr)]
+    nodes = [
+        Node(TorchModel(MLP(seed=100 + g)), parts[g], address=f"peer-{g}", protocol=CollectiveCommunicationProtocol, learner_kwargs={"batch_size": args.batch_size})
+        for g in gids
+    ]
+    for n in nodes:
+        n.start()
+    fed.finalize()
+    if args.eager:
+        for n in nodes:
+            eng = getattr(n.learner, "_engine", None)
+            if eng is not None:
+                eng.group.eager = True
+    fused = all(getattr(n.learner, "_engine", None) is not None for n in nodes)
+
+    total_rounds = args.warmup + args.steps
+    marks: dict = {}
+    round_end: dict = {}
+    dev_sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+
+    def hook(r: int, f) -> None:
+        if r == args.warmup - 1 or (args.warmup == 0 and r == -1):
+            f.barrier()
+            dev_sync()
+            marks["t0"] = time.perf_counter()
+        round_end[r] = time.perf_counter()
+        if r == total_rounds - 1:
+            dev_sync()
+            f.barrier()
+            marks["t1"] = time.perf_counter()
+
+    fed.round_hooks.append(hook)
+    if args.warmup == 0:
+        marks["t0"] = None
+    t_start = time.perf_counter()
+    if rank == 0:
+        nodes[0].set_start_learning(rounds=total_rounds, epochs=args.epochs)
+    if args.warmup == 0:
+        # no warmup: time from the start barrier of round 0 (includes capture)
+        fed.barrier()
+        dev_sync()
+        marks["t0"] = time.perf_counter()
+    wait_to_finish(nodes, timeout=3600)
+    t0, t1 = marks.get("t0"), marks.get("t1")
+    elapsed = (t1 - t0) if (t0 is not None and t1 is not None) else float("nan")
+    # max over ranks
+    if world > 1:
+        import torch.distributed as dist
+
+        dev = fed.device
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # accuracy curve of the local peers: test_metric logged at round r = model after round r-1
+    logs = logger.get_global_logs().get("experiment", {})
+    acc_by_round: dict = {}
+    for n in nodes:
+        for r, v in logs.get(n.addr, {}).get("test_metric", []):
+            acc_by_round.setdefault(r, []).append(v)
+    mean_acc = {r: float(np.mean(v)) for r, v in sorted(acc_by_round.items())}
+    t_target, r_target = None, None
+    for r, a in mean_acc.items():
+        if a >= args.target_acc and r >= 1 and (r - 1) in round_end:
+            t_target, r_target = round_end[r - 1] - t_start, r
+            break
+    final_acc = mean_acc[max(mean_acc)] if mean_acc else None
+    for n in nodes:
+        n.stop()
+
+    rps = args.steps / elapsed if elapsed == elapsed and elapsed > 0 else 0.0
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(rps, 3),
+            "unit": "rounds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / max(1, args.steps), 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(rps / BASELINE_ROUNDS_PER_SEC, 2),
+            "dtype": "bf16" if fused else "fp32",
+            "data": "synthetic (MNIST-shaped uint8 60k/10k, IID over peers), random-init weights",
+            "config": {
+                "model": "MLP 784-256-128-10 (reference MLP)",
+                "global_batch": args.batch_size * args.peers,
+                "local_batch": args.batch_size,
+                "seq_len": None,
+                "parallelism": f"fedavg-{args.peers}peers-dp{world}",
+                "peers": args.peers,
+                "peers_per_gpu": ppr,
+                "train_set_size": args.peers,
+                "epochs_per_round": args.epochs,
+                "optimizer": "adam lr=1e-3 (fresh per round)",
+                "aggregator": "FedAvg (weighted all-reduce)",
+                "engine": "fused-hip" + ("-eager" if args.eager else "-hipgraph") if fused else "autograd",
+            },
+            "time_to_target_s": None if t_target is None else round(t_target, 3),
+            "rounds_to_target": r_target,
+            "target_acc": args.target_acc,
+            "final_test_acc": None if final_acc is None else round(final_acc, 4),
+            "baseline_note": "vs_baseline = value / 0.5 rounds/s: derived ceiling of the reference's gossip pacing (BASELINE.md)",
+        }
+        print(json.dumps(out), flush=True)
+    fed.shutdown()
+
+
+if __name__ == "__main__":
+    main()

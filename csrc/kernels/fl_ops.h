@@ -1,0 +1,12 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "common.h"
+
+void fl_weighted_sum(float* out, const uint64_t* srcs, const float* w, int K, int64_t n, hipStream_t s);
+void fl_stacked_weighted_sum(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w, float scale, hipStream_t s);
+void fl_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64_t ld, const float* mask, hipStream_t s);
+void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s);
+void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
+                 const float* cg, const float* cl, hipStream_t s);
+void fl_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_t seed, hipStream_t s);

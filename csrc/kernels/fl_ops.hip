@@ -1,0 +1,178 @@
+// Federated-learning elementwise/reduction kernels (gfx950): FedAvg reductions, fused optimizers,
+// coordinate median, attack injection. All memory-bound: 16-byte vector accesses, grid-stride,
+// grid capped at 2048 blocks (cdna_hip_programming.md Guideline 11/13).
+#include "common.h"
+#include "fl_ops.h"
+
+#define FL_BLOCK 256
+
+static inline unsigned grid_for(int64_t n_vec) {
+  int64_t g = (n_vec + FL_BLOCK - 1) / FL_BLOCK;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// out[i] = Σ_k w[k] · src_k[i]   (src pointers in a device array)
+__global__ __launch_bounds__(FL_BLOCK) void k_weighted_sum(float* __restrict__ out, const uint64_t* __restrict__ srcs, const float* __restrict__ w, int K,
+                                                            int64_t n) {
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride) {
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(srcs[k])[i];
+      const float wk = w[k];
+      acc.x += wk * v.x; acc.y += wk * v.y; acc.z += wk * v.z; acc.w += wk * v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc += w[k] * reinterpret_cast<const float*>(srcs[k])[i];
+    out[i] = acc;
+  }
+}
+
+// out[i] = scale · Σ_p w[p] · stacked[p*ld + i]   (co-located peers, [P][ld] buffer)
+__global__ __launch_bounds__(FL_BLOCK) void k_stacked_weighted_sum(float* __restrict__ out, const float* __restrict__ stacked, int P, int64_t n, int64_t ld,
+                                                                    const float* __restrict__ w, float scale) {
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  const bool vec = (ld % 4) == 0;
+  if (vec) {
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride) {
+      float4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < P; ++p) {
+        const float wp = w[p];
+        if (wp == 0.f) continue;
+        const float4 v = reinterpret_cast<const float4*>(stacked + p * ld)[i];
+        acc.x += wp * v.x; acc.y += wp * v.y; acc.z += wp * v.z; acc.w += wp * v.w;
+      }
+      acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+      reinterpret_cast<float4*>(out)[i] = acc;
+    }
+  }
+  for (int64_t i = (vec ? n4 * 4 : 0) + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float acc = 0.f;
+    for (int p = 0; p < P; ++p) acc += w[p] * stacked[p * ld + i];
+    out[i] = acc * scale;
+  }
+}
+
+// stacked[p*ld + i] = src[i] for rows with mask[p] != 0 (mask null = all rows)
+__global__ __launch_bounds__(FL_BLOCK) void k_broadcast_rows(float* __restrict__ stacked, const float* __restrict__ src, int P, int64_t n, int64_t ld,
+                                                              const float* __restrict__ mask) {
+  const int p = blockIdx.y;
+  if (mask != nullptr && mask[p] == 0.f) return;
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  float* dst = stacked + p * ld;
+  if ((ld % 4) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride)
+      reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    for (int64_t i = n4 * 4 + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+  } else {
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+// per-coordinate median of K ≤ 16 models: insertion sort in registers
+__global__ __launch_bounds__(FL_BLOCK) void k_coordinate_median(float* __restrict__ out, const uint64_t* __restrict__ srcs, int K, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = k < K ? reinterpret_cast<const float*>(srcs[k])[i] : INFINITY;
+    // branch-free bubble network over 16 slots (padding = +inf sorts last)
+#pragma unroll
+    for (int a = 0; a < 16; ++a) {
+#pragma unroll
+      for (int b = 0; b < 15 - a; ++b) {
+        const float lo = fminf(v[b], v[b + 1]);
+        const float hi = fmaxf(v[b], v[b + 1]);
+        v[b] = lo;
+        v[b + 1] = hi;
+      }
+    }
+    float med;
+    if (K & 1) {
+      med = v[0];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) if (k == (K - 1) / 2) med = v[k];
+    } else {
+      float a0 = v[0], a1 = v[0];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k == K / 2 - 1) a0 = v[k];
+        if (k == K / 2) a1 = v[k];
+      }
+      med = 0.5f * (a0 + a1);
+    }
+    out[i] = med;
+  }
+}
+
+// Fused Adam / SGD over a flat fp32 buffer (torch.optim semantics) + optional FedProx/SCAFFOLD terms
+__global__ __launch_bounds__(FL_BLOCK) void k_opt_step(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ m,
+                                                        float* __restrict__ v, bf16* __restrict__ shadow, int64_t n, OptParams o, float bc1, float bc2s,
+                                                        const float* __restrict__ anchor, const float* __restrict__ cg, const float* __restrict__ cl) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float w = param[i];
+    float mm = m != nullptr ? m[i] : 0.f;
+    float vv = v != nullptr ? v[i] : 0.f;
+    opt_update(o, grad[i], w, mm, vv, bc1, bc2s, anchor, cg, cl, i);
+    param[i] = w;
+    if (m != nullptr) m[i] = mm;
+    if (v != nullptr) v[i] = vv;
+    if (shadow != nullptr) shadow[i] = (bf16)w;
+  }
+}
+
+// t = scale·t + σ·N(0,1), counter-based RNG (splitmix64 + Box-Muller)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(FL_BLOCK) void k_scale_add_noise(float* __restrict__ t, int64_t n, float scale, float sigma, uint64_t seed) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float val = t[i] * scale;
+    if (sigma != 0.f) {
+      const uint64_t r = splitmix64(seed * 0x100000001B3ull + (uint64_t)i);
+      const float u1 = ((r >> 40) + 1) * (1.0f / 16777217.0f);
+      const float u2 = ((r & 0xFFFFFFull)) * (1.0f / 16777216.0f);
+      val += sigma * sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
+    }
+    t[i] = val;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+void fl_weighted_sum(float* out, const uint64_t* srcs, const float* w, int K, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_weighted_sum, dim3(grid_for(n / 4 + 1)), dim3(FL_BLOCK), 0, s, out, srcs, w, K, n);
+}
+void fl_stacked_weighted_sum(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_stacked_weighted_sum, dim3(grid_for(n / 4 + 1)), dim3(FL_BLOCK), 0, s, out, stacked, P, n, ld, w, scale);
+}
+void fl_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64_t ld, const float* mask, hipStream_t s) {
+  unsigned gx = grid_for(n / 4 + 1);
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(k_broadcast_rows, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, src, P, n, ld, mask);
+}
+void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_coordinate_median, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, out, srcs, K, n);
+}
+void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
+                 const float* cg, const float* cl, hipStream_t s) {
+  const float bc1 = 1.f - powf(o.beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(o.beta2, (float)step));
+  hipLaunchKernelGGL(k_opt_step, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, param, grad, m, v, shadow, n, o, bc1, bc2s, anchor, cg, cl);
+}
+void fl_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_add_noise, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, t, n, scale, sigma, seed);
+}

@@ -1,0 +1,56 @@
+// Argument block shared by the grouped fused-MLP kernels and the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "common.h"
+
+#define MLP_EVAL_CHUNK 512
+
+struct MLPArgs {
+  int P, D0, D1, D2, D3, D0pad;
+  int64_t S;       // per-peer stride (elements) of params/shadow/m/v
+  int64_t numel;   // trainable elements per peer
+  int64_t off_w1, off_b1, off_w2, off_b2, off_w3, off_b3;
+  // parameters and optimizer state, [P][S]
+  float* params;
+  bf16* shadow;
+  bf16* w2t;       // [P][D1][D2] transposed bf16 copy of W2
+  float* m;
+  float* v;
+  const float* anchor;  // FedProx anchor [P][S] or null
+  const float* cg;      // SCAFFOLD global control variate [P][S] or null
+  const float* cl;      // SCAFFOLD local control variate  [P][S] or null
+  // training data: per-peer device pointers (uint8 [n][D0] images, int32 labels) + counts
+  const uint8_t* const* Xp;
+  const int* const* Yp;
+  const int* n;
+  const int* perm;  // [P][perm_stride] local indices (epoch permutation)
+  int64_t perm_stride;
+  // test data
+  const uint8_t* const* Xtp;
+  const int* const* Ytp;
+  const int* n_t;
+  // control
+  const int* active;  // [P]
+  const int* t0;      // [P] optimizer steps each peer already took in this fit
+  // workspace
+  bf16* H1;   // [P][h1_rows][D1]
+  int h1_rows;
+  bf16* H1T;  // [P][D1][Bpad]
+  bf16* XT;   // [P][D0pad][Bpad]
+  bf16* H2T;  // [P][D2][Bpad]
+  bf16* dH2T; // [P][D2][Bpad]
+  bf16* dH1T; // [P][D1][Bpad]
+  bf16* dlogT;// [P][16][Bpad]
+  int B, Bpad;
+  // accumulators
+  float* loss_acc;   // [P]
+  int* correct_acc;  // [P]
+  int* conf;         // [P][16][16] (eval) or null
+  OptParams opt;
+};
+
+bool mlp_shape_supported(int D0, int D1, int D2, int D3);
+void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s);
+void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s);
+void mlp_launch_sync_shadow(const MLPArgs& a, hipStream_t s);

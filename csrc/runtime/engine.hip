@@ -1,0 +1,301 @@
+// C++ runtime for the grouped fused-MLP engine + the C ABI of libmyfyp_hip.so.
+//
+// MLPEngine owns the per-step workspace of P co-located peers and a hipGraph holding one whole
+// local epoch (steps × {fc1_fwd, head, wgrad_opt}). A round's local training is then a single
+// hipGraphLaunch per epoch from the calling thread — Python (and the GIL) is off the per-step
+// path, and launch overhead is amortised by the graph (cdna_hip_programming.md §5.6 verdict:
+// launch-bound chains of small kernels belong in hipGraphs, not in a grid-barrier megakernel).
+//
+// Every entry point returns 0 on success, non-zero on failure (message via myfyp_last_error()).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../kernels/fl_ops.h"
+#include "../kernels/mlp_fused.h"
+
+static thread_local std::string g_last_error;
+
+#define CHECK_HIP(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      g_last_error = std::string(#expr) + ": " + hipGetErrorString(_e);                   \
+      return 1;                                                                           \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+
+struct MLPEngine {
+  MLPArgs a{};
+  int max_steps = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  int graph_steps = -1;
+  hipStream_t cap_stream = nullptr;
+  // engine-owned device buffers
+  void* ws = nullptr;
+  int* d_active = nullptr;
+  int* d_t0 = nullptr;
+  float* d_loss = nullptr;
+  int* d_correct = nullptr;
+  int* d_conf = nullptr;
+  std::vector<void*> owned;
+  std::mutex mu;
+  int max_test_rows = 0;
+
+  ~MLPEngine() {
+    if (exec) hipGraphExecDestroy(exec);
+    if (graph) hipGraphDestroy(graph);
+    if (cap_stream) hipStreamDestroy(cap_stream);
+    for (void* p : owned) hipFree(p);
+  }
+
+  void invalidate() {
+    if (exec) hipGraphExecDestroy(exec);
+    if (graph) hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    graph_steps = -1;
+  }
+
+  int alloc(void** p, size_t bytes) {
+    CHECK_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
+    CHECK_HIP(hipMemset(*p, 0, bytes < 16 ? 16 : bytes));
+    owned.push_back(*p);
+    return 0;
+  }
+
+  int capture(int steps) {
+    invalidate();
+    if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
+    for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
+    hipError_t e = hipStreamEndCapture(cap_stream, &graph);
+    if (e != hipSuccess) {
+      g_last_error = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+      graph = nullptr;
+      return 1;
+    }
+    CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    graph_steps = steps;
+    return 0;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int myfyp_version() { return 1; }
+const char* myfyp_last_error() { return g_last_error.c_str(); }
+
+// ------------------------------------------------------------------------------ generic FL ops
+int myfyp_weighted_sum(float* out, const uint64_t* srcs, const float* w, int K, int64_t n, void* stream) {
+  fl_weighted_sum(out, srcs, w, K, n, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_stacked_weighted_sum(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w, float scale, void* stream) {
+  fl_stacked_weighted_sum(out, stacked, P, n, ld, w, scale, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64_t ld, const float* mask, void* stream) {
+  fl_broadcast_rows(stacked, src, P, n, ld, mask, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, void* stream) {
+  if (K < 1 || K > 16) {
+    g_last_error = "coordinate_median supports 1..16 models";
+    return 2;
+  }
+  fl_coordinate_median(out, srcs, K, n, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_adam_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                    int step, const float* anchor, const float* cg, const float* cl, float mu, void* stream) {
+  OptParams o{0, lr, b1, b2, eps, wd, 0.f, 0, mu};
+  fl_opt_step(param, grad, m, v, shadow, n, o, step < 1 ? 1 : step, anchor, cg, cl, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_sgd_step(float* param, const float* grad, float* mom, int64_t n, float lr, float momentum, float wd, int nesterov, const float* anchor,
+                   const float* cg, const float* cl, float mu, void* stream) {
+  OptParams o{1, lr, 0.9f, 0.999f, 1e-8f, wd, momentum, nesterov, mu};
+  fl_opt_step(param, grad, momentum != 0.f ? mom : nullptr, nullptr, nullptr, n, o, 1, anchor, cg, cl, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_t seed, void* stream) {
+  fl_scale_add_noise(t, n, scale, sigma, seed, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ MLP engine
+int mlp_shape_ok(int D0, int D1, int D2, int D3) { return mlp_shape_supported(D0, D1, D2, D3) ? 1 : 0; }
+
+void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
+  if (!mlp_shape_supported(D0, D1, D2, D3) || P < 1 || B < 1 || B > 1024) {
+    g_last_error = "unsupported MLP shape";
+    return nullptr;
+  }
+  auto* e = new MLPEngine();
+  MLPArgs& a = e->a;
+  a.P = P;
+  a.D0 = D0; a.D1 = D1; a.D2 = D2; a.D3 = D3;
+  a.D0pad = (D0 + 15) / 16 * 16;
+  a.B = B;
+  a.Bpad = (B + 31) / 32 * 32;
+  a.h1_rows = a.Bpad > MLP_EVAL_CHUNK ? a.Bpad : MLP_EVAL_CHUNK;
+  a.off_w1 = 0;
+  a.off_b1 = (int64_t)D1 * D0;
+  a.off_w2 = a.off_b1 + D1;
+  a.off_b2 = a.off_w2 + (int64_t)D2 * D1;
+  a.off_w3 = a.off_b2 + D2;
+  a.off_b3 = a.off_w3 + (int64_t)D3 * D2;
+  a.numel = a.off_b3 + D3;
+  const size_t bp = (size_t)a.Bpad;
+  void* p;
+  int rc = 0;
+  rc |= e->alloc(&p, (size_t)P * a.h1_rows * D1 * 2); a.H1 = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * D1 * bp * 2); a.H1T = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * a.D0pad * bp * 2); a.XT = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * D2 * bp * 2); a.H2T = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * D2 * bp * 2); a.dH2T = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * D1 * bp * 2); a.dH1T = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * 16 * bp * 2); a.dlogT = (bf16*)p;
+  rc |= e->alloc(&p, (size_t)P * 4); e->d_active = (int*)p; a.active = e->d_active;
+  rc |= e->alloc(&p, (size_t)P * 4); e->d_t0 = (int*)p; a.t0 = e->d_t0;
+  rc |= e->alloc(&p, (size_t)P * 4); e->d_loss = (float*)p; a.loss_acc = e->d_loss;
+  rc |= e->alloc(&p, (size_t)P * 4); e->d_correct = (int*)p; a.correct_acc = e->d_correct;
+  rc |= e->alloc(&p, (size_t)P * 256 * 4); e->d_conf = (int*)p; a.conf = e->d_conf;
+  if (rc) {
+    delete e;
+    return nullptr;
+  }
+  a.opt = OptParams{0, 1e-3f, 0.9f, 0.999f, 1e-8f, 0.f, 0.f, 0, 0.f};
+  return e;
+}
+
+void mlp_engine_destroy(void* h) { delete (MLPEngine*)h; }
+
+int64_t mlp_engine_numel(void* h) { return ((MLPEngine*)h)->a.numel; }
+
+int mlp_engine_bind_params(void* h, float* params, bf16* shadow, bf16* w2t, float* m, float* v, int64_t S) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->a.params = params; e->a.shadow = shadow; e->a.w2t = w2t; e->a.m = m; e->a.v = v; e->a.S = S;
+  e->invalidate();
+  return 0;
+}
+
+int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, const int* n, const int* perm, int64_t perm_stride, int max_steps) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->a.Xp = (const uint8_t* const*)Xp; e->a.Yp = (const int* const*)Yp; e->a.n = n; e->a.perm = perm; e->a.perm_stride = perm_stride;
+  e->max_steps = max_steps;
+  e->invalidate();
+  return 0;
+}
+
+int mlp_engine_set_test_data(void* h, const uint64_t* Xtp, const uint64_t* Ytp, const int* n_t, int max_rows) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->a.Xtp = (const uint8_t* const*)Xtp; e->a.Ytp = (const int* const*)Ytp; e->a.n_t = n_t;
+  e->max_test_rows = max_rows;
+  return 0;
+}
+
+int mlp_engine_set_optimizer(void* h, int kind, float lr, float b1, float b2, float eps, float wd, float momentum, int nesterov, float mu) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  OptParams o{kind, lr, b1, b2, eps, wd, momentum, nesterov, mu};
+  if (memcmp(&o, &e->a.opt, sizeof(o)) != 0) {
+    e->a.opt = o;
+    e->invalidate();
+  }
+  return 0;
+}
+
+int mlp_engine_set_extras(void* h, const float* anchor, const float* cg, const float* cl) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (anchor != e->a.anchor || cg != e->a.cg || cl != e->a.cl) {
+    e->a.anchor = anchor; e->a.cg = cg; e->a.cl = cl;
+    e->invalidate();
+  }
+  return 0;
+}
+
+// Copy the active mask, zero the accumulators and refresh the bf16 shadows (stream-ordered).
+int mlp_engine_begin(void* h, const int* active_host, void* stream) {
+  auto* e = (MLPEngine*)h;
+  hipStream_t s = (hipStream_t)stream;
+  CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
+  CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
+  mlp_launch_sync_shadow(e->a, s);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// One local epoch for every active peer: a single graph replay (captured on first use).
+int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  hipStream_t s = (hipStream_t)stream;
+  if (e->max_steps <= 0) return 0;
+  if (!e->exec || e->graph_steps != e->max_steps) {
+    if (e->capture(e->max_steps)) return 1;
+  }
+  CHECK_HIP(hipMemcpyAsync(e->d_t0, t0_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  CHECK_HIP(hipGraphLaunch(e->exec, s));
+  return 0;
+}
+
+// Same epoch without the graph (debug / profiling A-B).
+int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
+  auto* e = (MLPEngine*)h;
+  hipStream_t s = (hipStream_t)stream;
+  CHECK_HIP(hipMemcpyAsync(e->d_t0, t0_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int mlp_engine_read_stats(void* h, float* loss_host, int* correct_host, void* stream) {
+  auto* e = (MLPEngine*)h;
+  hipStream_t s = (hipStream_t)stream;
+  CHECK_HIP(hipMemcpyAsync(loss_host, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(correct_host, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Forward the whole test split of every active peer: loss sum, correct count, confusion [P][16][16].
+int mlp_engine_eval(void* h, const int* active_host, float* loss_host, int* correct_host, int* conf_host, void* stream) {
+  auto* e = (MLPEngine*)h;
+  hipStream_t s = (hipStream_t)stream;
+  CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
+  CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
+  CHECK_HIP(hipMemsetAsync(e->d_conf, 0, sizeof(int) * e->a.P * 256, s));
+  mlp_launch_sync_shadow(e->a, s);
+  for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(e->a, base, s);
+  CHECK_HIP(hipGetLastError());
+  CHECK_HIP(hipMemcpyAsync(loss_host, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(correct_host, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(conf_host, e->d_conf, sizeof(int) * e->a.P * 256, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // extern "C"

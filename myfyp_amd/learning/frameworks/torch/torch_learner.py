@@ -75,6 +75,12 @@ class TorchLearner(Learner):
         self._flat: Optional[FlatParams] = None
         self._attach_module(model)
 
+    def close(self) -> None:
+        """Release the device slot (called by ``Node.stop``)."""
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None
+
     # ------------------------------------------------------------------ model plumbing
     def _attach_module(self, model: TorchModel) -> None:
         module = model.get_model()
@@ -92,7 +98,7 @@ class TorchLearner(Learner):
 
         if not MLPEngineHandle.supports(module):
             return None
-        return MLPEngineHandle.attach(module, self.device, self._self_addr)
+        return MLPEngineHandle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
 
     def flat_params(self) -> torch.Tensor:
         if self._engine is not None:
@@ -135,6 +141,8 @@ class TorchLearner(Learner):
     def set_data(self, data) -> None:
         super().set_data(data)
         self._data_cache.clear()
+        if self._engine is not None:
+            self._engine.group.invalidate_data()
 
     # ------------------------------------------------------------------ data
     def device_data(self, train: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -46,17 +46,22 @@ _SIGNATURES = {
     "myfyp_sgd_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
     # attacks / elementwise
     "myfyp_scale_add_noise": (c_int, [c_void_p, c_int64, c_float, c_float, ctypes.c_uint64, c_void_p]),
+
     # grouped MLP engine
-    "mlp_engine_create": (c_void_p, [c_int, c_int, c_void_p, c_int, c_int]),
+    "mlp_shape_ok": (c_int, [c_int, c_int, c_int, c_int]),
+    "mlp_engine_create": (c_void_p, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "mlp_engine_destroy": (None, [c_void_p]),
-    "mlp_engine_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "mlp_engine_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64]),
-    "mlp_engine_set_optimizer": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float, c_float, c_float]),
-    "mlp_engine_set_extras": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float]),
-    "mlp_engine_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
-    "mlp_engine_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
-    "mlp_engine_forward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
-    "mlp_engine_reset_graphs": (None, [c_void_p]),
+    "mlp_engine_numel": (c_int64, [c_void_p]),
+    "mlp_engine_bind_params": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
+    "mlp_engine_set_train_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int]),
+    "mlp_engine_set_test_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "mlp_engine_set_optimizer": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_float]),
+    "mlp_engine_set_extras": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_begin": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_run_epoch": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_run_epoch_eager": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_read_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 

@@ -1,0 +1,77 @@
+"""Build the native library (``python -m myfyp_amd.ops.build``).
+
+Compiles every ``csrc/**/*.hip`` for gfx950 with ``hipcc`` (each translation unit in parallel)
+and links ``myfyp_amd/_native/libmyfyp_hip.so`` in-tree, so the ``.so`` travels with the repo
+snapshot to the GPU box. Incremental: objects are rebuilt only when a source or header changed.
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+OUT_DIR = os.path.join(ROOT, "myfyp_amd", "_native")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(OUT_DIR, "libmyfyp_hip.so")
+ARCH = os.environ.get("MYFYP_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the native library)")
+
+
+def sources() -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max([os.path.getmtime(h) for h in hs] + [0.0])
+
+
+def _compile(src: str, hipcc: str, hdr_mtime: float, verbose: bool) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+    obj = os.path.join(OBJ_DIR, rel + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+        return obj
+    cmd = [hipcc, *FLAGS, "-I", os.path.join(CSRC, "kernels"), "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{res.stdout}\n{res.stderr}")
+    return obj
+
+
+def build(verbose: bool = False, jobs: int = 8) -> str:
+    """Compile + link; returns the library path."""
+    hipcc = _hipcc()
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
+    srcs = sources()
+    hdr = _headers_mtime()
+    with cf.ThreadPoolExecutor(max_workers=min(jobs, max(1, len(srcs)))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hipcc, hdr, verbose), srcs))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        tmp = LIB + ".tmp"
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

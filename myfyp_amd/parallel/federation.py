@@ -1,0 +1,352 @@
+"""Process-level federation runtime: one process per GPU, RCCL/xGMI weights plane.
+
+The reference moves every model through gRPC + pickle between peers and reduces on the host with
+NumPy. Here each process owns one GPU and hosts ``P`` co-located peers;
+the peers of all processes form one federation:
+
+* **control plane** — co-located peers talk over the in-process bus; peers on other ranks are
+  reached through :class:`StoreBus`, a mailbox over the ``torch.distributed`` TCPStore (no extra
+  dependency, works wherever ``torchrun`` works);
+* **weights plane** — round-level collectives executed ONCE per process by a *gang* of the local
+  peers' learning threads: votes are all-gathered so every rank computes the same train set; FedAvg
+  is one weighted all-reduce (``n_i``-weighted local partial sum on the GPU → ``all_reduce(SUM)``
+  over RCCL → scale → broadcast into every local peer's parameter row); the initial model is one
+  broadcast from the initiator's rank;
+* **fault tolerance** — a gang waits at most ``Settings.AGGREGATION_TIMEOUT`` for a co-located peer
+  and then proceeds without it (the reference's "aggregate whatever arrived", ``aggregator.py:192-208``);
+  cross-rank collectives run under the process-group timeout (``Settings.COLLECTIVE_TIMEOUT``).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from myfyp_amd.management.logger import logger
+from myfyp_amd.settings import Settings
+
+
+# ---------------------------------------------------------------------------------------------
+# cross-rank control bus
+# ---------------------------------------------------------------------------------------------
+class StoreBus:
+    """Ordered per-rank mailboxes on a ``torch.distributed.Store``."""
+
+    def __init__(self, store, rank: int, world: int, deliver: Callable[[str, str, dict], None]) -> None:
+        self.store = store
+        self.rank = rank
+        self.world = world
+        self._deliver = deliver
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._listen, name=f"storebus-{rank}", daemon=True)
+        self._thread.start()
+
+    def send(self, dest_rank: int, dest_addr: str, kind: str, msg: dict) -> None:
+        seq = self.store.add(f"mbox/{dest_rank}/ctr", 1)
+        self.store.set(f"mbox/{dest_rank}/{seq}", pickle.dumps((dest_addr, kind, msg)))
+
+    def _listen(self) -> None:
+        # non-blocking counter poll with adaptive back-off: control messages are rare (start/stop,
+        # heartbeats), and a blocking store.wait() would pin the store socket at shutdown
+        seq = 1
+        idle = 0.0005
+        while not self._stop.is_set():
+            try:
+                ctr = self.store.add(f"mbox/{self.rank}/ctr", 0)
+            except Exception:
+                if self._stop.wait(0.05):
+                    return
+                continue
+            if ctr < seq:
+                self._stop.wait(idle)
+                idle = min(idle * 2, 0.02)
+                continue
+            idle = 0.0005
+            while seq <= ctr and not self._stop.is_set():
+                key = f"mbox/{self.rank}/{seq}"
+                try:
+                    payload = self.store.get(key)
+                    self.store.delete_key(key)
+                except Exception:
+                    break
+                seq += 1
+                try:
+                    dest, kind, msg = pickle.loads(payload)
+                    self._deliver(dest, kind, msg)
+                except Exception as e:  # never kill the listener
+                    logger.error(f"rank{self.rank}", f"StoreBus delivery failed: {e}")
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=2.0)
+
+
+class RemotePeer:
+    """Stub for a peer on another rank; quacks like a protocol for the in-memory client."""
+
+    def __init__(self, fed: "Federation", rank: int, addr: str) -> None:
+        self.fed, self.rank, self.addr = fed, rank, addr
+
+    def is_running(self) -> bool:
+        return True
+
+    def handle_message(self, msg: dict) -> dict:
+        self.fed.bus.send(self.rank, self.addr, "msg", msg)
+        return {}
+
+    def handle_weights(self, msg: dict) -> dict:
+        self.fed.bus.send(self.rank, self.addr, "weights", msg)
+        return {}
+
+    def handshake(self, addr: str) -> bool:
+        return True
+
+    def remote_disconnect(self, addr: str) -> None:
+        pass
+
+
+# ---------------------------------------------------------------------------------------------
+# local gang: one op at a time, executed once per process by the last arriving peer thread
+# ---------------------------------------------------------------------------------------------
+class LocalGang:
+    """Barrier-with-payload across the co-located peers' learning threads."""
+
+    def __init__(self) -> None:
+        self._cv = threading.Condition()
+        self._gen = 0
+        self._arrived: Dict[str, Any] = {}
+        self._result: Dict[int, Any] = {}
+        self._error: Dict[int, BaseException] = {}
+
+    def run(self, member: str, members: List[str], payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: float) -> Any:
+        with self._cv:
+            gen = self._gen
+            self._arrived[member] = payload
+            deadline = time.time() + timeout
+            while gen == self._gen:
+                live = [m for m in members]
+                if set(live).issubset(self._arrived) or time.time() >= deadline:
+                    missing = set(live) - set(self._arrived)
+                    if missing:
+                        logger.warning(member, f"gang timeout; proceeding without {sorted(missing)}")
+                    arrived, self._arrived = self._arrived, {}
+                    self._gen += 1
+                    self._cv.release()
+                    try:
+                        res, err = fn(arrived), None
+                    except BaseException as e:
+                        res, err = None, e
+                    finally:
+                        self._cv.acquire()
+                    if err is not None:
+                        self._error[gen] = err
+                    else:
+                        self._result[gen] = res
+                    for old in [g for g in self._result if g < gen - 16]:
+                        del self._result[old]
+                    self._cv.notify_all()
+                    break
+                self._cv.wait(timeout=max(0.001, min(1.0, deadline - time.time())))
+            while gen not in self._result and gen not in self._error:
+                self._cv.wait(timeout=1.0)
+            if gen in self._error:
+                raise self._error[gen]
+            return self._result[gen]
+
+
+# ---------------------------------------------------------------------------------------------
+# federation
+# ---------------------------------------------------------------------------------------------
+class Federation:
+    """Singleton per process; created by :meth:`init`."""
+
+    _instance: Optional["Federation"] = None
+
+    def __init__(self, rank: int, world: int, local_rank: int, device: torch.device, store=None) -> None:
+        self.rank, self.world, self.local_rank = rank, world, local_rank
+        self.device = device
+        self.store = store
+        self.bus: Optional[StoreBus] = None
+        self.local_nodes: Dict[str, Any] = {}
+        self.local_order: List[str] = []
+        self.peers: Dict[str, int] = {}  # addr -> rank (all peers, after finalize)
+        self.gang = LocalGang()
+        self.finalized = threading.Event()
+        self.round_hooks: List[Callable[[int, "Federation"], None]] = []
+        self.stats: Dict[str, List[float]] = {}
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------ lifecycle
+    @classmethod
+    def init(cls, backend: Optional[str] = None) -> "Federation":
+        """Initialise from ``torchrun`` env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+        if cls._instance is not None:
+            return cls._instance
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+            device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            device = torch.device("cpu")
+        store = None
+        if world > 1:
+            import torch.distributed as dist
+
+            if not dist.is_initialized():
+                be = backend or ("nccl" if device.type == "cuda" else "gloo")
+                kw = {"timeout": datetime.timedelta(seconds=Settings.COLLECTIVE_TIMEOUT)}
+                if be == "nccl":
+                    kw["device_id"] = device
+                dist.init_process_group(backend=be, **kw)
+            store = _default_store()
+        cls._instance = cls(rank, world, local_rank, device, store)
+        if store is not None:
+            cls._instance.bus = StoreBus(store, rank, world, cls._instance._deliver)
+        return cls._instance
+
+    @classmethod
+    def get(cls) -> "Federation":
+        if cls._instance is None:
+            return cls.init()
+        return cls._instance
+
+    def shutdown(self) -> None:
+        """Stop the control bus and tear down the process group (call once, at exit)."""
+        if self.bus is not None:
+            self.bus.stop()
+            self.bus = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.barrier()
+                dist.destroy_process_group()
+        Federation._instance = None
+
+    @classmethod
+    def reset(cls) -> None:
+        inst = cls._instance
+        if inst is not None and inst.bus is not None:
+            inst.bus.stop()
+        cls._instance = None
+
+    def register_local(self, node) -> None:
+        with self._lock:
+            self.local_nodes[node.addr] = node
+            if node.addr not in self.local_order:
+                self.local_order.append(node.addr)
+
+    def finalize(self, connect: bool = True) -> List[str]:
+        """Exchange the peer lists of all ranks and connect every local node to every peer."""
+        local = list(self.local_order)
+        if self.world > 1:
+            import json
+
+            self.store.set(f"members/{self.rank}", json.dumps(local))
+            for r in range(self.world):
+                self.store.wait([f"members/{r}"])
+                for addr in json.loads(self.store.get(f"members/{r}")):
+                    self.peers[addr] = r
+        else:
+            for addr in local:
+                self.peers[addr] = 0
+        if connect:
+            for addr in local:
+                node = self.local_nodes[addr]
+                for other in self.peers:
+                    if other != addr:
+                        node.communication_protocol.connect(other)
+        self.finalized.set()
+        return self.all_peers()
+
+    def all_peers(self) -> List[str]:
+        return sorted(self.peers, key=lambda a: (self.peers[a], a))
+
+    def is_local(self, addr: str) -> bool:
+        return addr in self.local_nodes
+
+    def remote_stub(self, addr: str) -> Optional[RemotePeer]:
+        r = self.peers.get(addr)
+        if r is None or r == self.rank or self.bus is None:
+            return None
+        return RemotePeer(self, r, addr)
+
+    def _deliver(self, dest: str, kind: str, msg: dict) -> None:
+        from myfyp_amd.communication.protocols.memory.memory_communication_protocol import ServerRegistry
+
+        server = ServerRegistry.get(dest)
+        if server is None:
+            return
+        if kind == "weights":
+            server.handle_weights(msg)
+        else:
+            server.handle_message(msg)
+
+    # ------------------------------------------------------------------ collectives (gang leaders only)
+    def live_local(self) -> List[str]:
+        return [a for a in self.local_order if a in self.local_nodes and self.local_nodes[a].state.round is not None]
+
+    def gang_run(self, member: str, payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: Optional[float] = None) -> Any:
+        members = [a for a in self.local_order if a in self.local_nodes]
+        return self.gang.run(member, members, payload, fn, Settings.AGGREGATION_TIMEOUT if timeout is None else timeout)
+
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out: List[Any] = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place SUM all-reduce over RCCL (bucketed for large buffers)."""
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+
+        flat = t.view(-1)
+        bucket = max(1, Settings.BUCKET_BYTES // flat.element_size())
+        if flat.numel() <= bucket:
+            dist.all_reduce(flat)
+        else:
+            works = [dist.all_reduce(flat[i : i + bucket], async_op=True) for i in range(0, flat.numel(), bucket)]
+            for w in works:
+                w.wait()
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src_rank: int) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+
+        dist.broadcast(t, src=src_rank)
+        return t
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    def record(self, name: str, seconds: float) -> None:
+        self.stats.setdefault(name, []).append(seconds)
+
+
+def _default_store():
+    import torch.distributed as dist
+
+    try:
+        return dist.distributed_c10d._get_default_store()
+    except Exception:
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+        return dist.TCPStore(addr, port, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")) == 0)

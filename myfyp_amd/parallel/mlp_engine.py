@@ -1,7 +1,408 @@
-"""Placeholder; replaced by the grouped fused MLP engine."""
+"""Grouped fused MLP engine: co-located peers trained by ONE sequence of HIP launches.
+
+This replaces the reference's per-node Lightning ``Trainer`` (``lightning_learner.py:78-108``) and
+the Ray actor pool (``simulation/actor_pool.py``) for ReLU MLPs on MI355X:
+
+* every peer of the same architecture/batch size on a device gets a *slot* in one stacked
+  ``[capacity, S]`` fp32 parameter buffer (+ Adam moments, bf16 shadow, W2ᵀ shadow); the peer's
+  ``nn.Module`` parameters are views into its row, so ``state_dict``/wire format are unchanged;
+* ``fit`` calls from the peers' learning threads are *ganged*: the first arrival opens a batch,
+  which closes when every expected co-located peer arrived (or ``Settings.GANG_WINDOW`` passed);
+  one thread then runs the whole batch — each local epoch is ONE ``hipGraphLaunch`` of the C++
+  engine (``csrc/runtime/engine.hip``) whose kernels cover all peers via ``grid.z``;
+* ``evaluate`` is ganged the same way (one forward sweep over every peer's test split).
+
+Numerics: bf16 MFMA operands, fp32 accumulation, fp32 master weights and optimizer state,
+``torch.optim.Adam``/``SGD`` update rules, fresh optimizer state per ``fit`` (Lightning semantics).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+import time
+from typing import Dict, List, Optional, Set, Tuple
+
+import numpy as np
+import torch
+
+from myfyp_amd.ops import _native
+from myfyp_amd.settings import Settings
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def mlp_dims(module: torch.nn.Module) -> Optional[Tuple[int, int, int, int]]:
+    """(D0, D1, D2, D3) of a 3-Linear ReLU MLP (the reference architecture family) else None."""
+    from myfyp_amd.models.mlp import MLP
+
+    if not isinstance(module, MLP) or module.activation != "relu" or len(module.hidden_sizes) != 2:
+        return None
+    lins = module.linear_layers()
+    if any(lin.bias is None for lin in lins):
+        return None
+    return (lins[0].in_features, lins[0].out_features, lins[1].out_features, lins[2].out_features)
+
+
+class _Gang:
+    """Collects requests from co-located peers' threads and runs them as one batch."""
+
+    def __init__(self, run_batch) -> None:
+        self._run_batch = run_batch
+        self._cv = threading.Condition()
+        self._pending: Dict[int, object] = {}
+        self._results: Dict[int, object] = {}
+        self._errors: Dict[int, BaseException] = {}
+        self._running = False
+        self._t_first = 0.0
+        self.expected: Optional[Set[int]] = None
+
+    def submit(self, slot: int, req: object, default_expected: Set[int]) -> object:
+        window = Settings.GANG_WINDOW
+        with self._cv:
+            if not self._pending:
+                self._t_first = time.time()
+            self._pending[slot] = req
+            self._cv.notify_all()
+            while slot not in self._results and slot not in self._errors:
+                expected = self.expected if self.expected is not None else default_expected
+                complete = expected.issubset(self._pending.keys())
+                waited = time.time() - self._t_first
+                if not self._running and self._pending and (complete or waited >= window):
+                    batch, self._pending = self._pending, {}
+                    self._running = True
+                    self._cv.release()
+                    try:
+                        results = self._run_batch(batch)
+                        errors: Dict[int, BaseException] = {}
+                    except BaseException as e:  # propagate to every member of the batch
+                        results, errors = {}, {s: e for s in batch}
+                    finally:
+                        self._cv.acquire()
+                        self._running = False
+                    self._results.update(results)
+                    self._errors.update(errors)
+                    if self._pending:
+                        self._t_first = time.time()
+                    self._cv.notify_all()
+                else:
+                    self._cv.wait(timeout=max(0.0005, window - waited) if not self._running else 0.05)
+            if slot in self._errors:
+                raise self._errors.pop(slot)
+            return self._results.pop(slot)
+
+
+class MLPGroup:
+    """All peers of one (device, dims, batch size) — one native engine, one stacked buffer."""
+
+    _groups: Dict[tuple, "MLPGroup"] = {}
+    _lock = threading.Lock()
+
+    @classmethod
+    def get(cls, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int) -> "MLPGroup":
+        key = (str(device), dims, batch_size)
+        with cls._lock:
+            g = cls._groups.get(key)
+            if g is None:
+                g = cls(device, dims, batch_size)
+                cls._groups[key] = g
+            return g
+
+    @classmethod
+    def reset_all(cls) -> None:
+        with cls._lock:
+            for g in cls._groups.values():
+                g.close()
+            cls._groups.clear()
+
+    def __init__(self, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, capacity: int = 8) -> None:
+        self.device = device
+        self.dims = dims
+        self.B = batch_size
+        D0, D1, D2, D3 = dims
+        self.numel = D1 * D0 + D1 + D2 * D1 + D2 + D3 * D2 + D3
+        self.S = (self.numel + 63) // 64 * 64
+        self.lock = threading.RLock()
+        self.handles: Dict[int, "MLPEngineHandle"] = {}
+        self.capacity = 0
+        self._engine = None
+        self._engine_cap = 0
+        self._data_version = 0
+        self._bound_version = -1
+        self.extras: Dict[str, torch.Tensor] = {}
+        self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
+        self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
+        self._alloc(capacity)
+        self.fit_gang = _Gang(self._run_fit_batch)
+        self.eval_gang = _Gang(self._run_eval_batch)
+
+    # ------------------------------------------------------------------ buffers / slots
+    def _alloc(self, capacity: int) -> None:
+        old = (getattr(self, "params", None), getattr(self, "m", None), getattr(self, "v", None))
+        dev = self.device
+        D1, D2 = self.dims[1], self.dims[2]
+        params = torch.zeros(capacity, self.S, dtype=torch.float32, device=dev)
+        if old[0] is not None:
+            params[: self.capacity].copy_(old[0])
+        self.params = params
+        self.m = torch.zeros_like(params)
+        self.v = torch.zeros_like(params)
+        self.shadow = torch.zeros(capacity, self.S, dtype=torch.bfloat16, device=dev)
+        self.w2t = torch.zeros(capacity, D1 * D2, dtype=torch.bfloat16, device=dev)
+        self.capacity = capacity
+        for slot, h in self.handles.items():
+            h.flat.retarget(self.params[slot, : self.numel])
+        self._close_engine()
+
+    def _close_engine(self) -> None:
+        if self._engine is not None:
+            _native.load(required=True).mlp_engine_destroy(self._engine)
+            self._engine = None
+
+    def close(self) -> None:
+        self._close_engine()
+
+    def attach(self, handle: "MLPEngineHandle") -> int:
+        with self.lock:
+            slot = next((i for i in range(self.capacity) if i not in self.handles), None)
+            if slot is None:
+                self._alloc(self.capacity * 2)
+                slot = next(i for i in range(self.capacity) if i not in self.handles)
+            self.handles[slot] = handle
+            self._data_version += 1
+            return slot
+
+    def detach(self, slot: int) -> None:
+        with self.lock:
+            self.handles.pop(slot, None)
+            self._data_version += 1
+
+    def invalidate_data(self) -> None:
+        with self.lock:
+            self._data_version += 1
+
+    # ------------------------------------------------------------------ native engine
+    def _ensure_engine(self) -> None:
+        lib = _native.load(required=True)
+        if self._engine is None or self._engine_cap != self.capacity:
+            self._close_engine()
+            D0, D1, D2, D3 = self.dims
+            eng = lib.mlp_engine_create(self.capacity, D0, D1, D2, D3, self.B)
+            if not eng:
+                raise RuntimeError(f"mlp_engine_create failed: {lib.myfyp_last_error().decode()}")
+            self._engine = eng
+            self._engine_cap = self.capacity
+            self._bound_version = -1
+            _native.check(
+                lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
+            )
+        if self._bound_version != self._data_version:
+            self._bind_data()
+            self._bound_version = self._data_version
+
+    def _bind_data(self) -> None:
+        """(Re)build the per-peer data pointer tables (uploads each peer's split once)."""
+        lib = _native.load(required=True)
+        cap, dev = self.capacity, self.device
+        xs, ys, ns, xts, yts, nts = [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap
+        self._keep = []
+        for slot, h in self.handles.items():
+            (x, y), (xt, yt) = h.device_split(True), h.device_split(False)
+            xs[slot], ys[slot], ns[slot] = x.data_ptr(), y.data_ptr(), x.shape[0]
+            xts[slot], yts[slot], nts[slot] = xt.data_ptr(), yt.data_ptr(), xt.shape[0]
+            self._keep += [x, y, xt, yt]
+        self.n_train = ns
+        self.n_test = nts
+        self._tables = {
+            "Xp": torch.tensor(xs, dtype=torch.int64, device=dev),
+            "Yp": torch.tensor(ys, dtype=torch.int64, device=dev),
+            "n": torch.tensor(ns, dtype=torch.int32, device=dev),
+            "Xtp": torch.tensor(xts, dtype=torch.int64, device=dev),
+            "Ytp": torch.tensor(yts, dtype=torch.int64, device=dev),
+            "nt": torch.tensor(nts, dtype=torch.int32, device=dev),
+        }
+        self.nmax = max(1, max(ns) if ns else 1)
+        self.max_steps = (self.nmax + self.B - 1) // self.B
+        self.perm = torch.zeros(cap, self.nmax, dtype=torch.int32, device=dev)
+        self._perm_mask = torch.arange(self.nmax, device=dev).unsqueeze(0) >= torch.tensor(ns, device=dev).unsqueeze(1)
+        t = self._tables
+        _native.check(lib.mlp_engine_set_train_data(self._engine, _p(t["Xp"]), _p(t["Yp"]), _p(t["n"]), _p(self.perm), self.nmax, self.max_steps), "set_train_data")
+        _native.check(lib.mlp_engine_set_test_data(self._engine, _p(t["Xtp"]), _p(t["Ytp"]), _p(t["nt"]), max(nts) if nts else 0), "set_test_data")
+
+    def _extra_buffer(self, name: str) -> torch.Tensor:
+        buf = self.extras.get(name)
+        if buf is None or buf.shape[0] != self.capacity:
+            buf = torch.zeros(self.capacity, self.S, dtype=torch.float32, device=self.device)
+            self.extras[name] = buf
+        return buf
+
+    # ------------------------------------------------------------------ batched fit
+    def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
+        lib = _native.load(required=True)
+        with self.lock:
+            self._ensure_engine()
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            specs = list(batch.values())
+            spec, epochs = specs[0][0], max(r[1] for r in specs)
+            kind = 0 if spec.get("name", "adam") == "adam" else 1
+            extras_any = [r[2] for r in specs if r[2]]
+            mu = 0.0
+            anchor = cg = cl = None
+            if any("anchor" in e for e in extras_any):
+                anchor = self._extra_buffer("anchor")
+                mu = float(next(e["mu"] for e in extras_any if "anchor" in e))
+            if any("c_global" in e for e in extras_any):
+                cg, cl = self._extra_buffer("c_global"), self._extra_buffer("c_local")
+            for slot, (_, _, extra) in batch.items():
+                if anchor is not None:
+                    anchor[slot, : self.numel].copy_(extra["anchor"] if "anchor" in extra else self.params[slot, : self.numel])
+                if cg is not None:
+                    if "c_global" in extra:
+                        cg[slot, : self.numel].copy_(extra["c_global"])
+                        cl[slot, : self.numel].copy_(extra["c_local"])
+                    else:
+                        cg[slot].zero_()
+                        cl[slot].zero_()
+            _native.check(
+                lib.mlp_engine_set_optimizer(
+                    self._engine, kind, float(spec.get("lr", 1e-3)), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
+                    float(spec.get("eps", 1e-8)), float(spec.get("weight_decay", 0.0)), float(spec.get("momentum", 0.0)),
+                    int(bool(spec.get("nesterov", False))), mu,
+                ),
+                "set_optimizer",
+            )
+            _native.check(lib.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
+            active = np.zeros(self.capacity, dtype=np.int32)
+            for slot in batch:
+                active[slot] = 1
+                self.m[slot].zero_()
+                self.v[slot].zero_()
+            _native.check(lib.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
+            steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
+            keys = torch.empty(self.capacity, self.nmax, device=self.device)
+            run = lib.mlp_engine_run_epoch_eager if self.eager else lib.mlp_engine_run_epoch
+            for ep in range(epochs):
+                if self.perm_fn is not None:
+                    self.perm.copy_(self.perm_fn(ep))
+                else:
+                    keys.uniform_()
+                    keys.masked_fill_(self._perm_mask, 2.0)
+                    self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
+                t0 = (steps_pe * ep).astype(np.int32)
+                _native.check(run(self._engine, t0.ctypes.data, stream), "run_epoch")
+            loss = np.zeros(self.capacity, dtype=np.float32)
+            correct = np.zeros(self.capacity, dtype=np.int32)
+            _native.check(lib.mlp_engine_read_stats(self._engine, loss.ctypes.data, correct.ctypes.data, stream), "read_stats")
+        out = {}
+        for slot in batch:
+            n = max(1, self.n_train[slot] * epochs)
+            out[slot] = (int(steps_pe[slot] * epochs), float(loss[slot]) / n, float(correct[slot]) / n)
+        return out
+
+    def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
+        lib = _native.load(required=True)
+        with self.lock:
+            self._ensure_engine()
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            active = np.zeros(self.capacity, dtype=np.int32)
+            for slot in batch:
+                active[slot] = 1
+            loss = np.zeros(self.capacity, dtype=np.float32)
+            correct = np.zeros(self.capacity, dtype=np.int32)
+            conf = np.zeros((self.capacity, 16, 16), dtype=np.int32)
+            _native.check(lib.mlp_engine_eval(self._engine, active.ctypes.data, loss.ctypes.data, correct.ctypes.data, conf.ctypes.data, stream), "eval")
+        D3 = self.dims[3]
+        return {slot: (float(loss[slot]) / max(1, self.n_test[slot]), conf[slot, :D3, :D3].copy()) for slot in batch}
+
+    def expect(self, fit_slots: Optional[Set[int]] = None, eval_slots: Optional[Set[int]] = None) -> None:
+        """Tell the gangs exactly which slots will call (collective workflow knows it)."""
+        self.fit_gang.expected = fit_slots
+        self.eval_gang.expected = eval_slots
+
+    def default_expected(self) -> Set[int]:
+        return set(self.handles)
+
+
+class _RetargetableFlat:
+    """Parameter views of one module into a row of the group buffer."""
+
+    def __init__(self, module: torch.nn.Module, storage: torch.Tensor) -> None:
+        self.module = module
+        self.params = [p for p in module.parameters()]
+        self.retarget(storage, copy_in=True)
+
+    def retarget(self, storage: torch.Tensor, copy_in: bool = False) -> None:
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                view = storage[off : off + p.numel()].view_as(p)
+                if copy_in:
+                    view.copy_(p.data.to(view.dtype))
+                p.data = view
+                off += p.numel()
+        self.flat = storage
 
 
 class MLPEngineHandle:
+    """A learner's slot in an :class:`MLPGroup`."""
+
     @staticmethod
-    def supports(module) -> bool:
-        return False
+    def supports(module: torch.nn.Module) -> bool:
+        dims = mlp_dims(module)
+        if dims is None:
+            return False
+        lib = _native.load()
+        if lib is None:
+            # GPU + fused path requested but no library: fail loudly (no silent eager fallback)
+            raise RuntimeError(f"MI355X fused engine requested but native library unavailable: {_native.error()}")
+        return bool(lib.mlp_shape_ok(*dims))
+
+    @classmethod
+    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None) -> "MLPEngineHandle":
+        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner)
+
+    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None) -> None:
+        self.addr = addr
+        self.module = module
+        self.group = MLPGroup.get(device, mlp_dims(module), batch_size)
+        self.learner = learner
+        self._data_id = id(learner.data) if learner is not None else None
+        with self.group.lock:
+            self.slot = self.group.attach(self)
+            self.flat = _RetargetableFlat(module, self.group.params[self.slot, : self.group.numel])
+
+    def close(self) -> None:
+        self.group.detach(self.slot)
+
+    def flat_params(self) -> torch.Tensor:
+        return self.flat.flat
+
+    def device_split(self, train: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.learner is None or self.learner.data is None:
+            D0 = self.group.dims[0]
+            return torch.zeros(0, D0, dtype=torch.uint8, device=self.group.device), torch.zeros(0, dtype=torch.int32, device=self.group.device)
+        x, y = self.learner.device_data(train)
+        x = x.reshape(x.shape[0], -1)
+        if x.dtype != torch.uint8:
+            raise TypeError("fused MLP engine expects uint8 images")
+        if not x.is_contiguous():
+            x = x.contiguous()
+        return x, y.to(torch.int32)
+
+    def fit(self, learner, spec: dict, extra: dict) -> Tuple[int, float]:
+        if self.learner is not learner or getattr(self, "_data_id", None) != id(learner.data):
+            self.learner = learner
+            self._data_id = id(learner.data)
+            self.group.invalidate_data()
+        steps, loss, _acc = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
+        learner.global_step += steps
+        return steps, loss
+
+    def evaluate(self, learner) -> Tuple[float, np.ndarray]:
+        if self.learner is not learner or getattr(self, "_data_id", None) != id(learner.data):
+            self.learner = learner
+            self._data_id = id(learner.data)
+            self.group.invalidate_data()
+        return self.group.eval_gang.submit(self.slot, (), self.group.default_expected())

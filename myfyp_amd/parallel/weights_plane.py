@@ -1,0 +1,132 @@
+"""Round-level weight collectives executed by a local gang leader (see ``federation.py``).
+
+All functions receive ``arrived: {addr: payload}`` for the co-located peers that reached the gang
+and run identically on every rank (same call order ⇒ matching RCCL collectives).
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from myfyp_amd import ops
+from myfyp_amd.parallel.federation import Federation
+
+
+# ---------------------------------------------------------------------------------------------
+# learner state access
+# ---------------------------------------------------------------------------------------------
+def state_tensors(learner) -> List[torch.Tensor]:
+    """Device tensors that define a peer's model: flat trainable vector + floating buffers."""
+    out = [learner.flat_params()]
+    module = learner.model.get_model()
+    for b in module.buffers():
+        if b.is_floating_point():
+            out.append(b)
+    return out
+
+
+def _stacked_group(learners) -> Optional[Any]:
+    """Return the shared MLPGroup when every learner is a row of one stacked buffer."""
+    groups = {id(getattr(lr, "_engine", None) and lr._engine.group) for lr in learners}
+    if len(groups) != 1 or getattr(learners[0], "_engine", None) is None:
+        return None
+    return learners[0]._engine.group
+
+
+# ---------------------------------------------------------------------------------------------
+# initial model (reference: init_model gossip, start_learning_stage.py:82-112)
+# ---------------------------------------------------------------------------------------------
+def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str) -> None:
+    """Every peer adopts the initiator's weights: local copy + one RCCL broadcast per tensor."""
+    learners = {a: fed.local_nodes[a].learner for a in arrived}
+    src_rank = fed.peers.get(initiator, 0)
+    ref_addr = initiator if initiator in learners else next(iter(learners))
+    src = state_tensors(learners[ref_addr])
+    bufs = [t.detach().clone() for t in src]
+    for t in bufs:
+        fed.broadcast_(t, src_rank)
+    with torch.no_grad():
+        for a, lr in learners.items():
+            for dst, s in zip(state_tensors(lr), bufs):
+                dst.copy_(s)
+
+
+# ---------------------------------------------------------------------------------------------
+# votes
+# ---------------------------------------------------------------------------------------------
+def gather_votes(fed: Federation, arrived: Dict[str, Dict[str, int]]) -> Dict[str, Dict[str, int]]:
+    allv: Dict[str, Dict[str, int]] = {}
+    for part in fed.all_gather_object(dict(arrived)):
+        allv.update(part)
+    return allv
+
+
+# ---------------------------------------------------------------------------------------------
+# aggregation
+# ---------------------------------------------------------------------------------------------
+def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tuple[float, List[str]]:
+    """Sample-weighted mean of the trainers' models (weight 0 for non-trainers), result into every
+    local peer. One local weighted reduction kernel + one all-reduce + one broadcast kernel."""
+    t0 = time.perf_counter()
+    addrs = list(arrived)
+    learners = [fed.local_nodes[a].learner for a in addrs]
+    weights = [float(arrived[a][0]) for a in addrs]
+    contributors = [a for a, w in zip(addrs, weights) if w > 0]
+    group = _stacked_group(learners)
+    dev = learners[0].flat_params().device
+    if group is not None:
+        w = torch.zeros(group.capacity, dtype=torch.float32)
+        for lr, wt in zip(learners, weights):
+            w[lr._engine.slot] = wt
+        wsum_local = float(w.sum())
+        n = group.numel
+        buf = torch.empty(n + 1, dtype=torch.float32, device=dev)
+        ops.stacked_weighted_sum(group.params[:, :n], w.to(dev), buf[:n], 1.0)
+        buf[n] = wsum_local
+        fed.all_reduce_(buf)
+        total = buf[n:].clone()
+        buf[:n].div_(total.clamp_min(1e-12))
+        mask = torch.zeros(group.capacity, dtype=torch.float32)
+        for lr in learners:
+            mask[lr._engine.slot] = 1.0
+        ops.broadcast_rows(buf[:n], group.params[:, :n], mask.to(dev))
+        total_w = float(total)  # one sync per round
+    else:
+        states = [state_tensors(lr) for lr in learners]
+        flat = torch.cat([torch.cat([t.reshape(-1).float() for t in st]) for st in states[:1]])
+        n = flat.numel()
+        acc = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+        for st, wt in zip(states, weights):
+            if wt > 0:
+                acc[:n].add_(torch.cat([t.reshape(-1).float() for t in st]), alpha=wt)
+        acc[n] = sum(weights)
+        fed.all_reduce_(acc)
+        total_w = float(acc[n])
+        avg = acc[:n] / max(total_w, 1e-12)
+        with torch.no_grad():
+            for st in states:
+                off = 0
+                for t in st:
+                    t.copy_(avg[off : off + t.numel()].view_as(t).to(t.dtype))
+                    off += t.numel()
+    fed.record("aggregate", time.perf_counter() - t0)
+    return total_w, contributors
+
+
+def aggregate_generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> Any:
+    """Any aggregator: all-gather the trainers' wire models and reduce identically on every rank."""
+    local_models = {a: p[1] for a, p in arrived.items() if p[1] is not None}
+    everything: Dict[str, Any] = {}
+    for part in fed.all_gather_object(local_models):
+        everything.update(part)
+    models = [everything[a] for a in sorted(everything)]
+    if not models:
+        return None
+    agg = aggregator.aggregate(models)
+    for a in arrived:
+        fed.local_nodes[a].learner.set_model(agg)
+    return agg

@@ -1,0 +1,43 @@
+"""Collective vote (parity target: ``stages/base_node/vote_train_set_stage.py:43-184``).
+
+Each peer still casts its own ``TRAIN_SET_SIZE`` weighted votes (same sampling rule), but votes are
+all-gathered in one collective, so every rank tallies the identical vote set and the train set is
+consistent by construction — a precondition for RCCL collectives (SURVEY §7.4 hard part 1).
+"""
+
+from typing import Optional, Type
+
+from myfyp_amd.management.logger import logger
+from myfyp_amd.parallel import weights_plane
+from myfyp_amd.stages.base_node.vote_train_set_stage import make_votes, tally_votes
+from myfyp_amd.stages.collective._common import fed, set_gang_expectations
+from myfyp_amd.stages.stage import Stage, check_early_stop
+from myfyp_amd.stages.stage_factory import StageFactory
+
+
+class VoteTrainSetStage(Stage):
+    @staticmethod
+    def name() -> str:
+        return "VoteTrainSetStage"
+
+    @staticmethod
+    def execute(state=None, communication_protocol=None, **kwargs) -> Optional[Type[Stage]]:
+        if state is None or communication_protocol is None:
+            raise Exception("Invalid parameters on VoteTrainSetStage.")
+        if check_early_stop(state, raise_exception=False):
+            return None
+        logger.round_started(state.addr, state.experiment)
+        f = fed()
+        votes = make_votes(state.addr, f.all_peers(), state.round)
+
+        def leader(arrived):
+            allv = weights_plane.gather_votes(f, arrived)
+            train_set = tally_votes(allv)
+            set_gang_expectations(f, set(train_set), set(train_set))
+            return train_set
+
+        state.train_set = list(f.gang_run(state.addr, votes, leader))
+        logger.info(state.addr, f"🚂 Train set of {len(state.train_set)} nodes: {state.train_set}")
+        if state.addr in state.train_set:
+            return StageFactory.get_stage("TrainStage", "collective")
+        return StageFactory.get_stage("WaitAggregatedModelsStage", "collective")

@@ -1,0 +1,55 @@
+"""Collective wait (parity target: ``stages/base_node/wait_agg_models_stage.py:40-67``).
+
+A non-trainer contributes weight 0 to the same all-reduce, so collective membership never changes
+while the FedAvg result still only averages the train set (SURVEY §7.4 hard part 1).
+"""
+
+from typing import Optional, Type
+
+from myfyp_amd.parallel import weights_plane
+from myfyp_amd.stages.collective._common import fed
+from myfyp_amd.stages.stage import Stage
+from myfyp_amd.stages.stage_factory import StageFactory
+
+
+def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
+    f = fed()
+    kind = getattr(aggregator, "collective_kind", None)
+    model = learner.get_model()
+    n = model.num_samples if trainer else 0
+    wire = None
+    if trainer and kind != "mean":
+        wire = model.build_copy(params=model.get_parameters(), num_samples=model.num_samples, contributors=list(model.contributors), additional_info=dict(model.additional_info))
+    round_ = state.round
+
+    def leader(arrived):
+        if kind == "mean":
+            total, contributors = weights_plane.aggregate_mean(f, arrived)
+            extra = getattr(aggregator, "proximal_mu", None)
+        else:
+            weights_plane.aggregate_generic(f, arrived, aggregator)
+            extra = None
+        for hook in list(f.round_hooks):
+            hook(round_, f)
+        return extra
+
+    mu = f.gang_run(state.addr, (n, wire), leader)
+    if mu is not None:
+        model.add_info("fedprox", {"mu": mu})
+        learner.update_callbacks_with_model_info()
+    model.set_contribution(list(state.train_set) or [state.addr], max(1, model.num_samples))
+
+
+class WaitAggregatedModelsStage(Stage):
+    @staticmethod
+    def name() -> str:
+        return "WaitAggregatedModelsStage"
+
+    @staticmethod
+    def execute(state=None, communication_protocol=None, learner=None, aggregator=None, **kwargs) -> Optional[Type[Stage]]:
+        if state is None or communication_protocol is None or learner is None or aggregator is None:
+            raise Exception("Invalid parameters on WaitAggregatedModelsStage.")
+        if state.round is None:
+            return None
+        join_aggregation(state, learner, aggregator, trainer=False)
+        return StageFactory.get_stage("GossipModelStage", "collective")
