@@ -157,6 +157,11 @@ def main() -> None:
             t_target, r_target = round_end[r - 1] - t_start, r
             break
     final_acc = mean_acc[max(mean_acc)] if mean_acc else None
+    # per-stage wall-time breakdown of the first local peer (stderr, diagnostics only)
+    tm = logger.get_timings().get(nodes[0].addr, {})
+    brk = {k: round(1000 * float(np.median(v[args.warmup :] or v)), 3) for k, v in tm.items()}
+    print(f"[bench] rank {rank} median ms per call: {json.dumps(brk)} fed: "
+          f"{ {k: round(1000 * float(np.median(v)), 3) for k, v in fed.stats.items()} }", file=sys.stderr, flush=True)
     for n in nodes:
         n.stop()
 

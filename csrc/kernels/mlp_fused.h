@@ -5,6 +5,7 @@
 #include "common.h"
 
 #define MLP_EVAL_CHUNK 512
+#define MLP_MAX_BPAD 256  // largest padded local batch the fused engine supports
 
 struct MLPArgs {
   int P, D0, D1, D2, D3, D0pad;
@@ -37,7 +38,7 @@ struct MLPArgs {
   bf16* H1;   // [P][h1_rows][D1]
   int h1_rows;
   bf16* H1T;  // [P][D1][Bpad]
-  bf16* XT;   // [P][D0pad][Bpad]
+  bf16* XT;   // unused (Xᵀ slabs are staged in LDS by the wgrad kernel)
   bf16* H2T;  // [P][D2][Bpad]
   bf16* dH2T; // [P][D2][Bpad]
   bf16* dH1T; // [P][D1][Bpad]

@@ -38,18 +38,24 @@ __device__ __forceinline__ int64_t sample_index(const MLPArgs& a, bool train, in
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// K1: fc1 forward. grid = (D1/64, rows/(16*MT), P), block = 256 (4 waves: 4 column tiles of 16).
+// K1: fc1 forward. grid = (D1/32, rows/32, P), block = 256.
+//   Block tile = 32 rows × 32 cols (2×2 MFMA tiles); the 4 waves split K (= D0) four ways so
+//   each wave's dependent load chain is ≤ 8 k-steps, with all fragment loads of a chunk hoisted
+//   ahead of its MFMAs (the kernel is load-latency bound: 0.2 GFLOP/step for 8 peers). Partial
+//   accumulators are reduced through LDS; wave 0 runs the epilogue.
 // ---------------------------------------------------------------------------------------------
-template <int MT, bool TRAIN>
+template <bool TRAIN>
 __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base) {
+  constexpr int MT = 2, NT = 2, KCH = 8;
+  __shared__ __attribute__((aligned(16))) float sRed[3][64][MT * NT * 4];
   const int p = blockIdx.z;
   if (!a.active[p]) return;
   const int rows = TRAIN ? rows_valid_train(a, p, step) : rows_valid_eval(a, p, base);
   if (rows == 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 4, c = lane & 15;
-  const int row0 = blockIdx.y * (16 * MT);
-  const int n = blockIdx.x * 64 + wave * 16 + c;  // output column this lane's B-fragment covers
+  const int row0 = blockIdx.y * 32;
+  const int col0 = blockIdx.x * 32;
   const int D0 = a.D0, D1 = a.D1;
   const uint8_t* X = TRAIN ? a.Xp[p] : a.Xtp[p];
 
@@ -61,48 +67,82 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
     avalid[mt] = r < rows;
     arow[mt] = avalid[mt] ? X + sample_index(a, TRAIN, p, step, base, r) * (int64_t)D0 : X;
   }
-  const bf16* wrow = a.shadow + (int64_t)p * a.S + a.off_w1 + (int64_t)n * D0;
-  const bool write_xt = TRAIN && blockIdx.x == 0 && wave == 0;
-  bf16* xt = a.XT + (int64_t)p * a.D0pad * a.Bpad;
+  const bf16* wrow[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) wrow[nt] = a.shadow + (int64_t)p * a.S + a.off_w1 + (int64_t)(col0 + nt * 16 + c) * D0;
 
-  f32x4 acc[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+  // this wave's k-step range
+  const int ksteps = (D0 + 31) / 32;
+  const int per = (ksteps + 3) / 4;
+  const int ks_begin = wave * per;
+  const int ks_end = min(ksteps, ks_begin + per);
 
-  for (int k0 = 0; k0 < D0; k0 += 32) {
-    const int k = k0 + 8 * h;
-    const bool kin = k < D0;
-    const bf16x8 b = kin ? ld8(wrow + k) : zero_bf16x8();
+  f32x4 acc[MT][NT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const bf16x8 av = (kin && avalid[mt]) ? ld8_u8(arow[mt] + k) : zero_bf16x8();
-      if (write_xt && kin) {
-        const int r = row0 + mt * 16 + c;
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xt[(int64_t)(k + j) * a.Bpad + r] = av[j];
-      }
-      acc[mt] = mfma_bf16(av, b, acc[mt]);
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = zero4();
+
+  for (int ks0 = ks_begin; ks0 < ks_end; ks0 += KCH) {
+    bf16x8 af[KCH][MT], bfr[KCH][NT];
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) {
+      const int k = (ks0 + j) * 32 + 8 * h;
+      const bool kin = (ks0 + j) < ks_end && k < D0;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[j][mt] = (kin && avalid[mt]) ? ld8_u8(arow[mt] + k) : zero_bf16x8();
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bfr[j][nt] = kin ? ld8(wrow[nt] + k) : zero_bf16x8();
     }
+#pragma unroll
+    for (int j = 0; j < KCH; ++j)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_bf16(af[j][mt], bfr[j][nt], acc[mt][nt]);
   }
 
+  // cross-wave K reduction
+  if (wave > 0) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sRed[wave - 1][lane][(mt * NT + nt) * 4 + i] = acc[mt][nt][i];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[mt][nt][i] += sRed[w][lane][(mt * NT + nt) * 4 + i];
+
   // epilogue: + b1, ReLU, zero invalid rows; H1 row-major (+ H1ᵀ when training)
-  const int col = blockIdx.x * 64 + wave * 16 + c;
-  const float bias = a.params[(int64_t)p * a.S + a.off_b1 + col];
   bf16* H1 = a.H1 + (int64_t)p * a.h1_rows * D1;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    bf16x4 packed;
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = col0 + nt * 16 + c;
+    const float bias = a.params[(int64_t)p * a.S + a.off_b1 + col];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = row0 + mt * 16 + 4 * h + i;
-      float v = fmaxf(acc[mt][i] + bias, 0.f);
-      if (r >= rows) v = 0.f;
-      packed[i] = (bf16)v;
-      H1[(int64_t)r * D1 + col] = packed[i];
-    }
-    if (TRAIN) {
-      bf16* H1T = a.H1T + (int64_t)p * D1 * a.Bpad;
-      *reinterpret_cast<bf16x4*>(H1T + (int64_t)col * a.Bpad + row0 + mt * 16 + 4 * h) = packed;
+    for (int mt = 0; mt < MT; ++mt) {
+      bf16x4 packed;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = row0 + mt * 16 + 4 * h + i;
+        float v = fmaxf(acc[mt][nt][i] + bias, 0.f);
+        if (r >= rows) v = 0.f;
+        packed[i] = (bf16)v;
+        H1[(int64_t)r * D1 + col] = packed[i];
+      }
+      if (TRAIN) {
+        bf16* H1T = a.H1T + (int64_t)p * D1 * a.Bpad;
+        *reinterpret_cast<bf16x4*>(H1T + (int64_t)col * a.Bpad + row0 + mt * 16 + 4 * h) = packed;
+      }
     }
   }
 }
@@ -138,7 +178,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
 #pragma unroll
   for (int t = 0; t < TP2; ++t) h2[t] = zero4();
   const bf16* arow = H1 + (int64_t)(row0 + c) * D1;
-#pragma unroll 2
+#pragma unroll
   for (int k0 = 0; k0 < D1; k0 += 32) {
     const bf16x8 av = ld8(arow + k0 + 8 * h);
 #pragma unroll
@@ -288,10 +328,24 @@ __device__ __forceinline__ void update_elem(const MLPArgs& a, int64_t idx, float
   a.shadow[idx] = (bf16)w;
 }
 
+// Block decomposition (grid.x): [0, nb1) W1 blocks — 4 tiles sharing one 16-column slab of X
+// (staged once, transposed to bf16 in LDS) and 4 different 16-row blocks of W1; [nb1, nb1+nb2)
+// W2 blocks — 4 tiles each; [nb1+nb2, +nb3) W3 blocks. Bias gradients are row sums of the A
+// fragments and are produced by the waves whose column slab is 0.
+__device__ __forceinline__ float frag_sum(const bf16x8& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)v[j];
+  return s;
+}
+
 __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
+  constexpr int LDX = MLP_MAX_BPAD + 8;
+  __shared__ __attribute__((aligned(16))) bf16 sX[16 * LDX];
   const int p = blockIdx.z;
   if (!a.active[p]) return;
-  if (rows_valid_train(a, p, step) == 0) return;
+  const int rows = rows_valid_train(a, p, step);
+  if (rows == 0) return;
   float bc1, bc2s;
   step_bias_corr(a, p, step, bc1, bc2s);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -299,39 +353,68 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   const int D0 = a.D0, D1 = a.D1, D2 = a.D2, D3 = a.D3, Bp = a.Bpad;
   const int64_t pS = (int64_t)p * a.S;
   const int tiles_i = (D0 + 15) / 16;
-  const int tiles_w1 = (D1 / 16) * tiles_i;
-  const int nb1 = (tiles_w1 + 3) / 4;
-  const int tiles_w2 = (D2 / 16) * (D1 / 16);
-  const int nb2 = tiles_w2 / 4;
+  const int obg = D1 / 64;  // groups of 4 row-blocks of W1
+  const int nb1 = tiles_i * obg;
+  const int nb2 = (D2 / 16) * (D1 / 16) / 4;
   const int b = blockIdx.x;
 
   if (b < nb1) {
-    // ---- W1 tile: dW1[o][i] = Σ_b dH1ᵀ[o][b] · Xᵀ[i][b]
-    const int tile = b * 4 + wave;
-    if (tile >= tiles_w1) return;
-    const int ob = tile / tiles_i, ib = tile % tiles_i;
+    const int ib = b / obg, og = b % obg;
+    const int ob = og * 4 + wave;
+    // stage Xᵀ slab: sX[j][r] = X[sample(r)][ib*16 + j] (bf16), zero for invalid rows / cols ≥ D0
+    for (int r = threadIdx.x; r < Bp; r += 256) {
+      uint4 v = {0u, 0u, 0u, 0u};
+      const int i0 = ib * 16;
+      if (r < rows) {
+        const uint8_t* src = a.Xp[p] + sample_index(a, true, p, step, 0, r) * (int64_t)D0 + i0;
+        if (i0 + 16 <= D0) {
+          const uint2 lo = *reinterpret_cast<const uint2*>(src), hi = *reinterpret_cast<const uint2*>(src + 8);
+          v = uint4{lo.x, lo.y, hi.x, hi.y};
+        } else {
+          uint8_t tmp[16] = {0};
+          for (int j = 0; j < 16 && i0 + j < D0; ++j) tmp[j] = src[j];
+          v = *reinterpret_cast<const uint4*>(tmp);
+        }
+      }
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sX[j * LDX + r] = (bf16)(float)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu);
+    }
+    __syncthreads();
     const bf16* A = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)(ob * 16 + c) * Bp;
-    const bf16* Bm = a.XT + (int64_t)p * a.D0pad * Bp + (int64_t)(ib * 16 + c) * Bp;
     f32x4 acc = zero4();
-    for (int k0 = 0; k0 < Bp; k0 += 32) acc = mfma_bf16(ld8(A + k0 + 8 * h), ld8(Bm + k0 + 8 * h), acc);
+    float bsum = 0.f;
+    for (int k0 = 0; k0 < Bp; k0 += 32) {
+      const bf16x8 av = ld8(A + k0 + 8 * h);
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[c * LDX + k0 + 8 * h]);
+      if (ib == 0) bsum += frag_sum(av);
+      acc = mfma_bf16(av, bv, acc);
+    }
     const int i = ib * 16 + c;
     if (i < D0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = ob * 16 + 4 * h + r;
-        update_elem(a, pS + a.off_w1 + (int64_t)o * D0 + i, acc[r], bc1, bc2s);
-      }
+      for (int r = 0; r < 4; ++r) update_elem(a, pS + a.off_w1 + (int64_t)(ob * 16 + 4 * h + r) * D0 + i, acc[r], bc1, bc2s);
+    }
+    if (ib == 0) {
+      bsum += __shfl_xor(bsum, 16);
+      bsum += __shfl_xor(bsum, 32);
+      if (h == 0) update_elem(a, pS + a.off_b1 + ob * 16 + c, bsum, bc1, bc2s);
     }
     return;
   }
   if (b < nb1 + nb2) {
-    // ---- W2 tile: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b]; also refresh W2ᵀ shadow
+    // ---- W2 tile: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b]; also refresh the W2ᵀ shadow
     const int tile = (b - nb1) * 4 + wave;
     const int ob = tile / (D1 / 16), ib = tile % (D1 / 16);
     const bf16* A = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)(ob * 16 + c) * Bp;
     const bf16* Bm = a.H1T + (int64_t)p * D1 * Bp + (int64_t)(ib * 16 + c) * Bp;
     f32x4 acc = zero4();
-    for (int k0 = 0; k0 < Bp; k0 += 32) acc = mfma_bf16(ld8(A + k0 + 8 * h), ld8(Bm + k0 + 8 * h), acc);
+    float bsum = 0.f;
+    for (int k0 = 0; k0 < Bp; k0 += 32) {
+      const bf16x8 av = ld8(A + k0 + 8 * h);
+      if (ib == 0) bsum += frag_sum(av);
+      acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
+    }
     const int o1 = ib * 16 + c;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -340,52 +423,34 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
       update_elem(a, idx, acc[r], bc1, bc2s);
       a.w2t[(int64_t)p * D1 * D2 + (int64_t)o1 * D2 + o2] = a.shadow[idx];
     }
+    if (ib == 0) {
+      bsum += __shfl_xor(bsum, 16);
+      bsum += __shfl_xor(bsum, 32);
+      if (h == 0) update_elem(a, pS + a.off_b2 + ob * 16 + c, bsum, bc1, bc2s);
+    }
     return;
   }
-  // ---- biases + W3 (one block per peer)
-  const int tid = threadIdx.x;
-  for (int o = tid; o < D1; o += 256) {
-    const bf16* row = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)o * Bp;
-    float s = 0.f;
-    for (int k = 0; k < Bp; k += 8) {
-      const bf16x8 v = ld8(row + k);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)v[j];
-    }
-    update_elem(a, pS + a.off_b1 + o, s, bc1, bc2s);
+  // ---- W3 tiles: dW3[cls][o2] = Σ_b dlogitsᵀ[cls][b] · H2ᵀ[o2][b]  (classes padded to 16)
+  const int t = (b - nb1 - nb2) * 4 + wave;
+  if (t >= D2 / 16) return;
+  const bf16* A = a.dlogT + (int64_t)p * 16 * Bp + (int64_t)c * Bp;
+  const bf16* Bm = a.H2T + (int64_t)p * D2 * Bp + (int64_t)(t * 16 + c) * Bp;
+  f32x4 acc = zero4();
+  float bsum = 0.f;
+  for (int k0 = 0; k0 < Bp; k0 += 32) {
+    const bf16x8 av = ld8(A + k0 + 8 * h);
+    if (t == 0) bsum += frag_sum(av);
+    acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
   }
-  for (int o = tid; o < D2; o += 256) {
-    const bf16* row = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)o * Bp;
-    float s = 0.f;
-    for (int k = 0; k < Bp; k += 8) {
-      const bf16x8 v = ld8(row + k);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)v[j];
-    }
-    update_elem(a, pS + a.off_b2 + o, s, bc1, bc2s);
+  for (int r = 0; r < 4; ++r) {
+    const int cls = 4 * h + r;
+    if (cls < D3) update_elem(a, pS + a.off_w3 + (int64_t)cls * D2 + t * 16 + c, acc[r], bc1, bc2s);
   }
-  for (int e = tid; e < D3 * D2 + D3; e += 256) {
-    float s = 0.f;
-    if (e < D3 * D2) {
-      const int cls = e / D2, o2 = e % D2;
-      const bf16* dl = a.dlogT + (int64_t)p * 16 * Bp + (int64_t)cls * Bp;
-      const bf16* h2 = a.H2T + (int64_t)p * D2 * Bp + (int64_t)o2 * Bp;
-      for (int k = 0; k < Bp; k += 8) {
-        const bf16x8 x = ld8(dl + k), y = ld8(h2 + k);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)x[j] * (float)y[j];
-      }
-      update_elem(a, pS + a.off_w3 + e, s, bc1, bc2s);
-    } else {
-      const int cls = e - D3 * D2;
-      const bf16* dl = a.dlogT + (int64_t)p * 16 * Bp + (int64_t)cls * Bp;
-      for (int k = 0; k < Bp; k += 8) {
-        const bf16x8 x = ld8(dl + k);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)x[j];
-      }
-      update_elem(a, pS + a.off_b3 + cls, s, bc1, bc2s);
-    }
+  if (t == 0) {
+    bsum += __shfl_xor(bsum, 16);
+    bsum += __shfl_xor(bsum, 32);
+    if (h == 0 && c < D3) update_elem(a, pS + a.off_b3 + c, bsum, bc1, bc2s);
   }
 }
 
@@ -439,16 +504,16 @@ static void launch_head_dispatch(const MLPArgs& a, int step, int base, bool trai
 }
 
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s) {
-  hipLaunchKernelGGL((mlp_fc1_fwd<2, true>), dim3(a.D1 / 64, a.Bpad / 32, a.P), dim3(256), 0, s, a, step, 0);
+  hipLaunchKernelGGL((mlp_fc1_fwd<true>), dim3(a.D1 / 32, a.Bpad / 32, a.P), dim3(256), 0, s, a, step, 0);
   launch_head_dispatch(a, step, 0, true, a.Bpad, s);
-  const int tiles_i = (a.D0 + 15) / 16;
-  const int nb1 = ((a.D1 / 16) * tiles_i + 3) / 4;
+  const int nb1 = ((a.D0 + 15) / 16) * (a.D1 / 64);
   const int nb2 = (a.D2 / 16) * (a.D1 / 16) / 4;
-  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + 1, 1, a.P), dim3(256), 0, s, a, step);
+  const int nb3 = (a.D2 / 16 + 3) / 4;
+  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), 0, s, a, step);
 }
 
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s) {
-  hipLaunchKernelGGL((mlp_fc1_fwd<2, false>), dim3(a.D1 / 64, MLP_EVAL_CHUNK / 32, a.P), dim3(256), 0, s, a, 0, base);
+  hipLaunchKernelGGL((mlp_fc1_fwd<false>), dim3(a.D1 / 32, MLP_EVAL_CHUNK / 32, a.P), dim3(256), 0, s, a, 0, base);
   launch_head_dispatch(a, 0, base, false, MLP_EVAL_CHUNK, s);
 }
 

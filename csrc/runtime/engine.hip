@@ -143,7 +143,7 @@ int myfyp_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_
 int mlp_shape_ok(int D0, int D1, int D2, int D3) { return mlp_shape_supported(D0, D1, D2, D3) ? 1 : 0; }
 
 void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
-  if (!mlp_shape_supported(D0, D1, D2, D3) || P < 1 || B < 1 || B > 1024) {
+  if (!mlp_shape_supported(D0, D1, D2, D3) || P < 1 || B < 1 || (B + 31) / 32 * 32 > MLP_MAX_BPAD) {
     g_last_error = "unsupported MLP shape";
     return nullptr;
   }
@@ -167,7 +167,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
   int rc = 0;
   rc |= e->alloc(&p, (size_t)P * a.h1_rows * D1 * 2); a.H1 = (bf16*)p;
   rc |= e->alloc(&p, (size_t)P * D1 * bp * 2); a.H1T = (bf16*)p;
-  rc |= e->alloc(&p, (size_t)P * a.D0pad * bp * 2); a.XT = (bf16*)p;
+  a.XT = nullptr;
   rc |= e->alloc(&p, (size_t)P * D2 * bp * 2); a.H2T = (bf16*)p;
   rc |= e->alloc(&p, (size_t)P * D2 * bp * 2); a.dH2T = (bf16*)p;
   rc |= e->alloc(&p, (size_t)P * D1 * bp * 2); a.dH1T = (bf16*)p;

@@ -137,6 +137,9 @@ def test_fused_mlp_engine_matches_autograd(dev, B):
     learners, refs = [], []
     for i in range(2):
         m = MLP(seed=10 + i)
+        with torch.no_grad():  # small weights: unsaturated softmax keeps bf16/fp32 trajectories close
+            for prm in m.parameters():
+                prm.mul_(0.05)
         m.optimizer_spec = lambda: {"name": "sgd", "lr": lr}
         refs.append(copy.deepcopy(m).to(dev))
         learners.append(TorchLearner(TorchModel(m), parts[i], f"p{i}", batch_size=B))
@@ -175,4 +178,54 @@ def test_fused_mlp_engine_matches_autograd(dev, B):
             ref_loss = torch.nn.functional.cross_entropy(out, yt).item()
         assert abs(loss - ref_loss) / max(1e-6, abs(ref_loss)) < 0.05
         assert conf.sum() == xt.shape[0]
+    MLPGroup.reset_all()
+
+
+def test_fused_mlp_single_step_gradients(dev):
+    """Per-parameter gradient of ONE fused step (SGD, grad = Δw/lr) vs autograd, 3 peers, B=40."""
+    import copy
+    import threading
+
+    import torch.nn.functional as F
+
+    from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
+    from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
+    from myfyp_amd.learning.frameworks.torch import TorchLearner, TorchModel
+    from myfyp_amd.models import MLP
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+    from myfyp_amd.settings import Settings
+
+    MLPGroup.reset_all()
+    Settings.GANG_WINDOW = 5.0
+    B, P, lr = 40, 3, 1e-3
+    parts = synthetic_mnist(B * P, 60, seed=11).generate_partitions(P, RandomIIDPartitionStrategy)
+    learners, refs = [], []
+    for i in range(P):
+        m = MLP(seed=20 + i)
+        m.optimizer_spec = lambda: {"name": "sgd", "lr": lr}
+        refs.append(copy.deepcopy(m).to(dev))
+        learners.append(TorchLearner(TorchModel(m), parts[i], f"g{i}", batch_size=B))
+    g = learners[0]._engine.group
+    n = [parts[i].get_num_samples() for i in range(P)]
+
+    def perm_fn(ep):
+        out = torch.zeros(g.capacity, g.nmax, dtype=torch.int32)
+        for i, l in enumerate(learners):
+            out[l._engine.slot, : n[i]] = torch.arange(n[i], dtype=torch.int32)
+        return out.to(dev)
+
+    g.perm_fn = perm_fn
+    p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
+    ts = [threading.Thread(target=l.fit) for l in learners]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for i in range(P):
+        x, y = learners[i].device_data(True)
+        refs[i].zero_grad()
+        F.cross_entropy(refs[i](x[: min(B, n[i])]), y[: min(B, n[i])]).backward()
+        for (name, pe), pr, pz in zip(learners[i].model.get_model().named_parameters(), refs[i].parameters(), p0[i]):
+            ge, gr = (pz - pe.detach()) / lr, pr.grad
+            cos = F.cosine_similarity(ge.flatten(), gr.flatten(), dim=0).item()
+            rel = ((ge - gr).norm() / (gr.norm() + 1e-12)).item()
+            assert cos > 0.995 and rel < 0.08, f"peer {i} {name}: cos {cos:.4f} rel {rel:.4f}"
     MLPGroup.reset_all()
