@@ -81,10 +81,11 @@ __device__ __forceinline__ void opt_update(const OptParams& o, float g, float& w
   if (cg != nullptr) g += cg[idx] - cl[idx];
   if (o.weight_decay != 0.f) g += o.weight_decay * w;
   if (o.kind == 0) {
-    m = o.beta1 * m + (1.f - o.beta1) * g;
-    v = o.beta2 * v + (1.f - o.beta2) * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + o.eps;
-    w -= (o.lr / bc1) * m / denom;
+    m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
+    v = fmaf(o.beta2, v, (1.f - o.beta2) * g * g);
+    // torch.optim.Adam: w -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+    const float denom = sqrtf(v) * (1.f / bc2_sqrt) + o.eps;
+    w -= (o.lr / bc1) * __fdiv_rn(m, denom);
   } else {
     if (o.momentum != 0.f) {
       m = o.momentum * m + g;

@@ -32,6 +32,7 @@ struct MLPArgs {
   const int* const* Ytp;
   const int* n_t;
   // control
+  const int4* ctl;    // [P] {active, n_train, optimizer steps already taken (t0), n_test} — one scalar load
   const int* active;  // [P]
   const int* t0;      // [P] optimizer steps each peer already took in this fit
   // workspace

@@ -19,14 +19,21 @@
 
 namespace {
 
-__device__ __forceinline__ int rows_valid_train(const MLPArgs& a, int p, int step) {
-  int r = a.n[p] - step * a.B;
+__device__ __forceinline__ int rows_valid_train(const MLPArgs& a, const int4& ctl, int step) {
+  int r = ctl.y - step * a.B;
   return r < 0 ? 0 : (r > a.B ? a.B : r);
 }
 
-__device__ __forceinline__ int rows_valid_eval(const MLPArgs& a, int p, int base) {
-  int r = a.n_t[p] - base;
+__device__ __forceinline__ int rows_valid_eval(const MLPArgs& a, const int4& ctl, int base) {
+  int r = ctl.w - base;
   return r < 0 ? 0 : (r > MLP_EVAL_CHUNK ? MLP_EVAL_CHUNK : r);
+}
+
+// rows of this peer in this step (0 = inactive peer or exhausted data)
+template <bool TRAIN>
+__device__ __forceinline__ int peer_rows(const MLPArgs& a, const int4& ctl, int step, int base) {
+  if (!ctl.x) return 0;
+  return TRAIN ? rows_valid_train(a, ctl, step) : rows_valid_eval(a, ctl, base);
 }
 
 // local sample index of batch row r
@@ -49,14 +56,17 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
   constexpr int MT = 2, NT = 2, KCH = 8;
   __shared__ __attribute__((aligned(16))) float sRed[3][64][MT * NT * 4];
   const int p = blockIdx.z;
-  if (!a.active[p]) return;
-  const int rows = TRAIN ? rows_valid_train(a, p, step) : rows_valid_eval(a, p, base);
+  const int4 ctl = a.ctl[p];
+  const int rows = peer_rows<TRAIN>(a, ctl, step, base);
   if (rows == 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 4, c = lane & 15;
   const int row0 = blockIdx.y * 32;
   const int col0 = blockIdx.x * 32;
   const int D0 = a.D0, D1 = a.D1;
+  float bias[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) bias[nt] = a.params[(int64_t)p * a.S + a.off_b1 + col0 + nt * 16 + c];
   const uint8_t* X = TRAIN ? a.Xp[p] : a.Xtp[p];
 
   const uint8_t* arow[MT];
@@ -127,14 +137,13 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int col = col0 + nt * 16 + c;
-    const float bias = a.params[(int64_t)p * a.S + a.off_b1 + col];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       bf16x4 packed;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = row0 + mt * 16 + 4 * h + i;
-        float v = fmaxf(acc[mt][nt][i] + bias, 0.f);
+        float v = fmaxf(acc[mt][nt][i] + bias[nt], 0.f);
         if (r >= rows) v = 0.f;
         packed[i] = (bf16)v;
         H1[(int64_t)r * D1 + col] = packed[i];
@@ -153,15 +162,18 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
 template <int TP1, int TP2, bool TRAIN>
 __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   constexpr int D1 = TP1 * 64, D2 = TP2 * 64;
-  constexpr int LD2 = D2 + 8;  // padded LDS row (bf16) to spread banks
+  constexpr int LD1 = D1 + 8, LD2 = D2 + 8;  // padded LDS rows (bf16) to spread banks
   constexpr int LDD = 32 + 8;
+  constexpr int KS1 = D1 / 32, KS2 = D2 / 32;
+  __shared__ __attribute__((aligned(16))) bf16 sH1[16 * LD1];
   __shared__ __attribute__((aligned(16))) bf16 sH2[16 * LD2];
   __shared__ __attribute__((aligned(16))) bf16 sDH2[16 * LD2];
   __shared__ __attribute__((aligned(16))) bf16 sDlog[16 * LDD];
+  __shared__ __attribute__((aligned(16))) bf16 sW3[16 * LD2];
 
   const int p = blockIdx.z;
-  if (!a.active[p]) return;
-  const int rows = TRAIN ? rows_valid_train(a, p, step) : rows_valid_eval(a, p, base);
+  const int4 ctl = a.ctl[p];
+  const int rows = peer_rows<TRAIN>(a, ctl, step, base);
   if (rows == 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 4, c = lane & 15;
@@ -169,34 +181,89 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   const int D3 = a.D3;
   const int64_t pS = (int64_t)p * a.S;
   const bf16* H1 = a.H1 + (int64_t)p * a.h1_rows * D1;
+  const bool cin = c < D3;
+  // W3 (≤16 × D2 bf16) staged once in LDS with vector loads; rows ≥ D3 are zero
+  for (int e = threadIdx.x; e < 16 * (D2 / 8); e += 256) {
+    const int r = e / (D2 / 8), q = e % (D2 / 8);
+    *reinterpret_cast<bf16x8*>(&sW3[r * LD2 + q * 8]) = r < D3 ? ld8(a.shadow + pS + a.off_w3 + (int64_t)r * D2 + q * 8) : zero_bf16x8();
+  }
 
-  // zero the dlogits tile (k columns 16..31 stay zero = K padding)
+  // ---- issue every independent global load up front (the kernel is latency bound)
+  bf16x8 a1[KS1];
+  const bf16* arow = H1 + (int64_t)(row0 + c) * D1;
+#pragma unroll
+  for (int k = 0; k < KS1; ++k) a1[k] = ld8(arow + k * 32 + 8 * h);
+  bf16x8 w2f[KS1][TP2];
+#pragma unroll
+  for (int k = 0; k < KS1; ++k)
+#pragma unroll
+    for (int t = 0; t < TP2; ++t) w2f[k][t] = ld8(a.shadow + pS + a.off_w2 + (int64_t)((wave + 4 * t) * 16 + c) * D1 + k * 32 + 8 * h);
+  float b2v[TP2];
+#pragma unroll
+  for (int t = 0; t < TP2; ++t) b2v[t] = a.params[pS + a.off_b2 + (wave + 4 * t) * 16 + c];
+  // wave 0: logits operands + labels
+  bf16x8 w3f[KS2];
+  float b3 = 0.f;
+  int ylab[4] = {-1, -1, -1, -1};
+  if (wave == 0) {
+    b3 = cin ? a.params[pS + a.off_b3 + c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int grow = row0 + 4 * h + i;
+      if (grow < rows) {
+        const int64_t idx = sample_index(a, TRAIN, p, step, base, grow);
+        ylab[i] = TRAIN ? a.Yp[p][idx] : a.Ytp[p][idx];
+      }
+    }
+  }
+  // training: W3 columns for dH2 and W2ᵀ fragments for dH1
+  bf16x8 w3c[TP2];
+  bf16x8 w2tf[TRAIN ? TP1 : 1][TRAIN ? KS2 : 1];
+  if (TRAIN) {
+    const bf16* w2t = a.w2t + (int64_t)p * D1 * D2;
+#pragma unroll
+    for (int t = 0; t < (TRAIN ? TP1 : 1); ++t)
+#pragma unroll
+      for (int k = 0; k < (TRAIN ? KS2 : 1); ++k) w2tf[t][k] = ld8(w2t + (int64_t)((wave + 4 * t) * 16 + c) * D2 + k * 32 + 8 * h);
+  }
+
+  // stage H1 rows in LDS (mask for dH1) and zero the dlogits tile (k 16..31 = K padding)
+  if (TRAIN && wave == 0) {
+#pragma unroll
+    for (int k = 0; k < KS1; ++k) *reinterpret_cast<bf16x8*>(&sH1[c * LD1 + k * 32 + 8 * h]) = a1[k];
+  }
   for (int i = threadIdx.x; i < 16 * LDD; i += 256) sDlog[i] = (bf16)0.f;
+
+  __syncthreads();  // sW3 ready
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < KS2; ++k) w3f[k] = *reinterpret_cast<const bf16x8*>(&sW3[c * LD2 + k * 32 + 8 * h]);
+  }
+  if (TRAIN) {
+#pragma unroll
+    for (int t = 0; t < TP2; ++t) {
+      const int n = (wave + 4 * t) * 16 + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w3c[t][j] = (8 * h + j) < 16 ? sW3[(8 * h + j) * LD2 + n] : (bf16)0.f;
+    }
+  }
 
   // ---- H2 = relu(H1 · W2ᵀ + b2): wave owns column tiles {wave + 4*t}
   f32x4 h2[TP2];
 #pragma unroll
   for (int t = 0; t < TP2; ++t) h2[t] = zero4();
-  const bf16* arow = H1 + (int64_t)(row0 + c) * D1;
 #pragma unroll
-  for (int k0 = 0; k0 < D1; k0 += 32) {
-    const bf16x8 av = ld8(arow + k0 + 8 * h);
+  for (int k = 0; k < KS1; ++k)
 #pragma unroll
-    for (int t = 0; t < TP2; ++t) {
-      const int n = (wave + 4 * t) * 16 + c;
-      const bf16x8 bv = ld8(a.shadow + pS + a.off_w2 + (int64_t)n * D1 + k0 + 8 * h);
-      h2[t] = mfma_bf16(av, bv, h2[t]);
-    }
-  }
+    for (int t = 0; t < TP2; ++t) h2[t] = mfma_bf16(a1[k], w2f[k][t], h2[t]);
 #pragma unroll
   for (int t = 0; t < TP2; ++t) {
     const int col = (wave + 4 * t) * 16 + c;
-    const float bias = a.params[pS + a.off_b2 + col];
     bf16x4 packed;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = 4 * h + i;
-      float v = fmaxf(h2[t][i] + bias, 0.f);
+      float v = fmaxf(h2[t][i] + b2v[t], 0.f);
       if (row0 + r >= rows) v = 0.f;
       h2[t][i] = v;
       packed[i] = (bf16)v;
@@ -209,33 +276,20 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   // ---- logits, log-softmax, NLL, argmax, dlogits (wave 0)
   if (wave == 0) {
     f32x4 lg = zero4();
-    const bool cin = c < D3;
 #pragma unroll
-    for (int k0 = 0; k0 < D2; k0 += 32) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(&sH2[c * LD2 + k0 + 8 * h]);
-      const bf16x8 bv = cin ? ld8(a.shadow + pS + a.off_w3 + (int64_t)c * D2 + k0 + 8 * h) : zero_bf16x8();
-      lg = mfma_bf16(av, bv, lg);
-    }
-    const float b3 = cin ? a.params[pS + a.off_b3 + c] : 0.f;
+    for (int k = 0; k < KS2; ++k) lg = mfma_bf16(*reinterpret_cast<const bf16x8*>(&sH2[c * LD2 + k * 32 + 8 * h]), w3f[k], lg);
     float loss_part = 0.f;
     int correct_part = 0;
     bf16x4 dpack;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = 4 * h + i;
-      const int grow = row0 + r;
-      const bool rvalid = grow < rows;
+      const int y = ylab[i];
+      const bool rvalid = y >= 0;
       const float logit = cin ? lg[i] + b3 : -INFINITY;
       const float mx = warp_max16(logit);
       const float se = warp_sum16(cin ? __expf(logit - mx) : 0.f);
-      const float lse = mx + __logf(se);
-      const float logp = logit - lse;
-      int y = -1;
-      if (rvalid) {
-        const int64_t idx = sample_index(a, TRAIN, p, step, base, grow);
-        y = TRAIN ? a.Yp[p][idx] : a.Ytp[p][idx];
-      }
-      // argmax (first max), reduced over the 16 lanes of this row
+      const float logp = logit - (mx + __logf(se));
       int cand = (cin && logit == mx) ? c : 16;
       cand = min(cand, __shfl_xor(cand, 1));
       cand = min(cand, __shfl_xor(cand, 2));
@@ -244,7 +298,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
       if (rvalid && c == y) loss_part -= logp;
       if (rvalid && c == 0) {
         correct_part += (cand == y);
-        if (!TRAIN && a.conf != nullptr && y >= 0 && y < 16 && cand < 16) atomicAdd(&a.conf[(p * 16 + y) * 16 + cand], 1);
+        if (!TRAIN && a.conf != nullptr && y < 16 && cand < 16) atomicAdd(&a.conf[(p * 16 + y) * 16 + cand], 1);
       }
       float d = 0.f;
       if (TRAIN && rvalid && cin) d = (__expf(logp) - (c == y ? 1.f : 0.f)) / (float)rows;
@@ -264,22 +318,15 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
 
   // ---- dH2 = dlogits · W3 ⊙ [H2 > 0]   (K = 16 classes, padded to 32)
   {
-    bf16x8 av = *reinterpret_cast<const bf16x8*>(&sDlog[c * LDD + 8 * h]);
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(&sDlog[c * LDD + 8 * h]);
 #pragma unroll
     for (int t = 0; t < TP2; ++t) {
       const int n = (wave + 4 * t) * 16 + c;
-      bf16x8 bv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * h + j;
-        bv[j] = k < D3 ? a.shadow[pS + a.off_w3 + (int64_t)k * D2 + n] : (bf16)0.f;
-      }
-      f32x4 acc = mfma_bf16(av, bv, zero4());
+      const f32x4 acc = mfma_bf16(av, w3c[t], zero4());
       bf16x4 packed;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float v = h2[t][i] > 0.f ? acc[i] : 0.f;
-        packed[i] = (bf16)v;
+        packed[i] = (bf16)(h2[t][i] > 0.f ? acc[i] : 0.f);
         sDH2[(4 * h + i) * LD2 + n] = packed[i];
       }
       *reinterpret_cast<bf16x4*>(a.dH2T + (int64_t)p * D2 * a.Bpad + (int64_t)n * a.Bpad + row0 + 4 * h) = packed;
@@ -287,24 +334,19 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   }
   __syncthreads();
 
-  // ---- dH1 = dH2 · W2 ⊙ [H1 > 0]   (B operand from the transposed shadow W2ᵀ [D1][D2])
-  const bf16* w2t = a.w2t + (int64_t)p * D1 * D2;
+  // ---- dH1 = dH2 · W2 ⊙ [H1 > 0]   (B operand = W2ᵀ shadow, prefetched)
+  bf16x8 adh[KS2];
+#pragma unroll
+  for (int k = 0; k < KS2; ++k) adh[k] = *reinterpret_cast<const bf16x8*>(&sDH2[c * LD2 + k * 32 + 8 * h]);
 #pragma unroll
   for (int t = 0; t < TP1; ++t) {
     const int n = (wave + 4 * t) * 16 + c;
     f32x4 acc = zero4();
 #pragma unroll
-    for (int k0 = 0; k0 < D2; k0 += 32) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(&sDH2[c * LD2 + k0 + 8 * h]);
-      const bf16x8 bv = ld8(w2t + (int64_t)n * D2 + k0 + 8 * h);
-      acc = mfma_bf16(av, bv, acc);
-    }
+    for (int k = 0; k < KS2; ++k) acc = mfma_bf16(adh[k], w2tf[TRAIN ? t : 0][TRAIN ? k : 0], acc);
     bf16x4 packed;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float h1 = (float)H1[(int64_t)(row0 + 4 * h + i) * D1 + n];
-      packed[i] = (bf16)(h1 > 0.f ? acc[i] : 0.f);
-    }
+    for (int i = 0; i < 4; ++i) packed[i] = (bf16)((float)sH1[(4 * h + i) * LD1 + n] > 0.f ? acc[i] : 0.f);
     *reinterpret_cast<bf16x4*>(a.dH1T + (int64_t)p * D1 * a.Bpad + (int64_t)n * a.Bpad + row0 + 4 * h) = packed;
   }
 }
@@ -312,8 +354,8 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
 // ---------------------------------------------------------------------------------------------
 // K3: weight gradients + optimizer. grid = (nb_w1 + nb_w2 + 1, 1, P), block = 256.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void step_bias_corr(const MLPArgs& a, int p, int step, float& bc1, float& bc2s) {
-  const int t = a.t0[p] + step + 1;
+__device__ __forceinline__ void step_bias_corr(const MLPArgs& a, const int4& ctl, int step, float& bc1, float& bc2s) {
+  const int t = ctl.z + step + 1;
   bc1 = 1.f - __powf(a.opt.beta1, (float)t);
   bc2s = sqrtf(1.f - __powf(a.opt.beta2, (float)t));
 }
@@ -328,10 +370,13 @@ __device__ __forceinline__ void update_elem(const MLPArgs& a, int64_t idx, float
   a.shadow[idx] = (bf16)w;
 }
 
-// Block decomposition (grid.x): [0, nb1) W1 blocks — 4 tiles sharing one 16-column slab of X
-// (staged once, transposed to bf16 in LDS) and 4 different 16-row blocks of W1; [nb1, nb1+nb2)
-// W2 blocks — 4 tiles each; [nb1+nb2, +nb3) W3 blocks. Bias gradients are row sums of the A
-// fragments and are produced by the waves whose column slab is 0.
+// Block decomposition (grid.x): [0, nb1) W1 blocks — a 16-row × 64-column tile of W1 (4 waves ×
+// 16 columns) whose X slab (64 columns × batch) is staged once, transposed to bf16, in LDS;
+// [nb1, nb1+nb2) W2 blocks — 16 × 64 tiles; [nb1+nb2, +nb3) W3 blocks. After the MFMAs every block
+// re-lays its fp32 gradient tile out through LDS so that each thread updates 4 consecutive
+// elements (float4): a wave instruction then covers 4 rows × 256 contiguous bytes of params/m/v
+// (coalesced optimizer traffic — the dominant HBM/MALL stream of a step). Bias gradients are row
+// sums of A fragments, produced by the blocks whose column group is 0.
 __device__ __forceinline__ float frag_sum(const bf16x8& v) {
   float s = 0.f;
 #pragma unroll
@@ -339,46 +384,101 @@ __device__ __forceinline__ float frag_sum(const bf16x8& v) {
   return s;
 }
 
+// Block-wide vectorised optimizer update of a 16 × 64 tile: thread t owns row t>>4, columns
+// 4*(t&15)..+3 — a wave instruction touches 4 rows × 256 contiguous bytes. The optimizer state is
+// prefetched at block entry (independent of the gradient) so its latency hides under the staging
+// and the MFMAs; the gradient tile arrives through LDS (sG, fp32, row stride 68).
+struct TileState {
+  float4 w, m, v;
+  int64_t idx;
+  bool vec, live;
+};
+
+__device__ __forceinline__ TileState tile_prefetch(const MLPArgs& a, int64_t base, int ld, int row0, int col0, int ncols) {
+  TileState st;
+  const int tid = threadIdx.x;
+  const int r = tid >> 4, c4 = (tid & 15) * 4;
+  const int col = col0 + c4;
+  st.idx = base + (int64_t)(row0 + r) * ld + col;
+  st.live = col < ncols;
+  st.vec = st.live && col + 4 <= ncols && (ld & 3) == 0;
+  if (st.vec) {
+    st.w = *reinterpret_cast<const float4*>(a.params + st.idx);
+    st.m = *reinterpret_cast<const float4*>(a.m + st.idx);
+    st.v = a.opt.kind == 0 ? *reinterpret_cast<const float4*>(a.v + st.idx) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  return st;
+}
+
+__device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st, const float* sG, int row0, int col0, int ncols, float bc1, float bc2s,
+                                           bool w2t_refresh, int p) {
+  if (!st.live) return;
+  const int tid = threadIdx.x;
+  const int r = tid >> 4, c4 = (tid & 15) * 4;
+  const int col = col0 + c4;
+  const float* g = sG + r * 68 + c4;
+  const int64_t idx = st.idx;
+  if (st.vec) {
+    float wv[4] = {st.w.x, st.w.y, st.w.z, st.w.w}, mv[4] = {st.m.x, st.m.y, st.m.z, st.m.w}, vv[4] = {st.v.x, st.v.y, st.v.z, st.v.w};
+    bf16x4 sh;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      opt_update(a.opt, g[j], wv[j], mv[j], vv[j], bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
+      sh[j] = (bf16)wv[j];
+    }
+    *reinterpret_cast<float4*>(a.params + idx) = float4{wv[0], wv[1], wv[2], wv[3]};
+    *reinterpret_cast<float4*>(a.m + idx) = float4{mv[0], mv[1], mv[2], mv[3]};
+    if (a.opt.kind == 0) *reinterpret_cast<float4*>(a.v + idx) = float4{vv[0], vv[1], vv[2], vv[3]};
+    *reinterpret_cast<bf16x4*>(a.shadow + idx) = sh;
+    if (w2t_refresh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + row0 + r] = sh[j];
+    }
+  } else {
+    for (int j = 0; j < 4 && col + j < ncols; ++j) {
+      float w = a.params[idx + j], m = a.m[idx + j], v = a.opt.kind == 0 ? a.v[idx + j] : 0.f;
+      opt_update(a.opt, g[j], w, m, v, bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
+      a.params[idx + j] = w;
+      a.m[idx + j] = m;
+      if (a.opt.kind == 0) a.v[idx + j] = v;
+      a.shadow[idx + j] = (bf16)w;
+      if (w2t_refresh) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + row0 + r] = (bf16)w;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   constexpr int LDX = MLP_MAX_BPAD + 8;
-  __shared__ __attribute__((aligned(16))) bf16 sX[16 * LDX];
+  __shared__ __attribute__((aligned(16))) bf16 sX[64 * LDX];
+  __shared__ __attribute__((aligned(16))) float sG[16 * 68];
   const int p = blockIdx.z;
-  if (!a.active[p]) return;
-  const int rows = rows_valid_train(a, p, step);
+  const int4 ctl = a.ctl[p];
+  const int rows = peer_rows<true>(a, ctl, step, 0);
   if (rows == 0) return;
   float bc1, bc2s;
-  step_bias_corr(a, p, step, bc1, bc2s);
+  step_bias_corr(a, ctl, step, bc1, bc2s);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 4, c = lane & 15;
   const int D0 = a.D0, D1 = a.D1, D2 = a.D2, D3 = a.D3, Bp = a.Bpad;
   const int64_t pS = (int64_t)p * a.S;
-  const int tiles_i = (D0 + 15) / 16;
-  const int obg = D1 / 64;  // groups of 4 row-blocks of W1
-  const int nb1 = tiles_i * obg;
-  const int nb2 = (D2 / 16) * (D1 / 16) / 4;
+  const int cg1 = (D0 + 63) / 64;     // 64-column groups of W1
+  const int nb1 = (D1 / 16) * cg1;
+  const int nb2 = (D2 / 16) * (D1 / 64);
   const int b = blockIdx.x;
 
   if (b < nb1) {
-    const int ib = b / obg, og = b % obg;
-    const int ob = og * 4 + wave;
-    // stage Xᵀ slab: sX[j][r] = X[sample(r)][ib*16 + j] (bf16), zero for invalid rows / cols ≥ D0
-    for (int r = threadIdx.x; r < Bp; r += 256) {
-      uint4 v = {0u, 0u, 0u, 0u};
-      const int i0 = ib * 16;
-      if (r < rows) {
-        const uint8_t* src = a.Xp[p] + sample_index(a, true, p, step, 0, r) * (int64_t)D0 + i0;
-        if (i0 + 16 <= D0) {
-          const uint2 lo = *reinterpret_cast<const uint2*>(src), hi = *reinterpret_cast<const uint2*>(src + 8);
-          v = uint4{lo.x, lo.y, hi.x, hi.y};
-        } else {
-          uint8_t tmp[16] = {0};
-          for (int j = 0; j < 16 && i0 + j < D0; ++j) tmp[j] = src[j];
-          v = *reinterpret_cast<const uint4*>(tmp);
-        }
-      }
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    const int ob = b / cg1, ig = b % cg1;
+    const int i0 = ig * 64;
+    const TileState st = tile_prefetch(a, pS + a.off_w1, D0, ob * 16, i0, D0);
+    // ---- stage Xᵀ slab: sX[j][r] = X[sample(r)][i0 + j], j < 64 (bf16; 0 for invalid rows/cols).
+    //      Lanes run along r (consecutive LDS halves) so the transposing ds_write_b16s are conflict-free.
+    for (int e = threadIdx.x; e < Bp * 8; e += 256) {
+      const int r = e % Bp, q = e / Bp;  // row r, 8-byte chunk q of the 64-byte row segment
+      uint2 v = {0u, 0u};
+      const int col = i0 + q * 8;
+      if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xp[p] + sample_index(a, true, p, step, 0, r) * (int64_t)D0 + col);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) sX[j * LDX + r] = (bf16)(float)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      for (int j = 0; j < 8; ++j) sX[(q * 8 + j) * LDX + r] = (bf16)(float)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xffu);
     }
     __syncthreads();
     const bf16* A = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)(ob * 16 + c) * Bp;
@@ -386,48 +486,45 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
     float bsum = 0.f;
     for (int k0 = 0; k0 < Bp; k0 += 32) {
       const bf16x8 av = ld8(A + k0 + 8 * h);
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[c * LDX + k0 + 8 * h]);
-      if (ib == 0) bsum += frag_sum(av);
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[(wave * 16 + c) * LDX + k0 + 8 * h]);
+      if (ig == 0 && wave == 0) bsum += frag_sum(av);
       acc = mfma_bf16(av, bv, acc);
     }
-    const int i = ib * 16 + c;
-    if (i < D0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) update_elem(a, pS + a.off_w1 + (int64_t)(ob * 16 + 4 * h + r) * D0 + i, acc[r], bc1, bc2s);
-    }
-    if (ib == 0) {
+    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * 68 + wave * 16 + c] = acc[r];
+    if (ig == 0 && wave == 0) {
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
       if (h == 0) update_elem(a, pS + a.off_b1 + ob * 16 + c, bsum, bc1, bc2s);
     }
+    __syncthreads();
+    tile_apply(a, st, sG, ob * 16, i0, D0, bc1, bc2s, false, p);
     return;
   }
   if (b < nb1 + nb2) {
-    // ---- W2 tile: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b]; also refresh the W2ᵀ shadow
-    const int tile = (b - nb1) * 4 + wave;
-    const int ob = tile / (D1 / 16), ib = tile % (D1 / 16);
+    // ---- W2: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b], tile = 16 rows (o2) × 64 cols (o1)
+    const int bb = b - nb1;
+    const int ob = bb / (D1 / 64), ig = bb % (D1 / 64);
+    const int ib = ig * 4 + wave;
+    const TileState st = tile_prefetch(a, pS + a.off_w2, D1, ob * 16, ig * 64, D1);
     const bf16* A = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)(ob * 16 + c) * Bp;
     const bf16* Bm = a.H1T + (int64_t)p * D1 * Bp + (int64_t)(ib * 16 + c) * Bp;
     f32x4 acc = zero4();
     float bsum = 0.f;
     for (int k0 = 0; k0 < Bp; k0 += 32) {
       const bf16x8 av = ld8(A + k0 + 8 * h);
-      if (ib == 0) bsum += frag_sum(av);
+      if (ig == 0 && wave == 0) bsum += frag_sum(av);
       acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
     }
-    const int o1 = ib * 16 + c;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o2 = ob * 16 + 4 * h + r;
-      const int64_t idx = pS + a.off_w2 + (int64_t)o2 * D1 + o1;
-      update_elem(a, idx, acc[r], bc1, bc2s);
-      a.w2t[(int64_t)p * D1 * D2 + (int64_t)o1 * D2 + o2] = a.shadow[idx];
-    }
-    if (ib == 0) {
+    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * 68 + wave * 16 + c] = acc[r];
+    if (ig == 0 && wave == 0) {
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
       if (h == 0) update_elem(a, pS + a.off_b2 + ob * 16 + c, bsum, bc1, bc2s);
     }
+    __syncthreads();
+    tile_apply(a, st, sG, ob * 16, ig * 64, D1, bc1, bc2s, true, p);
     return;
   }
   // ---- W3 tiles: dW3[cls][o2] = Σ_b dlogitsᵀ[cls][b] · H2ᵀ[o2][b]  (classes padded to 16)
@@ -506,8 +603,8 @@ static void launch_head_dispatch(const MLPArgs& a, int step, int base, bool trai
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s) {
   hipLaunchKernelGGL((mlp_fc1_fwd<true>), dim3(a.D1 / 32, a.Bpad / 32, a.P), dim3(256), 0, s, a, step, 0);
   launch_head_dispatch(a, step, 0, true, a.Bpad, s);
-  const int nb1 = ((a.D0 + 15) / 16) * (a.D1 / 64);
-  const int nb2 = (a.D2 / 16) * (a.D1 / 16) / 4;
+  const int nb1 = (a.D1 / 16) * ((a.D0 + 63) / 64);
+  const int nb2 = (a.D2 / 16) * (a.D1 / 64);
   const int nb3 = (a.D2 / 16 + 3) / 4;
   hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), 0, s, a, step);
 }

@@ -41,6 +41,8 @@ struct MLPEngine {
   void* ws = nullptr;
   int* d_active = nullptr;
   int* d_t0 = nullptr;
+  int4* d_ctl = nullptr;
+  std::vector<int4> ctl_host;
   float* d_loss = nullptr;
   int* d_correct = nullptr;
   int* d_conf = nullptr;
@@ -174,6 +176,8 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
   rc |= e->alloc(&p, (size_t)P * 16 * bp * 2); a.dlogT = (bf16*)p;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_active = (int*)p; a.active = e->d_active;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_t0 = (int*)p; a.t0 = e->d_t0;
+  rc |= e->alloc(&p, (size_t)P * 16); e->d_ctl = (int4*)p; a.ctl = e->d_ctl;
+  e->ctl_host.assign(P, int4{0, 0, 0, 0});
   rc |= e->alloc(&p, (size_t)P * 4); e->d_loss = (float*)p; a.loss_acc = e->d_loss;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_correct = (int*)p; a.correct_acc = e->d_correct;
   rc |= e->alloc(&p, (size_t)P * 256 * 4); e->d_conf = (int*)p; a.conf = e->d_conf;
@@ -203,6 +207,16 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
   e->a.Xp = (const uint8_t* const*)Xp; e->a.Yp = (const int* const*)Yp; e->a.n = n; e->a.perm = perm; e->a.perm_stride = perm_stride;
   e->max_steps = max_steps;
   e->invalidate();
+  return 0;
+}
+
+// host copies of the per-peer sample counts (packed into the control words)
+int mlp_engine_set_counts(void* h, const int* n_host, const int* nt_host) {
+  auto* e = (MLPEngine*)h;
+  for (int p = 0; p < e->a.P; ++p) {
+    e->ctl_host[p].y = n_host[p];
+    e->ctl_host[p].w = nt_host[p];
+  }
   return 0;
 }
 
@@ -239,6 +253,7 @@ int mlp_engine_set_extras(void* h, const float* anchor, const float* cg, const f
 int mlp_engine_begin(void* h, const int* active_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
+  for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
   CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
@@ -256,7 +271,8 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   if (!e->exec || e->graph_steps != e->max_steps) {
     if (e->capture(e->max_steps)) return 1;
   }
-  CHECK_HIP(hipMemcpyAsync(e->d_t0, t0_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
+  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
   CHECK_HIP(hipGraphLaunch(e->exec, s));
   return 0;
 }
@@ -265,7 +281,8 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
 int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
-  CHECK_HIP(hipMemcpyAsync(e->d_t0, t0_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
+  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
   for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
   CHECK_HIP(hipGetLastError());
   return 0;
@@ -284,6 +301,8 @@ int mlp_engine_read_stats(void* h, float* loss_host, int* correct_host, void* st
 int mlp_engine_eval(void* h, const int* active_host, float* loss_host, int* correct_host, int* conf_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
+  for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
+  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
   CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));

@@ -55,6 +55,7 @@ _SIGNATURES = {
     "mlp_engine_bind_params": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
     "mlp_engine_set_train_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int]),
     "mlp_engine_set_test_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "mlp_engine_set_counts": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mlp_engine_set_optimizer": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float, c_float, c_float, c_int, c_float]),
     "mlp_engine_set_extras": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_begin": (c_int, [c_void_p, c_void_p, c_void_p]),

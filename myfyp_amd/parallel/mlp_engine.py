@@ -230,6 +230,9 @@ class MLPGroup:
         t = self._tables
         _native.check(lib.mlp_engine_set_train_data(self._engine, _p(t["Xp"]), _p(t["Yp"]), _p(t["n"]), _p(self.perm), self.nmax, self.max_steps), "set_train_data")
         _native.check(lib.mlp_engine_set_test_data(self._engine, _p(t["Xtp"]), _p(t["Ytp"]), _p(t["nt"]), max(nts) if nts else 0), "set_test_data")
+        n_host = np.asarray(ns, dtype=np.int32)
+        nt_host = np.asarray(nts, dtype=np.int32)
+        _native.check(lib.mlp_engine_set_counts(self._engine, n_host.ctypes.data, nt_host.ctypes.data), "set_counts")
 
     def _extra_buffer(self, name: str) -> torch.Tensor:
         buf = self.extras.get(name)
