@@ -85,20 +85,22 @@ class PercentageBasedNonIIDPartitionStrategy(DataPartitionStrategy):
         def split(data: Any) -> List[List[int]]:
             y = _labels(data, label_tag)
             classes = np.unique(y)
-            pools = {c: list(rng.permutation(np.nonzero(y == c)[0])) for c in classes}
             size = len(y) // num_partitions
-            out: List[List[int]] = []
+            pools = {c: list(rng.permutation(np.nonzero(y == c)[0])) for c in classes}
+            out: List[List[int]] = [[] for _ in range(num_partitions)]
+            # 1) reserve each partition's dominant-class share first
             for i in range(num_partitions):
                 dom = classes[i % len(classes)]
                 take = min(int(size * percentage), len(pools[dom]))
-                part = [pools[dom].pop() for _ in range(take)]
-                rest = [idx for c in classes for idx in pools[c]]
-                rng.shuffle(rest)
-                need = size - len(part)
-                chosen = set(rest[:need])
-                for c in classes:
-                    pools[c] = [j for j in pools[c] if j not in chosen]
-                out.append(sorted(part + list(chosen)))
+                out[i] = [pools[dom].pop() for _ in range(take)]
+            # 2) fill the rest IID from what remains
+            rest = np.asarray([idx for c in classes for idx in pools[c]], dtype=np.int64)
+            rng.shuffle(rest)
+            pos = 0
+            for i in range(num_partitions):
+                need = max(0, size - len(out[i]))
+                out[i] = sorted(out[i] + rest[pos : pos + need].tolist())
+                pos += need
             return out
 
         return split(train_data), split(test_data)

@@ -16,11 +16,14 @@ import numpy as np
 from myfyp_amd.learning.dataset.p2pfl_dataset import P2PFLDataset
 
 
-def _smooth_prototypes(rng: np.random.Generator, num_classes: int, shape: Tuple[int, ...]) -> np.ndarray:
+def _smooth_prototypes(rng: np.random.Generator, num_classes: int, shape: Tuple[int, ...], similarity: float = 0.0) -> np.ndarray:
+    """Smooth random 'stroke' images; ``similarity`` blends every class with a shared pattern
+    (higher = classes overlap more = harder task)."""
     h, w = shape[0], shape[1]
     protos = []
+    common = rng.random((7, 7) + shape[2:])
     for _ in range(num_classes):
-        coarse = rng.random((7, 7) + shape[2:])
+        coarse = (1 - similarity) * rng.random((7, 7) + shape[2:]) + similarity * common
         # bilinear upsample of a 7x7 grid -> smooth blobs
         yi = np.linspace(0, 6, h)
         xi = np.linspace(0, 6, w)
@@ -47,27 +50,37 @@ def _make(rng: np.random.Generator, protos: np.ndarray, n: int, noise: float, ma
     chunk = 4096
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        base = protos[labels[s:e]]
-        dy, dx = rng.integers(-max_shift, max_shift + 1, size=2)
-        base = np.roll(base, (int(dy), int(dx)), axis=(1, 2))
-        img = base * 255.0 + rng.normal(0.0, noise * 255.0, size=base.shape)
+        base = protos[labels[s:e]].copy()
+        # per-sample random translation (grouped by shift so it stays vectorised)
+        shifts = rng.integers(-max_shift, max_shift + 1, size=(e - s, 2))
+        for dy in range(-max_shift, max_shift + 1):
+            for dx in range(-max_shift, max_shift + 1):
+                sel = np.nonzero((shifts[:, 0] == dy) & (shifts[:, 1] == dx))[0]
+                if len(sel):
+                    base[sel] = np.roll(base[sel], (dy, dx), axis=(1, 2))
+        # MNIST-like statistics: near-zero background, noisy strokes of varying intensity, plus
+        # sparse background speckle. ``noise`` scales the stroke noise.
+        gain = rng.uniform(0.6, 1.2, size=(e - s,) + (1,) * (base.ndim - 1))
+        stroke = base > 0.05
+        img = base * 255.0 * gain + rng.normal(0.0, noise * 255.0, size=base.shape) * np.where(stroke, 1.0, 0.15)
+        img = np.where(rng.random(base.shape) < 0.02, rng.uniform(0, 255, size=base.shape), img)
         out[s:e] = np.clip(img, 0, 255).astype(np.uint8)
     return out, labels.astype(np.int64)
 
 
-def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234, noise: float = 0.9, max_shift: int = 2) -> P2PFLDataset:
+def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234, noise: float = 1.0, max_shift: int = 3, similarity: float = 0.6) -> P2PFLDataset:
     """MNIST-shaped dataset: ``image`` uint8[N,28,28], ``label`` int64[N] in 0..9."""
     rng = np.random.default_rng(seed)
-    protos = _smooth_prototypes(rng, 10, (28, 28))
+    protos = _smooth_prototypes(rng, 10, (28, 28), similarity)
     xtr, ytr = _make(rng, protos, n_train, noise, max_shift)
     xte, yte = _make(rng, protos, n_test, noise, max_shift)
     return P2PFLDataset.from_arrays({"image": xtr, "label": ytr}, {"image": xte, "label": yte})
 
 
-def synthetic_cifar10(n_train: int = 50000, n_test: int = 10000, seed: int = 4321, noise: float = 0.9, max_shift: int = 2) -> P2PFLDataset:
+def synthetic_cifar10(n_train: int = 50000, n_test: int = 10000, seed: int = 4321, noise: float = 1.0, max_shift: int = 3, similarity: float = 0.6) -> P2PFLDataset:
     """CIFAR-10-shaped dataset: ``image`` uint8[N,32,32,3], ``label`` int64[N] in 0..9."""
     rng = np.random.default_rng(seed)
-    protos = _smooth_prototypes(rng, 10, (32, 32, 3))
+    protos = _smooth_prototypes(rng, 10, (32, 32, 3), similarity)
     xtr, ytr = _make(rng, protos, n_train, noise, max_shift)
     xte, yte = _make(rng, protos, n_test, noise, max_shift)
     return P2PFLDataset.from_arrays({"image": xtr, "label": ytr}, {"image": xte, "label": yte})
