@@ -15,8 +15,8 @@ import threading
 from typing import Any, Dict, List, Optional
 
 from myfyp_amd.communication.protocols.base_protocol import BaseCommunicationProtocol
-from myfyp_amd.communication.protocols.client import Client
-from myfyp_amd.communication.protocols.exceptions import CommunicationError, NeighborNotConnectedError
+from myfyp_amd.communication.protocols.client import Client, StubClient
+from myfyp_amd.communication.protocols.exceptions import NeighborNotConnectedError
 from myfyp_amd.communication.protocols.neighbors import Neighbors
 from myfyp_amd.management.logger import logger
 
@@ -76,40 +76,12 @@ class InMemoryNeighbors(Neighbors):
         except Exception:
             pass
 
+    def temporary_stub(self, addr: str):
+        return ServerRegistry.get(addr)
 
-class InMemoryClient(Client):
-    """Sends by calling the peer protocol's handlers directly."""
 
-    def __init__(self, self_addr: str, neighbors: InMemoryNeighbors) -> None:
-        super().__init__(self_addr)
-        self._neighbors = neighbors
-
-    def send(self, nei: str, msg: dict, create_connection: bool = False, raise_error: bool = False, remove_on_error: bool = True) -> None:
-        try:
-            try:
-                server = self._neighbors.get(nei)[1]
-            except KeyError as e:
-                if not create_connection:
-                    raise NeighborNotConnectedError(f"Neighbor {nei} not found.") from e
-                server = None
-            if server is None and create_connection:
-                server = ServerRegistry.get(nei)
-            if server is None or not server.is_running():
-                raise NeighborNotConnectedError("Neighbor not directly connected (and create_connection is false).")
-            res = server.handle_weights(msg) if "weights" in msg else server.handle_message(msg)
-            if "error" in res:
-                raise CommunicationError(f"Error while sending a message: {msg['cmd']!r}: {res['error']!r}")
-        except Exception as e:
-            logger.info(self.self_addr, f"Cannot send message {msg['cmd']!r} to {nei}. Error: {e}")
-            if remove_on_error and not isinstance(e, CommunicationError):
-                self._neighbors.remove(nei, disconnect_msg=True)
-            if raise_error:
-                raise
-
-    def broadcast(self, msg: dict, node_list: Optional[List[str]] = None) -> None:
-        nodes = node_list if node_list is not None else list(self._neighbors.get_all(only_direct=True))
-        for n in nodes:
-            self.send(n, msg)
+class InMemoryClient(StubClient):
+    """Sends by calling the peer protocol's handlers directly (generic stub client)."""
 
 
 class InMemoryCommunicationProtocol(BaseCommunicationProtocol):

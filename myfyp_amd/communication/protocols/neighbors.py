@@ -29,6 +29,10 @@ class Neighbors:
     def disconnect(self, addr: str, disconnect_msg: bool = True) -> None:
         raise NotImplementedError
 
+    def temporary_stub(self, addr: str):
+        """A stub for a one-off send to a non-neighbour (``create_connection=True``)."""
+        return None
+
     def refresh_or_add(self, addr: str, time: float) -> None:
         with self.neis_lock:
             if addr in self.neis:
