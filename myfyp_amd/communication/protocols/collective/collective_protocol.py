@@ -52,6 +52,12 @@ class CollectiveCommunicationProtocol(InMemoryCommunicationProtocol):
         self.node = node
         Federation.get().register_local(node)
 
+    def stop(self) -> None:
+        inst = Federation._instance
+        if inst is not None:
+            inst.unregister_local(self.addr)
+        super().stop()
+
     def handshake(self, addr: str) -> bool:
         # remote peers connect through the StoreBus; accept both local and remote handshakes
         return self._neighbors.add(addr, non_direct=False, handshake_msg=False)

@@ -23,3 +23,10 @@ class P2PFLCallback(ABC):
 
     def get_info(self) -> Any:
         return self.additional_info
+
+    # checkpoint hooks: persistent per-client state that is not part of the model
+    def state_dict(self) -> dict:
+        return {}
+
+    def load_state_dict(self, state: dict) -> None:
+        pass

@@ -57,6 +57,8 @@ class SCAFFOLDCallback(TorchCallback):
         flat = learner.flat_params()
         if self.c_i is None or self.c_i.numel() != flat.numel():
             self.c_i = torch.zeros_like(flat)
+        elif self.c_i.device != flat.device:
+            self.c_i = self.c_i.to(flat.device)
         g = self.additional_info.get("global_c")
         self.c = _list_to_flat(g, flat) if g is not None else torch.zeros_like(flat)
         self.x0 = flat.detach().clone()
@@ -73,6 +75,13 @@ class SCAFFOLDCallback(TorchCallback):
         self.c_i = c_new
         self.additional_info["delta_y_i"] = _flat_to_list(y - self.x0, learner)
         self.additional_info["delta_c_i"] = _flat_to_list(delta_c, learner)
+
+    def state_dict(self) -> dict:
+        return {} if self.c_i is None else {"c_i": self.c_i.detach().cpu().numpy()}
+
+    def load_state_dict(self, state: dict) -> None:
+        if "c_i" in state:
+            self.c_i = torch.as_tensor(np.asarray(state["c_i"]), dtype=torch.float32)
 
 
 class FedProxCallback(TorchCallback):

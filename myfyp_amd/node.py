@@ -163,28 +163,34 @@ class Node:
         return self.learner.get_data()
 
     # ------------------------------------------------------------------ network learning
-    def _start_learning_thread(self, rounds: int, epochs: int) -> None:
+    def _start_learning_thread(self, rounds: int, epochs: int, start_round: int = 0) -> None:
         with self.state.start_thread_lock:
             if self._learning_thread is not None and self._learning_thread.is_alive():
                 return
             self.learning_workflow.finished = False
-            t = threading.Thread(target=self._start_learning, args=(rounds, epochs), name=f"learning_thread-{self.addr}", daemon=True)
+            t = threading.Thread(target=self._start_learning, args=(rounds, epochs, start_round), name=f"learning_thread-{self.addr}", daemon=True)
             self._learning_thread = t
             t.start()
 
-    def set_start_learning(self, rounds: int = 1, epochs: int = 1) -> Optional[str]:
+    def set_start_learning(self, rounds: int = 1, epochs: int = 1, start_round: int = 0) -> Optional[str]:
+        """Start network-wide learning. ``start_round > 0`` resumes an experiment whose first
+        ``start_round`` rounds are already done (restore models with
+        :func:`myfyp_amd.management.checkpoint.restore_node` first)."""
         self.assert_running(True)
         if rounds < 1:
             raise ZeroRoundsException("Rounds must be greater than 0.")
+        if not 0 <= start_round < rounds:
+            raise ValueError(f"start_round must be in [0, {rounds}), got {start_round}")
         if self.state.round is not None:
             logger.info(self.addr, "Learning already started")
             return None
         logger.info(self.addr, "🚀 Broadcasting start learning...")
         proto = self._communication_protocol
-        proto.broadcast(proto.build_msg(StartLearningCommand.get_name(), [str(rounds), str(epochs)]))
+        args = [str(rounds), str(epochs)] + ([str(start_round)] if start_round else [])
+        proto.broadcast(proto.build_msg(StartLearningCommand.get_name(), args))
         self.state.model_initialized_lock.release()
         proto.broadcast(proto.build_msg(ModelInitializedCommand.get_name()))
-        self._start_learning_thread(rounds, epochs)
+        self._start_learning_thread(rounds, epochs, start_round)
         return self.exp_name
 
     def set_stop_learning(self) -> None:
@@ -194,11 +200,12 @@ class Node:
         self._communication_protocol.broadcast(self._communication_protocol.build_msg(StopLearningCommand.get_name()))
         self._stop_learning()
 
-    def _start_learning(self, rounds: int, epochs: int) -> None:
+    def _start_learning(self, rounds: int, epochs: int, start_round: int = 0) -> None:
         try:
             self.learning_workflow.run(
                 rounds=rounds,
                 epochs=epochs,
+                start_round=start_round,
                 state=self.state,
                 learner=self.learner,
                 communication_protocol=self._communication_protocol,
@@ -207,7 +214,10 @@ class Node:
                 node=self,
             )
         except Exception as e:
-            logger.error(self.addr, f"Error {type(e).__name__}: {e}\n{traceback.format_exc()}")
+            if getattr(e, "fault_injected", False):
+                logger.warning(self.addr, f"learning thread ended by fault injection: {e}")
+            else:
+                logger.error(self.addr, f"Error {type(e).__name__}: {e}\n{traceback.format_exc()}")
             self.stop()
 
     def _stop_learning(self) -> None:

@@ -56,9 +56,10 @@ class NodeState:
     def exp_name(self) -> Optional[str]:
         return self.experiment.exp_name if self.experiment is not None else None
 
-    def set_experiment(self, exp_name: str, total_rounds: int) -> None:
+    def set_experiment(self, exp_name: str, total_rounds: int, start_round: int = 0) -> None:
         self.status = "Learning"
         self.experiment = Experiment(exp_name, total_rounds)
+        self.experiment.round = start_round  # > 0 when resuming from a checkpoint
 
     def increase_round(self) -> None:
         if self.experiment is None:

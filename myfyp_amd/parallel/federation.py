@@ -124,13 +124,20 @@ class LocalGang:
         self._result: Dict[int, Any] = {}
         self._error: Dict[int, BaseException] = {}
 
-    def run(self, member: str, members: List[str], payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: float) -> Any:
+    def poke(self) -> None:
+        """Membership changed (a peer left): let waiting members re-evaluate."""
+        with self._cv:
+            self._cv.notify_all()
+
+    def run(self, member: str, members: Callable[[], List[str]], payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: float) -> Any:
+        """``members`` is re-read on every wake-up so a peer that dies mid-round (fault injection,
+        crash) stops being waited for as soon as it unregisters."""
         with self._cv:
             gen = self._gen
             self._arrived[member] = payload
             deadline = time.time() + timeout
             while gen == self._gen:
-                live = [m for m in members]
+                live = members()
                 if set(live).issubset(self._arrived) or time.time() >= deadline:
                     missing = set(live) - set(self._arrived)
                     if missing:
@@ -295,8 +302,16 @@ class Federation:
         return [a for a in self.local_order if a in self.local_nodes and self.local_nodes[a].state.round is not None]
 
     def gang_run(self, member: str, payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: Optional[float] = None) -> Any:
-        members = [a for a in self.local_order if a in self.local_nodes]
+        def members() -> List[str]:
+            return [a for a in self.local_order if a in self.local_nodes]
+
         return self.gang.run(member, members, payload, fn, Settings.AGGREGATION_TIMEOUT if timeout is None else timeout)
+
+    def unregister_local(self, addr: str) -> None:
+        """A co-located peer stopped (or crashed): drop it from every future gang."""
+        with self._lock:
+            self.local_nodes.pop(addr, None)
+        self.gang.poke()
 
     def all_gather_object(self, obj: Any) -> List[Any]:
         if self.world == 1:

@@ -42,7 +42,7 @@ def _stacked_group(learners) -> Optional[Any]:
 # ---------------------------------------------------------------------------------------------
 def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str) -> None:
     """Every peer adopts the initiator's weights: local copy + one RCCL broadcast per tensor."""
-    learners = {a: fed.local_nodes[a].learner for a in arrived}
+    learners = {a: fed.local_nodes[a].learner for a in arrived if a in fed.local_nodes}
     src_rank = fed.peers.get(initiator, 0)
     ref_addr = initiator if initiator in learners else next(iter(learners))
     src = state_tensors(learners[ref_addr])
@@ -72,7 +72,7 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     """Sample-weighted mean of the trainers' models (weight 0 for non-trainers), result into every
     local peer. One local weighted reduction kernel + one all-reduce + one broadcast kernel."""
     t0 = time.perf_counter()
-    addrs = list(arrived)
+    addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
     learners = [fed.local_nodes[a].learner for a in addrs]
     weights = [float(arrived[a][0]) for a in addrs]
     contributors = [a for a, w in zip(addrs, weights) if w > 0]
@@ -128,5 +128,6 @@ def aggregate_generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], ag
         return None
     agg = aggregator.aggregate(models)
     for a in arrived:
-        fed.local_nodes[a].learner.set_model(agg)
+        if a in fed.local_nodes:
+            fed.local_nodes[a].learner.set_model(agg)
     return agg

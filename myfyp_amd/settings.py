@@ -92,6 +92,10 @@ class Settings:
     COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
     BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
 
+    # ---------------- CHECKPOINT (new: SURVEY §5.4)
+    CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
+    CHECKPOINT_EVERY: int = 1
+
     # nested aliases (FYP scripts: Settings.general.SEED)
     general = _Group(
         {
@@ -101,6 +105,8 @@ class Settings:
             "LOG_DIR": "LOG_DIR",
             "EXCLUDE_BEAT_LOGS": "EXCLUDE_BEAT_LOGS",
             "DISABLE_RAY": "DISABLE_RAY",
+            "CHECKPOINT_DIR": "CHECKPOINT_DIR",
+            "CHECKPOINT_EVERY": "CHECKPOINT_EVERY",
         }
     )
     heartbeat = _Group({"PERIOD": "HEARTBEAT_PERIOD", "TIMEOUT": "HEARTBEAT_TIMEOUT", "WAIT_CONVERGENCE": "WAIT_HEARTBEATS_CONVERGENCE"})

@@ -2,6 +2,7 @@
 
 from typing import Optional, Type
 
+from myfyp_amd.management.checkpoint import maybe_checkpoint
 from myfyp_amd.management.logger import logger
 from myfyp_amd.stages.base_node.train_stage import broadcast_metrics
 from myfyp_amd.stages.stage import Stage
@@ -25,6 +26,7 @@ class RoundFinishedStage(Stage):
         logger.info(state.addr, f"🎉 Round {state.round} of {state.total_rounds} finished.")
         if state.round is None or state.total_rounds is None:
             raise ValueError("Round or total rounds not set.")
+        maybe_checkpoint(state, learner)
         if state.round < state.total_rounds:
             return StageFactory.get_stage("VoteTrainSetStage")
         logger.info(state.addr, "🔬 Evaluating...")

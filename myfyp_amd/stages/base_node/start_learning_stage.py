@@ -23,7 +23,7 @@ class StartLearningStage(Stage):
         if rounds is None or epochs is None or state is None or learner is None or communication_protocol is None or aggregator is None:
             raise Exception("Invalid parameters on StartLearningStage.")
         with state.start_thread_lock:
-            state.set_experiment(exp_name, rounds)
+            state.set_experiment(exp_name, rounds, start_round=int(kwargs.get("start_round", 0) or 0))
             learner.set_epochs(epochs)
             logger.experiment_started(state.addr, state.experiment)
         begin = time.time()

@@ -25,7 +25,7 @@ class StartLearningStage(Stage):
             raise Exception("Invalid parameters on StartLearningStage.")
         f = fed()
         with state.start_thread_lock:
-            state.set_experiment(exp_name, rounds)
+            state.set_experiment(exp_name, rounds, start_round=int(kwargs.get("start_round", 0) or 0))
             learner.set_epochs(epochs)
             logger.experiment_started(state.addr, state.experiment)
         if not f.finalized.is_set():

@@ -5,7 +5,7 @@ workflow ends. Each stage's wall time is recorded with ``logger.log_timing`` (SU
 """
 
 import time
-from typing import List, Optional, Type
+from typing import Any, Callable, Dict, List, Optional, Type
 
 from myfyp_amd.management.logger import logger
 from myfyp_amd.stages.stage import Stage, check_early_stop
@@ -20,6 +20,8 @@ class StageWokflow:
         self.current_stage = first_stage
         self.history: List[str] = []
         self.finished = False
+        # called as hook(stage_name, kwargs) before each stage (fault injection, tracing)
+        self.hooks: List[Callable[[str, Dict[str, Any]], None]] = []
 
     def run(self, **kwargs) -> None:
         self.finished = False
@@ -31,6 +33,8 @@ class StageWokflow:
             while True:
                 logger.debug(state.addr, f"🏃 Running stage: {self.current_stage.name()}")
                 self.history.append(self.current_stage.name())
+                for hook in list(self.hooks):
+                    hook(self.current_stage.name(), kwargs)
                 t0 = time.time()
                 next_stage: Optional[Type[Stage]] = self.current_stage.execute(**kwargs)
                 logger.log_timing(state.addr, self.current_stage.name(), time.time() - t0)
