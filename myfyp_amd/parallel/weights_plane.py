@@ -117,6 +117,68 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     return total_w, contributors
 
 
+def _pack(learner) -> torch.Tensor:
+    return torch.cat([t.detach().reshape(-1).float() for t in state_tensors(learner)])
+
+
+def _unpack_into(learner, flat: torch.Tensor) -> None:
+    off = 0
+    with torch.no_grad():
+        for t in state_tensors(learner):
+            t.copy_(flat[off : off + t.numel()].view_as(t).to(t.dtype))
+            off += t.numel()
+
+
+def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) -> List[str]:
+    """Topology mixing ``x_i ← Σ_j W_ij x_j`` (see ``NeighborAvg``): co-located rows are combined
+    with the ``weighted_average`` kernel, rows of neighbours on other ranks arrive through one
+    grouped batch of point-to-point sends/receives (RCCL over xGMI; gloo on CPU). Every rank calls
+    this with the same peer list, so the P2P pattern matches by construction."""
+    t0 = time.perf_counter()
+    peers = fed.all_peers()
+    index = {a: i for i, a in enumerate(peers)}
+    w = aggregator.mixing_matrix(len(peers))
+    local = [a for a in peers if a in arrived and a in fed.local_nodes]
+    if not local:
+        fed.record("aggregate", time.perf_counter() - t0)
+        return []
+    rows = {a: _pack(fed.local_nodes[a].learner) for a in local}
+    ref = rows[local[0]]
+    # point-to-point plan: every (local peer, remote rank) edge sends once; every remote neighbour is received once
+    sends, recvs = {}, {}
+    for a in local:
+        i = index[a]
+        for j in np.nonzero(w[i])[0]:
+            b = peers[j]
+            rb = fed.peers[b]
+            if j == i or rb == fed.rank:
+                continue
+            sends[(a, rb)] = rows[a]
+            if b not in recvs:
+                recvs[b] = torch.empty_like(ref)
+    if sends or recvs:
+        import torch.distributed as dist
+
+        # per rank pair, sends and receives are both ordered by the source peer's index (NCCL ignores tags)
+        ops_ = [dist.P2POp(dist.isend, t, rb, tag=index[a]) for (a, rb), t in sorted(sends.items(), key=lambda kv: (index[kv[0][0]], kv[0][1]))]
+        ops_ += [dist.P2POp(dist.irecv, t, fed.peers[b], tag=index[b]) for b, t in sorted(recvs.items(), key=lambda kv: index[kv[0]])]
+        for req in dist.batch_isend_irecv(ops_):
+            req.wait()
+    src = dict(rows)
+    src.update(recvs)
+    mixed = {}
+    for a in local:
+        i = index[a]
+        nz = [j for j in np.nonzero(w[i])[0] if peers[j] in src]
+        ws = np.array([w[i, j] for j in nz], dtype=np.float64)
+        ws = ws / ws.sum()  # a dead neighbour's share folds back proportionally
+        mixed[a] = ops.weighted_average([[src[peers[j]]] for j in nz], [float(x) for x in ws])[0]
+    for a in local:
+        _unpack_into(fed.local_nodes[a].learner, mixed[a])
+    fed.record("aggregate", time.perf_counter() - t0)
+    return local
+
+
 def aggregate_generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> Any:
     """Any aggregator: all-gather the trainers' wire models and reduce identically on every rank."""
     local_models = {a: p[1] for a, p in arrived.items() if p[1] is not None}

@@ -67,6 +67,7 @@ _AGGREGATORS = {
     "fedprox": ("myfyp_amd.learning.aggregators.fedprox", "FedProx"),
     "krum": ("myfyp_amd.learning.aggregators.krum", "Krum"),
     "trimmedmean": ("myfyp_amd.learning.aggregators.trimmed_mean", "TrimmedMean"),
+    "neighboravg": ("myfyp_amd.learning.aggregators.neighbor_avg", "NeighborAvg"),
 }
 _MODELS = {"mlp": "MLP", "lenet5": "LeNet5", "lenet": "LeNet5", "resnet18": "ResNet18", "resnet": "ResNet18"}
 

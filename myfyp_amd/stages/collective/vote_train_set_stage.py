@@ -29,10 +29,13 @@ class VoteTrainSetStage(Stage):
         logger.round_started(state.addr, state.experiment)
         f = fed()
         votes = make_votes(state.addr, f.all_peers(), state.round)
+        everyone = bool(getattr(kwargs.get("aggregator"), "all_peers_train", False))
 
         def leader(arrived):
             allv = weights_plane.gather_votes(f, arrived)
-            train_set = tally_votes(allv)
+            # decentralised mixing (NeighborAvg): every live peer trains; the gather still runs so
+            # ranks learn who is alive
+            train_set = sorted(allv, key=lambda a: f.all_peers().index(a)) if everyone else tally_votes(allv)
             set_gang_expectations(f, set(train_set), set(train_set))
             return train_set
 

@@ -18,7 +18,7 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
     model = learner.get_model()
     n = model.num_samples if trainer else 0
     wire = None
-    if trainer and kind != "mean":
+    if trainer and kind not in ("mean", "neighbor"):
         wire = model.build_copy(params=model.get_parameters(), num_samples=model.num_samples, contributors=list(model.contributors), additional_info=dict(model.additional_info))
     round_ = state.round
 
@@ -26,6 +26,9 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
         if kind == "mean":
             total, contributors = weights_plane.aggregate_mean(f, arrived)
             extra = getattr(aggregator, "proximal_mu", None)
+        elif kind == "neighbor":
+            weights_plane.aggregate_neighbors(f, arrived, aggregator)
+            extra = None
         else:
             weights_plane.aggregate_generic(f, arrived, aggregator)
             extra = None
