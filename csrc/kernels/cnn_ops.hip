@@ -1,0 +1,596 @@
+// Memory-bound companions of the implicit-GEMM convolutions (grouped over peers, grid.y/z = peer):
+// input gather + u8->bf16 NHWC conversion, BatchNorm (finalize / apply+residual+ReLU / backward
+// reduce / finalize / apply), 2x2 max-pool and global average pool (fwd + bwd), log-softmax + NLL
+// head (loss, correct, confusion, dlogits), and the fused SGD(+momentum/wd, FedProx, SCAFFOLD)
+// update that also refreshes both bf16 weight shadows of every conv/fc layer in the same pass.
+// All activation kernels move 16 bytes (8 bf16 channels) per lane.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+struct bf8 { bf16 v[8]; };
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const bf8 b = __builtin_bit_cast(bf8, u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (float)b.v[j];
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  bf8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b.v[j] = (bf16)f[j];
+  return __builtin_bit_cast(uint4, b);
+}
+
+// ------------------------------------------------------------------------------------------------
+// input: x_p[perm_p[offset + b]] (u8 HWC) -> bf16 [B][H][W][Cp] * scale ; labels -> int32; nb[p]
+// ------------------------------------------------------------------------------------------------
+__global__ void k_input_prep(const uint8_t* const* xs, const int64_t* const* ys, const int* n_samples, const int* perm, int64_t perm_ps,
+                             int offset, int B, int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb) {
+  const int peer = blockIdx.y;
+  const int n = n_samples[peer];
+  const int valid = max(0, min(B, n - offset));
+  if (blockIdx.x == 0 && threadIdx.x == 0) nb[peer] = valid;
+  const int64_t pix = (int64_t)B * H * W;
+  const int cpp = Cp / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pix * cpp; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cpp);
+    const int64_t px = i / cpp;
+    const int b = (int)(px / (H * W));
+    const int hw = (int)(px - (int64_t)b * H * W);
+    float f[8];
+    if (b < valid) {
+      const int idx = perm ? perm[peer * perm_ps + offset + b] : offset + b;
+      const uint8_t* s = xs[peer] + ((int64_t)idx * H * W + hw) * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c8 * 8 + j;
+        f[j] = c < C ? scale * (float)s[c] : 0.f;
+      }
+      if (c8 == 0 && hw == 0) labels[peer * B + b] = (int)ys[peer][idx];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    }
+    *reinterpret_cast<uint4*>(out + peer * out_ps + px * Cp + c8 * 8) = pack8(f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// BatchNorm forward finalize: partial (sum, sumsq) rows -> scale/shift (+ running stats) or eval
+// ------------------------------------------------------------------------------------------------
+__global__ void k_bn_finalize(const float* stats, int64_t stats_ps, int rows, const int* nb, int hw, const float* gamma, const float* beta,
+                              int64_t param_ps, float* rmean, float* rvar, int64_t run_ps, int C, int Cp, float eps, float momentum, int train,
+                              float* ss, float* ms) {
+  const int peer = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  __shared__ float red[2][4][64];
+  float s = 0.f, sq = 0.f;
+  if (train && c < Cp) {
+    const float* st = stats + peer * stats_ps;
+    for (int r = rg; r < rows; r += 4) {
+      s += st[(r * 2 + 0) * Cp + c];
+      sq += st[(r * 2 + 1) * Cp + c];
+    }
+  }
+  red[0][rg][threadIdx.x & 63] = s;
+  red[1][rg][threadIdx.x & 63] = sq;
+  __syncthreads();
+  if (rg != 0 || c >= Cp) return;
+  float* ssp = ss + peer * 2 * Cp;
+  float* msp = ms + peer * 2 * Cp;
+  if (c >= C) {
+    ssp[c] = 0.f; ssp[Cp + c] = 0.f; msp[c] = 0.f; msp[Cp + c] = 0.f;
+    return;
+  }
+  float mean, var;
+  float* rm = rmean + peer * run_ps;
+  float* rv = rvar + peer * run_ps;
+  if (train) {
+    s = red[0][0][c & 63] + red[0][1][c & 63] + red[0][2][c & 63] + red[0][3][c & 63];
+    sq = red[1][0][c & 63] + red[1][1][c & 63] + red[1][2][c & 63] + red[1][3][c & 63];
+    const int n = nb[peer] * hw;
+    const float cnt = (float)max(1, n);
+    mean = s / cnt;
+    var = fmaxf(sq / cnt - mean * mean, 0.f);
+    if (n > 0) {  // a peer without samples this step keeps its running statistics
+      const float unbiased = cnt > 1.f ? var * cnt / (cnt - 1.f) : var;
+      rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+      rv[c] = (1.f - momentum) * rv[c] + momentum * unbiased;
+    }
+  } else {
+    mean = rm[c];
+    var = rv[c];
+  }
+  const float inv = rsqrtf(var + eps);
+  const float g = gamma[peer * param_ps + c], b = beta[peer * param_ps + c];
+  ssp[c] = g * inv;
+  ssp[Cp + c] = b - mean * g * inv;
+  msp[c] = mean;
+  msp[Cp + c] = inv;
+}
+
+// out = act(y*sc + sh [+ res] [+ y2*sc2 + sh2]) ; rows = nb[p]*hw
+__global__ void k_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf16* res, int64_t res_ps, const bf16* y2, int64_t y2_ps,
+                         const float* ss2, int relu, const int* nb, int hw, int Cp, bf16* out, int64_t out_ps) {
+  const int peer = blockIdx.y;
+  const int64_t rows = (int64_t)nb[peer] * hw;
+  const int cpp = Cp / 8;
+  const float* sp = ss + peer * 2 * Cp;
+  const float* sp2 = ss2 ? ss2 + peer * 2 * Cp : nullptr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cpp; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpp) * 8;
+    const int64_t off = (i / cpp) * Cp + c0;
+    float f[8], t[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + peer * y_ps + off), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], sp[c0 + j], sp[Cp + c0 + j]);
+    if (res != nullptr) {
+      unpack8(*reinterpret_cast<const uint4*>(res + peer * res_ps + off), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += t[j];
+    }
+    if (y2 != nullptr) {
+      unpack8(*reinterpret_cast<const uint4*>(y2 + peer * y2_ps + off), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += fmaf(t[j], sp2[c0 + j], sp2[Cp + c0 + j]);
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<uint4*>(out + peer * out_ps + off) = pack8(f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// BatchNorm backward: g = dz * [mask > 0]; partial (sum g, sum g*xhat) per block; optional g out
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps,
+                                                       const float* ms, const int* nb, int hw, int Cp, float* part, int64_t part_ps, bf16* gout,
+                                                       int64_t gout_ps) {
+  const int peer = blockIdx.y;
+  const int64_t rows = (int64_t)nb[peer] * hw;
+  const int cpp = Cp / 8;
+  const int rpp = 256 / cpp;  // rows per pass
+  const int tid = threadIdx.x;
+  const int c8 = tid % cpp, rr = tid / cpp;
+  const float* mp = ms + peer * 2 * Cp;
+  float mean[8], inv[8], sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = mp[c8 * 8 + j];
+    inv[j] = mp[Cp + c8 * 8 + j];
+    sg[j] = 0.f;
+    sgx[j] = 0.f;
+  }
+  if (rr < rpp) {
+    const int64_t per_blk = (rows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = blockIdx.x * per_blk, r1 = min(rows, r0 + per_blk);
+    for (int64_t r = r0 + rr; r < r1; r += rpp) {
+      const int64_t off = r * Cp + c8 * 8;
+      float g[8], t[8];
+      unpack8(*reinterpret_cast<const uint4*>(dz + peer * dz_ps + off), g);
+      if (mask != nullptr) {
+        unpack8(*reinterpret_cast<const uint4*>(mask + peer * mask_ps + off), t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+      }
+      if (gout != nullptr) *reinterpret_cast<uint4*>(gout + peer * gout_ps + off) = pack8(g);
+      unpack8(*reinterpret_cast<const uint4*>(y + peer * y_ps + off), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] += g[j];
+        sgx[j] += g[j] * (t[j] - mean[j]) * inv[j];
+      }
+    }
+  }
+  __shared__ float red[256][17];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[tid][j] = sg[j];
+    red[tid][8 + j] = sgx[j];
+  }
+  __syncthreads();
+  if (tid < cpp) {
+    float a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = 0.f;
+    for (int k = 0; k < rpp; ++k)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] += red[k * cpp + tid][j];
+    float* pp = part + peer * part_ps + (int64_t)blockIdx.x * 2 * Cp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pp[tid * 8 + j] = a[j];
+      pp[Cp + tid * 8 + j] = a[8 + j];
+    }
+  }
+}
+
+// sum partials -> dgamma/dbeta (accumulated into the flat grad) + apply coefficients
+__global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps,
+                                  const float* ms, float* dgamma, float* dbeta, int C, int Cp, float* coef) {
+  const int peer = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cp) return;
+  float* cp = coef + peer * 3 * Cp;
+  if (c >= C) {
+    cp[c] = 0.f; cp[Cp + c] = 0.f; cp[2 * Cp + c] = 0.f;
+    return;
+  }
+  const float* pp = part + peer * part_ps;
+  float sg = 0.f, sgx = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    sg += pp[b * 2 * Cp + c];
+    sgx += pp[b * 2 * Cp + Cp + c];
+  }
+  dgamma[peer * param_ps + c] += sgx;
+  dbeta[peer * param_ps + c] += sg;
+  const float cnt = (float)max(1, nb[peer] * hw);
+  const float inv = ms[peer * 2 * Cp + Cp + c];
+  cp[c] = gamma[peer * param_ps + c] * inv;
+  cp[Cp + c] = sg / cnt;
+  cp[2 * Cp + c] = sgx / cnt;
+}
+
+// dy = k1 * (g - mean_g - xhat * mean_gxhat), g recomputed from dz and mask
+__global__ void k_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms,
+                               const float* coef, const int* nb, int hw, int Cp, bf16* dy, int64_t dy_ps) {
+  const int peer = blockIdx.y;
+  const int64_t rows = (int64_t)nb[peer] * hw;
+  const int cpp = Cp / 8;
+  const float* mp = ms + peer * 2 * Cp;
+  const float* cp = coef + peer * 3 * Cp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cpp; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpp) * 8;
+    const int64_t off = (i / cpp) * Cp + c0;
+    float g[8], t[8];
+    unpack8(*reinterpret_cast<const uint4*>(dz + peer * dz_ps + off), g);
+    if (mask != nullptr) {
+      unpack8(*reinterpret_cast<const uint4*>(mask + peer * mask_ps + off), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+    }
+    unpack8(*reinterpret_cast<const uint4*>(y + peer * y_ps + off), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xh = (t[j] - mp[c]) * mp[Cp + c];
+      g[j] = cp[c] * (g[j] - cp[Cp + c] - xh * cp[2 * Cp + c]);
+    }
+    *reinterpret_cast<uint4*>(dy + peer * dy_ps + off) = pack8(g);
+  }
+}
+
+// dz * [mask > 0] (ReLU backward without BN, e.g. LeNet / fc layers) and optional bias-grad
+__global__ void k_relu_bwd(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const int* nb, int hw, int Cp, bf16* out, int64_t out_ps) {
+  const int peer = blockIdx.y;
+  const int64_t rows = (int64_t)nb[peer] * hw;
+  const int cpp = Cp / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * cpp; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t off = (i / cpp) * Cp + (i % cpp) * 8;
+    float g[8], t[8];
+    unpack8(*reinterpret_cast<const uint4*>(dz + peer * dz_ps + off), g);
+    unpack8(*reinterpret_cast<const uint4*>(mask + peer * mask_ps + off), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+    *reinterpret_cast<uint4*>(out + peer * out_ps + off) = pack8(g);
+  }
+}
+
+// column sums of a [rows][Cp] bf16 tensor accumulated into fp32 (bias gradients): one block per
+// 8-channel chunk group, atomics only once per block and channel
+__global__ __launch_bounds__(256) void k_colsum(const bf16* x, int64_t x_ps, const int* nb, int hw, int Cp, int C, float* out, int64_t out_ps) {
+  const int peer = blockIdx.y;
+  const int64_t rows = (int64_t)nb[peer] * hw;
+  const int cpp = Cp / 8;
+  const int rpp = max(1, 256 / cpp);
+  const int tid = threadIdx.x;
+  const int c8 = tid % cpp, rr = tid / cpp;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rr < rpp && tid < rpp * cpp) {
+    const int64_t per_blk = (rows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = blockIdx.x * per_blk, r1 = min(rows, r0 + per_blk);
+    for (int64_t r = r0 + rr; r < r1; r += rpp) {
+      float t[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + peer * x_ps + r * Cp + c8 * 8), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += t[j];
+    }
+  }
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid][j] = (rr < rpp && tid < rpp * cpp) ? acc[j] : 0.f;
+  __syncthreads();
+  if (tid < cpp) {
+    for (int k = 1; k < rpp; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += red[k * cpp + tid][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = tid * 8 + j;
+      if (c < C) atomicAdd(out + peer * out_ps + c, acc[j]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pooling
+// ------------------------------------------------------------------------------------------------
+__global__ void k_maxpool2_fwd(const bf16* x, int64_t x_ps, const int* nb, int H, int W, int Cp, bf16* out, int64_t out_ps) {
+  const int peer = blockIdx.y;
+  const int Ho = H / 2, Wo = W / 2, cpp = Cp / 8;
+  const int64_t n = (int64_t)nb[peer] * Ho * Wo * cpp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cpp);
+    const int64_t px = i / cpp;
+    const int b = (int)(px / (Ho * Wo)), rem = (int)(px % (Ho * Wo)), oh = rem / Wo, ow = rem % Wo;
+    float m[8], t[8];
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int dh = 0; dh < 2; ++dh)
+      for (int dw = 0; dw < 2; ++dw) {
+        unpack8(*reinterpret_cast<const uint4*>(x + peer * x_ps + (((int64_t)b * H + 2 * oh + dh) * W + 2 * ow + dw) * Cp + c8 * 8), t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], t[j]);
+      }
+    *reinterpret_cast<uint4*>(out + peer * out_ps + px * Cp + c8 * 8) = pack8(m);
+  }
+}
+
+// gradient to the first maximal element of each window (torch semantics)
+__global__ void k_maxpool2_bwd(const bf16* x, int64_t x_ps, const bf16* dy, int64_t dy_ps, const int* nb, int H, int W, int Cp, bf16* dx, int64_t dx_ps) {
+  const int peer = blockIdx.y;
+  const int Ho = H / 2, Wo = W / 2, cpp = Cp / 8;
+  const int64_t n = (int64_t)nb[peer] * Ho * Wo * cpp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cpp);
+    const int64_t px = i / cpp;
+    const int b = (int)(px / (Ho * Wo)), rem = (int)(px % (Ho * Wo)), oh = rem / Wo, ow = rem % Wo;
+    float v[4][8], g[8], m[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + peer * dy_ps + px * Cp + c8 * 8), g);
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int k = 0; k < 4; ++k) {
+      unpack8(*reinterpret_cast<const uint4*>(x + peer * x_ps + (((int64_t)b * H + 2 * oh + k / 2) * W + 2 * ow + k % 2) * Cp + c8 * 8), v[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], v[k][j]);
+    }
+    bool taken[8] = {false, false, false, false, false, false, false, false};
+    for (int k = 0; k < 4; ++k) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool hit = !taken[j] && v[k][j] == m[j];
+        o[j] = hit ? g[j] : 0.f;
+        taken[j] = taken[j] || hit;
+      }
+      *reinterpret_cast<uint4*>(dx + peer * dx_ps + (((int64_t)b * H + 2 * oh + k / 2) * W + 2 * ow + k % 2) * Cp + c8 * 8) = pack8(o);
+    }
+  }
+}
+
+__global__ void k_avgpool_fwd(const bf16* x, int64_t x_ps, const int* nb, int hw, int Cp, bf16* out, int64_t out_ps) {
+  const int peer = blockIdx.y;
+  const int cpp = Cp / 8;
+  const int64_t n = (int64_t)nb[peer] * cpp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cpp);
+    const int64_t b = i / cpp;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[8];
+    for (int k = 0; k < hw; ++k) {
+      unpack8(*reinterpret_cast<const uint4*>(x + peer * x_ps + (b * hw + k) * Cp + c8 * 8), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += t[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] *= 1.f / hw;
+    *reinterpret_cast<uint4*>(out + peer * out_ps + b * Cp + c8 * 8) = pack8(s);
+  }
+}
+
+__global__ void k_avgpool_bwd(const bf16* dy, int64_t dy_ps, const int* nb, int hw, int Cp, bf16* dx, int64_t dx_ps) {
+  const int peer = blockIdx.y;
+  const int cpp = Cp / 8;
+  const int64_t n = (int64_t)nb[peer] * hw * cpp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cpp);
+    const int64_t px = i / cpp, b = px / hw;
+    float t[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + peer * dy_ps + b * Cp + c8 * 8), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] *= 1.f / hw;
+    *reinterpret_cast<uint4*>(dx + peer * dx_ps + px * Cp + c8 * 8) = pack8(t);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// log-softmax + NLL: loss/correct sums, confusion, dlogits = (softmax - onehot) / nb
+// ------------------------------------------------------------------------------------------------
+__global__ void k_xent(const bf16* logits, int64_t lg_ps, int Lp, int K, const int* labels, int B, const int* nb, float* stats, int* confusion,
+                       bf16* dlogits, int64_t dl_ps) {
+  const int peer = blockIdx.y;
+  const int n = nb[peer];
+  float loss = 0.f, correct = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const bf16* row = logits + peer * lg_ps + (int64_t)b * Lp;
+    if (b >= n) {
+      if (dlogits != nullptr)
+        for (int k = 0; k < Lp; ++k) dlogits[peer * dl_ps + (int64_t)b * Lp + k] = (bf16)0.f;
+      continue;
+    }
+    float z[32];
+    float mx = -INFINITY;
+    int am = 0;
+    for (int k = 0; k < K; ++k) {
+      z[k] = (float)row[k];
+      if (z[k] > mx) { mx = z[k]; am = k; }
+    }
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += __expf(z[k] - mx);
+    const float lse = mx + __logf(se);
+    const int y = labels[peer * B + b];
+    loss += lse - z[y];
+    correct += (am == y) ? 1.f : 0.f;
+    if (confusion != nullptr) atomicAdd(confusion + (peer * 16 + y) * 16 + am, 1);
+    if (dlogits != nullptr) {
+      const float invn = 1.f / (float)n;
+      for (int k = 0; k < Lp; ++k) {
+        const float pk = k < K ? __expf(z[k] - lse) : 0.f;
+        dlogits[peer * dl_ps + (int64_t)b * Lp + k] = (bf16)((pk - (k == y ? 1.f : 0.f)) * invn);
+      }
+    }
+  }
+  loss = wave_sum(loss);
+  correct = wave_sum(correct);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(stats + peer * 4 + 0, loss);
+    atomicAdd(stats + peer * 4 + 1, correct);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused optimizer + bf16 weight shadows, one block row per parameter segment (grid.y), peer grid.z
+// ------------------------------------------------------------------------------------------------
+struct Segment {
+  int64_t off;       // element offset in the flat parameter vector
+  int n;             // elements
+  int kind;          // 0 plain, 1 conv/fc weight with shadows
+  int cout, cin, R, S, cp_in, cp_out;
+  int64_t wf_off, wt_off;   // offsets in the shadow buffers
+  const int* colmap;        // torch input-column -> engine channel (fc after NHWC flatten) or null
+};
+
+__global__ void k_sgd_shadow(float* w, float* g, float* mbuf, int64_t ps, const Segment* segs, OptParams o, const float* anchor, const float* cg,
+                             const float* cl, int update, bf16* wf, bf16* wt, int64_t shadow_ps, const int* active) {
+  const int peer = blockIdx.z;
+  if (active != nullptr && !active[peer]) return;
+  const Segment sg = segs[blockIdx.y];
+  float* wp = w + peer * ps;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < sg.n; i += gridDim.x * blockDim.x) {
+    const int64_t idx = sg.off + i;
+    float wv = wp[idx];
+    if (update) {
+      float mv = mbuf[peer * ps + idx], vv = 0.f;
+      opt_update(o, g[peer * ps + idx], wv, mv, vv, 1.f, 1.f, anchor ? anchor + peer * ps : nullptr, cg ? cg + peer * ps : nullptr,
+                 cl ? cl + peer * ps : nullptr, idx);
+      wp[idx] = wv;
+      mbuf[peer * ps + idx] = mv;
+    }
+    if (sg.kind == 1) {
+      const int rsz = sg.R * sg.S;
+      const int co = i / (sg.cin * rsz);
+      const int rem = i - co * sg.cin * rsz;
+      const int col = rem / rsz, rs = rem - col * rsz;
+      const int ci = sg.colmap ? sg.colmap[col] : col;
+      const bf16 b = (bf16)wv;
+      wf[peer * shadow_ps + sg.wf_off + ((int64_t)co * rsz + rs) * sg.cp_in + ci] = b;
+      wt[peer * shadow_ps + sg.wt_off + ((int64_t)ci * rsz + rs) * sg.cp_out + co] = b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// C API
+// ------------------------------------------------------------------------------------------------
+static inline int ew_blocks(int64_t work) {
+  const int64_t b = (work + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+static inline int ok() { return hipGetLastError() == hipSuccess ? 0 : 2; }
+
+extern "C" {
+int cnn_input_prep(const uint8_t* const* xs, const int64_t* const* ys, const int* n_samples, const int* perm, int64_t perm_ps, int offset, int B,
+                   int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb, int peers, void* s) {
+  hipLaunchKernelGGL(k_input_prep, dim3(ew_blocks((int64_t)B * H * W * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, xs, ys, n_samples, perm,
+                     perm_ps, offset, B, H, W, C, Cp, scale, out, out_ps, labels, nb);
+  return ok();
+}
+int cnn_bn_finalize(const float* stats, int64_t stats_ps, int rows, const int* nb, int hw, const float* gamma, const float* beta, int64_t param_ps,
+                    float* rmean, float* rvar, int64_t run_ps, int C, int Cp, float eps, float momentum, int train, float* ss, float* ms, int peers,
+                    void* s) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3((Cp + 63) / 64, peers), dim3(256), 0, (hipStream_t)s, stats, stats_ps, rows, nb, hw, gamma, beta, param_ps,
+                     rmean, rvar, run_ps, C, Cp, eps, momentum, train, ss, ms);
+  return ok();
+}
+int cnn_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf16* res, int64_t res_ps, const bf16* y2, int64_t y2_ps, const float* ss2,
+               int relu, const int* nb, int max_rows, int hw, int Cp, bf16* out, int64_t out_ps, int peers, void* s) {
+  hipLaunchKernelGGL(k_bn_act, dim3(ew_blocks((int64_t)max_rows * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, y, y_ps, ss, res, res_ps, y2,
+                     y2_ps, ss2, relu, nb, hw, Cp, out, out_ps);
+  return ok();
+}
+int cnn_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms, const int* nb,
+                      int hw, int Cp, float* part, int64_t part_ps, int nblk, bf16* gout, int64_t gout_ps, int peers, void* s) {
+  if (Cp / 8 > 256 || (Cp & 7)) return 1;
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, y, y_ps, ms, nb, hw, Cp, part,
+                     part_ps, gout, gout_ps);
+  return ok();
+}
+int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps, const float* ms,
+                        float* dgamma, float* dbeta, int C, int Cp, float* coef, int peers, void* s) {
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((Cp + 255) / 256, peers), dim3(256), 0, (hipStream_t)s, part, part_ps, nblk, nb, hw, gamma, param_ps,
+                     ms, dgamma, dbeta, C, Cp, coef);
+  return ok();
+}
+int cnn_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms,
+                     const float* coef, const int* nb, int max_rows, int hw, int Cp, bf16* dy, int64_t dy_ps, int peers, void* s) {
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(ew_blocks((int64_t)max_rows * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps,
+                     y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps);
+  return ok();
+}
+int cnn_relu_bwd(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const int* nb, int max_rows, int hw, int Cp, bf16* out,
+                 int64_t out_ps, int peers, void* s) {
+  hipLaunchKernelGGL(k_relu_bwd, dim3(ew_blocks((int64_t)max_rows * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, nb,
+                     hw, Cp, out, out_ps);
+  return ok();
+}
+int cnn_colsum(const bf16* x, int64_t x_ps, const int* nb, int hw, int Cp, int C, float* out, int64_t out_ps, int nblk, int peers, void* s) {
+  if (Cp / 8 > 256 || (Cp & 7)) return 1;
+  hipLaunchKernelGGL(k_colsum, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, x, x_ps, nb, hw, Cp, C, out, out_ps);
+  return ok();
+}
+int cnn_maxpool2(int bwd, const bf16* x, int64_t x_ps, const bf16* dy, int64_t dy_ps, const int* nb, int max_batch, int H, int W, int Cp, bf16* out,
+                 int64_t out_ps, int peers, void* s) {
+  const int64_t work = (int64_t)max_batch * (H / 2) * (W / 2) * (Cp / 8);
+  if (bwd)
+    hipLaunchKernelGGL(k_maxpool2_bwd, dim3(ew_blocks(work), peers), dim3(256), 0, (hipStream_t)s, x, x_ps, dy, dy_ps, nb, H, W, Cp, out, out_ps);
+  else
+    hipLaunchKernelGGL(k_maxpool2_fwd, dim3(ew_blocks(work), peers), dim3(256), 0, (hipStream_t)s, x, x_ps, nb, H, W, Cp, out, out_ps);
+  return ok();
+}
+int cnn_avgpool(int bwd, const bf16* x, int64_t x_ps, const int* nb, int max_batch, int hw, int Cp, bf16* out, int64_t out_ps, int peers, void* s) {
+  if (bwd)
+    hipLaunchKernelGGL(k_avgpool_bwd, dim3(ew_blocks((int64_t)max_batch * hw * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, x, x_ps, nb, hw, Cp,
+                       out, out_ps);
+  else
+    hipLaunchKernelGGL(k_avgpool_fwd, dim3(ew_blocks((int64_t)max_batch * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, x, x_ps, nb, hw, Cp, out,
+                       out_ps);
+  return ok();
+}
+int cnn_xent(const bf16* logits, int64_t lg_ps, int Lp, int K, const int* labels, int B, const int* nb, float* stats, int* confusion, bf16* dlogits,
+             int64_t dl_ps, int peers, void* s) {
+  if (K > 16 || Lp < K) return 1;
+  hipLaunchKernelGGL(k_xent, dim3(1, peers), dim3(256), 0, (hipStream_t)s, logits, lg_ps, Lp, K, labels, B, nb, stats, confusion, dlogits, dl_ps);
+  return ok();
+}
+int cnn_sgd_shadow(float* w, float* g, float* m, int64_t ps, const void* segs, int nseg, int max_seg, int kind, float lr, float momentum,
+                   float weight_decay, int nesterov, float mu, const float* anchor, const float* cg, const float* cl, int update, bf16* wf, bf16* wt,
+                   int64_t shadow_ps, const int* active, int peers, void* s) {
+  OptParams o;
+  o.kind = kind;
+  o.lr = lr;
+  o.beta1 = 0.9f;
+  o.beta2 = 0.999f;
+  o.eps = 1e-8f;
+  o.weight_decay = weight_decay;
+  o.momentum = momentum;
+  o.nesterov = nesterov;
+  o.mu = mu;
+  const int bq = (max_seg + 255) / 256;
+  const int bx = bq < 1 ? 1 : (bq > 1024 ? 1024 : bq);
+  hipLaunchKernelGGL(k_sgd_shadow, dim3(bx, nseg, peers), dim3(256), 0, (hipStream_t)s, w, g, m, ps, (const Segment*)segs, o, anchor, cg, cl, update,
+                     wf, wt, shadow_ps, active);
+  return ok();
+}
+int cnn_segment_size() { return (int)sizeof(Segment); }
+}

@@ -1,0 +1,54 @@
+// Grouped NHWC bf16 convolution / BatchNorm / pooling / loss kernels for the CNN engine
+// (LeNet-5, ResNet-18; BASELINE configs 3-5). Every kernel handles P co-located peers in one
+// launch (grid.z = peer): a peer's tensors live at base + peer * peer_stride.
+//
+// Layouts
+//   activations : [rows = n*H*W][Cp] bf16, Cp = round_up(C, 8) (padding channels are kept zero)
+//   conv weights: fp32 master in the flat parameter buffer, torch order [Cout][Cin][R][S];
+//                 bf16 shadows  Wf[Cout][R][S][Cp_in]  (forward / B operand, K-contiguous)
+//                               Wt[Cin ][R][S][Cp_out] (dgrad B operand, K-contiguous)
+//   fc layers   : 1x1 convolutions on a 1x1 image (H = W = 1)
+#pragma once
+#include <stdint.h>
+
+#include "common.h"
+
+struct ConvGemmArgs {
+  // A operand gather source: FWD = input activations X, DGRAD = output gradient dY
+  const bf16* src; int64_t src_ps;      // peer stride (elements)
+  int src_h, src_w, src_c;              // spatial dims + channel stride of src
+  // geometry of the rows (M) this GEMM produces: FWD = output pixels, DGRAD = input pixels
+  int out_h, out_w;
+  int R, S, stride, pad;
+  // B operand: [Ncol][K] bf16, K = R*S*src_c
+  const bf16* wt; int64_t wt_ps;
+  int ncol;          // output channel stride (Cp_out for FWD, Cp_in for DGRAD)
+  int ncol_valid;    // logical channels (columns >= ncol_valid are written as 0)
+  // epilogue
+  bf16* out; int64_t out_ps;
+  const float* bias; int64_t bias_ps;   // optional, per column
+  const bf16* resid; int64_t resid_ps;  // optional, same layout as out (added before relu)
+  int relu;
+  float* stats; int64_t stats_ps;       // optional BN partial sums [2*tiles_m][2][ncol]
+  // per-peer valid batch (rows = nb * out_h * out_w); nullptr = all max_batch rows
+  const int* nbatch;
+  int max_batch;
+};
+
+struct WgradArgs {
+  const bf16* dy; int64_t dy_ps;        // [rows][dy_c] (rows = n*Ho*Wo)
+  const bf16* x; int64_t x_ps;          // [n*H*W][x_c]
+  int H, W, x_c, Ho, Wo, dy_c;
+  int R, S, stride, pad;
+  int cout, cin;                        // logical
+  float* grad; int64_t grad_ps;         // torch layout [cout][cin][R][S] (fp32, accumulated)
+  const int* flat_perm;                 // optional: fc after NHWC flatten (see engine)
+  int k_per_split;                      // rows of M per split (multiple of 64)
+  const int* nbatch;
+  int max_batch;
+};
+
+extern "C" {
+int conv_gemm_launch(int mode, const ConvGemmArgs* a, int peers, void* stream);
+int conv_wgrad_launch(const WgradArgs* a, int peers, int splits, void* stream);
+}

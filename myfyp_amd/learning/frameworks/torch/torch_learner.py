@@ -94,11 +94,13 @@ class TorchLearner(Learner):
     def _maybe_attach_engine(self, module: torch.nn.Module):
         if self.device.type != "cuda" or not Settings.USE_FUSED_KERNELS:
             return None
+        from myfyp_amd.parallel.cnn_engine import CNNEngineHandle
         from myfyp_amd.parallel.mlp_engine import MLPEngineHandle
 
-        if not MLPEngineHandle.supports(module):
-            return None
-        return MLPEngineHandle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
+        for handle in (MLPEngineHandle, CNNEngineHandle):
+            if handle.supports(module):
+                return handle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
+        return None
 
     def flat_params(self) -> torch.Tensor:
         if self._engine is not None:

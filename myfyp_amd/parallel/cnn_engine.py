@@ -1,0 +1,908 @@
+"""Grouped CNN engine (LeNet-5 / ResNet-18): co-located peers trained by one sequence of HIP launches.
+
+BASELINE configs 3-5 train CNNs on CIFAR-shaped data; the reference has no CNN at all. Like the MLP
+engine (:mod:`myfyp_amd.parallel.mlp_engine`), every peer of one architecture/batch size on a device
+gets a slot in stacked buffers and every kernel covers all peers through ``grid.z``:
+
+* parameters live in one ``[capacity, S]`` fp32 buffer laid out ``[trainable params | BN running
+  mean | BN running var]`` — the peers' ``nn.Module`` parameters *and* BN buffers are views into
+  their row (wire format / ``state_dict`` unchanged; FedAvg over the stacked rows averages BN
+  statistics too, like the reference's ``state_dict`` averaging);
+* activations are NHWC bf16 (channels padded to a multiple of 8), weights get two bf16 shadows
+  (forward ``[Cout][R][S][Cin]`` and dgrad ``[Cin][R][S][Cout]``) refreshed by the fused SGD kernel;
+* a train step is: input gather/convert → per conv: implicit-GEMM MFMA conv with BN partial sums
+  fused in its epilogue → BN finalize → BN apply (+residual) + ReLU → … → avg-pool → fc →
+  log-softmax/NLL (+dlogits) → backward (BN reduce/finalize/apply, dgrad conv with the residual
+  gradient added in its epilogue, wgrad conv with transposed LDS reads) → SGD + shadow refresh;
+* a whole local epoch is captured once into a HIP graph (``torch.cuda.CUDAGraph``) and replayed.
+
+Numerics: bf16 activations/MFMA operands, fp32 accumulation, fp32 master weights, BN statistics and
+optimizer state; torch SGD (momentum, weight decay, fresh optimizer per ``fit``) and torch
+BatchNorm (biased batch variance for normalisation, unbiased running variance, momentum 0.1).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Dict, List, Optional, Set, Tuple
+
+import numpy as np
+import torch
+
+from myfyp_amd.ops import _native
+from myfyp_amd.parallel.mlp_engine import _Gang
+from myfyp_amd.settings import Settings
+
+c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+
+class ConvGemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("src", c_void_p), ("src_ps", c_int64), ("src_h", c_int), ("src_w", c_int), ("src_c", c_int),
+        ("out_h", c_int), ("out_w", c_int), ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int),
+        ("wt", c_void_p), ("wt_ps", c_int64), ("ncol", c_int), ("ncol_valid", c_int),
+        ("out", c_void_p), ("out_ps", c_int64), ("bias", c_void_p), ("bias_ps", c_int64),
+        ("resid", c_void_p), ("resid_ps", c_int64), ("relu", c_int), ("stats", c_void_p), ("stats_ps", c_int64),
+        ("nbatch", c_void_p), ("max_batch", c_int),
+    ]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [
+        ("dy", c_void_p), ("dy_ps", c_int64), ("x", c_void_p), ("x_ps", c_int64),
+        ("H", c_int), ("W", c_int), ("x_c", c_int), ("Ho", c_int), ("Wo", c_int), ("dy_c", c_int),
+        ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int), ("cout", c_int), ("cin", c_int),
+        ("grad", c_void_p), ("grad_ps", c_int64), ("flat_perm", c_void_p), ("k_per_split", c_int),
+        ("nbatch", c_void_p), ("max_batch", c_int),
+    ]
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [
+        ("off", c_int64), ("n", c_int), ("kind", c_int), ("cout", c_int), ("cin", c_int), ("R", c_int), ("S", c_int),
+        ("cp_in", c_int), ("cp_out", c_int), ("wf_off", c_int64), ("wt_off", c_int64), ("colmap", c_void_p),
+    ]
+
+
+_SIGS = {
+    "conv_gemm_launch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
+    "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
+    "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+    "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "cnn_bn_act": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_bn_bwd_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_bn_bwd_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "cnn_bn_bwd_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_relu_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_colsum": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p]),
+    "cnn_maxpool2": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_avgpool": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_xent": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_sgd_shadow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
+    "cnn_segment_size": (c_int, []),
+}
+
+
+def _lib():
+    lib = _native.load(required=True)
+    if not getattr(lib, "_cnn_sigs", False):
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        if lib.cnn_segment_size() != ctypes.sizeof(Segment):
+            raise RuntimeError("Segment layout mismatch between Python and the native library")
+        lib._cnn_sigs = True
+    return lib
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _cp(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"CNN engine: {what} failed (rc={rc})")
+
+
+# ------------------------------------------------------------------------------------------------
+# architecture description
+# ------------------------------------------------------------------------------------------------
+class ConvL:
+    """A conv (or fc = 1x1 conv on a 1x1 image) layer of the program."""
+
+    def __init__(self, name: str, cin: int, cout: int, k: int, stride: int, pad: int, h: int, w: int, weight, bias=None, colmap=None) -> None:
+        self.name, self.cin, self.cout, self.R, self.S, self.stride, self.pad = name, cin, cout, k, k, stride, pad
+        self.h, self.w = h, w
+        self.ho, self.wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+        self.cp_in, self.cp_out = _cp(cin), _cp(cout)
+        self.weight, self.bias = weight, bias
+        self.colmap = colmap  # torch input column -> engine channel (fc after NHWC flatten)
+
+
+class BNL:
+    def __init__(self, name: str, module: torch.nn.BatchNorm2d) -> None:
+        self.name, self.module = name, module
+        self.C = module.num_features
+        self.Cp = _cp(self.C)
+        self.eps, self.momentum = float(module.eps), float(module.momentum if module.momentum is not None else 0.1)
+
+
+def arch_of(module: torch.nn.Module) -> Optional[str]:
+    from myfyp_amd.models.cnn import LeNet5, ResNet18
+
+    if isinstance(module, ResNet18):
+        return "resnet18"
+    if isinstance(module, LeNet5):
+        return "lenet5"
+    return None
+
+
+def arch_key(module: torch.nn.Module) -> Optional[tuple]:
+    a = arch_of(module)
+    if a is None:
+        return None
+    shapes = tuple((n, tuple(p.shape)) for n, p in module.named_parameters())
+    return (a, shapes, float(getattr(module, "input_scale", 1.0)), int(getattr(module, "image_size", 32)))
+
+
+# ------------------------------------------------------------------------------------------------
+# the group
+# ------------------------------------------------------------------------------------------------
+class CNNGroup:
+    _groups: Dict[tuple, "CNNGroup"] = {}
+    _lock = threading.Lock()
+
+    @classmethod
+    def get(cls, device: torch.device, module: torch.nn.Module, batch_size: int) -> "CNNGroup":
+        key = (str(device), arch_key(module), batch_size)
+        with cls._lock:
+            g = cls._groups.get(key)
+            if g is None:
+                g = cls(device, module, batch_size)
+                cls._groups[key] = g
+            return g
+
+    @classmethod
+    def reset_all(cls) -> None:
+        with cls._lock:
+            cls._groups.clear()
+
+    def __init__(self, device: torch.device, template: torch.nn.Module, batch_size: int, capacity: int = 8) -> None:
+        self.device = device
+        self.B = batch_size
+        self.arch = arch_of(template)
+        self.lock = threading.RLock()
+        self.handles: Dict[int, "CNNEngineHandle"] = {}
+        self.capacity = 0
+        self.extras: Dict[str, torch.Tensor] = {}
+        self.perm_fn = None
+        self.eager = False
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._seen: set = set()
+        self._data_version = 0
+        self._bound_version = -1
+        self._describe(template)
+        self._alloc(capacity)
+        self.fit_gang = _Gang(self._run_fit_batch)
+        self.eval_gang = _Gang(self._run_eval_batch)
+
+    # ------------------------------------------------------------------ description
+    def _describe(self, m: torch.nn.Module) -> None:
+        params = [p for p in m.parameters()]
+        self.param_off: Dict[int, int] = {}
+        off = 0
+        for p in params:
+            self.param_off[id(p)] = off
+            off += p.numel()
+        self.n_params = off
+        self._param_names = {id(p): n for n, p in m.named_parameters()}
+        self.bns: List[BNL] = []
+        self.convs: List[ConvL] = []
+        self.in_scale = float(getattr(m, "input_scale", 1.0))
+        if self.arch == "resnet18":
+            self.in_c = m.conv1.in_channels
+            self.in_h = self.in_w = 32
+            self._resnet_desc(m)
+        else:
+            self.in_c = m.conv1.in_channels
+            self.in_h = self.in_w = int(getattr(m, "image_size", 32))
+            self._lenet_desc(m)
+        # BN running stats after the params: [rm(all BNs) | rv(all BNs)]
+        self.bn_off: Dict[str, int] = {}
+        o = 0
+        for bn in self.bns:
+            self.bn_off[bn.name] = o
+            o += bn.C
+        self.bn_total = o
+        self.numel = self.n_params + 2 * self.bn_total
+        self.S = (self.numel + 63) // 64 * 64
+        # shadows
+        self.shadow_off: Dict[str, Tuple[int, int]] = {}
+        so = 0
+        for c in self.convs:
+            nf = c.cp_out * c.R * c.S * c.cp_in
+            self.shadow_off[c.name] = (so, so + nf)
+            so += 2 * nf + 64
+        self.shadow_numel = so
+
+    def _off(self, p) -> int:
+        return self.param_off[id(p)]
+
+    def _resnet_desc(self, m) -> None:
+        h = 32
+        self.stem = ConvL("stem", m.conv1.in_channels, 64, 3, 1, 1, h, h, m.conv1.weight)
+        self.stem_bn = BNL("stem_bn", m.bn1)
+        self.convs.append(self.stem)
+        self.bns.append(self.stem_bn)
+        self.blocks = []
+        for bi, blk in enumerate(m.layers):
+            c1 = blk.conv1
+            cv1 = ConvL(f"b{bi}c1", c1.in_channels, c1.out_channels, 3, c1.stride[0], 1, h, h, c1.weight)
+            h2 = cv1.ho
+            cv2 = ConvL(f"b{bi}c2", blk.conv2.in_channels, blk.conv2.out_channels, 3, 1, 1, h2, h2, blk.conv2.weight)
+            bn1, bn2 = BNL(f"b{bi}bn1", blk.bn1), BNL(f"b{bi}bn2", blk.bn2)
+            proj = None
+            if len(blk.shortcut) > 0:
+                sc, sbn = blk.shortcut[0], blk.shortcut[1]
+                proj = (ConvL(f"b{bi}sc", sc.in_channels, sc.out_channels, 1, sc.stride[0], 0, h, h, sc.weight), BNL(f"b{bi}sbn", sbn))
+            self.convs += [cv1, cv2] + ([proj[0]] if proj else [])
+            self.bns += [bn1, bn2] + ([proj[1]] if proj else [])
+            self.blocks.append((cv1, bn1, cv2, bn2, proj))
+            h = h2
+        self.final_hw = h * h
+        self.fc = ConvL("fc", m.fc.in_features, m.fc.out_features, 1, 1, 0, 1, 1, m.fc.weight, m.fc.bias)
+        self.convs.append(self.fc)
+        self.n_classes = m.fc.out_features
+
+    def _lenet_desc(self, m) -> None:
+        h = self.in_h
+        self.l_c1 = ConvL("c1", m.conv1.in_channels, m.conv1.out_channels, m.conv1.kernel_size[0], 1, 0, h, h, m.conv1.weight, m.conv1.bias)
+        h1 = self.l_c1.ho // 2
+        self.l_c2 = ConvL("c2", m.conv2.in_channels, m.conv2.out_channels, m.conv2.kernel_size[0], 1, 0, h1, h1, m.conv2.weight, m.conv2.bias)
+        h2 = self.l_c2.ho // 2
+        C2 = m.conv2.out_channels
+        cp2 = _cp(C2)
+        flat_in = h2 * h2 * cp2
+        # torch flattens NCHW as (c, h, w); the engine's pooled tensor is (h, w, c) with padded c
+        colmap = np.zeros(C2 * h2 * h2, dtype=np.int32)
+        for c in range(C2):
+            for y in range(h2):
+                for x in range(h2):
+                    colmap[(c * h2 + y) * h2 + x] = (y * h2 + x) * cp2 + c
+        self.l_fc1 = ConvL("fc1", flat_in, m.fc1.out_features, 1, 1, 0, 1, 1, m.fc1.weight, m.fc1.bias, colmap=colmap)
+        self.l_fc1.cin_torch = C2 * h2 * h2
+        self.l_fc2 = ConvL("fc2", m.fc2.in_features, m.fc2.out_features, 1, 1, 0, 1, 1, m.fc2.weight, m.fc2.bias)
+        self.l_fc3 = ConvL("fc3", m.fc3.in_features, m.fc3.out_features, 1, 1, 0, 1, 1, m.fc3.weight, m.fc3.bias)
+        self.convs = [self.l_c1, self.l_c2, self.l_fc1, self.l_fc2, self.l_fc3]
+        self.lenet_h = (h, h1, h2)
+        self.n_classes = m.fc3.out_features
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self, capacity: int) -> None:
+        dev = self.device
+        old = getattr(self, "params", None)
+        params = torch.zeros(capacity, self.S, dtype=torch.float32, device=dev)
+        if old is not None:
+            params[: self.capacity].copy_(old)
+        self.params = params
+        self.grad = torch.zeros_like(params)
+        self.mom = torch.zeros_like(params)
+        self.shadow = torch.zeros(capacity, self.shadow_numel, dtype=torch.bfloat16, device=dev)
+        self.capacity = capacity
+        for slot, h in self.handles.items():
+            h.retarget()
+        self._acts: Dict[str, torch.Tensor] = {}
+        self._graphs.clear()
+        self._seen = set()
+        self._build_segments()
+
+    def _build_segments(self) -> None:
+        segs = []
+        self._keep_colmaps = []
+        for c in self.convs:
+            wf, wt = self.shadow_off[c.name]
+            cm = 0
+            if c.colmap is not None:
+                t = torch.from_numpy(c.colmap).to(self.device)
+                self._keep_colmaps.append(t)
+                cm = t.data_ptr()
+            cin_t = getattr(c, "cin_torch", c.cin)
+            segs.append(Segment(self._off(c.weight), c.weight.numel(), 1, c.cout, cin_t, c.R, c.S, c.cp_in, c.cp_out, wf, wt, cm))
+            if c.bias is not None:
+                segs.append(Segment(self._off(c.bias), c.bias.numel(), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+        for bn in self.bns:
+            for p in (bn.module.weight, bn.module.bias):
+                segs.append(Segment(self._off(p), p.numel(), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+        arr = (Segment * len(segs))(*segs)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.segs = raw.to(self.device)
+        self.nseg = len(segs)
+        self.max_seg = max(s.n for s in segs)
+
+    def act(self, name: str, rows: int, cp: int, dtype=torch.bfloat16) -> torch.Tensor:
+        t = self._acts.get(name)
+        if t is None:
+            t = torch.zeros(self.capacity, rows * cp, dtype=dtype, device=self.device)
+            self._acts[name] = t
+        return t
+
+    def fbuf(self, name: str, n: int) -> torch.Tensor:
+        return self.act(name, n, 1, torch.float32)
+
+    def ibuf(self, name: str, n: int) -> torch.Tensor:
+        return self.act(name, n, 1, torch.int32)
+
+    def attach(self, handle: "CNNEngineHandle") -> int:
+        with self.lock:
+            slot = next((i for i in range(self.capacity) if i not in self.handles), None)
+            if slot is None:
+                self._alloc(self.capacity * 2)
+                slot = next(i for i in range(self.capacity) if i not in self.handles)
+            self.handles[slot] = handle
+            self._data_version += 1
+            return slot
+
+    def detach(self, slot: int) -> None:
+        with self.lock:
+            self.handles.pop(slot, None)
+            self._data_version += 1
+
+    def invalidate_data(self) -> None:
+        with self.lock:
+            self._data_version += 1
+
+    def close(self) -> None:
+        self._graphs.clear()
+
+    def _extra_buffer(self, name: str) -> torch.Tensor:
+        buf = self.extras.get(name)
+        if buf is None or buf.shape[0] != self.capacity:
+            buf = torch.zeros(self.capacity, self.S, dtype=torch.float32, device=self.device)
+            self.extras[name] = buf
+        return buf
+
+    # ------------------------------------------------------------------ data binding
+    def _bind_data(self) -> None:
+        cap, dev = self.capacity, self.device
+        self._keep = []
+        xs, ys, ns, xts, yts, nts = [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap
+        for slot, h in self.handles.items():
+            (x, y), (xt, yt) = h.device_split(True), h.device_split(False)
+            xs[slot], ys[slot], ns[slot] = x.data_ptr(), y.data_ptr(), x.shape[0]
+            xts[slot], yts[slot], nts[slot] = xt.data_ptr(), yt.data_ptr(), xt.shape[0]
+            self._keep += [x, y, xt, yt]
+        self.n_train, self.n_test = ns, nts
+        self.tab = {
+            "xs": torch.tensor(xs, dtype=torch.int64, device=dev), "ys": torch.tensor(ys, dtype=torch.int64, device=dev),
+            "n": torch.tensor(ns, dtype=torch.int32, device=dev), "xts": torch.tensor(xts, dtype=torch.int64, device=dev),
+            "yts": torch.tensor(yts, dtype=torch.int64, device=dev), "nt": torch.tensor(nts, dtype=torch.int32, device=dev),
+        }
+        self.nmax = max(1, max(ns) if ns else 1)
+        self.ntmax = max(1, max(nts) if nts else 1)
+        self.perm = torch.zeros(cap, self.nmax, dtype=torch.int32, device=dev)
+        self._perm_mask = torch.arange(self.nmax, device=dev).unsqueeze(0) >= torch.tensor(ns, device=dev).unsqueeze(1)
+        self._graphs.clear()
+        self._seen = set()
+
+    def _ensure(self) -> None:
+        if self._bound_version != self._data_version:
+            self._bind_data()
+            self._bound_version = self._data_version
+
+    # ------------------------------------------------------------------ kernel wrappers
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None) -> None:
+        lib, P = _lib(), self.capacity
+        shadow_f, shadow_t = self.shadow_off[L.name]
+        a = ConvGemmArgs()
+        if mode == 0:
+            a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.h, L.w, L.cp_in
+            a.out_h, a.out_w = L.ho, L.wo
+            a.wt = self.shadow.data_ptr() + 2 * shadow_f
+            a.ncol, a.ncol_valid = L.cp_out, L.cout
+        else:
+            a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.ho, L.wo, L.cp_out
+            a.out_h, a.out_w = L.h, L.w
+            a.wt = self.shadow.data_ptr() + 2 * shadow_t
+            a.ncol, a.ncol_valid = L.cp_in, (L.cin if L.colmap is None else L.cp_in)
+        a.src_ps, a.wt_ps = src.shape[1], self.shadow.shape[1]
+        a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, L.pad
+        a.out, a.out_ps = out.data_ptr(), out.shape[1]
+        if bias and L.bias is not None:
+            a.bias, a.bias_ps = self.params.data_ptr() + 4 * self._off(L.bias), self.params.shape[1]
+        if resid is not None:
+            a.resid, a.resid_ps = resid.data_ptr(), resid.shape[1]
+        a.relu = int(relu)
+        if stats is not None:
+            a.stats, a.stats_ps = stats.data_ptr(), stats.shape[1]
+        a.nbatch, a.max_batch = self.nb.data_ptr(), self.B
+        _chk(lib.conv_gemm_launch(mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
+
+    def wgrad(self, L: ConvL, dy: torch.Tensor, x: torch.Tensor) -> None:
+        lib, P = _lib(), self.capacity
+        a = WgradArgs()
+        a.dy, a.dy_ps, a.x, a.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
+        a.H, a.W, a.x_c, a.Ho, a.Wo, a.dy_c = L.h, L.w, L.cp_in, L.ho, L.wo, L.cp_out
+        a.R, a.S, a.stride, a.pad, a.cout, a.cin = L.R, L.S, L.stride, L.pad, L.cout, getattr(L, "cin_torch", L.cin)
+        a.grad, a.grad_ps = self.grad.data_ptr() + 4 * self._off(L.weight), self.grad.shape[1]
+        if L.colmap is not None:
+            a.flat_perm = self._inv_colmap(L).data_ptr()
+        M = self.B * L.ho * L.wo
+        ncol = L.R * L.S * L.cp_in
+        tiles = ((L.cp_out + 127) // 128) * ((ncol + 127) // 128)
+        want = max(1, (4 * 256) // max(1, tiles * P))
+        k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
+        splits = (M + k_per - 1) // k_per
+        a.k_per_split, a.nbatch, a.max_batch = k_per, self.nb.data_ptr(), self.B
+        _chk(lib.conv_wgrad_launch(ctypes.byref(a), P, splits, self._stream()), f"wgrad {L.name}")
+
+    def _inv_colmap(self, L: ConvL) -> torch.Tensor:
+        key = f"_invcol_{L.name}"
+        t = getattr(self, key, None)
+        if t is None:
+            inv = np.full(L.cp_in, -1, dtype=np.int32)  # -1: padding channel of the flattened tensor
+            inv[L.colmap] = np.arange(len(L.colmap), dtype=np.int32)
+            t = torch.from_numpy(inv).to(self.device)
+            setattr(self, key, t)
+        return t
+
+    def bn_fin(self, bn: BNL, stats: torch.Tensor, rows: int, hw: int, train: bool) -> None:
+        lib, P = _lib(), self.capacity
+        g, b = bn.module.weight, bn.module.bias
+        ro = self.n_params + self.bn_off[bn.name]
+        base = self.params.data_ptr()
+        _chk(lib.cnn_bn_finalize(
+            _p(stats) if stats is not None else None, stats.shape[1] if stats is not None else 0, rows, self.nb.data_ptr(), hw,
+            base + 4 * self._off(g), base + 4 * self._off(b), self.params.shape[1], base + 4 * ro, base + 4 * (ro + self.bn_total), self.params.shape[1],
+            bn.C, bn.Cp, bn.eps, bn.momentum, int(train), self.ss(bn).data_ptr(), self.ms(bn).data_ptr(), P, self._stream()), f"bn_fin {bn.name}")
+
+    def ss(self, bn: BNL) -> torch.Tensor:
+        return self.fbuf(f"ss_{bn.name}", 2 * bn.Cp)
+
+    def ms(self, bn: BNL) -> torch.Tensor:
+        return self.fbuf(f"ms_{bn.name}", 2 * bn.Cp)
+
+    def bn_act(self, bn: BNL, y, out, hw, relu=True, res=None, y2=None, bn2: Optional[BNL] = None) -> None:
+        lib, P = _lib(), self.capacity
+        _chk(lib.cnn_bn_act(y.data_ptr(), y.shape[1], self.ss(bn).data_ptr(), _p(res), res.shape[1] if res is not None else 0, _p(y2),
+                            y2.shape[1] if y2 is not None else 0, self.ss(bn2).data_ptr() if bn2 is not None else None, int(relu), self.nb.data_ptr(),
+                            self.B * hw, hw, bn.Cp, out.data_ptr(), out.shape[1], P, self._stream()), f"bn_act {bn.name}")
+
+    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None) -> None:
+        lib, P = _lib(), self.capacity
+        nblk = max(1, min(128, (self.B * hw + 255) // 256))
+        part = self.fbuf(f"bnpart_{bn.name}", nblk * 2 * bn.Cp)
+        coef = self.fbuf(f"bncoef_{bn.name}", 3 * bn.Cp)
+        _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
+                                   self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
+                                   gout.shape[1] if gout is not None else 0, P, self._stream()), f"bn_bwd_reduce {bn.name}")
+        gbase = self.grad.data_ptr()
+        _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nblk, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
+                                     self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight), gbase + 4 * self._off(bn.module.bias),
+                                     bn.C, bn.Cp, coef.data_ptr(), P, self._stream()), f"bn_bwd_finalize {bn.name}")
+        _chk(lib.cnn_bn_bwd_apply(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
+                                  self.ms(bn).data_ptr(), coef.data_ptr(), self.nb.data_ptr(), self.B * hw, hw, bn.Cp, dy_out.data_ptr(),
+                                  dy_out.shape[1], P, self._stream()), f"bn_bwd_apply {bn.name}")
+
+    def relu_bwd(self, dz, mask, out, hw, cp) -> None:
+        _chk(_lib().cnn_relu_bwd(dz.data_ptr(), dz.shape[1], mask.data_ptr(), mask.shape[1], self.nb.data_ptr(), self.B * hw, hw, cp, out.data_ptr(),
+                                 out.shape[1], self.capacity, self._stream()), "relu_bwd")
+
+    def bias_grad(self, L: ConvL, dy, hw) -> None:
+        nblk = max(1, min(64, (self.B * hw + 255) // 256))
+        _chk(_lib().cnn_colsum(dy.data_ptr(), dy.shape[1], self.nb.data_ptr(), hw, L.cp_out, L.cout, self.grad.data_ptr() + 4 * self._off(L.bias),
+                               self.grad.shape[1], nblk, self.capacity, self._stream()), f"bias_grad {L.name}")
+
+    # ------------------------------------------------------------------ programs
+    def _prep(self, train: bool, offset: int) -> torch.Tensor:
+        lib, P, B = _lib(), self.capacity, self.B
+        cp0 = _cp(self.in_c)
+        x0 = self.act("x0", B * self.in_h * self.in_w, cp0)
+        t = self.tab
+        perm = self.perm if train else None
+        _chk(lib.cnn_input_prep(_p(t["xs"] if train else t["xts"]), _p(t["ys"] if train else t["yts"]), _p(t["n"] if train else t["nt"]), _p(perm),
+                                self.nmax if train else 0, offset, B, self.in_h, self.in_w, self.in_c, cp0, self.in_scale, x0.data_ptr(), x0.shape[1],
+                                self.labels.data_ptr(), self.nb.data_ptr(), P, self._stream()), "input_prep")
+        return x0
+
+    def _forward_resnet(self, x0: torch.Tensor, train: bool) -> torch.Tensor:
+        B = self.B
+        L, bn = self.stem, self.stem_bn
+        hw = L.ho * L.wo
+        y = self.act("y_stem", B * hw, L.cp_out)
+        st = self.fbuf("st_stem", _lib().conv_gemm_stats_rows(B, L.ho, L.wo) * 2 * L.cp_out) if train else None
+        self.conv(L, x0, y, stats=st)
+        self.bn_fin(bn, st, _lib().conv_gemm_stats_rows(B, L.ho, L.wo), hw, train)
+        a = self.act("a_stem", B * hw, L.cp_out)
+        self.bn_act(bn, y, a, hw)
+        for bi, (c1, bn1, c2, bn2, proj) in enumerate(self.blocks):
+            a_in = a
+            hw1 = c1.ho * c1.wo
+            rows1 = _lib().conv_gemm_stats_rows(B, c1.ho, c1.wo)
+            y1 = self.act(f"y1_{bi}", B * hw1, c1.cp_out)
+            st1 = self.fbuf(f"st1_{bi}", rows1 * 2 * c1.cp_out) if train else None
+            self.conv(c1, a_in, y1, stats=st1)
+            self.bn_fin(bn1, st1, rows1, hw1, train)
+            a1 = self.act(f"a1_{bi}", B * hw1, c1.cp_out)
+            self.bn_act(bn1, y1, a1, hw1)
+            y2 = self.act(f"y2_{bi}", B * hw1, c2.cp_out)
+            st2 = self.fbuf(f"st2_{bi}", rows1 * 2 * c2.cp_out) if train else None
+            self.conv(c2, a1, y2, stats=st2)
+            self.bn_fin(bn2, st2, rows1, hw1, train)
+            a = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
+            if proj is not None:
+                cs, bns = proj
+                ys = self.act(f"ys_{bi}", B * hw1, cs.cp_out)
+                sts = self.fbuf(f"sts_{bi}", rows1 * 2 * cs.cp_out) if train else None
+                self.conv(cs, a_in, ys, stats=sts)
+                self.bn_fin(bns, sts, rows1, hw1, train)
+                self.bn_act(bn2, y2, a, hw1, y2=ys, bn2=bns)
+            else:
+                self.bn_act(bn2, y2, a, hw1, res=a_in)
+        pooled = self.act("pooled", B, self.fc.cp_in)
+        _chk(_lib().cnn_avgpool(0, a.data_ptr(), a.shape[1], self.nb.data_ptr(), B, self.final_hw, self.fc.cp_in, pooled.data_ptr(), pooled.shape[1],
+                                self.capacity, self._stream()), "avgpool")
+        logits = self.act("logits", B, self.fc.cp_out)
+        self.conv(self.fc, pooled, logits, bias=True)
+        self._last_act = a
+        return logits
+
+    def _backward_resnet(self, dlogits: torch.Tensor) -> None:
+        B, lib = self.B, _lib()
+        fc = self.fc
+        pooled = self.act("pooled", B, fc.cp_in)
+        dpooled = self.act("dpooled", B, fc.cp_in)
+        self.conv(fc, dlogits, dpooled, mode=1)
+        self.wgrad(fc, dlogits, pooled)
+        self.bias_grad(fc, dlogits, 1)
+        last = self.blocks[-1][2]
+        hw = last.ho * last.wo
+        d = self.act(f"d_out_{len(self.blocks) - 1}", B * hw, last.cp_out)
+        _chk(lib.cnn_avgpool(1, dpooled.data_ptr(), dpooled.shape[1], self.nb.data_ptr(), B, self.final_hw, fc.cp_in, d.data_ptr(), d.shape[1],
+                             self.capacity, self._stream()), "avgpool_bwd")
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            c1, bn1, c2, bn2, proj = self.blocks[bi]
+            hw1 = c1.ho * c1.wo
+            a_out = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
+            a_in = self.act(f"a2_{bi - 1}", B * c1.h * c1.w, c1.cp_in) if bi > 0 else self.act("a_stem", B * c1.h * c1.w, c1.cp_in)
+            y1, a1, y2 = self.act(f"y1_{bi}", B * hw1, c1.cp_out), self.act(f"a1_{bi}", B * hw1, c1.cp_out), self.act(f"y2_{bi}", B * hw1, c2.cp_out)
+            dy2 = self.act(f"dy2_{bi}", B * hw1, c2.cp_out)
+            d_in = self.act(f"d_out_{bi - 1}" if bi > 0 else "d_stem", B * c1.h * c1.w, c1.cp_in)
+            if proj is not None:
+                cs, bns = proj
+                ys = self.act(f"ys_{bi}", B * hw1, cs.cp_out)
+                self.bn_bwd(bn2, d, a_out, y2, dy2, hw1)
+                dys = self.act(f"dys_{bi}", B * hw1, cs.cp_out)
+                self.bn_bwd(bns, d, a_out, ys, dys, hw1)
+                dsc = self.act(f"dsc_{bi}", B * c1.h * c1.w, c1.cp_in)
+                self.conv(cs, dys, dsc, mode=1)
+                self.wgrad(cs, dys, a_in)
+                resid = dsc
+            else:
+                g = self.act(f"g_{bi}", B * hw1, c2.cp_out)
+                self.bn_bwd(bn2, d, a_out, y2, dy2, hw1, gout=g)
+                resid = g
+            da1 = self.act(f"da1_{bi}", B * hw1, c1.cp_out)
+            self.conv(c2, dy2, da1, mode=1)
+            self.wgrad(c2, dy2, a1)
+            dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
+            self.bn_bwd(bn1, da1, a1, y1, dy1, hw1)
+            self.conv(c1, dy1, d_in, mode=1, resid=resid)
+            self.wgrad(c1, dy1, a_in)
+            d = d_in
+        L, bn = self.stem, self.stem_bn
+        hw = L.ho * L.wo
+        dys = self.act("dy_stem", B * hw, L.cp_out)
+        self.bn_bwd(bn, d, self.act("a_stem", B * hw, L.cp_out), self.act("y_stem", B * hw, L.cp_out), dys, hw)
+        self.wgrad(L, dys, self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c)))
+
+    def _forward_lenet(self, x0: torch.Tensor, train: bool) -> torch.Tensor:
+        B, lib, P = self.B, _lib(), self.capacity
+        c1, c2, f1, f2, f3 = self.l_c1, self.l_c2, self.l_fc1, self.l_fc2, self.l_fc3
+        h0, h1, h2 = self.lenet_h
+        z1 = self.act("z1", B * c1.ho * c1.wo, c1.cp_out)
+        self.conv(c1, x0, z1, bias=True, relu=True)
+        p1 = self.act("p1", B * h1 * h1, c1.cp_out)
+        _chk(lib.cnn_maxpool2(0, z1.data_ptr(), z1.shape[1], None, 0, self.nb.data_ptr(), B, c1.ho, c1.wo, c1.cp_out, p1.data_ptr(), p1.shape[1], P,
+                              self._stream()), "maxpool1")
+        z2 = self.act("z2", B * c2.ho * c2.wo, c2.cp_out)
+        self.conv(c2, p1, z2, bias=True, relu=True)
+        p2 = self.act("p2", B * h2 * h2, c2.cp_out)
+        _chk(lib.cnn_maxpool2(0, z2.data_ptr(), z2.shape[1], None, 0, self.nb.data_ptr(), B, c2.ho, c2.wo, c2.cp_out, p2.data_ptr(), p2.shape[1], P,
+                              self._stream()), "maxpool2")
+        # p2 [B][h2][w2][cp2] is exactly fc1's [B][1][1][h2*w2*cp2] input
+        z3 = self.act("z3", B, f1.cp_out)
+        self.conv(f1, p2, z3, bias=True, relu=True)
+        z4 = self.act("z4", B, f2.cp_out)
+        self.conv(f2, z3, z4, bias=True, relu=True)
+        logits = self.act("logits", B, f3.cp_out)
+        self.conv(f3, z4, logits, bias=True)
+        return logits
+
+    def _backward_lenet(self, dlogits: torch.Tensor) -> None:
+        B, lib, P = self.B, _lib(), self.capacity
+        c1, c2, f1, f2, f3 = self.l_c1, self.l_c2, self.l_fc1, self.l_fc2, self.l_fc3
+        h0, h1, h2 = self.lenet_h
+        z4, z3 = self.act("z4", B, f2.cp_out), self.act("z3", B, f1.cp_out)
+        p2, z2 = self.act("p2", B * h2 * h2, c2.cp_out), self.act("z2", B * c2.ho * c2.wo, c2.cp_out)
+        p1, z1 = self.act("p1", B * h1 * h1, c1.cp_out), self.act("z1", B * c1.ho * c1.wo, c1.cp_out)
+        x0 = self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c))
+        # fc3
+        self.wgrad(f3, dlogits, z4)
+        self.bias_grad(f3, dlogits, 1)
+        dz4 = self.act("dz4", B, f2.cp_out)
+        self.conv(f3, dlogits, dz4, mode=1)
+        g4 = self.act("g4", B, f2.cp_out)
+        self.relu_bwd(dz4, z4, g4, 1, f2.cp_out)
+        self.wgrad(f2, g4, z3)
+        self.bias_grad(f2, g4, 1)
+        dz3 = self.act("dz3", B, f1.cp_out)
+        self.conv(f2, g4, dz3, mode=1)
+        g3 = self.act("g3", B, f1.cp_out)
+        self.relu_bwd(dz3, z3, g3, 1, f1.cp_out)
+        self.wgrad(f1, g3, p2)
+        self.bias_grad(f1, g3, 1)
+        dp2 = self.act("dp2", B * h2 * h2, c2.cp_out)
+        self.conv(f1, g3, dp2, mode=1)
+        dz2 = self.act("dz2", B * c2.ho * c2.wo, c2.cp_out)
+        _chk(lib.cnn_maxpool2(1, z2.data_ptr(), z2.shape[1], dp2.data_ptr(), dp2.shape[1], self.nb.data_ptr(), B, c2.ho, c2.wo, c2.cp_out, dz2.data_ptr(),
+                              dz2.shape[1], P, self._stream()), "maxpool2_bwd")
+        g2 = self.act("g2", B * c2.ho * c2.wo, c2.cp_out)
+        self.relu_bwd(dz2, z2, g2, c2.ho * c2.wo, c2.cp_out)
+        self.wgrad(c2, g2, p1)
+        self.bias_grad(c2, g2, c2.ho * c2.wo)
+        dp1 = self.act("dp1", B * h1 * h1, c1.cp_out)
+        self.conv(c2, g2, dp1, mode=1)
+        dz1 = self.act("dz1", B * c1.ho * c1.wo, c1.cp_out)
+        _chk(lib.cnn_maxpool2(1, z1.data_ptr(), z1.shape[1], dp1.data_ptr(), dp1.shape[1], self.nb.data_ptr(), B, c1.ho, c1.wo, c1.cp_out, dz1.data_ptr(),
+                              dz1.shape[1], P, self._stream()), "maxpool1_bwd")
+        g1 = self.act("g1", B * c1.ho * c1.wo, c1.cp_out)
+        self.relu_bwd(dz1, z1, g1, c1.ho * c1.wo, c1.cp_out)
+        self.wgrad(c1, g1, x0)
+        self.bias_grad(c1, g1, c1.ho * c1.wo)
+
+    def _xent(self, logits, train: bool) -> None:
+        Lp = self.convs[-1].cp_out
+        dl = self.act("dlogits", self.B, Lp) if train else None
+        _chk(_lib().cnn_xent(logits.data_ptr(), logits.shape[1], Lp, self.n_classes, self.labels.data_ptr(), self.B, self.nb.data_ptr(),
+                             self.stat.data_ptr(), None if train else self.conf.data_ptr(), _p(dl), dl.shape[1] if dl is not None else 0, self.capacity,
+                             self._stream()), "xent")
+
+    def _train_step(self, offset: int) -> None:
+        x0 = self._prep(True, offset)
+        self.grad.zero_()
+        if self.arch == "resnet18":
+            logits = self._forward_resnet(x0, True)
+            self._xent(logits, True)
+            self._backward_resnet(self.act("dlogits", self.B, self.fc.cp_out))
+        else:
+            logits = self._forward_lenet(x0, True)
+            self._xent(logits, True)
+            self._backward_lenet(self.act("dlogits", self.B, self.l_fc3.cp_out))
+        self._optimizer(update=True)
+
+    def _optimizer(self, update: bool) -> None:
+        o = self._opt
+        _chk(_lib().cnn_sgd_shadow(self.params.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg,
+                                   self.max_seg, o["kind"], o["lr"], o["momentum"], o["weight_decay"], o["nesterov"], o["mu"], _p(o.get("anchor")),
+                                   _p(o.get("cg")), _p(o.get("cl")), int(update), self.shadow.data_ptr(), self.shadow.data_ptr(), self.shadow.shape[1],
+                                   self.nb.data_ptr() if update else None, self.capacity, self._stream()), "sgd_shadow")
+
+    def _shadow_sync(self) -> None:
+        saved = getattr(self, "_opt", None)
+        self._opt = {"kind": 1, "lr": 0.0, "momentum": 0.0, "weight_decay": 0.0, "nesterov": 0, "mu": 0.0}
+        self._optimizer(update=False)
+        if saved is not None:
+            self._opt = saved
+
+    # ------------------------------------------------------------------ batched fit / eval
+    def _common_buffers(self) -> None:
+        self.nb = self.ibuf("nb", 1)
+        self.labels = self.ibuf("labels", self.B)
+        self.stat = self.fbuf("stat", 4)
+        self.conf = self.ibuf("conf", 256)
+
+    def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
+        with self.lock, torch.cuda.device(self.device):
+            self._ensure()
+            self._common_buffers()
+            specs = list(batch.values())
+            spec, epochs = specs[0][0], max(r[1] for r in specs)
+            extras_any = [r[2] for r in specs if r[2]]
+            opt = {
+                "kind": 0 if spec.get("name", "sgd") == "adam" else 1, "lr": float(spec.get("lr", 0.01)), "momentum": float(spec.get("momentum", 0.0)),
+                "weight_decay": float(spec.get("weight_decay", 0.0)), "nesterov": int(bool(spec.get("nesterov", False))), "mu": 0.0,
+            }
+            if opt["kind"] == 0:
+                raise ValueError("CNN engine implements SGD (the models' optimizer); Adam is not supported here")
+            if any("anchor" in e for e in extras_any):
+                anchor = self._extra_buffer("anchor")
+                opt["mu"] = float(next(e["mu"] for e in extras_any if "anchor" in e))
+                for slot, (_, _, extra) in batch.items():
+                    anchor[slot, : self.n_params].copy_(extra["anchor"] if "anchor" in extra else self.params[slot, : self.n_params])
+                opt["anchor"] = anchor
+            if any("c_global" in e for e in extras_any):
+                cg, cl = self._extra_buffer("c_global"), self._extra_buffer("c_local")
+                for slot, (_, _, extra) in batch.items():
+                    if "c_global" in extra:
+                        cg[slot, : self.n_params].copy_(extra["c_global"])
+                        cl[slot, : self.n_params].copy_(extra["c_local"])
+                    else:
+                        cg[slot].zero_()
+                        cl[slot].zero_()
+                opt["cg"], opt["cl"] = cg, cl
+            self._opt = opt
+            # inactive slots must not train: zero their sample count for this fit
+            n_active = torch.tensor([self.n_train[s] if s in batch else 0 for s in range(self.capacity)], dtype=torch.int32, device=self.device)
+            self.tab["n"].copy_(n_active)
+            self.mom.zero_()
+            self._shadow_sync()
+            self.stat.zero_()
+            steps = (max(n_active.tolist()) + self.B - 1) // self.B
+            key = ("fit", steps, tuple(sorted(opt)), opt.get("kind"))
+            for ep in range(epochs):
+                if self.perm_fn is not None:
+                    self.perm.copy_(self.perm_fn(ep))
+                else:
+                    keys = torch.rand(self.capacity, self.nmax, device=self.device)
+                    keys.masked_fill_(self._perm_mask, 2.0)
+                    self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
+                self._run_steps(key, steps, lambda: [self._train_step(t * self.B) for t in range(steps)], scalars=opt)
+            stat = self.stat.view(self.capacity, 4).cpu().numpy()
+            self.tab["n"].copy_(torch.tensor(self.n_train, dtype=torch.int32, device=self.device))
+        out = {}
+        for slot in batch:
+            n = max(1, self.n_train[slot] * epochs)
+            out[slot] = (int((self.n_train[slot] + self.B - 1) // self.B) * epochs, float(stat[slot, 0]) / n, float(stat[slot, 1]) / n)
+        return out
+
+    def _run_steps(self, key, steps: int, body, scalars: Optional[dict] = None) -> None:
+        """Run ``body`` (a whole epoch of steps). The first run of a key is eager (it allocates every
+        buffer); later runs capture it once into a HIP graph and replay it. The graph bakes the
+        optimizer scalars and step offsets in, so they are part of the key."""
+        if self.eager or steps == 0:
+            body()
+            return
+        gkey = key + tuple(sorted((k, v) for k, v in (scalars or {}).items() if isinstance(v, (int, float))))
+        g = self._graphs.get(gkey)
+        if g is None:
+            if gkey not in self._seen:
+                self._seen.add(gkey)
+                body()
+                return
+            cur = torch.cuda.current_stream(self.device)
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(cur)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                body()
+            cur.wait_stream(s)
+            self._graphs[gkey] = g
+        g.replay()
+
+    def _eval_all(self) -> None:
+        steps = (self.ntmax + self.B - 1) // self.B
+
+        def body():
+            for t in range(steps):
+                x0 = self._prep(False, t * self.B)
+                logits = self._forward_resnet(x0, False) if self.arch == "resnet18" else self._forward_lenet(x0, False)
+                self._xent(logits, False)
+
+        self._run_steps(("eval", steps), steps, body)
+
+    def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
+        with self.lock, torch.cuda.device(self.device):
+            self._ensure()
+            self._common_buffers()
+            self._shadow_sync()
+            self.stat.zero_()
+            self.conf.zero_()
+            self._eval_all()
+            stat = self.stat.view(self.capacity, 4).cpu().numpy()
+            conf = self.conf.view(self.capacity, 16, 16).cpu().numpy()
+        K = self.n_classes
+        return {slot: (float(stat[slot, 0]) / max(1, self.n_test[slot]), conf[slot, :K, :K].copy()) for slot in batch}
+
+    def expect(self, fit_slots: Optional[Set[int]] = None, eval_slots: Optional[Set[int]] = None) -> None:
+        self.fit_gang.expected = fit_slots
+        self.eval_gang.expected = eval_slots
+
+    def default_expected(self) -> Set[int]:
+        return set(self.handles)
+
+
+class CNNEngineHandle:
+    """A learner's slot in a :class:`CNNGroup` (same interface as ``MLPEngineHandle``)."""
+
+    @staticmethod
+    def supports(module: torch.nn.Module) -> bool:
+        if arch_of(module) is None:
+            return False
+        if _native.load() is None:
+            raise RuntimeError(f"MI355X CNN engine requested but native library unavailable: {_native.error()}")
+        return True
+
+    @classmethod
+    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None) -> "CNNEngineHandle":
+        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner)
+
+    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None) -> None:
+        self.addr, self.module, self.learner = addr, module, learner
+        self.group = CNNGroup.get(device, module, batch_size)
+        self._data_id = id(learner.data) if learner is not None else None
+        with self.group.lock:
+            self.slot = self.group.attach(self)
+            self.retarget(copy_in=True)
+
+    def retarget(self, copy_in: bool = False) -> None:
+        g = self.group
+        row = g.params[self.slot]
+        with torch.no_grad():
+            off = 0
+            for p in self.module.parameters():
+                view = row[off : off + p.numel()].view_as(p)
+                if copy_in:
+                    view.copy_(p.data.to(view.dtype))
+                p.data = view
+                off += p.numel()
+            for bn in g.bns:
+                mod = self._module_bn(bn.name)
+                o = g.n_params + g.bn_off[bn.name]
+                rm = row[o : o + bn.C]
+                rv = row[o + g.bn_total : o + g.bn_total + bn.C]
+                if copy_in:
+                    rm.copy_(mod.running_mean.float())
+                    rv.copy_(mod.running_var.float())
+                mod.running_mean = rm
+                mod.running_var = rv
+
+    def _module_bn(self, name: str):
+        import re
+
+        m = self.module
+        if name == "stem_bn":
+            return m.bn1
+        mt = re.fullmatch(r"b(\d+)(bn1|bn2|sbn)", name)
+        blk = m.layers[int(mt.group(1))]
+        return {"bn1": blk.bn1, "bn2": blk.bn2, "sbn": blk.shortcut[1] if len(blk.shortcut) else None}[mt.group(2)]
+
+    def close(self) -> None:
+        self.group.detach(self.slot)
+
+    def flat_params(self) -> torch.Tensor:
+        return self.group.params[self.slot, : self.group.n_params]
+
+    def device_split(self, train: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+        g = self.group
+        if self.learner is None or self.learner.data is None:
+            return torch.zeros(0, g.in_h, g.in_w, g.in_c, dtype=torch.uint8, device=g.device), torch.zeros(0, dtype=torch.int64, device=g.device)
+        x, y = self.learner.device_data(train)
+        if x.dtype != torch.uint8:
+            raise TypeError("CNN engine expects uint8 images")
+        x = x.reshape(x.shape[0], g.in_h, g.in_w, g.in_c).contiguous()
+        return x, y.to(torch.int64).contiguous()
+
+    def _sync_data(self, learner) -> None:
+        if self.learner is not learner or self._data_id != id(learner.data):
+            self.learner = learner
+            self._data_id = id(learner.data)
+            self.group.invalidate_data()
+
+    def fit(self, learner, spec: dict, extra: dict) -> Tuple[int, float]:
+        self._sync_data(learner)
+        steps, loss, _acc = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
+        learner.global_step += steps
+        return steps, loss
+
+    def evaluate(self, learner) -> Tuple[float, np.ndarray]:
+        self._sync_data(learner)
+        return self.group.eval_gang.submit(self.slot, (), self.group.default_expected())

@@ -1,0 +1,202 @@
+"""GPU numerics of the CNN engine: implicit-GEMM conv kernels vs torch fp32, and whole LeNet-5 /
+ResNet-18 train steps (grouped peers) vs torch autograd + torch.optim.SGD semantics."""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _cp(c):
+    return (c + 7) // 8 * 8
+
+
+def _nhwc_pad(x_nchw, cp):
+    n, c, h, w = x_nchw.shape
+    out = torch.zeros(n, h, w, cp, device=x_nchw.device, dtype=torch.bfloat16)
+    out[..., :c] = x_nchw.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return out
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2)])
+def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
+    from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
+
+    lib = _lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = _bf(torch.randn(n, cin, h, h, device=dev))
+    w = _bf(torch.randn(cout, cin, k, k, device=dev) * (1.0 / (cin * k * k) ** 0.5))
+    y_ref = F.conv2d(x, w, stride=stride, padding=pad)
+    ho = y_ref.shape[2]
+    cpi, cpo = _cp(cin), _cp(cout)
+    xn = _nhwc_pad(x, cpi).reshape(1, -1).contiguous()
+    wf = torch.zeros(cpo, k, k, cpi, device=dev, dtype=torch.bfloat16)
+    wf[:cout, :, :, :cin] = w.permute(0, 2, 3, 1).to(torch.bfloat16)
+    wt = torch.zeros(cpi, k, k, cpo, device=dev, dtype=torch.bfloat16)
+    wt[:cin, :, :, :cout] = w.permute(1, 2, 3, 0).to(torch.bfloat16)
+    y = torch.zeros(1, n * ho * ho * cpo, device=dev, dtype=torch.bfloat16)
+    stats = torch.zeros(1, lib.conv_gemm_stats_rows(n, ho, ho) * 2 * cpo, device=dev)
+    a = ConvGemmArgs()
+    a.src, a.src_ps, a.src_h, a.src_w, a.src_c = xn.data_ptr(), 0, h, h, cpi
+    a.out_h, a.out_w, a.R, a.S, a.stride, a.pad = ho, ho, k, k, stride, pad
+    a.wt, a.wt_ps, a.ncol, a.ncol_valid = wf.data_ptr(), 0, cpo, cout
+    a.out, a.out_ps, a.relu, a.stats, a.stats_ps, a.max_batch = y.data_ptr(), 0, 0, stats.data_ptr(), 0, n
+    assert lib.conv_gemm_launch(0, ctypes.byref(a), 1, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    y_nhwc = y.view(n, ho, ho, cpo)[..., :cout].float()
+    ref = y_ref.permute(0, 2, 3, 1)
+    torch.testing.assert_close(y_nhwc, ref, atol=2e-2, rtol=2e-2)
+    assert y.view(n, ho, ho, cpo)[..., cout:].abs().max().item() == 0 if cpo > cout else True
+    st = stats.view(-1, 2, cpo).sum(0)
+    torch.testing.assert_close(st[0, :cout], ref.sum((0, 1, 2)), atol=0.5, rtol=2e-2)
+
+    # dgrad
+    dy = _bf(torch.randn_like(y_ref))
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dy, stride=stride, padding=pad)
+    dyn = _nhwc_pad(dy, cpo).reshape(1, -1).contiguous()
+    dx = torch.zeros(1, n * h * h * cpi, device=dev, dtype=torch.bfloat16)
+    b = ConvGemmArgs()
+    b.src, b.src_h, b.src_w, b.src_c = dyn.data_ptr(), ho, ho, cpo
+    b.out_h, b.out_w, b.R, b.S, b.stride, b.pad = h, h, k, k, stride, pad
+    b.wt, b.ncol, b.ncol_valid = wt.data_ptr(), cpi, cin
+    b.out, b.max_batch = dx.data_ptr(), n
+    assert lib.conv_gemm_launch(1, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dx.view(n, h, h, cpi)[..., :cin].float(), dx_ref.permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
+
+    # wgrad
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
+    grad = torch.zeros(1, cout * cin * k * k, device=dev)
+    c = WgradArgs()
+    c.dy, c.x = dyn.data_ptr(), xn.data_ptr()
+    c.H, c.W, c.x_c, c.Ho, c.Wo, c.dy_c = h, h, cpi, ho, ho, cpo
+    c.R, c.S, c.stride, c.pad, c.cout, c.cin = k, k, stride, pad, cout, cin
+    c.grad, c.k_per_split, c.max_batch = grad.data_ptr(), 128, n
+    M = n * ho * ho
+    assert lib.conv_wgrad_launch(ctypes.byref(c), 1, (M + 127) // 128, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    g = grad.view(cout, cin, k, k)
+    err = (g - dw_ref).norm() / dw_ref.norm()
+    assert err < 2e-2, float(err)
+
+
+def _make_learners(model_fn, n_peers, n_train, n_test, batch, lr, momentum=0.0, wd=0.0):
+    from myfyp_amd.learning.dataset.synthetic import synthetic_cifar10
+    from myfyp_amd.learning.frameworks.torch import TorchModel
+    from myfyp_amd.learning.frameworks.torch.torch_learner import TorchLearner
+    from myfyp_amd.parallel.cnn_engine import CNNGroup
+    from myfyp_amd.settings import Settings
+
+    CNNGroup.reset_all()
+    Settings.USE_FUSED_KERNELS = True
+    data = synthetic_cifar10(n_train * n_peers, n_test * n_peers, seed=3)
+    from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
+
+    parts = data.generate_partitions(n_peers, RandomIIDPartitionStrategy)
+    learners, refs = [], []
+    for i in range(n_peers):
+        m = model_fn(i)
+        m.optimizer_spec = lambda lr=lr, momentum=momentum, wd=wd: {"name": "sgd", "lr": lr, "momentum": momentum, "weight_decay": wd}
+        ref = model_fn(i).cuda()
+        lr_ = TorchLearner(TorchModel(m), parts[i], f"cnn-{i}", batch_size=batch, device="cuda")
+        assert lr_._engine is not None, "CNN engine not attached"
+        lr_.set_epochs(1)
+        learners.append(lr_)
+        refs.append(ref)
+    return learners, refs, parts
+
+
+def _torch_step(ref, x_u8, y, lr, momentum, wd):
+    ref.train()
+    opt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=momentum, weight_decay=wd)
+    opt.zero_grad()
+    loss = F.cross_entropy(ref(x_u8), y)
+    loss.backward()
+    opt.step()
+    return float(loss)
+
+
+def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
+    import threading
+
+    learners, refs, parts = _make_learners(model_fn, n_peers, batch, 64, batch, lr, momentum, wd)
+    g = learners[0]._engine.group
+    g.perm_fn = lambda ep: torch.arange(g.nmax, dtype=torch.int32, device="cuda").unsqueeze(0).repeat(g.capacity, 1)
+    before = [[p.detach().clone() for p in r.parameters()] for r in refs]
+    out = [None] * n_peers
+    ths = [threading.Thread(target=lambda i=i: out.__setitem__(i, learners[i].fit())) for i in range(n_peers)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    for i, (lr_, ref) in enumerate(zip(learners, refs)):
+        x, y = lr_.device_data(True)
+        _torch_step(ref, x[:batch], y[:batch], lr, momentum, wd)
+        eng = dict(lr_.model.get_model().named_parameters())
+        for (name, p_ref), p0 in zip(ref.named_parameters(), before[i]):
+            d_ref = (p_ref.detach() - p0).flatten()
+            d_eng = (eng[name].detach() - p0).flatten()
+            if d_ref.norm() < 1e-8:
+                continue
+            cos = F.cosine_similarity(d_ref, d_eng, dim=0)
+            rel = (d_ref - d_eng).norm() / d_ref.norm()
+            assert cos > 0.97 and rel < 0.25, (name, float(cos), float(rel))
+        # BN running statistics follow torch
+        for (name, b_ref) in ref.named_buffers():
+            if "running" in name:
+                b_eng = dict(lr_.model.get_model().named_buffers())[name]
+                torch.testing.assert_close(b_eng.float(), b_ref.float(), atol=5e-2, rtol=5e-2)
+    return learners, refs
+
+
+def test_lenet_train_step_matches_torch():
+    from myfyp_amd.models import LeNet5
+
+    _run_one_step(lambda i: LeNet5(seed=10 + i), n_peers=2, batch=32, lr=0.05)
+
+
+def test_resnet_train_step_matches_torch():
+    from myfyp_amd.models import ResNet18
+
+    _run_one_step(lambda i: ResNet18(seed=20 + i), n_peers=2, batch=16, lr=0.05, momentum=0.9, wd=5e-4)
+
+
+def test_cnn_eval_matches_torch():
+    from myfyp_amd.models import ResNet18
+
+    learners, refs, parts = _make_learners(lambda i: ResNet18(seed=30 + i), 2, 32, 48, 16, 0.05)
+    for lr_, ref in zip(learners, refs):
+        res = lr_.evaluate()
+        ref.load_state_dict(lr_.model.get_model().state_dict())
+        ref.eval()
+        x, y = lr_.device_data(False)
+        with torch.no_grad():
+            out = ref(x)
+        loss = float(F.cross_entropy(out, y))
+        acc = float((out.argmax(1) == y).float().mean())
+        assert abs(res["test_loss"] - loss) < 0.05 * max(1.0, loss), (res, loss)
+        assert abs(res["test_metric"] - acc) <= 2.0 / len(y) + 0.05
+
+
+def test_cnn_graph_replay_learns():
+    """Several fits (eager first, then captured + replayed HIP graph) keep learning."""
+    import threading
+
+    from myfyp_amd.models import LeNet5
+
+    learners, _, _ = _make_learners(lambda i: LeNet5(seed=40 + i), 2, 512, 256, 64, 0.05, momentum=0.9)
+    accs = []
+    for _ in range(4):
+        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        accs.append(learners[0].evaluate()["test_metric"])
+    assert len(learners[0]._engine.group._graphs) >= 1
+    assert accs[-1] > accs[0] or accs[-1] > 0.5, accs
