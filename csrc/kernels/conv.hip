@@ -24,6 +24,7 @@
 #define CG_BK 64
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -279,15 +280,11 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   auto frag_t = [&](const bf16* base, int ld, int col0, int k0) -> bf16x8 {
     const bf16* p0 = base + (k0 + 8 * g + q) * ld + col0 + 4 * p;
     const bf16* p1 = p0 + 4 * ld;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
-    bf16x8 r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      r[j] = __builtin_bit_cast(bf16, lo[j]);
-      r[4 + j] = __builtin_bit_cast(bf16, hi[j]);
-    }
-    return r;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+    // whole-vector bit cast (an element-wise short->bf16 cast miscompiles into lane-duplicating perms)
+    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, both);
   };
 
   f32x4 acc[FM][FN];

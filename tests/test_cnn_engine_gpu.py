@@ -115,20 +115,31 @@ def _make_learners(model_fn, n_peers, n_train, n_test, batch, lr, momentum=0.0, 
     return learners, refs, parts
 
 
-def _torch_step(ref, x_u8, y, lr, momentum, wd):
+def _torch_step(ref, x_u8, y, lr, momentum, wd, bf16=False):
     ref.train()
     opt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=momentum, weight_decay=wd)
     opt.zero_grad()
-    loss = F.cross_entropy(ref(x_u8), y)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+        loss = F.cross_entropy(ref(x_u8).float(), y)
     loss.backward()
     opt.step()
-    return float(loss)
+    return float(loss.detach())
 
 
-def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
+def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0, noise_floor=False):
+    """One grouped engine step vs torch fp32. With ``noise_floor`` the tolerance per parameter is
+    set by how far torch's own bf16-autocast step is from fp32 (deep nets: the bf16 floor is large)."""
     import threading
 
     learners, refs, parts = _make_learners(model_fn, n_peers, batch, 64, batch, lr, momentum, wd)
+    floors = [None] * n_peers
+    if noise_floor:
+        for i in range(n_peers):
+            r16 = model_fn(i).cuda()
+            p0 = [p.detach().clone() for p in r16.parameters()]
+            x, y = learners[i].device_data(True)
+            _torch_step(r16, x[:batch], y[:batch], lr, momentum, wd, bf16=True)
+            floors[i] = {n: (p.detach() - q).flatten() for (n, p), q in zip(r16.named_parameters(), p0)}
     g = learners[0]._engine.group
     g.perm_fn = lambda ep: torch.arange(g.nmax, dtype=torch.int32, device="cuda").unsqueeze(0).repeat(g.capacity, 1)
     before = [[p.detach().clone() for p in r.parameters()] for r in refs]
@@ -147,7 +158,11 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
                 continue
             cos = F.cosine_similarity(d_ref, d_eng, dim=0)
             rel = (d_ref - d_eng).norm() / d_ref.norm()
-            assert cos > 0.97 and rel < 0.25, (name, float(cos), float(rel))
+            if floors[i] is not None:
+                rel16 = float((d_ref - floors[i][name]).norm() / d_ref.norm())
+                assert rel < max(0.05, 1.5 * rel16), (name, float(rel), rel16)
+            else:
+                assert cos > 0.97 and rel < 0.25, (name, float(cos), float(rel))
         # BN running statistics follow torch
         for (name, b_ref) in ref.named_buffers():
             if "running" in name:
@@ -165,7 +180,7 @@ def test_lenet_train_step_matches_torch():
 def test_resnet_train_step_matches_torch():
     from myfyp_amd.models import ResNet18
 
-    _run_one_step(lambda i: ResNet18(seed=20 + i), n_peers=2, batch=16, lr=0.05, momentum=0.9, wd=5e-4)
+    _run_one_step(lambda i: ResNet18(seed=20 + i), n_peers=2, batch=16, lr=0.05, momentum=0.9, wd=5e-4, noise_floor=True)
 
 
 def test_cnn_eval_matches_torch():
@@ -185,18 +200,27 @@ def test_cnn_eval_matches_torch():
         assert abs(res["test_metric"] - acc) <= 2.0 / len(y) + 0.05
 
 
-def test_cnn_graph_replay_learns():
-    """Several fits (eager first, then captured + replayed HIP graph) keep learning."""
+def test_cnn_graph_replay_matches_eager():
+    """Fits replayed from the captured HIP graph reproduce the eager launch sequence and keep
+    lowering the training loss."""
     import threading
 
     from myfyp_amd.models import LeNet5
 
-    learners, _, _ = _make_learners(lambda i: LeNet5(seed=40 + i), 2, 512, 256, 64, 0.05, momentum=0.9)
-    accs = []
-    for _ in range(4):
-        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
-        [t.start() for t in ths]
-        [t.join() for t in ths]
-        accs.append(learners[0].evaluate()["test_metric"])
-    assert len(learners[0]._engine.group._graphs) >= 1
-    assert accs[-1] > accs[0] or accs[-1] > 0.5, accs
+    runs = []
+    for eager in (True, False):
+        learners, _, _ = _make_learners(lambda i: LeNet5(seed=40 + i), 2, 512, 256, 64, 0.05, momentum=0.9)
+        g = learners[0]._engine.group
+        g.eager = eager
+        losses = []
+        for _ in range(4):
+            ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+            [t.start() for t in ths]
+            [t.join() for t in ths]
+            losses.append(float(g.stat.view(g.capacity, 4)[0, 0]))
+        runs.append((losses, learners[0].flat_params().detach().clone(), len(g._graphs)))
+    (l_e, p_e, n_e), (l_g, p_g, n_g) = runs
+    assert n_e == 0 and n_g >= 1
+    assert l_g[-1] < l_g[0] and l_e[-1] < l_e[0]
+    np.testing.assert_allclose(l_e, l_g, rtol=1e-3)
+    torch.testing.assert_close(p_e, p_g, atol=1e-4, rtol=1e-3)
