@@ -1,0 +1,182 @@
+"""CNN federated benchmarks (BASELINE configs 3-5) on the grouped HIP CNN engine.
+
+    python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor      # config 3 (ring neighbour averaging)
+    python benchmarks/bench_cnn.py --model resnet18                          # config 4 (FedAvg + fused SGD)
+    python benchmarks/bench_cnn.py --model resnet18 --aggregator fedprox --dirichlet 0.5 --dropout  # config 5
+    python benchmarks/bench_cnn.py --model resnet18 --torch-step             # + torch/MIOpen step A/B
+
+Each timed round is a full federated round through the Node API and the collective workflow
+(vote → evaluate → one local epoch → aggregate). One JSON line on rank 0: rounds/s, train images/s,
+final accuracy. Data: synthetic CIFAR-10-shaped uint8 (no network), random-init weights.
+``--torch-step`` additionally times the same local step in PyTorch (bf16 autocast, channels-last,
+MIOpen convolutions, torch.optim.SGD) for one peer and reports both per-peer step times.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", choices=["lenet5", "resnet18"], default="resnet18")
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--batch-size", type=int, default=0, help="0 = 128 for resnet18, 64 for lenet5")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--aggregator", choices=["fedavg", "neighbor", "fedprox"], default="fedavg")
+    ap.add_argument("--dirichlet", type=float, default=0.0, help="non-IID Dirichlet alpha (0 = IID)")
+    ap.add_argument("--dropout", action="store_true", help="kill one peer at round 1 (fault tolerance)")
+    ap.add_argument("--n-train", type=int, default=50000)
+    ap.add_argument("--n-test", type=int, default=10000)
+    ap.add_argument("--torch-step", action="store_true")
+    ap.add_argument("--eager", action="store_true")
+    return ap.parse_args()
+
+
+def torch_step_ms(model_name: str, batch: int, iters: int = 20) -> float:
+    import torch
+    import torch.nn.functional as F
+
+    from myfyp_amd.models import LeNet5, ResNet18
+
+    m = (ResNet18 if model_name == "resnet18" else LeNet5)(seed=0).cuda().to(memory_format=torch.channels_last)
+    spec = m.optimizer_spec()
+    opt = torch.optim.SGD(m.parameters(), lr=spec["lr"], momentum=spec.get("momentum", 0.0), weight_decay=spec.get("weight_decay", 0.0))
+    x = torch.randint(0, 255, (batch, 32, 32, 3), dtype=torch.uint8, device="cuda")
+    y = torch.randint(0, 10, (batch,), device="cuda")
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x).float(), y)
+        loss.backward()
+        opt.step()
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step()
+    torch.cuda.synchronize()
+    return 1000 * (time.perf_counter() - t0) / iters
+
+
+def main() -> None:
+    args = parse()
+    import numpy as np
+    import torch
+
+    from myfyp_amd import fault_injection
+    from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
+    from myfyp_amd.learning.aggregators import FedAvg, FedProx, NeighborAvg
+    from myfyp_amd.learning.dataset.partition_strategies import DirichletPartitionStrategy, RandomIIDPartitionStrategy
+    from myfyp_amd.learning.dataset.synthetic import synthetic_cifar10
+    from myfyp_amd.learning.frameworks.torch import TorchModel
+    from myfyp_amd.management.logger import logger
+    from myfyp_amd.models import LeNet5, ResNet18
+    from myfyp_amd.node import Node
+    from myfyp_amd.parallel.federation import Federation
+    from myfyp_amd.settings import Settings
+    from myfyp_amd.utils.seed import set_seed
+    from myfyp_amd.utils.utils import wait_to_finish
+
+    set_seed(1234)
+    B = args.batch_size or (128 if args.model == "resnet18" else 64)
+    logger.set_level("WARNING")
+    Settings.LOG_LEVEL = "WARNING"
+    Settings.HEARTBEAT_TIMEOUT = 3600
+    Settings.TRAIN_SET_SIZE = args.peers
+    Settings.VOTE_TIMEOUT = Settings.AGGREGATION_TIMEOUT = 3600
+    Settings.BATCH_SIZE = B
+    Settings.GANG_WINDOW = 30.0
+    fed = Federation.init()
+    world, rank = fed.world, fed.rank
+    ppr = args.peers // world
+    data = synthetic_cifar10(args.n_train, args.n_test, seed=7)
+    if args.dirichlet > 0:
+        parts = data.generate_partitions(args.peers, DirichletPartitionStrategy, alpha=args.dirichlet)
+    else:
+        parts = data.generate_partitions(args.peers, RandomIIDPartitionStrategy)
+    mk = {"fedavg": FedAvg, "fedprox": lambda: FedProx(proximal_mu=0.01), "neighbor": lambda: NeighborAvg("ring")}[args.aggregator]
+    model_cls = ResNet18 if args.model == "resnet18" else LeNet5
+    gids = [rank * ppr + j for j in range(ppr)]
+    nodes = [Node(TorchModel(model_cls(seed=100 + g)), parts[g], address=f"cnn-{g}", protocol=CollectiveCommunicationProtocol, aggregator=mk(),
+                  learner_kwargs={"batch_size": B}) for g in gids]
+    for n in nodes:
+        n.start()
+    fed.finalize()
+    engines = [getattr(n.learner, "_engine", None) for n in nodes]
+    fused = all(e is not None for e in engines)
+    if args.eager and fused:
+        engines[0].group.eager = True
+    if args.dropout and rank == world - 1:
+        fault_injection.kill_at(nodes[-1], "TrainStage", round=min(1, args.warmup + args.rounds - 1))
+    total = args.warmup + args.rounds
+    marks, round_end = {}, {}
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+
+    def hook(r, f):
+        if r == args.warmup - 1:
+            f.barrier()
+            sync()
+            marks["t0"] = time.perf_counter()
+        round_end[r] = time.perf_counter()
+        if r == total - 1:
+            sync()
+            f.barrier()
+            marks["t1"] = time.perf_counter()
+
+    fed.round_hooks.append(hook)
+    t_start = time.perf_counter()
+    if rank == 0:
+        nodes[0].set_start_learning(rounds=total, epochs=1)
+    wait_to_finish(nodes, timeout=7200)
+    el = marks["t1"] - marks["t0"]
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([el], dtype=torch.float64, device=fed.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    logs = logger.get_global_logs().get("experiment", {})
+    accs = [logs[n.addr]["test_metric"][-1][1] for n in nodes if logs.get(n.addr, {}).get("test_metric")]
+    tm = logger.get_timings().get(nodes[0].addr, {})
+    brk = {k: round(1000 * float(np.median(v[args.warmup:] or v)), 2) for k, v in tm.items()}
+    print(f"[bench_cnn] rank {rank} median ms per call: {json.dumps(brk)}", file=sys.stderr, flush=True)
+    step_ms_engine = None
+    if fused and "fit" in tm:
+        steps = (len(parts[gids[0]].column("label")) + B - 1) // B
+        step_ms_engine = round(1000 * float(np.median(tm["fit"][args.warmup:] or tm["fit"])) / steps, 3)
+    for n in nodes:
+        n.stop()
+    out = {
+        "metric": f"rounds/sec, {args.model} {args.aggregator} {args.peers} peers",
+        "value": round(args.rounds / el, 4), "unit": "rounds/s", "n_gpus": world, "rounds": args.rounds, "warmup": args.warmup,
+        "ms_per_round": round(1000 * el / args.rounds, 2),
+        "train_images_per_s": round(args.n_train * args.rounds / el, 1),
+        "engine": ("fused-hip" + ("-eager" if args.eager else "-hipgraph")) if fused else "autograd",
+        "dtype": "bf16" if fused else "fp32", "data": "synthetic CIFAR-10-shaped uint8", "local_batch": B,
+        "partition": f"dirichlet({args.dirichlet})" if args.dirichlet else "iid", "dropout": args.dropout,
+        "final_test_acc_mean": round(float(np.mean(accs)), 4) if accs else None,
+        "engine_ms_per_grouped_step": step_ms_engine,
+    }
+    if args.torch_step and rank == 0 and torch.cuda.is_available():
+        t_ms = torch_step_ms(args.model, B)
+        out["torch_bf16_ms_per_peer_step"] = round(t_ms, 3)
+        out["torch_ms_for_all_peers_step"] = round(t_ms * ppr, 3)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    fed.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -76,10 +76,19 @@ class TorchLearner(Learner):
         self._attach_module(model)
 
     def close(self) -> None:
-        """Release the device slot (called by ``Node.stop``)."""
+        """Release the grouped-engine slot (called by ``Node.stop``); the learner keeps working on
+        a private copy of its parameters."""
         if self._engine is not None:
-            self._engine.close()
-            self._engine = None
+            eng, self._engine = self._engine, None
+            module = self.model.get_model()
+            with torch.no_grad():
+                for p in module.parameters():
+                    p.data = p.data.clone()
+                for name, b in list(module.named_buffers()):
+                    if b.is_floating_point():
+                        b.data = b.data.clone()
+            eng.close()
+            self._flat = FlatParams(module)
 
     # ------------------------------------------------------------------ model plumbing
     def _attach_module(self, model: TorchModel) -> None:

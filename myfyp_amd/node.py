@@ -135,6 +135,10 @@ class Node:
             self.aggregator.clear()
         with contextlib.suppress(Exception):
             logger.unregister_node(self.addr)
+        close = getattr(self.learner, "close", None)
+        if close is not None:
+            with contextlib.suppress(Exception):
+                close()  # frees a grouped-engine slot: co-located peers stop waiting for this one
 
     # ------------------------------------------------------------------ learning setters/getters
     def set_learner(self, learner: Learner) -> None:

@@ -189,8 +189,14 @@ class CNNGroup:
         self._bound_version = -1
         self._describe(template)
         self._alloc(capacity)
-        self.fit_gang = _Gang(self._run_fit_batch)
-        self.eval_gang = _Gang(self._run_eval_batch)
+    def detach(self, slot: int) -> None:
+        with self.lock:
+            self.handles.pop(slot, None)
+            self._data_version += 1
+        self.fit_gang.poke()
+        self.eval_gang.poke()
+        self.fit_gang.poke()
+        self.eval_gang.poke()
 
     # ------------------------------------------------------------------ description
     def _describe(self, m: torch.nn.Module) -> None:
@@ -352,6 +358,8 @@ class CNNGroup:
         with self.lock:
             self.handles.pop(slot, None)
             self._data_version += 1
+        self.fit_gang.poke()
+        self.eval_gang.poke()
 
     def invalidate_data(self) -> None:
         with self.lock:

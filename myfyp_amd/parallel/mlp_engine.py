@@ -49,8 +49,9 @@ def mlp_dims(module: torch.nn.Module) -> Optional[Tuple[int, int, int, int]]:
 class _Gang:
     """Collects requests from co-located peers' threads and runs them as one batch."""
 
-    def __init__(self, run_batch) -> None:
+    def __init__(self, run_batch, live_fn=None) -> None:
         self._run_batch = run_batch
+        self._live_fn = live_fn  # slots still attached (a stopped peer is never waited for)
         self._cv = threading.Condition()
         self._pending: Dict[int, object] = {}
         self._results: Dict[int, object] = {}
@@ -68,6 +69,8 @@ class _Gang:
             self._cv.notify_all()
             while slot not in self._results and slot not in self._errors:
                 expected = self.expected if self.expected is not None else default_expected
+                if self._live_fn is not None:
+                    expected = expected & self._live_fn()
                 complete = expected.issubset(self._pending.keys())
                 waited = time.time() - self._t_first
                 if not self._running and self._pending and (complete or waited >= window):
@@ -92,6 +95,10 @@ class _Gang:
             if slot in self._errors:
                 raise self._errors.pop(slot)
             return self._results.pop(slot)
+
+    def poke(self) -> None:
+        with self._cv:
+            self._cv.notify_all()
 
 
 class MLPGroup:
@@ -135,8 +142,8 @@ class MLPGroup:
         self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
         self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
         self._alloc(capacity)
-        self.fit_gang = _Gang(self._run_fit_batch)
-        self.eval_gang = _Gang(self._run_eval_batch)
+        self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
+        self.eval_gang = _Gang(self._run_eval_batch, lambda: set(self.handles))
 
     # ------------------------------------------------------------------ buffers / slots
     def _alloc(self, capacity: int) -> None:
@@ -178,6 +185,8 @@ class MLPGroup:
         with self.lock:
             self.handles.pop(slot, None)
             self._data_version += 1
+        self.fit_gang.poke()
+        self.eval_gang.poke()
 
     def invalidate_data(self) -> None:
         with self.lock:
