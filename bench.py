@@ -122,6 +122,15 @@ def main() -> None:
             marks["t1"] = time.perf_counter()
 
     fed.round_hooks.append(hook)
+    # evaluations resolve asynchronously: record when each round's accuracy actually landed on the host
+    landed: dict = {}
+    local_addrs = {n.addr for n in nodes}
+
+    def on_metric(addr, exp_name, rnd, metric, value, step):
+        if metric == "test_metric" and step is None and addr in local_addrs:
+            landed.setdefault(rnd, []).append((value, time.perf_counter()))
+
+    logger.add_metric_listener(on_metric)
     if args.warmup == 0:
         marks["t0"] = None
     t_start = time.perf_counter()
@@ -153,8 +162,9 @@ def main() -> None:
     mean_acc = {r: float(np.mean(v)) for r, v in sorted(acc_by_round.items())}
     t_target, r_target = None, None
     for r, a in mean_acc.items():
-        if a >= args.target_acc and r >= 1 and (r - 1) in round_end:
-            t_target, r_target = round_end[r - 1] - t_start, r
+        if a >= args.target_acc and r >= 1 and r in landed:
+            # time at which the last local peer's evaluation of the round-(r-1) model reached the host
+            t_target, r_target = max(t for _, t in landed[r]) - t_start, r
             break
     final_acc = mean_acc[max(mean_acc)] if mean_acc else None
     # per-stage wall-time breakdown of the first local peer (stderr, diagnostics only)

@@ -30,6 +30,31 @@ static thread_local std::string g_last_error;
 
 namespace {
 
+// Control words / active mask travel as kernel arguments (captured at launch), so the host never
+// enqueues a copy from pageable memory: nothing on the round's path blocks the host on the GPU.
+#define MLP_CTL_MAX 64
+struct CtlUpload {
+  int4 ctl[MLP_CTL_MAX];
+  int active[MLP_CTL_MAX];
+  int P;
+  int with_active;
+};
+__global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active) {
+  const int p = threadIdx.x;
+  if (p < u.P) {
+    ctl[p] = u.ctl[p];
+    if (u.with_active) active[p] = u.active[p];
+  }
+}
+
+#define MLP_RING 16
+struct ResultSlot {
+  float* loss = nullptr;
+  int* correct = nullptr;
+  int* conf = nullptr;
+  hipEvent_t ev = nullptr;
+};
+
 struct MLPEngine {
   MLPArgs a{};
   int max_steps = 0;
@@ -49,12 +74,42 @@ struct MLPEngine {
   std::vector<void*> owned;
   std::mutex mu;
   int max_test_rows = 0;
+  ResultSlot ring[MLP_RING];  // pinned host result buffers + completion events
 
   ~MLPEngine() {
     if (exec) hipGraphExecDestroy(exec);
     if (graph) hipGraphDestroy(graph);
     if (cap_stream) hipStreamDestroy(cap_stream);
     for (void* p : owned) hipFree(p);
+    for (auto& r : ring) {
+      if (r.ev) hipEventDestroy(r.ev);
+      if (r.loss) hipHostFree(r.loss);
+      if (r.correct) hipHostFree(r.correct);
+      if (r.conf) hipHostFree(r.conf);
+    }
+  }
+
+  int alloc_ring() {
+    for (auto& r : ring) {
+      CHECK_HIP(hipHostMalloc((void**)&r.loss, sizeof(float) * a.P, hipHostMallocDefault));
+      CHECK_HIP(hipHostMalloc((void**)&r.correct, sizeof(int) * a.P, hipHostMallocDefault));
+      CHECK_HIP(hipHostMalloc((void**)&r.conf, sizeof(int) * a.P * 256, hipHostMallocDefault));
+      CHECK_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+    }
+    return 0;
+  }
+
+  int upload(hipStream_t s, const int* active_host) {
+    CtlUpload u;
+    u.P = a.P;
+    u.with_active = active_host != nullptr;
+    for (int p = 0; p < a.P; ++p) {
+      u.ctl[p] = ctl_host[p];
+      u.active[p] = active_host ? active_host[p] : 0;
+    }
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(MLP_CTL_MAX), 0, s, u, d_ctl, d_active);
+    CHECK_HIP(hipGetLastError());
+    return 0;
   }
 
   void invalidate() {
@@ -145,7 +200,7 @@ int myfyp_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_
 int mlp_shape_ok(int D0, int D1, int D2, int D3) { return mlp_shape_supported(D0, D1, D2, D3) ? 1 : 0; }
 
 void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
-  if (!mlp_shape_supported(D0, D1, D2, D3) || P < 1 || B < 1 || (B + 31) / 32 * 32 > MLP_MAX_BPAD) {
+  if (!mlp_shape_supported(D0, D1, D2, D3) || P < 1 || P > MLP_CTL_MAX || B < 1 || (B + 31) / 32 * 32 > MLP_MAX_BPAD) {
     g_last_error = "unsupported MLP shape";
     return nullptr;
   }
@@ -181,6 +236,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
   rc |= e->alloc(&p, (size_t)P * 4); e->d_loss = (float*)p; a.loss_acc = e->d_loss;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_correct = (int*)p; a.correct_acc = e->d_correct;
   rc |= e->alloc(&p, (size_t)P * 256 * 4); e->d_conf = (int*)p; a.conf = e->d_conf;
+  rc |= e->alloc_ring();
   if (rc) {
     delete e;
     return nullptr;
@@ -249,12 +305,13 @@ int mlp_engine_set_extras(void* h, const float* anchor, const float* cg, const f
   return 0;
 }
 
-// Copy the active mask, zero the accumulators and refresh the bf16 shadows (stream-ordered).
+// Upload the active mask, zero the accumulators and refresh the bf16 shadows (stream-ordered,
+// never blocks the host).
 int mlp_engine_begin(void* h, const int* active_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
-  CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
   mlp_launch_sync_shadow(e->a, s);
@@ -272,7 +329,7 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
     if (e->capture(e->max_steps)) return 1;
   }
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
-  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
+  if (e->upload(s, nullptr)) return 1;
   CHECK_HIP(hipGraphLaunch(e->exec, s));
   return 0;
 }
@@ -282,39 +339,65 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
-  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
+  if (e->upload(s, nullptr)) return 1;
   for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
 
-int mlp_engine_read_stats(void* h, float* loss_host, int* correct_host, void* stream) {
+// ---- asynchronous results: enqueue D2H into pinned ring slot `slot`, fetch later
+int mlp_engine_stats_async(void* h, int slot, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
-  CHECK_HIP(hipMemcpyAsync(loss_host, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(correct_host, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  ResultSlot& r = e->ring[slot % MLP_RING];
+  CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
 
-// Forward the whole test split of every active peer: loss sum, correct count, confusion [P][16][16].
-int mlp_engine_eval(void* h, const int* active_host, float* loss_host, int* correct_host, int* conf_host, void* stream) {
+// Forward the whole test split of every active peer (loss sum, correct, confusion [P][16][16]) into slot.
+int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
+  ResultSlot& r = e->ring[slot % MLP_RING];
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
-  CHECK_HIP(hipMemcpyAsync(e->d_ctl, e->ctl_host.data(), sizeof(int4) * e->a.P, hipMemcpyHostToDevice, s));
-  CHECK_HIP(hipMemcpyAsync(e->d_active, active_host, sizeof(int) * e->a.P, hipMemcpyHostToDevice, s));
+  if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_conf, 0, sizeof(int) * e->a.P * 256, s));
   mlp_launch_sync_shadow(e->a, s);
   for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(e->a, base, s);
   CHECK_HIP(hipGetLastError());
-  CHECK_HIP(hipMemcpyAsync(loss_host, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(correct_host, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(conf_host, e->d_conf, sizeof(int) * e->a.P * 256, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipMemcpyAsync(r.conf, e->d_conf, sizeof(int) * e->a.P * 256, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
+}
+
+// Wait for slot's event, copy its pinned results out (conf may be null).
+int mlp_engine_fetch(void* h, int slot, float* loss_host, int* correct_host, int* conf_host) {
+  auto* e = (MLPEngine*)h;
+  ResultSlot& r = e->ring[slot % MLP_RING];
+  CHECK_HIP(hipEventSynchronize(r.ev));
+  memcpy(loss_host, r.loss, sizeof(float) * e->a.P);
+  memcpy(correct_host, r.correct, sizeof(int) * e->a.P);
+  if (conf_host) memcpy(conf_host, r.conf, sizeof(int) * e->a.P * 256);
+  return 0;
+}
+
+int mlp_engine_ring_size() { return MLP_RING; }
+
+// synchronous conveniences (tests / tools)
+int mlp_engine_read_stats(void* h, float* loss_host, int* correct_host, void* stream) {
+  if (mlp_engine_stats_async(h, MLP_RING - 1, stream)) return 1;
+  return mlp_engine_fetch(h, MLP_RING - 1, loss_host, correct_host, nullptr);
+}
+
+int mlp_engine_eval(void* h, const int* active_host, float* loss_host, int* correct_host, int* conf_host, void* stream) {
+  if (mlp_engine_eval_async(h, active_host, MLP_RING - 1, stream)) return 1;
+  return mlp_engine_fetch(h, MLP_RING - 1, loss_host, correct_host, conf_host);
 }
 
 }  // extern "C"

@@ -36,6 +36,7 @@ from myfyp_amd.learning.frameworks.p2pfl_model import P2PFLModel
 from myfyp_amd.learning.frameworks.torch.torch_model import TorchModel
 from myfyp_amd.management.logger import logger
 from myfyp_amd.parallel.flat_params import FlatParams
+from myfyp_amd.parallel.pending import Pending, resolve
 from myfyp_amd.settings import Settings, resolve_device
 
 
@@ -196,7 +197,11 @@ class TorchLearner(Learner):
             steps, mean_loss = self._fit_autograd(spec)
         logger.log_timing(self._self_addr, "fit", time.time() - t0)
         if mean_loss is not None:
-            logger.log_metric(self._self_addr, "train_loss", float(mean_loss), step=self.global_step)
+            snap, addr, gs = logger.experiment_snapshot(self._self_addr), self._self_addr, self.global_step
+            if isinstance(mean_loss, Pending):  # fused engine: logged when the device result lands
+                mean_loss.add_done_callback(lambda v: logger.log_metric_at(addr, snap, "train_loss", float(v), step=gs))
+            else:
+                logger.log_metric_at(addr, snap, "train_loss", float(mean_loss), step=gs)
         for cb in self.callbacks:
             if hasattr(cb, "on_train_end"):
                 cb.on_train_end(self, steps, float(spec.get("lr", 1e-3)))
@@ -252,7 +257,7 @@ class TorchLearner(Learner):
     def evaluate_raw(self) -> Tuple[float, np.ndarray]:
         """(mean test NLL, confusion matrix [C, C])."""
         if self._engine is not None:
-            return self._engine.evaluate(self)
+            return resolve(self._engine.evaluate(self))
         module = self.model.get_model()
         module.eval()
         x_all, y_all = self.device_data(train=False)
@@ -273,13 +278,10 @@ class TorchLearner(Learner):
         c = int(round(conf.numel() ** 0.5))
         return float(loss_sum) / x_all.shape[0], conf.view(c, c).cpu().numpy()
 
-    def evaluate(self) -> Dict[str, float]:
-        t0 = time.time()
-        if self.data is None or self.data.get_num_samples(train=False) == 0:
-            return {}
-        loss, conf = self.evaluate_raw()
+    @staticmethod
+    def _results(loss: float, conf: np.ndarray) -> Dict[str, float]:
         m = classification_metrics(conf)
-        results = {
+        return {
             "test_loss": float(loss),
             "test_metric": m["accuracy"],
             "test_accuracy": m["accuracy"],
@@ -287,10 +289,31 @@ class TorchLearner(Learner):
             "test_precision": m["precision"],
             "test_recall": m["recall"],
         }
-        for k, v in results.items():
-            logger.log_metric(self._self_addr, k, v)
+
+    def evaluate_async(self) -> Pending:
+        """Enqueue the evaluation and return at once; the metrics are logged against the round in
+        which it was issued when the device result lands (the round's hot path never waits for the
+        GPU). ``evaluate()`` is this plus a wait."""
+        t0 = time.time()
+        if self.data is None or self.data.get_num_samples(train=False) == 0:
+            return Pending.completed({})
+        snap, addr = logger.experiment_snapshot(self._self_addr), self._self_addr
+        raw = self._engine.evaluate(self) if self._engine is not None else self.evaluate_raw()
+        if not isinstance(raw, Pending):
+            raw = Pending.completed(raw)
+
+        def done(lc) -> Dict[str, float]:
+            results = self._results(*lc)
+            for k, v in results.items():
+                logger.log_metric_at(addr, snap, k, v)
+            return results
+
+        out = raw.map(done)
         logger.log_timing(self._self_addr, "evaluate", time.time() - t0)
-        return results
+        return out
+
+    def evaluate(self) -> Dict[str, float]:
+        return self.evaluate_async().result()
 
     def get_framework(self) -> str:
         return Framework.PYTORCH.value

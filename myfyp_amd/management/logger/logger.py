@@ -61,6 +61,7 @@ class P2PFLogger:
         self.local_metrics = LocalMetricStorage(disable_locks=disable_locks)
         self.global_metrics = GlobalMetricStorage(disable_locks=disable_locks)
         self.timings: Dict[str, Dict[str, List[float]]] = {}
+        self.metric_listeners: List[Callable] = []
         self._round_hooks: List[Callable[[str, str, Optional[Experiment]], None]] = []
 
         self._logger = logging.getLogger("myfyp_amd")
@@ -120,17 +121,39 @@ class P2PFLogger:
 
     # ------------------------------------------------------------------ metrics
     def log_metric(self, addr: str, metric: str, value: float, round: Optional[int] = None, step: Optional[int] = None) -> None:
-        """Log a metric; dropped if the node has not started an experiment (reference semantics)."""
+        """Log a metric; dropped if the node has not started an experiment (reference semantics).
+        ``round`` overrides the experiment's current round (the reference ignores it)."""
+        self.log_metric_at(addr, self.experiment_snapshot(addr), metric, value, step=step, round=round)
+
+    def experiment_snapshot(self, addr: str) -> Optional[tuple]:
+        """``(exp_name, round)`` of ``addr``'s running experiment, or None — captured when a device
+        result is enqueued so a metric that lands later is filed under the round that produced it."""
         node = self._nodes.get(addr)
-        if node is None:
-            return
-        experiment = node.get("Experiment")
+        experiment = node.get("Experiment") if node is not None else None
         if experiment is None or experiment.round is None or experiment.exp_name is None:
+            return None
+        return (experiment.exp_name, experiment.round)
+
+    def log_metric_at(self, addr: str, snapshot: Optional[tuple], metric: str, value: float, step: Optional[int] = None, round: Optional[int] = None) -> None:
+        if snapshot is None:
             return
+        exp_name, rnd = snapshot
+        if round is not None:
+            rnd = round
         if step is None:
-            self.global_metrics.add_log(experiment.exp_name, experiment.round, metric, addr, value)
+            self.global_metrics.add_log(exp_name, rnd, metric, addr, value)
         else:
-            self.local_metrics.add_log(experiment.exp_name, experiment.round, metric, addr, value, step)
+            self.local_metrics.add_log(exp_name, rnd, metric, addr, value, step)
+        for fn in list(self.metric_listeners):
+            fn(addr, exp_name, rnd, metric, value, step)
+
+    def add_metric_listener(self, fn: Callable) -> None:
+        """``fn(addr, exp_name, round, metric, value, step)`` after every stored metric."""
+        self.metric_listeners.append(fn)
+
+    def remove_metric_listener(self, fn: Callable) -> None:
+        if fn in self.metric_listeners:
+            self.metric_listeners.remove(fn)
 
     def get_local_logs(self) -> LocalLogsType:
         return self.local_metrics.get_all_logs()

@@ -63,6 +63,10 @@ _SIGNATURES = {
     "mlp_engine_run_epoch_eager": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mlp_engine_read_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_stats_async": (c_int, [c_void_p, c_int, c_void_p]),
+    "mlp_engine_eval_async": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "mlp_engine_fetch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_ring_size": (c_int, []),
 }
 
 

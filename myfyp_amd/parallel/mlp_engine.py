@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from myfyp_amd.ops import _native
+from myfyp_amd.parallel.pending import Pending, Resolver
 from myfyp_amd.settings import Settings
 
 
@@ -144,6 +145,11 @@ class MLPGroup:
         self._alloc(capacity)
         self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
         self.eval_gang = _Gang(self._run_eval_batch, lambda: set(self.handles))
+        # asynchronous results: pinned ring slots on the engine, resolved in order by one thread
+        self.resolver = Resolver(f"mlp-results-{device}")
+        self._ring = 0
+        self._next_slot = 0
+        self._slot_free: List[threading.Event] = []
 
     # ------------------------------------------------------------------ buffers / slots
     def _alloc(self, capacity: int) -> None:
@@ -304,14 +310,40 @@ class MLPGroup:
                     self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
                 t0 = (steps_pe * ep).astype(np.int32)
                 _native.check(run(self._engine, t0.ctypes.data, stream), "run_epoch")
-            loss = np.zeros(self.capacity, dtype=np.float32)
-            correct = np.zeros(self.capacity, dtype=np.int32)
-            _native.check(lib.mlp_engine_read_stats(self._engine, loss.ctypes.data, correct.ctypes.data, stream), "read_stats")
+            k = self._take_slot()
+            _native.check(lib.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
+            raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=False))
         out = {}
         for slot in batch:
             n = max(1, self.n_train[slot] * epochs)
-            out[slot] = (int(steps_pe[slot] * epochs), float(loss[slot]) / n, float(correct[slot]) / n)
+            out[slot] = (int(steps_pe[slot] * epochs), raw.map(lambda r, s=slot, n=n: (float(r[0][s]) / n, float(r[1][s]) / n)))
         return out
+
+    # ------------------------------------------------------------------ result ring
+    def _take_slot(self) -> int:
+        lib = _native.load(required=True)
+        if not self._slot_free:
+            self._ring = int(lib.mlp_engine_ring_size())
+            self._slot_free = [threading.Event() for _ in range(self._ring)]
+            for e in self._slot_free:
+                e.set()
+        k = self._next_slot % self._ring
+        self._next_slot += 1
+        if not self._slot_free[k].wait(timeout=Settings.AGGREGATION_TIMEOUT):
+            raise RuntimeError("device result ring stalled")
+        self._slot_free[k].clear()
+        return k
+
+    def _fetch(self, k: int, with_conf: bool):
+        lib = _native.load(required=True)
+        loss = np.zeros(self.capacity, dtype=np.float32)
+        correct = np.zeros(self.capacity, dtype=np.int32)
+        conf = np.zeros((self.capacity, 16, 16), dtype=np.int32) if with_conf else None
+        try:
+            _native.check(lib.mlp_engine_fetch(self._engine, k, loss.ctypes.data, correct.ctypes.data, conf.ctypes.data if with_conf else None), "fetch")
+        finally:
+            self._slot_free[k].set()
+        return loss, correct, conf
 
     def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
@@ -321,12 +353,11 @@ class MLPGroup:
             active = np.zeros(self.capacity, dtype=np.int32)
             for slot in batch:
                 active[slot] = 1
-            loss = np.zeros(self.capacity, dtype=np.float32)
-            correct = np.zeros(self.capacity, dtype=np.int32)
-            conf = np.zeros((self.capacity, 16, 16), dtype=np.int32)
-            _native.check(lib.mlp_engine_eval(self._engine, active.ctypes.data, loss.ctypes.data, correct.ctypes.data, conf.ctypes.data, stream), "eval")
+            k = self._take_slot()
+            _native.check(lib.mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
+            raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=True))
         D3 = self.dims[3]
-        return {slot: (float(loss[slot]) / max(1, self.n_test[slot]), conf[slot, :D3, :D3].copy()) for slot in batch}
+        return {slot: raw.map(lambda r, s=slot: (float(r[0][s]) / max(1, self.n_test[s]), r[2][s, :D3, :D3].copy())) for slot in batch}
 
     def expect(self, fit_slots: Optional[Set[int]] = None, eval_slots: Optional[Set[int]] = None) -> None:
         """Tell the gangs exactly which slots will call (collective workflow knows it)."""
@@ -408,11 +439,12 @@ class MLPEngineHandle:
             self.learner = learner
             self._data_id = id(learner.data)
             self.group.invalidate_data()
-        steps, loss, _acc = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
+        steps, stats = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
         learner.global_step += steps
-        return steps, loss
+        return steps, stats.map(lambda v: v[0])  # mean train loss, resolved asynchronously
 
-    def evaluate(self, learner) -> Tuple[float, np.ndarray]:
+    def evaluate(self, learner) -> "Pending":
+        """Enqueue the grouped evaluation; the returned Pending resolves to (mean NLL, confusion)."""
         if self.learner is not learner or getattr(self, "_data_id", None) != id(learner.data):
             self.learner = learner
             self._data_id = id(learner.data)

@@ -79,22 +79,24 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     group = _stacked_group(learners)
     dev = learners[0].flat_params().device
     if group is not None:
-        w = torch.zeros(group.capacity, dtype=torch.float32)
+        # weights/mask go up through pinned memory with non-blocking copies and nothing is read
+        # back: the host never waits for the GPU here (the total weight stays on the device)
+        pin = dev.type == "cuda"
+        wm = torch.zeros(2, group.capacity, dtype=torch.float32, pin_memory=pin)
         for lr, wt in zip(learners, weights):
-            w[lr._engine.slot] = wt
-        wsum_local = float(w.sum())
+            wm[0, lr._engine.slot] = wt
+            wm[1, lr._engine.slot] = 1.0
+        wsum_local = float(sum(weights))
+        wm_d = wm.to(dev, non_blocking=True)
         n = group.numel
         buf = torch.empty(n + 1, dtype=torch.float32, device=dev)
-        ops.stacked_weighted_sum(group.params[:, :n], w.to(dev), buf[:n], 1.0)
-        buf[n] = wsum_local
+        ops.stacked_weighted_sum(group.params[:, :n], wm_d[0], buf[:n], 1.0)
+        buf[n:].fill_(wsum_local)
         fed.all_reduce_(buf)
         total = buf[n:].clone()
         buf[:n].div_(total.clamp_min(1e-12))
-        mask = torch.zeros(group.capacity, dtype=torch.float32)
-        for lr in learners:
-            mask[lr._engine.slot] = 1.0
-        ops.broadcast_rows(buf[:n], group.params[:, :n], mask.to(dev))
-        total_w = float(total)  # one sync per round
+        ops.broadcast_rows(buf[:n], group.params[:, :n], wm_d[1])
+        total_w = total
     else:
         states = [state_tensors(lr) for lr in learners]
         flat = torch.cat([torch.cat([t.reshape(-1).float() for t in st]) for st in states[:1]])

@@ -26,8 +26,12 @@ class TrainStage(Stage):
         try:
             check_early_stop(state)
             aggregator.set_nodes_to_aggregate(state.train_set)
-            results = learner.evaluate()
-            logger.debug(state.addr, f"📈 Evaluated. Results: {results}")
+            # metrics are only logged here (reference: train_stage.py:104-117), so the evaluation is
+            # enqueued and its results are filed under this round when they land — no GPU wait
+            if hasattr(learner, "evaluate_async"):
+                learner.evaluate_async()
+            else:
+                logger.debug(state.addr, f"📈 Evaluated. Results: {learner.evaluate()}")
             check_early_stop(state)
             learner.fit()
             check_early_stop(state)
