@@ -189,14 +189,8 @@ class CNNGroup:
         self._bound_version = -1
         self._describe(template)
         self._alloc(capacity)
-    def detach(self, slot: int) -> None:
-        with self.lock:
-            self.handles.pop(slot, None)
-            self._data_version += 1
-        self.fit_gang.poke()
-        self.eval_gang.poke()
-        self.fit_gang.poke()
-        self.eval_gang.poke()
+        self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
+        self.eval_gang = _Gang(self._run_eval_batch, lambda: set(self.handles))
 
     # ------------------------------------------------------------------ description
     def _describe(self, m: torch.nn.Module) -> None:
