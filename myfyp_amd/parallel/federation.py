@@ -188,6 +188,7 @@ class Federation:
         self.round_hooks: List[Callable[[int, "Federation"], None]] = []
         self.stats: Dict[str, List[float]] = {}
         self._lock = threading.Lock()
+        self._cpu_pg = None
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
@@ -215,6 +216,8 @@ class Federation:
                 dist.init_process_group(backend=be, **kw)
             store = _default_store()
         cls._instance = cls(rank, world, local_rank, device, store)
+        if world > 1:
+            cls._instance._cpu_group()
         if store is not None:
             cls._instance.bus = StoreBus(store, rank, world, cls._instance._deliver)
         return cls._instance
@@ -314,13 +317,23 @@ class Federation:
         self.gang.poke()
 
     def all_gather_object(self, obj: Any) -> List[Any]:
+        """Control-plane gather (votes, wire models) over a CPU (gloo) group: an object gather on the
+        RCCL group would pickle through device memory and synchronise the host with every queued
+        kernel, stalling the asynchronous round pipeline."""
         if self.world == 1:
             return [obj]
         import torch.distributed as dist
 
         out: List[Any] = [None] * self.world
-        dist.all_gather_object(out, obj)
+        dist.all_gather_object(out, obj, group=self._cpu_group())
         return out
+
+    def _cpu_group(self):
+        if self._cpu_pg is None:
+            import torch.distributed as dist
+
+            self._cpu_pg = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+        return self._cpu_pg
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place SUM all-reduce over RCCL (bucketed for large buffers)."""
