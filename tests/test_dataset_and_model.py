@@ -113,3 +113,31 @@ def test_model_zoo_forward_shapes():
     assert ResNet18()(x).shape == (4, 10)
     out = MLP()(torch.randint(0, 255, (4, 28, 28), dtype=torch.uint8))
     assert torch.allclose(out.exp().sum(1), torch.ones(4), atol=1e-5)
+
+
+def test_interop_adapters_and_export():
+    import numpy as np
+
+    from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
+    from myfyp_amd.learning.frameworks.flax import FlaxModel
+    from myfyp_amd.learning.frameworks.learner_factory import LearnerFactory
+    from myfyp_amd.learning.frameworks.simulation import try_init_learner_with_ray
+    from myfyp_amd.learning.frameworks.tensorflow import KerasModel
+    from myfyp_amd.learning.frameworks.torch.export import PyTorchExportStrategy
+    from myfyp_amd.utils.check_ray import ray_installed
+
+    km = KerasModel(None, params=[np.ones((2, 3), np.float32), np.zeros(3, np.float32)], num_samples=4)
+    back = KerasModel(None)
+    back.set_parameters(km.encode_parameters())
+    assert [p.shape for p in back.get_parameters()] == [(2, 3), (3,)]
+    with pytest.raises(ValueError):
+        LearnerFactory.create_learner(km)
+    fm = FlaxModel(None, init_params={"dense": {"kernel": np.ones((2, 2)), "bias": np.zeros(2)}})
+    fm.set_parameters([np.full(2, 3.0), np.full((2, 2), 5.0)])  # sorted order: bias, kernel
+    assert fm.tree["dense"]["kernel"][0, 0] == 5.0 and fm.get_framework() == "flax"
+    assert ray_installed() is False
+    sentinel = object()
+    assert try_init_learner_with_ray(sentinel) is sentinel
+    dl = PyTorchExportStrategy.export(synthetic_mnist(64, 16), batch_size=8)
+    batch = next(iter(dl))
+    assert batch["image"].shape == (8, 28, 28) and batch["label"].shape == (8,)
