@@ -27,6 +27,11 @@ struct MLPArgs {
   const int* n;
   const int* perm;  // [P][perm_stride] local indices (epoch permutation)
   int64_t perm_stride;
+  // the epoch's batches, gathered once in permutation order at the start of the epoch so that the
+  // per-step kernels read contiguous rows instead of chasing perm -> pointer table -> row
+  uint8_t* Xb;      // [P][xb_rows][D0]
+  int* Yb;          // [P][xb_rows]
+  int64_t xb_rows;  // max_steps * B
   // test data
   const uint8_t* const* Xtp;
   const int* const* Ytp;
@@ -56,3 +61,4 @@ bool mlp_shape_supported(int D0, int D1, int D2, int D3);
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s);
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s);
 void mlp_launch_sync_shadow(const MLPArgs& a, hipStream_t s);
+void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s);

@@ -17,6 +17,23 @@
 #include "common.h"
 #include "mlp_fused.h"
 
+// Optional per-block phase timestamps (build with -DMLP_STAMPS; read with mlp_debug_stamps).
+#ifdef MLP_STAMPS
+__device__ unsigned long long g_mlp_stamps[3][4096][4];
+#define MLP_STAMP(k, i)                                                                                         \
+  do {                                                                                                          \
+    const unsigned _b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                        \
+    if (threadIdx.x == 0 && _b < 4096) g_mlp_stamps[k][_b][i] = wall_clock64();                                \
+  } while (0)
+extern "C" int mlp_debug_stamps(void* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mlp_stamps), sizeof(g_mlp_stamps)) == hipSuccess ? 0 : 1;
+}
+#else
+#define MLP_STAMP(k, i) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
 __device__ __forceinline__ int rows_valid_train(const MLPArgs& a, const int4& ctl, int step) {
@@ -36,11 +53,8 @@ __device__ __forceinline__ int peer_rows(const MLPArgs& a, const int4& ctl, int 
   return TRAIN ? rows_valid_train(a, ctl, step) : rows_valid_eval(a, ctl, base);
 }
 
-// local sample index of batch row r
-__device__ __forceinline__ int64_t sample_index(const MLPArgs& a, bool train, int p, int step, int base, int r) {
-  if (train) return a.perm[(int64_t)p * a.perm_stride + (int64_t)step * a.B + r];
-  return base + r;
-}
+// training row r of step `step` in the epoch-gathered batch buffer
+__device__ __forceinline__ int64_t batch_row(const MLPArgs& a, int p, int step, int r) { return (int64_t)p * a.xb_rows + (int64_t)step * a.B + r; }
 
 }  // namespace
 
@@ -53,6 +67,7 @@ __device__ __forceinline__ int64_t sample_index(const MLPArgs& a, bool train, in
 // ---------------------------------------------------------------------------------------------
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base) {
+  if (TRAIN) MLP_STAMP(0, 0);
   constexpr int MT = 2, NT = 2, KCH = 8;
   __shared__ __attribute__((aligned(16))) float sRed[3][64][MT * NT * 4];
   const int p = blockIdx.z;
@@ -67,7 +82,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
   float bias[2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) bias[nt] = a.params[(int64_t)p * a.S + a.off_b1 + col0 + nt * 16 + c];
-  const uint8_t* X = TRAIN ? a.Xp[p] : a.Xtp[p];
+  const uint8_t* X = TRAIN ? a.Xb : a.Xtp[p];
 
   const uint8_t* arow[MT];
   bool avalid[MT];
@@ -75,7 +90,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
   for (int mt = 0; mt < MT; ++mt) {
     const int r = row0 + mt * 16 + c;
     avalid[mt] = r < rows;
-    arow[mt] = avalid[mt] ? X + sample_index(a, TRAIN, p, step, base, r) * (int64_t)D0 : X;
+    arow[mt] = avalid[mt] ? X + (TRAIN ? batch_row(a, p, step, r) : (int64_t)(base + r)) * (int64_t)D0 : X;
   }
   const bf16* wrow[NT];
 #pragma unroll
@@ -112,6 +127,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_bf16(af[j][mt], bfr[j][nt], acc[mt][nt]);
   }
 
+  if (TRAIN) MLP_STAMP(0, 1);
   // cross-wave K reduction
   if (wave > 0) {
 #pragma unroll
@@ -123,6 +139,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
   }
   __syncthreads();
   if (wave != 0) return;
+  if (TRAIN) MLP_STAMP(0, 2);
 #pragma unroll
   for (int w = 0; w < 3; ++w)
 #pragma unroll
@@ -154,6 +171,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
       }
     }
   }
+  if (TRAIN) MLP_STAMP(0, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -161,6 +179,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
 // ---------------------------------------------------------------------------------------------
 template <int TP1, int TP2, bool TRAIN>
 __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
+  if (TRAIN) MLP_STAMP(1, 0);
   constexpr int D1 = TP1 * 64, D2 = TP2 * 64;
   constexpr int LD1 = D1 + 8, LD2 = D2 + 8;  // padded LDS rows (bf16) to spread banks
   constexpr int LDD = 32 + 8;
@@ -211,8 +230,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
     for (int i = 0; i < 4; ++i) {
       const int grow = row0 + 4 * h + i;
       if (grow < rows) {
-        const int64_t idx = sample_index(a, TRAIN, p, step, base, grow);
-        ylab[i] = TRAIN ? a.Yp[p][idx] : a.Ytp[p][idx];
+        ylab[i] = TRAIN ? a.Yb[batch_row(a, p, step, grow)] : a.Ytp[p][base + grow];
       }
     }
   }
@@ -235,6 +253,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   for (int i = threadIdx.x; i < 16 * LDD; i += 256) sDlog[i] = (bf16)0.f;
 
   __syncthreads();  // sW3 ready
+  if (TRAIN) MLP_STAMP(1, 1);
   if (wave == 0) {
 #pragma unroll
     for (int k = 0; k < KS2; ++k) w3f[k] = *reinterpret_cast<const bf16x8*>(&sW3[c * LD2 + k * 32 + 8 * h]);
@@ -315,6 +334,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   }
   if (!TRAIN) return;
   __syncthreads();
+  MLP_STAMP(1, 2);
 
   // ---- dH2 = dlogits · W3 ⊙ [H2 > 0]   (K = 16 classes, padded to 32)
   {
@@ -349,6 +369,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
     for (int i = 0; i < 4; ++i) packed[i] = (bf16)((float)sH1[(4 * h + i) * LD1 + n] > 0.f ? acc[i] : 0.f);
     *reinterpret_cast<bf16x4*>(a.dH1T + (int64_t)p * D1 * a.Bpad + (int64_t)n * a.Bpad + row0 + 4 * h) = packed;
   }
+  MLP_STAMP(1, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -447,10 +468,17 @@ __device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st
   }
 }
 
+// LDS is sized at launch for the real padded batch (sG 4352 B + sX 64 x (Bpad + 8) bf16): at
+// Bpad = 64 a block needs 13.6 KB instead of the 38 KB a MLP_MAX_BPAD-sized static array took, so
+// 8 blocks fit per CU and the whole grid (≈1.9k blocks for 8 peers) is resident in one pass.
+static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * 68 * sizeof(float) + (size_t)64 * (Bpad + 8) * sizeof(bf16); }
+
 __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
-  constexpr int LDX = MLP_MAX_BPAD + 8;
-  __shared__ __attribute__((aligned(16))) bf16 sX[64 * LDX];
-  __shared__ __attribute__((aligned(16))) float sG[16 * 68];
+  extern __shared__ __attribute__((aligned(16))) char smem_wg[];
+  float* sG = reinterpret_cast<float*>(smem_wg);
+  bf16* sX = reinterpret_cast<bf16*>(smem_wg + 16 * 68 * sizeof(float));
+  const int LDX = a.Bpad + 8;
+  MLP_STAMP(2, 0);
   const int p = blockIdx.z;
   const int4 ctl = a.ctl[p];
   const int rows = peer_rows<true>(a, ctl, step, 0);
@@ -476,11 +504,12 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
       const int r = e % Bp, q = e / Bp;  // row r, 8-byte chunk q of the 64-byte row segment
       uint2 v = {0u, 0u};
       const int col = i0 + q * 8;
-      if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xp[p] + sample_index(a, true, p, step, 0, r) * (int64_t)D0 + col);
+      if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xb + batch_row(a, p, step, r) * (int64_t)D0 + col);
 #pragma unroll
       for (int j = 0; j < 8; ++j) sX[(q * 8 + j) * LDX + r] = (bf16)(float)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xffu);
     }
     __syncthreads();
+    MLP_STAMP(2, 1);
     const bf16* A = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)(ob * 16 + c) * Bp;
     f32x4 acc = zero4();
     float bsum = 0.f;
@@ -498,7 +527,9 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
       if (h == 0) update_elem(a, pS + a.off_b1 + ob * 16 + c, bsum, bc1, bc2s);
     }
     __syncthreads();
+    MLP_STAMP(2, 2);
     tile_apply(a, st, sG, ob * 16, i0, D0, bc1, bc2s, false, p);
+    MLP_STAMP(2, 3);
     return;
   }
   if (b < nb1 + nb2) {
@@ -549,6 +580,27 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
     bsum += __shfl_xor(bsum, 32);
     if (h == 0 && c < D3) update_elem(a, pS + a.off_b3 + c, bsum, bc1, bc2s);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// epoch gather: Xb[p][i] = X_p[perm_p[i]], Yb[p][i] = Y_p[perm_p[i]] for i < n_p (first node of
+// every epoch graph). grid = (ceil(xb_rows / 4), 1, P), block = 256 = 4 rows x 64 lanes (8 B each).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
+  const int p = blockIdx.z;
+  const int n = a.ctl[p].y;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n || i >= a.xb_rows || !a.ctl[p].x) return;
+  const int64_t src = a.perm[(int64_t)p * a.perm_stride + i];
+  const uint8_t* xs = a.Xp[p] + src * (int64_t)a.D0;
+  uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
+  for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];
+  if (lane == 0) a.Yb[(int64_t)p * a.xb_rows + i] = a.Yp[p][src];
+}
+
+void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_gather_epoch, dim3((unsigned)((a.xb_rows + 3) / 4), 1, a.P), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -606,7 +658,7 @@ void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s) {
   const int nb1 = (a.D1 / 16) * ((a.D0 + 63) / 64);
   const int nb2 = (a.D2 / 16) * (a.D1 / 64);
   const int nb3 = (a.D2 / 16 + 3) / 4;
-  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), 0, s, a, step);
+  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), wgrad_lds_bytes(a.Bpad), s, a, step);
 }
 
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s) {

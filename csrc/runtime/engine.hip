@@ -81,6 +81,8 @@ struct MLPEngine {
     if (graph) hipGraphDestroy(graph);
     if (cap_stream) hipStreamDestroy(cap_stream);
     for (void* p : owned) hipFree(p);
+    if (a.Xb) hipFree(a.Xb);
+    if (a.Yb) hipFree(a.Yb);
     for (auto& r : ring) {
       if (r.ev) hipEventDestroy(r.ev);
       if (r.loss) hipHostFree(r.loss);
@@ -131,6 +133,7 @@ struct MLPEngine {
     invalidate();
     if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
     CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
+    mlp_launch_gather_epoch(a, cap_stream);
     for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
     hipError_t e = hipStreamEndCapture(cap_stream, &graph);
     if (e != hipSuccess) {
@@ -262,6 +265,18 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
   std::lock_guard<std::mutex> g(e->mu);
   e->a.Xp = (const uint8_t* const*)Xp; e->a.Yp = (const int* const*)Yp; e->a.n = n; e->a.perm = perm; e->a.perm_stride = perm_stride;
   e->max_steps = max_steps;
+  const int64_t rows = (int64_t)(max_steps > 0 ? max_steps : 1) * e->a.B;
+  if (rows != e->a.xb_rows) {  // epoch batch buffers
+    if (e->a.Xb) hipFree(e->a.Xb);
+    if (e->a.Yb) hipFree(e->a.Yb);
+    e->a.Xb = nullptr;
+    e->a.Yb = nullptr;
+    CHECK_HIP(hipMalloc((void**)&e->a.Xb, (size_t)e->a.P * rows * e->a.D0));
+    CHECK_HIP(hipMalloc((void**)&e->a.Yb, (size_t)e->a.P * rows * sizeof(int)));
+    CHECK_HIP(hipMemset(e->a.Xb, 0, (size_t)e->a.P * rows * e->a.D0));
+    CHECK_HIP(hipMemset(e->a.Yb, 0, (size_t)e->a.P * rows * sizeof(int)));
+    e->a.xb_rows = rows;
+  }
   e->invalidate();
   return 0;
 }
@@ -340,6 +355,7 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
   if (e->upload(s, nullptr)) return 1;
+  mlp_launch_gather_epoch(e->a, s);
   for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
   CHECK_HIP(hipGetLastError());
   return 0;

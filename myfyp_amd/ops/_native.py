@@ -22,7 +22,7 @@ _LOCK = threading.Lock()
 _ERR: Optional[str] = None
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
-LIB_PATH = os.path.join(LIB_DIR, "libmyfyp_hip.so")
+LIB_PATH = os.environ.get("MYFYP_NATIVE_LIB") or os.path.join(LIB_DIR, "libmyfyp_hip.so")  # override: diagnostics builds
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -67,6 +67,7 @@ _SIGNATURES = {
     "mlp_engine_eval_async": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "mlp_engine_fetch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_ring_size": (c_int, []),
+    "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
 }
 
 

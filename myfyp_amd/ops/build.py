@@ -40,12 +40,12 @@ def _headers_mtime() -> float:
     return max([os.path.getmtime(h) for h in hs] + [0.0])
 
 
-def _compile(src: str, hipcc: str, hdr_mtime: float, verbose: bool) -> str:
+def _compile(src: str, hipcc: str, hdr_mtime: float, verbose: bool, obj_dir: str = OBJ_DIR, extra: tuple = ()) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-    obj = os.path.join(OBJ_DIR, rel + ".o")
+    obj = os.path.join(obj_dir, rel + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
         return obj
-    cmd = [hipcc, *FLAGS, "-I", os.path.join(CSRC, "kernels"), "-c", src, "-o", obj]
+    cmd = [hipcc, *FLAGS, *extra, "-I", os.path.join(CSRC, "kernels"), "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -54,24 +54,32 @@ def _compile(src: str, hipcc: str, hdr_mtime: float, verbose: bool) -> str:
     return obj
 
 
-def build(verbose: bool = False, jobs: int = 8) -> str:
-    """Compile + link; returns the library path."""
+def build(verbose: bool = False, jobs: int = 8, variant: str = "") -> str:
+    """Compile + link; returns the library path. ``variant="stamps"`` builds a diagnostic copy with
+    per-block phase timestamps (``-DMLP_STAMPS``) under build/stamps/ (select it at run time with
+    ``MYFYP_NATIVE_LIB``)."""
     hipcc = _hipcc()
-    os.makedirs(OBJ_DIR, exist_ok=True)
-    os.makedirs(OUT_DIR, exist_ok=True)
+    obj_dir, lib, extra = OBJ_DIR, LIB, ()
+    if variant == "stamps":
+        obj_dir = os.path.join(ROOT, "build", "obj_stamps")
+        lib = os.path.join(ROOT, "build", "stamps", "libmyfyp_hip.so")
+        extra = ("-DMLP_STAMPS",)
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sources()
     hdr = _headers_mtime()
     with cf.ThreadPoolExecutor(max_workers=min(jobs, max(1, len(srcs)))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hipcc, hdr, verbose), srcs))
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, hipcc, hdr, verbose, obj_dir, extra), srcs))
+    LIB_ = lib
+    if not os.path.exists(LIB_) or os.path.getmtime(LIB_) < max(os.path.getmtime(o) for o in objs):
+        tmp = LIB_ + ".tmp"
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")
-        os.replace(tmp, LIB)
-    return LIB
+        os.replace(tmp, LIB_)
+    return LIB_
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build(verbose="-v" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))
