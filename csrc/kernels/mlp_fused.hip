@@ -405,10 +405,14 @@ __device__ __forceinline__ float frag_sum(const bf16x8& v) {
   return s;
 }
 
-// Block-wide vectorised optimizer update of a 16 × 64 tile: thread t owns row t>>4, columns
-// 4*(t&15)..+3 — a wave instruction touches 4 rows × 256 contiguous bytes. The optimizer state is
+// Block-wide vectorised optimizer update of a 16 × 128 tile: thread t owns row t>>5, columns
+// 4*(t&31)..+3 — a wave instruction touches 2 rows × 512 contiguous bytes. The optimizer state is
 // prefetched at block entry (independent of the gradient) so its latency hides under the staging
 // and the MFMAs; the gradient tile arrives through LDS (sG, fp32, row stride 68).
+#define WG_WAVES 8                 // waves per wgrad block
+#define WG_COLS (16 * WG_WAVES)     // columns of a gradient tile (16 rows x 128)
+#define WG_LDG (WG_COLS + 4)        // fp32 row stride of the LDS gradient tile
+
 struct TileState {
   float4 w, m, v;
   int64_t idx;
@@ -418,7 +422,7 @@ struct TileState {
 __device__ __forceinline__ TileState tile_prefetch(const MLPArgs& a, int64_t base, int ld, int row0, int col0, int ncols) {
   TileState st;
   const int tid = threadIdx.x;
-  const int r = tid >> 4, c4 = (tid & 15) * 4;
+  const int r = tid >> 5, c4 = (tid & 31) * 4;  // 512 threads: 16 rows x 32 float4 columns
   const int col = col0 + c4;
   st.idx = base + (int64_t)(row0 + r) * ld + col;
   st.live = col < ncols;
@@ -435,9 +439,9 @@ __device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st
                                            bool w2t_refresh, int p) {
   if (!st.live) return;
   const int tid = threadIdx.x;
-  const int r = tid >> 4, c4 = (tid & 15) * 4;
+  const int r = tid >> 5, c4 = (tid & 31) * 4;
   const int col = col0 + c4;
-  const float* g = sG + r * 68 + c4;
+  const float* g = sG + r * WG_LDG + c4;
   const int64_t idx = st.idx;
   if (st.vec) {
     float wv[4] = {st.w.x, st.w.y, st.w.z, st.w.w}, mv[4] = {st.m.x, st.m.y, st.m.z, st.m.w}, vv[4] = {st.v.x, st.v.y, st.v.z, st.v.w};
@@ -468,15 +472,17 @@ __device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st
   }
 }
 
-// LDS is sized at launch for the real padded batch (sG 4352 B + sX 64 x (Bpad + 8) bf16): at
-// Bpad = 64 a block needs 13.6 KB instead of the 38 KB a MLP_MAX_BPAD-sized static array took, so
-// 8 blocks fit per CU and the whole grid (≈1.9k blocks for 8 peers) is resident in one pass.
-static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * 68 * sizeof(float) + (size_t)64 * (Bpad + 8) * sizeof(bf16); }
+// LDS is sized at launch for the real padded batch (sG 16 x 132 fp32 + sX 128 x (Bpad + 8) bf16 =
+// 26.9 KB at Bpad = 64, instead of a MLP_MAX_BPAD-sized static array). Blocks are 512 threads over
+// 16 x 128 tiles: half the workgroups of a 256-thread / 16 x 64 decomposition, so the dispatcher
+// spreads the grid (≈1k blocks for 8 peers) over ~3 µs instead of ~6 µs (measured with the
+// -DMLP_STAMPS build: block start times spanned 6 µs of a 12.7 µs kernel).
+static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * WG_LDG * sizeof(float) + (size_t)WG_COLS * (Bpad + 8) * sizeof(bf16); }
 
-__global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
+__global__ __launch_bounds__(512) void mlp_wgrad_opt(MLPArgs a, int step) {
   extern __shared__ __attribute__((aligned(16))) char smem_wg[];
   float* sG = reinterpret_cast<float*>(smem_wg);
-  bf16* sX = reinterpret_cast<bf16*>(smem_wg + 16 * 68 * sizeof(float));
+  bf16* sX = reinterpret_cast<bf16*>(smem_wg + 16 * WG_LDG * sizeof(float));
   const int LDX = a.Bpad + 8;
   MLP_STAMP(2, 0);
   const int p = blockIdx.z;
@@ -489,19 +495,20 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   const int h = lane >> 4, c = lane & 15;
   const int D0 = a.D0, D1 = a.D1, D2 = a.D2, D3 = a.D3, Bp = a.Bpad;
   const int64_t pS = (int64_t)p * a.S;
-  const int cg1 = (D0 + 63) / 64;     // 64-column groups of W1
+  const int cg1 = (D0 + WG_COLS - 1) / WG_COLS;  // 128-column groups of W1
+  const int cg2 = (D1 + WG_COLS - 1) / WG_COLS;  // 128-column groups of W2
   const int nb1 = (D1 / 16) * cg1;
-  const int nb2 = (D2 / 16) * (D1 / 64);
+  const int nb2 = (D2 / 16) * cg2;
   const int b = blockIdx.x;
 
   if (b < nb1) {
     const int ob = b / cg1, ig = b % cg1;
-    const int i0 = ig * 64;
+    const int i0 = ig * WG_COLS;
     const TileState st = tile_prefetch(a, pS + a.off_w1, D0, ob * 16, i0, D0);
-    // ---- stage Xᵀ slab: sX[j][r] = X[sample(r)][i0 + j], j < 64 (bf16; 0 for invalid rows/cols).
+    // ---- stage Xᵀ slab: sX[j][r] = Xb[step row r][i0 + j], j < 128 (bf16; 0 for invalid rows/cols).
     //      Lanes run along r (consecutive LDS halves) so the transposing ds_write_b16s are conflict-free.
-    for (int e = threadIdx.x; e < Bp * 8; e += 256) {
-      const int r = e % Bp, q = e / Bp;  // row r, 8-byte chunk q of the 64-byte row segment
+    for (int e = threadIdx.x; e < Bp * (WG_COLS / 8); e += 512) {
+      const int r = e % Bp, q = e / Bp;  // row r, 8-byte chunk q of the 128-byte row segment
       uint2 v = {0u, 0u};
       const int col = i0 + q * 8;
       if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xb + batch_row(a, p, step, r) * (int64_t)D0 + col);
@@ -513,14 +520,16 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
     const bf16* A = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)(ob * 16 + c) * Bp;
     f32x4 acc = zero4();
     float bsum = 0.f;
-    for (int k0 = 0; k0 < Bp; k0 += 32) {
-      const bf16x8 av = ld8(A + k0 + 8 * h);
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[(wave * 16 + c) * LDX + k0 + 8 * h]);
-      if (ig == 0 && wave == 0) bsum += frag_sum(av);
-      acc = mfma_bf16(av, bv, acc);
+    if (i0 + wave * 16 < D0) {
+      for (int k0 = 0; k0 < Bp; k0 += 32) {
+        const bf16x8 av = ld8(A + k0 + 8 * h);
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[(wave * 16 + c) * LDX + k0 + 8 * h]);
+        if (ig == 0 && wave == 0) bsum += frag_sum(av);
+        acc = mfma_bf16(av, bv, acc);
+      }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * 68 + wave * 16 + c] = acc[r];
+    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * WG_LDG + wave * 16 + c] = acc[r];
     if (ig == 0 && wave == 0) {
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
@@ -533,33 +542,35 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
     return;
   }
   if (b < nb1 + nb2) {
-    // ---- W2: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b], tile = 16 rows (o2) × 64 cols (o1)
+    // ---- W2: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b], tile = 16 rows (o2) × 128 cols (o1)
     const int bb = b - nb1;
-    const int ob = bb / (D1 / 64), ig = bb % (D1 / 64);
-    const int ib = ig * 4 + wave;
-    const TileState st = tile_prefetch(a, pS + a.off_w2, D1, ob * 16, ig * 64, D1);
-    const bf16* A = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)(ob * 16 + c) * Bp;
-    const bf16* Bm = a.H1T + (int64_t)p * D1 * Bp + (int64_t)(ib * 16 + c) * Bp;
+    const int ob = bb / cg2, ig = bb % cg2;
+    const int ib = ig * WG_WAVES + wave;
+    const TileState st = tile_prefetch(a, pS + a.off_w2, D1, ob * 16, ig * WG_COLS, D1);
     f32x4 acc = zero4();
     float bsum = 0.f;
-    for (int k0 = 0; k0 < Bp; k0 += 32) {
-      const bf16x8 av = ld8(A + k0 + 8 * h);
-      if (ig == 0 && wave == 0) bsum += frag_sum(av);
-      acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
+    if (ib * 16 < D1) {
+      const bf16* A = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)(ob * 16 + c) * Bp;
+      const bf16* Bm = a.H1T + (int64_t)p * D1 * Bp + (int64_t)(ib * 16 + c) * Bp;
+      for (int k0 = 0; k0 < Bp; k0 += 32) {
+        const bf16x8 av = ld8(A + k0 + 8 * h);
+        if (ig == 0 && wave == 0) bsum += frag_sum(av);
+        acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
+      }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * 68 + wave * 16 + c] = acc[r];
+    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * WG_LDG + wave * 16 + c] = acc[r];
     if (ig == 0 && wave == 0) {
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
       if (h == 0) update_elem(a, pS + a.off_b2 + ob * 16 + c, bsum, bc1, bc2s);
     }
     __syncthreads();
-    tile_apply(a, st, sG, ob * 16, ig * 64, D1, bc1, bc2s, true, p);
+    tile_apply(a, st, sG, ob * 16, ig * WG_COLS, D1, bc1, bc2s, true, p);
     return;
   }
   // ---- W3 tiles: dW3[cls][o2] = Σ_b dlogitsᵀ[cls][b] · H2ᵀ[o2][b]  (classes padded to 16)
-  const int t = (b - nb1 - nb2) * 4 + wave;
+  const int t = (b - nb1 - nb2) * WG_WAVES + wave;
   if (t >= D2 / 16) return;
   const bf16* A = a.dlogT + (int64_t)p * 16 * Bp + (int64_t)c * Bp;
   const bf16* Bm = a.H2T + (int64_t)p * D2 * Bp + (int64_t)(t * 16 + c) * Bp;
@@ -655,10 +666,10 @@ static void launch_head_dispatch(const MLPArgs& a, int step, int base, bool trai
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s) {
   hipLaunchKernelGGL((mlp_fc1_fwd<true>), dim3(a.D1 / 32, a.Bpad / 32, a.P), dim3(256), 0, s, a, step, 0);
   launch_head_dispatch(a, step, 0, true, a.Bpad, s);
-  const int nb1 = (a.D1 / 16) * ((a.D0 + 63) / 64);
-  const int nb2 = (a.D2 / 16) * (a.D1 / 64);
-  const int nb3 = (a.D2 / 16 + 3) / 4;
-  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), wgrad_lds_bytes(a.Bpad), s, a, step);
+  const int nb1 = (a.D1 / 16) * ((a.D0 + WG_COLS - 1) / WG_COLS);
+  const int nb2 = (a.D2 / 16) * ((a.D1 + WG_COLS - 1) / WG_COLS);
+  const int nb3 = (a.D2 / 16 + WG_WAVES - 1) / WG_WAVES;
+  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(512), wgrad_lds_bytes(a.Bpad), s, a, step);
 }
 
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s) {

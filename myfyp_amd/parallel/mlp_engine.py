@@ -295,8 +295,10 @@ class MLPGroup:
             active = np.zeros(self.capacity, dtype=np.int32)
             for slot in batch:
                 active[slot] = 1
-                self.m[slot].zero_()
-                self.v[slot].zero_()
+            # fresh optimizer state per fit (Lightning semantics); slots not training this round are
+            # zeroed as well — they start fresh when they next train — so this is 2 launches, not 2P
+            self.m.zero_()
+            self.v.zero_()
             _native.check(lib.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
             steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
             keys = torch.empty(self.capacity, self.nmax, device=self.device)
