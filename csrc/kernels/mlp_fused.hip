@@ -405,85 +405,123 @@ __device__ __forceinline__ float frag_sum(const bf16x8& v) {
   return s;
 }
 
-// Block-wide vectorised optimizer update of a 16 × 128 tile: thread t owns row t>>5, columns
-// 4*(t&31)..+3 — a wave instruction touches 2 rows × 512 contiguous bytes. The optimizer state is
-// prefetched at block entry (independent of the gradient) so its latency hides under the staging
-// and the MFMAs; the gradient tile arrives through LDS (sG, fp32, row stride 68).
-#define WG_WAVES 8                 // waves per wgrad block
-#define WG_COLS (16 * WG_WAVES)     // columns of a gradient tile (16 rows x 128)
-#define WG_LDG (WG_COLS + 4)        // fp32 row stride of the LDS gradient tile
+// Block-wide vectorised optimizer update of a 16 × WG_COLS tile by 256 threads: float4 chunk q of
+// the row-major tile (q = tid + 256 k) is row q / (WG_COLS/4) — every wave instruction covers
+// contiguous row segments of params/m/v. The optimizer state is prefetched at block entry
+// (independent of the gradient) so its latency hides under the staging and the MFMAs; the
+// gradient tile arrives through LDS (sG, fp32, row stride WG_LDG).
+//
+// Tile choice, measured with the -DMLP_STAMPS build (8 peers, B = 64): 16 × 64 tiles / 4 waves
+// finish the kernel first (≈12.7 µs). Fatter tiles dispatch faster (the grid is launched at
+// ≈1 wave/ns: 1664 × 4 waves start over 5.9 µs, 576 × 4 over 0.3 µs) but each block's optimizer
+// chunk grows and the kernel — ≈49 MB of fp32 w/m/v traffic per step — ends later (16 × 256:
+// 14.3 µs; 16 × 128 with 8 waves: 13.7 µs).
+#define WG_WAVES 4                       // waves per wgrad block
+#define WG_NT 1                          // 16-column MFMA tiles per wave
+#define WG_COLS (16 * WG_WAVES * WG_NT)  // columns of a gradient tile (16 rows x 64)
+#define WG_LDG (WG_COLS + 4)             // fp32 row stride of the LDS gradient tile
+#define WG_Q (16 * WG_COLS / 4 / 256)    // float4 chunks per thread
 
 struct TileState {
-  float4 w, m, v;
-  int64_t idx;
-  bool vec, live;
+  float4 w[WG_Q], m[WG_Q], v[WG_Q];
+  int64_t base;
+  int row0, col0, ncols, ld;
 };
+
+__device__ __forceinline__ void chunk_pos(int k, int& r, int& c4) {
+  const int q = threadIdx.x + 256 * k;
+  r = q / (WG_COLS / 4);
+  c4 = (q % (WG_COLS / 4)) * 4;
+}
 
 __device__ __forceinline__ TileState tile_prefetch(const MLPArgs& a, int64_t base, int ld, int row0, int col0, int ncols) {
   TileState st;
-  const int tid = threadIdx.x;
-  const int r = tid >> 5, c4 = (tid & 31) * 4;  // 512 threads: 16 rows x 32 float4 columns
-  const int col = col0 + c4;
-  st.idx = base + (int64_t)(row0 + r) * ld + col;
-  st.live = col < ncols;
-  st.vec = st.live && col + 4 <= ncols && (ld & 3) == 0;
-  if (st.vec) {
-    st.w = *reinterpret_cast<const float4*>(a.params + st.idx);
-    st.m = *reinterpret_cast<const float4*>(a.m + st.idx);
-    st.v = a.opt.kind == 0 ? *reinterpret_cast<const float4*>(a.v + st.idx) : float4{0.f, 0.f, 0.f, 0.f};
+  st.base = base;
+  st.row0 = row0;
+  st.col0 = col0;
+  st.ncols = ncols;
+  st.ld = ld;
+#pragma unroll
+  for (int k = 0; k < WG_Q; ++k) {
+    int r, c4;
+    chunk_pos(k, r, c4);
+    const int col = col0 + c4;
+    if (col + 4 <= ncols && (ld & 3) == 0) {
+      const int64_t idx = base + (int64_t)(row0 + r) * ld + col;
+      st.w[k] = *reinterpret_cast<const float4*>(a.params + idx);
+      st.m[k] = *reinterpret_cast<const float4*>(a.m + idx);
+      st.v[k] = a.opt.kind == 0 ? *reinterpret_cast<const float4*>(a.v + idx) : float4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   return st;
 }
 
-__device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st, const float* sG, int row0, int col0, int ncols, float bc1, float bc2s,
-                                           bool w2t_refresh, int p) {
-  if (!st.live) return;
-  const int tid = threadIdx.x;
-  const int r = tid >> 5, c4 = (tid & 31) * 4;
-  const int col = col0 + c4;
-  const float* g = sG + r * WG_LDG + c4;
-  const int64_t idx = st.idx;
-  if (st.vec) {
-    float wv[4] = {st.w.x, st.w.y, st.w.z, st.w.w}, mv[4] = {st.m.x, st.m.y, st.m.z, st.m.w}, vv[4] = {st.v.x, st.v.y, st.v.z, st.v.w};
-    bf16x4 sh;
+__device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st, const float* sG, float bc1, float bc2s, bool w2t_refresh, int p) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      opt_update(a.opt, g[j], wv[j], mv[j], vv[j], bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
-      sh[j] = (bf16)wv[j];
-    }
-    *reinterpret_cast<float4*>(a.params + idx) = float4{wv[0], wv[1], wv[2], wv[3]};
-    *reinterpret_cast<float4*>(a.m + idx) = float4{mv[0], mv[1], mv[2], mv[3]};
-    if (a.opt.kind == 0) *reinterpret_cast<float4*>(a.v + idx) = float4{vv[0], vv[1], vv[2], vv[3]};
-    *reinterpret_cast<bf16x4*>(a.shadow + idx) = sh;
-    if (w2t_refresh) {
+  for (int k = 0; k < WG_Q; ++k) {
+    int r, c4;
+    chunk_pos(k, r, c4);
+    const int col = st.col0 + c4;
+    if (col >= st.ncols) continue;
+    const float* g = sG + r * WG_LDG + c4;
+    const int64_t idx = st.base + (int64_t)(st.row0 + r) * st.ld + col;
+    if (col + 4 <= st.ncols && (st.ld & 3) == 0) {
+      float wv[4] = {st.w[k].x, st.w[k].y, st.w[k].z, st.w[k].w}, mv[4] = {st.m[k].x, st.m[k].y, st.m[k].z, st.m[k].w},
+            vv[4] = {st.v[k].x, st.v[k].y, st.v[k].z, st.v[k].w};
+      bf16x4 sh;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + row0 + r] = sh[j];
-    }
-  } else {
-    for (int j = 0; j < 4 && col + j < ncols; ++j) {
-      float w = a.params[idx + j], m = a.m[idx + j], v = a.opt.kind == 0 ? a.v[idx + j] : 0.f;
-      opt_update(a.opt, g[j], w, m, v, bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
-      a.params[idx + j] = w;
-      a.m[idx + j] = m;
-      if (a.opt.kind == 0) a.v[idx + j] = v;
-      a.shadow[idx + j] = (bf16)w;
-      if (w2t_refresh) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + row0 + r] = (bf16)w;
+      for (int j = 0; j < 4; ++j) {
+        opt_update(a.opt, g[j], wv[j], mv[j], vv[j], bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
+        sh[j] = (bf16)wv[j];
+      }
+      *reinterpret_cast<float4*>(a.params + idx) = float4{wv[0], wv[1], wv[2], wv[3]};
+      *reinterpret_cast<float4*>(a.m + idx) = float4{mv[0], mv[1], mv[2], mv[3]};
+      if (a.opt.kind == 0) *reinterpret_cast<float4*>(a.v + idx) = float4{vv[0], vv[1], vv[2], vv[3]};
+      *reinterpret_cast<bf16x4*>(a.shadow + idx) = sh;
+      if (w2t_refresh) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + st.row0 + r] = sh[j];
+      }
+    } else {
+      for (int j = 0; j < 4 && col + j < st.ncols; ++j) {
+        float w = a.params[idx + j], m = a.m[idx + j], v = a.opt.kind == 0 ? a.v[idx + j] : 0.f;
+        opt_update(a.opt, g[j], w, m, v, bc1, bc2s, a.anchor, a.cg, a.cl, idx + j);
+        a.params[idx + j] = w;
+        a.m[idx + j] = m;
+        if (a.opt.kind == 0) a.v[idx + j] = v;
+        a.shadow[idx + j] = (bf16)w;
+        if (w2t_refresh) a.w2t[(int64_t)p * a.D1 * a.D2 + (int64_t)(col + j) * a.D2 + st.row0 + r] = (bf16)w;
+      }
     }
   }
 }
 
-// LDS is sized at launch for the real padded batch (sG 16 x 132 fp32 + sX 128 x (Bpad + 8) bf16 =
-// 26.9 KB at Bpad = 64, instead of a MLP_MAX_BPAD-sized static array). Blocks are 512 threads over
-// 16 x 128 tiles: half the workgroups of a 256-thread / 16 x 64 decomposition, so the dispatcher
-// spreads the grid (≈1k blocks for 8 peers) over ~3 µs instead of ~6 µs (measured with the
-// -DMLP_STAMPS build: block start times spanned 6 µs of a 12.7 µs kernel).
-static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * WG_LDG * sizeof(float) + (size_t)WG_COLS * (Bpad + 8) * sizeof(bf16); }
+// LDS is sized at launch for the real padded batch: sG 16 x (WG_COLS + 4) fp32 + the X slab, Bpad
+// rows x (WG_COLS + 8) bf16, staged ROW-major (coalesced 8-byte global loads along a sample row, one
+// ds_write_b128 per 8 pixels) and read as MFMA B fragments with the gfx950 transposed LDS read
+// (ds_read_b64_tr_b16) — no per-element transposing LDS writes (50 KB at Bpad = 64).
+#define WG_LDXR (WG_COLS + 8)
+static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * WG_LDG * sizeof(float) + (size_t)Bpad * WG_LDXR * sizeof(bf16); }
 
-__global__ __launch_bounds__(512) void mlp_wgrad_opt(MLPArgs a, int step) {
+typedef short mlp_s16x4 __attribute__((ext_vector_type(4)));
+typedef short mlp_s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) mlp_s16x4 mlp_lds_s16x4;
+
+// B fragment B[k0 + 8 (lane>>4) + j][n0 + (lane & 15)] from a row-major [k][n] bf16 LDS image
+// (two 4-row transposed reads; EXEC must be full — call from wave-uniform control flow only)
+__device__ __forceinline__ bf16x8 frag_b_tr(const bf16* base, int ld, int k0, int n0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const bf16* p0 = base + (k0 + 8 * g + q) * ld + n0 + 4 * pp;
+  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
+  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0 + 4 * ld));
+  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   extern __shared__ __attribute__((aligned(16))) char smem_wg[];
   float* sG = reinterpret_cast<float*>(smem_wg);
   bf16* sX = reinterpret_cast<bf16*>(smem_wg + 16 * WG_LDG * sizeof(float));
-  const int LDX = a.Bpad + 8;
   MLP_STAMP(2, 0);
   const int p = blockIdx.z;
   const int4 ctl = a.ctl[p];
@@ -491,82 +529,72 @@ __global__ __launch_bounds__(512) void mlp_wgrad_opt(MLPArgs a, int step) {
   if (rows == 0) return;
   float bc1, bc2s;
   step_bias_corr(a, ctl, step, bc1, bc2s);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
   const int h = lane >> 4, c = lane & 15;
   const int D0 = a.D0, D1 = a.D1, D2 = a.D2, D3 = a.D3, Bp = a.Bpad;
   const int64_t pS = (int64_t)p * a.S;
-  const int cg1 = (D0 + WG_COLS - 1) / WG_COLS;  // 128-column groups of W1
-  const int cg2 = (D1 + WG_COLS - 1) / WG_COLS;  // 128-column groups of W2
+  const int cg1 = (D0 + WG_COLS - 1) / WG_COLS;  // 256-column groups of W1
+  const int cg2 = (D1 + WG_COLS - 1) / WG_COLS;  // 256-column groups of W2
   const int nb1 = (D1 / 16) * cg1;
   const int nb2 = (D2 / 16) * cg2;
   const int b = blockIdx.x;
 
-  if (b < nb1) {
-    const int ob = b / cg1, ig = b % cg1;
+  if (b < nb1 + nb2) {
+    const bool w1 = b < nb1;
+    const int bb = w1 ? b : b - nb1;
+    const int cg = w1 ? cg1 : cg2;
+    const int ob = bb / cg, ig = bb % cg;
     const int i0 = ig * WG_COLS;
-    const TileState st = tile_prefetch(a, pS + a.off_w1, D0, ob * 16, i0, D0);
-    // ---- stage Xᵀ slab: sX[j][r] = Xb[step row r][i0 + j], j < 128 (bf16; 0 for invalid rows/cols).
-    //      Lanes run along r (consecutive LDS halves) so the transposing ds_write_b16s are conflict-free.
-    for (int e = threadIdx.x; e < Bp * (WG_COLS / 8); e += 512) {
-      const int r = e % Bp, q = e / Bp;  // row r, 8-byte chunk q of the 128-byte row segment
-      uint2 v = {0u, 0u};
-      const int col = i0 + q * 8;
-      if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xb + batch_row(a, p, step, r) * (int64_t)D0 + col);
+    const int ncols = w1 ? D0 : D1;
+    const TileState st = tile_prefetch(a, pS + (w1 ? a.off_w1 : a.off_w2), ncols, ob * 16, i0, ncols);
+    if (w1) {
+      // ---- stage the X slab row-major: sX[r][j] = Xb[step row r][i0 + j] as bf16 (0 outside);
+      //      a wave covers 2 rows x 256 contiguous bytes per load instruction.
+      for (int e = threadIdx.x; e < Bp * (WG_COLS / 8); e += 256) {
+        const int r = e / (WG_COLS / 8), q = e % (WG_COLS / 8);
+        uint2 v = {0u, 0u};
+        const int col = i0 + q * 8;
+        if (r < rows && col < D0) v = *reinterpret_cast<const uint2*>(a.Xb + batch_row(a, p, step, r) * (int64_t)D0 + col);
+        bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sX[(q * 8 + j) * LDX + r] = (bf16)(float)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xffu);
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)(float)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xffu);
+        *reinterpret_cast<bf16x8*>(&sX[r * WG_LDXR + q * 8]) = o;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     MLP_STAMP(2, 1);
-    const bf16* A = a.dH1T + (int64_t)p * D1 * Bp + (int64_t)(ob * 16 + c) * Bp;
-    f32x4 acc = zero4();
+    // dW[o][i] = Σ_b A[o][b] · B[i][b]:  A = dH1ᵀ (W1) or dH2ᵀ (W2); B = Xᵀ slab in LDS (W1) or H1ᵀ (W2)
+    const bf16* A = (w1 ? a.dH1T + (int64_t)p * D1 * Bp : a.dH2T + (int64_t)p * D2 * Bp) + (int64_t)(ob * 16 + c) * Bp;
+    f32x4 acc[WG_NT];
+#pragma unroll
+    for (int t = 0; t < WG_NT; ++t) acc[t] = zero4();
     float bsum = 0.f;
-    if (i0 + wave * 16 < D0) {
-      for (int k0 = 0; k0 < Bp; k0 += 32) {
-        const bf16x8 av = ld8(A + k0 + 8 * h);
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sX[(wave * 16 + c) * LDX + k0 + 8 * h]);
-        if (ig == 0 && wave == 0) bsum += frag_sum(av);
-        acc = mfma_bf16(av, bv, acc);
+    for (int k0 = 0; k0 < Bp; k0 += 32) {
+      const bf16x8 av = ld8(A + k0 + 8 * h);
+      if (ig == 0 && wave == 0) bsum += frag_sum(av);
+#pragma unroll
+      for (int t = 0; t < WG_NT; ++t) {
+        const int i = i0 + (wave * WG_NT + t) * 16;  // first column of this n-tile
+        if (i >= ncols) continue;
+        const bf16x8 bv = w1 ? frag_b_tr(sX, WG_LDXR, k0, (wave * WG_NT + t) * 16)
+                             : ld8(a.H1T + (int64_t)p * D1 * Bp + (int64_t)(i + c) * Bp + k0 + 8 * h);
+        acc[t] = mfma_bf16(av, bv, acc[t]);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * WG_LDG + wave * 16 + c] = acc[r];
+    for (int t = 0; t < WG_NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sG[(4 * h + r) * WG_LDG + (wave * WG_NT + t) * 16 + c] = acc[t][r];
     if (ig == 0 && wave == 0) {
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
-      if (h == 0) update_elem(a, pS + a.off_b1 + ob * 16 + c, bsum, bc1, bc2s);
+      if (h == 0) update_elem(a, pS + (w1 ? a.off_b1 : a.off_b2) + ob * 16 + c, bsum, bc1, bc2s);
     }
     __syncthreads();
     MLP_STAMP(2, 2);
-    tile_apply(a, st, sG, ob * 16, i0, D0, bc1, bc2s, false, p);
+    tile_apply(a, st, sG, bc1, bc2s, !w1, p);
     MLP_STAMP(2, 3);
-    return;
-  }
-  if (b < nb1 + nb2) {
-    // ---- W2: dW2[o2][o1] = Σ_b dH2ᵀ[o2][b] · H1ᵀ[o1][b], tile = 16 rows (o2) × 128 cols (o1)
-    const int bb = b - nb1;
-    const int ob = bb / cg2, ig = bb % cg2;
-    const int ib = ig * WG_WAVES + wave;
-    const TileState st = tile_prefetch(a, pS + a.off_w2, D1, ob * 16, ig * WG_COLS, D1);
-    f32x4 acc = zero4();
-    float bsum = 0.f;
-    if (ib * 16 < D1) {
-      const bf16* A = a.dH2T + (int64_t)p * D2 * Bp + (int64_t)(ob * 16 + c) * Bp;
-      const bf16* Bm = a.H1T + (int64_t)p * D1 * Bp + (int64_t)(ib * 16 + c) * Bp;
-      for (int k0 = 0; k0 < Bp; k0 += 32) {
-        const bf16x8 av = ld8(A + k0 + 8 * h);
-        if (ig == 0 && wave == 0) bsum += frag_sum(av);
-        acc = mfma_bf16(av, ld8(Bm + k0 + 8 * h), acc);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sG[(4 * h + r) * WG_LDG + wave * 16 + c] = acc[r];
-    if (ig == 0 && wave == 0) {
-      bsum += __shfl_xor(bsum, 16);
-      bsum += __shfl_xor(bsum, 32);
-      if (h == 0) update_elem(a, pS + a.off_b2 + ob * 16 + c, bsum, bc1, bc2s);
-    }
-    __syncthreads();
-    tile_apply(a, st, sG, ob * 16, ig * WG_COLS, D1, bc1, bc2s, true, p);
     return;
   }
   // ---- W3 tiles: dW3[cls][o2] = Σ_b dlogitsᵀ[cls][b] · H2ᵀ[o2][b]  (classes padded to 16)
@@ -669,7 +697,7 @@ void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s) {
   const int nb1 = (a.D1 / 16) * ((a.D0 + WG_COLS - 1) / WG_COLS);
   const int nb2 = (a.D2 / 16) * ((a.D1 + WG_COLS - 1) / WG_COLS);
   const int nb3 = (a.D2 / 16 + WG_WAVES - 1) / WG_WAVES;
-  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(512), wgrad_lds_bytes(a.Bpad), s, a, step);
+  hipLaunchKernelGGL(mlp_wgrad_opt, dim3(nb1 + nb2 + nb3, 1, a.P), dim3(256), wgrad_lds_bytes(a.Bpad), s, a, step);
 }
 
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s) {
