@@ -43,6 +43,12 @@ __device__ __forceinline__ bf16x8 ld8_u8(const uint8_t* p) {
   return r;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and meets the
+// other waves, but leaves global loads in flight (``__syncthreads()`` also drains vmcnt, which
+// stalls every wave on prefetches it does not need yet). Single asm with a memory clobber so the
+// compiler moves no memory access across it. Never use it to publish global-memory data.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float warp_sum16(float v) {
   // reduce across the 16 lanes of a lane-group (lanes sharing l>>4)
   v += __shfl_xor(v, 1);

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void mlp_fc1_fwd(MLPArgs a, int step, int base
 #pragma unroll
         for (int i = 0; i < 4; ++i) sRed[wave - 1][lane][(mt * NT + nt) * 4 + i] = acc[mt][nt][i];
   }
-  __syncthreads();
+  lds_barrier();
   if (wave != 0) return;
   if (TRAIN) MLP_STAMP(0, 2);
 #pragma unroll
@@ -234,16 +234,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
       }
     }
   }
-  // training: W3 columns for dH2 and W2ᵀ fragments for dH1
   bf16x8 w3c[TP2];
-  bf16x8 w2tf[TRAIN ? TP1 : 1][TRAIN ? KS2 : 1];
-  if (TRAIN) {
-    const bf16* w2t = a.w2t + (int64_t)p * D1 * D2;
-#pragma unroll
-    for (int t = 0; t < (TRAIN ? TP1 : 1); ++t)
-#pragma unroll
-      for (int k = 0; k < (TRAIN ? KS2 : 1); ++k) w2tf[t][k] = ld8(w2t + (int64_t)((wave + 4 * t) * 16 + c) * D2 + k * 32 + 8 * h);
-  }
 
   // stage H1 rows in LDS (mask for dH1) and zero the dlogits tile (k 16..31 = K padding)
   if (TRAIN && wave == 0) {
@@ -252,8 +243,18 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
   }
   for (int i = threadIdx.x; i < 16 * LDD; i += 256) sDlog[i] = (bf16)0.f;
 
-  __syncthreads();  // sW3 ready
+  lds_barrier();  // sW3 / sH1 / sDlog ready; H1 and W2 loads may still be in flight
   if (TRAIN) MLP_STAMP(1, 1);
+  // training: W2ᵀ fragments for dH1, only needed in the last phase — issued here so their
+  // latency hides under the H2 / logits / softmax phases instead of delaying the first barrier
+  bf16x8 w2tf[TRAIN ? TP1 : 1][TRAIN ? KS2 : 1];
+  if (TRAIN) {
+    const bf16* w2t = a.w2t + (int64_t)p * D1 * D2;
+#pragma unroll
+    for (int t = 0; t < (TRAIN ? TP1 : 1); ++t)
+#pragma unroll
+      for (int k = 0; k < (TRAIN ? KS2 : 1); ++k) w2tf[t][k] = ld8(w2t + (int64_t)((wave + 4 * t) * 16 + c) * D2 + k * 32 + 8 * h);
+  }
   if (wave == 0) {
 #pragma unroll
     for (int k = 0; k < KS2; ++k) w3f[k] = *reinterpret_cast<const bf16x8*>(&sW3[c * LD2 + k * 32 + 8 * h]);
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
     }
     if (TRAIN) *reinterpret_cast<bf16x4*>(a.H2T + (int64_t)p * D2 * a.Bpad + (int64_t)col * a.Bpad + row0 + 4 * h) = packed;
   }
-  __syncthreads();
+  lds_barrier();
 
   // ---- logits, log-softmax, NLL, argmax, dlogits (wave 0)
   if (wave == 0) {
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
     }
   }
   if (!TRAIN) return;
-  __syncthreads();
+  lds_barrier();
   MLP_STAMP(1, 2);
 
   // ---- dH2 = dlogits · W3 ⊙ [H2 > 0]   (K = 16 classes, padded to 32)
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(256) void mlp_head(MLPArgs a, int step, int base) {
       *reinterpret_cast<bf16x4*>(a.dH2T + (int64_t)p * D2 * a.Bpad + (int64_t)n * a.Bpad + row0 + 4 * h) = packed;
     }
   }
-  __syncthreads();
+  lds_barrier();
 
   // ---- dH1 = dH2 · W2 ⊙ [H1 > 0]   (B operand = W2ᵀ shadow, prefetched)
   bf16x8 adh[KS2];
@@ -561,7 +562,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
         for (int j = 0; j < 8; ++j) o[j] = (bf16)(float)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xffu);
         *reinterpret_cast<bf16x8*>(&sX[r * WG_LDXR + q * 8]) = o;
       }
-      __syncthreads();
+      lds_barrier();
     }
     MLP_STAMP(2, 1);
     // dW[o][i] = Σ_b A[o][b] · B[i][b]:  A = dH1ᵀ (W1) or dH2ᵀ (W2); B = Xᵀ slab in LDS (W1) or H1ᵀ (W2)
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
       bsum += __shfl_xor(bsum, 32);
       if (h == 0) update_elem(a, pS + (w1 ? a.off_b1 : a.off_b2) + ob * 16 + c, bsum, bc1, bc2s);
     }
-    __syncthreads();
+    lds_barrier();
     MLP_STAMP(2, 2);
     tile_apply(a, st, sG, bc1, bc2s, !w1, p);
     MLP_STAMP(2, 3);

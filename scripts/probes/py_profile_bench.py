@@ -34,5 +34,6 @@ s = io.StringIO()
 st = pstats.Stats(profiles[0], stream=s)
 for p in profiles[1:]:
     st.add(p)
-st.sort_stats("tottime").print_stats(60)
+st.sort_stats("tottime").print_stats(40)
+st.sort_stats("cumulative").print_stats("myfyp_amd", 60)
 print(s.getvalue()[:12000], file=sys.stderr)
