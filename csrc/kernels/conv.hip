@@ -8,7 +8,7 @@
 //   Operands are register-staged into a double-buffered LDS image whose 16-byte chunks are
 //   XOR-swizzled (chunk ^ ((row >> 1) & 7)) so every ds_read_b128 fragment read is conflict-free;
 //   one barrier per K-step (the next tile's global loads are in flight during the MFMAs).
-//   Fused epilogue: + bias, + residual, ReLU, zeroed channel padding, BatchNorm partial sums.
+//   Fused epilogue: + bias, + residual, ReLU, zeroed channel padding, BatchNorm sums (atomics).
 //   XCD-aware bijective block remap so tiles sharing an operand panel land on one L2.
 //
 // k_conv_wgrad<BM, BN>: dW[co][(r,s,ci)] = sum_m dY[m][co] · im2col(X)[m][(r,s,ci)]
@@ -32,6 +32,16 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// x / d for 0 <= x < 2^22 with a float reciprocal and one correction step (the gathers divide
+// by runtime geometry — Wo, Ho*Wo, S, channel chunks — in their inner loops; integer division is
+// a long VALU sequence on CDNA)
+__device__ __forceinline__ int fdiv(int x, int d, float inv) {
+  int q = (int)((float)x * inv);
+  q -= (q * d > x) ? 1 : 0;
+  q += ((q + 1) * d <= x) ? 1 : 0;
+  return q;
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 template <int MODE, int BN>
@@ -50,16 +60,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
-  if (m0 >= M) {  // tile past this peer's batch: only clear its BN partial rows
-    if (a.stats != nullptr) {
-      float* st = a.stats + peer * a.stats_ps;
-      for (int i = tid; i < 2 * 2 * BN; i += 256) {
-        const int rr = i / (2 * BN), rem = i % (2 * BN), which = rem / BN, c = n0 + rem % BN;
-        if (c < a.ncol) st[((tm * 2 + rr) * 2 + which) * a.ncol + c] = 0.f;
-      }
-    }
-    return;
-  }
+  if (m0 >= M) return;  // tile past this peer's batch
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
     }
   }
 
+  const float inv_cpp = 1.f / (float)cpp, inv_S = 1.f / (float)a.S, inv_st = 1.f / (float)a.stride;
   uint4 ra[4], rb[NB];
   auto load = [&](int kt) {
     const int k = kt * CG_BK + cc * 8;
@@ -95,9 +97,9 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
     int r = 0, s = 0, c8 = 0;
     if (kok) {
       const int q8 = k >> 3;
-      const int rs = q8 / cpp;
+      const int rs = fdiv(q8, cpp, inv_cpp);
       c8 = q8 - rs * cpp;
-      r = rs / a.S;
+      r = fdiv(rs, a.S, inv_S);
       s = rs - r * a.S;
     }
 #pragma unroll
@@ -109,9 +111,9 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
         w = a_bw[i] + s;
       } else {
         const int th = a_bh[i] - r, tw = a_bw[i] - s;
-        ok = ok && th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
-        h = th / a.stride;
-        w = tw / a.stride;
+        h = th >= 0 ? fdiv(th, a.stride, inv_st) : -1;
+        w = tw >= 0 ? fdiv(tw, a.stride, inv_st) : -1;
+        ok = ok && th >= 0 && tw >= 0 && h * a.stride == th && w * a.stride == tw;
       }
       ok = ok && h >= 0 && w >= 0 && h < a.src_h && w < a.src_w;
       ra[i] = ok ? *reinterpret_cast<const uint4*>(src + (int64_t)(a_img[i] + h * a.src_w + w) * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
@@ -191,14 +193,16 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
       }
     }
     if (a.stats != nullptr) {
+      // BatchNorm batch statistics: the wave's column sums go straight into the peer's [2][ncol]
+      // accumulator (no partial-row slab, no serial reduction kernel; bn_finalize reads and re-zeroes it)
       s += __shfl_xor(s, 16);
       s += __shfl_xor(s, 32);
       ss += __shfl_xor(ss, 16);
       ss += __shfl_xor(ss, 32);
       if ((lane >> 4) == 0 && cok) {
         float* st = a.stats + peer * a.stats_ps;
-        st[((tm * 2 + wr) * 2 + 0) * a.ncol + col] = s;
-        st[((tm * 2 + wr) * 2 + 1) * a.ncol + col] = ss;
+        atomicAdd(st + col, s);
+        atomicAdd(st + a.ncol + col, ss);
       }
     }
   }
@@ -245,6 +249,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   const int cca = tid % CA;
   const bool acol_ok = co0 + cca * 8 < a.dy_c;
 
+  const float inv_hwo = 1.f / (float)hwo, inv_wo = 1.f / (float)a.Wo;
   uint4 ra[NA], rb[NBr];
   auto load = [&](int m_base) {
 #pragma unroll
@@ -258,8 +263,8 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
       bool ok = bcol_ok && m < kend;
       int64_t off = 0;
       if (ok) {
-        const int img = m / hwo, rem = m - img * hwo;
-        const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+        const int img = fdiv(m, hwo, inv_hwo), rem = m - img * hwo;
+        const int oh = fdiv(rem, a.Wo, inv_wo), ow = rem - oh * a.Wo;
         const int h = oh * a.stride - a.pad + br, w = ow * a.stride - a.pad + bs;
         ok = h >= 0 && w >= 0 && h < a.H && w < a.W;
         off = ((int64_t)(img * a.H + h) * a.W + w) * a.x_c + bci;
@@ -363,9 +368,8 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) {
-  return 2 * ((max_batch * out_h * out_w + CG_BM - 1) / CG_BM);
-}
+// rows of the BN statistics buffer a conv epilogue writes: one (sum, sumsq) accumulator row
+extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) { return 1; }
 
 extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, void* stream) {
   const WgradArgs& a = *pa;

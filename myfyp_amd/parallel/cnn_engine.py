@@ -82,6 +82,7 @@ _SIGS = {
     "cnn_xent": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_sgd_shadow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "cnn_segment_size": (c_int, []),
+    "cnn_shadow_rebuild": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
 }
 
 
@@ -308,8 +309,10 @@ class CNNGroup:
         for c in self.convs:
             wf, wt = self.shadow_off[c.name]
             cm = 0
-            if c.colmap is not None:
-                t = torch.from_numpy(c.colmap).to(self.device)
+            if c.colmap is not None:  # the shadow kernels map engine channel -> torch input column
+                inv = np.full(c.cp_in, -1, dtype=np.int32)
+                inv[c.colmap] = np.arange(len(c.colmap), dtype=np.int32)
+                t = torch.from_numpy(inv).to(self.device)
                 self._keep_colmaps.append(t)
                 cm = t.data_ptr()
             cin_t = getattr(c, "cin_torch", c.cin)
@@ -324,6 +327,10 @@ class CNNGroup:
         self.segs = raw.to(self.device)
         self.nseg = len(segs)
         self.max_seg = max(s.n for s in segs)
+        self.max_cout = max(c.cout for c in self.convs)
+        self.max_tr_tiles = max(((c.cp_in + 31) // 32) * ((c.cp_out + 31) // 32) * c.R * c.S for c in self.convs)
+        if max(getattr(c, "cin_torch", c.cin) * c.R * c.S for c in self.convs) > 4608:
+            raise ValueError("conv layer too wide for the shadow kernel (cin * R * S > 4608)")
 
     def act(self, name: str, rows: int, cp: int, dtype=torch.bfloat16) -> torch.Tensor:
         t = self._acts.get(name)
@@ -693,10 +700,15 @@ class CNNGroup:
 
     def _optimizer(self, update: bool) -> None:
         o = self._opt
-        _chk(_lib().cnn_sgd_shadow(self.params.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg,
-                                   self.max_seg, o["kind"], o["lr"], o["momentum"], o["weight_decay"], o["nesterov"], o["mu"], _p(o.get("anchor")),
-                                   _p(o.get("cg")), _p(o.get("cl")), int(update), self.shadow.data_ptr(), self.shadow.data_ptr(), self.shadow.shape[1],
-                                   self.nb.data_ptr() if update else None, self.capacity, self._stream()), "sgd_shadow")
+        lib = _lib()
+        active = self.nb.data_ptr() if update else None
+        if update:
+            _chk(lib.cnn_sgd_shadow(self.params.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg,
+                                    self.max_seg, o["kind"], o["lr"], o["momentum"], o["weight_decay"], o["nesterov"], o["mu"], _p(o.get("anchor")),
+                                    _p(o.get("cg")), _p(o.get("cl")), 1, self.shadow.data_ptr(), self.shadow.data_ptr(), self.shadow.shape[1],
+                                    active, self.capacity, self._stream()), "sgd")
+        _chk(lib.cnn_shadow_rebuild(self.params.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg, self.max_cout, self.max_tr_tiles,
+                                    self.shadow.data_ptr(), self.shadow.shape[1], active, self.capacity, self._stream()), "shadow_rebuild")
 
     def _shadow_sync(self) -> None:
         saved = getattr(self, "_opt", None)
