@@ -1,0 +1,223 @@
+// Node-local control-plane collectives over POSIX shared memory.
+//
+// The collective workflow exchanges a few hundred bytes per round between ranks (train-set votes,
+// live-peer lists).  The reference does this with TTL-relayed gRPC broadcasts
+// (p2pfl/stages/base_node/vote_train_set_stage.py:101-107 + grpc_server.py:211-215); a gloo
+// all_gather_object costs two TCP collectives plus pickling (~1-5 ms for 8 ranks), which is the
+// same order as a whole MLP round on MI355X.  All ranks of a single-node job share one mapping:
+//
+//   [Header 256 B][RankCtl x world (128 B each)][data: world x 2 parity slots x slot_bytes]
+//
+// allgather(gen): write own payload into parity slot (gen & 1), publish `arrived = gen` with a
+// release store, spin (pause -> yield) until every rank published >= gen, then copy all slots out.
+// Two parity slots suffice: a rank can only write generation g+2 into parity (g & 1) after every
+// rank arrived at g+1, i.e. after every rank finished reading generation g.
+//
+// Payloads larger than the slot publish an overflow marker; every rank then sees the overflow and
+// the caller falls back to the gloo path collectively (no rank can diverge).
+//
+// Plain C ABI (ctypes), host-only: no GPU state is touched.
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+namespace {
+
+constexpr uint64_t kMagic = 0x6d79667970736d63ull;  // "myfypsmc"
+constexpr uint64_t kOverflow = ~0ull;
+
+struct Header {
+  std::atomic<uint64_t> magic;
+  int32_t world;
+  int32_t pad;
+  uint64_t slot_bytes;
+  std::atomic<int32_t> attached;
+  char reserved[256 - 32];
+};
+static_assert(sizeof(Header) == 256, "header layout");
+
+struct alignas(128) RankCtl {
+  std::atomic<uint64_t> arrived;  // last published generation
+  uint64_t len[2];                // payload length per parity slot (kOverflow = too large)
+};
+static_assert(sizeof(RankCtl) == 128, "rank ctl layout");
+
+struct Handle {
+  void* base;
+  size_t bytes;
+  int rank;
+  int world;
+  uint64_t slot_bytes;
+  uint64_t gen;
+  Header* hdr() const { return reinterpret_cast<Header*>(base); }
+  RankCtl* ctl(int r) const { return reinterpret_cast<RankCtl*>(static_cast<char*>(base) + sizeof(Header)) + r; }
+  char* slot(int r, int parity) const {
+    char* d = static_cast<char*>(base) + sizeof(Header) + sizeof(RankCtl) * world;
+    return d + (static_cast<size_t>(r) * 2 + parity) * slot_bytes;
+  }
+};
+
+size_t total_bytes(int world, uint64_t slot_bytes) {
+  return sizeof(Header) + sizeof(RankCtl) * world + static_cast<size_t>(world) * 2 * slot_bytes;
+}
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+}
+
+// spin briefly, then yield; returns false on timeout
+template <class Pred>
+bool wait_until(Pred ready, double timeout_s) {
+  for (int i = 0; i < 4096; ++i) {
+    if (ready()) return true;
+    cpu_relax();
+  }
+  const double t0 = now_s();
+  for (uint64_t i = 0;; ++i) {
+    if (ready()) return true;
+    sched_yield();
+    if ((i & 255) == 0 && timeout_s > 0 && now_s() - t0 > timeout_s) return ready();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int shmc_version() { return 1; }
+
+// Rank 0 creates (`create`=1) the segment, the others attach. Returns nullptr on failure (errno set).
+void* shmc_open(const char* name, int rank, int world, uint64_t slot_bytes, int create, double timeout_s) {
+  if (world < 1 || rank < 0 || rank >= world || slot_bytes < 64) {
+    errno = EINVAL;
+    return nullptr;
+  }
+  slot_bytes = (slot_bytes + 127) & ~uint64_t(127);
+  const size_t bytes = total_bytes(world, slot_bytes);
+  int fd = -1;
+  if (create) {
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) return nullptr;
+    if (ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+      close(fd);
+      shm_unlink(name);
+      return nullptr;
+    }
+  } else {
+    const double t0 = now_s();
+    for (;;) {
+      fd = shm_open(name, O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat st;
+        if (fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes) break;
+        close(fd);
+        fd = -1;
+      }
+      if (now_s() - t0 > timeout_s) {
+        errno = ETIMEDOUT;
+        return nullptr;
+      }
+      usleep(1000);
+    }
+  }
+  void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (base == MAP_FAILED) return nullptr;
+  Handle* h = new Handle{base, bytes, rank, world, slot_bytes, 0};
+  Header* hd = h->hdr();
+  if (create) {
+    std::memset(base, 0, sizeof(Header) + sizeof(RankCtl) * world);
+    hd->world = world;
+    hd->slot_bytes = slot_bytes;
+    hd->magic.store(kMagic, std::memory_order_release);
+  } else {
+    if (!wait_until([&] { return hd->magic.load(std::memory_order_acquire) == kMagic; }, timeout_s) || hd->world != world ||
+        hd->slot_bytes != slot_bytes) {
+      munmap(base, bytes);
+      delete h;
+      errno = EPROTO;
+      return nullptr;
+    }
+  }
+  hd->attached.fetch_add(1, std::memory_order_acq_rel);
+  return h;
+}
+
+// Block until all `world` ranks attached (then the creator may unlink the name). 0 ok, -1 timeout.
+int shmc_wait_attached(void* handle, double timeout_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  return wait_until([&] { return h->hdr()->attached.load(std::memory_order_acquire) >= h->world; }, timeout_s) ? 0 : -1;
+}
+
+int shmc_unlink(const char* name) { return shm_unlink(name); }
+
+uint64_t shmc_slot_bytes(void* handle) { return static_cast<Handle*>(handle)->slot_bytes; }
+
+// All-gather of variable-length byte payloads.  `out` has room for world * slot_bytes; rank r's
+// payload lands at out + r * slot_bytes with its length in lens[r].
+// Returns 0 on success, 1 if some rank's payload overflowed its slot (all ranks return 1 for the
+// same generation), -1 on timeout (a rank died or stalled).
+int shmc_allgather(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, double timeout_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  const uint64_t gen = ++h->gen;
+  const int par = static_cast<int>(gen & 1);
+  RankCtl* me = h->ctl(h->rank);
+  if (n <= h->slot_bytes) {
+    std::memcpy(h->slot(h->rank, par), in, n);
+    me->len[par] = n;
+  } else {
+    me->len[par] = kOverflow;
+  }
+  me->arrived.store(gen, std::memory_order_release);
+  int rc = 0;
+  for (int r = 0; r < h->world; ++r) {
+    RankCtl* c = h->ctl(r);
+    if (!wait_until([&] { return c->arrived.load(std::memory_order_acquire) >= gen; }, timeout_s)) return -1;
+    const uint64_t len = c->len[par];
+    if (len == kOverflow) {
+      rc = 1;
+      lens[r] = 0;
+      continue;
+    }
+    lens[r] = len;
+    std::memcpy(static_cast<char*>(out) + static_cast<size_t>(r) * h->slot_bytes, h->slot(r, par), len);
+  }
+  return rc;
+}
+
+// Barrier = all-gather of nothing.
+int shmc_barrier(void* handle, double timeout_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  const uint64_t gen = ++h->gen;
+  h->ctl(h->rank)->len[gen & 1] = 0;
+  h->ctl(h->rank)->arrived.store(gen, std::memory_order_release);
+  for (int r = 0; r < h->world; ++r) {
+    RankCtl* c = h->ctl(r);
+    if (!wait_until([&] { return c->arrived.load(std::memory_order_acquire) >= gen; }, timeout_s)) return -1;
+  }
+  return 0;
+}
+
+void shmc_close(void* handle) {
+  Handle* h = static_cast<Handle*>(handle);
+  if (!h) return;
+  munmap(h->base, h->bytes);
+  delete h;
+}
+
+}  // extern "C"

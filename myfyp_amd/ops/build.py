@@ -20,6 +20,7 @@ CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "myfyp_amd", "_native")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(OUT_DIR, "libmyfyp_hip.so")
+HOST_LIB = os.path.join(OUT_DIR, "libmyfyp_host.so")
 ARCH = os.environ.get("MYFYP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wno-unused-result"]
 
@@ -81,5 +82,29 @@ def build(verbose: bool = False, jobs: int = 8, variant: str = "") -> str:
     return LIB_
 
 
+def host_sources() -> List[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+
+
+def build_host(verbose: bool = False) -> str:
+    """Host-only runtime pieces (shared-memory control-plane collectives): plain C++17, built with
+    the system compiler so CPU-only hosts have them too. Atomic replace: concurrent ranks may race."""
+    srcs = host_sources()
+    if os.path.exists(HOST_LIB) and os.path.getmtime(HOST_LIB) >= max(os.path.getmtime(s) for s in srcs):
+        return HOST_LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++") or "/opt/rocm/llvm/bin/clang++"
+    tmp = f"{HOST_LIB}.{os.getpid()}.tmp"
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", *srcs, "-o", tmp, "-lrt"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"host library build failed:\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, HOST_LIB)
+    return HOST_LIB
+
+
 if __name__ == "__main__":
+    print(build_host(verbose="-v" in sys.argv))
     print(build(verbose="-v" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))

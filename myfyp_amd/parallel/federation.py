@@ -189,6 +189,7 @@ class Federation:
         self.stats: Dict[str, List[float]] = {}
         self._lock = threading.Lock()
         self._cpu_pg = None
+        self.shm = None  # node-local shared-memory control plane (single-node jobs)
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
@@ -218,6 +219,7 @@ class Federation:
         cls._instance = cls(rank, world, local_rank, device, store)
         if world > 1:
             cls._instance._cpu_group()
+            cls._instance._init_shm()
         if store is not None:
             cls._instance.bus = StoreBus(store, rank, world, cls._instance._deliver)
         return cls._instance
@@ -228,8 +230,30 @@ class Federation:
             return cls.init()
         return cls._instance
 
+    def _init_shm(self) -> None:
+        """All ranks on one host (the single-node MI355X case) → control-plane gathers go through a
+        shared-memory segment (``csrc/host/shm_collective.cpp``) instead of gloo TCP."""
+        if not Settings.SHM_CONTROL_PLANE or self.store is None:
+            return
+        import socket
+
+        from myfyp_amd.parallel.shm_collective import ShmCollective
+
+        try:
+            with open("/proc/sys/kernel/random/boot_id") as f:
+                host = socket.gethostname() + "/" + f.read().strip()
+        except OSError:
+            host = socket.gethostname()
+        self.store.set(f"fedhost/{self.rank}", host)
+        if any(self.store.get(f"fedhost/{r}").decode() != host for r in range(self.world)):
+            return
+        self.shm = ShmCollective.create(self.store, self.rank, self.world, timeout=float(Settings.COLLECTIVE_TIMEOUT))
+
     def shutdown(self) -> None:
         """Stop the control bus and tear down the process group (call once, at exit)."""
+        if self.shm is not None:
+            self.shm.close()
+            self.shm = None
         if self.bus is not None:
             self.bus.stop()
             self.bus = None
@@ -246,6 +270,9 @@ class Federation:
         inst = cls._instance
         if inst is not None and inst.bus is not None:
             inst.bus.stop()
+        if inst is not None and inst.shm is not None:
+            inst.shm.close()
+            inst.shm = None
         cls._instance = None
 
     def register_local(self, node) -> None:
@@ -322,6 +349,11 @@ class Federation:
         kernel, stalling the asynchronous round pipeline."""
         if self.world == 1:
             return [obj]
+        if self.shm is not None:
+            got = self.shm.allgather_object(obj)
+            if got is not None:
+                return got
+            # some rank's payload exceeded the shared slot: every rank takes the gloo path together
         import torch.distributed as dist
 
         out: List[Any] = [None] * self.world

@@ -91,6 +91,7 @@ class Settings:
     GANG_WINDOW: float = 0.05  # seconds a grouped fit waits for expected co-located peers
     COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
     BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
+    SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
 
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
@@ -148,6 +149,7 @@ class Settings:
             "GANG_WINDOW": "GANG_WINDOW",
             "COLLECTIVE_TIMEOUT": "COLLECTIVE_TIMEOUT",
             "BUCKET_BYTES": "BUCKET_BYTES",
+            "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
         }
     )
 
