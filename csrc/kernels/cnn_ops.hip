@@ -457,87 +457,91 @@ __global__ void k_xent(const bf16* logits, int64_t lg_ps, int Lp, int K, const i
 }
 
 // ------------------------------------------------------------------------------------------------
-// fused optimizer + bf16 weight shadows, one block row per parameter segment (grid.y), peer grid.z
+// fused optimizer + bf16 weight shadow refresh
+//
+// One block per work item (grid.x) and peer (grid.y); the work table lists (segment, row) pairs so
+// no block is launched empty (a (max_cout x n_segments) grid dispatched ~250k idle blocks per step).
+//   conv/fc weight row co (kind 1): the Wf-layout gradient row [R*S][cp_in] is staged into LDS
+//     (coalesced, padded rows: conflict-free column reads), the torch-order master row
+//     W[co][cin][R][S] and its momentum are updated in one coalesced pass (FedProx / SCAFFOLD /
+//     weight decay / Nesterov via opt_update), the new row is kept in LDS and written out as the
+//     bf16 shadow row Wf[co][R][S][cp_in] (engine channel order; colmaps for fc after a flatten).
+//   plain vector chunk (kind 0: biases, BN affine): elementwise update of 256 elements.
+// Consumed gradients that are accumulated with atomics are re-zeroed here (no per-step memset).
 // ------------------------------------------------------------------------------------------------
 struct Segment {
-  int64_t off;       // element offset in the flat parameter vector
-  int n;             // elements
-  int kind;          // 0 plain, 1 conv/fc weight with shadows
+  int64_t off;          // element offset in the flat parameter vector (torch order)
+  int n;                // elements
+  int kind;             // 0 plain, 1 conv/fc weight with a Wf shadow
   int cout, cin, R, S, cp_in, cp_out;
-  int64_t wf_off, wt_off;   // offsets in the shadow buffers
-  const int* colmap;        // torch input-column -> engine channel (fc after NHWC flatten) or null
+  int zero_after;       // re-zero the consumed gradient (atomically accumulated ones)
+  int pad_;
+  int64_t wf_off;       // offset of the layer's Wf shadow (bf16) and Wf-layout gradient (fp32)
+  const int* e2t;       // engine input channel -> torch input column (fc after flatten) or null
+  const int* t2e;       // torch input column -> engine input channel, or null
 };
 
-__global__ void k_sgd_shadow(float* w, float* g, float* mbuf, int64_t ps, const Segment* segs, OptParams o, const float* anchor, const float* cg,
-                             const float* cl, int update, bf16* wf, bf16* wt, int64_t shadow_ps, const int* active) {
-  const int peer = blockIdx.z;
-  if (active != nullptr && !active[peer]) return;
-  const Segment sg = segs[blockIdx.y];
-  float* wp = w + peer * ps;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < sg.n; i += gridDim.x * blockDim.x) {
-    const int64_t idx = sg.off + i;
-    float wv = wp[idx];
-    if (update) {
-      float mv = mbuf[peer * ps + idx], vv = 0.f;
-      opt_update(o, g[peer * ps + idx], wv, mv, vv, 1.f, 1.f, anchor ? anchor + peer * ps : nullptr, cg ? cg + peer * ps : nullptr,
-                 cl ? cl + peer * ps : nullptr, idx);
-      wp[idx] = wv;
-      mbuf[peer * ps + idx] = mv;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// bf16 weight shadows of the conv/fc layers, rebuilt after each optimizer step with coalesced
-// traffic (a scattered per-element write from the optimizer cost 1.3 ms per ResNet-18 step):
-//   k_shadow_fwd   : block per output channel: W[co][cin][R][S] (contiguous fp32) -> LDS ->
-//                    Wf[co][R][S][cp_in] rows (engine channel order, colmap for flattened fc inputs)
-//   k_shadow_tr    : 32 x 32 LDS-tiled transpose per (r, s): Wf[co][rs][ci] -> Wt[ci][rs][co]
-// ------------------------------------------------------------------------------------------------
 #define SHADOW_MAX_ROW 4608  // cin * R * S floats of one output channel (512 * 3 * 3)
+#define GRAD_MAX_ROW (4608 + 16)
 
-__global__ __launch_bounds__(256) void k_shadow_fwd(const float* w, int64_t ps, const Segment* segs, bf16* shadow, int64_t shadow_ps, const int* active) {
-  const int peer = blockIdx.z;
+__global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbuf, int64_t ps, const float* gf, int64_t gf_ps,
+                                                  const Segment* segs, const int2* work, OptParams o, const float* anchor, const float* cg,
+                                                  const float* cl, int update, bf16* shadow, int64_t shadow_ps, const int* active) {
+  const int peer = blockIdx.y;
   if (active != nullptr && !active[peer]) return;
-  const Segment sg = segs[blockIdx.y];
-  const int co = blockIdx.x;
-  if (sg.kind != 1 || co >= sg.cout) return;
-  __shared__ float row[SHADOW_MAX_ROW];
-  const int rsz = sg.R * sg.S, n = sg.cin * rsz;
-  const float* src = w + peer * ps + sg.off + (int64_t)co * n;
-  for (int i = threadIdx.x; i < n; i += 256) row[i] = src[i];
-  __syncthreads();
-  bf16* dst = shadow + peer * shadow_ps + sg.wf_off + (int64_t)co * rsz * sg.cp_in;
-  for (int i = threadIdx.x; i < rsz * sg.cp_in; i += 256) {
-    const int rs = i / sg.cp_in, ci = i - rs * sg.cp_in;
-    const int tc = sg.colmap ? sg.colmap[ci] : (ci < sg.cin ? ci : -1);  // colmap here = engine -> torch
-    dst[i] = (bf16)(tc >= 0 ? row[tc * rsz + rs] : 0.f);
+  const int2 wk = work[blockIdx.x];
+  const Segment sg = segs[wk.x];
+  const int tid = threadIdx.x;
+  float* wp = w + peer * ps;
+  float* mp = mbuf + peer * ps;
+  const float* ap = anchor ? anchor + peer * ps : nullptr;
+  const float* cgp = cg ? cg + peer * ps : nullptr;
+  const float* clp = cl ? cl + peer * ps : nullptr;
+  float vdummy = 0.f;
+  if (sg.kind == 0) {
+    const int i = wk.y * 256 + tid;
+    if (!update || i >= sg.n) return;
+    const int64_t idx = sg.off + i;
+    float* gp = g + peer * ps + idx;
+    float wv = wp[idx], mv = mp[idx];
+    opt_update(o, *gp, wv, mv, vdummy, 1.f, 1.f, ap, cgp, clp, idx);
+    wp[idx] = wv;
+    mp[idx] = mv;
+    if (sg.zero_after) *gp = 0.f;
+    return;
   }
-}
-
-__global__ __launch_bounds__(256) void k_shadow_tr(const Segment* segs, bf16* shadow, int64_t shadow_ps, const int* active) {
-  const int peer = blockIdx.z;
-  if (active != nullptr && !active[peer]) return;
-  const Segment sg = segs[blockIdx.y];
-  if (sg.kind != 1) return;
-  const int rsz = sg.R * sg.S;
-  const int tci = (sg.cp_in + 31) / 32, tco = (sg.cp_out + 31) / 32;
-  const int t = blockIdx.x;
-  if (t >= tci * tco * rsz) return;
-  const int rs = t / (tci * tco), rem = t - rs * tci * tco;
-  const int ci0 = (rem / tco) * 32, co0 = (rem % tco) * 32;
-  __shared__ bf16 tile[32][34];
-  const bf16* wf = shadow + peer * shadow_ps + sg.wf_off;
-  bf16* wt = shadow + peer * shadow_ps + sg.wt_off;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  for (int k = ty; k < 32; k += 8) {
-    const int co = co0 + k, ci = ci0 + tx;
-    tile[k][tx] = (co < sg.cp_out && ci < sg.cp_in) ? wf[((int64_t)co * rsz + rs) * sg.cp_in + ci] : (bf16)0.f;
+  __shared__ float gl[GRAD_MAX_ROW];
+  __shared__ float wl[SHADOW_MAX_ROW];
+  const int co = wk.y;
+  const int rsz = sg.R * sg.S, n = sg.cin * rsz, nf = rsz * sg.cp_in, ldg = sg.cp_in + 1;
+  const int64_t row = sg.off + (int64_t)co * n;
+  if (update) {
+    float* grow = const_cast<float*>(gf) + peer * gf_ps + sg.wf_off + (int64_t)co * nf;
+    for (int j = tid; j < nf; j += 256) {
+      const int rs = j / sg.cp_in, ci = j - rs * sg.cp_in;
+      gl[rs * ldg + ci] = grow[j];
+      if (sg.zero_after) grow[j] = 0.f;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const int ct = i / rsz, rs = i - ct * rsz;
+      const int ce = sg.t2e ? sg.t2e[ct] : ct;
+      const int64_t idx = row + i;
+      float wv = wp[idx], mv = mp[idx];
+      opt_update(o, gl[rs * ldg + ce], wv, mv, vdummy, 1.f, 1.f, ap, cgp, clp, idx);
+      wp[idx] = wv;
+      mp[idx] = mv;
+      wl[i] = wv;
+    }
+  } else {
+    for (int i = tid; i < n; i += 256) wl[i] = wp[row + i];
   }
   __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int ci = ci0 + k, co = co0 + tx;
-    if (ci < sg.cp_in && co < sg.cp_out) wt[((int64_t)ci * rsz + rs) * sg.cp_out + co] = tile[tx][k];
+  bf16* dst = shadow + peer * shadow_ps + sg.wf_off + (int64_t)co * nf;
+  for (int j = tid; j < nf; j += 256) {
+    const int rs = j / sg.cp_in, ci = j - rs * sg.cp_in;
+    const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
+    dst[j] = (bf16)(tc >= 0 ? wl[tc * rsz + rs] : 0.f);
   }
 }
 
@@ -624,9 +628,10 @@ int cnn_xent(const bf16* logits, int64_t lg_ps, int Lp, int K, const int* labels
   hipLaunchKernelGGL(k_xent, dim3(1, peers), dim3(256), 0, (hipStream_t)s, logits, lg_ps, Lp, K, labels, B, nb, stats, confusion, dlogits, dl_ps);
   return ok();
 }
-int cnn_sgd_shadow(float* w, float* g, float* m, int64_t ps, const void* segs, int nseg, int max_seg, int kind, float lr, float momentum,
-                   float weight_decay, int nesterov, float mu, const float* anchor, const float* cg, const float* cl, int update, bf16* wf, bf16* wt,
-                   int64_t shadow_ps, const int* active, int peers, void* s) {
+// one fused optimizer + shadow pass (update = 0: shadow refresh only)
+int cnn_opt_step(float* w, float* g, float* m, int64_t ps, const float* gf, int64_t gf_ps, const void* segs, const void* work, int nwork, int kind,
+                 float lr, float momentum, float weight_decay, int nesterov, float mu, const float* anchor, const float* cg, const float* cl, int update,
+                 bf16* shadow, int64_t shadow_ps, const int* active, int peers, void* s) {
   OptParams o;
   o.kind = kind;
   o.lr = lr;
@@ -637,18 +642,9 @@ int cnn_sgd_shadow(float* w, float* g, float* m, int64_t ps, const void* segs, i
   o.momentum = momentum;
   o.nesterov = nesterov;
   o.mu = mu;
-  const int bq = (max_seg + 255) / 256;
-  const int bx = bq < 1 ? 1 : (bq > 1024 ? 1024 : bq);
-  if (update)
-    hipLaunchKernelGGL(k_sgd_shadow, dim3(bx, nseg, peers), dim3(256), 0, (hipStream_t)s, w, g, m, ps, (const Segment*)segs, o, anchor, cg, cl, update,
-                       wf, wt, shadow_ps, active);
-  return ok();
-}
-// rebuild every conv/fc shadow (max_cout = largest cout, max_tr_tiles = largest (cp_in/32)(cp_out/32)RS)
-int cnn_shadow_rebuild(const float* w, int64_t ps, const void* segs, int nseg, int max_cout, int max_tr_tiles, bf16* shadow, int64_t shadow_ps,
-                       const int* active, int peers, void* s) {
-  hipLaunchKernelGGL(k_shadow_fwd, dim3(max_cout, nseg, peers), dim3(256), 0, (hipStream_t)s, w, ps, (const Segment*)segs, shadow, shadow_ps, active);
-  hipLaunchKernelGGL(k_shadow_tr, dim3(max_tr_tiles, nseg, peers), dim3(256), 0, (hipStream_t)s, (const Segment*)segs, shadow, shadow_ps, active);
+  if (nwork < 1) return 1;
+  hipLaunchKernelGGL(k_opt_step, dim3(nwork, peers), dim3(256), 0, (hipStream_t)s, w, g, m, ps, gf, gf_ps, (const Segment*)segs, (const int2*)work, o,
+                     anchor, cg, cl, update, shadow, shadow_ps, active);
   return ok();
 }
 int cnn_segment_size() { return (int)sizeof(Segment); }

@@ -5,8 +5,9 @@
 // Layouts
 //   activations : [rows = n*H*W][Cp] bf16, Cp = round_up(C, 8) (padding channels are kept zero)
 //   conv weights: fp32 master in the flat parameter buffer, torch order [Cout][Cin][R][S];
-//                 bf16 shadows  Wf[Cout][R][S][Cp_in]  (forward / B operand, K-contiguous)
-//                               Wt[Cin ][R][S][Cp_out] (dgrad B operand, K-contiguous)
+//                 one bf16 shadow Wf[Cp_out][R][S][Cp_in] (forward B operand K-contiguous; the
+//                 dgrad reads it N-contiguous through the LDS transpose read);
+//                 gradient in the same Wf layout, fp32
 //   fc layers   : 1x1 convolutions on a 1x1 image (H = W = 1)
 #pragma once
 #include <stdint.h>
@@ -20,9 +21,9 @@ struct ConvGemmArgs {
   // geometry of the rows (M) this GEMM produces: FWD = output pixels, DGRAD = input pixels
   int out_h, out_w;
   int R, S, stride, pad;
-  // B operand: [Ncol][K] bf16, K = R*S*src_c
+  // B operand: the Wf shadow (FWD: [Ncol][K], K = R*S*src_c; DGRAD: [co][R*S][Ncol])
   const bf16* wt; int64_t wt_ps;
-  int ncol;          // output channel stride (Cp_out for FWD, Cp_in for DGRAD)
+  int ncol;          // output channel stride (Cp_out for FWD, Cp_in for DGRAD = Wf row length)
   int ncol_valid;    // logical channels (columns >= ncol_valid are written as 0)
   // epilogue
   bf16* out; int64_t out_ps;
@@ -40,9 +41,8 @@ struct WgradArgs {
   const bf16* x; int64_t x_ps;          // [n*H*W][x_c]
   int H, W, x_c, Ho, Wo, dy_c;
   int R, S, stride, pad;
-  int cout, cin;                        // logical
-  float* grad; int64_t grad_ps;         // torch layout [cout][cin][R][S] (fp32, accumulated)
-  const int* flat_perm;                 // optional: fc after NHWC flatten (see engine)
+  float* grad; int64_t grad_ps;         // Wf layout [dy_c][R][S][x_c] fp32
+  int accumulate;                       // 1: atomic add (required when splits > 1), 0: store
   int k_per_split;                      // rows of M per split (multiple of 64)
   const int* nbatch;
   int max_batch;

@@ -1,21 +1,25 @@
 // Implicit-GEMM convolutions on MFMA (gfx950, wave64), grouped over co-located peers.
 //
 // k_conv_gemm<MODE, BN>: C[M][Ncol] = A[M][K] · B[K][Ncol]
-//   MODE 0 (forward) : rows = output pixels, A = im2col(X) gathered on the fly, K = (r, s, ci)
+//   MODE 0 (forward) : rows = output pixels, A = im2col(X) gathered on the fly, K = (r, s, ci),
+//                      B = Wf[co][r][s][ci] rows (K-contiguous), staged [n][k] XOR-swizzled
 //   MODE 1 (dgrad)   : rows = input pixels,  A = dY gathered at ((h+pad-r)/st, (w+pad-s)/st) when
-//                      divisible (zero otherwise), K = (r, s, co); B = Wt[ci][r][s][co]
+//                      divisible (zero otherwise), K = (r, s, co); B[k][ci] = Wf[co][r][s][ci] is
+//                      N-contiguous, staged [k][n] and read as MFMA fragments with the gfx950 LDS
+//                      transpose read (ds_read_b64_tr_b16) — no transposed weight copy exists
 //   128 x BN tile, BK = 64, 256 threads = 4 waves (2 x 2), 16x16x32 bf16 MFMA, fp32 accumulate.
-//   Operands are register-staged into a double-buffered LDS image whose 16-byte chunks are
-//   XOR-swizzled (chunk ^ ((row >> 1) & 7)) so every ds_read_b128 fragment read is conflict-free;
-//   one barrier per K-step (the next tile's global loads are in flight during the MFMAs).
+//   A is register-staged into a double-buffered LDS image whose 16-byte chunks are XOR-swizzled
+//   (chunk ^ ((row >> 1) & 7)) so every ds_read_b128 fragment read is conflict-free; one barrier
+//   per K-step (the next tile's global loads are in flight during the MFMAs).
 //   Fused epilogue: + bias, + residual, ReLU, zeroed channel padding, BatchNorm sums (atomics).
 //   XCD-aware bijective block remap so tiles sharing an operand panel land on one L2.
 //
 // k_conv_wgrad<BM, BN>: dW[co][(r,s,ci)] = sum_m dY[m][co] · im2col(X)[m][(r,s,ci)]
 //   K = pixels (split over blockIdx.y), both operands staged [m][channels] as loaded and read
-//   as MFMA fragments with the gfx950 LDS transpose read (ds_read_b64_tr_b16); the epilogue
-//   scatters straight into the fp32 gradient in torch [Cout][Cin][R][S] order (atomic add over
-//   splits).
+//   as MFMA fragments with the transposed LDS read. The gradient is written in the GEMM's own
+//   (Wf) layout [cp_out][R][S][cp_in] fp32: 16 lanes of a row write 64 contiguous bytes (plain
+//   stores when the pixel dimension is not split, fp32 atomics otherwise). The optimizer kernel
+//   maps it to torch order through LDS (a torch-order scatter here cost ~0.45 ms per layer).
 #include <hip/hip_runtime.h>
 
 #include "conv.h"
@@ -46,9 +50,13 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((
 
 template <int MODE, int BN>
 __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
-  constexpr int NB = BN / 32;          // B rows per thread
+  constexpr int NB = BN / 32;          // B 16-byte chunks per thread
   constexpr int NF = BN / 32;          // n-fragments per wave (wave covers BN/2 columns)
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (CG_BM + BN) * CG_BK];
+  constexpr bool BT = MODE == 1;       // B staged [k][n] (N-contiguous source)
+  constexpr int LBT = BN + 8;          // padded row stride of the [k][n] image
+  constexpr int BSZ = BT ? CG_BK * LBT : BN * CG_BK;
+  constexpr int BUF = CG_BM * CG_BK + BSZ;
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
 
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
@@ -90,6 +98,9 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
   }
 
   const float inv_cpp = 1.f / (float)cpp, inv_S = 1.f / (float)a.S, inv_st = 1.f / (float)a.stride;
+  const float inv_srcc = 1.f / (float)a.src_c;
+  constexpr int BCH = BN / 8;          // MODE 1: 16-byte chunks per staged k row
+  const int bt_c = tid % BCH, bt_r = tid / BCH;
   uint4 ra[4], rb[NB];
   auto load = [&](int kt) {
     const int k = kt * CG_BK + cc * 8;
@@ -118,19 +129,49 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
       ok = ok && h >= 0 && w >= 0 && h < a.src_h && w < a.src_w;
       ra[i] = ok ? *reinterpret_cast<const uint4*>(src + (int64_t)(a_img[i] + h * a.src_w + w) * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
     }
+    if (!BT) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rb[i] = (kok && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < NB; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
+        rb[i] = (kok && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      // k row = (r, s, co): Wf[co][rs][n0 + 8 * chunk ..] (ncol = Wf row length = cp_in)
+      const int n = n0 + bt_c * 8;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int kk = kt * CG_BK + bt_r + (256 / BCH) * i;
+        bool ok = kk < Ktot && n < a.ncol;
+        int64_t off = 0;
+        if (ok) {
+          const int rs = fdiv(kk, a.src_c, inv_srcc), co = kk - rs * a.src_c;
+          off = ((int64_t)co * (a.R * a.S) + rs) * a.ncol + n;
+        }
+        rb[i] = ok ? *reinterpret_cast<const uint4*>(wt + off) : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto store = [&](int buf) {
-    bf16* As = lds + buf * (CG_BM + BN) * CG_BK;
+    bf16* As = lds + buf * BUF;
     bf16* Bs = As + CG_BM * CG_BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(As + swz((tid >> 3) + 32 * i, cc)) = ra[i];
+    if (!BT) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + swz((tid >> 3) + 32 * i, cc)) = rb[i];
+      for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + swz((tid >> 3) + 32 * i, cc)) = rb[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + (bt_r + (256 / BCH) * i) * LBT + bt_c * 8) = rb[i];
+    }
+  };
+  // transposed fragment (MODE 1 B): lane i of group g gets column (col0 + i), rows k0 + 8g + 0..7
+  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  auto frag_t = [&](const bf16* base, int col0, int k0) -> bf16x8 {
+    const bf16* p0 = base + (k0 + 8 * tg + tq) * LBT + col0 + 4 * tp;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * LBT));
+    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, both);
   };
 
   f32x4 acc[4][NF];
@@ -145,7 +186,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load(kt + 1);
-    const bf16* As = lds + cur * (CG_BM + BN) * CG_BK;
+    const bf16* As = lds + cur * BUF;
     const bf16* Bs = As + CG_BM * CG_BK;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -154,7 +195,8 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+      for (int j = 0; j < NF; ++j)
+        bfr[j] = BT ? frag_t(Bs, wc * (BN / 2) + j * 16, h * 32) : ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -324,22 +366,22 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
     cur ^= 1;
   }
 
+  // Wf-layout gradient [dy_c][ncol_tot]: lanes 0..15 of a row group write 16 consecutive floats
   float* grad = a.grad + peer * a.grad_ps;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
     if (n >= ncol_tot) continue;
-    const int rs = n / a.x_c, ci = n - rs * a.x_c;
-    if (a.flat_perm == nullptr && ci >= a.cin) continue;
-    const int r = rs / a.S, s = rs - r * a.S;
-    const int cidx = a.flat_perm ? a.flat_perm[ci] : ci;
-    if (cidx < 0) continue;  // padding channel of a flattened input
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int co = co0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-        if (co < a.cout) atomicAdd(grad + ((int64_t)(co * a.cin + cidx) * a.R + r) * a.S + s, acc[i][j][e]);
+        if (co < a.dy_c) {
+          float* dst = grad + (int64_t)co * ncol_tot + n;
+          if (a.accumulate) atomicAdd(dst, acc[i][j][e]);
+          else *dst = acc[i][j][e];
+        }
       }
     }
   }
@@ -374,6 +416,7 @@ extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) { retur
 extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, void* stream) {
   const WgradArgs& a = *pa;
   if ((a.x_c & 7) || (a.dy_c & 7) || (a.k_per_split & 63) || peers < 1 || splits < 1) return 1;
+  if (splits > 1 && !a.accumulate) return 1;  // split-K partial sums must be added
   const int ncol = a.R * a.S * a.x_c;
   const bool wm = a.dy_c > 64, wn = ncol > 64;
   const int BM = wm ? 128 : 64, BN = wn ? 128 : 64;

@@ -8,8 +8,10 @@ gets a slot in stacked buffers and every kernel covers all peers through ``grid.
   mean | BN running var]`` — the peers' ``nn.Module`` parameters *and* BN buffers are views into
   their row (wire format / ``state_dict`` unchanged; FedAvg over the stacked rows averages BN
   statistics too, like the reference's ``state_dict`` averaging);
-* activations are NHWC bf16 (channels padded to a multiple of 8), weights get two bf16 shadows
-  (forward ``[Cout][R][S][Cin]`` and dgrad ``[Cin][R][S][Cout]``) refreshed by the fused SGD kernel;
+* activations are NHWC bf16 (channels padded to a multiple of 8); each conv/fc weight has one bf16
+  shadow ``Wf[Cout][R][S][Cin]`` (the forward B operand; the dgrad reads it N-contiguous through the
+  LDS transpose read) and an fp32 gradient in the same layout, both handled by one fused
+  optimizer kernel that maps between the GEMM layout and the torch-order master row in LDS;
 * a train step is: input gather/convert → per conv: implicit-GEMM MFMA conv with BN partial sums
   fused in its epilogue → BN finalize → BN apply (+residual) + ReLU → … → avg-pool → fc →
   log-softmax/NLL (+dlogits) → backward (BN reduce/finalize/apply, dgrad conv with the residual
@@ -52,8 +54,8 @@ class WgradArgs(ctypes.Structure):
     _fields_ = [
         ("dy", c_void_p), ("dy_ps", c_int64), ("x", c_void_p), ("x_ps", c_int64),
         ("H", c_int), ("W", c_int), ("x_c", c_int), ("Ho", c_int), ("Wo", c_int), ("dy_c", c_int),
-        ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int), ("cout", c_int), ("cin", c_int),
-        ("grad", c_void_p), ("grad_ps", c_int64), ("flat_perm", c_void_p), ("k_per_split", c_int),
+        ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int),
+        ("grad", c_void_p), ("grad_ps", c_int64), ("accumulate", c_int), ("k_per_split", c_int),
         ("nbatch", c_void_p), ("max_batch", c_int),
     ]
 
@@ -61,7 +63,8 @@ class WgradArgs(ctypes.Structure):
 class Segment(ctypes.Structure):
     _fields_ = [
         ("off", c_int64), ("n", c_int), ("kind", c_int), ("cout", c_int), ("cin", c_int), ("R", c_int), ("S", c_int),
-        ("cp_in", c_int), ("cp_out", c_int), ("wf_off", c_int64), ("wt_off", c_int64), ("colmap", c_void_p),
+        ("cp_in", c_int), ("cp_out", c_int), ("zero_after", c_int), ("pad_", c_int), ("wf_off", c_int64),
+        ("e2t", c_void_p), ("t2e", c_void_p),
     ]
 
 
@@ -80,9 +83,9 @@ _SIGS = {
     "cnn_maxpool2": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_avgpool": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_xent": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
-    "cnn_sgd_shadow": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
+    "cnn_opt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_float,
+                             c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "cnn_segment_size": (c_int, []),
-    "cnn_shadow_rebuild": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
 }
 
 
@@ -223,13 +226,12 @@ class CNNGroup:
         self.bn_total = o
         self.numel = self.n_params + 2 * self.bn_total
         self.S = (self.numel + 63) // 64 * 64
-        # shadows
-        self.shadow_off: Dict[str, Tuple[int, int]] = {}
+        # Wf shadows (bf16) and Wf-layout gradients (fp32) share offsets
+        self.shadow_off: Dict[str, int] = {}
         so = 0
         for c in self.convs:
-            nf = c.cp_out * c.R * c.S * c.cp_in
-            self.shadow_off[c.name] = (so, so + nf)
-            so += 2 * nf + 64
+            self.shadow_off[c.name] = so
+            so += c.cp_out * c.R * c.S * c.cp_in + 64
         self.shadow_numel = so
 
     def _off(self, p) -> int:
@@ -295,6 +297,7 @@ class CNNGroup:
         self.grad = torch.zeros_like(params)
         self.mom = torch.zeros_like(params)
         self.shadow = torch.zeros(capacity, self.shadow_numel, dtype=torch.bfloat16, device=dev)
+        self.gradf = torch.zeros(capacity, self.shadow_numel, dtype=torch.float32, device=dev)
         self.capacity = capacity
         for slot, h in self.handles.items():
             h.retarget()
@@ -304,33 +307,35 @@ class CNNGroup:
         self._build_segments()
 
     def _build_segments(self) -> None:
-        segs = []
+        segs, work = [], []
         self._keep_colmaps = []
         for c in self.convs:
-            wf, wt = self.shadow_off[c.name]
-            cm = 0
-            if c.colmap is not None:  # the shadow kernels map engine channel -> torch input column
+            e2t = t2e = 0
+            if c.colmap is not None:  # fc after the NHWC flatten: engine channel <-> torch column maps
                 inv = np.full(c.cp_in, -1, dtype=np.int32)
                 inv[c.colmap] = np.arange(len(c.colmap), dtype=np.int32)
-                t = torch.from_numpy(inv).to(self.device)
-                self._keep_colmaps.append(t)
-                cm = t.data_ptr()
+                te, tt = torch.from_numpy(inv).to(self.device), torch.from_numpy(np.asarray(c.colmap, dtype=np.int32)).to(self.device)
+                self._keep_colmaps += [te, tt]
+                e2t, t2e = te.data_ptr(), tt.data_ptr()
             cin_t = getattr(c, "cin_torch", c.cin)
-            segs.append(Segment(self._off(c.weight), c.weight.numel(), 1, c.cout, cin_t, c.R, c.S, c.cp_in, c.cp_out, wf, wt, cm))
+            if cin_t * c.R * c.S > 4608 or (c.cp_in + 1) * c.R * c.S > 4624:
+                raise ValueError(f"conv layer {c.name} too wide for the optimizer kernel (cin * R * S > 4608)")
+            accumulate = int(self._wgrad_split(c)[1] > 1)
+            work += [(len(segs), co) for co in range(c.cout)]
+            segs.append(Segment(self._off(c.weight), c.weight.numel(), 1, c.cout, cin_t, c.R, c.S, c.cp_in, c.cp_out, accumulate, 0, self.shadow_off[c.name], e2t, t2e))
             if c.bias is not None:
-                segs.append(Segment(self._off(c.bias), c.bias.numel(), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+                work += [(len(segs), k) for k in range((c.bias.numel() + 255) // 256)]
+                segs.append(Segment(self._off(c.bias), c.bias.numel(), 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0))
         for bn in self.bns:
             for p in (bn.module.weight, bn.module.bias):
-                segs.append(Segment(self._off(p), p.numel(), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+                work += [(len(segs), k) for k in range((p.numel() + 255) // 256)]
+                segs.append(Segment(self._off(p), p.numel(), 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0))
         arr = (Segment * len(segs))(*segs)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self.segs = raw.to(self.device)
         self.nseg = len(segs)
-        self.max_seg = max(s.n for s in segs)
-        self.max_cout = max(c.cout for c in self.convs)
-        self.max_tr_tiles = max(((c.cp_in + 31) // 32) * ((c.cp_out + 31) // 32) * c.R * c.S for c in self.convs)
-        if max(getattr(c, "cin_torch", c.cin) * c.R * c.S for c in self.convs) > 4608:
-            raise ValueError("conv layer too wide for the shadow kernel (cin * R * S > 4608)")
+        self.work = torch.tensor(work, dtype=torch.int32).reshape(-1, 2).to(self.device)
+        self.nwork = len(work)
 
     def act(self, name: str, rows: int, cp: int, dtype=torch.bfloat16) -> torch.Tensor:
         t = self._acts.get(name)
@@ -410,7 +415,7 @@ class CNNGroup:
 
     def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None) -> None:
         lib, P = _lib(), self.capacity
-        shadow_f, shadow_t = self.shadow_off[L.name]
+        shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
         if mode == 0:
             a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.h, L.w, L.cp_in
@@ -420,7 +425,7 @@ class CNNGroup:
         else:
             a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.ho, L.wo, L.cp_out
             a.out_h, a.out_w = L.h, L.w
-            a.wt = self.shadow.data_ptr() + 2 * shadow_t
+            a.wt = self.shadow.data_ptr() + 2 * shadow_f
             a.ncol, a.ncol_valid = L.cp_in, (L.cin if L.colmap is None else L.cp_in)
         a.src_ps, a.wt_ps = src.shape[1], self.shadow.shape[1]
         a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, L.pad
@@ -435,33 +440,26 @@ class CNNGroup:
         a.nbatch, a.max_batch = self.nb.data_ptr(), self.B
         _chk(lib.conv_gemm_launch(mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
+    def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
+        """(pixels per split, splits): split the pixel (K) dimension only until ~4 tiles per CU exist."""
+        M = self.B * L.ho * L.wo
+        ncol = L.R * L.S * L.cp_in
+        tiles = ((L.cp_out + 127) // 128) * ((ncol + 127) // 128)
+        want = max(1, (4 * 256) // max(1, tiles * self.capacity))
+        k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
+        return k_per, (M + k_per - 1) // k_per
+
     def wgrad(self, L: ConvL, dy: torch.Tensor, x: torch.Tensor) -> None:
         lib, P = _lib(), self.capacity
         a = WgradArgs()
         a.dy, a.dy_ps, a.x, a.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
         a.H, a.W, a.x_c, a.Ho, a.Wo, a.dy_c = L.h, L.w, L.cp_in, L.ho, L.wo, L.cp_out
-        a.R, a.S, a.stride, a.pad, a.cout, a.cin = L.R, L.S, L.stride, L.pad, L.cout, getattr(L, "cin_torch", L.cin)
-        a.grad, a.grad_ps = self.grad.data_ptr() + 4 * self._off(L.weight), self.grad.shape[1]
-        if L.colmap is not None:
-            a.flat_perm = self._inv_colmap(L).data_ptr()
-        M = self.B * L.ho * L.wo
-        ncol = L.R * L.S * L.cp_in
-        tiles = ((L.cp_out + 127) // 128) * ((ncol + 127) // 128)
-        want = max(1, (4 * 256) // max(1, tiles * P))
-        k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
-        splits = (M + k_per - 1) // k_per
+        a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, L.pad
+        a.grad, a.grad_ps = self.gradf.data_ptr() + 4 * self.shadow_off[L.name], self.gradf.shape[1]
+        k_per, splits = self._wgrad_split(L)
+        a.accumulate = int(splits > 1)  # must match the segment's zero_after (the optimizer re-zeroes)
         a.k_per_split, a.nbatch, a.max_batch = k_per, self.nb.data_ptr(), self.B
         _chk(lib.conv_wgrad_launch(ctypes.byref(a), P, splits, self._stream()), f"wgrad {L.name}")
-
-    def _inv_colmap(self, L: ConvL) -> torch.Tensor:
-        key = f"_invcol_{L.name}"
-        t = getattr(self, key, None)
-        if t is None:
-            inv = np.full(L.cp_in, -1, dtype=np.int32)  # -1: padding channel of the flattened tensor
-            inv[L.colmap] = np.arange(len(L.colmap), dtype=np.int32)
-            t = torch.from_numpy(inv).to(self.device)
-            setattr(self, key, t)
-        return t
 
     def bn_fin(self, bn: BNL, stats: torch.Tensor, rows: int, hw: int, train: bool) -> None:
         lib, P = _lib(), self.capacity
@@ -687,7 +685,6 @@ class CNNGroup:
 
     def _train_step(self, offset: int) -> None:
         x0 = self._prep(True, offset)
-        self.grad.zero_()
         if self.arch == "resnet18":
             logits = self._forward_resnet(x0, True)
             self._xent(logits, True)
@@ -699,16 +696,14 @@ class CNNGroup:
         self._optimizer(update=True)
 
     def _optimizer(self, update: bool) -> None:
+        """SGD on the torch-order master rows + bf16 Wf shadow rows, one fused launch (update=False:
+        shadow refresh only). Atomically accumulated gradients are re-zeroed as they are consumed."""
         o = self._opt
-        lib = _lib()
-        active = self.nb.data_ptr() if update else None
-        if update:
-            _chk(lib.cnn_sgd_shadow(self.params.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg,
-                                    self.max_seg, o["kind"], o["lr"], o["momentum"], o["weight_decay"], o["nesterov"], o["mu"], _p(o.get("anchor")),
-                                    _p(o.get("cg")), _p(o.get("cl")), 1, self.shadow.data_ptr(), self.shadow.data_ptr(), self.shadow.shape[1],
-                                    active, self.capacity, self._stream()), "sgd")
-        _chk(lib.cnn_shadow_rebuild(self.params.data_ptr(), self.params.shape[1], self.segs.data_ptr(), self.nseg, self.max_cout, self.max_tr_tiles,
-                                    self.shadow.data_ptr(), self.shadow.shape[1], active, self.capacity, self._stream()), "shadow_rebuild")
+        _chk(_lib().cnn_opt_step(self.params.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(), self.params.shape[1], self.gradf.data_ptr(),
+                                 self.gradf.shape[1], self.segs.data_ptr(), self.work.data_ptr(), self.nwork, o["kind"], o["lr"], o["momentum"],
+                                 o["weight_decay"], o["nesterov"], o["mu"], _p(o.get("anchor")), _p(o.get("cg")), _p(o.get("cl")), int(update),
+                                 self.shadow.data_ptr(), self.shadow.shape[1], self.nb.data_ptr() if update else None, self.capacity, self._stream()),
+             "optimizer")
 
     def _shadow_sync(self) -> None:
         saved = getattr(self, "_opt", None)

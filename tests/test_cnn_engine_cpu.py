@@ -19,13 +19,22 @@ def test_group_describes_model(cls):
     assert g.n_params == sum(p.numel() for p in m.parameters())
     n_bn = sum(mod.num_features for mod in m.modules() if isinstance(mod, torch.nn.BatchNorm2d))
     assert g.bn_total == n_bn and g.numel == g.n_params + 2 * n_bn
-    assert ctypes.sizeof(Segment) == 64
+    assert ctypes.sizeof(Segment) == 72
     # every trainable tensor is covered by exactly one optimizer segment
     raw = g.segs.numpy().tobytes()
     segs = (Segment * g.nseg).from_buffer_copy(raw)
     covered = sorted((s.off, s.off + s.n) for s in segs)
     assert covered[0][0] == 0 and covered[-1][1] == g.n_params
     assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+    # the optimizer work table: one item per weight row (kind 1) / per 256-element chunk (kind 0), nothing empty
+    work = g.work.numpy()
+    assert g.nwork == len(work)
+    for si, s in enumerate(segs):
+        items = sorted(int(x) for x in work[work[:, 0] == si][:, 1])
+        assert items == list(range(s.cout if s.kind == 1 else (s.n + 255) // 256))
+    # Wf-layout gradient/shadow regions do not overlap
+    offs = sorted((g.shadow_off[c.name], g.shadow_off[c.name] + c.cp_out * c.R * c.S * c.cp_in) for c in g.convs)
+    assert all(a[1] <= b[0] for a, b in zip(offs, offs[1:])) and offs[-1][1] <= g.shadow_numel
     assert g.fit_gang is not None and g.eval_gang is not None
 
 

@@ -41,8 +41,6 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
     xn = _nhwc_pad(x, cpi).reshape(1, -1).contiguous()
     wf = torch.zeros(cpo, k, k, cpi, device=dev, dtype=torch.bfloat16)
     wf[:cout, :, :, :cin] = w.permute(0, 2, 3, 1).to(torch.bfloat16)
-    wt = torch.zeros(cpi, k, k, cpo, device=dev, dtype=torch.bfloat16)
-    wt[:cin, :, :, :cout] = w.permute(1, 2, 3, 0).to(torch.bfloat16)
     y = torch.zeros(1, n * ho * ho * cpo, device=dev, dtype=torch.bfloat16)
     stats = torch.zeros(1, lib.conv_gemm_stats_rows(n, ho, ho) * 2 * cpo, device=dev)
     a = ConvGemmArgs()
@@ -67,7 +65,7 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
     b = ConvGemmArgs()
     b.src, b.src_h, b.src_w, b.src_c = dyn.data_ptr(), ho, ho, cpo
     b.out_h, b.out_w, b.R, b.S, b.stride, b.pad = h, h, k, k, stride, pad
-    b.wt, b.ncol, b.ncol_valid = wt.data_ptr(), cpi, cin
+    b.wt, b.ncol, b.ncol_valid = wf.data_ptr(), cpi, cin  # dgrad reads the same Wf shadow (transposed LDS reads)
     b.out, b.max_batch = dx.data_ptr(), n
     assert lib.conv_gemm_launch(1, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
@@ -75,18 +73,22 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
 
     # wgrad
     dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
-    grad = torch.zeros(1, cout * cin * k * k, device=dev)
-    c = WgradArgs()
-    c.dy, c.x = dyn.data_ptr(), xn.data_ptr()
-    c.H, c.W, c.x_c, c.Ho, c.Wo, c.dy_c = h, h, cpi, ho, ho, cpo
-    c.R, c.S, c.stride, c.pad, c.cout, c.cin = k, k, stride, pad, cout, cin
-    c.grad, c.k_per_split, c.max_batch = grad.data_ptr(), 128, n
     M = n * ho * ho
-    assert lib.conv_wgrad_launch(ctypes.byref(c), 1, (M + 127) // 128, torch.cuda.current_stream().cuda_stream) == 0
-    torch.cuda.synchronize()
-    g = grad.view(cout, cin, k, k)
-    err = (g - dw_ref).norm() / dw_ref.norm()
-    assert err < 2e-2, float(err)
+    for k_per in (128, (M + 63) // 64 * 64):  # split-K (atomics) and one split (plain stores)
+        splits = (M + k_per - 1) // k_per
+        grad = torch.zeros(1, cpo * k * k * cpi, device=dev)  # Wf layout [cp_out][R][S][cp_in]
+        c = WgradArgs()
+        c.dy, c.x = dyn.data_ptr(), xn.data_ptr()
+        c.H, c.W, c.x_c, c.Ho, c.Wo, c.dy_c = h, h, cpi, ho, ho, cpo
+        c.R, c.S, c.stride, c.pad = k, k, stride, pad
+        c.grad, c.accumulate, c.k_per_split, c.max_batch = grad.data_ptr(), int(splits > 1), k_per, n
+        assert lib.conv_wgrad_launch(ctypes.byref(c), 1, splits, torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        gw = grad.view(cpo, k, k, cpi)
+        g = gw[:cout, :, :, :cin].permute(0, 3, 1, 2)
+        err = (g - dw_ref).norm() / dw_ref.norm()
+        assert err < 2e-2, (k_per, float(err))
+        assert gw[cout:].abs().max().item() == 0 if cpo > cout else True
 
 
 def _make_learners(model_fn, n_peers, n_train, n_test, batch, lr, momentum=0.0, wd=0.0):
