@@ -137,6 +137,8 @@ def main() -> None:
 
     fed.round_hooks.append(hook)
     t_start = time.perf_counter()
+    if args.warmup == 0:  # time from the start (includes graph capture)
+        marks["t0"] = t_start
     if rank == 0:
         nodes[0].set_start_learning(rounds=total, epochs=1)
     wait_to_finish(nodes, timeout=7200)

@@ -7,7 +7,8 @@
 //                      divisible (zero otherwise), K = (r, s, co); B[k][ci] = Wf[co][r][s][ci] is
 //                      N-contiguous, staged [k][n] and read as MFMA fragments with the gfx950 LDS
 //                      transpose read (ds_read_b64_tr_b16) — no transposed weight copy exists
-//   128 x BN tile, BK = 64, 256 threads = 4 waves (2 x 2), 16x16x32 bf16 MFMA, fp32 accumulate.
+//   128 x BN tiles (2 x 2 waves, each 64 rows), BK = 64, 256 threads, 16x16x32 bf16 MFMA, fp32
+//   accumulate.
 //   A is register-staged into a double-buffered LDS image whose 16-byte chunks are XOR-swizzled
 //   (chunk ^ ((row >> 1) & 7)) so every ds_read_b128 fragment read is conflict-free; one barrier
 //   per K-step (the next tile's global loads are in flight during the MFMAs).
@@ -15,7 +16,7 @@
 //   XCD-aware bijective block remap so tiles sharing an operand panel land on one L2.
 //
 // k_conv_wgrad<BM, BN>: dW[co][(r,s,ci)] = sum_m dY[m][co] · im2col(X)[m][(r,s,ci)]
-//   K = pixels (split over blockIdx.y), both operands staged [m][channels] as loaded and read
+//   K = pixels (split over workgroups), both operands staged [m][channels] as loaded and read
 //   as MFMA fragments with the transposed LDS read. The gradient is written in the GEMM's own
 //   (Wf) layout [cp_out][R][S][cp_in] fp32: 16 lanes of a row write 64 contiguous bytes (plain
 //   stores when the pixel dimension is not split, fp32 atomics otherwise). The optimizer kernel
@@ -24,7 +25,6 @@
 
 #include "conv.h"
 
-#define CG_BM 128
 #define CG_BK 64
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -48,23 +48,60 @@ __device__ __forceinline__ int fdiv(int x, int d, float inv) {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
+// [k][W] images read with ds_read_b64_tr_b16 (W = 64 or 128 bf16, unpadded rows): 8-byte granules
+// XOR-permuted by a row function so that the 32 lanes of a half-wave (rows 8g+q, g = 0/1, q = 0..3,
+// four granules each) hit 32 distinct bank granules; the permutation is a multiple of 4 granules,
+// so a lane's 4 elements and a writer's 16-byte chunk stay contiguous (measured: ~1-1.6 bank
+// conflicts per LDS instruction with a +8-element row pad instead).
+template <int W>
+__device__ __forceinline__ int trf(int row) {
+  if (W == 128) return ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+  return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 2;
+}
+template <int W>
+__device__ __forceinline__ int tr_off(int row, int col) {  // col multiple of 4
+  return row * W + ((((col >> 2) ^ trf<W>(row))) << 2);
+}
+// transposed MFMA fragment from a [k][W] image: lane i of group g gets column (col0 + i), rows k0 + 8g + 0..7
+template <int W>
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = k0 + 8 * g + q;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<W>(r0, col0 + 4 * p)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<W>(r0 + 4, col0 + 4 * p)));
+  // whole-vector bit cast (an element-wise short->bf16 cast miscompiles into lane-duplicating perms)
+  const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, both);
+}
+
 template <int MODE, int BN>
-__global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
+__global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
+  // MODE 0 forward, MODE 1 dgrad (all taps), MODE 2 strided dgrad by output parity class
+  // (blockIdx.y = class (ph, pw): rows are the dX pixels (2hh+ph, 2ww+pw), K walks only the taps
+  // r = r0 + 2i, s = s0 + 2j that reach them — a plain stride-2 dgrad multiplies zeros for 3 of
+  // every 4 (pixel, tap) pairs)
+  constexpr int BM = 128;
+  constexpr int AR = BM / 32;          // A rows (16-byte chunks) per thread
   constexpr int NB = BN / 32;          // B 16-byte chunks per thread
-  constexpr int NF = BN / 32;          // n-fragments per wave (wave covers BN/2 columns)
-  constexpr bool BT = MODE == 1;       // B staged [k][n] (N-contiguous source)
-  constexpr int LBT = BN + 8;          // padded row stride of the [k][n] image
-  constexpr int BSZ = BT ? CG_BK * LBT : BN * CG_BK;
-  constexpr int BUF = CG_BM * CG_BK + BSZ;
+  constexpr int NF = BN / 32;          // n-fragments per wave (2 x 2 waves, each 64 x BN/2)
+  constexpr bool BT = MODE != 0;       // B staged [k][n] (N-contiguous source)
+  constexpr int BUF = BM * CG_BK + BN * CG_BK;
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
 
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
-  const int hw = a.out_h * a.out_w;
+  // row geometry (MODE 2: the parity class's sub-grid of dX)
+  const int ph = MODE == 2 ? (int)(blockIdx.y >> 1) : 0, pw = MODE == 2 ? (int)(blockIdx.y & 1) : 0;
+  const int rh = MODE == 2 ? (a.out_h - ph + 1) >> 1 : a.out_h;
+  const int rw = MODE == 2 ? (a.out_w - pw + 1) >> 1 : a.out_w;
+  const int r0 = MODE == 2 ? (ph + a.pad) & 1 : 0, s0 = MODE == 2 ? (pw + a.pad) & 1 : 0;
+  const int tR = MODE == 2 ? (a.R - r0 + 1) >> 1 : a.R;  // taps walked along r / s
+  const int tS = MODE == 2 ? (a.S - s0 + 1) >> 1 : a.S;
+  const int hw = rh * rw;
   const int M = nb * hw;
   const int wgid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tn = wgid % tiles_n, tm = wgid / tiles_n;
-  const int m0 = tm * CG_BM, n0 = tn * BN;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
@@ -72,122 +109,153 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
-  const int Ktot = a.R * a.S * a.src_c;
+  const int Ktot = (tR > 0 && tS > 0) ? tR * tS * a.src_c : 0;  // 0: a parity class no tap reaches (zeros + resid)
   const int nk = (Ktot + CG_BK - 1) / CG_BK;
   const int cc = tid & 7;            // this thread's 16-byte chunk within a K-step
   const int cpp = a.src_c >> 3;      // chunks per pixel
 
-  // per-thread A rows (fixed for the whole K loop)
-  int a_img[4], a_bh[4], a_bw[4];
-  bool a_ok[4];
+  // per-thread A rows (fixed for the whole K loop): a_bh/a_bw = source coordinate of tap (0, 0)
+  int a_img[AR], a_bh[AR], a_bw[AR];
+  bool a_ok[AR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < AR; ++i) {
     const int m = m0 + (tid >> 3) + 32 * i;
     a_ok[i] = m < M;
     const int mm = a_ok[i] ? m : 0;
     const int img = mm / hw, rem = mm - img * hw;
-    const int oh = rem / a.out_w, ow = rem - oh * a.out_w;
+    const int oh = rem / rw, ow = rem - oh * rw;
     a_img[i] = img * a.src_h * a.src_w;
     if (MODE == 0) {
       a_bh[i] = oh * a.stride - a.pad;
       a_bw[i] = ow * a.stride - a.pad;
-    } else {
+    } else if (MODE == 1) {
       a_bh[i] = oh + a.pad;
       a_bw[i] = ow + a.pad;
+    } else {  // dY row of tap (r0, s0) for dX pixel (2oh+ph, 2ow+pw); tap i steps back one dY row
+      a_bh[i] = oh + ((ph + a.pad - r0) >> 1);
+      a_bw[i] = ow + ((pw + a.pad - s0) >> 1);
     }
   }
 
-  const float inv_cpp = 1.f / (float)cpp, inv_S = 1.f / (float)a.S, inv_st = 1.f / (float)a.stride;
-  const float inv_srcc = 1.f / (float)a.src_c;
-  constexpr int BCH = BN / 8;          // MODE 1: 16-byte chunks per staged k row
+  // K-walk state, advanced incrementally (the im2col index math was ~6-22 VALU per MFMA with a
+  // division-based decomposition per K-step): this thread's A chunk is q8 = kt * 8 + cc of
+  // (tap r, tap s, c8); B rows (MODE 1/2) are (tap, co) pairs
+  const float inv_st = 1.f / (float)a.stride;
+  int ar = 0, as_ = 0, ac8 = cc;
+  while (ac8 >= cpp) {
+    ac8 -= cpp;
+    if (++as_ == tS) { as_ = 0; ++ar; }
+  }
+  int a_pix[AR];  // MODE 0: pixel index of tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < AR; ++i) a_pix[i] = a_img[i] + a_bh[i] * a.src_w + a_bw[i];
+  constexpr int BCH = BN / 8;          // BT: 16-byte chunks per staged k row
   const int bt_c = tid % BCH, bt_r = tid / BCH;
-  uint4 ra[4], rb[NB];
+  int b_t[NB], b_co[NB];
+  if (BT) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int kk = bt_r + (256 / BCH) * i;
+      b_t[i] = kk / a.src_c;
+      b_co[i] = kk - b_t[i] * a.src_c;
+    }
+  }
+  const int RS = a.R * a.S, TT = tR * tS;
+  uint4 ra[AR], rb[NB];
   auto load = [&](int kt) {
     const int k = kt * CG_BK + cc * 8;
-    const bool kok = k < Ktot;
-    int r = 0, s = 0, c8 = 0;
-    if (kok) {
-      const int q8 = k >> 3;
-      const int rs = fdiv(q8, cpp, inv_cpp);
-      c8 = q8 - rs * cpp;
-      r = fdiv(rs, a.S, inv_S);
-      s = rs - r * a.S;
-    }
+    const bool kok = ar < tR;
+    const int r = ar, s = as_, c8 = ac8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < AR; ++i) {
       bool ok = kok && a_ok[i];
-      int h, w;
+      int pix;
       if (MODE == 0) {
-        h = a_bh[i] + r;
-        w = a_bw[i] + s;
+        ok = ok && (unsigned)(a_bh[i] + r) < (unsigned)a.src_h && (unsigned)(a_bw[i] + s) < (unsigned)a.src_w;
+        pix = a_pix[i] + r * a.src_w + s;
+      } else if (MODE == 2) {
+        const int h = a_bh[i] - r, w = a_bw[i] - s;
+        ok = ok && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)a.src_w;
+        pix = a_img[i] + h * a.src_w + w;
       } else {
         const int th = a_bh[i] - r, tw = a_bw[i] - s;
-        h = th >= 0 ? fdiv(th, a.stride, inv_st) : -1;
-        w = tw >= 0 ? fdiv(tw, a.stride, inv_st) : -1;
-        ok = ok && th >= 0 && tw >= 0 && h * a.stride == th && w * a.stride == tw;
+        int h, w;
+        if (a.stride == 1) {
+          h = th;
+          w = tw;
+        } else {
+          h = th >= 0 ? fdiv(th, a.stride, inv_st) : -1;
+          w = tw >= 0 ? fdiv(tw, a.stride, inv_st) : -1;
+          ok = ok && h * a.stride == th && w * a.stride == tw;
+        }
+        ok = ok && th >= 0 && tw >= 0 && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)a.src_w;
+        pix = a_img[i] + h * a.src_w + w;
       }
-      ok = ok && h >= 0 && w >= 0 && h < a.src_h && w < a.src_w;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(src + (int64_t)(a_img[i] + h * a.src_w + w) * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
+    }
+    // advance the A chunk by one K-step (8 chunks)
+    ac8 += 8;
+    while (ac8 >= cpp) {
+      ac8 -= cpp;
+      if (++as_ == tS) { as_ = 0; ++ar; }
     }
     if (!BT) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int n = n0 + (tid >> 3) + 32 * i;
-        rb[i] = (kok && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
+        rb[i] = (k < Ktot && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
       }
     } else {
-      // k row = (r, s, co): Wf[co][rs][n0 + 8 * chunk ..] (ncol = Wf row length = cp_in)
+      // k row = (tap, co): Wf[co][r][s][n0 + 8 * chunk ..] (ncol = Wf row length = cp_in)
       const int n = n0 + bt_c * 8;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int kk = kt * CG_BK + bt_r + (256 / BCH) * i;
-        bool ok = kk < Ktot && n < a.ncol;
-        int64_t off = 0;
-        if (ok) {
-          const int rs = fdiv(kk, a.src_c, inv_srcc), co = kk - rs * a.src_c;
-          off = ((int64_t)co * (a.R * a.S) + rs) * a.ncol + n;
+        const bool ok = b_t[i] < TT && n < a.ncol;
+        int rs = b_t[i];
+        if (MODE == 2) {
+          const int ti = tS == 1 ? b_t[i] : b_t[i] / tS, tj = b_t[i] - ti * tS;
+          rs = (r0 + 2 * ti) * a.S + s0 + 2 * tj;
         }
-        rb[i] = ok ? *reinterpret_cast<const uint4*>(wt + off) : make_uint4(0, 0, 0, 0);
+        rb[i] = ok ? *reinterpret_cast<const uint4*>(wt + (b_co[i] * RS + rs) * a.ncol + n) : make_uint4(0, 0, 0, 0);
+        b_co[i] += CG_BK;
+        while (b_co[i] >= a.src_c) {
+          b_co[i] -= a.src_c;
+          ++b_t[i];
+        }
       }
     }
   };
   auto store = [&](int buf) {
     bf16* As = lds + buf * BUF;
-    bf16* Bs = As + CG_BM * CG_BK;
+    bf16* Bs = As + BM * CG_BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(As + swz((tid >> 3) + 32 * i, cc)) = ra[i];
+    for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(As + swz((tid >> 3) + 32 * i, cc)) = ra[i];
     if (!BT) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + swz((tid >> 3) + 32 * i, cc)) = rb[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + (bt_r + (256 / BCH) * i) * LBT + bt_c * 8) = rb[i];
+      for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + tr_off<BN>(bt_r + (256 / BCH) * i, bt_c * 8)) = rb[i];
     }
   };
-  // transposed fragment (MODE 1 B): lane i of group g gets column (col0 + i), rows k0 + 8g + 0..7
-  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  auto frag_t = [&](const bf16* base, int col0, int k0) -> bf16x8 {
-    const bf16* p0 = base + (k0 + 8 * tg + tq) * LBT + col0 + 4 * tp;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * LBT));
-    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, both);
-  };
-
   f32x4 acc[4][NF];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
 
-  load(0);
-  store(0);
+  // one register stage (loads of K-step kt+1 in flight during kt's MFMAs); measured: a second
+  // register stage with LDS-only barriers is 20-60 % slower here (VGPR pressure, occupancy)
+  if (nk > 0) {
+    load(0);
+    store(0);
+  }
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load(kt + 1);
     const bf16* As = lds + cur * BUF;
-    const bf16* Bs = As + CG_BM * CG_BK;
+    const bf16* Bs = As + BM * CG_BK;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int ch = h * 4 + (lane >> 4);
@@ -196,7 +264,7 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
       for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
 #pragma unroll
       for (int j = 0; j < NF; ++j)
-        bfr[j] = BT ? frag_t(Bs, wc * (BN / 2) + j * 16, h * 32) : ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+        bfr[j] = BT ? frag_tr<BN>(Bs, wc * (BN / 2) + j * 16, h * 32, lane) : ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -211,6 +279,18 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
   bf16* out = a.out + peer * a.out_ps;
   const bf16* resid = a.resid ? a.resid + peer * a.resid_ps : nullptr;
   const float* bias = a.bias ? a.bias + peer * a.bias_ps : nullptr;
+  // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
+  auto out_row = [&](int m) -> int {
+    if (MODE != 2) return m;
+    const int img = m / hw, rem = m - img * hw;
+    const int hh = rem / rw, ww = rem - hh * rw;
+    return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
+  };
+  int orow[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) orow[i][e] = out_row(m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + e);
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
     const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
@@ -224,11 +304,12 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
       for (int e = 0; e < 4; ++e) {
         const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + e;
         if (row < M && cok) {
+          const int64_t o = (int64_t)orow[i][e] * a.ncol + col;
           float v = acc[i][j][e] + bv;
-          if (resid != nullptr) v += (float)resid[(int64_t)row * a.ncol + col];
+          if (resid != nullptr) v += (float)resid[o];
           if (a.relu) v = fmaxf(v, 0.f);
           if (!cvalid) v = 0.f;
-          out[(int64_t)row * a.ncol + col] = (bf16)v;
+          out[o] = (bf16)v;
           s += v;
           ss += v * v;
         }
@@ -254,21 +335,25 @@ __global__ __launch_bounds__(256) void k_conv_gemm(ConvGemmArgs a, int tiles_m, 
 // weight gradient
 // ------------------------------------------------------------------------------------------------
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, int tiles_n) {
-  constexpr int LA = BM + 8, LB = BN + 8;        // padded LDS row strides (elements)
+__global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, int tiles_n, int splits) {
   constexpr int FM = BM / 32, FN = BN / 32;       // fragments per wave
   constexpr int CA = BM / 8, CB = BN / 8;         // 16-byte chunks per staged row
   constexpr int NA = 64 * CA / 256, NBr = 64 * CB / 256;
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 64 * (LA + LB)];
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * 64 * (BM + BN)];
 
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
   const int M = nb * a.Ho * a.Wo;
-  const int kbeg = blockIdx.y * a.k_per_split;
+  // grid.x = splits x tiles: consecutive remapped ids (one XCD) share a split, i.e. the same dY / X
+  // rows, so the tiles of one pixel range hit one L2 (the split index in grid.y spread them over all
+  // eight: 2.5 % L2 hits measured on the 64-channel layers)
+  const int ntile = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, ntile * splits);
+  const int split = wgid / ntile, tile = wgid - split * ntile;
+  const int kbeg = split * a.k_per_split;
   const int kend = min(M, kbeg + a.k_per_split);
   if (kbeg >= kend) return;
-  const int wgid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
   const int co0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -291,7 +376,19 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   const int cca = tid % CA;
   const bool acol_ok = co0 + cca * 8 < a.dy_c;
 
-  const float inv_hwo = 1.f / (float)hwo, inv_wo = 1.f / (float)a.Wo;
+  // per-row output coordinates (img, oh, ow) of this thread's B rows, advanced by +64 pixels per
+  // K-step with carries (no per-step division)
+  int b_img[NBr], b_oh[NBr], b_ow[NBr];
+#pragma unroll
+  for (int i = 0; i < NBr; ++i) {
+    const int m = kbeg + tid / CB + (256 / CB) * i;
+    b_img[i] = m / hwo;
+    const int rem = m - b_img[i] * hwo;
+    b_oh[i] = rem / a.Wo;
+    b_ow[i] = rem - b_oh[i] * a.Wo;
+  }
+  const int d_img = 64 / hwo, d_rem = 64 - d_img * hwo, d_oh = d_rem / a.Wo, d_ow = d_rem - d_oh * a.Wo;
+  const int hb = br - a.pad, wb = bs - a.pad;
   uint4 ra[NA], rb[NBr];
   auto load = [&](int m_base) {
 #pragma unroll
@@ -302,38 +399,24 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 #pragma unroll
     for (int i = 0; i < NBr; ++i) {
       const int m = m_base + tid / CB + (256 / CB) * i;
-      bool ok = bcol_ok && m < kend;
-      int64_t off = 0;
-      if (ok) {
-        const int img = fdiv(m, hwo, inv_hwo), rem = m - img * hwo;
-        const int oh = fdiv(rem, a.Wo, inv_wo), ow = rem - oh * a.Wo;
-        const int h = oh * a.stride - a.pad + br, w = ow * a.stride - a.pad + bs;
-        ok = h >= 0 && w >= 0 && h < a.H && w < a.W;
-        off = ((int64_t)(img * a.H + h) * a.W + w) * a.x_c + bci;
-      }
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
+      const int h = b_oh[i] * a.stride + hb, w = b_ow[i] * a.stride + wb;
+      const bool ok = bcol_ok && m < kend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) : make_uint4(0, 0, 0, 0);
+      b_ow[i] += d_ow;
+      if (b_ow[i] >= a.Wo) { b_ow[i] -= a.Wo; ++b_oh[i]; }
+      b_oh[i] += d_oh;
+      if (b_oh[i] >= a.Ho) { b_oh[i] -= a.Ho; ++b_img[i]; }
+      b_img[i] += d_img;
     }
   };
   auto store = [&](int buf) {
-    bf16* As = lds + buf * 64 * (LA + LB);
-    bf16* Bs = As + 64 * LA;
+    bf16* As = lds + buf * 64 * (BM + BN);
+    bf16* Bs = As + 64 * BM;
 #pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(As + (tid / CA + (256 / CA) * i) * LA + cca * 8) = ra[i];
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(As + tr_off<BM>(tid / CA + (256 / CA) * i, cca * 8)) = ra[i];
 #pragma unroll
-    for (int i = 0; i < NBr; ++i) *reinterpret_cast<uint4*>(Bs + (tid / CB + (256 / CB) * i) * LB + ccb * 8) = rb[i];
+    for (int i = 0; i < NBr; ++i) *reinterpret_cast<uint4*>(Bs + tr_off<BN>(tid / CB + (256 / CB) * i, ccb * 8)) = rb[i];
   };
-  // transposed fragment: lane i of group g gets column (col0 + i), rows k0 + 8g + 0..7
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  auto frag_t = [&](const bf16* base, int ld, int col0, int k0) -> bf16x8 {
-    const bf16* p0 = base + (k0 + 8 * g + q) * ld + col0 + 4 * p;
-    const bf16* p1 = p0 + 4 * ld;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
-    // whole-vector bit cast (an element-wise short->bf16 cast miscompiles into lane-duplicating perms)
-    const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, both);
-  };
-
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -347,15 +430,15 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load(kbeg + (kt + 1) * 64);
-    const bf16* As = lds + cur * 64 * (LA + LB);
-    const bf16* Bs = As + 64 * LA;
+    const bf16* As = lds + cur * 64 * (BM + BN);
+    const bf16* Bs = As + 64 * BM;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = frag_t(As, LA, wr * (BM / 2) + i * 16, h * 32);
+      for (int i = 0; i < FM; ++i) af[i] = frag_tr<BM>(As, wr * (BM / 2) + i * 16, h * 32, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = frag_t(Bs, LB, wc * (BN / 2) + j * 16, h * 32);
+      for (int j = 0; j < FN; ++j) bfr[j] = frag_tr<BN>(Bs, wc * (BN / 2) + j * 16, h * 32, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -392,21 +475,26 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 // ------------------------------------------------------------------------------------------------
 extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, void* stream) {
   const ConvGemmArgs& a = *pa;
-  if ((a.src_c & 7) || (a.ncol & 7) || peers < 1) return 1;
-  const int M = a.max_batch * a.out_h * a.out_w;
-  const int tiles_m = (M + CG_BM - 1) / CG_BM;
+  if ((a.src_c & 7) || (a.ncol & 7) || peers < 1 || mode < 0 || mode > 1) return 1;
   const bool wide = a.ncol > 64;
-  const int BN = wide ? 128 : 64;
-  const int tiles_n = (a.ncol + BN - 1) / BN;
-  dim3 grid(tiles_m * tiles_n, 1, peers), block(256);
+  const bool parity = mode == 1 && a.stride == 2;  // strided dgrad: one launch row per parity class
+  const int rows = parity ? ((a.out_h + 1) >> 1) * ((a.out_w + 1) >> 1) : a.out_h * a.out_w;
+  const int tiles_m = (a.max_batch * rows + 127) / 128;
+  const int tiles_n = (a.ncol + (wide ? 127 : 63)) / (wide ? 128 : 64);
+  dim3 grid(tiles_m * tiles_n, parity ? 4 : 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
+#define CG_LAUNCH(M_, BN_) hipLaunchKernelGGL((k_conv_gemm<M_, BN_>), grid, block, 0, s, a, tiles_m, tiles_n)
   if (mode == 0) {
-    if (wide) hipLaunchKernelGGL((k_conv_gemm<0, 128>), grid, block, 0, s, a, tiles_m, tiles_n);
-    else hipLaunchKernelGGL((k_conv_gemm<0, 64>), grid, block, 0, s, a, tiles_m, tiles_n);
+    if (wide) CG_LAUNCH(0, 128);
+    else CG_LAUNCH(0, 64);
+  } else if (parity) {
+    if (wide) CG_LAUNCH(2, 128);
+    else CG_LAUNCH(2, 64);
   } else {
-    if (wide) hipLaunchKernelGGL((k_conv_gemm<1, 128>), grid, block, 0, s, a, tiles_m, tiles_n);
-    else hipLaunchKernelGGL((k_conv_gemm<1, 64>), grid, block, 0, s, a, tiles_m, tiles_n);
+    if (wide) CG_LAUNCH(1, 128);
+    else CG_LAUNCH(1, 64);
   }
+#undef CG_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -421,11 +509,11 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   const bool wm = a.dy_c > 64, wn = ncol > 64;
   const int BM = wm ? 128 : 64, BN = wn ? 128 : 64;
   const int tiles_m = (a.dy_c + BM - 1) / BM, tiles_n = (ncol + BN - 1) / BN;
-  dim3 grid(tiles_m * tiles_n, splits, peers), block(256);
+  dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
-  if (wm && wn) hipLaunchKernelGGL((k_conv_wgrad<128, 128>), grid, block, 0, s, a, tiles_m, tiles_n);
-  else if (wm) hipLaunchKernelGGL((k_conv_wgrad<128, 64>), grid, block, 0, s, a, tiles_m, tiles_n);
-  else if (wn) hipLaunchKernelGGL((k_conv_wgrad<64, 128>), grid, block, 0, s, a, tiles_m, tiles_n);
-  else hipLaunchKernelGGL((k_conv_wgrad<64, 64>), grid, block, 0, s, a, tiles_m, tiles_n);
+  if (wm && wn) hipLaunchKernelGGL((k_conv_wgrad<128, 128>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
+  else if (wm) hipLaunchKernelGGL((k_conv_wgrad<128, 64>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
+  else if (wn) hipLaunchKernelGGL((k_conv_wgrad<64, 128>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
+  else hipLaunchKernelGGL((k_conv_wgrad<64, 64>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

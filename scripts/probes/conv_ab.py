@@ -1,0 +1,48 @@
+"""Time the conv GEMM (forward / dgrad) on ResNet-18 CIFAR shapes, 8 peers, batch 128 (TF/s per shape)."""
+import ctypes
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch
+
+from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, _lib
+
+lib = _lib()
+P, B = 8, 128
+dev = torch.device("cuda")
+shapes = [("l1 3x3 64", 64, 64, 32, 1), ("l2 3x3 128", 128, 128, 16, 1), ("l3 3x3 256", 256, 256, 8, 1), ("l4 3x3 512", 512, 512, 4, 1),
+          ("l2.c1 s2 64->128", 64, 128, 32, 2)]
+for name, cin, cout, h, st in shapes:
+    ho = (h + 2 - 3) // st + 1
+    x = torch.randn(P, B * h * h * cin, device=dev).to(torch.bfloat16)
+    wf = (torch.randn(P, cout * 9 * cin, device=dev) * 0.05).to(torch.bfloat16)
+    y = torch.empty(P, B * ho * ho * cout, device=dev, dtype=torch.bfloat16)
+    dy = torch.randn(P, B * ho * ho * cout, device=dev).to(torch.bfloat16)
+    dx = torch.empty(P, B * h * h * cin, device=dev, dtype=torch.bfloat16)
+    flops = 2 * P * B * ho * ho * cout * 9 * cin
+    for mode in (0, 1):
+        a = ConvGemmArgs()
+        if mode == 0:
+            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = x.data_ptr(), x.shape[1], h, h, cin
+            a.out_h, a.out_w, a.ncol, a.ncol_valid = ho, ho, cout, cout
+            a.out, a.out_ps = y.data_ptr(), y.shape[1]
+        else:
+            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
+            a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
+            a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
+        a.R = a.S = 3
+        a.stride, a.pad = st, 1
+        a.wt, a.wt_ps, a.max_batch = wf.data_ptr(), wf.shape[1], B
+        s = torch.cuda.current_stream().cuda_stream
+        for _ in range(3):
+            assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, s) == 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            lib.conv_gemm_launch(mode, ctypes.byref(a), P, s)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1000
+        useful = flops if mode == 0 or st == 1 else flops  # dgrad useful work = forward FLOPs
+        print(f"{name:18s} mode {mode}: {us:8.1f} us ({useful / us / 1e6:6.0f} TF/s useful)", flush=True)

@@ -26,7 +26,7 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
-@pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2)])
+@pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3)])
 def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
 
