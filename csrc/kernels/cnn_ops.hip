@@ -207,11 +207,13 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
     for (int k = 0; k < rpp; ++k)
 #pragma unroll
       for (int j = 0; j < 16; ++j) a[j] += red[k * cpp + tid][j];
-    float* pp = part + peer * part_ps + (int64_t)blockIdx.x * 2 * Cp;
+    // straight into the peer's [2][Cp] accumulator (the finalize kernel reads and re-zeroes it;
+    // a partial-row slab made the finalize a serial 128-row walk, ~22 us per BatchNorm)
+    float* pp = part + peer * part_ps;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      pp[tid * 8 + j] = a[j];
-      pp[Cp + tid * 8 + j] = a[8 + j];
+      atomicAdd(pp + tid * 8 + j, a[j]);
+      atomicAdd(pp + Cp + tid * 8 + j, a[8 + j]);
     }
   }
 }
@@ -223,15 +225,13 @@ __global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= Cp) return;
   float* cp = coef + peer * 3 * Cp;
+  float* pp = const_cast<float*>(part) + peer * part_ps;
+  const float sg = pp[c], sgx = pp[Cp + c];
+  pp[c] = 0.f;
+  pp[Cp + c] = 0.f;
   if (c >= C) {
     cp[c] = 0.f; cp[Cp + c] = 0.f; cp[2 * Cp + c] = 0.f;
     return;
-  }
-  const float* pp = part + peer * part_ps;
-  float sg = 0.f, sgx = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    sg += pp[b * 2 * Cp + c];
-    sgx += pp[b * 2 * Cp + Cp + c];
   }
   dgamma[peer * param_ps + c] += sgx;
   dbeta[peer * param_ps + c] += sg;

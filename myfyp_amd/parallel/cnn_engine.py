@@ -486,7 +486,7 @@ class CNNGroup:
     def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None) -> None:
         lib, P = _lib(), self.capacity
         nblk = max(1, min(128, (self.B * hw + 255) // 256))
-        part = self.fbuf(f"bnpart_{bn.name}", nblk * 2 * bn.Cp)
+        part = self.fbuf(f"bnsum_{bn.name}", 2 * bn.Cp)  # atomically accumulated, re-zeroed by the finalize
         coef = self.fbuf(f"bncoef_{bn.name}", 3 * bn.Cp)
         _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
                                    self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
