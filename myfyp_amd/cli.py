@@ -99,13 +99,18 @@ def launch(
 
 @app.command("run")
 def run_config(config: str = typer.Argument(..., help="YAML experiment file")) -> None:
-    """Run a YAML-described experiment (see myfyp_amd/examples/configs)."""
+    """Run a YAML-described experiment (see myfyp_amd/examples/configs). Under ``torchrun`` each
+    rank hosts its share of the peers (collective protocol) and rank 0 prints the merged results."""
     from myfyp_amd.runner import run_experiment
 
     if not os.path.exists(config):
         console.print(f"[red]No such file: {config}")
         raise typer.Exit(code=1)
-    run_experiment(config)
+    res = run_experiment(config)
+    if res.get("world", 1) > 1:
+        from myfyp_amd.parallel.federation import Federation
+
+        Federation.get().shutdown()
 
 
 @exp_app.command("list")

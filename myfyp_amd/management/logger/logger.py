@@ -155,6 +155,23 @@ class P2PFLogger:
         if fn in self.metric_listeners:
             self.metric_listeners.remove(fn)
 
+    def merge_logs(self, global_logs: GlobalLogsType, local_logs: LocalLogsType) -> None:
+        """Insert metric records produced by another process (other ranks' peers) into this store —
+        the role of the reference's central Ray logger actor (``ray_logger.py:32-250``)."""
+        for exp, nodes in (global_logs or {}).items():
+            for node, metrics in nodes.items():
+                for metric, series in metrics.items():
+                    for rnd, val in series:
+                        self.global_metrics.add_log(exp, rnd, metric, node, val)
+        for exp, rounds in (local_logs or {}).items():
+            for rnd, nodes in rounds.items():
+                for node, metrics in nodes.items():
+                    for metric, series in metrics.items():
+                        mine = self.local_metrics.get_all_logs().get(exp, {}).get(rnd, {}).get(node, {}).get(metric, [])
+                        for step, val in series:
+                            if (step, val) not in mine:
+                                self.local_metrics.add_log(exp, rnd, metric, node, val, step)
+
     def get_local_logs(self) -> LocalLogsType:
         return self.local_metrics.get_all_logs()
 

@@ -360,6 +360,19 @@ class Federation:
         dist.all_gather_object(out, obj, group=self._cpu_group())
         return out
 
+    def gather_logs(self) -> None:
+        """Collective (every rank calls it): merge every rank's metric stores into every rank's
+        logger, so ``logger.get_global_logs()`` shows all peers of the job (the reference's
+        multi-process runs centralise logs in one Ray actor, ``ray_logger.py:32-250``)."""
+        if self.world == 1:
+            return
+        from myfyp_amd.management.logger import logger
+
+        mine = (self.rank, logger.get_global_logs(), logger.get_local_logs())
+        for rank, g, loc in self.all_gather_object(mine):
+            if rank != self.rank:
+                logger.merge_logs(g, loc)
+
     def _cpu_group(self):
         if self._cpu_pg is None:
             import torch.distributed as dist

@@ -221,26 +221,33 @@ def run_experiment(cfg: Any, verbose: bool = True) -> Dict[str, Any]:
 
         fed = Federation.init()
     nodes: List[Any] = []
+    by_index: Dict[int, Any] = {}
     start_round = 0
     t_start = time.time()
+    # one process per GPU (torchrun): rank r builds the contiguous block of peers it owns
+    world, rank = (fed.world, fed.rank) if fed is not None else (1, 0)
+    local = [i for i in range(n) if (i * world) // n == rank]
     try:
-        for i in range(n):
+        for i in local:
             model = build_model(exp.get("model"), seed=None if seed is None else int(seed), index=i if not exp.get("same_init") else 0)
             node = Node(model, parts[i], address=_address(proto_key, i, name), protocol=protocol, aggregator=build_aggregator(exp.get("aggregator")), exp_name=name)
             node.start()
             nodes.append(node)
+            by_index[i] = node
         if ck.get("resume") and ck.get("dir"):
             metas = [ckpt.restore_node(nd, directory=ck["dir"], exp_name=name) for nd in nodes]
             start_round = min(int(m.get("round", 0)) for m in metas)
         att = exp.get("attack")
-        if att:
-            victim = nodes[int(att.get("node", 0))]
+        if att and int(att.get("node", 0)) in by_index:
+            victim = by_index[int(att.get("node", 0))]
             if att.get("persistent"):
                 fault_injection.ModelPoisoning(victim, att.get("kind", "sign_flip"), float(att.get("sigma", 0.1)), float(att.get("factor", -1.0)), int(att.get("seed", 0)))
             else:
                 fault_injection.apply_attack(victim, att.get("kind", "sign_flip"), float(att.get("sigma", 0.1)), float(att.get("factor", -1.0)), int(att.get("seed", 0)))
         for f in exp.get("faults") or []:
-            victim = nodes[int(f["node"])]
+            if int(f["node"]) not in by_index:
+                continue
+            victim = by_index[int(f["node"])]
             if "kill_at" in f:
                 fault_injection.kill_at(victim, f["kill_at"], f.get("round"))
             if "delay_at" in f:
@@ -252,9 +259,12 @@ def run_experiment(cfg: Any, verbose: bool = True) -> Dict[str, Any]:
             TopologyFactory.connect_nodes(TopologyFactory.generate_matrix(topo, n), nodes)
             wait_convergence(nodes, n - 1, only_direct=False, wait=float(net.get("convergence_timeout", 60)))
         t_start = time.time()
-        nodes[0].set_start_learning(rounds=rounds, epochs=epochs, start_round=start_round)
+        if rank == 0:  # the start message reaches the other ranks' peers over the control bus
+            nodes[0].set_start_learning(rounds=rounds, epochs=epochs, start_round=start_round)
         wait_to_finish(nodes, timeout=float(exp.get("wait_timeout", 3600)))
         elapsed = time.time() - t_start
+        if fed is not None:
+            fed.gather_logs()
         res = {
             "exp_name": name,
             "elapsed_s": elapsed,
@@ -263,8 +273,10 @@ def run_experiment(cfg: Any, verbose: bool = True) -> Dict[str, Any]:
             "histories": {nd.addr: list(nd.learning_workflow.history) for nd in nodes},
             "nodes": [nd.addr for nd in nodes],
             "start_round": start_round,
+            "rank": rank,
+            "world": world,
         }
-        if verbose:
+        if verbose and rank == 0:
             print(format_results(res))
         return res
     finally:

@@ -239,3 +239,18 @@ def test_cli_lists_and_helps():
     assert r.exit_code == 0 and "--protocol" in r.output
     r = CliRunner().invoke(app, ["experiment", "run", "does-not-exist"])
     assert r.exit_code == 1
+
+
+@pytest.mark.slow
+def test_yaml_runner_split_over_two_ranks():
+    """run_experiment under torchrun: each rank hosts its block of peers, the attack lands on the
+    owning rank only, and the metric stores are merged so every rank sees all four peers."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29700 + os.getpid() % 150), os.path.join(root, "tests", "workers", "runner_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert res.returncode == 0, res.stderr[-3000:] + res.stdout[-2000:]
+    assert res.stdout.count(" OK ") == 2, res.stdout
