@@ -10,11 +10,17 @@ from myfyp_amd.learning.frameworks import Framework
 from myfyp_amd.learning.frameworks.p2pfl_model import P2PFLModel
 
 
+class ModelNotBuiltError(Exception):
+    """A Keras model without weights (never built/called) was wrapped (reference ``keras_model.py:38``)."""
+
+
 class KerasModel(P2PFLModel):
     """``get_weights()/set_weights()`` order, like the reference ``KerasModel``; works without
     TensorFlow when built from a parameter list (``KerasModel(None, params=[...])``)."""
 
     def __init__(self, model: Any = None, params=None, **kwargs) -> None:
+        if model is not None and hasattr(model, "built") and not model.built:
+            raise ModelNotBuiltError("The Keras model must be built (called once or given an input shape) before wrapping it")
         self._params: List[np.ndarray] = [np.asarray(w) for w in model.get_weights()] if model is not None else []
         super().__init__(model, params=params, **kwargs)
 

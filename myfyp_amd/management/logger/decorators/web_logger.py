@@ -12,16 +12,30 @@ from myfyp_amd.management.node_monitor import NodeMonitor
 from myfyp_amd.management.web_services import P2pflWebServices
 
 
+class DictFormatter(logging.Formatter):
+    """Log record → the dashboard's log dict (``timestamp``, ``node``, ``level``, ``message``)."""
+
+    def format(self, record: logging.LogRecord) -> dict:  # type: ignore[override]
+        return {
+            "timestamp": datetime.datetime.fromtimestamp(record.created),
+            "node": getattr(record, "node", "-"),
+            "level": record.levelno,
+            "message": record.getMessage(),
+        }
+
+
 class P2pflWebLogHandler(logging.Handler):
     """Forwards log records to the dashboard."""
 
     def __init__(self, p2pfl_web: P2pflWebServices) -> None:
         super().__init__()
         self._p2pfl_web = p2pfl_web
+        self.setFormatter(DictFormatter())
 
     def emit(self, record: logging.LogRecord) -> None:
         try:
-            self._p2pfl_web.send_log(datetime.datetime.fromtimestamp(record.created), getattr(record, "node", "-"), record.levelno, record.getMessage())
+            d = self.formatter.format(record)  # type: ignore[union-attr]
+            self._p2pfl_web.send_log(d["timestamp"], d["node"], d["level"], d["message"])
         except Exception:
             pass
 

@@ -210,7 +210,9 @@ class Federation:
             import torch.distributed as dist
 
             if not dist.is_initialized():
-                be = backend or ("nccl" if device.type == "cuda" else "gloo")
+                # MYFYP_DIST_BACKEND=gloo rehearses a multi-rank job on ONE GPU (RCCL refuses two
+                # ranks on one device); production multi-GPU jobs use RCCL ("nccl")
+                be = backend or os.environ.get("MYFYP_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
                 kw = {"timeout": datetime.timedelta(seconds=Settings.COLLECTIVE_TIMEOUT)}
                 if be == "nccl":
                     kw["device_id"] = device
