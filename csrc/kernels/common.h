@@ -43,6 +43,21 @@ __device__ __forceinline__ bf16x8 ld8_u8(const uint8_t* p) {
   return r;
 }
 
+typedef short mlp_s16x4 __attribute__((ext_vector_type(4)));
+typedef short mlp_s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) mlp_s16x4 mlp_lds_s16x4;
+
+// B fragment B[k0 + 8 (lane>>4) + j][n0 + (lane & 15)] from a row-major [k][n] bf16 LDS image
+// (two 4-row transposed reads; EXEC must be full — call from wave-uniform control flow only)
+__device__ __forceinline__ bf16x8 frag_b_tr(const bf16* base, int ld, int k0, int n0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const bf16* p0 = base + (k0 + 8 * g + q) * ld + n0 + 4 * pp;
+  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
+  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0 + 4 * ld));
+  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and meets the
 // other waves, but leaves global loads in flight (``__syncthreads()`` also drains vmcnt, which
 // stalls every wave on prefetches it does not need yet). Single asm with a memory clobber so the

@@ -6,6 +6,13 @@
 void fl_weighted_sum(float* out, const uint64_t* srcs, const float* w, int K, int64_t n, hipStream_t s);
 void fl_stacked_weighted_sum(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w, float scale, hipStream_t s);
 void fl_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64_t ld, const float* mask, hipStream_t s);
+#define FEDAVG_MAX_PEERS 64
+struct FedAvgWeights {
+  float w[FEDAVG_MAX_PEERS];
+  float wsum;
+};
+void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
+void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
 void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s);
 void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
                  const float* cg, const float* cl, hipStream_t s);

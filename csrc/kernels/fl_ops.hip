@@ -77,6 +77,71 @@ __global__ __launch_bounds__(FL_BLOCK) void k_broadcast_rows(float* __restrict__
   }
 }
 
+// FedAvg over a stacked [P][ld] group with the per-peer weights / mask passed BY VALUE (kernel
+// arguments): no host→device copy, nothing for the host to wait on.
+//   reduce: out[i] = Σ_p w[p] · stacked[p*ld + i] (i < n), out[n] = wsum
+//   apply:  stacked[p*ld + i] = out[i] / max(out[n], 1e-12) for rows with mask bit p set
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ out, const float* __restrict__ stacked, int P, int64_t n, int64_t ld,
+                                                             FedAvgWeights w) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  const int64_t t0 = blockIdx.x * FL_BLOCK + threadIdx.x;
+  if (t0 == 0) out[n] = w.wsum;
+  if ((ld % 4) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = t0; i < n4; i += stride) {
+      float4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < P; ++p) {
+        const float wp = w.w[p];
+        if (wp == 0.f) continue;
+        const float4 v = reinterpret_cast<const float4*>(stacked + p * ld)[i];
+        acc.x += wp * v.x; acc.y += wp * v.y; acc.z += wp * v.z; acc.w += wp * v.w;
+      }
+      reinterpret_cast<float4*>(out)[i] = acc;
+    }
+    for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
+      float acc = 0.f;
+      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      out[i] = acc;
+    }
+  } else {
+    for (int64_t i = t0; i < n; i += stride) {
+      float acc = 0.f;
+      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      out[i] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_apply(float* __restrict__ stacked, const float* __restrict__ out, int P, int64_t n, int64_t ld,
+                                                            unsigned long long mask) {
+  const int p = blockIdx.y;
+  if (!((mask >> p) & 1ull)) return;
+  const float inv = 1.f / fmaxf(out[n], 1e-12f);
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  float* dst = stacked + p * ld;
+  if ((ld % 4) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride) {
+      float4 v = reinterpret_cast<const float4*>(out)[i];
+      v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+      reinterpret_cast<float4*>(dst)[i] = v;
+    }
+    for (int64_t i = n4 * 4 + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) dst[i] = out[i] * inv;
+  } else {
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) dst[i] = out[i] * inv;
+  }
+}
+
+void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, stacked, P, n, ld, w);
+}
+
+void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s) {
+  unsigned gx = grid_for((n + 3) / 4);
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(k_fedavg_apply, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, out, P, n, ld, mask);
+}
+
 // per-coordinate median of K ≤ 16 models: insertion sort in registers
 __global__ __launch_bounds__(FL_BLOCK) void k_coordinate_median(float* __restrict__ out, const uint64_t* __restrict__ srcs, int K, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;

@@ -27,6 +27,8 @@ struct MLPArgs {
   const int* n;
   const int* perm;  // [P][perm_stride] local indices (epoch permutation)
   int64_t perm_stride;
+  int shuffle_native;                // 1: permutation drawn in the gather kernel from *seed
+  const unsigned long long* seed;    // epoch shuffle key (device word, uploaded per epoch)
   // the epoch's batches, gathered once in permutation order at the start of the epoch so that the
   // per-step kernels read contiguous rows instead of chasing perm -> pointer table -> row
   uint8_t* Xb;      // [P][xb_rows][D0]

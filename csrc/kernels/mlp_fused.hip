@@ -504,21 +504,6 @@ __device__ __forceinline__ void tile_apply(const MLPArgs& a, const TileState& st
 #define WG_LDXR (WG_COLS + 8)
 static inline size_t wgrad_lds_bytes(int Bpad) { return 16 * WG_LDG * sizeof(float) + (size_t)Bpad * WG_LDXR * sizeof(bf16); }
 
-typedef short mlp_s16x4 __attribute__((ext_vector_type(4)));
-typedef short mlp_s16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) mlp_s16x4 mlp_lds_s16x4;
-
-// B fragment B[k0 + 8 (lane>>4) + j][n0 + (lane & 15)] from a row-major [k][n] bf16 LDS image
-// (two 4-row transposed reads; EXEC must be full — call from wave-uniform control flow only)
-__device__ __forceinline__ bf16x8 frag_b_tr(const bf16* base, int ld, int k0, int n0) {
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const bf16* p0 = base + (k0 + 8 * g + q) * ld + n0 + 4 * pp;
-  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
-  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0 + 4 * ld));
-  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
 __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   extern __shared__ __attribute__((aligned(16))) char smem_wg[];
   float* sG = reinterpret_cast<float*>(smem_wg);
@@ -622,6 +607,40 @@ __global__ __launch_bounds__(256) void mlp_wgrad_opt(MLPArgs a, int step) {
   }
 }
 
+// Keyed pseudo-random permutation of [0, n): 4-round balanced Feistel network on the smallest even
+// bit width covering n, cycle-walked back into range (expected < 4 rounds of walking). Used to draw
+// each peer's epoch order without a host-side sort.
+__device__ __forceinline__ unsigned mix32(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ unsigned feistel_perm(unsigned x, unsigned n, unsigned long long key) {
+  if (n <= 1) return 0;
+  int bits = 32 - __clz(n - 1);
+  if (bits < 2) bits = 2;
+  if (bits & 1) ++bits;
+  const int half = bits / 2;
+  const unsigned mask = (1u << half) - 1u;
+  const unsigned k0 = (unsigned)key, k1 = (unsigned)(key >> 32);
+  unsigned y = x;
+  do {
+    unsigned L = y >> half, R = y & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned f = mix32(R ^ ((r & 1) ? k1 : k0) ^ (0x9e3779b9u * (unsigned)(r + 1))) & mask;
+      const unsigned t = L ^ f;
+      L = R;
+      R = t;
+    }
+    y = (L << half) | R;
+  } while (y >= n);
+  return y;
+}
+
 // ---------------------------------------------------------------------------------------------
 // epoch gather: Xb[p][i] = X_p[perm_p[i]], Yb[p][i] = Y_p[perm_p[i]] for i < n_p (first node of
 // every epoch graph). grid = (ceil(xb_rows / 4), 1, P), block = 256 = 4 rows x 64 lanes (8 B each).
@@ -632,7 +651,8 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= n || i >= a.xb_rows || !a.ctl[p].x) return;
-  const int64_t src = a.perm[(int64_t)p * a.perm_stride + i];
+  const int64_t src = a.shuffle_native ? (int64_t)feistel_perm((unsigned)i, (unsigned)n, *a.seed ^ (0x9e3779b97f4a7c15ull * (unsigned long long)(p + 1)))
+                                       : (int64_t)a.perm[(int64_t)p * a.perm_stride + i];
   const uint8_t* xs = a.Xp[p] + src * (int64_t)a.D0;
   uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
   for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];

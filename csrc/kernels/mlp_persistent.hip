@@ -1,0 +1,817 @@
+// Weight-stationary persistent epoch kernel for the reference MLP (784-256-128-10) on gfx950.
+//
+// Why: the 3-launch step (mlp_fused.hip) re-reads and re-writes every peer's fp32 master weights and
+// Adam moments each step (~49 MB/step for 8 peers) and pays three kernel boundaries per step. Here a
+// whole local epoch is ONE launch and the optimizer state never leaves the chip: every peer is a
+// gang of 17 workgroups (512 threads, one per CU) that live for the epoch —
+//
+//   owner g (g = 0..15) keeps W1 rows 16g..16g+15 (+ b1 slice) and W2 columns 16g..16g+15 as fp32
+//            {w, m, v} IN REGISTERS, laid out exactly as the MFMA operand/result fragments that use
+//            them, and the step's input batch in LDS. It computes H1[:, 16g:16g+16] (forward),
+//            dH1 slice = dH2 · W2[:, slice] ⊙ [H1>0], dW1 rows, dW2 columns, and applies Adam/SGD to
+//            its own registers.
+//   head     keeps W3, b2, b3; computes H2 = relu(H1·W2ᵀ+b2), logits, log-softmax + NLL, dlogits,
+//            dH2 = dlogits·W3 ⊙ [H2>0], dW3, db2, db3.
+//
+// Per step the gang exchanges three small tiles through L2 (H1 2 KB per owner → head; dH2 16 KB head →
+// owners; the updated bf16 W2 slice 4 KB per owner → head), with write-through (sc1) stores, a drained
+// sc1 flag per producer and sc1 loads on the consumer (cdna_hip_programming.md §6 Guideline 16, valid
+// form row 1 of MI355X_MICROARCH.md's hand-off table). Flags carry the step number, so no flag is ever
+// reset inside a launch; the launch's memset node zeroes them. Every spin is bounded (1 s) and sets a
+// sticky error word the host checks with the step statistics.
+//
+// Fragment bookkeeping. MFMA v_mfma_f32_16x16x32_bf16: lane (h = l>>4, c = l&15) holds
+// A[c][8h+j], B[8h+j][c], C[4h+i][c]. A weight-gradient tile computed as C[m = input index][n = c]
+// puts 4h+i of the input dimension in lane (h, c); a 32-wide K step split into two such tiles gives
+// lane h the inputs {4h..4h+3, 16+4h..16+4h+3}. The forward (and dH1) MFMAs therefore use the
+// K-slot permutation κ(h, j) = j < 4 ? 4h + j : 16 + 4h + (j − 4) on BOTH operands, so the gradient
+// of a weight lands in the very lane and register slot that holds the weight: the optimizer is an
+// in-register epilogue with no data movement.
+//
+// Placement: block b serves XCD slot b % 8, so the 17 workgroups of a gang share one XCD's L2 under
+// round-robin dispatch (speed only — the protocol does not depend on placement).
+#include "mlp_persistent.h"
+
+// Optional phase timestamps (build with -DMLP_STAMPS): peer 0's owner 0 and head, steps < 32,
+// read with mlp_debug_persistent_stamps (wall_clock64 ticks, 100 MHz).
+#ifdef MLP_STAMPS
+__device__ unsigned long long g_pe_stamps[2][32][8];
+#define PE_STAMP(role, t, i)                                                               \
+  do {                                                                                     \
+    if (p == 0 && threadIdx.x == 0 && (t) < 32) g_pe_stamps[role][t][i] = wall_clock64(); \
+  } while (0)
+extern "C" int mlp_debug_persistent_stamps(void* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pe_stamps), sizeof(g_pe_stamps)) == hipSuccess ? 0 : 1;
+}
+#else
+#define PE_STAMP(role, t, i) \
+  do {                       \
+  } while (0)
+#endif
+
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int NT = 512;  // threads per workgroup (8 waves)
+constexpr int NG = 16;   // owners per peer (D1 / 16)
+constexpr int PD1 = 256, PD2 = 128;
+constexpr int ROLES = NG + 1;
+constexpr int FLAG_LINE = 32;  // u32 per flag: one 128-byte line each
+constexpr int FLAGS_PER_PEER = 2 * NG + 1;
+constexpr int F_H1 = 0, F_W2 = NG, F_DH2 = 2 * NG;
+constexpr unsigned long long SPIN_TICKS = 100000000ull;  // wall_clock64 runs at 100 MHz: 1 s
+constexpr int KS1_MAX = 32;                              // D0 <= 1024
+constexpr int LD2 = PD2 + 8;                             // bf16 row stride of [*][128] LDS tiles
+constexpr int LDH = PD1 + 8;                             // bf16 row stride of [*][256] LDS tiles
+constexpr int LDL = 40;                                  // dlogits [b][32 (classes, K-padded)] + 8
+constexpr int LDW3 = PD2 + 8;                            // W3 bf16 [32][128] + 8
+
+__device__ __forceinline__ unsigned* flag_at(unsigned* flags, int p, int idx) {
+  return flags + ((size_t)p * FLAGS_PER_PEER + idx) * FLAG_LINE;
+}
+__device__ __forceinline__ void st_wt(void* ptr, unsigned long long v) {  // 8-byte write-through store
+  __hip_atomic_store((gu64*)ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
+  return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }
+
+__device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Producer side: every storing wave drains its write-through stores, the workgroup meets, ONE lane
+// stores the flag (sc1).
+__device__ __forceinline__ void publish(unsigned* flags, int p, int idx, unsigned value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag_at(flags, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer side: wave 0 polls flags idx0..idx0+n-1 (one lane each, relaxed sc1 loads + s_sleep) until
+// all reach `target`, then the workgroup meets; every later load of the handed-off bytes is an sc1
+// load. Bounded: gives up after SPIN_TICKS or when another workgroup gave up.
+__device__ bool wg_wait(unsigned* flags, int p, int idx0, int n, unsigned target, int* err, int* sOk) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned* f = flag_at(flags, p, idx0 + (lane < n ? lane : 0));
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    for (;;) {
+      const unsigned v = lane < n ? __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__all(v >= target)) break;
+      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        ok = 0;
+        break;
+      }
+      if (wall_clock64() - t0 > SPIN_TICKS) {
+        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *sOk = ok;
+  }
+  __syncthreads();
+  const int ok = *sOk;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+  return ok != 0;
+}
+
+__device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
+  const int r = n - t * a.B;
+  return r < 0 ? 0 : (r > a.B ? a.B : r);
+}
+
+__device__ __forceinline__ void bias_corr(const MLPArgs& a, int t0, int t, float& bc1, float& bc2s) {
+  const int k = t0 + t + 1;
+  bc1 = 1.f - __powf(a.opt.beta1, (float)k);
+  bc2s = sqrtf(1.f - __powf(a.opt.beta2, (float)k));
+}
+
+__device__ __forceinline__ void upd(const MLPArgs& a, float g, float& w, float& m, float& v, float bc1, float bc2s) {
+  opt_update(a.opt, g, w, m, v, bc1, bc2s, nullptr, nullptr, nullptr, 0);
+}
+
+// ---- LDS carving (all offsets multiples of 16 bytes; dynamic region only: Guideline 17)
+struct OwnerLds {
+  int ldx;  // bf16 row stride of the X tile
+  size_t x, red, dh2, h1, dh1, w2g, b1, db1, ok, total;
+};
+__host__ __device__ inline size_t al16(size_t v) { return (v + 15) / 16 * 16; }
+__host__ __device__ inline OwnerLds owner_lds(int Bpad, int D0) {
+  OwnerLds L;
+  const int ks1 = (D0 + 31) / 32;
+  L.ldx = ks1 * 32 + 8;
+  const int MT = Bpad / 16;
+  size_t o = 0;
+  L.x = o;   o += al16((size_t)Bpad * L.ldx * 2);
+  L.red = o; o += al16((size_t)8 * MT * 64 * 16);
+  L.dh2 = o; o += al16((size_t)Bpad * LD2 * 2);
+  L.h1 = o;  o += al16((size_t)Bpad * 16 * 2);
+  L.dh1 = o; o += al16((size_t)Bpad * 16 * 2);
+  L.w2g = o; o += al16((size_t)PD2 * 16 * 2);
+  L.b1 = o;  o += al16(3 * 16 * 4);
+  L.db1 = o; o += al16(16 * 4);
+  L.ok = o;  o += 16;
+  L.total = o;
+  return L;
+}
+struct HeadLds {
+  size_t w2, h1, h2, dlog, w3, red, b2, b3, ok, total;
+};
+__host__ __device__ inline HeadLds head_lds(int Bpad) {
+  HeadLds L;
+  const int MT = Bpad / 16;
+  size_t o = 0;
+  L.w2 = o;   o += al16((size_t)PD2 * LDH * 2);
+  L.h1 = o;   o += al16((size_t)Bpad * LDH * 2);  // also the dH2 staging tile (disjoint lifetimes)
+  L.h2 = o;   o += al16((size_t)Bpad * LD2 * 2);
+  L.dlog = o; o += al16((size_t)Bpad * LDL * 2);
+  L.w3 = o;   o += al16((size_t)32 * LDW3 * 2);
+  L.red = o;  o += al16((size_t)4 * MT * 64 * 16);
+  L.b2 = o;   o += al16(3 * PD2 * 4);
+  L.b3 = o;   o += al16(3 * 16 * 4);
+  L.ok = o;   o += 16;
+  L.total = o;
+  return L;
+}
+
+// =============================================================================================
+// owner workgroup
+// =============================================================================================
+template <int BP>
+__device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, char* smem) {
+  constexpr int MT = BP / 16;
+  constexpr int XPT = BP / 4;  // max 8-byte X chunks per thread (D0 <= 1024)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int D0 = a.D0, KS1 = (D0 + 31) / 32;
+  const OwnerLds L = owner_lds(BP, D0);
+  const int LDX = L.ldx;
+  bf16* sX = reinterpret_cast<bf16*>(smem + L.x);
+  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
+  bf16* sDH2 = reinterpret_cast<bf16*>(smem + L.dh2);
+  bf16* sH1 = reinterpret_cast<bf16*>(smem + L.h1);
+  bf16* sDH1 = reinterpret_cast<bf16*>(smem + L.dh1);
+  bf16* sW2g = reinterpret_cast<bf16*>(smem + L.w2g);
+  float* sB1 = reinterpret_cast<float*>(smem + L.b1);  // [3][16] w, m, v
+  float* sDb1 = reinterpret_cast<float*>(smem + L.db1);
+  int* sOk = reinterpret_cast<int*>(smem + L.ok);
+
+  const int4 ctl = a.ctl[p];
+  const int n = ctl.y;
+  const int nsteps = (n + a.B - 1) / a.B;
+  const int64_t pS = (int64_t)p * a.S;
+  const bool adam = a.opt.kind == 0;
+
+  // ---- resident state: W1 rows (all waves; wave w owns K steps w, w+8, w+16, w+24) and the W2
+  //      column slice (waves 4..7; wave 4+k owns o2 32k..32k+31)
+  float w1[4][8], m1[4][8], v1[4][8];
+  float w2[8], m2[8], v2[8];
+  const int orow = NG * g + c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int s = wave + 8 * q;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int k = 32 * s + 16 * half + 4 * h;
+      float4 wv = {0.f, 0.f, 0.f, 0.f}, mv = wv, vv = wv;
+      if (s < KS1 && k < D0) {
+        const int64_t idx = pS + a.off_w1 + (int64_t)orow * D0 + k;
+        wv = *reinterpret_cast<const float4*>(a.params + idx);
+        mv = *reinterpret_cast<const float4*>(a.m + idx);
+        if (adam) vv = *reinterpret_cast<const float4*>(a.v + idx);
+      }
+      const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w1[q][4 * half + i] = wa[i];
+        m1[q][4 * half + i] = ma[i];
+        v1[q][4 * half + i] = va[i];
+      }
+    }
+  }
+  const int ww = wave - 4;  // W2 wave index (valid for wave >= 4)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    w2[j] = m2[j] = v2[j] = 0.f;
+    if (wave >= 4) {
+      const int64_t idx = pS + a.off_w2 + (int64_t)(32 * ww + kappa(h, j)) * PD1 + NG * g + c;
+      w2[j] = a.params[idx];
+      m2[j] = a.m[idx];
+      if (adam) v2[j] = a.v[idx];
+    }
+  }
+  if (tid < 16) {
+    const int64_t idx = pS + a.off_b1 + NG * g + tid;
+    sB1[tid] = a.params[idx];
+    sB1[16 + tid] = a.m[idx];
+    sB1[32 + tid] = adam ? a.v[idx] : 0.f;
+  }
+
+  // ---- X staging: rows of step t (bf16, zero rows beyond the valid batch; the K padding
+  //      columns D0..KS1*32 are zeroed once and never written again)
+  const int xchunks = BP * (D0 / 8);
+  const int cpr = D0 / 8;
+  uint2 xr[XPT];
+  auto x_load = [&](int t, int tv) {
+    const int rows = rows_at(a, n, t);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tv + NT * k;
+      xr[k] = uint2{0u, 0u};
+      if (e < xchunks) {
+        const int r = e / cpr, q = e - r * cpr;
+        if (r < rows) xr[k] = *reinterpret_cast<const uint2*>(a.Xb + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + 8 * q);
+      }
+    }
+  };
+  auto x_store = [&](int tv) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int e = tv + NT * k;
+      if (e < xchunks) {
+        const int r = e / cpr, q = e - r * cpr;
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)(float)((((j < 4) ? xr[k].x : xr[k].y) >> (8 * (j & 3))) & 0xffu);
+        *reinterpret_cast<bf16x8*>(sX + r * LDX + 8 * q) = o;
+      }
+    }
+  };
+  for (int e = tid; e < BP * (KS1 * 32 - D0); e += NT) {
+    const int r = e / (KS1 * 32 - D0), q = e % (KS1 * 32 - D0);
+    sX[r * LDX + D0 + q] = (bf16)0.f;
+  }
+  if (nsteps > 0) {
+    x_load(0, tid);
+    x_store(tid);
+  }
+
+  // ---- initial W2 publish (version 1)
+  auto publish_w2 = [&](unsigned version) {
+    if (wave >= 4) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
+    }
+    __syncthreads();
+    {
+      const int row = tid >> 2, part = tid & 3;  // 128 rows x 4 chunks of 4 bf16 = 512 stores
+      const unsigned long long v = *reinterpret_cast<const unsigned long long*>(sW2g + row * 16 + 4 * part);
+      st_wt(pb.w2x + ((int64_t)p * PD2 + row) * PD1 + NG * g + 4 * part, v);
+    }
+    publish(pb.flags, p, F_W2 + g, version);
+  };
+  publish_w2(1u);
+
+  for (int t = 0; t < nsteps; ++t) {
+    // per-iteration copy of the thread index, opaque to the compiler: every address below is
+    // re-derived each step instead of being hoisted out of the loop and kept live (VGPR pressure)
+    int tv = tid;
+    asm volatile("" : "+v"(tv));
+    const int rows = rows_at(a, n, t);
+    float bc1, bc2s;
+    bias_corr(a, ctl.z, t, bc1, bc2s);
+    if (tid < 16) sDb1[tid] = 0.f;
+    if (g == 0) PE_STAMP(0, t, 0);
+
+    // ================= A: H1 slice = relu(X · W1sliceᵀ + b1), split-K over the 8 waves
+    {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        if (s < KS1) {
+          bf16x8 bw;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bw[j] = (bf16)w1[q][j];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bf16* xp = sX + (16 * mt + c) * LDX + 32 * s + 4 * h;
+            const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
+            acc[mt] = mfma_bf16(af, bw, acc[mt]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // bound the live fragment set (register pressure)
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc[mt];
+    }
+    lds_barrier();
+    if (tid < MT * 64) {
+      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
+      f32x4 s = sRed[mt * 64 + (tid & 63)];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      const float bias = sB1[cc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * mt + 4 * hh + i;
+        const float v = b < rows ? fmaxf(s[i] + bias, 0.f) : 0.f;
+        sH1[b * 16 + cc] = (bf16)v;
+      }
+    }
+    lds_barrier();
+    if (tid < BP * 4) {
+      const int b = tv >> 2, part = tv & 3;
+      st_wt(pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + 4 * part, *reinterpret_cast<const unsigned long long*>(sH1 + b * 16 + 4 * part));
+    }
+    publish(pb.flags, p, F_H1 + g, (unsigned)(t + 1));
+    if (g == 0) PE_STAMP(0, t, 1);
+
+    // next step's batch: global loads in flight while the head works
+    const bool more = t + 1 < nsteps;
+    if (more) x_load(t + 1, tv);
+
+    // ================= C: backward of this slice
+    if (!wg_wait(pb.flags, p, F_DH2, 1, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (g == 0) PE_STAMP(0, t, 2);
+#pragma unroll
+    for (int k = 0; k < BP / 16; ++k) {  // BP x 128 bf16 = BP*32 chunks of 8 B
+      const int e = tv + NT * k;
+      const int b = e >> 5, q = e & 31;
+      const unsigned long long v = ld_wt(pb.dh2x + ((int64_t)p * BP + b) * PD2 + 4 * q);
+      *reinterpret_cast<unsigned long long*>(sDH2 + b * LD2 + 4 * q) = v;
+    }
+    lds_barrier();
+    // C1: dH1 partials (waves 4..7: K = o2 block of the wave), W2 before this step's update
+    if (wave >= 4) {
+      bf16x8 bw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bw[j] = (bf16)w2[j];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16* dp = sDH2 + (16 * mt + c) * LD2 + 32 * ww + 4 * h;
+        const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(dp), *reinterpret_cast<const bf16x4*>(dp + 16));
+        sRed[(ww * MT + mt) * 64 + lane] = mfma_bf16(af, bw, zero4());
+      }
+    }
+    lds_barrier();
+    if (tid < MT * 64) {
+      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
+      f32x4 s = sRed[mt * 64 + (tid & 63)];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      float db = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * mt + 4 * hh + i;
+        const bf16 d = (bf16)((float)sH1[b * 16 + cc] > 0.f ? s[i] : 0.f);
+        sDH1[b * 16 + cc] = d;
+        db += (float)d;
+      }
+      db += __shfl_xor(db, 16);
+      db += __shfl_xor(db, 32);
+      if (hh == 0) atomicAdd(&sDb1[cc], db);
+    }
+    lds_barrier();
+    // C3: dW2 columns + update (waves 4..7), then publish the bf16 slice for the head's next step
+    if (wave >= 4) {
+      float gr[8];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int kb = 0; kb < BP / 32; ++kb)
+          acc = mfma_bf16(frag_b_tr(sDH2, LD2, 32 * kb, 32 * ww + 16 * tt), frag_b_tr(sH1, 16, 32 * kb, 0), acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) upd(a, gr[j], w2[j], m2[j], v2[j], bc1, bc2s);
+    }
+    publish_w2((unsigned)(t + 2));
+    if (g == 0) PE_STAMP(0, t, 3);
+    // C2: dW1 rows + update (all waves, their own K steps)
+    {
+      bf16x8 bd[BP / 32];
+#pragma unroll
+      for (int kb = 0; kb < BP / 32; ++kb) bd[kb] = frag_b_tr(sDH1, 16, 32 * kb, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        if (s < KS1) {
+          float gr[8];
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            f32x4 acc = zero4();
+#pragma unroll
+            for (int kb = 0; kb < BP / 32; ++kb) acc = mfma_bf16(frag_b_tr(sX, LDX, 32 * kb, 32 * s + 16 * tt), bd[kb], acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) upd(a, gr[j], w1[q][j], m1[q][j], v1[q][j], bc1, bc2s);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (tid < 16) upd(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], bc1, bc2s);
+    __syncthreads();  // every wave is done with sX / sDH1 / sB1
+    if (g == 0) PE_STAMP(0, t, 4);
+    if (more) x_store(tv);
+    __syncthreads();
+    if (g == 0) PE_STAMP(0, t, 5);
+  }
+
+  // ---- write the state back (fp32 master, moments, bf16 shadow). The row / peer offsets are
+  //      laundered through empty asm so the compiler re-derives these addresses here instead of
+  //      keeping the prologue's ~70 VGPRs of 64-bit addresses alive across the whole step loop.
+  int orow_w = orow;
+  int64_t pS_w = pS;
+  asm volatile("" : "+v"(orow_w), "+s"(pS_w));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int s = wave + 8 * q;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int k = 32 * s + 16 * half + 4 * h;
+      if (s < KS1 && k < D0) {
+        const int64_t idx = pS_w + a.off_w1 + (int64_t)orow_w * D0 + k;
+        const int j0 = 4 * half;
+        *reinterpret_cast<float4*>(a.params + idx) = float4{w1[q][j0], w1[q][j0 + 1], w1[q][j0 + 2], w1[q][j0 + 3]};
+        *reinterpret_cast<float4*>(a.m + idx) = float4{m1[q][j0], m1[q][j0 + 1], m1[q][j0 + 2], m1[q][j0 + 3]};
+        if (adam) *reinterpret_cast<float4*>(a.v + idx) = float4{v1[q][j0], v1[q][j0 + 1], v1[q][j0 + 2], v1[q][j0 + 3]};
+        bf16x4 sh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sh[i] = (bf16)w1[q][j0 + i];
+        *reinterpret_cast<bf16x4*>(a.shadow + idx) = sh;
+      }
+    }
+  }
+  if (wave >= 4) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o2 = 32 * ww + kappa(h, j);
+      const int64_t idx = pS_w + a.off_w2 + (int64_t)o2 * PD1 + orow_w;
+      a.params[idx] = w2[j];
+      a.m[idx] = m2[j];
+      if (adam) a.v[idx] = v2[j];
+      a.shadow[idx] = (bf16)w2[j];
+      a.w2t[(int64_t)p * PD1 * PD2 + (int64_t)orow_w * PD2 + o2] = (bf16)w2[j];
+    }
+  }
+  if (tid < 16) {
+    const int64_t idx = pS_w + a.off_b1 + NG * g + tid;
+    a.params[idx] = sB1[tid];
+    a.m[idx] = sB1[16 + tid];
+    if (adam) a.v[idx] = sB1[32 + tid];
+    a.shadow[idx] = (bf16)sB1[tid];
+  }
+}
+
+// =============================================================================================
+// head workgroup
+// =============================================================================================
+template <int BP>
+__device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* smem) {
+  constexpr int MT = BP / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int D3 = a.D3;
+  const HeadLds L = head_lds(BP);
+  bf16* sW2 = reinterpret_cast<bf16*>(smem + L.w2);
+  bf16* sH1 = reinterpret_cast<bf16*>(smem + L.h1);
+  bf16* sDH2 = sH1;  // dH2 staging reuses the H1 tile (H1 is dead after the H2 GEMM)
+  bf16* sH2 = reinterpret_cast<bf16*>(smem + L.h2);
+  bf16* sDlog = reinterpret_cast<bf16*>(smem + L.dlog);
+  bf16* sW3 = reinterpret_cast<bf16*>(smem + L.w3);
+  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
+  float* sB2 = reinterpret_cast<float*>(smem + L.b2);  // [3][128]
+  float* sB3 = reinterpret_cast<float*>(smem + L.b3);  // [3][16]
+  int* sOk = reinterpret_cast<int*>(smem + L.ok);
+
+  const int4 ctl = a.ctl[p];
+  const int n = ctl.y;
+  const int nsteps = (n + a.B - 1) / a.B;
+  const int64_t pS = (int64_t)p * a.S;
+  const bool adam = a.opt.kind == 0;
+  const bool cin = c < D3;
+
+  // resident W3 (waves 0..3, wave w owns o2 32w..32w+31), biases in LDS
+  float w3[8], m3[8], v3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    w3[j] = m3[j] = v3[j] = 0.f;
+    if (wave < 4 && cin) {
+      const int64_t idx = pS + a.off_w3 + (int64_t)c * PD2 + 32 * wave + kappa(h, j);
+      w3[j] = a.params[idx];
+      m3[j] = a.m[idx];
+      if (adam) v3[j] = a.v[idx];
+    }
+  }
+  for (int e = tid; e < 32 * LDW3; e += NT) sW3[e] = (bf16)0.f;
+  for (int e = tid; e < BP * LDL; e += NT) sDlog[e] = (bf16)0.f;
+  if (tid < PD2) {
+    const int64_t idx = pS + a.off_b2 + tid;
+    sB2[tid] = a.params[idx];
+    sB2[PD2 + tid] = a.m[idx];
+    sB2[2 * PD2 + tid] = adam ? a.v[idx] : 0.f;
+  } else if (tid < PD2 + 16) {
+    const int k = tid - PD2;
+    const int64_t idx = pS + a.off_b3 + k;
+    sB3[k] = k < D3 ? a.params[idx] : 0.f;
+    sB3[16 + k] = k < D3 ? a.m[idx] : 0.f;
+    sB3[32 + k] = (k < D3 && adam) ? a.v[idx] : 0.f;
+  }
+  __syncthreads();
+  if (wave < 4 && cin) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sW3[c * LDW3 + 32 * wave + kappa(h, j)] = (bf16)w3[j];
+  }
+  float loss_acc = 0.f, correct_acc = 0.f;
+
+  for (int t = 0; t < nsteps; ++t) {
+    int tv = tid;  // opaque per-iteration thread index (see owner)
+    asm volatile("" : "+v"(tv));
+    const int rows = rows_at(a, n, t);
+    float bc1, bc2s;
+    bias_corr(a, ctl.z, t, bc1, bc2s);
+
+    // ---- W2 (bf16, version t+1) and H1 (step t) from the owners
+    PE_STAMP(1, t, 0);
+    if (!wg_wait(pb.flags, p, F_W2, NG, (unsigned)(t + 1), pb.err, sOk)) return;
+    PE_STAMP(1, t, 1);
+    unsigned long long w2r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // 128 x 256 bf16 = 8192 chunks of 8 B
+      const int e = tv + NT * k;
+      w2r[k] = ld_wt(pb.w2x + (int64_t)p * PD2 * PD1 + (int64_t)e * 4);
+    }
+    if (!wg_wait(pb.flags, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
+    PE_STAMP(1, t, 2);
+    unsigned long long h1r[BP / 8];
+#pragma unroll
+    for (int k = 0; k < BP / 8; ++k) {  // BP x 256 bf16 = BP*64 chunks
+      const int e = tv + NT * k;
+      h1r[k] = ld_wt(pb.h1x + (int64_t)p * BP * PD1 + (int64_t)e * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tv + NT * k;
+      *reinterpret_cast<unsigned long long*>(sW2 + (e >> 6) * LDH + 4 * (e & 63)) = w2r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < BP / 8; ++k) {
+      const int e = tv + NT * k;
+      *reinterpret_cast<unsigned long long*>(sH1 + (e >> 6) * LDH + 4 * (e & 63)) = h1r[k];
+    }
+    lds_barrier();
+
+    // ---- H2 = relu(H1 · W2ᵀ + b2): wave w owns output columns 16w..16w+15
+    {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+#pragma unroll
+      for (int ks = 0; ks < PD1 / 32; ++ks) {
+        const bf16x8 bw = ld8(sW2 + (16 * wave + c) * LDH + 32 * ks + 8 * h);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_bf16(ld8(sH1 + (16 * mt + c) * LDH + 32 * ks + 8 * h), bw, acc[mt]);
+      }
+      const int o2 = 16 * wave + c;
+      const float bias = sB2[o2];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = 16 * mt + 4 * h + i;
+          sH2[b * LD2 + o2] = (bf16)(b < rows ? fmaxf(acc[mt][i] + bias, 0.f) : 0.f);
+        }
+    }
+    lds_barrier();
+    PE_STAMP(1, t, 3);
+    // ---- logits partials (waves 0..3: K = o2 block of the wave, W3 before this step's update)
+    if (wave < 4) {
+      bf16x8 bw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bw[j] = (bf16)w3[j];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16* hp = sH2 + (16 * mt + c) * LD2 + 32 * wave + 4 * h;
+        sRed[(wave * MT + mt) * 64 + lane] = mfma_bf16(cat8(*reinterpret_cast<const bf16x4*>(hp), *reinterpret_cast<const bf16x4*>(hp + 16)), bw, zero4());
+      }
+    }
+    lds_barrier();
+    // ---- log-softmax + NLL + argmax + dlogits (wave w < MT: batch rows 16w..16w+15)
+    if (wave < MT) {
+      f32x4 lg = sRed[wave * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) lg += sRed[(w * MT + wave) * 64 + lane];
+      const float b3 = sB3[c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * wave + 4 * h + i;
+        const bool rvalid = b < rows;
+        const int y = rvalid ? a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b] : -1;
+        const float logit = cin ? lg[i] + b3 : -INFINITY;
+        const float mx = warp_max16(logit);
+        const float se = warp_sum16(cin ? __expf(logit - mx) : 0.f);
+        const float logp = logit - (mx + __logf(se));
+        int cand = (cin && logit == mx) ? c : 16;
+        cand = min(cand, __shfl_xor(cand, 1));
+        cand = min(cand, __shfl_xor(cand, 2));
+        cand = min(cand, __shfl_xor(cand, 4));
+        cand = min(cand, __shfl_xor(cand, 8));
+        if (rvalid && c == y) loss_acc -= logp;
+        if (rvalid && c == 0) correct_acc += (cand == y) ? 1.f : 0.f;
+        const float d = (rvalid && cin) ? (__expf(logp) - (c == y ? 1.f : 0.f)) / (float)rows : 0.f;
+        sDlog[b * LDL + c] = (bf16)d;
+      }
+    }
+    lds_barrier();
+    PE_STAMP(1, t, 4);
+    // ---- dH2 = dlogits · W3 ⊙ [H2 > 0] (wave w: columns 16w..16w+15; K = classes padded to 32)
+    {
+      const bf16x8 bw = frag_b_tr(sW3, LDW3, 0, 16 * wave);
+      const int o2 = 16 * wave + c;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 acc = mfma_bf16(ld8(sDlog + (16 * mt + c) * LDL + 8 * h), bw, zero4());
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = 16 * mt + 4 * h + i;
+          sDH2[b * LD2 + o2] = (bf16)((float)sH2[b * LD2 + o2] > 0.f ? acc[i] : 0.f);
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < BP / 16; ++k) {
+      const int e = tv + NT * k;
+      const int b = e >> 5, q = e & 31;
+      st_wt(pb.dh2x + ((int64_t)p * BP + b) * PD2 + 4 * q, *reinterpret_cast<const unsigned long long*>(sDH2 + b * LD2 + 4 * q));
+    }
+    publish(pb.flags, p, F_DH2, (unsigned)(t + 1));
+    PE_STAMP(1, t, 5);
+
+    // ---- off the critical path: dW3 (waves 0..3), db2 (waves 4,5), db3 (wave 6)
+    if (wave < 4) {
+      float gr[8];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int kb = 0; kb < BP / 32; ++kb)
+          acc = mfma_bf16(frag_b_tr(sH2, LD2, 32 * kb, 32 * wave + 16 * tt), frag_b_tr(sDlog, LDL, 32 * kb, 0), acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
+      }
+      if (cin) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          upd(a, gr[j], w3[j], m3[j], v3[j], bc1, bc2s);
+          sW3[c * LDW3 + 32 * wave + kappa(h, j)] = (bf16)w3[j];
+        }
+      }
+    } else if (wave < 6) {
+      const int o2 = tid - 256;
+      float db = 0.f;
+      for (int b = 0; b < BP; ++b) db += (float)sDH2[b * LD2 + o2];
+      upd(a, db, sB2[o2], sB2[PD2 + o2], sB2[2 * PD2 + o2], bc1, bc2s);
+    } else if (wave == 6 && lane < D3) {
+      float db = 0.f;
+      for (int b = 0; b < BP; ++b) db += (float)sDlog[b * LDL + lane];
+      upd(a, db, sB3[lane], sB3[16 + lane], sB3[32 + lane], bc1, bc2s);
+    }
+    __syncthreads();
+    PE_STAMP(1, t, 6);
+  }
+
+  // ---- write back W3 / b2 / b3 and the epoch's loss / accuracy sums
+  if (wave < 4 && cin) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t idx = pS + a.off_w3 + (int64_t)c * PD2 + 32 * wave + kappa(h, j);
+      a.params[idx] = w3[j];
+      a.m[idx] = m3[j];
+      if (adam) a.v[idx] = v3[j];
+      a.shadow[idx] = (bf16)w3[j];
+    }
+  }
+  if (tid < PD2) {
+    const int64_t idx = pS + a.off_b2 + tid;
+    a.params[idx] = sB2[tid];
+    a.m[idx] = sB2[PD2 + tid];
+    if (adam) a.v[idx] = sB2[2 * PD2 + tid];
+    a.shadow[idx] = (bf16)sB2[tid];
+  } else if (tid < PD2 + 16 && tid - PD2 < D3) {
+    const int k = tid - PD2;
+    const int64_t idx = pS + a.off_b3 + k;
+    a.params[idx] = sB3[k];
+    a.m[idx] = sB3[16 + k];
+    if (adam) a.v[idx] = sB3[32 + k];
+    a.shadow[idx] = (bf16)sB3[k];
+  }
+  if (wave < MT) {
+    const float l = wave_sum(loss_acc), cr = wave_sum(correct_acc);
+    if (lane == 0) {
+      atomicAdd(&a.loss_acc[p], l);
+      atomicAdd(&a.correct_acc[p], (int)(cr + 0.5f));
+    }
+  }
+}
+
+template <int BP>
+__global__ __launch_bounds__(NT) void mlp_persistent_epoch(MLPArgs a, MLPPersistBufs pb) {
+  extern __shared__ __attribute__((aligned(16))) char smem_pe[];
+  const int b = blockIdx.x;
+  const int slot = b & 7, idx = b >> 3;
+  const int p = (idx / ROLES) * 8 + slot;
+  const int role = idx % ROLES;
+  if (p >= a.P) return;
+  const int4 ctl = a.ctl[p];
+  if (!ctl.x || ctl.y <= 0) return;
+  if (role < NG)
+    owner<BP>(a, pb, p, role, smem_pe);
+  else
+    head<BP>(a, pb, p, smem_pe);
+}
+
+}  // namespace
+
+bool mlp_persistent_supported(const MLPArgs& a) {
+  if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
+  if (a.D0 % 8 != 0 || (a.D0 + 31) / 32 > KS1_MAX) return false;
+  if (a.Bpad != 32 && a.Bpad != 64) return false;
+  if (a.anchor != nullptr || a.cg != nullptr || a.cl != nullptr) return false;
+  if (a.opt.kind == 1 && a.opt.momentum != 0.f) return false;  // SGD momentum buffer: 3-launch path
+  const size_t lds = owner_lds(a.Bpad, a.D0).total > head_lds(a.Bpad).total ? owner_lds(a.Bpad, a.D0).total : head_lds(a.Bpad).total;
+  return lds <= 160 * 1024;
+}
+
+size_t mlp_persistent_bytes(int P, int Bpad) { return (size_t)P * ((size_t)Bpad * PD1 + (size_t)PD2 * PD1 + (size_t)Bpad * PD2) * sizeof(bf16); }
+size_t mlp_persistent_flag_bytes(int P) { return (size_t)P * FLAGS_PER_PEER * FLAG_LINE * sizeof(unsigned); }
+int mlp_persistent_blocks(int P) { return 8 * ROLES * ((P + 7) / 8); }
+
+static size_t persistent_lds(const MLPArgs& a) {
+  const size_t lo = owner_lds(a.Bpad, a.D0).total, lh = head_lds(a.Bpad).total;
+  return lo > lh ? lo : lh;
+}
+
+hipError_t mlp_persistent_prepare(const MLPArgs& a) {
+  const int lds = (int)persistent_lds(a);
+  if (a.Bpad == 64) return hipFuncSetAttribute((const void*)mlp_persistent_epoch<64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  return hipFuncSetAttribute((const void*)mlp_persistent_epoch<32>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
+  if (e != hipSuccess) return e;
+  const size_t lds = persistent_lds(a);
+  const dim3 grid(mlp_persistent_blocks(a.P)), block(NT);
+  if (a.Bpad == 64)
+    hipLaunchKernelGGL(mlp_persistent_epoch<64>, grid, block, lds, s, a, pb);
+  else
+    hipLaunchKernelGGL(mlp_persistent_epoch<32>, grid, block, lds, s, a, pb);
+  return hipGetLastError();
+}

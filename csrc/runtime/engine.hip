@@ -16,6 +16,8 @@
 
 #include "../kernels/fl_ops.h"
 #include "../kernels/mlp_fused.h"
+#include "../kernels/mlp_persistent.h"
+#include <cstdlib>
 
 static thread_local std::string g_last_error;
 
@@ -36,15 +38,17 @@ namespace {
 struct CtlUpload {
   int4 ctl[MLP_CTL_MAX];
   int active[MLP_CTL_MAX];
+  unsigned long long seed;  // epoch shuffle key (in-kernel permutation)
   int P;
   int with_active;
 };
-__global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active) {
+__global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long long* seed) {
   const int p = threadIdx.x;
   if (p < u.P) {
     ctl[p] = u.ctl[p];
     if (u.with_active) active[p] = u.active[p];
   }
+  if (p == 0) *seed = u.seed;
 }
 
 #define MLP_RING 16
@@ -52,6 +56,7 @@ struct ResultSlot {
   float* loss = nullptr;
   int* correct = nullptr;
   int* conf = nullptr;
+  int* err = nullptr;
   hipEvent_t ev = nullptr;
 };
 
@@ -67,6 +72,8 @@ struct MLPEngine {
   int* d_active = nullptr;
   int* d_t0 = nullptr;
   int4* d_ctl = nullptr;
+  unsigned long long* d_seed = nullptr;
+  unsigned long long seed_host = 0;
   std::vector<int4> ctl_host;
   float* d_loss = nullptr;
   int* d_correct = nullptr;
@@ -75,6 +82,17 @@ struct MLPEngine {
   std::mutex mu;
   int max_test_rows = 0;
   ResultSlot ring[MLP_RING];  // pinned host result buffers + completion events
+  // weight-stationary persistent epoch (mlp_persistent.hip): exchange buffers + mode
+  MLPPersistBufs pb{};
+  int persist_mode = -1;  // -1 auto (eligible configs), 0 off
+  int num_cus = 0;
+  bool graph_persistent = false;
+
+  bool use_persistent() const {
+    if (persist_mode == 0 || pb.h1x == nullptr) return false;
+    if (a.P * 17 > num_cus) return false;  // every gang must be co-resident (one workgroup per CU)
+    return mlp_persistent_supported(a);
+  }
 
   ~MLPEngine() {
     if (exec) hipGraphExecDestroy(exec);
@@ -88,6 +106,7 @@ struct MLPEngine {
       if (r.loss) hipHostFree(r.loss);
       if (r.correct) hipHostFree(r.correct);
       if (r.conf) hipHostFree(r.conf);
+      if (r.err) hipHostFree(r.err);
     }
   }
 
@@ -96,6 +115,8 @@ struct MLPEngine {
       CHECK_HIP(hipHostMalloc((void**)&r.loss, sizeof(float) * a.P, hipHostMallocDefault));
       CHECK_HIP(hipHostMalloc((void**)&r.correct, sizeof(int) * a.P, hipHostMallocDefault));
       CHECK_HIP(hipHostMalloc((void**)&r.conf, sizeof(int) * a.P * 256, hipHostMallocDefault));
+      CHECK_HIP(hipHostMalloc((void**)&r.err, sizeof(int), hipHostMallocDefault));
+      *r.err = 0;
       CHECK_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     }
     return 0;
@@ -105,11 +126,12 @@ struct MLPEngine {
     CtlUpload u;
     u.P = a.P;
     u.with_active = active_host != nullptr;
+    u.seed = seed_host;
     for (int p = 0; p < a.P; ++p) {
       u.ctl[p] = ctl_host[p];
       u.active[p] = active_host ? active_host[p] : 0;
     }
-    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(MLP_CTL_MAX), 0, s, u, d_ctl, d_active);
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(MLP_CTL_MAX), 0, s, u, d_ctl, d_active, d_seed);
     CHECK_HIP(hipGetLastError());
     return 0;
   }
@@ -134,7 +156,19 @@ struct MLPEngine {
     if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
     CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
     mlp_launch_gather_epoch(a, cap_stream);
-    for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
+    graph_persistent = use_persistent();
+    if (graph_persistent) {
+      hipError_t le = mlp_launch_persistent_epoch(a, pb, cap_stream);
+      if (le != hipSuccess) {
+        hipGraph_t g = nullptr;
+        hipStreamEndCapture(cap_stream, &g);
+        if (g) hipGraphDestroy(g);
+        g_last_error = std::string("persistent epoch launch: ") + hipGetErrorString(le);
+        return 1;
+      }
+    } else {
+      for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
+    }
     hipError_t e = hipStreamEndCapture(cap_stream, &graph);
     if (e != hipSuccess) {
       g_last_error = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
@@ -167,6 +201,35 @@ int myfyp_stacked_weighted_sum(float* out, const float* stacked, int P, int64_t 
 }
 int myfyp_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64_t ld, const float* mask, void* stream) {
   fl_broadcast_rows(stacked, src, P, n, ld, mask, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// FedAvg of a stacked [P][ld] group: weights / mask by value (P <= 64); out has n + 1 floats.
+int myfyp_fedavg_stacked_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w_host, void* stream) {
+  if (P < 1 || P > FEDAVG_MAX_PEERS) {
+    g_last_error = "fedavg_stacked: 1..64 rows";
+    return 2;
+  }
+  FedAvgWeights w{};
+  double sum = 0.0;
+  for (int p = 0; p < P; ++p) {
+    w.w[p] = w_host[p];
+    sum += w_host[p];
+  }
+  w.wsum = (float)sum;
+  fl_fedavg_reduce(out, stacked, P, n, ld, w, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_fedavg_stacked_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, const float* mask_host, void* stream) {
+  if (P < 1 || P > FEDAVG_MAX_PEERS) {
+    g_last_error = "fedavg_stacked: 1..64 rows";
+    return 2;
+  }
+  unsigned long long mask = 0;
+  for (int p = 0; p < P; ++p)
+    if (mask_host[p] != 0.f) mask |= 1ull << p;
+  fl_fedavg_apply(stacked, out, P, n, ld, mask, (hipStream_t)stream);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -235,11 +298,32 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
   rc |= e->alloc(&p, (size_t)P * 4); e->d_active = (int*)p; a.active = e->d_active;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_t0 = (int*)p; a.t0 = e->d_t0;
   rc |= e->alloc(&p, (size_t)P * 16); e->d_ctl = (int4*)p; a.ctl = e->d_ctl;
+  rc |= e->alloc(&p, 16); e->d_seed = (unsigned long long*)p; a.seed = e->d_seed;
   e->ctl_host.assign(P, int4{0, 0, 0, 0});
   rc |= e->alloc(&p, (size_t)P * 4); e->d_loss = (float*)p; a.loss_acc = e->d_loss;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_correct = (int*)p; a.correct_acc = e->d_correct;
   rc |= e->alloc(&p, (size_t)P * 256 * 4); e->d_conf = (int*)p; a.conf = e->d_conf;
   rc |= e->alloc_ring();
+  {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&e->num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const char* env = getenv("MYFYP_MLP_PERSISTENT");
+    if (env && env[0] == '0') e->persist_mode = 0;
+    if (D1 == 256 && D2 == 128 && (a.Bpad == 32 || a.Bpad == 64)) {
+      const size_t xb = mlp_persistent_bytes(P, a.Bpad);
+      rc |= e->alloc(&p, xb);
+      e->pb.h1x = (bf16*)p;
+      e->pb.w2x = e->pb.h1x + (size_t)P * a.Bpad * 256;
+      e->pb.dh2x = e->pb.w2x + (size_t)P * 128 * 256;
+      e->pb.flag_bytes = mlp_persistent_flag_bytes(P);
+      rc |= e->alloc(&p, e->pb.flag_bytes);
+      e->pb.flags = (unsigned*)p;
+      rc |= e->alloc(&p, 16);
+      e->pb.err = (int*)p;
+      if (mlp_persistent_prepare(a) != hipSuccess) e->persist_mode = 0;
+    }
+  }
   if (rc) {
     delete e;
     return nullptr;
@@ -329,10 +413,51 @@ int mlp_engine_begin(void* h, const int* active_host, void* stream) {
   if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
+  if (e->pb.err) CHECK_HIP(hipMemsetAsync(e->pb.err, 0, 16, s));
   mlp_launch_sync_shadow(e->a, s);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+
+// Zero the Adam moments of every slot (fresh optimizer state per fit; one memset node each).
+int mlp_engine_zero_state(void* h, void* stream) {
+  auto* e = (MLPEngine*)h;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t bytes = (size_t)e->a.P * e->a.S * sizeof(float);
+  CHECK_HIP(hipMemsetAsync(e->a.m, 0, bytes, s));
+  if (e->a.v) CHECK_HIP(hipMemsetAsync(e->a.v, 0, bytes, s));
+  return 0;
+}
+
+// Epoch shuffle: native = 1 draws every peer's permutation inside the gather kernel (keyed
+// Feistel permutation, key uploaded per epoch with the control words); 0 reads `perm`.
+int mlp_engine_set_shuffle(void* h, int native) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (native != e->a.shuffle_native) {
+    e->a.shuffle_native = native;
+    e->invalidate();
+  }
+  return 0;
+}
+int mlp_engine_set_epoch_seed(void* h, unsigned long long seed) {
+  ((MLPEngine*)h)->seed_host = seed;
+  return 0;
+}
+
+// Persistent-epoch mode: -1 auto (default; MYFYP_MLP_PERSISTENT=0 turns it off), 0 off.
+int mlp_engine_set_persistent(void* h, int mode) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (mode != e->persist_mode) {
+    e->persist_mode = mode;
+    e->invalidate();
+  }
+  return 0;
+}
+
+// 1 if the next epoch runs as the persistent kernel.
+int mlp_engine_uses_persistent(void* h) { return ((MLPEngine*)h)->use_persistent() ? 1 : 0; }
 
 // One local epoch for every active peer: a single graph replay (captured on first use).
 int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
@@ -356,7 +481,11 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
   if (e->upload(s, nullptr)) return 1;
   mlp_launch_gather_epoch(e->a, s);
-  for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
+  if (e->use_persistent()) {
+    CHECK_HIP(mlp_launch_persistent_epoch(e->a, e->pb, s));
+  } else {
+    for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
+  }
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -368,6 +497,10 @@ int mlp_engine_stats_async(void* h, int slot, void* stream) {
   ResultSlot& r = e->ring[slot % MLP_RING];
   CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
+  if (e->pb.err)
+    CHECK_HIP(hipMemcpyAsync(r.err, e->pb.err, sizeof(int), hipMemcpyDeviceToHost, s));
+  else
+    *r.err = 0;
   CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
@@ -388,6 +521,7 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipMemcpyAsync(r.conf, e->d_conf, sizeof(int) * e->a.P * 256, hipMemcpyDeviceToHost, s));
+  *r.err = 0;
   CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
@@ -400,6 +534,10 @@ int mlp_engine_fetch(void* h, int slot, float* loss_host, int* correct_host, int
   memcpy(loss_host, r.loss, sizeof(float) * e->a.P);
   memcpy(correct_host, r.correct, sizeof(int) * e->a.P);
   if (conf_host) memcpy(conf_host, r.conf, sizeof(int) * e->a.P * 256);
+  if (*r.err != 0) {
+    g_last_error = "persistent MLP epoch gave up (a gang workgroup was not resident or a hand-off timed out)";
+    return 3;
+  }
   return 0;
 }
 

@@ -51,6 +51,15 @@ def _lib():
     return _native.load(required=True)
 
 
+def fast_lib():
+    """Native library with GIL-holding bindings for launch-only entry points (see _native.load_fast)."""
+    return _native.load_fast()
+
+
+def check(rc: int, what: str) -> None:
+    _native.check(rc, what)
+
+
 # ---------------------------------------------------------------------------------------------
 # aggregation
 # ---------------------------------------------------------------------------------------------

@@ -18,6 +18,7 @@ import threading
 from typing import Optional
 
 _LIB: Optional[ctypes.CDLL] = None
+_FAST: Optional[ctypes.PyDLL] = None
 _LOCK = threading.Lock()
 _ERR: Optional[str] = None
 
@@ -67,6 +68,13 @@ _SIGNATURES = {
     "mlp_engine_eval_async": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "mlp_engine_fetch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_ring_size": (c_int, []),
+    "mlp_engine_set_persistent": (c_int, [c_void_p, c_int]),
+    "mlp_engine_zero_state": (c_int, [c_void_p, c_void_p]),
+    "mlp_engine_set_shuffle": (c_int, [c_void_p, c_int]),
+    "mlp_engine_set_epoch_seed": (c_int, [c_void_p, ctypes.c_uint64]),
+    "myfyp_fedavg_stacked_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "myfyp_fedavg_stacked_apply": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "mlp_engine_uses_persistent": (c_int, [c_void_p]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
 }
 
@@ -95,6 +103,29 @@ def load(required: bool = False) -> Optional[ctypes.CDLL]:
     if _LIB is None and required:
         raise RuntimeError(_ERR or "native library unavailable")
     return _LIB
+
+
+def load_fast() -> ctypes.PyDLL:
+    """The same library bound as a ``PyDLL``: calls keep the GIL. Use it ONLY for entry points that
+    merely enqueue work (launches, async copies, parameter setters). Releasing and re-taking the GIL
+    around a microsecond-long call costs far more than the call when several peer threads run
+    Python concurrently: the caller queues behind whichever thread got the GIL (up to the
+    interpreter's switch interval); blocking calls (event waits) go through :func:`load`."""
+    global _FAST
+    if _FAST is not None:
+        return _FAST
+    load(required=True)
+    with _LOCK:
+        if _FAST is None:
+            lib = ctypes.PyDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in _SIGNATURES.items():
+                fn = getattr(lib, name, None)
+                if fn is None:
+                    continue
+                fn.restype = res
+                fn.argtypes = args
+            _FAST = lib
+    return _FAST
 
 
 def available() -> bool:

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 import pickle
 import threading
 import time
@@ -197,6 +198,8 @@ class Federation:
         """Initialise from ``torchrun`` env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
         if cls._instance is not None:
             return cls._instance
+        if Settings.GIL_SWITCH_INTERVAL:
+            sys.setswitchinterval(float(Settings.GIL_SWITCH_INTERVAL))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))

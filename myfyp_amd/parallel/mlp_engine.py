@@ -19,6 +19,7 @@ Numerics: bf16 MFMA operands, fp32 accumulation, fp32 master weights and optimiz
 from __future__ import annotations
 
 import ctypes
+import random
 import threading
 import time
 from typing import Dict, List, Optional, Set, Tuple
@@ -142,6 +143,10 @@ class MLPGroup:
         self.extras: Dict[str, torch.Tensor] = {}
         self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
         self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
+        # weight-stationary persistent epoch kernel (csrc/kernels/mlp_persistent.hip): None = auto
+        # (used whenever the shape/optimizer is eligible), False = always the 3-launch step path
+        self.persistent: Optional[bool] = None
+        self._fedavg_buf: Optional[torch.Tensor] = None
         self._alloc(capacity)
         self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
         self.eval_gang = _Gang(self._run_eval_batch, lambda: set(self.handles))
@@ -213,9 +218,23 @@ class MLPGroup:
             _native.check(
                 lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
             )
+        if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
+            _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
         if self._bound_version != self._data_version:
             self._bind_data()
             self._bound_version = self._data_version
+
+    def fedavg_buffer(self) -> torch.Tensor:
+        """Device scratch of numel + 1 floats for the stacked FedAvg (weighted sum | Σw)."""
+        if self._fedavg_buf is None or self._fedavg_buf.numel() != self.numel + 1:
+            self._fedavg_buf = torch.empty(self.numel + 1, dtype=torch.float32, device=self.device)
+        return self._fedavg_buf
+
+    def uses_persistent(self) -> bool:
+        """True if the next local epoch runs as the weight-stationary persistent kernel."""
+        with self.lock:
+            self._ensure_engine()
+            return bool(_native.load(required=True).mlp_engine_uses_persistent(self._engine))
 
     def _bind_data(self) -> None:
         """(Re)build the per-peer data pointer tables (uploads each peer's split once)."""
@@ -241,7 +260,6 @@ class MLPGroup:
         self.nmax = max(1, max(ns) if ns else 1)
         self.max_steps = (self.nmax + self.B - 1) // self.B
         self.perm = torch.zeros(cap, self.nmax, dtype=torch.int32, device=dev)
-        self._perm_mask = torch.arange(self.nmax, device=dev).unsqueeze(0) >= torch.tensor(ns, device=dev).unsqueeze(1)
         t = self._tables
         _native.check(lib.mlp_engine_set_train_data(self._engine, _p(t["Xp"]), _p(t["Yp"]), _p(t["n"]), _p(self.perm), self.nmax, self.max_steps), "set_train_data")
         _native.check(lib.mlp_engine_set_test_data(self._engine, _p(t["Xtp"]), _p(t["Ytp"]), _p(t["nt"]), max(nts) if nts else 0), "set_test_data")
@@ -283,37 +301,37 @@ class MLPGroup:
                     else:
                         cg[slot].zero_()
                         cl[slot].zero_()
+            fast = _native.load_fast()
             _native.check(
-                lib.mlp_engine_set_optimizer(
+                fast.mlp_engine_set_optimizer(
                     self._engine, kind, float(spec.get("lr", 1e-3)), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
                     float(spec.get("eps", 1e-8)), float(spec.get("weight_decay", 0.0)), float(spec.get("momentum", 0.0)),
                     int(bool(spec.get("nesterov", False))), mu,
                 ),
                 "set_optimizer",
             )
-            _native.check(lib.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
+            _native.check(fast.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
             active = np.zeros(self.capacity, dtype=np.int32)
             for slot in batch:
                 active[slot] = 1
             # fresh optimizer state per fit (Lightning semantics); slots not training this round are
-            # zeroed as well — they start fresh when they next train — so this is 2 launches, not 2P
-            self.m.zero_()
-            self.v.zero_()
-            _native.check(lib.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
+            # zeroed as well — they start fresh when they next train — so this is 2 memsets, not 2P
+            _native.check(fast.mlp_engine_zero_state(self._engine, stream), "zero_state")
+            _native.check(fast.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
             steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
-            keys = torch.empty(self.capacity, self.nmax, device=self.device)
-            run = lib.mlp_engine_run_epoch_eager if self.eager else lib.mlp_engine_run_epoch
+            # epoch order: drawn on the device inside the gather kernel (keyed Feistel permutation
+            # per peer, key from the seeded Python RNG) unless a test pins explicit permutations
+            _native.check(fast.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
+            run = fast.mlp_engine_run_epoch_eager if self.eager else fast.mlp_engine_run_epoch
             for ep in range(epochs):
                 if self.perm_fn is not None:
                     self.perm.copy_(self.perm_fn(ep))
                 else:
-                    keys.uniform_()
-                    keys.masked_fill_(self._perm_mask, 2.0)
-                    self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
+                    _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
                 t0 = (steps_pe * ep).astype(np.int32)
                 _native.check(run(self._engine, t0.ctypes.data, stream), "run_epoch")
             k = self._take_slot()
-            _native.check(lib.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
+            _native.check(fast.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=False))
         out = {}
         for slot in batch:
@@ -356,7 +374,7 @@ class MLPGroup:
             for slot in batch:
                 active[slot] = 1
             k = self._take_slot()
-            _native.check(lib.mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
+            _native.check(_native.load_fast().mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=True))
         D3 = self.dims[3]
         return {slot: raw.map(lambda r, s=slot: (float(r[0][s]) / max(1, self.n_test[s]), r[2][s, :D3, :D3].copy())) for slot in batch}
@@ -368,6 +386,38 @@ class MLPGroup:
 
     def default_expected(self) -> Set[int]:
         return set(self.handles)
+
+
+def feistel_perm(x: int, n: int, key: int) -> int:
+    """Host mirror of the gather kernel's epoch permutation (``feistel_perm`` in mlp_fused.hip):
+    4-round balanced Feistel network on the smallest even bit width covering n, cycle-walked."""
+    if n <= 1:
+        return 0
+    bits = max(2, (n - 1).bit_length())
+    bits += bits & 1
+    half = bits // 2
+    mask = (1 << half) - 1
+    k0, k1 = key & 0xFFFFFFFF, (key >> 32) & 0xFFFFFFFF
+
+    def mix32(v: int) -> int:
+        v &= 0xFFFFFFFF
+        v ^= v >> 16
+        v = (v * 0x7FEB352D) & 0xFFFFFFFF
+        v ^= v >> 15
+        v = (v * 0x846CA68B) & 0xFFFFFFFF
+        v ^= v >> 16
+        return v
+
+    y = x
+    while True:
+        lo, hi = y & mask, y >> half
+        left, right = hi, lo
+        for r in range(4):
+            f = mix32(right ^ (k1 if r & 1 else k0) ^ ((0x9E3779B9 * (r + 1)) & 0xFFFFFFFF)) & mask
+            left, right = right, left ^ f
+        y = (left << half) | right
+        if y < n:
+            return y
 
 
 class _RetargetableFlat:

@@ -78,24 +78,36 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     contributors = [a for a, w in zip(addrs, weights) if w > 0]
     group = _stacked_group(learners)
     dev = learners[0].flat_params().device
-    if group is not None:
-        # weights/mask go up through pinned memory with non-blocking copies and nothing is read
-        # back: the host never waits for the GPU here (the total weight stays on the device)
-        pin = dev.type == "cuda"
-        wm = torch.zeros(2, group.capacity, dtype=torch.float32, pin_memory=pin)
+    if group is not None and dev.type == "cuda":
+        # one native reduction kernel (weights as kernel arguments) -> RCCL all-reduce over the
+        # n + 1 floats (weighted sum | Σw) -> one native normalise-and-broadcast kernel; no host
+        # tensor traffic and nothing the host waits on
+        w = np.zeros(group.capacity, dtype=np.float32)
+        mask = np.zeros(group.capacity, dtype=np.float32)
+        for lr, wt in zip(learners, weights):
+            w[lr._engine.slot] = wt
+            mask[lr._engine.slot] = 1.0
+        n = group.numel
+        buf = group.fedavg_buffer()
+        fast = ops.fast_lib()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, stream), "fedavg_reduce")
+        fed.all_reduce_(buf)
+        ops.check(fast.myfyp_fedavg_stacked_apply(group.params.data_ptr(), buf.data_ptr(), group.capacity, n, group.S, mask.ctypes.data, stream), "fedavg_apply")
+        total_w = float(sum(weights))  # local share; the global Σw stays on the device (buf[n])
+    elif group is not None:
+        wm = torch.zeros(2, group.capacity, dtype=torch.float32)
         for lr, wt in zip(learners, weights):
             wm[0, lr._engine.slot] = wt
             wm[1, lr._engine.slot] = 1.0
-        wsum_local = float(sum(weights))
-        wm_d = wm.to(dev, non_blocking=True)
         n = group.numel
         buf = torch.empty(n + 1, dtype=torch.float32, device=dev)
-        ops.stacked_weighted_sum(group.params[:, :n], wm_d[0], buf[:n], 1.0)
-        buf[n:].fill_(wsum_local)
+        ops.stacked_weighted_sum(group.params[:, :n], wm[0], buf[:n], 1.0)
+        buf[n:].fill_(float(sum(weights)))
         fed.all_reduce_(buf)
         total = buf[n:].clone()
         buf[:n].div_(total.clamp_min(1e-12))
-        ops.broadcast_rows(buf[:n], group.params[:, :n], wm_d[1])
+        ops.broadcast_rows(buf[:n], group.params[:, :n], wm[1])
         total_w = total
     else:
         states = [state_tensors(lr) for lr in learners]

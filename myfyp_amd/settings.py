@@ -92,6 +92,9 @@ class Settings:
     COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
     BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
     SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
+    # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
+    # GIL over often, and a thread returning from a device call waits up to this long for it
+    GIL_SWITCH_INTERVAL: float | None = 2e-4
 
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
@@ -150,6 +153,7 @@ class Settings:
             "COLLECTIVE_TIMEOUT": "COLLECTIVE_TIMEOUT",
             "BUCKET_BYTES": "BUCKET_BYTES",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
+            "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
         }
     )
 

@@ -118,9 +118,11 @@ def _reference_mlp_run(module, x, y, perm, B, lr, steps):
         opt.step()
 
 
+@pytest.mark.parametrize("persistent", [None, False], ids=["persistent", "steps"])
 @pytest.mark.parametrize("B", [32, 48])
-def test_fused_mlp_engine_matches_autograd(dev, B):
-    """One local epoch of the grouped engine (2 peers, SGD) vs per-peer fp32 autograd."""
+def test_fused_mlp_engine_matches_autograd(dev, B, persistent):
+    """One local epoch of the grouped engine (2 peers, SGD) vs per-peer fp32 autograd, on the
+    weight-stationary persistent epoch kernel and on the 3-launch step path."""
     import copy
 
     from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
@@ -145,6 +147,8 @@ def test_fused_mlp_engine_matches_autograd(dev, B):
         learners.append(TorchLearner(TorchModel(m), parts[i], f"p{i}", batch_size=B))
     assert all(lr_._engine is not None for lr_ in learners)
     group = learners[0]._engine.group
+    group.persistent = persistent
+    assert group.uses_persistent() == (persistent is not False)
     n = [parts[i].get_num_samples() for i in range(2)]
     perms = [torch.randperm(n[i], generator=torch.Generator().manual_seed(i)) for i in range(2)]
 
@@ -181,7 +185,8 @@ def test_fused_mlp_engine_matches_autograd(dev, B):
     MLPGroup.reset_all()
 
 
-def test_fused_mlp_single_step_gradients(dev):
+@pytest.mark.parametrize("persistent", [None, False], ids=["persistent", "steps"])
+def test_fused_mlp_single_step_gradients(dev, persistent):
     """Per-parameter gradient of ONE fused step (SGD, grad = Δw/lr) vs autograd, 3 peers, B=40."""
     import copy
     import threading
@@ -206,6 +211,8 @@ def test_fused_mlp_single_step_gradients(dev):
         refs.append(copy.deepcopy(m).to(dev))
         learners.append(TorchLearner(TorchModel(m), parts[i], f"g{i}", batch_size=B))
     g = learners[0]._engine.group
+    g.persistent = persistent
+    assert g.uses_persistent() == (persistent is not False)
     n = [parts[i].get_num_samples() for i in range(P)]
 
     def perm_fn(ep):
@@ -228,4 +235,59 @@ def test_fused_mlp_single_step_gradients(dev):
             cos = F.cosine_similarity(ge.flatten(), gr.flatten(), dim=0).item()
             rel = ((ge - gr).norm() / (gr.norm() + 1e-12)).item()
             assert cos > 0.995 and rel < 0.08, f"peer {i} {name}: cos {cos:.4f} rel {rel:.4f}"
+    MLPGroup.reset_all()
+
+
+@pytest.mark.parametrize("B", [64, 32])
+def test_persistent_epoch_matches_step_path_adam(dev, B):
+    """Several Adam epochs on 3 peers: persistent epoch kernel vs 3-launch step path from identical
+    weights and batch order (same bf16 rounding points; only accumulation order differs)."""
+    import threading
+
+    from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
+    from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
+    from myfyp_amd.learning.frameworks.torch import TorchLearner, TorchModel
+    from myfyp_amd.models import MLP
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+    from myfyp_amd.settings import Settings
+
+    Settings.GANG_WINDOW = 5.0
+    P = 3
+    parts = synthetic_mnist(900, 100, seed=5).generate_partitions(P, RandomIIDPartitionStrategy)
+    results = {}
+    for mode in (None, False):
+        MLPGroup.reset_all()
+        learners = []
+        for i in range(P):
+            m = MLP(seed=30 + i)
+            m.optimizer_spec = lambda: {"name": "adam", "lr": 1e-3}
+            learners.append(TorchLearner(TorchModel(m), parts[i], f"a{i}", batch_size=B))
+        g = learners[0]._engine.group
+        g.persistent = mode
+        assert g.uses_persistent() == (mode is not False)
+        n = [parts[i].get_num_samples() for i in range(P)]
+
+        def perm_fn(ep, g=g, learners=learners, n=n):
+            out = torch.zeros(g.capacity, g.nmax, dtype=torch.int32)
+            for i, l in enumerate(learners):
+                out[l._engine.slot, : n[i]] = torch.randperm(n[i], generator=torch.Generator().manual_seed(100 * ep + i)).to(torch.int32)
+            return out.to(dev)
+
+        g.perm_fn = perm_fn
+        for lr_ in learners:
+            lr_.set_epochs(2)
+        ts = [threading.Thread(target=l.fit) for l in learners]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        torch.cuda.synchronize()
+        results[mode] = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
+        results[(mode, "loss")] = [l.evaluate_raw()[0] for l in learners]
+    init = [[p.detach().clone() for p in MLP(seed=30 + i).parameters()] for i in range(P)]
+    for i in range(P):
+        for k, (pp, ps, p0) in enumerate(zip(results[None][i], results[False][i], init[i])):
+            d_p, d_s = pp.cpu() - p0, ps.cpu() - p0
+            rel = ((d_p - d_s).norm() / (d_s.norm() + 1e-12)).item()
+            assert rel < 0.05, f"peer {i} param {k}: persistent vs step-path update mismatch {rel:.4f}"
+        lp, ls = results[(None, "loss")][i], results[(False, "loss")][i]
+        assert abs(lp - ls) / ls < 0.05, (lp, ls)
     MLPGroup.reset_all()

@@ -1,6 +1,7 @@
 """CPU reference path of the fused ops (the GPU kernels are checked against the same math in
 test_kernels_gpu.py)."""
 
+import pytest
 import torch
 
 from myfyp_amd import ops
@@ -47,3 +48,18 @@ def test_reductions_reference():
     t = a.clone()
     ops.scale_add_noise(t, -1.0, 0.0)
     torch.testing.assert_close(t, -a)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 1000, 7500])
+def test_epoch_feistel_permutation_is_bijective(n):
+    """The fused engine draws each peer's epoch order on the device with a keyed Feistel
+    permutation; its host mirror must be a bijection of [0, n) and differ between keys."""
+    from myfyp_amd.parallel.mlp_engine import feistel_perm
+
+    for key in (0, 0x1234_5678_9ABC_DEF0):
+        perm = [feistel_perm(i, n, key) for i in range(n)]
+        assert sorted(perm) == list(range(n))
+    if n >= 64:
+        a = [feistel_perm(i, n, 1) for i in range(n)]
+        b = [feistel_perm(i, n, 2) for i in range(n)]
+        assert a != b and a != list(range(n))
