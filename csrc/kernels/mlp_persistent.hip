@@ -127,14 +127,56 @@ __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
   return r < 0 ? 0 : (r > a.B ? a.B : r);
 }
 
-__device__ __forceinline__ void bias_corr(const MLPArgs& a, int t0, int t, float& bc1, float& bc2s) {
+// Per-step optimizer constants: lr_t = lr / (1 - β1^t), inv = 1 / sqrt(1 - β2^t).
+__device__ __forceinline__ void bias_corr(const MLPArgs& a, int t0, int t, float& lr_t, float& inv) {
   const int k = t0 + t + 1;
-  bc1 = 1.f - __powf(a.opt.beta1, (float)k);
-  bc2s = sqrtf(1.f - __powf(a.opt.beta2, (float)k));
+  lr_t = a.opt.lr / (1.f - __powf(a.opt.beta1, (float)k));
+  inv = 1.f / sqrtf(1.f - __powf(a.opt.beta2, (float)k));
 }
 
-__device__ __forceinline__ void upd(const MLPArgs& a, float g, float& w, float& m, float& v, float bc1, float bc2s) {
-  opt_update(a.opt, g, w, m, v, bc1, bc2s, nullptr, nullptr, nullptr, 0);
+// torch.optim.Adam / SGD(no momentum) update in registers. The register-resident epilogue runs on
+// the step's critical path (~15 k parameters per owner workgroup), so it uses the hardware
+// v_sqrt_f32 / v_rcp_f32 (1 ulp) instead of the IEEE-exact division sequence of opt_update.
+__device__ __forceinline__ void upd(const MLPArgs& a, float g, float& w, float& m, float& v, float lr_t, float inv) {
+  const OptParams& o = a.opt;
+  if (o.weight_decay != 0.f) g = fmaf(o.weight_decay, w, g);
+  if (o.kind == 0) {
+    m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
+    v = fmaf(o.beta2, v, (1.f - o.beta2) * (g * g));
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv, o.eps);
+    w = fmaf(-lr_t, m * __builtin_amdgcn_rcpf(denom), w);
+  } else {
+    w = fmaf(-o.lr, g, w);
+  }
+}
+
+// 16-lane (one MFMA row group) butterfly reductions on DPP: quad_perm xor1, xor2, then
+// row_half_mirror and row_mirror — VALU-latency instead of ds_bpermute round trips.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ int row_min16(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  return min(v, dpp_i<0x140>(v));
 }
 
 // ---- LDS carving (all offsets multiples of 16 bytes; dynamic region only: Guideline 17)
@@ -187,7 +229,7 @@ __host__ __device__ inline HeadLds head_lds(int Bpad) {
 template <int BP>
 __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, char* smem) {
   constexpr int MT = BP / 16;
-  constexpr int XPT = BP / 4;  // max 8-byte X chunks per thread (D0 <= 1024)
+  constexpr int XPT = BP / 4;  // 8-byte X chunks per lane: 4 K steps x BP rows x 4 chunks / 64 lanes
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, c = lane & 15;
@@ -255,33 +297,42 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     sB1[32 + tid] = adam ? a.v[idx] : 0.f;
   }
 
-  // ---- X staging: rows of step t (bf16, zero rows beyond the valid batch; the K padding
-  //      columns D0..KS1*32 are zeroed once and never written again)
-  const int xchunks = BP * (D0 / 8);
-  const int cpr = D0 / 8;
-  uint2 xr[XPT];
-  auto x_load = [&](int t, int tv) {
+  // ---- X staging. Every wave only ever reads its OWN K-step columns of the batch tile (the
+  //      forward A fragments and the dW1 Xᵀ fragments of K steps w, w+8, w+16, w+24), so each
+  //      wave stages exactly those columns itself, with no workgroup barrier: bf16 in LDS, rows
+  //      beyond the valid batch zero; the K padding columns D0..KS1*32 are zeroed once.
+  //      Chunk k of lane l: K step wave + 8 (k / (BP/16)), row ((k % (BP/16)) * 64 + l) / 4,
+  //      8 columns at 8 * (l % 4).
+  auto xw_addr = [&](int t, int k, int lv, bool& ok, int& r, int& col) {
+    const int q = k / (BP / 16), kk = k % (BP / 16);
+    const int s = wave + 8 * q;
+    const int idx = kk * 64 + lv;
+    r = idx >> 2;
+    col = 32 * s + 8 * (idx & 3);
+    ok = s < KS1 && col < D0;
+    return a.Xb + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + col;
+  };
+  auto xw_load = [&](int t, int lv, uint2 (&xr)[XPT]) {
     const int rows = rows_at(a, n, t);
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
-      const int e = tv + NT * k;
-      xr[k] = uint2{0u, 0u};
-      if (e < xchunks) {
-        const int r = e / cpr, q = e - r * cpr;
-        if (r < rows) xr[k] = *reinterpret_cast<const uint2*>(a.Xb + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + 8 * q);
-      }
+      bool ok;
+      int r, col;
+      const uint8_t* src = xw_addr(t, k, lv, ok, r, col);
+      xr[k] = (ok && r < rows) ? *reinterpret_cast<const uint2*>(src) : uint2{0u, 0u};
     }
   };
-  auto x_store = [&](int tv) {
+  auto xw_store = [&](int t, int lv, const uint2 (&xr)[XPT]) {
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
-      const int e = tv + NT * k;
-      if (e < xchunks) {
-        const int r = e / cpr, q = e - r * cpr;
+      bool ok;
+      int r, col;
+      xw_addr(t, k, lv, ok, r, col);
+      if (ok) {
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (bf16)(float)((((j < 4) ? xr[k].x : xr[k].y) >> (8 * (j & 3))) & 0xffu);
-        *reinterpret_cast<bf16x8*>(sX + r * LDX + 8 * q) = o;
+        *reinterpret_cast<bf16x8*>(sX + r * LDX + col) = o;
       }
     }
   };
@@ -290,8 +341,9 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     sX[r * LDX + D0 + q] = (bf16)0.f;
   }
   if (nsteps > 0) {
-    x_load(0, tid);
-    x_store(tid);
+    uint2 xr[XPT];
+    xw_load(0, lane, xr);
+    xw_store(0, lane, xr);
   }
 
   // ---- initial W2 publish (version 1)
@@ -316,8 +368,8 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     int tv = tid;
     asm volatile("" : "+v"(tv));
     const int rows = rows_at(a, n, t);
-    float bc1, bc2s;
-    bias_corr(a, ctl.z, t, bc1, bc2s);
+    float lr_t, inv_bc2;
+    bias_corr(a, ctl.z, t, lr_t, inv_bc2);
     if (tid < 16) sDb1[tid] = 0.f;
     if (g == 0) PE_STAMP(0, t, 0);
 
@@ -367,9 +419,20 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     publish(pb.flags, p, F_H1 + g, (unsigned)(t + 1));
     if (g == 0) PE_STAMP(0, t, 1);
 
-    // next step's batch: global loads in flight while the head works
+    // next step's batch: pull this wave's columns into the XCD's L2 while the head works (the
+    // loads are consumed right away, so no registers stay live across the backward phase); they
+    // are re-read from L2 and staged after this wave's dW1 update
     const bool more = t + 1 < nsteps;
-    if (more) x_load(t + 1, tv);
+    if (more) {
+      uint2 xr[XPT];
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
+      xw_load(t + 1, lv, xr);
+      unsigned sink = 0;
+#pragma unroll
+      for (int k = 0; k < XPT; ++k) sink ^= xr[k].x ^ xr[k].y;
+      asm volatile("" ::"v"(sink));
+    }
 
     // ================= C: backward of this slice
     if (!wg_wait(pb.flags, p, F_DH2, 1, (unsigned)(t + 1), pb.err, sOk)) return;
@@ -413,7 +476,9 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       if (hh == 0) atomicAdd(&sDb1[cc], db);
     }
     lds_barrier();
-    // C3: dW2 columns + update (waves 4..7), then publish the bf16 slice for the head's next step
+    if (g == 0) PE_STAMP(0, t, 3);
+    // C3 (waves 4..7): dW2 columns + update, bf16 slice staged in LDS for the publish below.
+    // C2 (every wave, its own K steps): dW1 rows + update — waves 0..3 start on it at once.
     if (wave >= 4) {
       float gr[8];
 #pragma unroll
@@ -426,11 +491,11 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
         for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) upd(a, gr[j], w2[j], m2[j], v2[j], bc1, bc2s);
+      for (int j = 0; j < 8; ++j) {
+        upd(a, gr[j], w2[j], m2[j], v2[j], lr_t, inv_bc2);
+        sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
+      }
     }
-    publish_w2((unsigned)(t + 2));
-    if (g == 0) PE_STAMP(0, t, 3);
-    // C2: dW1 rows + update (all waves, their own K steps)
     {
       bf16x8 bd[BP / 32];
 #pragma unroll
@@ -449,16 +514,27 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
             for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) upd(a, gr[j], w1[q][j], m1[q][j], v1[q][j], bc1, bc2s);
+          for (int j = 0; j < 8; ++j) upd(a, gr[j], w1[q][j], m1[q][j], v1[q][j], lr_t, inv_bc2);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (tid < 16) upd(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], bc1, bc2s);
-    __syncthreads();  // every wave is done with sX / sDH1 / sB1
+    if (tid < 16) upd(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], lr_t, inv_bc2);
+    if (more) {  // this wave's columns of the next batch (L2-resident by now)
+      uint2 xr[XPT];
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
+      xw_load(t + 1, lv, xr);
+      xw_store(t + 1, lv, xr);
+    }
+    __syncthreads();  // sDH1 / sB1 reads done; sW2g complete
     if (g == 0) PE_STAMP(0, t, 4);
-    if (more) x_store(tv);
-    __syncthreads();
+    // updated W2 slice to the head (write-through) and the next batch into LDS; one drain + flag
+    {
+      const int row = tv >> 2, part = tv & 3;
+      st_wt(pb.w2x + ((int64_t)p * PD2 + row) * PD1 + NG * g + 4 * part, *reinterpret_cast<const unsigned long long*>(sW2g + row * 16 + 4 * part));
+    }
+    publish(pb.flags, p, F_W2 + g, (unsigned)(t + 2));
     if (g == 0) PE_STAMP(0, t, 5);
   }
 
@@ -574,36 +650,41 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     int tv = tid;  // opaque per-iteration thread index (see owner)
     asm volatile("" : "+v"(tv));
     const int rows = rows_at(a, n, t);
-    float bc1, bc2s;
-    bias_corr(a, ctl.z, t, bc1, bc2s);
+    float lr_t, inv_bc2;
+    bias_corr(a, ctl.z, t, lr_t, inv_bc2);
 
     // ---- W2 (bf16, version t+1) and H1 (step t) from the owners
     PE_STAMP(1, t, 0);
     if (!wg_wait(pb.flags, p, F_W2, NG, (unsigned)(t + 1), pb.err, sOk)) return;
     PE_STAMP(1, t, 1);
-    unsigned long long w2r[16];
+    {
+      // W2 lands well before H1 (the owners publish it ahead of their forward): stage it now
+      unsigned long long w2r[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {  // 128 x 256 bf16 = 8192 chunks of 8 B
-      const int e = tv + NT * k;
-      w2r[k] = ld_wt(pb.w2x + (int64_t)p * PD2 * PD1 + (int64_t)e * 4);
+      for (int k = 0; k < 16; ++k) {  // 128 x 256 bf16 = 8192 chunks of 8 B
+        const int e = tv + NT * k;
+        w2r[k] = ld_wt(pb.w2x + (int64_t)p * PD2 * PD1 + (int64_t)e * 4);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = tv + NT * k;
+        *reinterpret_cast<unsigned long long*>(sW2 + (e >> 6) * LDH + 4 * (e & 63)) = w2r[k];
+      }
     }
     if (!wg_wait(pb.flags, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
     PE_STAMP(1, t, 2);
-    unsigned long long h1r[BP / 8];
+    {
+      unsigned long long h1r[BP / 8];
 #pragma unroll
-    for (int k = 0; k < BP / 8; ++k) {  // BP x 256 bf16 = BP*64 chunks
-      const int e = tv + NT * k;
-      h1r[k] = ld_wt(pb.h1x + (int64_t)p * BP * PD1 + (int64_t)e * 4);
-    }
+      for (int k = 0; k < BP / 8; ++k) {  // BP x 256 bf16 = BP*64 chunks
+        const int e = tv + NT * k;
+        h1r[k] = ld_wt(pb.h1x + (int64_t)p * BP * PD1 + (int64_t)e * 4);
+      }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tv + NT * k;
-      *reinterpret_cast<unsigned long long*>(sW2 + (e >> 6) * LDH + 4 * (e & 63)) = w2r[k];
-    }
-#pragma unroll
-    for (int k = 0; k < BP / 8; ++k) {
-      const int e = tv + NT * k;
-      *reinterpret_cast<unsigned long long*>(sH1 + (e >> 6) * LDH + 4 * (e & 63)) = h1r[k];
+      for (int k = 0; k < BP / 8; ++k) {
+        const int e = tv + NT * k;
+        *reinterpret_cast<unsigned long long*>(sH1 + (e >> 6) * LDH + 4 * (e & 63)) = h1r[k];
+      }
     }
     lds_barrier();
 
@@ -654,14 +735,10 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
         const bool rvalid = b < rows;
         const int y = rvalid ? a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b] : -1;
         const float logit = cin ? lg[i] + b3 : -INFINITY;
-        const float mx = warp_max16(logit);
-        const float se = warp_sum16(cin ? __expf(logit - mx) : 0.f);
+        const float mx = row_max16(logit);
+        const float se = row_sum16(cin ? __expf(logit - mx) : 0.f);
         const float logp = logit - (mx + __logf(se));
-        int cand = (cin && logit == mx) ? c : 16;
-        cand = min(cand, __shfl_xor(cand, 1));
-        cand = min(cand, __shfl_xor(cand, 2));
-        cand = min(cand, __shfl_xor(cand, 4));
-        cand = min(cand, __shfl_xor(cand, 8));
+        const int cand = row_min16((cin && logit == mx) ? c : 16);
         if (rvalid && c == y) loss_acc -= logp;
         if (rvalid && c == 0) correct_acc += (cand == y) ? 1.f : 0.f;
         const float d = (rvalid && cin) ? (__expf(logp) - (c == y ? 1.f : 0.f)) / (float)rows : 0.f;
@@ -709,7 +786,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
       if (cin) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          upd(a, gr[j], w3[j], m3[j], v3[j], bc1, bc2s);
+          upd(a, gr[j], w3[j], m3[j], v3[j], lr_t, inv_bc2);
           sW3[c * LDW3 + 32 * wave + kappa(h, j)] = (bf16)w3[j];
         }
       }
@@ -717,11 +794,11 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
       const int o2 = tid - 256;
       float db = 0.f;
       for (int b = 0; b < BP; ++b) db += (float)sDH2[b * LD2 + o2];
-      upd(a, db, sB2[o2], sB2[PD2 + o2], sB2[2 * PD2 + o2], bc1, bc2s);
+      upd(a, db, sB2[o2], sB2[PD2 + o2], sB2[2 * PD2 + o2], lr_t, inv_bc2);
     } else if (wave == 6 && lane < D3) {
       float db = 0.f;
       for (int b = 0; b < BP; ++b) db += (float)sDlog[b * LDL + lane];
-      upd(a, db, sB3[lane], sB3[16 + lane], sB3[32 + lane], bc1, bc2s);
+      upd(a, db, sB3[lane], sB3[16 + lane], sB3[32 + lane], lr_t, inv_bc2);
     }
     __syncthreads();
     PE_STAMP(1, t, 6);

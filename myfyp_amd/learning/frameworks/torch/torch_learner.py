@@ -196,6 +196,16 @@ class TorchLearner(Learner):
         else:
             steps, mean_loss = self._fit_autograd(spec)
         logger.log_timing(self._self_addr, "fit", time.time() - t0)
+        return self._fit_done(steps, mean_loss, spec)
+
+    def fit_request(self) -> Tuple[dict, int, dict]:
+        """(optimizer spec, epochs, corrections) of a fit that a fused-round leader runs for this
+        peer (collective workflow: evaluate + fit + FedAvg of all co-located peers in one gang op);
+        the peer's own bookkeeping then happens in :meth:`_fit_done`."""
+        self._interrupt.clear()
+        return self._optimizer_spec(), self.epochs, self._gather_corrections()
+
+    def _fit_done(self, steps: int, mean_loss, spec: dict) -> P2PFLModel:
         if mean_loss is not None:
             snap, addr, gs = logger.experiment_snapshot(self._self_addr), self._self_addr, self.global_step
             if isinstance(mean_loss, Pending):  # fused engine: logged when the device result lands
@@ -297,10 +307,18 @@ class TorchLearner(Learner):
         t0 = time.time()
         if self.data is None or self.data.get_num_samples(train=False) == 0:
             return Pending.completed({})
-        snap, addr = logger.experiment_snapshot(self._self_addr), self._self_addr
+        snap = logger.experiment_snapshot(self._self_addr)
         raw = self._engine.evaluate(self) if self._engine is not None else self.evaluate_raw()
+        out = self._evaluate_done(raw, snap)
+        logger.log_timing(self._self_addr, "evaluate", time.time() - t0)
+        return out
+
+    def _evaluate_done(self, raw, snap) -> Pending:
+        """Metrics of an issued evaluation (``raw`` = (loss, confusion) or its Pending), logged under
+        the experiment snapshot taken when it was issued."""
         if not isinstance(raw, Pending):
             raw = Pending.completed(raw)
+        addr = self._self_addr
 
         def done(lc) -> Dict[str, float]:
             results = self._results(*lc)
@@ -308,9 +326,7 @@ class TorchLearner(Learner):
                 logger.log_metric_at(addr, snap, k, v)
             return results
 
-        out = raw.map(done)
-        logger.log_timing(self._self_addr, "evaluate", time.time() - t0)
-        return out
+        return raw.map(done)
 
     def evaluate(self) -> Dict[str, float]:
         return self.evaluate_async().result()

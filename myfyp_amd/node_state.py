@@ -24,6 +24,7 @@ class NodeState:
         self.status = "Idle"
         self.simulation = simulation
         self.experiment_config = None
+        self.fused_round = False  # collective workflow: this round runs as one fused gang op
         self.models_aggregated: Dict[str, List[str]] = {}
         self.nei_status: Dict[str, int] = {}
         self.train_set: List[str] = []

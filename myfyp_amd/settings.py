@@ -95,6 +95,8 @@ class Settings:
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
     GIL_SWITCH_INTERVAL: float | None = 2e-4
+    # collective workflow: evaluate + fit + FedAvg of co-located fused-engine peers as ONE gang op
+    FUSED_ROUND: bool = True
 
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
@@ -154,6 +156,7 @@ class Settings:
             "BUCKET_BYTES": "BUCKET_BYTES",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
+            "FUSED_ROUND": "FUSED_ROUND",
         }
     )
 

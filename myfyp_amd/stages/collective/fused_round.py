@@ -1,0 +1,75 @@
+"""One gang operation per round for co-located fused-engine peers: evaluate + fit + FedAvg.
+
+The collective workflow normally crosses three barriers per round after the vote (evaluation gang,
+fit gang, aggregation gang), each waking every co-located peer thread. When the vote leader finds
+that every local peer is a fused-engine learner of one group without training callbacks and the
+aggregator is sample-weighted averaging, the train / wait stages instead join ONE gang whose leader
+enqueues, in stream order, the evaluation of every trainer, the grouped local epoch(s) and the
+FedAvg collective. Each peer thread then only files its own results (metrics are logged when the
+device results land). Observable behaviour — stage history, metrics, contributions, the FedAvg
+result — is that of the three-gang path (``train_stage.py`` / ``wait_agg_models_stage.py``;
+reference ``stages/base_node/train_stage.py:44-100``).
+"""
+
+from __future__ import annotations
+
+import time
+
+from myfyp_amd.management.logger import logger
+from myfyp_amd.parallel import weights_plane
+from myfyp_amd.settings import Settings
+from myfyp_amd.stages.collective._common import fed
+
+
+def eligible(f, aggregator) -> bool:
+    """Decided once per round by the vote leader, so every co-located peer takes the same path."""
+    if not Settings.FUSED_ROUND or getattr(aggregator, "collective_kind", None) != "mean":
+        return False
+    groups = set()
+    for a in f.local_order:
+        node = f.local_nodes.get(a)
+        if node is None:
+            continue
+        lr = node.learner
+        eng = getattr(lr, "_engine", None)
+        if eng is None or getattr(lr, "callbacks", None) or not hasattr(lr, "fit_request"):
+            return False
+        groups.add(id(eng.group))
+    return len(groups) == 1
+
+
+def join(state, learner, aggregator, trainer: bool) -> None:
+    f = fed()
+    t0 = time.time()
+    snap = logger.experiment_snapshot(state.addr)
+    req = learner.fit_request() if trainer else None
+    n = learner.num_train_samples() if trainer else 0
+    has_test = trainer and learner.data is not None and learner.data.get_num_samples(train=False) > 0
+    round_ = state.round
+
+    def leader(arrived):
+        addrs = [a for a in arrived if a in f.local_nodes]  # a peer may die after arriving
+        trainers = [a for a in addrs if arrived[a][0]]
+        out = {}
+        if trainers:
+            group = f.local_nodes[trainers[0]].learner._engine.group
+            slot = {a: f.local_nodes[a].learner._engine.slot for a in trainers}
+            evs = group._run_eval_batch({slot[a]: () for a in trainers if arrived[a][3]})
+            fits = group._run_fit_batch({slot[a]: arrived[a][2] for a in trainers})
+            for a in trainers:
+                out[a] = (evs.get(slot[a]), fits[slot[a]])
+        weights_plane.aggregate_mean(f, {a: (arrived[a][1], None) for a in addrs})
+        for hook in list(f.round_hooks):
+            hook(round_, f)
+        return out
+
+    res = f.gang_run(state.addr, (trainer, n, req, has_test), leader)
+    if trainer:
+        ev, (steps, raw) = res[state.addr]
+        if ev is not None:
+            learner._evaluate_done(ev, snap)
+        learner.global_step += steps
+        learner._fit_done(steps, raw.map(lambda v: v[0]), req[0])
+    model = learner.get_model()
+    model.set_contribution(list(state.train_set) or [state.addr], max(1, model.num_samples))
+    logger.log_timing(state.addr, "fused_round", time.time() - t0)

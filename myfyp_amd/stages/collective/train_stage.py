@@ -9,6 +9,7 @@ import time
 from typing import Optional, Type
 
 from myfyp_amd.management.logger import logger
+from myfyp_amd.stages.collective import fused_round
 from myfyp_amd.stages.collective.wait_agg_models_stage import join_aggregation
 from myfyp_amd.stages.stage import EarlyStopException, Stage, check_early_stop
 from myfyp_amd.stages.stage_factory import StageFactory
@@ -26,6 +27,9 @@ class TrainStage(Stage):
         try:
             check_early_stop(state)
             aggregator.set_nodes_to_aggregate(state.train_set)
+            if getattr(state, "fused_round", False):
+                fused_round.join(state, learner, aggregator, trainer=True)
+                return StageFactory.get_stage("GossipModelStage", "collective")
             # metrics are only logged here (reference: train_stage.py:104-117), so the evaluation is
             # enqueued and its results are filed under this round when they land — no GPU wait
             if hasattr(learner, "evaluate_async"):

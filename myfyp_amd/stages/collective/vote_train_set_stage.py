@@ -10,6 +10,7 @@ from typing import Optional, Type
 from myfyp_amd.management.logger import logger
 from myfyp_amd.parallel import weights_plane
 from myfyp_amd.stages.base_node.vote_train_set_stage import make_votes, tally_votes
+from myfyp_amd.stages.collective import fused_round
 from myfyp_amd.stages.collective._common import fed, set_gang_expectations
 from myfyp_amd.stages.stage import Stage, check_early_stop
 from myfyp_amd.stages.stage_factory import StageFactory
@@ -29,7 +30,8 @@ class VoteTrainSetStage(Stage):
         logger.round_started(state.addr, state.experiment)
         f = fed()
         votes = make_votes(state.addr, f.all_peers(), state.round)
-        everyone = bool(getattr(kwargs.get("aggregator"), "all_peers_train", False))
+        aggregator = kwargs.get("aggregator")
+        everyone = bool(getattr(aggregator, "all_peers_train", False))
 
         def leader(arrived):
             allv = weights_plane.gather_votes(f, arrived)
@@ -37,9 +39,10 @@ class VoteTrainSetStage(Stage):
             # ranks learn who is alive
             train_set = sorted(allv, key=lambda a: f.all_peers().index(a)) if everyone else tally_votes(allv)
             set_gang_expectations(f, set(train_set), set(train_set))
-            return train_set
+            return train_set, fused_round.eligible(f, aggregator)
 
-        state.train_set = list(f.gang_run(state.addr, votes, leader))
+        train_set, state.fused_round = f.gang_run(state.addr, votes, leader)
+        state.train_set = list(train_set)
         logger.info(state.addr, f"🚂 Train set of {len(state.train_set)} nodes: {state.train_set}")
         if state.addr in state.train_set:
             return StageFactory.get_stage("TrainStage", "collective")

@@ -54,5 +54,10 @@ class WaitAggregatedModelsStage(Stage):
             raise Exception("Invalid parameters on WaitAggregatedModelsStage.")
         if state.round is None:
             return None
-        join_aggregation(state, learner, aggregator, trainer=False)
+        if getattr(state, "fused_round", False):
+            from myfyp_amd.stages.collective import fused_round
+
+            fused_round.join(state, learner, aggregator, trainer=False)
+        else:
+            join_aggregation(state, learner, aggregator, trainer=False)
         return StageFactory.get_stage("GossipModelStage", "collective")

@@ -38,7 +38,7 @@ assert lib.mlp_debug_persistent_stamps(st.ctypes.data) == 0
 st = st.astype(np.int64)
 t0 = st[0, 0, 0]
 us = lambda v: (v - t0) / 100.0
-print("owner: A(fwd+publish) | wait dH2 | C1+C3+W2 publish | C2 (dW1+Adam) | X stage | step")
+print("owner: A(fwd+publish) | wait dH2 | dH2 load+C1 | C2+C3 (dW1,dW2+Adam) | W2 publish+X stage | step")
 print("head : wait W2 | wait H1+loads | H2 | logits+softmax | dH2+publish | dW3/bias | step")
 for t in range(2, 12):
     o, h = st[0, t], st[1, t]
@@ -49,4 +49,4 @@ for t in range(2, 12):
     print(f"t={t:2d} owner {' '.join(f'{x:6.2f}' for x in do)} | {step_o:6.2f}   head {' '.join(f'{x:6.2f}' for x in dh)} | {step_h:6.2f}")
 print("owner A start -> head H1 ready (us):", [round((st[1, t, 2] - st[0, t, 0]) / 100.0, 2) for t in range(2, 8)])
 print("head dH2 published -> owner dH2 seen (us):", [round((st[0, t, 2] - st[1, t, 5]) / 100.0, 2) for t in range(2, 8)])
-print("owner W2 published -> head W2 seen (us):", [round((st[1, t + 1, 1] - st[0, t, 3]) / 100.0, 2) for t in range(2, 8)])
+print("owner W2 published -> head W2 seen (us):", [round((st[1, t + 1, 1] - st[0, t, 5]) / 100.0, 2) for t in range(2, 8)])

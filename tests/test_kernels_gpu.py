@@ -241,7 +241,8 @@ def test_fused_mlp_single_step_gradients(dev, persistent):
 @pytest.mark.parametrize("B", [64, 32])
 def test_persistent_epoch_matches_step_path_adam(dev, B):
     """Several Adam epochs on 3 peers: persistent epoch kernel vs 3-launch step path from identical
-    weights and batch order (same bf16 rounding points; only accumulation order differs)."""
+    weights and batch order (same bf16 rounding points; accumulation order and the epilogue's
+    reciprocal differ)."""
     import threading
 
     from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
@@ -287,7 +288,10 @@ def test_persistent_epoch_matches_step_path_adam(dev, B):
         for k, (pp, ps, p0) in enumerate(zip(results[None][i], results[False][i], init[i])):
             d_p, d_s = pp.cpu() - p0, ps.cpu() - p0
             rel = ((d_p - d_s).norm() / (d_s.norm() + 1e-12)).item()
-            assert rel < 0.05, f"peer {i} param {k}: persistent vs step-path update mismatch {rel:.4f}"
+            # Adam normalises every coordinate, so 1-ulp differences (hardware rcp/sqrt in the
+            # persistent epilogue vs the IEEE division of the step path) and accumulation order
+            # move small-gradient coordinates by ~lr; the SGD tests above pin the gradients tightly
+            assert rel < 0.1, f"peer {i} param {k}: persistent vs step-path update mismatch {rel:.4f}"
         lp, ls = results[(None, "loss")][i], results[(False, "loss")][i]
         assert abs(lp - ls) / ls < 0.05, (lp, ls)
     MLPGroup.reset_all()
