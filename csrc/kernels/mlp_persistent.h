@@ -5,7 +5,7 @@
 // Exchange buffers of one engine (allocated when the persistent path is eligible).
 struct MLPPersistBufs {
   bf16* h1x;        // [P][Bpad][256]   owner g -> head: H1 columns 16g..16g+15
-  bf16* w2x;        // [P][128][256]    owner g -> head: bf16 W2 columns 16g..16g+15 (after update)
+  bf16* w2x;        // [P][8][8][64][8]  owner g -> head: updated bf16 W2 in the head's B-fragment order
   bf16* dh2x;       // [P][Bpad][128]   head -> owners: dH2
   unsigned* flags;  // [P][33][32] one 128-B line per flag (16 H1, 16 W2, 1 dH2); zeroed per launch
   size_t flag_bytes;

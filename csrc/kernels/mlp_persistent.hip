@@ -137,10 +137,11 @@ __device__ __forceinline__ void bias_corr(const MLPArgs& a, int t0, int t, float
 // torch.optim.Adam / SGD(no momentum) update in registers. The register-resident epilogue runs on
 // the step's critical path (~15 k parameters per owner workgroup), so it uses the hardware
 // v_sqrt_f32 / v_rcp_f32 (1 ulp) instead of the IEEE-exact division sequence of opt_update.
+template <bool ADAM>
 __device__ __forceinline__ void upd(const MLPArgs& a, float g, float& w, float& m, float& v, float lr_t, float inv) {
   const OptParams& o = a.opt;
-  if (o.weight_decay != 0.f) g = fmaf(o.weight_decay, w, g);
-  if (o.kind == 0) {
+  g = fmaf(o.weight_decay, w, g);  // weight_decay = 0: exact no-op, and no branch
+  if (ADAM) {
     m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
     v = fmaf(o.beta2, v, (1.f - o.beta2) * (g * g));
     const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv, o.eps);
@@ -204,13 +205,12 @@ __host__ __device__ inline OwnerLds owner_lds(int Bpad, int D0) {
   return L;
 }
 struct HeadLds {
-  size_t w2, h1, h2, dlog, w3, red, b2, b3, ok, total;
+  size_t h1, h2, dlog, w3, red, b2, b3, ok, total;
 };
 __host__ __device__ inline HeadLds head_lds(int Bpad) {
   HeadLds L;
   const int MT = Bpad / 16;
   size_t o = 0;
-  L.w2 = o;   o += al16((size_t)PD2 * LDH * 2);
   L.h1 = o;   o += al16((size_t)Bpad * LDH * 2);  // also the dH2 staging tile (disjoint lifetimes)
   L.h2 = o;   o += al16((size_t)Bpad * LD2 * 2);
   L.dlog = o; o += al16((size_t)Bpad * LDL * 2);
@@ -226,7 +226,7 @@ __host__ __device__ inline HeadLds head_lds(int Bpad) {
 // =============================================================================================
 // owner workgroup
 // =============================================================================================
-template <int BP>
+template <int BP, bool ADAM>
 __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, char* smem) {
   constexpr int MT = BP / 16;
   constexpr int XPT = BP / 4;  // 8-byte X chunks per lane: 4 K steps x BP rows x 4 chunks / 64 lanes
@@ -250,7 +250,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
   const int n = ctl.y;
   const int nsteps = (n + a.B - 1) / a.B;
   const int64_t pS = (int64_t)p * a.S;
-  const bool adam = a.opt.kind == 0;
+  constexpr bool adam = ADAM;
 
   // ---- resident state: W1 rows (all waves; wave w owns K steps w, w+8, w+16, w+24) and the W2
   //      column slice (waves 4..7; wave 4+k owns o2 32k..32k+31)
@@ -346,6 +346,16 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     xw_store(0, lane, xr);
   }
 
+  // ---- the bf16 W2 slice goes to the head in ITS B-fragment order: chunk (wave w, K step ks,
+  //      lane l) = 8 bf16 W2[16w + (l & 15)][32ks + 8(l >> 4) .. +8] at w2x[p][w][ks][l], so each
+  //      head wave reads 1 KB contiguous per load instruction. This owner's 16 columns are K step
+  //      g/2, lane groups 2(g&1) and 2(g&1)+1. One 8-byte write-through store per thread.
+  auto w2_store = [&](int tv) {
+    const int o2 = tv >> 2, part = tv & 3, half = part >> 1, sub = part & 1;
+    const int lane_h = 2 * (g & 1) + half;
+    const int64_t chunk = (((int64_t)p * 8 + (o2 >> 4)) * (PD1 / 32) + (g >> 1)) * 64 + lane_h * 16 + (o2 & 15);
+    st_wt(pb.w2x + chunk * 8 + 4 * sub, *reinterpret_cast<const unsigned long long*>(sW2g + o2 * 16 + 4 * part));
+  };
   // ---- initial W2 publish (version 1)
   auto publish_w2 = [&](unsigned version) {
     if (wave >= 4) {
@@ -353,11 +363,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       for (int j = 0; j < 8; ++j) sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
     }
     __syncthreads();
-    {
-      const int row = tid >> 2, part = tid & 3;  // 128 rows x 4 chunks of 4 bf16 = 512 stores
-      const unsigned long long v = *reinterpret_cast<const unsigned long long*>(sW2g + row * 16 + 4 * part);
-      st_wt(pb.w2x + ((int64_t)p * PD2 + row) * PD1 + NG * g + 4 * part, v);
-    }
+    w2_store(tid);
     publish(pb.flags, p, F_W2 + g, version);
   };
   publish_w2(1u);
@@ -492,7 +498,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        upd(a, gr[j], w2[j], m2[j], v2[j], lr_t, inv_bc2);
+        upd<ADAM>(a, gr[j], w2[j], m2[j], v2[j], lr_t, inv_bc2);
         sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
       }
     }
@@ -514,12 +520,11 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
             for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) upd(a, gr[j], w1[q][j], m1[q][j], v1[q][j], lr_t, inv_bc2);
+          for (int j = 0; j < 8; ++j) upd<ADAM>(a, gr[j], w1[q][j], m1[q][j], v1[q][j], lr_t, inv_bc2);
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (tid < 16) upd(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], lr_t, inv_bc2);
+    if (tid < 16) upd<ADAM>(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], lr_t, inv_bc2);
     if (more) {  // this wave's columns of the next batch (L2-resident by now)
       uint2 xr[XPT];
       int lv = lane;
@@ -530,10 +535,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     __syncthreads();  // sDH1 / sB1 reads done; sW2g complete
     if (g == 0) PE_STAMP(0, t, 4);
     // updated W2 slice to the head (write-through) and the next batch into LDS; one drain + flag
-    {
-      const int row = tv >> 2, part = tv & 3;
-      st_wt(pb.w2x + ((int64_t)p * PD2 + row) * PD1 + NG * g + 4 * part, *reinterpret_cast<const unsigned long long*>(sW2g + row * 16 + 4 * part));
-    }
+    w2_store(tv);
     publish(pb.flags, p, F_W2 + g, (unsigned)(t + 2));
     if (g == 0) PE_STAMP(0, t, 5);
   }
@@ -587,7 +589,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
 // =============================================================================================
 // head workgroup
 // =============================================================================================
-template <int BP>
+template <int BP, bool ADAM>
 __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* smem) {
   constexpr int MT = BP / 16;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -595,7 +597,6 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   const int h = lane >> 4, c = lane & 15;
   const int D3 = a.D3;
   const HeadLds L = head_lds(BP);
-  bf16* sW2 = reinterpret_cast<bf16*>(smem + L.w2);
   bf16* sH1 = reinterpret_cast<bf16*>(smem + L.h1);
   bf16* sDH2 = sH1;  // dH2 staging reuses the H1 tile (H1 is dead after the H2 GEMM)
   bf16* sH2 = reinterpret_cast<bf16*>(smem + L.h2);
@@ -610,7 +611,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   const int n = ctl.y;
   const int nsteps = (n + a.B - 1) / a.B;
   const int64_t pS = (int64_t)p * a.S;
-  const bool adam = a.opt.kind == 0;
+  constexpr bool adam = ADAM;
   const bool cin = c < D3;
 
   // resident W3 (waves 0..3, wave w owns o2 32w..32w+31), biases in LDS
@@ -657,18 +658,16 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     PE_STAMP(1, t, 0);
     if (!wg_wait(pb.flags, p, F_W2, NG, (unsigned)(t + 1), pb.err, sOk)) return;
     PE_STAMP(1, t, 1);
+    // W2 (bf16) goes straight into this wave's B fragments — rows 16w..16w+15 of W2, all 256
+    // inputs (32 VGPRs): it lands well before H1 (the owners publish it ahead of their forward)
+    // and never touches LDS
+    bf16x8 w2f[PD1 / 32];
     {
-      // W2 lands well before H1 (the owners publish it ahead of their forward): stage it now
-      unsigned long long w2r[16];
+      const bf16* wfrag = pb.w2x + (((int64_t)p * 8 + wave) * (PD1 / 32) * 64 + lane) * 8;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {  // 128 x 256 bf16 = 8192 chunks of 8 B
-        const int e = tv + NT * k;
-        w2r[k] = ld_wt(pb.w2x + (int64_t)p * PD2 * PD1 + (int64_t)e * 4);
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = tv + NT * k;
-        *reinterpret_cast<unsigned long long*>(sW2 + (e >> 6) * LDH + 4 * (e & 63)) = w2r[k];
+      for (int ks = 0; ks < PD1 / 32; ++ks) {
+        const unsigned long long lo = ld_wt(wfrag + ks * 64 * 8), hi = ld_wt(wfrag + ks * 64 * 8 + 4);
+        w2f[ks] = __builtin_bit_cast(bf16x8, (unsigned long long __attribute__((ext_vector_type(2)))){lo, hi});
       }
     }
     if (!wg_wait(pb.flags, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
@@ -695,9 +694,8 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
 #pragma unroll
       for (int ks = 0; ks < PD1 / 32; ++ks) {
-        const bf16x8 bw = ld8(sW2 + (16 * wave + c) * LDH + 32 * ks + 8 * h);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_bf16(ld8(sH1 + (16 * mt + c) * LDH + 32 * ks + 8 * h), bw, acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_bf16(ld8(sH1 + (16 * mt + c) * LDH + 32 * ks + 8 * h), w2f[ks], acc[mt]);
       }
       const int o2 = 16 * wave + c;
       const float bias = sB2[o2];
@@ -786,7 +784,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
       if (cin) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          upd(a, gr[j], w3[j], m3[j], v3[j], lr_t, inv_bc2);
+          upd<ADAM>(a, gr[j], w3[j], m3[j], v3[j], lr_t, inv_bc2);
           sW3[c * LDW3 + 32 * wave + kappa(h, j)] = (bf16)w3[j];
         }
       }
@@ -794,11 +792,11 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
       const int o2 = tid - 256;
       float db = 0.f;
       for (int b = 0; b < BP; ++b) db += (float)sDH2[b * LD2 + o2];
-      upd(a, db, sB2[o2], sB2[PD2 + o2], sB2[2 * PD2 + o2], lr_t, inv_bc2);
+      upd<ADAM>(a, db, sB2[o2], sB2[PD2 + o2], sB2[2 * PD2 + o2], lr_t, inv_bc2);
     } else if (wave == 6 && lane < D3) {
       float db = 0.f;
       for (int b = 0; b < BP; ++b) db += (float)sDlog[b * LDL + lane];
-      upd(a, db, sB3[lane], sB3[16 + lane], sB3[32 + lane], lr_t, inv_bc2);
+      upd<ADAM>(a, db, sB3[lane], sB3[16 + lane], sB3[32 + lane], lr_t, inv_bc2);
     }
     __syncthreads();
     PE_STAMP(1, t, 6);
@@ -838,7 +836,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   }
 }
 
-template <int BP>
+template <int BP, bool ADAM>
 __global__ __launch_bounds__(NT) void mlp_persistent_epoch(MLPArgs a, MLPPersistBufs pb) {
   extern __shared__ __attribute__((aligned(16))) char smem_pe[];
   const int b = blockIdx.x;
@@ -849,9 +847,9 @@ __global__ __launch_bounds__(NT) void mlp_persistent_epoch(MLPArgs a, MLPPersist
   const int4 ctl = a.ctl[p];
   if (!ctl.x || ctl.y <= 0) return;
   if (role < NG)
-    owner<BP>(a, pb, p, role, smem_pe);
+    owner<BP, ADAM>(a, pb, p, role, smem_pe);
   else
-    head<BP>(a, pb, p, smem_pe);
+    head<BP, ADAM>(a, pb, p, smem_pe);
 }
 
 }  // namespace
@@ -875,10 +873,16 @@ static size_t persistent_lds(const MLPArgs& a) {
   return lo > lh ? lo : lh;
 }
 
+template <int BP, bool ADAM>
+static hipError_t prepare_one(int lds) {
+  return hipFuncSetAttribute((const void*)mlp_persistent_epoch<BP, ADAM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
 hipError_t mlp_persistent_prepare(const MLPArgs& a) {
   const int lds = (int)persistent_lds(a);
-  if (a.Bpad == 64) return hipFuncSetAttribute((const void*)mlp_persistent_epoch<64>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  return hipFuncSetAttribute((const void*)mlp_persistent_epoch<32>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipError_t e = a.Bpad == 64 ? prepare_one<64, true>(lds) : prepare_one<32, true>(lds);
+  if (e != hipSuccess) return e;
+  return a.Bpad == 64 ? prepare_one<64, false>(lds) : prepare_one<32, false>(lds);
 }
 
 hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s) {
@@ -886,9 +890,17 @@ hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& p
   if (e != hipSuccess) return e;
   const size_t lds = persistent_lds(a);
   const dim3 grid(mlp_persistent_blocks(a.P)), block(NT);
-  if (a.Bpad == 64)
-    hipLaunchKernelGGL(mlp_persistent_epoch<64>, grid, block, lds, s, a, pb);
-  else
-    hipLaunchKernelGGL(mlp_persistent_epoch<32>, grid, block, lds, s, a, pb);
+  const bool adam = a.opt.kind == 0;
+  if (a.Bpad == 64) {
+    if (adam)
+      hipLaunchKernelGGL((mlp_persistent_epoch<64, true>), grid, block, lds, s, a, pb);
+    else
+      hipLaunchKernelGGL((mlp_persistent_epoch<64, false>), grid, block, lds, s, a, pb);
+  } else {
+    if (adam)
+      hipLaunchKernelGGL((mlp_persistent_epoch<32, true>), grid, block, lds, s, a, pb);
+    else
+      hipLaunchKernelGGL((mlp_persistent_epoch<32, false>), grid, block, lds, s, a, pb);
+  }
   return hipGetLastError();
 }

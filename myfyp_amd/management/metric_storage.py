@@ -57,11 +57,16 @@ class GlobalMetricStorage:
     def __init__(self, disable_locks: bool = False) -> None:
         self.exp_dicts: GlobalLogsType = {}
         self.lock: Optional[Lock] = None if disable_locks else Lock()
+        self._seen: dict = {}  # (exp, node, metric) -> rounds already stored (O(1) first-value-wins)
 
     def add_log(self, exp_name: str, round: int, metric: str, node: str, val: Union[int, float]) -> None:
         with self.lock or _NullLock():
             series = self.exp_dicts.setdefault(exp_name, {}).setdefault(node, {}).setdefault(metric, [])
-            if all(r != round for r, _ in series):
+            seen = self._seen.get((exp_name, node, metric))
+            if seen is None or len(seen) != len(series):  # (re)build if the series was edited directly
+                seen = self._seen[(exp_name, node, metric)] = {r for r, _ in series}
+            if round not in seen:
+                seen.add(round)
                 series.append((round, val))
 
     def get_all_logs(self) -> GlobalLogsType:

@@ -191,6 +191,7 @@ class Federation:
         self._lock = threading.Lock()
         self._cpu_pg = None
         self.shm = None  # node-local shared-memory control plane (single-node jobs)
+        self._round_driver = None
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
@@ -335,6 +336,15 @@ class Federation:
     # ------------------------------------------------------------------ collectives (gang leaders only)
     def live_local(self) -> List[str]:
         return [a for a in self.local_order if a in self.local_nodes and self.local_nodes[a].state.round is not None]
+
+    def round_driver(self):
+        """Lock-step round driver of the co-located peers (stages/collective/driver.py)."""
+        with self._lock:
+            if self._round_driver is None:
+                from myfyp_amd.stages.collective.driver import RoundDriver
+
+                self._round_driver = RoundDriver(self)
+            return self._round_driver
 
     def gang_run(self, member: str, payload: Any, fn: Callable[[Dict[str, Any]], Any], timeout: Optional[float] = None) -> Any:
         def members() -> List[str]:

@@ -97,6 +97,8 @@ class Settings:
     GIL_SWITCH_INTERVAL: float | None = 2e-4
     # collective workflow: evaluate + fit + FedAvg of co-located fused-engine peers as ONE gang op
     FUSED_ROUND: bool = True
+    # ... and the rounds of all co-located fused peers are driven by ONE host thread (driver.py)
+    ROUND_DRIVER: bool = True
 
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
@@ -157,6 +159,7 @@ class Settings:
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",
+            "ROUND_DRIVER": "ROUND_DRIVER",
         }
     )
 

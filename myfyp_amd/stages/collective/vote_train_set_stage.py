@@ -10,7 +10,7 @@ from typing import Optional, Type
 from myfyp_amd.management.logger import logger
 from myfyp_amd.parallel import weights_plane
 from myfyp_amd.stages.base_node.vote_train_set_stage import make_votes, tally_votes
-from myfyp_amd.stages.collective import fused_round
+from myfyp_amd.stages.collective import driver, fused_round
 from myfyp_amd.stages.collective._common import fed, set_gang_expectations
 from myfyp_amd.stages.stage import Stage, check_early_stop
 from myfyp_amd.stages.stage_factory import StageFactory
@@ -39,10 +39,15 @@ class VoteTrainSetStage(Stage):
             # ranks learn who is alive
             train_set = sorted(allv, key=lambda a: f.all_peers().index(a)) if everyone else tally_votes(allv)
             set_gang_expectations(f, set(train_set), set(train_set))
-            return train_set, fused_round.eligible(f, aggregator)
+            return train_set, fused_round.eligible(f, aggregator), driver.eligible(f, aggregator)
 
-        train_set, state.fused_round = f.gang_run(state.addr, votes, leader)
+        train_set, state.fused_round, drive = f.gang_run(state.addr, votes, leader)
         state.train_set = list(train_set)
+        if drive:
+            # the remaining rounds of every co-located peer run on one driver thread (driver.py);
+            # this peer's workflow ends when its experiment does
+            f.round_driver().enter(dict(kwargs, state=state, communication_protocol=communication_protocol))
+            return None
         logger.info(state.addr, f"🚂 Train set of {len(state.train_set)} nodes: {state.train_set}")
         if state.addr in state.train_set:
             return StageFactory.get_stage("TrainStage", "collective")

@@ -34,6 +34,9 @@ s = io.StringIO()
 st = pstats.Stats(profiles[0], stream=s)
 for p in profiles[1:]:
     st.add(p)
+out = os.environ.get("PSTATS_OUT")
+if out:
+    st.dump_stats(out)
 st.sort_stats("tottime").print_stats(40)
 st.sort_stats("cumulative").print_stats("myfyp_amd", 60)
 print(s.getvalue()[:12000], file=sys.stderr)

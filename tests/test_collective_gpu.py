@@ -1,0 +1,79 @@
+"""Collective workflow on the fused MLP engine (MI355X): the threaded stage path, the fused round
+(evaluate + fit + FedAvg in one gang op) and the lock-step round driver must give the reference
+invariants — stage-history pattern, equal models, learning — and the same trajectories."""
+
+import time
+
+import pytest
+import torch
+
+from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
+from myfyp_amd.learning.aggregators import FedAvg
+from myfyp_amd.learning.dataset.partition_strategies import RandomIIDPartitionStrategy
+from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
+from myfyp_amd.learning.frameworks.torch import TorchModel
+from myfyp_amd.management.logger import logger
+from myfyp_amd.models import MLP
+from myfyp_amd.node import Node
+from myfyp_amd.parallel.federation import Federation
+from myfyp_amd.parallel.mlp_engine import MLPGroup
+from myfyp_amd.settings import Settings
+from myfyp_amd.utils.utils import check_equal_models, wait_to_finish
+
+pytestmark = pytest.mark.gpu
+
+
+def _history_ok(history, rounds):
+    expected_round = ["VoteTrainSetStage", "TrainStage|WaitAggregatedModelsStage", "GossipModelStage", "RoundFinishedStage"]
+    assert history[0] == "StartLearningStage"
+    body = history[1:]
+    assert len(body) == 4 * rounds, history
+    for i, name in enumerate(body):
+        assert name in expected_round[i % 4].split("|"), history
+
+
+@pytest.mark.parametrize("mode", ["driver", "fused_round", "threaded"])
+def test_collective_fused_engine_modes(mode):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from myfyp_amd.utils.seed import set_seed
+
+    saved = (Settings.FUSED_ROUND, Settings.ROUND_DRIVER, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW)
+    Settings.FUSED_ROUND = mode != "threaded"
+    Settings.ROUND_DRIVER = mode == "driver"
+    Settings.BATCH_SIZE = 64
+    Settings.TRAIN_SET_SIZE = 3
+    Settings.GANG_WINDOW = 5.0
+    set_seed(11)
+    MLPGroup.reset_all()
+    Federation.reset()
+    fed = Federation.init()
+    n, rounds = 4, 3
+    parts = synthetic_mnist(8000, 800, seed=5).generate_partitions(n, RandomIIDPartitionStrategy)
+    exp = f"cg-{mode}-{time.time_ns()}"
+    nodes = [
+        Node(TorchModel(MLP(seed=i)), parts[i], address=f"cg-{mode}-{i}-{time.time_ns()}", aggregator=FedAvg(), protocol=CollectiveCommunicationProtocol, exp_name=exp)
+        for i in range(n)
+    ]
+    try:
+        for nd in nodes:
+            nd.start()
+        assert all(nd.learner._engine is not None for nd in nodes)
+        fed.finalize()
+        nodes[0].set_start_learning(rounds=rounds, epochs=1)
+        wait_to_finish(nodes, timeout=120)
+        for nd in nodes:
+            _history_ok(nd.learning_workflow.history, rounds)
+        check_equal_models(nodes, atol=1e-5)
+        logs = logger.get_global_logs()[exp]
+        final = [dict(logs[nd.addr]["test_metric"])[rounds] for nd in nodes]
+        assert min(final) > 0.8, final
+        timings = [logger.get_timings().get(nd.addr, {}) for nd in nodes]
+        assert any("driver_round" in t for t in timings) == (mode == "driver")
+        assert any("fused_round" in t for t in timings) == (mode == "fused_round")
+    finally:
+        for nd in nodes:
+            nd.stop()
+        Federation.reset()
+        MLPGroup.reset_all()
+        Settings.FUSED_ROUND, Settings.ROUND_DRIVER, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW = saved
