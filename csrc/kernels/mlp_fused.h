@@ -32,6 +32,7 @@ struct MLPArgs {
   // the epoch's batches, gathered once in permutation order at the start of the epoch so that the
   // per-step kernels read contiguous rows instead of chasing perm -> pointer table -> row
   uint8_t* Xb;      // [P][xb_rows][D0]
+  bf16* Xb16;       // same batches as bf16 (persistent path; null otherwise)
   int* Yb;          // [P][xb_rows]
   int64_t xb_rows;  // max_steps * B
   // test data

@@ -656,6 +656,10 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   const uint8_t* xs = a.Xp[p] + src * (int64_t)a.D0;
   uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
   for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];
+  if (a.Xb16 != nullptr) {  // bf16 copy for the persistent epoch kernel (converted once per epoch)
+    bf16* xh = a.Xb16 + ((int64_t)p * a.xb_rows + i) * a.D0;
+    for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<bf16x8*>(xh)[q] = ld8_u8(xs + 8 * q);
+  }
   if (lane == 0) a.Yb[(int64_t)p * a.xb_rows + i] = a.Yp[p][src];
 }
 

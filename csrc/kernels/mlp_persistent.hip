@@ -79,6 +79,12 @@ __device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byt
 }
 __device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }
 
+typedef short pe_s16x4 __attribute__((ext_vector_type(4)));
+// v_mfma_f32_16x16x16_bf16: A lane (h, c) = A[c][4h..4h+3], B = B[4h..4h+3][c], C as 16x16x32
+__device__ __forceinline__ f32x4 mfma16_bf16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(pe_s16x4, a), __builtin_bit_cast(pe_s16x4, b), c, 0, 0, 0);
+}
+
 __device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
@@ -255,7 +261,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
   // ---- resident state: W1 rows (all waves; wave w owns K steps w, w+8, w+16, w+24) and the W2
   //      column slice (waves 4..7; wave 4+k owns o2 32k..32k+31)
   float w1[4][8], m1[4][8], v1[4][8];
-  float w2[8], m2[8], v2[8];
+  float w2[4], m2[4], v2[4];
   const int orow = NG * g + c;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -279,16 +285,14 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       }
     }
   }
-  const int ww = wave - 4;  // W2 wave index (valid for wave >= 4)
+  // W2 slice: wave w holds W2[16w + 4h + j][16g + c], j < 4 — the B fragment of a 16x16x16 MFMA
+  // over its 16 o2 rows and, identically, the lane layout of the dW2 tile C[o2][o] it computes
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    w2[j] = m2[j] = v2[j] = 0.f;
-    if (wave >= 4) {
-      const int64_t idx = pS + a.off_w2 + (int64_t)(32 * ww + kappa(h, j)) * PD1 + NG * g + c;
-      w2[j] = a.params[idx];
-      m2[j] = a.m[idx];
-      if (adam) v2[j] = a.v[idx];
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int64_t idx = pS + a.off_w2 + (int64_t)(16 * wave + 4 * h + j) * PD1 + NG * g + c;
+    w2[j] = a.params[idx];
+    m2[j] = a.m[idx];
+    v2[j] = adam ? a.v[idx] : 0.f;
   }
   if (tid < 16) {
     const int64_t idx = pS + a.off_b1 + NG * g + tid;
@@ -310,41 +314,23 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     r = idx >> 2;
     col = 32 * s + 8 * (idx & 3);
     ok = s < KS1 && col < D0;
-    return a.Xb + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + col;
+    return a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + col;
   };
-  auto xw_load = [&](int t, int lv, uint2 (&xr)[XPT]) {
+  auto xw_stage = [&](int t, int lv) {  // batch t -> LDS (16-byte bf16 chunks, no conversion)
     const int rows = rows_at(a, n, t);
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
       bool ok;
       int r, col;
-      const uint8_t* src = xw_addr(t, k, lv, ok, r, col);
-      xr[k] = (ok && r < rows) ? *reinterpret_cast<const uint2*>(src) : uint2{0u, 0u};
-    }
-  };
-  auto xw_store = [&](int t, int lv, const uint2 (&xr)[XPT]) {
-#pragma unroll
-    for (int k = 0; k < XPT; ++k) {
-      bool ok;
-      int r, col;
-      xw_addr(t, k, lv, ok, r, col);
-      if (ok) {
-        bf16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (bf16)(float)((((j < 4) ? xr[k].x : xr[k].y) >> (8 * (j & 3))) & 0xffu);
-        *reinterpret_cast<bf16x8*>(sX + r * LDX + col) = o;
-      }
+      const bf16* src = xw_addr(t, k, lv, ok, r, col);
+      if (ok) *reinterpret_cast<uint4*>(sX + r * LDX + col) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
     }
   };
   for (int e = tid; e < BP * (KS1 * 32 - D0); e += NT) {
     const int r = e / (KS1 * 32 - D0), q = e % (KS1 * 32 - D0);
     sX[r * LDX + D0 + q] = (bf16)0.f;
   }
-  if (nsteps > 0) {
-    uint2 xr[XPT];
-    xw_load(0, lane, xr);
-    xw_store(0, lane, xr);
-  }
+  if (nsteps > 0) xw_stage(0, lane);
 
   // ---- the bf16 W2 slice goes to the head in ITS B-fragment order: chunk (wave w, K step ks,
   //      lane l) = 8 bf16 W2[16w + (l & 15)][32ks + 8(l >> 4) .. +8] at w2x[p][w][ks][l], so each
@@ -358,10 +344,8 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
   };
   // ---- initial W2 publish (version 1)
   auto publish_w2 = [&](unsigned version) {
-    if (wave >= 4) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
-    }
+    for (int j = 0; j < 4; ++j) sW2g[(16 * wave + 4 * h + j) * 16 + c] = (bf16)w2[j];
     __syncthreads();
     w2_store(tid);
     publish(pb.flags, p, F_W2 + g, version);
@@ -429,14 +413,16 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     // loads are consumed right away, so no registers stay live across the backward phase); they
     // are re-read from L2 and staged after this wave's dW1 update
     const bool more = t + 1 < nsteps;
-    if (more) {
-      uint2 xr[XPT];
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      xw_load(t + 1, lv, xr);
+    if (more) {  // one 4-byte load per 64-byte row segment pulls the line into L2
+      const int rows_n = rows_at(a, n, t + 1);
       unsigned sink = 0;
 #pragma unroll
-      for (int k = 0; k < XPT; ++k) sink ^= xr[k].x ^ xr[k].y;
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        const int r = lane;  // rows 0..63 (BP <= 64)
+        if (s < KS1 && r < rows_n && r < BP)
+          sink ^= *reinterpret_cast<const unsigned*>(a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B + r) * D0 + 32 * s);
+      }
       asm volatile("" ::"v"(sink));
     }
 
@@ -451,24 +437,21 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       *reinterpret_cast<unsigned long long*>(sDH2 + b * LD2 + 4 * q) = v;
     }
     lds_barrier();
-    // C1: dH1 partials (waves 4..7: K = o2 block of the wave), W2 before this step's update
-    if (wave >= 4) {
-      bf16x8 bw;
+    // C1: dH1 partials — every wave its 16 o2 rows (K = 16), W2 before this step's update
+    {
+      bf16x4 bw;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bw[j] = (bf16)w2[j];
+      for (int j = 0; j < 4; ++j) bw[j] = (bf16)w2[j];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16* dp = sDH2 + (16 * mt + c) * LD2 + 32 * ww + 4 * h;
-        const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(dp), *reinterpret_cast<const bf16x4*>(dp + 16));
-        sRed[(ww * MT + mt) * 64 + lane] = mfma_bf16(af, bw, zero4());
-      }
+      for (int mt = 0; mt < MT; ++mt)
+        sRed[(wave * MT + mt) * 64 + lane] = mfma16_bf16(*reinterpret_cast<const bf16x4*>(sDH2 + (16 * mt + c) * LD2 + 16 * wave + 4 * h), bw, zero4());
     }
     lds_barrier();
     if (tid < MT * 64) {
       const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
       f32x4 s = sRed[mt * 64 + (tid & 63)];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
       float db = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -483,33 +466,41 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     }
     lds_barrier();
     if (g == 0) PE_STAMP(0, t, 3);
-    // C3 (waves 4..7): dW2 columns + update, bf16 slice staged in LDS for the publish below.
-    // C2 (every wave, its own K steps): dW1 rows + update — waves 0..3 start on it at once.
-    if (wave >= 4) {
-      float gr[8];
+    // C3 (every wave, its 16 o2 rows): dW2 tile + update, bf16 slice staged in LDS for the publish
+    // below; then C2 (every wave, its own K steps): dW1 rows + update
+    {
+      f32x4 acc = zero4();
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        f32x4 acc = zero4();
+      for (int kb = 0; kb < BP / 32; ++kb) acc = mfma_bf16(frag_b_tr(sDH2, LD2, 32 * kb, 16 * wave), frag_b_tr(sH1, 16, 32 * kb, 0), acc);
 #pragma unroll
-        for (int kb = 0; kb < BP / 32; ++kb)
-          acc = mfma_bf16(frag_b_tr(sDH2, LD2, 32 * kb, 32 * ww + 16 * tt), frag_b_tr(sH1, 16, 32 * kb, 0), acc);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gr[4 * tt + i] = acc[i];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        upd<ADAM>(a, gr[j], w2[j], m2[j], v2[j], lr_t, inv_bc2);
-        sW2g[(32 * ww + kappa(h, j)) * 16 + c] = (bf16)w2[j];
+      for (int j = 0; j < 4; ++j) {
+        upd<ADAM>(a, acc[j], w2[j], m2[j], v2[j], lr_t, inv_bc2);
+        sW2g[(16 * wave + 4 * h + j) * 16 + c] = (bf16)w2[j];
       }
     }
     {
       bf16x8 bd[BP / 32];
 #pragma unroll
       for (int kb = 0; kb < BP / 32; ++kb) bd[kb] = frag_b_tr(sDH1, 16, 32 * kb, 0);
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
+      const int rows_next = more ? rows_at(a, n, t + 1) : 0;
+      const bf16* xnext = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int s = wave + 8 * q;
+        __builtin_amdgcn_sched_barrier(0);
         if (s < KS1) {
+          // the next batch's columns of this K step (L2-resident since the touch above): issued
+          // first, landed in LDS right after this K step's dW1 MFMAs have read the current ones
+          constexpr int XQ = BP / 16;
+          uint4 xq[XQ];
+#pragma unroll
+          for (int kk = 0; kk < XQ; ++kk) {
+            const int idx = kk * 64 + lv;
+            const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+            xq[kk] = (more && col < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + col)) : uint4{0u, 0u, 0u, 0u};
+          }
           float gr[8];
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt) {
@@ -521,17 +512,18 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) upd<ADAM>(a, gr[j], w1[q][j], m1[q][j], v1[q][j], lr_t, inv_bc2);
+          if (more) {
+#pragma unroll
+            for (int kk = 0; kk < XQ; ++kk) {
+              const int idx = kk * 64 + lv;
+              const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+              if (col < D0) *reinterpret_cast<uint4*>(sX + r * LDX + col) = xq[kk];
+            }
+          }
         }
       }
     }
     if (tid < 16) upd<ADAM>(a, sDb1[tid], sB1[tid], sB1[16 + tid], sB1[32 + tid], lr_t, inv_bc2);
-    if (more) {  // this wave's columns of the next batch (L2-resident by now)
-      uint2 xr[XPT];
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      xw_load(t + 1, lv, xr);
-      xw_store(t + 1, lv, xr);
-    }
     __syncthreads();  // sDH1 / sB1 reads done; sW2g complete
     if (g == 0) PE_STAMP(0, t, 4);
     // updated W2 slice to the head (write-through) and the next batch into LDS; one drain + flag
@@ -565,17 +557,15 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       }
     }
   }
-  if (wave >= 4) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int o2 = 32 * ww + kappa(h, j);
-      const int64_t idx = pS_w + a.off_w2 + (int64_t)o2 * PD1 + orow_w;
-      a.params[idx] = w2[j];
-      a.m[idx] = m2[j];
-      if (adam) a.v[idx] = v2[j];
-      a.shadow[idx] = (bf16)w2[j];
-      a.w2t[(int64_t)p * PD1 * PD2 + (int64_t)orow_w * PD2 + o2] = (bf16)w2[j];
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int o2 = 16 * wave + 4 * h + j;
+    const int64_t idx = pS_w + a.off_w2 + (int64_t)o2 * PD1 + orow_w;
+    a.params[idx] = w2[j];
+    a.m[idx] = m2[j];
+    if (adam) a.v[idx] = v2[j];
+    a.shadow[idx] = (bf16)w2[j];
+    a.w2t[(int64_t)p * PD1 * PD2 + (int64_t)orow_w * PD2 + o2] = (bf16)w2[j];
   }
   if (tid < 16) {
     const int64_t idx = pS_w + a.off_b1 + NG * g + tid;

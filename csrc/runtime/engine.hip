@@ -89,7 +89,7 @@ struct MLPEngine {
   bool graph_persistent = false;
 
   bool use_persistent() const {
-    if (persist_mode == 0 || pb.h1x == nullptr) return false;
+    if (persist_mode == 0 || pb.h1x == nullptr || a.Xb16 == nullptr) return false;
     if (a.P * 17 > num_cus) return false;  // every gang must be co-resident (one workgroup per CU)
     return mlp_persistent_supported(a);
   }
@@ -100,6 +100,7 @@ struct MLPEngine {
     if (cap_stream) hipStreamDestroy(cap_stream);
     for (void* p : owned) hipFree(p);
     if (a.Xb) hipFree(a.Xb);
+    if (a.Xb16) hipFree(a.Xb16);
     if (a.Yb) hipFree(a.Yb);
     for (auto& r : ring) {
       if (r.ev) hipEventDestroy(r.ev);
@@ -155,8 +156,12 @@ struct MLPEngine {
     invalidate();
     if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
     CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
-    mlp_launch_gather_epoch(a, cap_stream);
     graph_persistent = use_persistent();
+    {
+      MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
+      if (!graph_persistent) ga.Xb16 = nullptr;
+      mlp_launch_gather_epoch(ga, cap_stream);
+    }
     if (graph_persistent) {
       hipError_t le = mlp_launch_persistent_epoch(a, pb, cap_stream);
       if (le != hipSuccess) {
@@ -352,13 +357,19 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
   const int64_t rows = (int64_t)(max_steps > 0 ? max_steps : 1) * e->a.B;
   if (rows != e->a.xb_rows) {  // epoch batch buffers
     if (e->a.Xb) hipFree(e->a.Xb);
+    if (e->a.Xb16) hipFree(e->a.Xb16);
     if (e->a.Yb) hipFree(e->a.Yb);
     e->a.Xb = nullptr;
+    e->a.Xb16 = nullptr;
     e->a.Yb = nullptr;
     CHECK_HIP(hipMalloc((void**)&e->a.Xb, (size_t)e->a.P * rows * e->a.D0));
     CHECK_HIP(hipMalloc((void**)&e->a.Yb, (size_t)e->a.P * rows * sizeof(int)));
     CHECK_HIP(hipMemset(e->a.Xb, 0, (size_t)e->a.P * rows * e->a.D0));
     CHECK_HIP(hipMemset(e->a.Yb, 0, (size_t)e->a.P * rows * sizeof(int)));
+    if (e->pb.h1x != nullptr) {
+      CHECK_HIP(hipMalloc((void**)&e->a.Xb16, (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
+      CHECK_HIP(hipMemset(e->a.Xb16, 0, (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
+    }
     e->a.xb_rows = rows;
   }
   e->invalidate();
@@ -480,7 +491,11 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
   if (e->upload(s, nullptr)) return 1;
-  mlp_launch_gather_epoch(e->a, s);
+  {
+    MLPArgs ga = e->a;
+    if (!e->use_persistent()) ga.Xb16 = nullptr;
+    mlp_launch_gather_epoch(ga, s);
+  }
   if (e->use_persistent()) {
     CHECK_HIP(mlp_launch_persistent_epoch(e->a, e->pb, s));
   } else {

@@ -25,7 +25,12 @@ lib.mlp_debug_persistent_stamps.argtypes = [ctypes.c_void_p]
 lib.mlp_debug_persistent_stamps.restype = ctypes.c_int
 P, B = int(os.environ.get("PEERS", "8")), 64
 parts = synthetic_mnist(60000, 10000, seed=1).generate_partitions(8, RandomIIDPartitionStrategy)
-ls = [TorchLearner(TorchModel(MLP(seed=i)), parts[i], f"p{i}", batch_size=B, device="cuda") for i in range(P)]
+ls = []
+for i in range(P):
+    m = MLP(seed=i)
+    if os.environ.get("OPT") == "sgd":
+        m.optimizer_spec = lambda: {"name": "sgd", "lr": 1e-3}
+    ls.append(TorchLearner(TorchModel(m), parts[i], f"p{i}", batch_size=B, device="cuda"))
 g = ls[0]._engine.group
 assert g.uses_persistent()
 for it in range(2):
