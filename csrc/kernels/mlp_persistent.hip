@@ -211,7 +211,7 @@ __host__ __device__ inline OwnerLds owner_lds(int Bpad, int D0) {
   return L;
 }
 struct HeadLds {
-  size_t h1, h2, dlog, w3, red, b2, b3, ok, total;
+  size_t h1, h2, dlog, w3, b2, b3, ok, total;
 };
 __host__ __device__ inline HeadLds head_lds(int Bpad) {
   HeadLds L;
@@ -221,7 +221,6 @@ __host__ __device__ inline HeadLds head_lds(int Bpad) {
   L.h2 = o;   o += al16((size_t)Bpad * LD2 * 2);
   L.dlog = o; o += al16((size_t)Bpad * LDL * 2);
   L.w3 = o;   o += al16((size_t)32 * LDW3 * 2);
-  L.red = o;  o += al16((size_t)4 * MT * 64 * 16);
   L.b2 = o;   o += al16(3 * PD2 * 4);
   L.b3 = o;   o += al16(3 * 16 * 4);
   L.ok = o;   o += 16;
@@ -592,7 +591,6 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   bf16* sH2 = reinterpret_cast<bf16*>(smem + L.h2);
   bf16* sDlog = reinterpret_cast<bf16*>(smem + L.dlog);
   bf16* sW3 = reinterpret_cast<bf16*>(smem + L.w3);
-  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
   float* sB2 = reinterpret_cast<float*>(smem + L.b2);  // [3][128]
   float* sB3 = reinterpret_cast<float*>(smem + L.b3);  // [3][16]
   int* sOk = reinterpret_cast<int*>(smem + L.ok);
@@ -699,23 +697,14 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     }
     lds_barrier();
     PE_STAMP(1, t, 3);
-    // ---- logits partials (waves 0..3: K = o2 block of the wave, W3 before this step's update)
-    if (wave < 4) {
-      bf16x8 bw;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bw[j] = (bf16)w3[j];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16* hp = sH2 + (16 * mt + c) * LD2 + 32 * wave + 4 * h;
-        sRed[(wave * MT + mt) * 64 + lane] = mfma_bf16(cat8(*reinterpret_cast<const bf16x4*>(hp), *reinterpret_cast<const bf16x4*>(hp + 16)), bw, zero4());
-      }
-    }
-    lds_barrier();
-    // ---- log-softmax + NLL + argmax + dlogits (wave w < MT: batch rows 16w..16w+15)
+    // ---- logits + log-softmax + NLL + argmax + dlogits: wave w < MT owns batch rows 16w..16w+15
+    //      and all 128 inputs (4 chained MFMAs, W3 bf16 from LDS, before this step's update), so
+    //      the row statistics need no cross-wave reduction
     if (wave < MT) {
-      f32x4 lg = sRed[wave * 64 + lane];
+      f32x4 lg = zero4();
 #pragma unroll
-      for (int w = 1; w < 4; ++w) lg += sRed[(w * MT + wave) * 64 + lane];
+      for (int ks = 0; ks < PD2 / 32; ++ks)
+        lg = mfma_bf16(ld8(sH2 + (16 * wave + c) * LD2 + 32 * ks + 8 * h), ld8(sW3 + c * LDW3 + 32 * ks + 8 * h), lg);
       const float b3 = sB3[c];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -751,7 +740,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     }
     lds_barrier();
 #pragma unroll
-    for (int k = 0; k < BP / 16; ++k) {
+    for (int k = 0; k < BP / 16; ++k) {  // row-wise 8-byte chunks: whole 256-byte rows per wave
       const int e = tv + NT * k;
       const int b = e >> 5, q = e & 31;
       st_wt(pb.dh2x + ((int64_t)p * BP + b) * PD2 + 4 * q, *reinterpret_cast<const unsigned long long*>(sDH2 + b * LD2 + 4 * q));
