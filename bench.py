@@ -40,8 +40,8 @@ BASELINE_ROUNDS_PER_SEC = 0.5
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed federated rounds")
-    ap.add_argument("--warmup", type=int, default=3, help="untimed rounds (graph capture, caches)")
+    ap.add_argument("--steps", type=int, default=200, help="timed federated rounds (~2 ms each on MI355X)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed rounds (graph capture, caches)")
     ap.add_argument("--peers", type=int, default=8)
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--epochs", type=int, default=1)
@@ -170,6 +170,11 @@ def main() -> None:
     # per-stage wall-time breakdown of the first local peer (stderr, diagnostics only)
     tm = logger.get_timings().get(nodes[0].addr, {})
     brk = {k: round(1000 * float(np.median(v[args.warmup :] or v)), 3) for k, v in tm.items()}
+    ends = [round_end[r] for r in sorted(round_end) if r >= args.warmup - 1]
+    if len(ends) > 2:
+        d = np.diff(ends) * 1000.0
+        print(f"[bench] rank {rank} round-end interval ms: p10 {np.percentile(d, 10):.3f} p50 {np.percentile(d, 50):.3f} "
+              f"p90 {np.percentile(d, 90):.3f} max {d.max():.3f}", file=sys.stderr, flush=True)
     print(f"[bench] rank {rank} median ms per call: {json.dumps(brk)} fed: "
           f"{ {k: round(1000 * float(np.median(v)), 3) for k, v in fed.stats.items()} }", file=sys.stderr, flush=True)
     for n in nodes:
