@@ -719,6 +719,13 @@ class CNNGroup:
         self.stat = self.fbuf("stat", 4)
         self.conf = self.ibuf("conf", 256)
 
+    def fedavg_buffer(self) -> torch.Tensor:
+        """Device scratch of numel + 1 floats for the stacked FedAvg (weighted sum | Σw)."""
+        buf = getattr(self, "_fedavg_buf", None)
+        if buf is None or buf.numel() != self.numel + 1:
+            buf = self._fedavg_buf = torch.empty(self.numel + 1, dtype=torch.float32, device=self.device)
+        return buf
+
     def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         with self.lock, torch.cuda.device(self.device):
             self._ensure()

@@ -144,11 +144,12 @@ class RoundDriver:
             for a, m in cur.items():
                 lr = m.kw["learner"]
                 if a in out:
-                    ev, (steps, raw) = out[a]
+                    ev, fit = out[a]
                     if ev is not None:
                         lr._evaluate_done(ev, snaps[a])
+                    steps, mean_loss = fused_round.fit_result(fit)
                     lr.global_step += steps
-                    lr._fit_done(steps, raw.map(lambda v: v[0]), reqs[a][0])
+                    lr._fit_done(steps, mean_loss, reqs[a][0])
                 model = lr.get_model()
                 model.set_contribution(train_set or [a], max(1, model.num_samples))
             # ---- GossipModelStage (no-op after the all-reduce) and RoundFinishedStage

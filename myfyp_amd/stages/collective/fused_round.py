@@ -17,8 +17,17 @@ import time
 
 from myfyp_amd.management.logger import logger
 from myfyp_amd.parallel import weights_plane
+from myfyp_amd.parallel.pending import Pending
 from myfyp_amd.settings import Settings
 from myfyp_amd.stages.collective._common import fed
+
+
+def fit_result(fit):
+    """(steps, mean train loss) of a group fit result: the MLP engine returns (steps, Pending of
+    (loss, acc)) resolved asynchronously; the CNN engine (steps, loss, acc) as host floats."""
+    if isinstance(fit[1], Pending):
+        return fit[0], fit[1].map(lambda v: v[0])
+    return fit[0], float(fit[1])
 
 
 def eligible(f, aggregator) -> bool:
@@ -65,11 +74,12 @@ def join(state, learner, aggregator, trainer: bool) -> None:
 
     res = f.gang_run(state.addr, (trainer, n, req, has_test), leader)
     if trainer:
-        ev, (steps, raw) = res[state.addr]
+        ev, fit = res[state.addr]
         if ev is not None:
             learner._evaluate_done(ev, snap)
+        steps, mean_loss = fit_result(fit)
         learner.global_step += steps
-        learner._fit_done(steps, raw.map(lambda v: v[0]), req[0])
+        learner._fit_done(steps, mean_loss, req[0])
     model = learner.get_model()
     model.set_contribution(list(state.train_set) or [state.addr], max(1, model.num_samples))
     logger.log_timing(state.addr, "fused_round", time.time() - t0)
