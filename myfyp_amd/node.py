@@ -41,6 +41,7 @@ from myfyp_amd.learning.aggregators.fedavg import FedAvg
 from myfyp_amd.learning.frameworks.learner import Learner
 from myfyp_amd.learning.frameworks.learner_factory import LearnerFactory
 from myfyp_amd.learning.frameworks.p2pfl_model import P2PFLModel
+from myfyp_amd.learning.frameworks.simulation import try_init_learner_with_ray
 from myfyp_amd.management.logger import logger
 from myfyp_amd.node_state import NodeState
 from myfyp_amd.stages.workflows import LearningWorkflow
@@ -68,7 +69,8 @@ class Node:
         self.aggregator.set_node_name(self.addr)
         if learner is None:
             learner = LearnerFactory.create_learner(model)
-        self.learner: Learner = learner(model, data, self.addr, self.aggregator, **(learner_kwargs or {}))
+        # plain learner, or (Settings.SIMULATION_POOL) one pinned to a device of the simulation pool
+        self.learner: Learner = try_init_learner_with_ray(learner, model, data, self.addr, self.aggregator, **(learner_kwargs or {}))
         self.exp_name = exp_name
         self._running = False
         self.state = NodeState(self.addr, simulation=simulation)

@@ -100,6 +100,11 @@ class Settings:
     # ... and the rounds of all co-located fused peers are driven by ONE host thread (driver.py)
     ROUND_DRIVER: bool = True
 
+    # ---------------- SIMULATION (Ray actor pool → device pool, learning/frameworks/simulation)
+    SIMULATION_POOL: bool = False  # True: learners run fit/evaluate as jobs on per-device worker streams
+    SIMULATION_RESOURCES: Dict[str, float] | None = None  # per virtual client, e.g. {"num_cpus": 1, "num_gpus": 0.25}
+    SIMULATION_WORKERS_PER_GPU: int = 4  # default pool shape when GPUs are visible
+
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
     CHECKPOINT_EVERY: int = 1
@@ -113,6 +118,9 @@ class Settings:
             "LOG_DIR": "LOG_DIR",
             "EXCLUDE_BEAT_LOGS": "EXCLUDE_BEAT_LOGS",
             "DISABLE_RAY": "DISABLE_RAY",
+            "SIMULATION_POOL": "SIMULATION_POOL",
+            "SIMULATION_RESOURCES": "SIMULATION_RESOURCES",
+            "SIMULATION_WORKERS_PER_GPU": "SIMULATION_WORKERS_PER_GPU",
             "CHECKPOINT_DIR": "CHECKPOINT_DIR",
             "CHECKPOINT_EVERY": "CHECKPOINT_EVERY",
         }
