@@ -56,6 +56,7 @@ struct Handle {
   int world;
   uint64_t slot_bytes;
   uint64_t gen;
+  bool owns_map = true;  // false for shmc_view handles (same mapping, another rank)
   Header* hdr() const { return reinterpret_cast<Header*>(base); }
   RankCtl* ctl(int r) const { return reinterpret_cast<RankCtl*>(static_cast<char*>(base) + sizeof(Header)) + r; }
   char* slot(int r, int parity) const {
@@ -138,7 +139,7 @@ void* shmc_open(const char* name, int rank, int world, uint64_t slot_bytes, int 
   void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (base == MAP_FAILED) return nullptr;
-  Handle* h = new Handle{base, bytes, rank, world, slot_bytes, 0};
+  Handle* h = new Handle{base, bytes, rank, world, slot_bytes, 0, true};
   Header* hd = h->hdr();
   if (create) {
     std::memset(base, 0, sizeof(Header) + sizeof(RankCtl) * world);
@@ -213,10 +214,24 @@ int shmc_barrier(void* handle, double timeout_s) {
   return 0;
 }
 
+// A second rank's handle onto the SAME mapping as `handle` (threads as ranks inside one process:
+// the ThreadSanitizer driver csrc/host/tests/shm_collective_tsan.cpp uses it so that every rank's
+// accesses hit the same addresses and the publish/acquire protocol is checked, not just run).
+void* shmc_view(void* handle, int rank) {
+  Handle* h = static_cast<Handle*>(handle);
+  if (!h || rank < 0 || rank >= h->world) {
+    errno = EINVAL;
+    return nullptr;
+  }
+  Handle* v = new Handle{h->base, h->bytes, rank, h->world, h->slot_bytes, 0, false};
+  v->hdr()->attached.fetch_add(1, std::memory_order_acq_rel);
+  return v;
+}
+
 void shmc_close(void* handle) {
   Handle* h = static_cast<Handle*>(handle);
   if (!h) return;
-  munmap(h->base, h->bytes);
+  if (h->owns_map) munmap(h->base, h->bytes);
   delete h;
 }
 

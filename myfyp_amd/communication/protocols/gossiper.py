@@ -21,6 +21,7 @@ from typing import Any, Callable, Deque, List, Optional, Tuple
 from myfyp_amd.communication.protocols.client import Client
 from myfyp_amd.management.logger import logger
 from myfyp_amd.settings import Settings
+from myfyp_amd.utils.lockcheck import make_lock
 
 
 class Gossiper(threading.Thread):
@@ -34,7 +35,7 @@ class Gossiper(threading.Thread):
         self.messages_per_period = Settings.GOSSIP_MESSAGES_PER_PERIOD if messages_per_period is None else messages_per_period
         self._processed: Deque[int] = collections.deque()
         self._processed_set: set = set()
-        self._processed_lock = threading.Lock()
+        self._processed_lock = make_lock("Gossiper.processed")
         self._pending: Deque[Tuple[Any, List[str]]] = collections.deque()
         self._cv = threading.Condition()
         self._terminate = threading.Event()

@@ -11,6 +11,7 @@ import time
 from typing import Any, Dict, Tuple
 
 from myfyp_amd.management.logger import logger
+from myfyp_amd.utils.lockcheck import make_lock
 
 NeighborEntry = Tuple[Any, Any, float]
 
@@ -21,7 +22,7 @@ class Neighbors:
     def __init__(self, self_addr: str) -> None:
         self.self_addr = self_addr
         self.neis: Dict[str, NeighborEntry] = {}
-        self.neis_lock = threading.RLock()
+        self.neis_lock = make_lock("Neighbors.neis", reentrant=True)
 
     def connect(self, addr: str, non_direct: bool = False, handshake_msg: bool = True) -> NeighborEntry:
         raise NotImplementedError

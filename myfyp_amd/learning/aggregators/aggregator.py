@@ -21,6 +21,7 @@ from typing import List, Optional
 from myfyp_amd.learning.frameworks.p2pfl_model import P2PFLModel
 from myfyp_amd.management.logger import logger
 from myfyp_amd.settings import Settings
+from myfyp_amd.utils.lockcheck import make_lock
 
 
 class NoModelsToAggregateError(Exception):
@@ -38,7 +39,7 @@ class Aggregator:
         self._train_set: List[str] = []
         self._models: List[P2PFLModel] = []
         self.partial_aggregation = False
-        self._agg_lock = threading.Lock()
+        self._agg_lock = make_lock("Aggregator.agg")
         self._finish_aggregation_event = threading.Event()
         self._finish_aggregation_event.set()
 

@@ -16,6 +16,7 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 import numpy as np
 
 from myfyp_amd.learning.frameworks.exceptions import DecodingParamsError
+from myfyp_amd.management.tracing import traced
 
 _SAFE_GLOBALS = {
     ("numpy", "ndarray"),
@@ -66,6 +67,7 @@ class P2PFLModel:
         return self.model
 
     # ------------------------------------------------------------------ wire format
+    @traced("encode")
     def encode_parameters(self, params: Optional[List[np.ndarray]] = None) -> bytes:
         if params is None:
             params = self.get_parameters()

@@ -38,6 +38,7 @@ from myfyp_amd.management.logger import logger
 from myfyp_amd.parallel.flat_params import FlatParams
 from myfyp_amd.parallel.pending import Pending, resolve
 from myfyp_amd.settings import Settings, resolve_device
+from myfyp_amd.management.tracing import traced
 
 
 def classification_metrics(confusion: np.ndarray) -> Dict[str, float]:
@@ -184,6 +185,7 @@ class TorchLearner(Learner):
                 extra.update(cb.grad_correction())
         return extra
 
+    @traced("fit")
     def fit(self) -> P2PFLModel:
         self._interrupt.clear()
         for cb in self.callbacks:
@@ -328,6 +330,7 @@ class TorchLearner(Learner):
 
         return raw.map(done)
 
+    @traced("evaluate")
     def evaluate(self) -> Dict[str, float]:
         return self.evaluate_async().result()
 

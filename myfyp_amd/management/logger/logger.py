@@ -22,6 +22,7 @@ from typing import Any, Callable, Dict, List, Optional, Union
 from myfyp_amd.experiment import Experiment
 from myfyp_amd.management.metric_storage import GlobalLogsType, GlobalMetricStorage, LocalLogsType, LocalMetricStorage
 from myfyp_amd.settings import Settings
+from myfyp_amd.utils.lockcheck import make_lock
 
 
 class NodeNotRegistered(Exception):
@@ -57,7 +58,7 @@ class P2PFLogger:
 
     def __init__(self, nodes: Optional[Dict[str, Dict[str, Any]]] = None, disable_locks: bool = False) -> None:
         self._nodes: Dict[str, Dict[Any, Any]] = nodes if nodes else {}
-        self._nodes_lock = threading.RLock()
+        self._nodes_lock = make_lock("Logger.nodes", reentrant=True)
         self.local_metrics = LocalMetricStorage(disable_locks=disable_locks)
         self.global_metrics = GlobalMetricStorage(disable_locks=disable_locks)
         self.timings: Dict[str, Dict[str, List[float]]] = {}

@@ -14,6 +14,7 @@ import threading
 from typing import Dict, List, Optional
 
 from myfyp_amd.experiment import Experiment
+from myfyp_amd.utils.lockcheck import make_lock
 
 
 class NodeState:
@@ -34,8 +35,8 @@ class NodeState:
         self.round_votes: Dict[int, Dict[str, Dict[str, int]]] = {}
         self.experiment: Optional[Experiment] = None
 
-        self.train_set_votes_lock = threading.Lock()
-        self.start_thread_lock = threading.Lock()
+        self.train_set_votes_lock = make_lock("NodeState.train_set_votes")
+        self.start_thread_lock = make_lock("NodeState.start_thread")
         self.wait_votes_ready_lock = threading.Lock()
         self.votes_event = threading.Event()
         self.model_initialized_lock = threading.Lock()

@@ -105,6 +105,27 @@ def build_host(verbose: bool = False) -> str:
     return HOST_LIB
 
 
+def build_sanitized(sanitize: str = "thread", verbose: bool = False) -> str:
+    """Host runtime + its multi-threaded stress driver (``csrc/host/tests``) built with
+    ``-fsanitize=<sanitize>`` ("thread", "address,undefined"): SURVEY §5.2's sanitizer job for the
+    native host code. GPU code is not instrumented (no device sanitizers on this pool)."""
+    tag = sanitize.replace(",", "_")
+    out_dir = os.path.join(ROOT, "build", "sanitize", tag)
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "shm_collective_stress")
+    srcs = host_sources() + sorted(glob.glob(os.path.join(CSRC, "host", "tests", "*.cpp")))
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(s) for s in srcs):
+        return exe
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
+    cmd = [cxx, "-O1", "-g", "-std=c++17", f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", *srcs, "-o", exe, "-lrt", "-pthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"sanitizer build failed:\n{res.stdout}\n{res.stderr}")
+    return exe
+
+
 if __name__ == "__main__":
     print(build_host(verbose="-v" in sys.argv))
     print(build(verbose="-v" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))

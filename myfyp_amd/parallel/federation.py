@@ -31,6 +31,7 @@ import torch
 
 from myfyp_amd.management.logger import logger
 from myfyp_amd.settings import Settings
+from myfyp_amd.utils.lockcheck import make_lock
 
 
 # ---------------------------------------------------------------------------------------------
@@ -188,7 +189,7 @@ class Federation:
         self.finalized = threading.Event()
         self.round_hooks: List[Callable[[int, "Federation"], None]] = []
         self.stats: Dict[str, List[float]] = {}
-        self._lock = threading.Lock()
+        self._lock = make_lock("Federation.state")
         self._cpu_pg = None
         self.shm = None  # node-local shared-memory control plane (single-node jobs)
         self._round_driver = None

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from myfyp_amd import ops
+from myfyp_amd.management.tracing import traced
 from myfyp_amd.parallel.federation import Federation
 
 
@@ -68,6 +69,7 @@ def gather_votes(fed: Federation, arrived: Dict[str, Dict[str, int]]) -> Dict[st
 # ---------------------------------------------------------------------------------------------
 # aggregation
 # ---------------------------------------------------------------------------------------------
+@traced("aggregate_mean")
 def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tuple[float, List[str]]:
     """Sample-weighted mean of the trainers' models (weight 0 for non-trainers), result into every
     local peer. One local weighted reduction kernel + one all-reduce + one broadcast kernel."""
@@ -143,6 +145,7 @@ def _unpack_into(learner, flat: torch.Tensor) -> None:
             off += t.numel()
 
 
+@traced("aggregate_neighbors")
 def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) -> List[str]:
     """Topology mixing ``x_i ← Σ_j W_ij x_j`` (see ``NeighborAvg``): co-located rows are combined
     with the ``weighted_average`` kernel, rows of neighbours on other ranks arrive through one

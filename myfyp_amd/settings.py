@@ -105,6 +105,10 @@ class Settings:
     SIMULATION_RESOURCES: Dict[str, float] | None = None  # per virtual client, e.g. {"num_cpus": 1, "num_gpus": 0.25}
     SIMULATION_WORKERS_PER_GPU: int = 4  # default pool shape when GPUs are visible
 
+    # ---------------- DEBUG (new: SURVEY §5.1/§5.2)
+    LOCK_CHECK: bool | str = False  # True/"record": lock-order inversions recorded; "raise": raised (utils/lockcheck.py)
+    TRACE_MARKERS: bool = False  # roctx ranges around fit / evaluate / aggregation / stages (management/tracing.py)
+
     # ---------------- CHECKPOINT (new: SURVEY §5.4)
     CHECKPOINT_DIR: str | None = None  # None = off; else save every CHECKPOINT_EVERY rounds
     CHECKPOINT_EVERY: int = 1

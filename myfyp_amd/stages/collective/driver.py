@@ -23,8 +23,10 @@ from typing import Any, Dict
 
 from myfyp_amd.management.checkpoint import maybe_checkpoint
 from myfyp_amd.management.logger import logger
+from myfyp_amd.management.tracing import mark
 from myfyp_amd.parallel import weights_plane
 from myfyp_amd.settings import Settings
+from myfyp_amd.utils.lockcheck import make_lock
 from myfyp_amd.stages.base_node.vote_train_set_stage import make_votes, tally_votes
 from myfyp_amd.stages.collective import fused_round
 
@@ -56,7 +58,7 @@ class RoundDriver:
 
     def __init__(self, f) -> None:
         self.f = f
-        self.lock = threading.Lock()
+        self.lock = make_lock("RoundDriver.members")
         self.members: Dict[str, _Member] = {}
         self.active = False
 
@@ -116,6 +118,7 @@ class RoundDriver:
             if not cur:
                 return
             t0 = time.time()
+            mark("driver_round")
             states = {a: m.kw["state"] for a, m in cur.items()}
             round_ = next(iter(states.values())).round
             train_set = list(next(iter(states.values())).train_set)

@@ -8,6 +8,7 @@ import time
 from typing import Any, Callable, Dict, List, Optional, Type
 
 from myfyp_amd.management.logger import logger
+from myfyp_amd.management.tracing import trace_range
 from myfyp_amd.stages.stage import Stage, check_early_stop
 from myfyp_amd.stages.stage_factory import StageFactory
 
@@ -36,7 +37,8 @@ class StageWokflow:
                 for hook in list(self.hooks):
                     hook(self.current_stage.name(), kwargs)
                 t0 = time.time()
-                next_stage: Optional[Type[Stage]] = self.current_stage.execute(**kwargs)
+                with trace_range(f"{self.current_stage.name()}/{state.addr}"):
+                    next_stage: Optional[Type[Stage]] = self.current_stage.execute(**kwargs)
                 logger.log_timing(state.addr, self.current_stage.name(), time.time() - t0)
                 if next_stage is None or check_early_stop(state, raise_exception=False):
                     break
