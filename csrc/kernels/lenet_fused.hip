@@ -1,0 +1,732 @@
+// Fused LeNet-5 step for the grouped CNN engine (BASELINE config 3: 8 peers, LeNet-5 on CIFAR-shaped
+// data, ring neighbour averaging).
+//
+// Why: LeNet's layers are tiny (6 and 16 channels, 120/84/10 units). Run layer by layer through the
+// generic implicit-GEMM conv kernels a step is ~32 launches of 4–27 µs each (0.35 ms for 8 peers ×
+// 64 images, profiles/r1h_lenet), almost all of it fixed cost: 128-wide MFMA tiles over 6 valid
+// channels, activations round-tripped through HBM between layers. Here ONE workgroup (8 waves) takes
+// IPW images of one peer through the whole network and back with every activation resident in LDS:
+//
+//   uint8 HWC gather (epoch permutation) → conv1 5×5 + bias + ReLU + 2×2 max-pool (argmax kept) →
+//   conv2 + ReLU + pool → fc1/fc2/fc3 → log-softmax + NLL (stats, confusion, dlogits) → fc3/fc2/fc1
+//   dgrad with the ReLU masks → pool-2 backward → conv2 weight gradient + conv2 dgrad → pool-1
+//   backward (on the fly) → conv1 weight gradient.
+//
+// Every contraction is a v_mfma_f32_16x16x16_bf16 over operands gathered straight from LDS; a conv
+// M-tile is 4 pooled positions × their 2×2 windows, so one lane's 4 accumulator rows are exactly
+// one pooling window and the max-pool (with its argmax) happens in registers. Conv weight/bias
+// gradients are reduced over the workgroup's images by the MFMA K loop and written as one fp32
+// record per workgroup; the small second kernel sums a peer's records and computes the fc weight
+// gradients (K = whole batch) — no global atomics (32 workgroups adding into the same 2.9 k
+// addresses serialised at L2 and stalled the next vmcnt wait by microseconds). The optimizer
+// (k_opt_step, cnn_ops.hip) then updates the master rows and refreshes the bf16 shadows read here.
+//
+// Fragment conventions (16x16x16 bf16 MFMA): lane l, h = l >> 4, c = l & 15 holds A[c][4h..4h+3],
+// B[4h..4h+3][c] and accumulator rows C[4h+i][c], i < 4.
+#include "lenet_fused.h"
+
+// Optional phase timestamps (-DMLP_STAMPS diagnostics build): workgroup (0, 0) of the last step,
+// wall_clock64 ticks (100 MHz), read with lenet_debug_stamps.
+#ifdef MLP_STAMPS
+__device__ unsigned long long g_ln_stamps[24];
+#define LN_STAMP(i)                                                                         \
+  do {                                                                                      \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_ln_stamps[i] = wall_clock64(); \
+  } while (0)
+extern "C" int lenet_debug_stamps(void* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ln_stamps), sizeof(g_ln_stamps)) == hipSuccess ? 0 : 1;
+}
+#else
+#define LN_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+namespace {
+
+constexpr int NT = 512;  // 8 waves
+typedef short ln_s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(ln_s16x4, a), __builtin_bit_cast(ln_s16x4, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x4 zero_b4() { return bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f}; }
+// Weight loads with an out-of-layer guard: the load itself is unconditional (clamped to a valid
+// address) and the value is selected afterwards, so a run of them stays in flight together instead
+// of being serialised behind per-load branches.
+__device__ __forceinline__ bf16 ldsel(const bf16* base, int64_t i, bool ok) {
+  const bf16 v = base[ok ? i : 0];
+  return ok ? v : (bf16)0.f;
+}
+__device__ __forceinline__ bf16x4 ldsel4(const bf16* base, int64_t i, bool ok) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(base + (ok ? i : 0));
+  return ok ? v : zero_b4();
+}
+
+// network constants (checked on the host by lenet_fused_supported)
+constexpr int IH = 32, Z1 = 28, P1H = 14, Z2 = 10, P2H = 5;
+constexpr int NP1 = P1H * P1H;       // 196 pooled positions after conv1
+constexpr int NP2 = P2H * P2H;       // 25 after conv2
+constexpr int F0 = NP2 * 16;         // 400 fc1 inputs, engine order (y, x, c)
+constexpr int F1 = 120, F2 = 84, F3 = 10;
+constexpr int LD3 = 128, LD4 = 96;  // row strides of z3 / z4 (K-padded)
+constexpr int LW1 = F0;              // LDS row stride of the fc1 weights: the LDS-DMA image is lane-linear
+constexpr int W1_KB = (F1 * F0 * 2 + 1023) / 1024;  // 1-KB LDS-DMA pieces of the fc1 weight matrix (94)
+constexpr int W1_PER_WAVE = (W1_KB + 7) / 8;
+constexpr int SXR = IH * 4 + 4;       // LDS row stride of the input image (bf16): rows 264 B apart, not 256
+constexpr int ZH = Z2 + 8;             // dZ2 with a 4-pixel zero halo: the conv2 dgrad gathers need no bounds checks
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+// per-workgroup conv gradient record (fp32), reduced over the peer's workgroups by k_lenet_fc_grad:
+// dW1 in its Wf layout [8][25][8] | dW2 [16][25][8] | db1 [16] | db2 [16]
+constexpr int PR_W1 = 0, PR_W2 = 1600, PR_B1 = 4800, PR_B2 = 4816, PR_N = 4832;
+// per-peer fc activation block [B][864] (bf16): p2 | z3 | z4 | dz3 | dz4 | dlogits
+constexpr int A_P2 = 0, A_Z3 = 400, A_Z4 = 528, A_DZ3 = 624, A_DZ4 = 752, A_DL = 848, A_W = 864;
+
+template <int IPW>
+struct Lds {
+  static constexpr int KP2 = (IPW * 100 + 15) / 16 * 16;  // conv2-wgrad K (pixels) padded
+  static constexpr int x = 0;                                        // bf16 [IPW][32][SXR] (pixel = 4 channels)
+  static constexpr int p1 = x + IPW * IH * SXR * 2;                  // bf16 [IPW][196][8]
+  static constexpr int a1 = p1 + IPW * NP1 * 8 * 2;                  // u8   [IPW][196][8] (argmax, 4 = none)
+  static constexpr int dp1 = a1 + IPW * NP1 * 8;                     // bf16 [IPW][196][8]
+  static constexpr int p2 = dp1 + IPW * NP1 * 8 * 2;                 // bf16 [IPW][400]
+  static constexpr int a2 = p2 + IPW * F0 * 2;                       // u8   [IPW][400]
+  static constexpr int z3 = a2 + IPW * F0;                           // bf16 [IPW][128]
+  static constexpr int z4 = z3 + IPW * LD3 * 2;                      // bf16 [IPW][96]
+  static constexpr int dz3 = z4 + IPW * LD4 * 2;                     // bf16 [IPW][128]
+  static constexpr int dz4 = dz3 + IPW * LD3 * 2;                    // bf16 [IPW][96]
+  static constexpr int dl = dz4 + IPW * LD4 * 2;                     // bf16 [IPW][16]
+  static constexpr int lg = dl + IPW * 16 * 2;                       // f32  [IPW][16]
+  static constexpr int dp2 = lg + IPW * 16 * 4;                      // f32  [IPW][400]
+  static constexpr int dz2c = dp2 + IPW * F0 * 4;                    // bf16 [16][KP2] channel-major dZ2
+  static constexpr int tb1 = dz2c + 16 * KP2 * 2;                    // int [IPW*196]: X offset of each pooled-1 window
+  static constexpr int tb2 = tb1 + IPW * NP1 * 4;                    // int [KP2]: P1 offset of each conv2 pixel (-1 pad)
+  static constexpr int w1 = tb2 + KP2 * 4;                           // bf16 [120][400]: fc1 weights (LDS-DMA from the shadow);
+                                                                     // after fc1 dgrad: dZ2 halo image + dense dZ1
+  static constexpr int dz2h = w1;                                    // bf16 [IPW][18][18][16]
+  static constexpr int dz1 = dz2h + IPW * ZH * ZH * 16 * 2;          // bf16 [IPW*196][8][4]: dZ1 per pooled window
+  static constexpr int misc = w1 + W1_PER_WAVE * 8 * 1024;           // int lab[8] | idx[8] | f32 db1[16] | f32 db2[16]
+  static constexpr int total = misc + 16 * 4 + 32 * 4;
+};
+
+template <int IPW>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lenet_step(LenetArgs a) {
+  using L = Lds<IPW>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* sX = reinterpret_cast<bf16*>(smem + L::x);
+  bf16* sP1 = reinterpret_cast<bf16*>(smem + L::p1);
+  uint8_t* sA1 = reinterpret_cast<uint8_t*>(smem + L::a1);
+  bf16* sDP1 = reinterpret_cast<bf16*>(smem + L::dp1);
+  bf16* sP2 = reinterpret_cast<bf16*>(smem + L::p2);
+  uint8_t* sA2 = reinterpret_cast<uint8_t*>(smem + L::a2);
+  bf16* sZ3 = reinterpret_cast<bf16*>(smem + L::z3);
+  bf16* sZ4 = reinterpret_cast<bf16*>(smem + L::z4);
+  bf16* sDZ3 = reinterpret_cast<bf16*>(smem + L::dz3);
+  bf16* sDZ4 = reinterpret_cast<bf16*>(smem + L::dz4);
+  bf16* sDL = reinterpret_cast<bf16*>(smem + L::dl);
+  float* sLG = reinterpret_cast<float*>(smem + L::lg);
+  float* sDP2 = reinterpret_cast<float*>(smem + L::dp2);
+  bf16* sDZ2c = reinterpret_cast<bf16*>(smem + L::dz2c);
+  int* sLab = reinterpret_cast<int*>(smem + L::misc);
+  int* sTb1 = reinterpret_cast<int*>(smem + L::tb1);
+  int* sTb2 = reinterpret_cast<int*>(smem + L::tb2);
+  bf16* sW1 = reinterpret_cast<bf16*>(smem + L::w1);
+  bf16* sDZ2h = reinterpret_cast<bf16*>(smem + L::dz2h);
+  bf16* sDZ1 = reinterpret_cast<bf16*>(smem + L::dz1);
+  float* sDb1 = reinterpret_cast<float*>(smem + L::misc + 64);
+  float* sDb2 = sDb1 + 16;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int p = blockIdx.y;
+  const int b0 = blockIdx.x * IPW;
+  const int n_all = a.n_samples[p];
+  const int valid = max(0, min(a.B, n_all - a.offset));
+  if (blockIdx.x == 0 && tid == 0) a.nb[p] = valid;
+  if (b0 >= valid && !a.train) return;  // evaluation: nothing to count here (training still zero-fills act rows)
+  LN_STAMP(0);
+
+  const bf16* shw = a.shadow + (int64_t)p * a.shadow_ps;
+  const float* prm = a.params + (int64_t)p * a.params_ps;
+
+  // the conv forward B fragments are requested first so their latency overlaps the input gather
+  bf16x4 wf1[7], wf2[13];
+#pragma unroll
+  for (int kc = 0; kc < 7; ++kc) {
+    const int tap = 4 * kc + h;
+    wf1[kc] = ldsel4(shw, a.w_c1 + (c * 25 + tap) * 8, c < 6 && tap < 25);  // shadow channels 3..7 are zero
+  }
+#pragma unroll
+  for (int kc = 0; kc < 13; ++kc) {
+    const int tap = 2 * kc + (h >> 1), ci0 = 4 * (h & 1);
+    wf2[kc] = ldsel4(shw, a.w_c2 + (c * 25 + tap) * 8 + ci0, tap < 25);  // shadow channels 6, 7 are zero
+  }
+  const float bias1 = c < 6 ? prm[a.b_c1 + c] : 0.f;
+  const float bias2 = prm[a.b_c2 + c];
+
+  // ---------------- input gather: sample index + label per image, then uint8 HWC -> bf16
+  //                  [img][y][x][4] * scale (all loads of a thread in flight together)
+  int* sIdx = sLab + 8;
+  if (tid < IPW) {
+    const int b = b0 + tid;
+    int idx = -1, lab = -1;
+    if (b < valid) {
+      idx = a.perm ? a.perm[(int64_t)p * a.perm_ps + a.offset + b] : a.offset + b;
+      lab = (int)a.ys[p][idx];
+    }
+    sLab[tid] = lab;
+    sIdx[tid] = idx;
+  }
+  if (tid < 32) sDb1[tid] = 0.f;  // db1 and db2
+  for (int e = tid; e < 16 * L::KP2; e += NT) sDZ2c[e] = (bf16)0.f;
+  for (int e = tid; e < IPW * NP1; e += NT) {  // conv1 wgrad: top-left X element of pooled window e
+    const int li = e / NP1, pp = e - li * NP1;
+    sTb1[e] = (li * IH + 2 * (pp / P1H)) * SXR + 2 * (pp % P1H) * 4;
+  }
+  for (int e = tid; e < L::KP2; e += NT) {  // conv2 wgrad: P1 element of conv2 output pixel e
+    const int li = e / 100, pix = e - li * 100;
+    sTb2[e] = e < IPW * 100 ? (li * NP1 + (pix / Z2) * P1H + pix % Z2) * 8 : 0;  // pad: A is zero there
+  }
+  __syncthreads();
+  LN_STAMP(1);
+  {
+    constexpr int PIX = IPW * IH * IH / NT;
+    uint8_t px[PIX][3];
+#pragma unroll
+    for (int it = 0; it < PIX; ++it) {
+      const int e = tid + it * NT;
+      const int li = e / (IH * IH), hw = e - li * (IH * IH);
+      const int idx = sIdx[li];
+      const uint8_t* src = a.xs[p] + ((int64_t)(idx >= 0 ? idx : 0) * IH * IH + hw) * 3;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) px[it][ch] = idx >= 0 ? src[ch] : (uint8_t)0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < PIX; ++it) {
+      const int e = tid + it * NT, row = e / IH;  // row = image * 32 + y
+      *reinterpret_cast<bf16x4*>(sX + row * SXR + (e - row * IH) * 4) =
+          bf16x4{(bf16)(a.scale * (float)px[it][0]), (bf16)(a.scale * (float)px[it][1]), (bf16)(a.scale * (float)px[it][2]), (bf16)0.f};
+    }
+  }
+  __syncthreads();
+  LN_STAMP(2);
+
+  // fc1 weights (96 KB, read by fc1 forward and dgrad) -> LDS by LDS-DMA, in flight during conv1
+  // (every earlier global load has landed, so nothing below waits on the DMA before conv1's barrier)
+  {
+    // consume the landed conv operands here: a later first use would otherwise wait vmcnt(0) and
+    // drain the DMA
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const uint2 u = __builtin_bit_cast(uint2, wf1[k]);
+      asm volatile("" ::"v"(u.x), "v"(u.y));
+    }
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const uint2 u = __builtin_bit_cast(uint2, wf2[k]);
+      asm volatile("" ::"v"(u.x), "v"(u.y));
+    }
+    asm volatile("" ::"v"(bias1), "v"(bias2));
+    const char* src = reinterpret_cast<const char*>(shw + a.w_f1);
+#pragma unroll
+    for (int q = 0; q < W1_PER_WAVE; ++q) {
+      const int piece = q * 8 + wave;
+      int off = piece * 1024 + lane * 16;
+      if (off >= F1 * F0 * 2) off = 0;  // tail lanes re-read piece 0; their bytes land past the matrix
+      __builtin_amdgcn_global_load_lds((glb_void*)(src + off), (lds_void*)(smem + L::w1 + piece * 1024), 16, 0, 0);
+    }
+  }
+
+  // ---------------- conv1 (3->6, 5x5) + bias + ReLU + 2x2 max-pool
+  // K = (tap, ci4): k = 16kc + 4h + j <-> tap 4kc + h, channel j; M-tile = 4 pooled positions x 2x2
+  {
+    const float bias = bias1;
+    for (int t = wave; t < IPW * (NP1 / 4); t += 8) {
+      const int li = t / (NP1 / 4), tt = t - li * (NP1 / 4);
+      const int pp = 4 * tt + (c >> 2), sub = c & 3;
+      const int oy = 2 * (pp / P1H) + (sub >> 1), ox = 2 * (pp % P1H) + (sub & 1);
+      const bf16* xb = sX + (li * IH + oy) * SXR + ox * 4;
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < 7; ++kc) {
+        const int tap = 4 * kc + h;
+        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+        const bf16x4 av = tap < 25 ? *reinterpret_cast<const bf16x4*>(xb + ky * SXR + kx * 4) : zero_b4();
+        acc = mfma16(av, wf1[kc], acc);
+      }
+      // lane (h, c): pooled position 4tt + h, its 2x2 window in acc[0..3], channel c
+      float m = acc[0];
+      int am = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (acc[i] > m) { m = acc[i]; am = i; }
+      m += bias;
+      if (c < 8) {
+        const int o = (li * NP1 + 4 * tt + h) * 8 + c;
+        sP1[o] = (bf16)(c < 6 ? fmaxf(m, 0.f) : 0.f);
+        sA1[o] = (uint8_t)((c < 6 && m > 0.f) ? am : 4);
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(3);
+
+  // ---------------- conv2 (6->16, 5x5) + bias + ReLU + 2x2 max-pool; K = (tap, ci8): 13 chunks
+  {
+    const float bias = bias2;
+    for (int t = wave; t < IPW * 7; t += 8) {
+      const int li = t / 7, tt = t - li * 7;
+      const int pp = 4 * tt + (c >> 2), sub = c & 3;
+      const int oy = 2 * (pp / P2H) + (sub >> 1), ox = 2 * (pp % P2H) + (sub & 1);
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < 13; ++kc) {
+        const int tap = 2 * kc + (h >> 1), ci0 = 4 * (h & 1);
+        const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+        const bf16x4 av = (pp < NP2 && tap < 25) ? *reinterpret_cast<const bf16x4*>(sP1 + (li * NP1 + (oy + ky) * P1H + ox + kx) * 8 + ci0) : zero_b4();
+        acc = mfma16(av, wf2[kc], acc);
+      }
+      const int ppo = 4 * tt + h;
+      if (ppo < NP2) {
+        float m = acc[0];
+        int am = 0;
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+          if (acc[i] > m) { m = acc[i]; am = i; }
+        m += bias;
+        sP2[li * F0 + ppo * 16 + c] = (bf16)fmaxf(m, 0.f);
+        sA2[li * F0 + ppo * 16 + c] = (uint8_t)(m > 0.f ? am : 4);
+      }
+    }
+  }
+  __syncthreads();
+  LN_STAMP(4);
+
+  // ---------------- fc1 400 -> 120 (+ReLU): wave = N tile, A rows = images
+  // fc2 / fc3 operands from global (forward B fragments and the dgrad ones) are requested now and
+  // consumed after fc1
+  bf16x4 f2w[LD3 / 16], f3w[LD4 / 16];
+  bf16 f3d[4], f2d[LD4 / 16][4];
+  {
+    const int n = 16 * wave + c;
+#pragma unroll
+    for (int kc = 0; kc < LD3 / 16; ++kc) {
+      const int k0 = 16 * kc + 4 * h;
+      f2w[kc] = ldsel4(shw, a.w_f2 + (int64_t)n * F1 + k0, wave < LD4 / 16 && n < F2 && k0 < F1);
+    }
+#pragma unroll
+    for (int kc = 0; kc < LD4 / 16; ++kc) {
+      const int k0 = 16 * kc + 4 * h;
+      f3w[kc] = ldsel4(shw, a.w_f3 + c * 88 + k0, wave == 0 && c < F3 && k0 < F2);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f3d[j] = ldsel(shw, a.w_f3 + (4 * h + j) * 88 + n, wave < LD4 / 16 && 4 * h + j < F3 && n < F2);
+#pragma unroll
+    for (int kc = 0; kc < LD4 / 16; ++kc)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f2d[kc][j] = ldsel(shw, a.w_f2 + (int64_t)(16 * kc + 4 * h + j) * F1 + n, 16 * kc + 4 * h + j < F2 && n < F1);
+  }
+  {
+    const int n = 16 * wave + c;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < F0 / 16; ++kc) {
+      const int k0 = 16 * kc + 4 * h;
+      const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sP2 + c * F0 + k0) : zero_b4();
+      const bf16x4 bv = n < F1 ? *reinterpret_cast<const bf16x4*>(sW1 + n * LW1 + k0) : zero_b4();
+      acc = mfma16(av, bv, acc);
+    }
+    const float bias = n < F1 ? prm[a.b_f1 + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * h + i < IPW) sZ3[(4 * h + i) * LD3 + n] = (bf16)(n < F1 ? fmaxf(acc[i] + bias, 0.f) : 0.f);
+  }
+  __syncthreads();
+  LN_STAMP(5);
+  // ---------------- fc2 120 -> 84 (+ReLU)
+  if (wave < LD4 / 16) {
+    const int n = 16 * wave + c;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < LD3 / 16; ++kc) {
+      const int k0 = 16 * kc + 4 * h;
+      const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sZ3 + c * LD3 + k0) : zero_b4();
+      acc = mfma16(av, f2w[kc], acc);
+    }
+    const float bias = n < F2 ? prm[a.b_f2 + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * h + i < IPW) sZ4[(4 * h + i) * LD4 + n] = (bf16)(n < F2 ? fmaxf(acc[i] + bias, 0.f) : 0.f);
+  }
+  __syncthreads();
+  LN_STAMP(6);
+  // ---------------- fc3 84 -> 10 (logits)
+  if (wave == 0) {
+    const int n = c;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < LD4 / 16; ++kc) {
+      const int k0 = 16 * kc + 4 * h;
+      const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sZ4 + c * LD4 + k0) : zero_b4();
+      acc = mfma16(av, f3w[kc], acc);
+    }
+    const float bias = n < F3 ? prm[a.b_f3 + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * h + i < IPW) sLG[(4 * h + i) * 16 + n] = acc[i] + bias;
+  }
+  __syncthreads();
+  LN_STAMP(7);
+  // ---------------- log-softmax + NLL: loss / correct sums, confusion, dlogits = (p - onehot) / n
+  if (tid < IPW) {
+    const int lab = sLab[tid];
+    const float* z = sLG + tid * 16;
+    float mx = z[0];
+    int am = 0;
+    for (int k = 1; k < F3; ++k)
+      if (z[k] > mx) { mx = z[k]; am = k; }
+    float se = 0.f;
+    for (int k = 0; k < F3; ++k) se += __expf(z[k] - mx);
+    const float lse = mx + __logf(se);
+    if (lab >= 0) {
+      atomicAdd(a.stats + p * 4 + 0, lse - z[lab]);
+      atomicAdd(a.stats + p * 4 + 1, am == lab ? 1.f : 0.f);
+      if (a.confusion) atomicAdd(a.confusion + (p * 16 + lab) * 16 + am, 1);
+    }
+    const float invn = valid > 0 ? 1.f / (float)valid : 0.f;
+    for (int k = 0; k < 16; ++k) {
+      const float d = (lab >= 0 && k < F3) ? (__expf(z[k] - lse) - (k == lab ? 1.f : 0.f)) * invn : 0.f;
+      sDL[tid * 16 + k] = (bf16)d;
+    }
+  }
+  if (!a.train) return;
+  __syncthreads();
+  LN_STAMP(8);
+
+  // ---------------- fc3 dgrad: dz4 = dlogits . W3 (x ReLU mask)
+  if (wave < LD4 / 16) {
+    const int k = 16 * wave + c;
+    const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sDL + c * 16 + 4 * h) : zero_b4();
+    const bf16x4 bv = bf16x4{f3d[0], f3d[1], f3d[2], f3d[3]};
+    const f32x4 acc = mfma16(av, bv, zero4());
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int img = 4 * h + i;
+      if (img < IPW) sDZ4[img * LD4 + k] = (bf16)((float)sZ4[img * LD4 + k] > 0.f ? acc[i] : 0.f);
+    }
+  }
+  __syncthreads();
+  LN_STAMP(9);
+  // ---------------- fc2 dgrad: dz3 = dz4 . W2 (x ReLU mask)
+  {
+    const int k = 16 * wave + c;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < LD4 / 16; ++kc) {
+      const int n0 = 16 * kc + 4 * h;
+      const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sDZ4 + c * LD4 + n0) : zero_b4();
+      const bf16x4 bv = bf16x4{f2d[kc][0], f2d[kc][1], f2d[kc][2], f2d[kc][3]};
+      acc = mfma16(av, bv, acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int img = 4 * h + i;
+      if (img < IPW) sDZ3[img * LD3 + k] = (bf16)((float)sZ3[img * LD3 + k] > 0.f ? acc[i] : 0.f);
+    }
+  }
+  __syncthreads();
+  LN_STAMP(10);
+  // ---------------- fc1 dgrad: dp2 = dz3 . W1 (25 N tiles)
+  for (int nt = wave; nt < F0 / 16; nt += 8) {
+    const int k = 16 * nt + c;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < LD3 / 16; ++kc) {
+      const int n0 = 16 * kc + 4 * h;
+      const bf16x4 av = c < IPW ? *reinterpret_cast<const bf16x4*>(sDZ3 + c * LD3 + n0) : zero_b4();
+      bf16x4 bv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = n0 + j < F1 ? sW1[(n0 + j) * LW1 + k] : (bf16)0.f;
+      acc = mfma16(av, bv, acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * h + i < IPW) sDP2[(4 * h + i) * F0 + k] = acc[i];
+  }
+  __syncthreads();
+  LN_STAMP(11);
+
+  // ---------------- fc activations -> global (fc weight-gradient kernel); pool-2 backward
+  {
+    bf16* act = a.act + (int64_t)p * a.act_ps + (int64_t)b0 * A_W;
+    for (int e = tid; e < IPW * A_W; e += NT) {
+      const int li = e / A_W, col = e - li * A_W;
+      bf16 v;
+      if (col < A_Z3) v = sP2[li * F0 + col];
+      else if (col < A_Z4) v = sZ3[li * LD3 + col - A_Z3];
+      else if (col < A_DZ3) v = sZ4[li * LD4 + col - A_Z4];
+      else if (col < A_DZ4) v = sDZ3[li * LD3 + col - A_DZ3];
+      else if (col < A_DL) v = sDZ4[li * LD4 + col - A_DZ4];
+      else v = sDL[li * 16 + col - A_DL];
+      act[e] = v;
+    }
+  }
+  // conv2 dgrad B fragments W2[co = 4h+j][tap][ci = c]: requested now, used after the wgrad
+  bf16x4 wb[25];
+#pragma unroll
+  for (int kc = 0; kc < 25; ++kc)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wb[kc][j] = ldsel(shw, a.w_c2 + ((4 * h + j) * 25 + kc) * 8 + c, c < 6);
+  {  // conv2 bias gradient: pooled gradients that pass the argmax (each thread sees one channel)
+    float db = 0.f;
+    for (int e = tid; e < IPW * F0; e += NT) db += sA2[e] < 4 ? sDP2[e] : 0.f;
+    db += __shfl_xor(db, 16);
+    db += __shfl_xor(db, 32);
+    if (lane < 16) atomicAdd(&sDb2[lane], db);
+  }
+  // pool-2 backward, one pixel (16 channels) per iteration: dZ2 as a zero-haloed pixel-major image
+  // (conv2 dgrad A operand) and channel-major (conv2 wgrad A operand); the fc1 weights in the
+  // aliased region are dead after fc1 dgrad
+  for (int q = tid; q < IPW * ZH * ZH; q += NT) {
+    const int li = q / (ZH * ZH), yx = q - li * (ZH * ZH);
+    const int oy = yx / ZH - 4, ox = yx - ZH * (yx / ZH) - 4;
+    bf16 v[16];
+#pragma unroll
+    for (int co = 0; co < 16; ++co) v[co] = (bf16)0.f;
+    if (oy >= 0 && oy < Z2 && ox >= 0 && ox < Z2) {
+      const int r0 = li * F0 + ((oy >> 1) * P2H + (ox >> 1)) * 16;
+      const int sub = (oy & 1) * 2 + (ox & 1);
+#pragma unroll
+      for (int co = 0; co < 16; ++co) {
+        v[co] = (bf16)(sA2[r0 + co] == sub ? sDP2[r0 + co] : 0.f);
+        sDZ2c[co * L::KP2 + li * 100 + oy * Z2 + ox] = v[co];
+      }
+    }
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int co = 0; co < 8; ++co) {
+      lo[co] = v[co];
+      hi[co] = v[8 + co];
+    }
+    *reinterpret_cast<bf16x8*>(sDZ2h + q * 16) = lo;
+    *reinterpret_cast<bf16x8*>(sDZ2h + q * 16 + 8) = hi;
+  }
+  __syncthreads();
+  LN_STAMP(12);
+
+  float* prec = a.part + (int64_t)p * a.part_ps + (int64_t)blockIdx.x * PR_N;  // this workgroup's record
+  // ---------------- conv2 weight gradient: dW2[co][tap][ci] = sum_m dZ2[m][co] P1[m + tap][ci]
+  //                  M = co (16), N = (tap, ci8) 200 -> 13 tiles, K = pixels of the IPW images.
+  //                  Lanes of invalid taps (or K padding, where A is zero) read any P1 element: their
+  //                  products are never stored.
+  for (int nt = wave; nt < 13; nt += 8) {
+    const int n = 16 * nt + c;
+    const int tap = n >> 3, ci = n & 7;
+    const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+    const int toff = tap < 25 ? (ky * P1H + kx) * 8 + ci : 0;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kc = 0; kc < L::KP2 / 16; ++kc) {
+      const int m0 = 16 * kc + 4 * h;
+      const bf16x4 av = *reinterpret_cast<const bf16x4*>(sDZ2c + c * L::KP2 + m0);
+      const int4 tb = *reinterpret_cast<const int4*>(sTb2 + m0);
+      const bf16x4 bv = bf16x4{sP1[tb.x + toff], sP1[tb.y + toff], sP1[tb.z + toff], sP1[tb.w + toff]};
+      acc = mfma16(av, bv, acc);
+    }
+    if (tap < 25 && ci < 6) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) prec[PR_W2 + ((4 * h + i) * 25 + tap) * 8 + ci] = acc[i];
+    }
+  }
+  LN_STAMP(15);
+  // ---------------- conv2 dgrad: dP1[m][ci] = sum_(tap, co) dZ2[m - tap][co] W2[co][tap][ci]
+  //                  M = pooled-1 pixels of the IPW images, N = ci (16), K = (tap, co16): 25 chunks
+  {
+    LN_STAMP(16);
+    constexpr int MT = (IPW * NP1 + 15) / 16;
+    for (int mt = wave; mt < MT; mt += 8) {
+      const int m = min(16 * mt + c, IPW * NP1 - 1);  // padding rows recompute the last pixel (not stored)
+      const int li = m / NP1, pix = m - li * NP1;
+      const int y = pix / P1H, x = pix - P1H * (pix / P1H);
+      const bf16* base = sDZ2h + ((li * ZH + y + 4) * ZH + x + 4) * 16 + 4 * h;
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < 25; ++kc) {
+        const int ky = kc / 5, kx = kc - 5 * (kc / 5);
+        acc = mfma16(*reinterpret_cast<const bf16x4*>(base - (ky * ZH + kx) * 16), wb[kc], acc);
+      }
+      if (c < 8) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mo = 16 * mt + 4 * h + i;
+          if (mo < IPW * NP1) sDP1[mo * 8 + c] = (bf16)acc[i];
+        }
+      }
+    }
+  }
+  LN_STAMP(17);
+  __syncthreads();
+  LN_STAMP(13);
+  // pool-1 backward (ReLU folded into the argmax): dense dZ1 per pooled window [ppg][co][sub], and the
+  // conv1 bias gradient
+  {
+    float db = 0.f;  // this thread's channel is tid & 7 throughout
+    for (int e = tid; e < IPW * NP1 * 8; e += NT) {
+      const int am = sA1[e];
+      const bf16 g = sDP1[e];
+      const bf16 z = (bf16)0.f;
+      *reinterpret_cast<bf16x4*>(sDZ1 + e * 4) = bf16x4{am == 0 ? g : z, am == 1 ? g : z, am == 2 ? g : z, am == 3 ? g : z};
+      db += am < 4 ? (float)g : 0.f;
+    }
+    db += __shfl_xor(db, 8);
+    db += __shfl_xor(db, 16);
+    db += __shfl_xor(db, 32);
+    if (lane < 6) atomicAdd(&sDb1[lane], db);
+  }
+  __syncthreads();
+  // ---------------- conv1 weight gradient: dW1[co][tap][ci] = sum_m dZ1[m][co] X[m + tap][ci];
+  //                  K = IPW x 196 windows x 4 pixels. Invalid (tap, ci) lanes read channel 3 (zero).
+  if (wave < 7) {
+    const int n = 16 * wave + c;
+    const int tap = n >> 2, ci = n & 3;
+    const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+    const int toff = (tap < 25 && ci < 3) ? ky * SXR + kx * 4 + ci : 3;
+    const int cc = c < 8 ? c : 7;
+    f32x4 acc = zero4();
+#pragma unroll 4
+    for (int kc = 0; kc < IPW * NP1 / 4; ++kc) {
+      const int ppg = 4 * kc + h;  // pooled window (image-major) of this lane's 4 K rows
+      const bf16* xb = sX + sTb1[ppg] + toff;
+      const bf16x4 av = *reinterpret_cast<const bf16x4*>(sDZ1 + (ppg * 8 + cc) * 4);
+      const bf16x4 bv = bf16x4{xb[0], xb[4], xb[SXR], xb[SXR + 4]};
+      acc = mfma16(av, bv, acc);
+    }
+    if (tap < 25 && ci < 3) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * h + i < 6) prec[PR_W1 + ((4 * h + i) * 25 + tap) * 8 + ci] = acc[i];
+    }
+  }
+  __syncthreads();
+  LN_STAMP(14);
+  if (tid < 6) prec[PR_B1 + tid] = sDb1[tid];
+  if (tid >= 32 && tid < 48) prec[PR_B2 + tid - 32] = sDb2[tid - 32];
+}
+
+// fc weight and bias gradients over the whole batch (K = B): one 16x16 output tile per wave.
+// Weight tiles: fc1 8 x 25, fc2 6 x 8, fc3 1 x 6; bias tiles (B operand = ones): fc1 8, fc2 6, fc3 1.
+constexpr int FC_WTILES = 8 * 25 + 6 * 8 + 6;
+constexpr int FC_TILES = FC_WTILES + 8 + 6 + 1;
+constexpr int FC_BLOCKS = (FC_TILES + 3) / 4;
+constexpr int RED_BLOCKS = (PR_N + 255) / 256;
+template <int IPW>
+__global__ __launch_bounds__(256) void k_lenet_fc_grad(LenetArgs a) {
+  const int p = blockIdx.y;
+  if (blockIdx.x >= FC_BLOCKS) {  // conv weight / bias gradients: sum of the step kernel's records
+    const int e = (blockIdx.x - FC_BLOCKS) * 256 + threadIdx.x;
+    if (e >= PR_N) return;
+    int64_t dst = -1;
+    bool bias = false;
+    if (e < PR_W2) {
+      const int co = e / 200, tap = (e % 200) >> 3, ci = e & 7;
+      if (co < 6 && tap < 25 && ci < 3) dst = a.w_c1 + e;
+    } else if (e < PR_B1) {
+      const int r = e - PR_W2, tap = (r % 200) >> 3, ci = r & 7;
+      if (tap < 25 && ci < 6) dst = a.w_c2 + r;
+    } else if (e < PR_B2) {
+      if (e - PR_B1 < 6) { dst = a.b_c1 + e - PR_B1; bias = true; }
+    } else {
+      dst = a.b_c2 + e - PR_B2;
+      bias = true;
+    }
+    if (dst < 0) return;
+    const float* rec = a.part + (int64_t)p * a.part_ps + e;
+    const int G = a.B / IPW;
+    float s = 0.f;
+#pragma unroll 8
+    for (int w = 0; w < G; ++w) s += rec[(int64_t)w * PR_N];
+    (bias ? a.g + (int64_t)p * a.g_ps : a.gf + (int64_t)p * a.gf_ps)[dst] = s;
+    return;
+  }
+  const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= FC_TILES) return;
+  const bf16* act = a.act + (int64_t)p * a.act_ps;
+  const int B = a.B;
+  int dcol, xcol, nout, nin, ld, nt, kt;
+  int64_t woff;
+  bool bias = false;
+  if (t < 200) {
+    nt = t / 25; kt = t % 25; dcol = A_DZ3; xcol = A_P2; nout = F1; nin = F0; ld = F0; woff = a.w_f1;
+  } else if (t < 248) {
+    nt = (t - 200) / 8; kt = (t - 200) % 8; dcol = A_DZ4; xcol = A_Z3; nout = F2; nin = F1; ld = F1; woff = a.w_f2;
+  } else if (t < FC_WTILES) {
+    nt = 0; kt = t - 248; dcol = A_DL; xcol = A_Z4; nout = F3; nin = F2; ld = 88; woff = a.w_f3;
+  } else {
+    const int u = t - FC_WTILES;
+    bias = true; kt = 0; xcol = 0; ld = 0;
+    if (u < 8) { nt = u; dcol = A_DZ3; nout = F1; nin = 1; woff = a.b_f1; }
+    else if (u < 14) { nt = u - 8; dcol = A_DZ4; nout = F2; nin = 1; woff = a.b_f2; }
+    else { nt = 0; dcol = A_DL; nout = F3; nin = 1; woff = a.b_f3; }
+  }
+  const int n = 16 * nt + c, k = 16 * kt + c;
+  f32x4 acc = zero4();
+  for (int b64 = 0; b64 < B; b64 += 64) {  // 4 K chunks per trip: their 32 loads are in flight together
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bf16x4 av, bv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b = b64 + 16 * q + 4 * h + j;
+        av[j] = (b < B && n < nout) ? act[(int64_t)b * A_W + dcol + n] : (bf16)0.f;
+        bv[j] = b < B ? (bias ? (bf16)1.f : (k < nin ? act[(int64_t)b * A_W + xcol + k] : (bf16)0.f)) : (bf16)0.f;
+      }
+      acc = mfma16(av, bv, acc);
+    }
+  }
+  // C[row 4h+i = output unit][col c = input (bias tiles: every column holds the sum)]
+  float* dst = bias ? a.g + (int64_t)p * a.g_ps + woff : a.gf + (int64_t)p * a.gf_ps + woff;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int no = 16 * nt + 4 * h + i;
+    if (no < nout && k < nin) dst[bias ? no : (int64_t)no * ld + k] = acc[i];
+  }
+}
+
+template <int IPW>
+hipError_t launch_step(const LenetArgs& a, int peers, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lenet_step<IPW>), hipFuncAttributeMaxDynamicSharedMemorySize, Lds<IPW>::total);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_lenet_step<IPW>, dim3(a.B / IPW, peers), dim3(NT), Lds<IPW>::total, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !a.train) return e;
+  hipLaunchKernelGGL(k_lenet_fc_grad<IPW>, dim3(FC_BLOCKS + RED_BLOCKS, peers), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int lenet_args_size() { return (int)sizeof(LenetArgs); }
+
+int lenet_fused_supported(int in_c, int in_h, int c1, int c2, int f1, int f2, int f3, int B) {
+  return in_c == 3 && in_h == IH && c1 == 6 && c2 == 16 && f1 == F1 && f2 == F2 && f3 == F3 && B > 0 && B % 2 == 0 && B <= 4096;
+}
+
+int lenet_fused_step(const LenetArgs* a, int peers, int ipw, void* stream) {
+  if (a == nullptr || peers <= 0 || a->B <= 0 || a->B % ipw != 0) return 1;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (ipw == 2) e = launch_step<2>(*a, peers, s);
+  else return 1;
+  return e == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"

@@ -26,6 +26,7 @@ BatchNorm (biased batch variance for normalisation, unbiased running variance, m
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Dict, List, Optional, Set, Tuple
 
@@ -60,6 +61,23 @@ class WgradArgs(ctypes.Structure):
     ]
 
 
+class LenetArgs(ctypes.Structure):
+    """Mirror of ``LenetArgs`` (csrc/kernels/lenet_fused.h)."""
+
+    _fields_ = [
+        ("xs", c_void_p), ("ys", c_void_p), ("n_samples", c_void_p), ("perm", c_void_p), ("perm_ps", c_int64), ("offset", c_int), ("B", c_int),
+        ("scale", c_float), ("shadow", c_void_p), ("shadow_ps", c_int64), ("w_c1", c_int64), ("w_c2", c_int64), ("w_f1", c_int64), ("w_f2", c_int64),
+        ("w_f3", c_int64), ("params", c_void_p), ("params_ps", c_int64), ("b_c1", c_int64), ("b_c2", c_int64), ("b_f1", c_int64), ("b_f2", c_int64),
+        ("b_f3", c_int64), ("gf", c_void_p), ("gf_ps", c_int64), ("g", c_void_p), ("g_ps", c_int64), ("act", c_void_p), ("act_ps", c_int64), ("part", c_void_p), ("part_ps", c_int64),
+        ("stats", c_void_p), ("confusion", c_void_p), ("nb", c_void_p), ("train", c_int),
+    ]
+
+
+LENET_ACT_W = 864  # per-image fc activation block of the fused LeNet step (lenet_fused.hip A_W)
+LENET_IPW = 2  # images per workgroup of the fused LeNet step
+LENET_PART_N = 4832  # floats per workgroup conv-gradient record (lenet_fused.hip PR_N)
+
+
 class Segment(ctypes.Structure):
     _fields_ = [
         ("off", c_int64), ("n", c_int), ("kind", c_int), ("cout", c_int), ("cin", c_int), ("R", c_int), ("S", c_int),
@@ -86,6 +104,9 @@ _SIGS = {
     "cnn_opt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_float, c_int, c_float,
                              c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     "cnn_segment_size": (c_int, []),
+    "lenet_fused_supported": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "lenet_fused_step": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "lenet_args_size": (c_int, []),
 }
 
 
@@ -97,6 +118,8 @@ def _lib():
             fn.restype, fn.argtypes = res, args
         if lib.cnn_segment_size() != ctypes.sizeof(Segment):
             raise RuntimeError("Segment layout mismatch between Python and the native library")
+        if lib.lenet_args_size() != ctypes.sizeof(LenetArgs):
+            raise RuntimeError("LenetArgs layout mismatch between Python and the native library")
         lib._cnn_sigs = True
     return lib
 
@@ -191,6 +214,7 @@ class CNNGroup:
         self._seen: set = set()
         self._data_version = 0
         self._bound_version = -1
+        self.lenet_fused = False
         self._describe(template)
         self._alloc(capacity)
         self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
@@ -285,6 +309,11 @@ class CNNGroup:
         self.convs = [self.l_c1, self.l_c2, self.l_fc1, self.l_fc2, self.l_fc3]
         self.lenet_h = (h, h1, h2)
         self.n_classes = m.fc3.out_features
+        # whole step in one fused kernel (lenet_fused.hip) when the shapes are the reference LeNet-5's
+        self.lenet_fused = False
+        if Settings.USE_FUSED_KERNELS and os.environ.get("MYFYP_LENET_FUSED", "1") != "0" and self.device.type == "cuda":
+            self.lenet_fused = bool(_lib().lenet_fused_supported(self.in_c, h, m.conv1.out_channels, m.conv2.out_channels, m.fc1.out_features,
+                                                                  m.fc2.out_features, m.fc3.out_features, self.B)) and self.B % LENET_IPW == 0
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self, capacity: int) -> None:
@@ -321,6 +350,8 @@ class CNNGroup:
             if cin_t * c.R * c.S > 4608 or (c.cp_in + 1) * c.R * c.S > 4624:
                 raise ValueError(f"conv layer {c.name} too wide for the optimizer kernel (cin * R * S > 4608)")
             accumulate = int(self._wgrad_split(c)[1] > 1)
+            if getattr(self, "lenet_fused", False) and c.name in ("c1", "c2"):
+                accumulate = 1  # the fused step adds its per-workgroup conv gradients atomically
             work += [(len(segs), co) for co in range(c.cout)]
             segs.append(Segment(self._off(c.weight), c.weight.numel(), 1, c.cout, cin_t, c.R, c.S, c.cp_in, c.cp_out, accumulate, 0, self.shadow_off[c.name], e2t, t2e))
             if c.bias is not None:
@@ -684,6 +715,10 @@ class CNNGroup:
                              self._stream()), "xent")
 
     def _train_step(self, offset: int) -> None:
+        if self.arch != "resnet18" and self.lenet_fused:
+            self._lenet_fused(True, offset)
+            self._optimizer(update=True)
+            return
         x0 = self._prep(True, offset)
         if self.arch == "resnet18":
             logits = self._forward_resnet(x0, True)
@@ -694,6 +729,30 @@ class CNNGroup:
             self._xent(logits, True)
             self._backward_lenet(self.act("dlogits", self.B, self.l_fc3.cp_out))
         self._optimizer(update=True)
+
+    def _lenet_fused(self, train: bool, offset: int) -> None:
+        """One fused LeNet-5 step (train: forward + backward + gradients; eval: forward + loss /
+        confusion) for every peer: ``lenet_fused.hip``."""
+        t, P, B = self.tab, self.capacity, self.B
+        a = LenetArgs()
+        a.xs, a.ys, a.n_samples = _p(t["xs"] if train else t["xts"]), _p(t["ys"] if train else t["yts"]), _p(t["n"] if train else t["nt"])
+        a.perm, a.perm_ps = (_p(self.perm), self.nmax) if train else (None, 0)
+        a.offset, a.B, a.scale = offset, B, self.in_scale
+        a.shadow, a.shadow_ps = self.shadow.data_ptr(), self.shadow.shape[1]
+        so = self.shadow_off
+        a.w_c1, a.w_c2, a.w_f1, a.w_f2, a.w_f3 = so["c1"], so["c2"], so["fc1"], so["fc2"], so["fc3"]
+        a.params, a.params_ps = self.params.data_ptr(), self.params.shape[1]
+        L = (self.l_c1, self.l_c2, self.l_fc1, self.l_fc2, self.l_fc3)
+        a.b_c1, a.b_c2, a.b_f1, a.b_f2, a.b_f3 = (self._off(x.bias) for x in L)
+        a.gf, a.gf_ps = self.gradf.data_ptr(), self.gradf.shape[1]
+        a.g, a.g_ps = self.grad.data_ptr(), self.grad.shape[1]
+        act = self.act("lenet_act", B * LENET_ACT_W, 1)
+        a.act, a.act_ps = act.data_ptr(), act.shape[1]
+        part = self.fbuf("lenet_part", (B // LENET_IPW) * LENET_PART_N)
+        a.part, a.part_ps = part.data_ptr(), part.shape[1]
+        a.stats, a.confusion, a.nb = self.stat.data_ptr(), None if train else self.conf.data_ptr(), self.nb.data_ptr()
+        a.train = int(train)
+        _chk(_lib().lenet_fused_step(ctypes.byref(a), P, LENET_IPW, self._stream()), "lenet_fused_step")
 
     def _optimizer(self, update: bool) -> None:
         """SGD on the torch-order master rows + bf16 Wf shadow rows, one fused launch (update=False:
@@ -809,6 +868,9 @@ class CNNGroup:
 
         def body():
             for t in range(steps):
+                if self.arch != "resnet18" and self.lenet_fused:
+                    self._lenet_fused(False, t * self.B)
+                    continue
                 x0 = self._prep(False, t * self.B)
                 logits = self._forward_resnet(x0, False) if self.arch == "resnet18" else self._forward_lenet(x0, False)
                 self._xent(logits, False)

@@ -173,10 +173,62 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0, noise_floo
     return learners, refs
 
 
-def test_lenet_train_step_matches_torch():
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_lenet_train_step_matches_torch(fused, monkeypatch):
+    """fused = the one-kernel LeNet step (lenet_fused.hip); 0 = the layer-by-layer conv kernels."""
     from myfyp_amd.models import LeNet5
 
-    _run_one_step(lambda i: LeNet5(seed=10 + i), n_peers=2, batch=32, lr=0.05)
+    monkeypatch.setenv("MYFYP_LENET_FUSED", fused)
+    learners, _ = _run_one_step(lambda i: LeNet5(seed=10 + i), n_peers=2, batch=32, lr=0.05, momentum=0.9)
+    assert learners[0]._engine.group.lenet_fused == (fused == "1")
+
+
+def test_lenet_fused_epoch_matches_layerwise_path(monkeypatch):
+    """A whole epoch with a partial last batch and momentum: fused step vs the layer-by-layer path."""
+    import threading
+
+    from myfyp_amd.models import LeNet5
+
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MYFYP_LENET_FUSED", fused)
+        learners, _, _ = _make_learners(lambda i: LeNet5(seed=50 + i), 3, 100, 40, 32, 0.05, momentum=0.9)
+        g = learners[0]._engine.group
+        assert g.lenet_fused == (fused == "1")
+        p0 = [lr_.flat_params().detach().clone() for lr_ in learners]
+        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        loss = g.stat.view(g.capacity, 4)[:3, :2].clone()
+        ev = [lr_.evaluate() for lr_ in learners]
+        runs.append(([lr_.flat_params().detach().clone() - q for lr_, q in zip(learners, p0)], loss, ev))
+    (d_f, l_f, e_f), (d_l, l_l, e_l) = runs
+    for a, b in zip(d_f, d_l):
+        cos = F.cosine_similarity(a, b, dim=0)
+        rel = (a - b).norm() / b.norm()
+        assert cos > 0.98 and rel < 0.2, (float(cos), float(rel))
+    torch.testing.assert_close(l_f, l_l, rtol=3e-2, atol=1e-2)  # (loss sum, correct) per peer
+    for a, b in zip(e_f, e_l):
+        assert abs(a["test_loss"] - b["test_loss"]) < 0.05 * max(1.0, b["test_loss"]), (a, b)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_lenet_eval_matches_torch(fused, monkeypatch):
+    from myfyp_amd.models import LeNet5
+
+    monkeypatch.setenv("MYFYP_LENET_FUSED", fused)
+    learners, refs, parts = _make_learners(lambda i: LeNet5(seed=60 + i), 2, 32, 70, 32, 0.05)
+    for lr_, ref in zip(learners, refs):
+        res = lr_.evaluate()
+        ref.load_state_dict(lr_.model.get_model().state_dict())
+        ref.eval()
+        x, y = lr_.device_data(False)
+        with torch.no_grad():
+            out = ref(x)
+        loss = float(F.cross_entropy(out, y))
+        acc = float((out.argmax(1) == y).float().mean())
+        assert abs(res["test_loss"] - loss) < 0.03 * max(1.0, loss), (res, loss)
+        assert abs(res["test_metric"] - acc) <= 2.0 / len(y) + 0.03
 
 
 def test_resnet_train_step_matches_torch():
