@@ -102,7 +102,8 @@ struct Lds {
   static constexpr int dz2c = dp2 + IPW * F0 * 4;                    // bf16 [16][KP2] channel-major dZ2
   static constexpr int tb1 = dz2c + 16 * KP2 * 2;                    // int [IPW*196]: X offset of each pooled-1 window
   static constexpr int tb2 = tb1 + IPW * NP1 * 4;                    // int [KP2]: P1 offset of each conv2 pixel (-1 pad)
-  static constexpr int w1 = tb2 + KP2 * 4;                           // bf16 [120][400]: fc1 weights (LDS-DMA from the shadow);
+  static constexpr int w2 = tb2 + KP2 * 4;                           // bf16 [16][25][8]: conv2 weights (Wf shadow copy)
+  static constexpr int w1 = w2 + 16 * 25 * 8 * 2;                    // bf16 [120][400]: fc1 weights (LDS-DMA from the shadow);
                                                                      // after fc1 dgrad: dZ2 halo image + dense dZ1
   static constexpr int dz2h = w1;                                    // bf16 [IPW][18][18][16]
   static constexpr int dz1 = dz2h + IPW * ZH * ZH * 16 * 2;          // bf16 [IPW*196][8][4]: dZ1 per pooled window
@@ -132,6 +133,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   int* sTb1 = reinterpret_cast<int*>(smem + L::tb1);
   int* sTb2 = reinterpret_cast<int*>(smem + L::tb2);
   bf16* sW1 = reinterpret_cast<bf16*>(smem + L::w1);
+  bf16* sW2 = reinterpret_cast<bf16*>(smem + L::w2);
   bf16* sDZ2h = reinterpret_cast<bf16*>(smem + L::dz2h);
   bf16* sDZ1 = reinterpret_cast<bf16*>(smem + L::dz1);
   float* sDb1 = reinterpret_cast<float*>(smem + L::misc + 64);
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
   if (tid < 32) sDb1[tid] = 0.f;  // db1 and db2
   for (int e = tid; e < 16 * L::KP2; e += NT) sDZ2c[e] = (bf16)0.f;
+  if (tid < 16 * 25) *reinterpret_cast<uint4*>(sW2 + tid * 8) = *reinterpret_cast<const uint4*>(shw + a.w_c2 + tid * 8);
   for (int e = tid; e < IPW * NP1; e += NT) {  // conv1 wgrad: top-left X element of pooled window e
     const int li = e / NP1, pp = e - li * NP1;
     sTb1[e] = (li * IH + 2 * (pp / P1H)) * SXR + 2 * (pp % P1H) * 4;
@@ -462,24 +465,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // ---------------- fc activations -> global (fc weight-gradient kernel); pool-2 backward
   {
     bf16* act = a.act + (int64_t)p * a.act_ps + (int64_t)b0 * A_W;
-    for (int e = tid; e < IPW * A_W; e += NT) {
-      const int li = e / A_W, col = e - li * A_W;
-      bf16 v;
-      if (col < A_Z3) v = sP2[li * F0 + col];
-      else if (col < A_Z4) v = sZ3[li * LD3 + col - A_Z3];
-      else if (col < A_DZ3) v = sZ4[li * LD4 + col - A_Z4];
-      else if (col < A_DZ4) v = sDZ3[li * LD3 + col - A_DZ3];
-      else if (col < A_DL) v = sDZ4[li * LD4 + col - A_DZ4];
-      else v = sDL[li * 16 + col - A_DL];
-      act[e] = v;
+    for (int e = tid; e < IPW * A_W / 8; e += NT) {  // 16-byte pieces (every segment is 8-aligned)
+      const int li = e / (A_W / 8), col = (e - li * (A_W / 8)) * 8;
+      const bf16* src;
+      if (col < A_Z3) src = sP2 + li * F0 + col;
+      else if (col < A_Z4) src = sZ3 + li * LD3 + col - A_Z3;
+      else if (col < A_DZ3) src = sZ4 + li * LD4 + col - A_Z4;
+      else if (col < A_DZ4) src = sDZ3 + li * LD3 + col - A_DZ3;
+      else if (col < A_DL) src = sDZ4 + li * LD4 + col - A_DZ4;
+      else src = sDL + li * 16 + col - A_DL;
+      *reinterpret_cast<uint4*>(act + li * A_W + col) = *reinterpret_cast<const uint4*>(src);
     }
   }
-  // conv2 dgrad B fragments W2[co = 4h+j][tap][ci = c]: requested now, used after the wgrad
-  bf16x4 wb[25];
-#pragma unroll
-  for (int kc = 0; kc < 25; ++kc)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wb[kc][j] = ldsel(shw, a.w_c2 + ((4 * h + j) * 25 + kc) * 8 + c, c < 6);
   {  // conv2 bias gradient: pooled gradients that pass the argmax (each thread sees one channel)
     float db = 0.f;
     for (int e = tid; e < IPW * F0; e += NT) db += sA2[e] < 4 ? sDP2[e] : 0.f;
@@ -499,10 +496,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (oy >= 0 && oy < Z2 && ox >= 0 && ox < Z2) {
       const int r0 = li * F0 + ((oy >> 1) * P2H + (ox >> 1)) * 16;
       const int sub = (oy & 1) * 2 + (ox & 1);
+      const uint4 am4 = *reinterpret_cast<const uint4*>(sA2 + r0);  // 16 argmax bytes
+      const unsigned amw[4] = {am4.x, am4.y, am4.z, am4.w};
 #pragma unroll
-      for (int co = 0; co < 16; ++co) {
-        v[co] = (bf16)(sA2[r0 + co] == sub ? sDP2[r0 + co] : 0.f);
-        sDZ2c[co * L::KP2 + li * 100 + oy * Z2 + ox] = v[co];
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 g4 = *reinterpret_cast<const float4*>(sDP2 + r0 + 4 * q4);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = 4 * q4 + j;
+          v[co] = (bf16)((int)((amw[q4] >> (8 * j)) & 0xffu) == sub ? gv[j] : 0.f);
+          sDZ2c[co * L::KP2 + li * 100 + oy * Z2 + ox] = v[co];
+        }
       }
     }
     bf16x8 lo, hi;
@@ -545,6 +550,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // ---------------- conv2 dgrad: dP1[m][ci] = sum_(tap, co) dZ2[m - tap][co] W2[co][tap][ci]
   //                  M = pooled-1 pixels of the IPW images, N = ci (16), K = (tap, co16): 25 chunks
   {
+    // B fragments W2[co = 4h+j][tap][ci = c] from the LDS copy (scattered 2-byte global loads cost
+    // ~16 address cycles each in the texture path; from LDS they are cheap)
+    bf16x4 wb[25];
+    const int cc = c < 8 ? c : 7;
+#pragma unroll
+    for (int kc = 0; kc < 25; ++kc)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16 v = sW2[((4 * h + j) * 25 + kc) * 8 + cc];
+        wb[kc][j] = c < 6 ? v : (bf16)0.f;
+      }
     LN_STAMP(16);
     constexpr int MT = (IPW * NP1 + 15) / 16;
     for (int mt = wave; mt < MT; mt += 8) {
