@@ -13,6 +13,7 @@ struct FedAvgWeights {
 };
 void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
 void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
+void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, unsigned long long mask, hipStream_t s);
 void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s);
 void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
                  const float* cg, const float* cl, hipStream_t s);

@@ -132,6 +132,46 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_apply(float* __restrict__ s
   }
 }
 
+// Single-rank FedAvg (no all-reduce between reduce and apply): each thread forms the weighted mean
+// of its coordinates over the rows and writes it into every masked row — one launch instead of two.
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_local(float* __restrict__ stacked, int P, int64_t n, int64_t ld, FedAvgWeights w,
+                                                           unsigned long long mask) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  const float inv = 1.f / fmaxf(w.wsum, 1e-12f);
+  if ((ld % 4) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride) {
+      float4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < P; ++p) {
+        const float wp = w.w[p];
+        if (wp == 0.f) continue;
+        const float4 v = reinterpret_cast<const float4*>(stacked + p * ld)[i];
+        acc.x += wp * v.x; acc.y += wp * v.y; acc.z += wp * v.z; acc.w += wp * v.w;
+      }
+      acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
+      for (int p = 0; p < P; ++p)
+        if ((mask >> p) & 1ull) reinterpret_cast<float4*>(stacked + p * ld)[i] = acc;
+    }
+    for (int64_t i = n4 * 4 + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+      float acc = 0.f;
+      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if ((mask >> p) & 1ull) stacked[p * ld + i] = acc * inv;
+    }
+  } else {
+    for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+      float acc = 0.f;
+      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if ((mask >> p) & 1ull) stacked[p * ld + i] = acc * inv;
+    }
+  }
+}
+
+void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, unsigned long long mask, hipStream_t s) {
+  hipLaunchKernelGGL(k_fedavg_local, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, stacked, P, n, ld, w, mask);
+}
+
 void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s) {
   hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, stacked, P, n, ld, w);
 }

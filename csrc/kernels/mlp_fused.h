@@ -35,12 +35,15 @@ struct MLPArgs {
   bf16* Xb16;       // same batches as bf16 (persistent path; null otherwise)
   int* Yb;          // [P][xb_rows]
   int64_t xb_rows;  // max_steps * B
+  unsigned* flags_zero;  // persistent epoch: hand-off flag lines zeroed by the gather kernel (or null)
+  int flags_per_peer;    // u32 words per peer
   // test data
   const uint8_t* const* Xtp;
   const int* const* Ytp;
   const int* n_t;
   // control
-  const int4* ctl;    // [P] {active, n_train, optimizer steps already taken (t0), n_test} — one scalar load
+  const int4* ctl;    // [P] {active (bit 0; bit 1 = fresh optimizer state), n_train, optimizer steps already
+                      //      taken (t0), n_test} — one scalar load
   const int* active;  // [P]
   const int* t0;      // [P] optimizer steps each peer already took in this fit
   // workspace

@@ -650,13 +650,16 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   const int n = a.ctl[p].y;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  if (a.flags_zero != nullptr && blockIdx.x == 0)  // the persistent epoch's flags start at 0 (replaces a memset node)
+    for (int q = threadIdx.x; q < a.flags_per_peer; q += 256) a.flags_zero[(int64_t)p * a.flags_per_peer + q] = 0u;
   if (i >= n || i >= a.xb_rows || !a.ctl[p].x) return;
   const int64_t src = a.shuffle_native ? (int64_t)feistel_perm((unsigned)i, (unsigned)n, *a.seed ^ (0x9e3779b97f4a7c15ull * (unsigned long long)(p + 1)))
                                        : (int64_t)a.perm[(int64_t)p * a.perm_stride + i];
   const uint8_t* xs = a.Xp[p] + src * (int64_t)a.D0;
-  uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
-  for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];
-  if (a.Xb16 != nullptr) {  // bf16 copy for the persistent epoch kernel (converted once per epoch)
+  if (a.Xb16 == nullptr) {  // uint8 rows for the step path
+    uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
+    for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];
+  } else {  // bf16 rows for the persistent epoch kernel (converted once per epoch; it never reads Xb)
     bf16* xh = a.Xb16 + ((int64_t)p * a.xb_rows + i) * a.D0;
     for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<bf16x8*>(xh)[q] = ld8_u8(xs + 8 * q);
   }

@@ -19,4 +19,5 @@ size_t mlp_persistent_flag_bytes(int P);
 int mlp_persistent_blocks(int P);
 hipError_t mlp_persistent_prepare(const MLPArgs& a);  // kernel attributes (once per engine)
 // Zero the flags (memset node) and launch one whole epoch for every active peer.
-hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s);
+// zero_flags = false: the epoch's gather kernel already zeroed them (MLPArgs::flags_zero).
+hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s, bool zero_flags = true);

@@ -252,6 +252,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
   int* sOk = reinterpret_cast<int*>(smem + L.ok);
 
   const int4 ctl = a.ctl[p];
+  const bool fresh = (ctl.x & 2) != 0;  // fresh optimizer state this fit: moments start at 0
   const int n = ctl.y;
   const int nsteps = (n + a.B - 1) / a.B;
   const int64_t pS = (int64_t)p * a.S;
@@ -272,8 +273,10 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
       if (s < KS1 && k < D0) {
         const int64_t idx = pS + a.off_w1 + (int64_t)orow * D0 + k;
         wv = *reinterpret_cast<const float4*>(a.params + idx);
-        mv = *reinterpret_cast<const float4*>(a.m + idx);
-        if (adam) vv = *reinterpret_cast<const float4*>(a.v + idx);
+        if (!fresh) {
+          mv = *reinterpret_cast<const float4*>(a.m + idx);
+          if (adam) vv = *reinterpret_cast<const float4*>(a.v + idx);
+        }
       }
       const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
@@ -290,14 +293,14 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
   for (int j = 0; j < 4; ++j) {
     const int64_t idx = pS + a.off_w2 + (int64_t)(16 * wave + 4 * h + j) * PD1 + NG * g + c;
     w2[j] = a.params[idx];
-    m2[j] = a.m[idx];
-    v2[j] = adam ? a.v[idx] : 0.f;
+    m2[j] = fresh ? 0.f : a.m[idx];
+    v2[j] = (adam && !fresh) ? a.v[idx] : 0.f;
   }
   if (tid < 16) {
     const int64_t idx = pS + a.off_b1 + NG * g + tid;
     sB1[tid] = a.params[idx];
-    sB1[16 + tid] = a.m[idx];
-    sB1[32 + tid] = adam ? a.v[idx] : 0.f;
+    sB1[16 + tid] = fresh ? 0.f : a.m[idx];
+    sB1[32 + tid] = (adam && !fresh) ? a.v[idx] : 0.f;
   }
 
   // ---- X staging. Every wave only ever reads its OWN K-step columns of the batch tile (the
@@ -596,6 +599,7 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   int* sOk = reinterpret_cast<int*>(smem + L.ok);
 
   const int4 ctl = a.ctl[p];
+  const bool fresh = (ctl.x & 2) != 0;  // fresh optimizer state this fit: moments start at 0
   const int n = ctl.y;
   const int nsteps = (n + a.B - 1) / a.B;
   const int64_t pS = (int64_t)p * a.S;
@@ -610,8 +614,8 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     if (wave < 4 && cin) {
       const int64_t idx = pS + a.off_w3 + (int64_t)c * PD2 + 32 * wave + kappa(h, j);
       w3[j] = a.params[idx];
-      m3[j] = a.m[idx];
-      if (adam) v3[j] = a.v[idx];
+      m3[j] = fresh ? 0.f : a.m[idx];
+      if (adam) v3[j] = fresh ? 0.f : a.v[idx];
     }
   }
   for (int e = tid; e < 32 * LDW3; e += NT) sW3[e] = (bf16)0.f;
@@ -619,14 +623,14 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
   if (tid < PD2) {
     const int64_t idx = pS + a.off_b2 + tid;
     sB2[tid] = a.params[idx];
-    sB2[PD2 + tid] = a.m[idx];
-    sB2[2 * PD2 + tid] = adam ? a.v[idx] : 0.f;
+    sB2[PD2 + tid] = fresh ? 0.f : a.m[idx];
+    sB2[2 * PD2 + tid] = (adam && !fresh) ? a.v[idx] : 0.f;
   } else if (tid < PD2 + 16) {
     const int k = tid - PD2;
     const int64_t idx = pS + a.off_b3 + k;
     sB3[k] = k < D3 ? a.params[idx] : 0.f;
-    sB3[16 + k] = k < D3 ? a.m[idx] : 0.f;
-    sB3[32 + k] = (k < D3 && adam) ? a.v[idx] : 0.f;
+    sB3[16 + k] = (k < D3 && !fresh) ? a.m[idx] : 0.f;
+    sB3[32 + k] = (k < D3 && adam && !fresh) ? a.v[idx] : 0.f;
   }
   __syncthreads();
   if (wave < 4 && cin) {
@@ -864,9 +868,11 @@ hipError_t mlp_persistent_prepare(const MLPArgs& a) {
   return a.Bpad == 64 ? prepare_one<64, false>(lds) : prepare_one<32, false>(lds);
 }
 
-hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
-  if (e != hipSuccess) return e;
+hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s, bool zero_flags) {
+  if (zero_flags) {
+    hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
+    if (e != hipSuccess) return e;
+  }
   const size_t lds = persistent_lds(a);
   const dim3 grid(mlp_persistent_blocks(a.P)), block(NT);
   const bool adam = a.opt.kind == 0;

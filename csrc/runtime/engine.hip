@@ -41,19 +41,76 @@ struct CtlUpload {
   unsigned long long seed;  // epoch shuffle key (in-kernel permutation)
   int P;
   int with_active;
+  // accumulators zeroed by the same launch (null = leave): the fit's loss / correct / give-up word,
+  // or the evaluation's loss / correct / confusion
+  float* zero_loss;
+  int* zero_correct;
+  int* zero_err;
+  int* zero_conf;
 };
 __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long long* seed) {
   const int p = threadIdx.x;
   if (p < u.P) {
     ctl[p] = u.ctl[p];
     if (u.with_active) active[p] = u.active[p];
+    if (u.zero_loss) u.zero_loss[p] = 0.f;
+    if (u.zero_correct) u.zero_correct[p] = 0;
   }
-  if (p == 0) *seed = u.seed;
+  if (u.zero_conf)
+    for (int q = p; q < u.P * 256; q += blockDim.x) u.zero_conf[q] = 0;
+  if (p == 0) {
+    *seed = u.seed;
+    if (u.zero_err) *u.zero_err = 0;
+  }
+}
+
+// Evaluation snapshot for the overlapped evaluation, in one launch: fp32 copy + bf16 shadow + W2T of
+// every peer's parameters (the epoch rewrites the live rows while the evaluation reads these), plus
+// the evaluation's control words and zeroed accumulators (block 0).
+__global__ __launch_bounds__(256) void k_eval_snapshot(MLPArgs a, float* params_out, bf16* shadow_out, bf16* w2t_out, CtlUpload u, int4* ctl,
+                                                       int* active) {
+  const int p = blockIdx.y;
+  if (blockIdx.x == 0 && p == 0) {
+    const int t = threadIdx.x;
+    if (t < u.P) {
+      ctl[t] = u.ctl[t];
+      active[t] = u.active[t];
+      u.zero_loss[t] = 0.f;
+      u.zero_correct[t] = 0;
+    }
+    for (int q = t; q < u.P * 256; q += blockDim.x) u.zero_conf[q] = 0;
+  }
+  const int64_t pS = (int64_t)p * a.S;
+  const int64_t n = a.numel;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float f = a.params[pS + i];
+    params_out[pS + i] = f;
+    const bf16 v = (bf16)f;
+    shadow_out[pS + i] = v;
+    const int64_t j = i - a.off_w2;
+    if (j >= 0 && j < (int64_t)a.D1 * a.D2) {
+      const int o2 = (int)(j / a.D1), o1 = (int)(j % a.D1);
+      w2t_out[(int64_t)p * a.D1 * a.D2 + (int64_t)o1 * a.D2 + o2] = v;
+    }
+  }
+}
+
+// Results -> pinned, host-mapped ring slot in ONE launch (instead of one copy per buffer).
+__global__ void k_publish(const float* loss, const int* correct, const int* err, const int* conf, int P, float* o_loss, int* o_correct,
+                          int* o_err, int* o_conf) {
+  const int t = threadIdx.x;
+  if (t < P) {
+    o_loss[t] = loss[t];
+    o_correct[t] = correct[t];
+  }
+  if (t == 0) *o_err = err ? *err : 0;
+  if (conf && o_conf)
+    for (int q = t; q < P * 256; q += blockDim.x) o_conf[q] = conf[q];
 }
 
 #define MLP_RING 16
 struct ResultSlot {
-  float* loss = nullptr;
+  float* loss = nullptr;  // pinned host memory, mapped: the same pointers are written by k_publish
   int* correct = nullptr;
   int* conf = nullptr;
   int* err = nullptr;
@@ -87,6 +144,23 @@ struct MLPEngine {
   int persist_mode = -1;  // -1 auto (eligible configs), 0 off
   int num_cus = 0;
   bool graph_persistent = false;
+  // deferred to the epoch's control upload on the persistent path (fewer tiny launches per round)
+  bool pending_zero_acc = false;  // zero loss / correct / give-up word
+  bool pending_fresh = false;     // fresh optimizer state: the kernel starts the moments at 0
+  std::vector<int> active_host_cache;
+  // evaluation overlapped with the epoch (persistent path): it reads a snapshot of the parameters
+  // taken on the main stream and runs on its own stream on the CUs the epoch's gangs leave free
+  hipStream_t eval_stream = nullptr;
+  hipEvent_t ev_snap = nullptr, ev_eval_done = nullptr;
+  bool eval_pending = false;
+  float* params_snap = nullptr;
+  bf16* shadow_snap = nullptr;
+  bf16* w2t_snap = nullptr;
+  int64_t snap_S = 0;
+  int4* d_ctl_eval = nullptr;
+  int* d_active_eval = nullptr;
+  float* d_loss_eval = nullptr;
+  int* d_correct_eval = nullptr;
 
   bool use_persistent() const {
     if (persist_mode == 0 || pb.h1x == nullptr || a.Xb16 == nullptr) return false;
@@ -95,6 +169,15 @@ struct MLPEngine {
   }
 
   ~MLPEngine() {
+    if (eval_stream) {
+      hipStreamSynchronize(eval_stream);
+      hipStreamDestroy(eval_stream);
+    }
+    if (ev_snap) hipEventDestroy(ev_snap);
+    if (ev_eval_done) hipEventDestroy(ev_eval_done);
+    if (params_snap) hipFree(params_snap);
+    if (shadow_snap) hipFree(shadow_snap);
+    if (w2t_snap) hipFree(w2t_snap);
     if (exec) hipGraphExecDestroy(exec);
     if (graph) hipGraphDestroy(graph);
     if (cap_stream) hipStreamDestroy(cap_stream);
@@ -113,27 +196,68 @@ struct MLPEngine {
 
   int alloc_ring() {
     for (auto& r : ring) {
-      CHECK_HIP(hipHostMalloc((void**)&r.loss, sizeof(float) * a.P, hipHostMallocDefault));
-      CHECK_HIP(hipHostMalloc((void**)&r.correct, sizeof(int) * a.P, hipHostMallocDefault));
-      CHECK_HIP(hipHostMalloc((void**)&r.conf, sizeof(int) * a.P * 256, hipHostMallocDefault));
-      CHECK_HIP(hipHostMalloc((void**)&r.err, sizeof(int), hipHostMallocDefault));
+      const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;  // written by k_publish
+      CHECK_HIP(hipHostMalloc((void**)&r.loss, sizeof(float) * a.P, fl));
+      CHECK_HIP(hipHostMalloc((void**)&r.correct, sizeof(int) * a.P, fl));
+      CHECK_HIP(hipHostMalloc((void**)&r.conf, sizeof(int) * a.P * 256, fl));
+      CHECK_HIP(hipHostMalloc((void**)&r.err, sizeof(int), fl));
       *r.err = 0;
       CHECK_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     }
     return 0;
   }
 
-  int upload(hipStream_t s, const int* active_host) {
-    CtlUpload u;
+  int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false) {
+    CtlUpload u{};
     u.P = a.P;
     u.with_active = active_host != nullptr;
     u.seed = seed_host;
     for (int p = 0; p < a.P; ++p) {
       u.ctl[p] = ctl_host[p];
+      if (fresh && u.ctl[p].x) u.ctl[p].x |= 2;
       u.active[p] = active_host ? active_host[p] : 0;
+    }
+    if (zero_fit) {
+      u.zero_loss = d_loss;
+      u.zero_correct = d_correct;
+      u.zero_err = pb.err;
     }
     hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(MLP_CTL_MAX), 0, s, u, d_ctl, d_active, d_seed);
     CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+
+  int publish(hipStream_t s, ResultSlot& r, const float* loss, const int* correct, const int* err, const int* conf) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, loss, correct, err, conf, a.P, r.loss, r.correct, r.err, conf ? r.conf : nullptr);
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+
+  // evaluation resources for the overlapped path (allocated on first use)
+  int ensure_eval_side() {
+    if (!eval_stream) {
+      CHECK_HIP(hipStreamCreateWithFlags(&eval_stream, hipStreamNonBlocking));
+      CHECK_HIP(hipEventCreateWithFlags(&ev_snap, hipEventDisableTiming));
+      CHECK_HIP(hipEventCreateWithFlags(&ev_eval_done, hipEventDisableTiming));
+      void* p;
+      if (alloc(&p, (size_t)a.P * 16)) return 1;
+      d_ctl_eval = (int4*)p;
+      if (alloc(&p, (size_t)a.P * 4)) return 1;
+      d_active_eval = (int*)p;
+      if (alloc(&p, (size_t)a.P * 4)) return 1;
+      d_loss_eval = (float*)p;
+      if (alloc(&p, (size_t)a.P * 4)) return 1;
+      d_correct_eval = (int*)p;
+    }
+    if (snap_S != a.S) {
+      if (params_snap) hipFree(params_snap);
+      if (shadow_snap) hipFree(shadow_snap);
+      if (w2t_snap) hipFree(w2t_snap);
+      CHECK_HIP(hipMalloc((void**)&params_snap, (size_t)a.P * a.S * sizeof(float)));
+      CHECK_HIP(hipMalloc((void**)&shadow_snap, (size_t)a.P * a.S * sizeof(bf16)));
+      CHECK_HIP(hipMalloc((void**)&w2t_snap, (size_t)a.P * a.D1 * a.D2 * sizeof(bf16)));
+      snap_S = a.S;
+    }
     return 0;
   }
 
@@ -160,10 +284,14 @@ struct MLPEngine {
     {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
+      if (graph_persistent) {  // ... which also zeroes the hand-off flags (no memset node)
+        ga.flags_zero = pb.flags;
+        ga.flags_per_peer = (int)(pb.flag_bytes / sizeof(unsigned) / a.P);
+      }
       mlp_launch_gather_epoch(ga, cap_stream);
     }
     if (graph_persistent) {
-      hipError_t le = mlp_launch_persistent_epoch(a, pb, cap_stream);
+      hipError_t le = mlp_launch_persistent_epoch(a, pb, cap_stream, false);
       if (le != hipSuccess) {
         hipGraph_t g = nullptr;
         hipStreamEndCapture(cap_stream, &g);
@@ -235,6 +363,25 @@ int myfyp_fedavg_stacked_apply(float* stacked, const float* out, int P, int64_t 
   for (int p = 0; p < P; ++p)
     if (mask_host[p] != 0.f) mask |= 1ull << p;
   fl_fedavg_apply(stacked, out, P, n, ld, mask, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// Single-rank FedAvg of a stacked group in one launch (weights and mask by value).
+int myfyp_fedavg_stacked_local(float* stacked, int P, int64_t n, int64_t ld, const float* w_host, const float* mask_host, void* stream) {
+  if (P < 1 || P > FEDAVG_MAX_PEERS) {
+    g_last_error = "fedavg_stacked: 1..64 rows";
+    return 2;
+  }
+  FedAvgWeights w{};
+  double sum = 0.0;
+  unsigned long long mask = 0;
+  for (int p = 0; p < P; ++p) {
+    w.w[p] = w_host[p];
+    sum += w_host[p];
+    if (mask_host[p] != 0.f) mask |= 1ull << p;
+  }
+  w.wsum = (float)sum;
+  fl_fedavg_local(stacked, P, n, ld, w, mask, (hipStream_t)stream);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -421,6 +568,13 @@ int mlp_engine_begin(void* h, const int* active_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
+  if (e->use_persistent()) {
+    // the persistent epoch reads the fp32 master rows (no shadow refresh needed) and the next
+    // epoch upload carries the mask and zeroes the accumulators: nothing to launch here
+    e->active_host_cache.assign(active_host, active_host + e->a.P);
+    e->pending_zero_acc = true;
+    return 0;
+  }
   if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
@@ -434,6 +588,10 @@ int mlp_engine_begin(void* h, const int* active_host, void* stream) {
 int mlp_engine_zero_state(void* h, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
+  if (e->use_persistent()) {  // the next persistent epoch starts its moments at 0 in registers
+    e->pending_fresh = true;
+    return 0;
+  }
   const size_t bytes = (size_t)e->a.P * e->a.S * sizeof(float);
   CHECK_HIP(hipMemsetAsync(e->a.m, 0, bytes, s));
   if (e->a.v) CHECK_HIP(hipMemsetAsync(e->a.v, 0, bytes, s));
@@ -480,7 +638,9 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
     if (e->capture(e->max_steps)) return 1;
   }
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
-  if (e->upload(s, nullptr)) return 1;
+  const bool pa = e->graph_persistent && e->pending_zero_acc;
+  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh)) return 1;
+  if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
   CHECK_HIP(hipGraphLaunch(e->exec, s));
   return 0;
 }
@@ -490,10 +650,13 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
-  if (e->upload(s, nullptr)) return 1;
+  const bool pers = e->use_persistent();
+  const bool pa = pers && e->pending_zero_acc;
+  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, pers && e->pending_fresh)) return 1;
+  if (pers) e->pending_zero_acc = e->pending_fresh = false;
   {
     MLPArgs ga = e->a;
-    if (!e->use_persistent()) ga.Xb16 = nullptr;
+    if (!pers) ga.Xb16 = nullptr;
     mlp_launch_gather_epoch(ga, s);
   }
   if (e->use_persistent()) {
@@ -510,12 +673,11 @@ int mlp_engine_stats_async(void* h, int slot, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   ResultSlot& r = e->ring[slot % MLP_RING];
-  CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
-  if (e->pb.err)
-    CHECK_HIP(hipMemcpyAsync(r.err, e->pb.err, sizeof(int), hipMemcpyDeviceToHost, s));
-  else
-    *r.err = 0;
+  if (e->pending_zero_acc) {  // a fit with no epoch launched: zero what it would have zeroed
+    if (e->upload(s, e->active_host_cache.data(), true, false)) return 1;
+    e->pending_zero_acc = false;
+  }
+  if (e->publish(s, r, e->d_loss, e->d_correct, e->pb.err, nullptr)) return 1;
   CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
@@ -526,6 +688,51 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   hipStream_t s = (hipStream_t)stream;
   ResultSlot& r = e->ring[slot % MLP_RING];
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].x = active_host[p];
+  if (e->use_persistent()) {
+    // Overlapped evaluation: snapshot the parameters on the main stream (one launch: control words,
+    // accumulators, fp32 + bf16 + W2T copies), then evaluate the snapshot on the side stream while
+    // the main stream goes on to the epoch, whose gangs leave ~half of the CUs free. The previous
+    // evaluation must be done with the snapshot buffers before they are overwritten.
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->ensure_eval_side()) return 1;
+    if (e->eval_pending) CHECK_HIP(hipStreamWaitEvent(s, e->ev_eval_done, 0));
+    CtlUpload u{};
+    u.P = e->a.P;
+    u.with_active = 1;
+    u.seed = e->seed_host;
+    for (int p = 0; p < e->a.P; ++p) {
+      u.ctl[p] = e->ctl_host[p];
+      u.active[p] = active_host[p];
+    }
+    u.zero_loss = e->d_loss_eval;
+    u.zero_correct = e->d_correct_eval;
+    u.zero_conf = e->d_conf;
+    MLPArgs ea = e->a;
+    ea.params = e->params_snap;
+    ea.shadow = e->shadow_snap;
+    ea.w2t = e->w2t_snap;
+    ea.ctl = e->d_ctl_eval;
+    ea.active = e->d_active_eval;
+    ea.loss_acc = e->d_loss_eval;
+    ea.correct_acc = e->d_correct_eval;
+    {
+      const int64_t blocks = (e->a.numel + 255) / 256;
+      hipLaunchKernelGGL(k_eval_snapshot, dim3((unsigned)(blocks < 1024 ? blocks : 1024), e->a.P), dim3(256), 0, s, e->a, e->params_snap,
+                         e->shadow_snap, e->w2t_snap, u, e->d_ctl_eval, e->d_active_eval);
+      CHECK_HIP(hipGetLastError());
+    }
+    CHECK_HIP(hipEventRecord(e->ev_snap, s));
+    hipStream_t es = e->eval_stream;
+    CHECK_HIP(hipStreamWaitEvent(es, e->ev_snap, 0));
+    for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(ea, base, es);
+    CHECK_HIP(hipGetLastError());
+    if (e->publish(es, r, e->d_loss_eval, e->d_correct_eval, nullptr, e->d_conf)) return 1;
+    CHECK_HIP(hipEventRecord(r.ev, es));
+    CHECK_HIP(hipEventRecord(e->ev_eval_done, es));
+    e->eval_pending = true;
+    return 0;
+  }
+  if (e->eval_pending) CHECK_HIP(hipStreamWaitEvent(s, e->ev_eval_done, 0));
   if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
@@ -533,10 +740,7 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   mlp_launch_sync_shadow(e->a, s);
   for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(e->a, base, s);
   CHECK_HIP(hipGetLastError());
-  CHECK_HIP(hipMemcpyAsync(r.loss, e->d_loss, sizeof(float) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(r.correct, e->d_correct, sizeof(int) * e->a.P, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipMemcpyAsync(r.conf, e->d_conf, sizeof(int) * e->a.P * 256, hipMemcpyDeviceToHost, s));
-  *r.err = 0;
+  if (e->publish(s, r, e->d_loss, e->d_correct, nullptr, e->d_conf)) return 1;
   CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }

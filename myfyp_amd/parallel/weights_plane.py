@@ -90,12 +90,16 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
             w[lr._engine.slot] = wt
             mask[lr._engine.slot] = 1.0
         n = group.numel
-        buf = group.fedavg_buffer()
         fast = ops.fast_lib()
         stream = torch.cuda.current_stream(dev).cuda_stream
-        ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, stream), "fedavg_reduce")
-        fed.all_reduce_(buf)
-        ops.check(fast.myfyp_fedavg_stacked_apply(group.params.data_ptr(), buf.data_ptr(), group.capacity, n, group.S, mask.ctypes.data, stream), "fedavg_apply")
+        if fed.world == 1:  # nothing to all-reduce: weighted mean and write-back in one launch
+            ops.check(fast.myfyp_fedavg_stacked_local(group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, mask.ctypes.data, stream),
+                      "fedavg_local")
+        else:
+            buf = group.fedavg_buffer()
+            ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, stream), "fedavg_reduce")
+            fed.all_reduce_(buf)
+            ops.check(fast.myfyp_fedavg_stacked_apply(group.params.data_ptr(), buf.data_ptr(), group.capacity, n, group.S, mask.ctypes.data, stream), "fedavg_apply")
         total_w = float(sum(weights))  # local share; the global Σw stays on the device (buf[n])
     elif group is not None:
         wm = torch.zeros(2, group.capacity, dtype=torch.float32)
