@@ -645,29 +645,62 @@ __device__ unsigned feistel_perm(unsigned x, unsigned n, unsigned long long key)
 // epoch gather: Xb[p][i] = X_p[perm_p[i]], Yb[p][i] = Y_p[perm_p[i]] for i < n_p (first node of
 // every epoch graph). grid = (ceil(xb_rows / 4), 1, P), block = 256 = 4 rows x 64 lanes (8 B each).
 // ---------------------------------------------------------------------------------------------
+constexpr int GATHER_RPW = 4;  // rows per wave: their loads are in flight together
 __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   const int p = blockIdx.z;
   const int n = a.ctl[p].y;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (a.flags_zero != nullptr && blockIdx.x == 0)  // the persistent epoch's flags start at 0 (replaces a memset node)
     for (int q = threadIdx.x; q < a.flags_per_peer; q += 256) a.flags_zero[(int64_t)p * a.flags_per_peer + q] = 0u;
-  if (i >= n || i >= a.xb_rows || !a.ctl[p].x) return;
-  const int64_t src = a.shuffle_native ? (int64_t)feistel_perm((unsigned)i, (unsigned)n, *a.seed ^ (0x9e3779b97f4a7c15ull * (unsigned long long)(p + 1)))
-                                       : (int64_t)a.perm[(int64_t)p * a.perm_stride + i];
-  const uint8_t* xs = a.Xp[p] + src * (int64_t)a.D0;
-  if (a.Xb16 == nullptr) {  // uint8 rows for the step path
-    uint8_t* xd = a.Xb + ((int64_t)p * a.xb_rows + i) * a.D0;
-    for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<uint2*>(xd)[q] = reinterpret_cast<const uint2*>(xs)[q];
-  } else {  // bf16 rows for the persistent epoch kernel (converted once per epoch; it never reads Xb)
-    bf16* xh = a.Xb16 + ((int64_t)p * a.xb_rows + i) * a.D0;
-    for (int q = lane; q < a.D0 / 8; q += 64) reinterpret_cast<bf16x8*>(xh)[q] = ld8_u8(xs + 8 * q);
+  if (!a.ctl[p].x) return;
+  const int i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GATHER_RPW;
+  const uint8_t* xp = a.Xp[p];
+  const int* yp = a.Yp[p];
+  constexpr int QPL = 4;  // uint2 pieces per lane per row (D0 <= 2048)
+  int64_t src[GATHER_RPW];
+#pragma unroll
+  for (int r = 0; r < GATHER_RPW; ++r) {
+    const int i = i0 + r;
+    const bool ok = i < n && i < a.xb_rows;
+    src[r] = !ok ? -1
+                 : (a.shuffle_native ? (int64_t)feistel_perm((unsigned)i, (unsigned)n, *a.seed ^ (0x9e3779b97f4a7c15ull * (unsigned long long)(p + 1)))
+                                     : (int64_t)a.perm[(int64_t)p * a.perm_stride + i]);
   }
-  if (lane == 0) a.Yb[(int64_t)p * a.xb_rows + i] = a.Yp[p][src];
+  uint2 v[GATHER_RPW][QPL];
+#pragma unroll
+  for (int r = 0; r < GATHER_RPW; ++r)
+#pragma unroll
+    for (int k = 0; k < QPL; ++k) {
+      const int q = lane + 64 * k;
+      v[r][k] = (src[r] >= 0 && q < a.D0 / 8) ? reinterpret_cast<const uint2*>(xp + src[r] * (int64_t)a.D0)[q] : uint2{0u, 0u};
+    }
+#pragma unroll
+  for (int r = 0; r < GATHER_RPW; ++r) {
+    if (src[r] < 0) continue;
+    const int64_t row = (int64_t)p * a.xb_rows + i0 + r;
+#pragma unroll
+    for (int k = 0; k < QPL; ++k) {
+      const int q = lane + 64 * k;
+      if (q >= a.D0 / 8) continue;
+      if (a.Xb16 == nullptr) {  // uint8 rows for the step path
+        reinterpret_cast<uint2*>(a.Xb + row * a.D0)[q] = v[r][k];
+      } else {  // bf16 rows for the persistent epoch kernel (converted once per epoch; it never reads Xb)
+        bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          h[j] = (bf16)(float)((v[r][k].x >> (8 * j)) & 0xffu);
+          h[4 + j] = (bf16)(float)((v[r][k].y >> (8 * j)) & 0xffu);
+        }
+        reinterpret_cast<bf16x8*>(a.Xb16 + row * a.D0)[q] = h;
+      }
+    }
+    if (lane == 0) a.Yb[row] = yp[src[r]];
+  }
 }
 
 void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_gather_epoch, dim3((unsigned)((a.xb_rows + 3) / 4), 1, a.P), dim3(256), 0, s, a);
+  const int64_t waves = (a.xb_rows + GATHER_RPW - 1) / GATHER_RPW;
+  hipLaunchKernelGGL(mlp_gather_epoch, dim3((unsigned)((waves + 3) / 4), 1, a.P), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -701,7 +734,7 @@ static void launch_head(const MLPArgs& a, int step, int base, bool train, int ro
 }
 
 bool mlp_shape_supported(int D0, int D1, int D2, int D3) {
-  if (D0 <= 0 || D0 % 8 != 0 || D3 < 1 || D3 > 16) return false;
+  if (D0 <= 0 || D0 % 8 != 0 || D0 > 2048 || D3 < 1 || D3 > 16) return false;
   const int t1 = D1 / 64, t2 = D2 / 64;
   if (D1 % 64 || D2 % 64) return false;
   return (t1 == 4 && t2 == 2) || (t1 == 2 && t2 == 1) || (t1 == 4 && t2 == 4) || (t1 == 8 && t2 == 4) || (t1 == 2 && t2 == 2) ||
