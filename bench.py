@@ -168,7 +168,10 @@ def main() -> None:
             break
     final_acc = mean_acc[max(mean_acc)] if mean_acc else None
     # per-stage wall-time breakdown of the first local peer (stderr, diagnostics only)
-    tm = logger.get_timings().get(nodes[0].addr, {})
+    tm = dict(logger.get_timings().get(nodes[0].addr, {}))
+    for nd in nodes:  # the round driver logs its host time per round under one of the local peers
+        if "driver_round" in logger.get_timings().get(nd.addr, {}):
+            tm["driver_round"] = logger.get_timings()[nd.addr]["driver_round"]
     brk = {k: round(1000 * float(np.median(v[args.warmup :] or v)), 3) for k, v in tm.items()}
     ends = [round_end[r] for r in sorted(round_end) if r >= args.warmup - 1]
     if len(ends) > 2:
