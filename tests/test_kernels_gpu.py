@@ -47,6 +47,35 @@ def test_stacked_sum_and_broadcast(dev):
             torch.testing.assert_close(st[p], before[p])
 
 
+@pytest.mark.parametrize("N,ld", [(235146, 235200), (5003, 5005)])
+def test_fedavg_stacked_local_and_split(dev, N, ld):
+    """Single-rank FedAvg in one kernel == reduce + apply (the multi-rank form) == torch."""
+    from myfyp_amd import ops
+
+    P = 8
+    st = torch.randn(P, ld, device=dev)
+    w = np.array([3, 0, 1, 2, 5, 0, 4, 1], dtype=np.float32)
+    mask = np.array([1, 1, 1, 0, 1, 1, 1, 0], dtype=np.float32)
+    ref = (torch.from_numpy(w).to(dev).view(-1, 1) * st[:, :N]).sum(0) / float(w.sum())
+    fast = ops.fast_lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    a = st.clone()
+    ops.check(fast.myfyp_fedavg_stacked_local(a.data_ptr(), P, N, ld, w.ctypes.data, mask.ctypes.data, stream), "local")
+    b = st.clone()
+    buf = torch.empty(N + 1, device=dev)
+    ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), b.data_ptr(), P, N, ld, w.ctypes.data, stream), "reduce")
+    ops.check(fast.myfyp_fedavg_stacked_apply(b.data_ptr(), buf.data_ptr(), P, N, ld, mask.ctypes.data, stream), "apply")
+    torch.cuda.synchronize()
+    for p in range(P):
+        if mask[p]:
+            torch.testing.assert_close(a[p, :N], ref, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(b[p, :N], ref, rtol=1e-5, atol=1e-5)
+        else:
+            torch.testing.assert_close(a[p], st[p])
+            torch.testing.assert_close(b[p], st[p])
+        torch.testing.assert_close(a[p, N:], st[p, N:])  # padding untouched
+
+
 @pytest.mark.parametrize("k", [1, 2, 5, 8, 16])
 def test_coordinate_median(dev, k):
     from myfyp_amd import ops
