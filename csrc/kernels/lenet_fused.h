@@ -32,6 +32,18 @@ struct LenetArgs {
   // per-workgroup conv gradient records [P][B / ipw][4832] fp32 (reduced by the second kernel)
   float* part;
   int64_t part_ps;
+  // fused optimizer (SGD + momentum / weight decay / Nesterov / FedProx / SCAFFOLD) applied by the
+  // second kernel where each gradient is produced: master rows, momentum and bf16 shadow updated in
+  // place (no k_opt_step launch). mom == null: gradients only (into gf / g).
+  float* wmaster;  // the params rows (writable view)
+  float* mom;
+  bf16* shadow_rw;
+  const float* anchor;
+  const float* cg;
+  const float* cl;
+  OptParams opt;
+  int64_t t_c1, t_c2, t_f1, t_f2, t_f3;  // torch-order offsets of the weight tensors
+  const int* f1_e2t;                     // fc1: engine input column -> torch column
   // outputs
   float* stats;    // [P][4]: loss sum, correct
   int* confusion;  // [P][16][16] or null

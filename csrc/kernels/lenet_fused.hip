@@ -637,6 +637,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 constexpr int FC_WTILES = 8 * 25 + 6 * 8 + 6;
 constexpr int FC_TILES = FC_WTILES + 8 + 6 + 1;
 constexpr int FC_BLOCKS = (FC_TILES + 3) / 4;
+
+// One parameter's optimizer step: torch-order master element ti, its momentum, the FedProx /
+// SCAFFOLD terms, and the bf16 Wf-layout shadow element si (< 0: a bias, no shadow). Peers without
+// samples this step keep their parameters (k_opt_step's `active`).
+__device__ __forceinline__ void apply_update(const LenetArgs& a, int p, float g, int64_t ti, int64_t si) {
+  if (a.nb[p] <= 0) return;
+  const int64_t ps = a.params_ps;
+  float* w = a.wmaster + (int64_t)p * ps;
+  float* m = a.mom + (int64_t)p * ps;
+  float wv = w[ti], mv = m[ti], vv = 0.f;
+  opt_update(a.opt, g, wv, mv, vv, 1.f, 1.f, a.anchor ? a.anchor + (int64_t)p * ps : nullptr, a.cg ? a.cg + (int64_t)p * ps : nullptr,
+             a.cl ? a.cl + (int64_t)p * ps : nullptr, ti);
+  w[ti] = wv;
+  m[ti] = mv;
+  if (si >= 0) a.shadow_rw[(int64_t)p * a.shadow_ps + si] = (bf16)wv;
+}
 constexpr int RED_BLOCKS = (PR_N + 255) / 256;
 template <int IPW>
 __global__ __launch_bounds__(256) void k_lenet_fc_grad(LenetArgs a) {
@@ -664,7 +680,21 @@ __global__ __launch_bounds__(256) void k_lenet_fc_grad(LenetArgs a) {
     float s = 0.f;
 #pragma unroll 8
     for (int w = 0; w < G; ++w) s += rec[(int64_t)w * PR_N];
-    (bias ? a.g + (int64_t)p * a.g_ps : a.gf + (int64_t)p * a.gf_ps)[dst] = s;
+    if (a.mom == nullptr) {
+      (bias ? a.g + (int64_t)p * a.g_ps : a.gf + (int64_t)p * a.gf_ps)[dst] = s;
+      return;
+    }
+    // torch-order index of this element; the shadow index is dst for weights
+    int64_t ti;
+    if (bias) {
+      ti = dst;
+    } else if (e < PR_W2) {
+      ti = a.t_c1 + ((e / 200) * 3 + (e & 7)) * 25 + ((e % 200) >> 3);
+    } else {
+      const int r = e - PR_W2;
+      ti = a.t_c2 + ((r / 200) * 6 + (r & 7)) * 25 + ((r % 200) >> 3);
+    }
+    apply_update(a, p, s, ti, bias ? -1 : dst);
     return;
   }
   const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
@@ -704,11 +734,27 @@ __global__ __launch_bounds__(256) void k_lenet_fc_grad(LenetArgs a) {
     }
   }
   // C[row 4h+i = output unit][col c = input (bias tiles: every column holds the sum)]
-  float* dst = bias ? a.g + (int64_t)p * a.g_ps + woff : a.gf + (int64_t)p * a.gf_ps + woff;
+  if (a.mom == nullptr) {
+    float* dst = bias ? a.g + (int64_t)p * a.g_ps + woff : a.gf + (int64_t)p * a.gf_ps + woff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int no = 16 * nt + 4 * h + i;
+      if (no < nout && k < nin) dst[bias ? no : (int64_t)no * ld + k] = acc[i];
+    }
+    return;
+  }
+  const int64_t tw = t < 200 ? a.t_f1 : t < 248 ? a.t_f2 : a.t_f3;
+  const int tld = t < 200 ? F0 : t < 248 ? F1 : F2;  // torch row length
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int no = 16 * nt + 4 * h + i;
-    if (no < nout && k < nin) dst[bias ? no : (int64_t)no * ld + k] = acc[i];
+    if (no >= nout || k >= nin) continue;
+    if (bias) {
+      if (c == 0) apply_update(a, p, acc[i], woff + no, -1);
+    } else {
+      const int kt_ = t < 200 ? a.f1_e2t[k] : k;
+      apply_update(a, p, acc[i], tw + (int64_t)no * tld + kt_, woff + (int64_t)no * ld + k);
+    }
   }
 }
 

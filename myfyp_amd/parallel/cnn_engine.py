@@ -69,6 +69,10 @@ class LenetArgs(ctypes.Structure):
         ("scale", c_float), ("shadow", c_void_p), ("shadow_ps", c_int64), ("w_c1", c_int64), ("w_c2", c_int64), ("w_f1", c_int64), ("w_f2", c_int64),
         ("w_f3", c_int64), ("params", c_void_p), ("params_ps", c_int64), ("b_c1", c_int64), ("b_c2", c_int64), ("b_f1", c_int64), ("b_f2", c_int64),
         ("b_f3", c_int64), ("gf", c_void_p), ("gf_ps", c_int64), ("g", c_void_p), ("g_ps", c_int64), ("act", c_void_p), ("act_ps", c_int64), ("part", c_void_p), ("part_ps", c_int64),
+        ("wmaster", c_void_p), ("mom", c_void_p), ("shadow_rw", c_void_p), ("anchor", c_void_p), ("cg", c_void_p), ("cl", c_void_p),
+        ("opt_kind", c_int), ("opt_lr", c_float), ("opt_beta1", c_float), ("opt_beta2", c_float), ("opt_eps", c_float), ("opt_wd", c_float),
+        ("opt_momentum", c_float), ("opt_nesterov", c_int), ("opt_mu", c_float),
+        ("t_c1", c_int64), ("t_c2", c_int64), ("t_f1", c_int64), ("t_f2", c_int64), ("t_f3", c_int64), ("f1_e2t", c_void_p),
         ("stats", c_void_p), ("confusion", c_void_p), ("nb", c_void_p), ("train", c_int),
     ]
 
@@ -716,8 +720,7 @@ class CNNGroup:
 
     def _train_step(self, offset: int) -> None:
         if self.arch != "resnet18" and self.lenet_fused:
-            self._lenet_fused(True, offset)
-            self._optimizer(update=True)
+            self._lenet_fused(True, offset)  # forward, backward and the SGD step
             return
         x0 = self._prep(True, offset)
         if self.arch == "resnet18":
@@ -752,6 +755,14 @@ class CNNGroup:
         a.part, a.part_ps = part.data_ptr(), part.shape[1]
         a.stats, a.confusion, a.nb = self.stat.data_ptr(), None if train else self.conf.data_ptr(), self.nb.data_ptr()
         a.train = int(train)
+        if train:  # SGD applied by the fc-gradient kernel where each gradient is produced (no k_opt_step)
+            o = self._opt
+            a.wmaster, a.mom, a.shadow_rw = self.params.data_ptr(), self.mom.data_ptr(), self.shadow.data_ptr()
+            a.anchor, a.cg, a.cl = _p(o.get("anchor")), _p(o.get("cg")), _p(o.get("cl"))
+            a.opt_kind, a.opt_lr, a.opt_beta1, a.opt_beta2, a.opt_eps = o["kind"], o["lr"], 0.9, 0.999, 1e-8
+            a.opt_wd, a.opt_momentum, a.opt_nesterov, a.opt_mu = o["weight_decay"], o["momentum"], o["nesterov"], o["mu"]
+            a.t_c1, a.t_c2, a.t_f1, a.t_f2, a.t_f3 = (self._off(x.weight) for x in L)
+            a.f1_e2t = self._keep_colmaps[0].data_ptr()  # fc1 is the only layer with a column map (engine -> torch)
         _chk(_lib().lenet_fused_step(ctypes.byref(a), P, LENET_IPW, self._stream()), "lenet_fused_step")
 
     def _optimizer(self, update: bool) -> None:
