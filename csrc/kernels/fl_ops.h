@@ -14,6 +14,16 @@ struct FedAvgWeights {
 void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
 void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
 void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, unsigned long long mask, hipStream_t s);
+// Topology mixing of a stacked group in place: row p <- sum_k w[p][k] * row idx[p][k] (P <= 16 rows,
+// <= 8 sources per row; rows with nsrc == 0 are left alone).
+#define MIX_MAX_PEERS 16
+#define MIX_MAX_SRC 8
+struct MixPlan {
+  float w[MIX_MAX_PEERS][MIX_MAX_SRC];
+  unsigned char idx[MIX_MAX_PEERS][MIX_MAX_SRC];
+  unsigned char nsrc[MIX_MAX_PEERS];
+};
+void fl_neighbor_mix(float* stacked, int P, int64_t n, int64_t ld, const MixPlan& m, hipStream_t s);
 void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s);
 void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
                  const float* cg, const float* cl, hipStream_t s);

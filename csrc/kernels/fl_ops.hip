@@ -182,6 +182,52 @@ void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t
   hipLaunchKernelGGL(k_fedavg_apply, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, out, P, n, ld, mask);
 }
 
+// Gossip neighbour averaging of co-located peers (reference: aggregator over the neighbours'
+// models, p2pfl/learning/aggregators/fedavg.py driven by gossip_weights). One thread owns a float4
+// column of every row: it loads all P rows into registers, then writes each row's mixture back, so
+// the in-place update never reads a row another thread has already written.
+template <int P>
+__global__ __launch_bounds__(FL_BLOCK) void k_neighbor_mix(float* __restrict__ stacked, int64_t n4, int64_t ld, MixPlan m) {
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n4; i += stride) {
+    float4 v[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) v[p] = reinterpret_cast<const float4*>(stacked + p * ld)[i];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int ns = m.nsrc[p];
+      if (ns == 0) continue;
+      float4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < MIX_MAX_SRC; ++k) {
+        if (k >= ns) break;
+        const float wk = m.w[p][k];
+        float4 s = v[0];
+        // register-array select (a dynamic index would spill v to scratch)
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+          if (q == m.idx[p][k]) s = v[q];
+        acc.x += wk * s.x; acc.y += wk * s.y; acc.z += wk * s.z; acc.w += wk * s.w;
+      }
+      reinterpret_cast<float4*>(stacked + p * ld)[i] = acc;
+    }
+  }
+}
+
+void fl_neighbor_mix(float* stacked, int P, int64_t n, int64_t ld, const MixPlan& m, hipStream_t s) {
+  // rows are padded to ld (a multiple of 4); mixing the padding too keeps every access a float4
+  const int64_t n4 = (n + 3) / 4;
+  const dim3 g(grid_for(n4)), b(FL_BLOCK);
+  switch (P) {
+#define MIX_CASE(K) \
+  case K: hipLaunchKernelGGL(k_neighbor_mix<K>, g, b, 0, s, stacked, n4, ld, m); break;
+    MIX_CASE(1) MIX_CASE(2) MIX_CASE(3) MIX_CASE(4) MIX_CASE(5) MIX_CASE(6) MIX_CASE(7) MIX_CASE(8)
+    MIX_CASE(9) MIX_CASE(10) MIX_CASE(11) MIX_CASE(12) MIX_CASE(13) MIX_CASE(14) MIX_CASE(15) MIX_CASE(16)
+#undef MIX_CASE
+    default: break;
+  }
+}
+
 // per-coordinate median of K ≤ 16 models: insertion sort in registers
 __global__ __launch_bounds__(FL_BLOCK) void k_coordinate_median(float* __restrict__ out, const uint64_t* __restrict__ srcs, int K, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;

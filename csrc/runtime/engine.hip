@@ -385,6 +385,34 @@ int myfyp_fedavg_stacked_local(float* stacked, int P, int64_t n, int64_t ld, con
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+// Topology mixing of a stacked group in one launch. w_host is the dense [P][P] mixing matrix
+// (row p: the weights of the sources of row p, already renormalised); rows of an all-zero matrix
+// row are left untouched. ld must be a multiple of 4 (stacked rows are padded to 64 floats).
+int myfyp_neighbor_mix_stacked(float* stacked, int P, int64_t n, int64_t ld, const float* w_host, void* stream) {
+  if (P < 1 || P > MIX_MAX_PEERS || (ld % 4) != 0 || ld < ((n + 3) / 4) * 4) {
+    g_last_error = "neighbor_mix_stacked: 1..16 rows, ld a multiple of 4 covering n";
+    return 2;
+  }
+  MixPlan m{};
+  for (int p = 0; p < P; ++p) {
+    int k = 0;
+    for (int q = 0; q < P; ++q) {
+      const float wq = w_host[p * P + q];
+      if (wq == 0.f) continue;
+      if (k == MIX_MAX_SRC) {
+        g_last_error = "neighbor_mix_stacked: more than 8 sources in a row";
+        return 2;
+      }
+      m.w[p][k] = wq;
+      m.idx[p][k] = (unsigned char)q;
+      ++k;
+    }
+    m.nsrc[p] = (unsigned char)k;
+  }
+  fl_neighbor_mix(stacked, P, n, ld, m, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
 int myfyp_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, void* stream) {
   if (K < 1 || K > 16) {
     g_last_error = "coordinate_median supports 1..16 models";

@@ -163,6 +163,25 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
     if not local:
         fed.record("aggregate", time.perf_counter() - t0)
         return []
+    learners = [fed.local_nodes[a].learner for a in local]
+    group = _stacked_group(learners)
+    if fed.world == 1 and group is not None and group.params.is_cuda and group.capacity <= 16 and group.S % 4 == 0:
+        # every neighbour is a row of the same stacked engine buffer: the whole mixing step is one
+        # in-place kernel (row p <- Σ_q M[p, q] row q); no per-peer pack / average / unpack launches
+        mix = np.zeros((group.capacity, group.capacity), dtype=np.float32)
+        local_set = set(local)
+        for a, lr in zip(local, learners):
+            i = index[a]
+            nz = [j for j in np.nonzero(w[i])[0] if peers[j] in local_set]  # one rank: the sources are the local arrivals
+            ws = np.array([w[i, j] for j in nz], dtype=np.float64)
+            ws = ws / ws.sum()
+            for j, x in zip(nz, ws):
+                mix[lr._engine.slot, fed.local_nodes[peers[j]].learner._engine.slot] += x
+        stream = torch.cuda.current_stream(group.params.device).cuda_stream
+        ops.check(ops.fast_lib().myfyp_neighbor_mix_stacked(group.params.data_ptr(), group.capacity, group.numel, group.S, mix.ctypes.data, stream),
+                  "neighbor_mix")
+        fed.record("aggregate", time.perf_counter() - t0)
+        return local
     rows = {a: _pack(fed.local_nodes[a].learner) for a in local}
     ref = rows[local[0]]
     # point-to-point plan: every (local peer, remote rank) edge sends once; every remote neighbour is received once

@@ -76,6 +76,35 @@ def test_fedavg_stacked_local_and_split(dev, N, ld):
         torch.testing.assert_close(a[p, N:], st[p, N:])  # padding untouched
 
 
+@pytest.mark.parametrize("P", [3, 8, 16])
+def test_neighbor_mix_stacked(dev, P):
+    """In-place topology mixing of stacked rows == M @ rows in torch (ring + an idle row + a dead
+    neighbour renormalised away)."""
+    from myfyp_amd import ops
+
+    N, ld = 62006, 62016
+    st = torch.randn(P, ld, device=dev)
+    m = np.zeros((P, P), dtype=np.float32)
+    for p in range(P):
+        for q in {p, (p - 1) % P, (p + 1) % P}:
+            m[p, q] = 1.0
+    m[P - 1] = 0.0  # an idle row is left alone
+    if P > 3:
+        m[:, 2] = 0.0  # peer 2 died: nobody reads it
+        m[2, 2] = 1.0
+    m = m / np.maximum(m.sum(1, keepdims=True), 1e-12)
+    m[P - 1] = 0.0
+    ref = torch.from_numpy(m).to(dev).double() @ st.double()
+    a = st.clone()
+    ops.check(ops.fast_lib().myfyp_neighbor_mix_stacked(a.data_ptr(), P, N, ld, m.ctypes.data, torch.cuda.current_stream().cuda_stream), "mix")
+    torch.cuda.synchronize()
+    for p in range(P - 1):
+        torch.testing.assert_close(a[p, :N].double(), ref[p, :N], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(a[P - 1], st[P - 1])
+    bad = np.ones((17, 17), dtype=np.float32)
+    assert ops.fast_lib().myfyp_neighbor_mix_stacked(a.data_ptr(), 17, N, ld, bad.ctypes.data, torch.cuda.current_stream().cuda_stream) == 2
+
+
 @pytest.mark.parametrize("k", [1, 2, 5, 8, 16])
 def test_coordinate_median(dev, k):
     from myfyp_amd import ops
