@@ -15,9 +15,9 @@ void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_
 void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
 void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, unsigned long long mask, hipStream_t s);
 // Topology mixing of a stacked group in place: row p <- sum_k w[p][k] * row idx[p][k] (P <= 16 rows,
-// <= 8 sources per row; rows with nsrc == 0 are left alone).
+// up to P sources per row; rows with nsrc == 0 are left alone).
 #define MIX_MAX_PEERS 16
-#define MIX_MAX_SRC 8
+#define MIX_MAX_SRC MIX_MAX_PEERS  // a row may mix every local peer (full / star topologies)
 struct MixPlan {
   float w[MIX_MAX_PEERS][MIX_MAX_SRC];
   unsigned char idx[MIX_MAX_PEERS][MIX_MAX_SRC];

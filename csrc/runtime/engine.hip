@@ -400,7 +400,7 @@ int myfyp_neighbor_mix_stacked(float* stacked, int P, int64_t n, int64_t ld, con
       const float wq = w_host[p * P + q];
       if (wq == 0.f) continue;
       if (k == MIX_MAX_SRC) {
-        g_last_error = "neighbor_mix_stacked: more than 8 sources in a row";
+        g_last_error = "neighbor_mix_stacked: more sources in a row than MIX_MAX_SRC";
         return 2;
       }
       m.w[p][k] = wq;

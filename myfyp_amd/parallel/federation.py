@@ -31,6 +31,7 @@ import torch
 
 from myfyp_amd.management.logger import logger
 from myfyp_amd.settings import Settings
+from myfyp_amd.learning.frameworks.p2pfl_model import safe_loads
 from myfyp_amd.utils.lockcheck import make_lock
 
 
@@ -79,7 +80,8 @@ class StoreBus:
                     break
                 seq += 1
                 try:
-                    dest, kind, msg = pickle.loads(payload)
+                    # the TCPStore is unauthenticated: decode with the restricted unpickler
+                    dest, kind, msg = safe_loads(payload)
                     self._deliver(dest, kind, msg)
                 except Exception as e:  # never kill the listener
                     logger.error(f"rank{self.rank}", f"StoreBus delivery failed: {e}")

@@ -105,6 +105,22 @@ def test_neighbor_mix_stacked(dev, P):
     assert ops.fast_lib().myfyp_neighbor_mix_stacked(a.data_ptr(), 17, N, ld, bad.ctypes.data, torch.cuda.current_stream().cuda_stream) == 2
 
 
+@pytest.mark.parametrize("P", [10, 16])
+def test_neighbor_mix_stacked_full_topology(dev, P):
+    """Full / star topologies give a row more than 8 sources (Metropolis weights keep w_ii > 0):
+    the single-kernel mix must accept every local peer as a source."""
+    from myfyp_amd import ops
+
+    N, ld = 4099, 4100
+    st = torch.randn(P, ld, device=dev)
+    m = np.full((P, P), 1.0 / P, dtype=np.float32)
+    ref = torch.from_numpy(m).to(dev).double() @ st.double()
+    a = st.clone()
+    ops.check(ops.fast_lib().myfyp_neighbor_mix_stacked(a.data_ptr(), P, N, ld, m.ctypes.data, torch.cuda.current_stream().cuda_stream), "mix")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a[:, :N].double(), ref[:, :N], rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("k", [1, 2, 5, 8, 16])
 def test_coordinate_median(dev, k):
     from myfyp_amd import ops
