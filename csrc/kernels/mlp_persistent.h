@@ -21,3 +21,25 @@ hipError_t mlp_persistent_prepare(const MLPArgs& a);  // kernel attributes (once
 // Zero the flags (memset node) and launch one whole epoch for every active peer.
 // zero_flags = false: the epoch's gather kernel already zeroed them (MLPArgs::flags_zero).
 hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s, bool zero_flags = true);
+
+// ---- fp32 variant (mlp_persistent_f32.hip): exact fp32 products, fp32 accumulation and state;
+//      gangs of 16 owners + 8 heads, one launch per group of 8 peers.
+struct MLPPersistF32Bufs {
+  float* h1x;       // [P][Bpad][256]      owner g -> heads: H1 columns 16g..16g+15
+  float* plx;       // [P][8][Bpad][16]    head hd -> heads: partial logits over its H2 slice
+  float* dh2x;      // [P][2][Bpad][128]   head hd -> owners: dH2 columns 16hd..16hd+15 (step parity)
+  unsigned* flags;  // [P][32][32] one 128-B line per flag (16 H1, 8 PL, 8 dH2); zeroed per launch
+  size_t flag_bytes;
+  int* err;         // sticky give-up word (shared with the bf16 path)
+  float* w2chk;     // debug: owners' W2 replica after the epoch [P][128][256], or null
+};
+
+bool mlp_persistent_f32_supported(const MLPArgs& a);
+size_t mlp_persistent_f32_bytes(int P, int Bpad);
+size_t mlp_persistent_f32_flag_bytes(int P);
+int mlp_persistent_f32_gang();             // workgroups (CUs) per peer
+int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
+hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
+hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);
+// fp32 forward of every active peer's whole test split (loss sum, correct, confusion) in one launch
+void mlp_launch_eval_f32(const MLPArgs& a, int max_rows, hipStream_t s);

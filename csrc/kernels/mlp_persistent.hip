@@ -31,6 +31,7 @@
 // Placement: block b serves XCD slot b % 8, so the 17 workgroups of a gang share one XCD's L2 under
 // round-robin dispatch (speed only — the protocol does not depend on placement).
 #include "mlp_persistent.h"
+#include "persist_common.h"
 
 // Optional phase timestamps (build with -DMLP_STAMPS): peer 0's owner 0 and head, steps < 32,
 // read with mlp_debug_persistent_stamps (wall_clock64 ticks, 100 MHz).
@@ -51,32 +52,27 @@ extern "C" int mlp_debug_persistent_stamps(void* out) {
 
 namespace {
 
-typedef __attribute__((address_space(1))) unsigned gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
+using persist::gu32;
+using persist::gu64;
+using persist::ld_wt;
+using persist::row_max16;
+using persist::row_min16;
+using persist::row_sum16;
+using persist::st_wt;
+using persist::al16;
 
 constexpr int NT = 512;  // threads per workgroup (8 waves)
 constexpr int NG = 16;   // owners per peer (D1 / 16)
 constexpr int PD1 = 256, PD2 = 128;
 constexpr int ROLES = NG + 1;
-constexpr int FLAG_LINE = 32;  // u32 per flag: one 128-byte line each
 constexpr int FLAGS_PER_PEER = 2 * NG + 1;
 constexpr int F_H1 = 0, F_W2 = NG, F_DH2 = 2 * NG;
-constexpr unsigned long long SPIN_TICKS = 100000000ull;  // wall_clock64 runs at 100 MHz: 1 s
 constexpr int KS1_MAX = 32;                              // D0 <= 1024
 constexpr int LD2 = PD2 + 8;                             // bf16 row stride of [*][128] LDS tiles
 constexpr int LDH = PD1 + 8;                             // bf16 row stride of [*][256] LDS tiles
 constexpr int LDL = 40;                                  // dlogits [b][32 (classes, K-padded)] + 8
 constexpr int LDW3 = PD2 + 8;                            // W3 bf16 [32][128] + 8
 
-__device__ __forceinline__ unsigned* flag_at(unsigned* flags, int p, int idx) {
-  return flags + ((size_t)p * FLAGS_PER_PEER + idx) * FLAG_LINE;
-}
-__device__ __forceinline__ void st_wt(void* ptr, unsigned long long v) {  // 8-byte write-through store
-  __hip_atomic_store((gu64*)ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
-  return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }
 
 typedef short pe_s16x4 __attribute__((ext_vector_type(4)));
@@ -89,43 +85,11 @@ __device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// Producer side: every storing wave drains its write-through stores, the workgroup meets, ONE lane
-// stores the flag (sc1).
 __device__ __forceinline__ void publish(unsigned* flags, int p, int idx, unsigned value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag_at(flags, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  persist::publish(flags, FLAGS_PER_PEER, p, idx, value);
 }
-
-// Consumer side: wave 0 polls flags idx0..idx0+n-1 (one lane each, relaxed sc1 loads + s_sleep) until
-// all reach `target`, then the workgroup meets; every later load of the handed-off bytes is an sc1
-// load. Bounded: gives up after SPIN_TICKS or when another workgroup gave up.
-__device__ bool wg_wait(unsigned* flags, int p, int idx0, int n, unsigned target, int* err, int* sOk) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const unsigned* f = flag_at(flags, p, idx0 + (lane < n ? lane : 0));
-    const unsigned long long t0 = wall_clock64();
-    int ok = 1;
-    for (;;) {
-      const unsigned v = lane < n ? __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
-      if (__all(v >= target)) break;
-      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
-      }
-      if (wall_clock64() - t0 > SPIN_TICKS) {
-        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) *sOk = ok;
-  }
-  __syncthreads();
-  const int ok = *sOk;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
-  return ok != 0;
+__device__ __forceinline__ bool wg_wait(unsigned* flags, int p, int idx0, int n, unsigned target, int* err, int* sOk) {
+  return persist::wg_wait(flags, FLAGS_PER_PEER, p, idx0, n, target, err, sOk);
 }
 
 __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
@@ -133,11 +97,8 @@ __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
   return r < 0 ? 0 : (r > a.B ? a.B : r);
 }
 
-// Per-step optimizer constants: lr_t = lr / (1 - β1^t), inv = 1 / sqrt(1 - β2^t).
 __device__ __forceinline__ void bias_corr(const MLPArgs& a, int t0, int t, float& lr_t, float& inv) {
-  const int k = t0 + t + 1;
-  lr_t = a.opt.lr / (1.f - __powf(a.opt.beta1, (float)k));
-  inv = 1.f / sqrtf(1.f - __powf(a.opt.beta2, (float)k));
+  persist::bias_corr(a.opt, t0, t, lr_t, inv);
 }
 
 // torch.optim.Adam / SGD(no momentum) update in registers. The register-resident epilogue runs on
@@ -157,41 +118,11 @@ __device__ __forceinline__ void upd(const MLPArgs& a, float g, float& w, float& 
   }
 }
 
-// 16-lane (one MFMA row group) butterfly reductions on DPP: quad_perm xor1, xor2, then
-// row_half_mirror and row_mirror — VALU-latency instead of ds_bpermute round trips.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ float row_max16(float v) {
-  v = fmaxf(v, dpp_f<0xB1>(v));
-  v = fmaxf(v, dpp_f<0x4E>(v));
-  v = fmaxf(v, dpp_f<0x141>(v));
-  return fmaxf(v, dpp_f<0x140>(v));
-}
-__device__ __forceinline__ float row_sum16(float v) {
-  v += dpp_f<0xB1>(v);
-  v += dpp_f<0x4E>(v);
-  v += dpp_f<0x141>(v);
-  return v + dpp_f<0x140>(v);
-}
-__device__ __forceinline__ int row_min16(int v) {
-  v = min(v, dpp_i<0xB1>(v));
-  v = min(v, dpp_i<0x4E>(v));
-  v = min(v, dpp_i<0x141>(v));
-  return min(v, dpp_i<0x140>(v));
-}
-
 // ---- LDS carving (all offsets multiples of 16 bytes; dynamic region only: Guideline 17)
 struct OwnerLds {
   int ldx;  // bf16 row stride of the X tile
   size_t x, red, dh2, h1, dh1, w2g, b1, db1, ok, total;
 };
-__host__ __device__ inline size_t al16(size_t v) { return (v + 15) / 16 * 16; }
 __host__ __device__ inline OwnerLds owner_lds(int Bpad, int D0) {
   OwnerLds L;
   const int ks1 = (D0 + 31) / 32;
@@ -848,7 +779,7 @@ bool mlp_persistent_supported(const MLPArgs& a) {
 }
 
 size_t mlp_persistent_bytes(int P, int Bpad) { return (size_t)P * ((size_t)Bpad * PD1 + (size_t)PD2 * PD1 + (size_t)Bpad * PD2) * sizeof(bf16); }
-size_t mlp_persistent_flag_bytes(int P) { return (size_t)P * FLAGS_PER_PEER * FLAG_LINE * sizeof(unsigned); }
+size_t mlp_persistent_flag_bytes(int P) { return (size_t)P * FLAGS_PER_PEER * persist::FLAG_LINE * sizeof(unsigned); }
 int mlp_persistent_blocks(int P) { return 8 * ROLES * ((P + 7) / 8); }
 
 static size_t persistent_lds(const MLPArgs& a) {

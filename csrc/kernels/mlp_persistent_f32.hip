@@ -1,0 +1,1081 @@
+// fp32 weight-stationary persistent epoch kernel for the reference MLP (784-256-128-10) on gfx950,
+// plus the fp32 evaluation kernel. This is the precision of the reference: Lightning's default
+// fp32 Trainer with torch.optim.Adam (/root/reference/p2pfl/learning/frameworks/pytorch/
+// lightning_learner.py:82-89, lightning_model.py:181-183), uint8 pixels cast to float
+// (lightning_model.py:187).
+//
+// Arithmetic. Every product is an exact fp32 product and every sum an fp32 sum:
+//   * X·W1ᵀ (forward) and dH1ᵀ·X (dW1): X is uint8, so exact in bf16. The fp32 operand is split
+//     EXACTLY into three bf16 terms (hi + mid + lo carry its 24 significand bits, split3 below),
+//     so three v_mfma_f32_16x16x32_bf16 against the exact-bf16 X give exact products accumulated
+//     in fp32 — at 3/16 of the cost of the f32-input MFMA for the two 12.5k-element GEMMs that
+//     dominate the step.
+//   * every other GEMM (H2, logits, dH2, dH1, dW2, dW3, bias column sums) runs on
+//     v_mfma_f32_16x16x4_f32: f32 in, f32 accumulate, bit-for-bit a k-ordered fmaf chain
+//     (cdna_hip_programming.md §3 'FP32-input MFMA').
+//   * fp32 master weights and Adam moments live in registers for the whole epoch, hand-offs are
+//     fp32.
+//
+// Gang of one peer: 24 workgroups of 512 threads, one per CU, alive for the whole epoch.
+//   owner g (g < 16): W1 rows 16g..16g+15 (+ b1 slice) in the fragment layout of the MFMAs that
+//       use them (as mlp_persistent.hip: the K-slot permutation κ puts each weight's gradient in
+//       the lane/register that holds the weight), the batch tile in LDS; computes the H1 slice,
+//       dH1 slice, dW1 rows; keeps a REPLICA of W2 columns 16g..16g+15 for dH1.
+//   head hd (hd < 8): W2 rows 16hd..16hd+15 (all 256 inputs), b2 slice, W3 columns 16hd..+16,
+//       a replica of b3; computes the H2 slice, partial logits, (redundantly) the log-softmax +
+//       NLL + dlogits of the whole batch, the dH2 slice, dW2 rows, dW3 slice, db2, db3.
+// The W2 replica in the owners is updated from its own dW2 tile, computed with the SAME k-ordered
+// f32 MFMA chain over the batch as the head's, and the same optimizer code: it stays bit-identical
+// to the head's rows with no W2 traffic at all (checked by a GPU test through `w2chk`).
+//
+// Per step three hand-offs, all write-through (sc1) stores + drained flag + sc1 loads
+// (persist_common.h): H1 slices owners → heads (16 × 4 KB), partial logits head ↔ head (8 × 4 KB),
+// dH2 slices heads → owners (8 × 4 KB, double-buffered by step parity because the owners re-read
+// the previous step's tile for their deferred W2-replica update).
+#include "mlp_persistent.h"
+#include "persist_common.h"
+
+namespace {
+
+using persist::al16;
+using persist::gu32;
+using persist::row_max16;
+using persist::row_min16;
+using persist::row_sum16;
+using persist::st_wt32;
+
+constexpr int NT = 512;  // threads per workgroup (8 waves)
+constexpr int NG = 16;   // owners per peer (D1 / 16)
+constexpr int NH = 8;    // heads per peer (D2 / 16)
+constexpr int ROLES = NG + NH;
+constexpr int PD1 = 256, PD2 = 128;
+constexpr int FPP = NG + 2 * NH;  // flags per peer
+constexpr int F_H1 = 0, F_PL = NG, F_DH2 = NG + NH;
+constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 799
+
+// K steps of the W1 GEMMs: D0 columns plus at least one padding column, column D0, which carries
+// b1: the X tile holds 1 there for valid rows, so the forward MFMAs add b1 and the dW1 MFMAs
+// produce db1 in the register slot that holds b1 (no separate bias add, sum or update).
+__host__ __device__ inline int ks1_of(int D0) { return D0 / 32 + 1; }
+constexpr int LDD = PD2 + 4;   // fp32 row stride of the owner's dH2 tile [B][128]
+constexpr int LDH1 = PD1 + 4;  // fp32 row stride of the head's H1 tile [B][256]
+constexpr int LD16 = 20;       // fp32 row stride of [*][16] tiles
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_f32(float a, float b, const f32x4& c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }
+__device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
+__device__ __forceinline__ float ld_wt32(const float* p) {  // 4-byte L1-bypassing (sc1) load
+  return __builtin_bit_cast(float, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ float4 as_f4(const u32x4& v) { return __builtin_bit_cast(float4, v); }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+// 16-byte sc1 load (L1 bypass) of a handed-off tile
+__device__ __forceinline__ float4 ld_sc1_16(__amdgpu_buffer_rsrc_t r, int byte_off) { return as_f4(__builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16)); }
+
+// frag_b_tr (common.h) with the lane index passed in (a per-step laundered copy)
+__device__ __forceinline__ bf16x8 frag_b_tr_l(const bf16* base, int ld, int k0, int n0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const bf16* p0 = base + (k0 + 8 * g + q) * ld + n0 + 4 * pp;
+  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
+  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0 + 4 * ld));
+  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// Exact split of fp32 values into three bf16 terms: x == hi + mid + lo. hi = RNE(x) leaves a
+// remainder that is a multiple of x's 24-bit ulp below 2^16 ulps, mid takes its top 8 bits and lo
+// the last <= 8 (both subtractions are exact), so the three terms carry all 24 significand bits.
+__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bf16 a = (bf16)x[j];
+    const float r = x[j] - (float)a;
+    const bf16 b = (bf16)r;
+    hi[j] = a;
+    mid[j] = b;
+    lo[j] = (bf16)(r - (float)b);
+  }
+}
+// acc += A · (hi + mid + lo), smallest terms first
+__device__ __forceinline__ f32x4 mfma3(const bf16x8& a, const bf16x8& hi, const bf16x8& mid, const bf16x8& lo, f32x4 acc) {
+  acc = mfma_bf16(a, lo, acc);
+  acc = mfma_bf16(a, mid, acc);
+  return mfma_bf16(a, hi, acc);
+}
+
+// Per-element constant of the FedProx / SCAFFOLD gradient terms: g += mu·(w − anchor) + (c − c_i)
+// is g += mu·w + e with e = (c − c_i) − mu·anchor (the mu·w part is folded into weight decay).
+__device__ __forceinline__ float extra_at(const MLPArgs& a, int64_t idx) {
+  float e = 0.f;
+  if (a.cg != nullptr) e = a.cg[idx] - a.cl[idx];
+  if (a.anchor != nullptr) e = fmaf(-a.opt.mu, a.anchor[idx], e);
+  return e;
+}
+
+// torch.optim.Adam / SGD(+momentum, nesterov) update of one register-resident element. The same
+// code updates the head's W2 rows and the owners' W2 replica: identical inputs give identical bits.
+template <bool ADAM, bool EXTRA>
+__device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, float& m, float& v, float e, float lr_t, float inv, float wdmu) {
+  g = fmaf(wdmu, w, g);  // weight decay (+ FedProx mu); 0: exact no-op
+  if (EXTRA) g += e;
+  if (ADAM) {
+    m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
+    v = fmaf(o.beta2, v, (1.f - o.beta2) * (g * g));
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv, o.eps);
+    w = fmaf(-lr_t, m * __builtin_amdgcn_rcpf(denom), w);
+  } else {
+    if (o.momentum != 0.f) {
+      m = fmaf(o.momentum, m, g);
+      g = o.nesterov ? fmaf(o.momentum, m, g) : m;
+    }
+    w = fmaf(-o.lr, g, w);
+  }
+}
+
+__device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
+  const int r = n - t * a.B;
+  return r < 0 ? 0 : (r > a.B ? a.B : r);
+}
+
+// ---- LDS carving (16-byte aligned offsets)
+struct OwnerLds32 {
+  int ldx;  // bf16 row stride of the X tile
+  int ldt;  // bf16 row stride of the transposed dH1 split tiles [3][16][B]
+  size_t x, red, h1, dh1s, w1x, ok, total;
+};
+__host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0) {
+  OwnerLds32 L;
+  const int ks1 = ks1_of(D0);
+  L.ldx = ks1 * 32 + 8;
+  L.ldt = Bpad + 8;
+  const int MT = Bpad / 16;
+  const size_t red = (size_t)8 * MT * 64 * 16, dh2 = (size_t)Bpad * LDD * 4;
+  size_t o = 0;
+  L.x = o;    o += al16((size_t)Bpad * L.ldx * 2);
+  L.red = o;  o += al16(red > dh2 ? red : dh2);  // cross-wave partials, overlaid by the dH2 tile
+  L.h1 = o;   o += al16((size_t)2 * Bpad * 16 * 4);  // own H1 slice, step-parity double buffer
+  L.dh1s = o; o += al16((size_t)3 * 16 * L.ldt * 2);  // dH1ᵀ as hi / mid / lo bf16 (exact split)
+  L.w1x = o;  o += al16((size_t)4 * 16 * 32 * 4);     // W1 state of K step 24 (w, m, v, e)
+  L.ok = o;   o += 16;
+  L.total = o;
+  return L;
+}
+struct HeadLds32 {
+  size_t h1, red, h2, lg, dlog, dh2, w3, b2, b3, ok, total;
+};
+__host__ __device__ inline HeadLds32 head_lds32(int Bpad) {
+  HeadLds32 L;
+  const int MT = Bpad / 16;
+  size_t o = 0;
+  L.h1 = o;   o += al16((size_t)Bpad * LDH1 * 4);
+  L.red = o;  o += al16((size_t)8 * MT * 64 * 16);
+  L.h2 = o;   o += al16((size_t)Bpad * LD16 * 4);
+  L.lg = o;   o += al16((size_t)Bpad * LD16 * 4);
+  L.dlog = o; o += al16((size_t)Bpad * LD16 * 4);
+  L.dh2 = o;  o += al16((size_t)Bpad * LD16 * 4);
+  L.w3 = o;   o += al16((size_t)16 * LD16 * 4);
+  L.b2 = o;   o += al16(4 * 16 * 4);
+  L.b3 = o;   o += al16(4 * 16 * 4);
+  L.ok = o;   o += 16;
+  L.total = o;
+  return L;
+}
+
+// =============================================================================================
+// owner workgroup
+// =============================================================================================
+// W1 state of one K step (16 rows × 32 columns, κ slot order) for the lanes of a wave, kept either in
+// registers (K steps < 24: three per wave) or, for K step 24 (wave 0, D0 > 767), in LDS: four
+// register slots per wave would not fit beside the working set of two waves per SIMD.
+constexpr int RQ = 3;  // register-resident K steps per wave
+
+template <int BP, bool ADAM, bool EXTRA>
+__device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem) {
+  constexpr int MT = BP / 16;
+  constexpr int XPT = BP / 4;  // 16-byte X chunks per lane: 4 K steps x BP rows x 4 chunks / 64 lanes
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int D0 = a.D0, KS1 = ks1_of(D0);
+  const OwnerLds32 L = owner_lds32(BP, D0);
+  const int LDX = L.ldx, LDT = L.ldt;
+  bf16* sX = reinterpret_cast<bf16*>(smem + L.x);
+  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
+  float* sDH2 = reinterpret_cast<float*>(smem + L.red);
+  float* sH1 = reinterpret_cast<float*>(smem + L.h1);
+  bf16* sD3 = reinterpret_cast<bf16*>(smem + L.dh1s);  // [hi, mid, lo][o1 local][b]
+  float* sW1x = reinterpret_cast<float*>(smem + L.w1x);  // [w, m, v, e][16][32]: K step 24
+  int* sOk = reinterpret_cast<int*>(smem + L.ok);
+
+  const OptParams& o = a.opt;
+  const int4 ctl = a.ctl[p];
+  const bool fresh = (ctl.x & 2) != 0;
+  const int n = ctl.y;
+  const int nsteps = (n + a.B - 1) / a.B;
+  const int64_t pS = (int64_t)p * a.S;
+  const float wdmu = o.weight_decay + (a.anchor != nullptr ? o.mu : 0.f);
+
+  // ---- resident W1 rows: wave w owns K steps w, w+8, w+16 (registers) and w+24 (LDS), κ slot
+  //      order; the slot of column D0 holds b1
+  float w1[RQ][8], m1[RQ][8], v1[RQ][8], e1[RQ][8];
+  const int orow = NG * g + c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int s = wave + 8 * q;
+    if (q == RQ && s >= KS1) break;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int k = 32 * s + 16 * half + 4 * h;
+      float4 wv = {0.f, 0.f, 0.f, 0.f}, mv = wv, vv = wv, ev = wv;
+      if (s < KS1 && k < D0) {
+        const int64_t idx = pS + a.off_w1 + (int64_t)orow * D0 + k;
+        wv = *reinterpret_cast<const float4*>(a.params + idx);
+        if (!fresh) {
+          mv = *reinterpret_cast<const float4*>(a.m + idx);
+          if (ADAM) vv = *reinterpret_cast<const float4*>(a.v + idx);
+        }
+        if (EXTRA) ev = float4{extra_at(a, idx), extra_at(a, idx + 1), extra_at(a, idx + 2), extra_at(a, idx + 3)};
+      } else if (s < KS1 && k == D0) {  // the bias column
+        const int64_t idx = pS + a.off_b1 + orow;
+        wv.x = a.params[idx];
+        if (!fresh) {
+          mv.x = a.m[idx];
+          if (ADAM) vv.x = a.v[idx];
+        }
+        if (EXTRA) ev.x = extra_at(a, idx);
+      }
+      if (q < RQ) {
+        const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w},
+                    ea[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          w1[q][4 * half + i] = wa[i];
+          m1[q][4 * half + i] = ma[i];
+          v1[q][4 * half + i] = va[i];
+          e1[q][4 * half + i] = ea[i];
+        }
+      } else {
+        const int off = c * 32 + 16 * half + 4 * h;
+        *reinterpret_cast<float4*>(sW1x + off) = wv;
+        *reinterpret_cast<float4*>(sW1x + 512 + off) = mv;
+        *reinterpret_cast<float4*>(sW1x + 1024 + off) = vv;
+        *reinterpret_cast<float4*>(sW1x + 1536 + off) = ev;
+      }
+    }
+  }
+  // ---- W2 replica: wave w holds W2[16w + 4h + i][16g + c] — the lane layout of its dW2 tile and,
+  //      with the k order o2 = 16w + 4h + ks, the B fragment of its dH1 MFMAs
+  float w2c[4], m2c[4], v2c[4], e2c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t idx = pS + a.off_w2 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NG * g + c;
+    w2c[i] = a.params[idx];
+    m2c[i] = fresh ? 0.f : a.m[idx];
+    v2c[i] = (ADAM && !fresh) ? a.v[idx] : 0.f;
+    e2c[i] = EXTRA ? extra_at(a, idx) : 0.f;
+  }
+
+  // ---- X staging (each wave stages only its own K-step columns; see mlp_persistent.hip); the
+  //      chunk at column D0 carries the bias input: 1 for valid rows, 0 beyond the batch
+  auto bias_chunk = [](bool valid) { return uint4{valid ? 0x3F80u : 0u, 0u, 0u, 0u}; };  // bf16 1.0
+  auto xw_stage = [&](int t, int lv) {
+    const int rows = rows_at(a, n, t);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = k / (BP / 16), kk = k % (BP / 16);
+      const int s = wave + 8 * q;
+      const int idx = kk * 64 + lv;
+      const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+      if (s < KS1 && col < D0) {
+        const bf16* src = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + col;
+        *reinterpret_cast<uint4*>(sX + r * LDX + col) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
+      } else if (s < KS1 && col == D0) {
+        *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows);
+      }
+    }
+  };
+  for (int e = tid; e < BP * (KS1 * 32 - D0); e += NT) {
+    const int r = e / (KS1 * 32 - D0), q = e % (KS1 * 32 - D0);
+    sX[r * LDX + D0 + q] = (bf16)0.f;
+  }
+  if (nsteps > 0) xw_stage(0, lane);
+
+  // deferred W2-replica update of step tp: dW2[o2][16g + c] over the batch, with dH2(tp) re-read
+  // (sc1) from the step-parity buffer and H1(tp) from this workgroup's LDS
+  auto w2_replica_update = [&](int tp) {
+    const float* dh2 = pb.dh2x + ((int64_t)p * 2 + (tp & 1)) * BP * PD2;
+    const float* h1p = sH1 + (tp & 1) * BP * 16;
+    float av[BP / 4];
+#pragma unroll
+    for (int kb = 0; kb < BP / 4; ++kb) av[kb] = ld_wt32(dh2 + (4 * kb + h) * PD2 + 16 * wave + c);
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(av[kb], h1p[(4 * kb + h) * 16 + c], acc);
+    float lr_p, inv_p;
+    persist::bias_corr(o, ctl.z, tp, lr_p, inv_p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, acc[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_p, inv_p, wdmu);
+  };
+  __syncthreads();  // sW1x written
+
+  for (int t = 0; t < nsteps; ++t) {
+    int tv = tid;  // per-iteration opaque thread index (addresses re-derived each step: VGPR pressure)
+    asm volatile("" : "+v"(tv));
+    const int rows = rows_at(a, n, t);
+    float lr_t, inv_bc2;
+    persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
+    float* sH1c = sH1 + (t & 1) * BP * 16;
+
+    // ================= A: H1 slice = relu(X · W1sliceᵀ + b1), split-K over the 8 waves
+    {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        if (s < KS1) {
+          // lane coordinates laundered per K step: the compiler would otherwise hoist every LDS
+          // address of the loop out of it and spill them
+          int lq = lane;
+          asm volatile("" : "+v"(lq));
+          const int hq = lq >> 4, cq = lq & 15;
+          float wq[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wq[j] = q < RQ ? w1[q < RQ ? q : 0][j] : sW1x[cq * 32 + kappa(hq, j)];
+          bf16x8 bh, bm, bl;
+          split3(wq, bh, bm, bl);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * hq;
+            const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
+            acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc[mt];
+    }
+    lds_barrier();
+    if (tid < MT * 64) {
+      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
+      f32x4 s = sRed[mt * 64 + (tid & 63)];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * mt + 4 * hh + i;
+        const float v = b < rows ? fmaxf(s[i], 0.f) : 0.f;  // b1 came in through the bias column
+        sH1c[b * 16 + cc] = v;
+        st_wt32(pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + cc, v);
+      }
+    }
+    persist::publish(pb.flags, FPP, p, F_H1 + g, (unsigned)(t + 1));
+
+    // the previous step's W2-replica update runs while the heads work on this step's H1
+    if (t > 0) w2_replica_update(t - 1);
+
+    // next step's batch: pull this wave's columns into the XCD's L2 (staged after the dW1 MFMAs)
+    const bool more = t + 1 < nsteps;
+    if (more) {
+      const int rows_n = rows_at(a, n, t + 1);
+      unsigned sink = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        const int r = lane;
+        if (s < KS1 && 32 * s < D0 && r < rows_n && r < BP)
+          sink ^= *reinterpret_cast<const unsigned*>(a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B + r) * D0 + 32 * s);
+      }
+      asm volatile("" ::"v"(sink));
+    }
+
+    // ================= C: backward of this slice
+    if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    {
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2, BP * PD2 * 4);
+      float4 v[BP / 16];
+#pragma unroll
+      for (int k = 0; k < BP / 16; ++k) v[k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 128 fp32 = BP*32 chunks
+#pragma unroll
+      for (int k = 0; k < BP / 16; ++k) {
+        const int e = tv + NT * k;
+        *reinterpret_cast<float4*>(sDH2 + (e >> 5) * LDD + 4 * (e & 31)) = v[k];
+      }
+    }
+    lds_barrier();
+    // C1: dH1 partials — wave w sums its 16 o2 rows (k order o2 = 16w + 4h + ks)
+    {
+      f32x4 acc1[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float4 av = *reinterpret_cast<const float4*>(sDH2 + (16 * mt + c) * LDD + 16 * wave + 4 * h);
+        f32x4 acc = mfma_f32(av.x, w2c[0], zero4());
+        acc = mfma_f32(av.y, w2c[1], acc);
+        acc = mfma_f32(av.z, w2c[2], acc);
+        acc1[mt] = mfma_f32(av.w, w2c[3], acc);
+      }
+      lds_barrier();  // every wave has read its dH2 fragments before the partials overwrite them
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc1[mt];
+    }
+    lds_barrier();
+    if (tid < MT * 64) {
+      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
+      f32x4 s = sRed[mt * 64 + (tid & 63)];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      bf16x4 dh, dm, dl;  // exact three-term split of dH1 (the B operand of the dW1 MFMAs)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = sH1c[(16 * mt + 4 * hh + i) * 16 + cc] > 0.f ? s[i] : 0.f;
+        const bf16 x0 = (bf16)d;
+        const float r = d - (float)x0;
+        const bf16 x1 = (bf16)r;
+        dh[i] = x0;
+        dm[i] = x1;
+        dl[i] = (bf16)(r - (float)x1);
+      }
+      const int off = cc * LDT + 16 * mt + 4 * hh;
+      *reinterpret_cast<bf16x4*>(sD3 + off) = dh;
+      *reinterpret_cast<bf16x4*>(sD3 + 16 * LDT + off) = dm;
+      *reinterpret_cast<bf16x4*>(sD3 + 32 * LDT + off) = dl;
+    }
+    lds_barrier();
+    // C2 (every wave, its own K steps): dW1 rows (and db1, in the bias slot) against the exact
+    // three-term split of dH1, W1 update, the next batch's columns staged right after this K
+    // step's reads
+    {
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
+      const int rows_next = more ? rows_at(a, n, t + 1) : 0;
+      const bf16* xnext = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = wave + 8 * q;
+        __builtin_amdgcn_sched_barrier(0);
+        if (s < KS1) {
+          int lq = lane;
+          asm volatile("" : "+v"(lq));
+          const bf16* dfrag = sD3 + (lq & 15) * LDT + 8 * (lq >> 4);
+          constexpr int XQ = BP / 16;
+          uint4 xq[XQ];
+#pragma unroll
+          for (int kk = 0; kk < XQ; ++kk) {
+            const int idx = kk * 64 + lv;
+            const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+            xq[kk] = (more && col < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + col)) : uint4{0u, 0u, 0u, 0u};
+          }
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            f32x4 acc = zero4();  // C[k = 32s + 16tt + 4h + i][o1 = c]
+#pragma unroll
+            for (int kb = 0; kb < BP / 32; ++kb)
+              acc = mfma3(frag_b_tr_l(sX, LDX, 32 * kb, 32 * s + 16 * tt, lq), ld8(dfrag + 32 * kb), ld8(dfrag + 16 * LDT + 32 * kb),
+                          ld8(dfrag + 32 * LDT + 32 * kb), acc);
+            if (q < RQ) {
+              const int qq = q < RQ ? q : 0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                upd32<ADAM, EXTRA>(o, acc[i], w1[qq][4 * tt + i], m1[qq][4 * tt + i], v1[qq][4 * tt + i], e1[qq][4 * tt + i], lr_t, inv_bc2, wdmu);
+            } else {  // the LDS-resident K step
+              const int off = (lq & 15) * 32 + 16 * tt + 4 * (lq >> 4);
+              float4 w = *reinterpret_cast<float4*>(sW1x + off), m = *reinterpret_cast<float4*>(sW1x + 512 + off),
+                     v = *reinterpret_cast<float4*>(sW1x + 1024 + off), e = *reinterpret_cast<float4*>(sW1x + 1536 + off);
+              upd32<ADAM, EXTRA>(o, acc[0], w.x, m.x, v.x, e.x, lr_t, inv_bc2, wdmu);
+              upd32<ADAM, EXTRA>(o, acc[1], w.y, m.y, v.y, e.y, lr_t, inv_bc2, wdmu);
+              upd32<ADAM, EXTRA>(o, acc[2], w.z, m.z, v.z, e.z, lr_t, inv_bc2, wdmu);
+              upd32<ADAM, EXTRA>(o, acc[3], w.w, m.w, v.w, e.w, lr_t, inv_bc2, wdmu);
+              *reinterpret_cast<float4*>(sW1x + off) = w;
+              *reinterpret_cast<float4*>(sW1x + 512 + off) = m;
+              *reinterpret_cast<float4*>(sW1x + 1024 + off) = v;
+            }
+          }
+          if (more) {
+#pragma unroll
+            for (int kk = 0; kk < XQ; ++kk) {
+              const int idx = kk * 64 + lv;
+              const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+              if (col < D0)
+                *reinterpret_cast<uint4*>(sX + r * LDX + col) = xq[kk];
+              else if (col == D0)
+                *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows_next);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- write the state back (fp32 master weights and moments; b1 from the bias slot)
+  int orow_w = orow;
+  int64_t pS_w = pS;
+  asm volatile("" : "+v"(orow_w), "+s"(pS_w));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int s = wave + 8 * q;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int k = 32 * s + 16 * half + 4 * h;
+      if (s >= KS1 || k > D0) continue;
+      float4 w, m, v;
+      if (q < RQ) {
+        const int qq = q < RQ ? q : 0;
+        const int j0 = 4 * half;
+        w = float4{w1[qq][j0], w1[qq][j0 + 1], w1[qq][j0 + 2], w1[qq][j0 + 3]};
+        m = float4{m1[qq][j0], m1[qq][j0 + 1], m1[qq][j0 + 2], m1[qq][j0 + 3]};
+        v = float4{v1[qq][j0], v1[qq][j0 + 1], v1[qq][j0 + 2], v1[qq][j0 + 3]};
+      } else {
+        const int off = c * 32 + 16 * half + 4 * h;
+        w = *reinterpret_cast<float4*>(sW1x + off);
+        m = *reinterpret_cast<float4*>(sW1x + 512 + off);
+        v = *reinterpret_cast<float4*>(sW1x + 1024 + off);
+      }
+      if (k < D0) {
+        const int64_t idx = pS_w + a.off_w1 + (int64_t)orow_w * D0 + k;
+        *reinterpret_cast<float4*>(a.params + idx) = w;
+        *reinterpret_cast<float4*>(a.m + idx) = m;
+        if (ADAM) *reinterpret_cast<float4*>(a.v + idx) = v;
+      } else {  // k == D0: b1 from the bias slot
+        const int64_t idx = pS_w + a.off_b1 + orow_w;
+        a.params[idx] = w.x;
+        a.m[idx] = m.x;
+        if (ADAM) a.v[idx] = v.x;
+      }
+    }
+  }
+  if (pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
+    if (nsteps > 0) w2_replica_update(nsteps - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NG * g + c] = w2c[i];
+  }
+}
+
+// =============================================================================================
+// head workgroup
+// =============================================================================================
+template <int BP, bool ADAM, bool EXTRA>
+__device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int hd, char* smem) {
+  constexpr int MT = BP / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int D3 = a.D3;
+  const HeadLds32 L = head_lds32(BP);
+  float* sH1 = reinterpret_cast<float*>(smem + L.h1);
+  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
+  float* sH2 = reinterpret_cast<float*>(smem + L.h2);
+  float* sLg = reinterpret_cast<float*>(smem + L.lg);
+  float* sDlog = reinterpret_cast<float*>(smem + L.dlog);
+  float* sDH2 = reinterpret_cast<float*>(smem + L.dh2);
+  float* sW3 = reinterpret_cast<float*>(smem + L.w3);  // [class][o2 local]
+  float* sB2 = reinterpret_cast<float*>(smem + L.b2);  // [4][16] w, m, v, e
+  float* sB3 = reinterpret_cast<float*>(smem + L.b3);  // [4][16] (replicated in every head)
+  int* sOk = reinterpret_cast<int*>(smem + L.ok);
+
+  const OptParams& o = a.opt;
+  const int4 ctl = a.ctl[p];
+  const bool fresh = (ctl.x & 2) != 0;
+  const int n = ctl.y;
+  const int nsteps = (n + a.B - 1) / a.B;
+  const int64_t pS = (int64_t)p * a.S;
+  const float wdmu = o.weight_decay + (a.anchor != nullptr ? o.mu : 0.f);
+  const bool cin = c < D3;
+  const int o2 = 16 * hd + c;  // this lane's W2 row
+
+  // ---- W2 rows: w2[gg][i] = W2[16hd + c][16g + 4h + i], g = 2·wave + gg
+  float w2[2][4], m2[2][4], v2[2][4], e2[2][4];
+#pragma unroll
+  for (int gg = 0; gg < 2; ++gg) {
+    const int64_t idx = pS + a.off_w2 + (int64_t)o2 * PD1 + 16 * (2 * wave + gg) + 4 * h;
+    const float4 wv = *reinterpret_cast<const float4*>(a.params + idx);
+    float4 mv = {0.f, 0.f, 0.f, 0.f}, vv = mv;
+    if (!fresh) {
+      mv = *reinterpret_cast<const float4*>(a.m + idx);
+      if (ADAM) vv = *reinterpret_cast<const float4*>(a.v + idx);
+    }
+    const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w2[gg][i] = wa[i];
+      m2[gg][i] = ma[i];
+      v2[gg][i] = va[i];
+      e2[gg][i] = EXTRA ? extra_at(a, idx + i) : 0.f;
+    }
+  }
+  // ---- W3 slice (wave 0): w3[i] = W3[c][16hd + 4h + i] — the lane layout of the dW3 tile
+  float w3[4] = {0.f, 0.f, 0.f, 0.f}, m3[4] = {0.f, 0.f, 0.f, 0.f}, v3[4] = {0.f, 0.f, 0.f, 0.f}, e3[4] = {0.f, 0.f, 0.f, 0.f};
+  if (wave == 0 && cin) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = pS + a.off_w3 + (int64_t)c * PD2 + 16 * hd + 4 * h + i;
+      w3[i] = a.params[idx];
+      m3[i] = fresh ? 0.f : a.m[idx];
+      v3[i] = (ADAM && !fresh) ? a.v[idx] : 0.f;
+      e3[i] = EXTRA ? extra_at(a, idx) : 0.f;
+    }
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sW3[c * LD16 + 4 * h + i] = w3[i];
+  }
+  if (tid < 16) {
+    const int64_t idx = pS + a.off_b2 + 16 * hd + tid;
+    sB2[tid] = a.params[idx];
+    sB2[16 + tid] = fresh ? 0.f : a.m[idx];
+    sB2[32 + tid] = (ADAM && !fresh) ? a.v[idx] : 0.f;
+    sB2[48 + tid] = EXTRA ? extra_at(a, idx) : 0.f;
+  } else if (tid >= 64 && tid < 80) {
+    const int k = tid - 64;
+    const int64_t idx = pS + a.off_b3 + k;
+    const bool kin = k < D3;
+    sB3[k] = kin ? a.params[idx] : 0.f;
+    sB3[16 + k] = (kin && !fresh) ? a.m[idx] : 0.f;
+    sB3[32 + k] = (kin && ADAM && !fresh) ? a.v[idx] : 0.f;
+    sB3[48 + k] = (kin && EXTRA) ? extra_at(a, idx) : 0.f;
+  }
+  __syncthreads();
+  float loss_acc = 0.f, correct_acc = 0.f;
+
+  for (int t = 0; t < nsteps; ++t) {
+    int tv = tid;
+    asm volatile("" : "+v"(tv));
+    const int rows = rows_at(a, n, t);
+    float lr_t, inv_bc2;
+    persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
+
+    // ---- H1(t) from the 16 owners -> LDS (16-byte sc1 loads)
+    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
+    {
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + (int64_t)p * BP * PD1, BP * PD1 * 4);
+      float4 v[BP / 8];
+#pragma unroll
+      for (int k = 0; k < BP / 8; ++k) v[k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 256 fp32 = BP*64 chunks
+#pragma unroll
+      for (int k = 0; k < BP / 8; ++k) {
+        const int e = tv + NT * k;
+        *reinterpret_cast<float4*>(sH1 + (e >> 6) * LDH1 + 4 * (e & 63)) = v[k];
+      }
+    }
+    lds_barrier();
+    // ---- H2 slice = relu(H1 · W2rowsᵀ + b2); wave w sums o1 in [32w, 32w+32) (k order 16g + 4h + i)
+    {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int g = 2 * wave + gg;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float4 av = *reinterpret_cast<const float4*>(sH1 + (16 * mt + c) * LDH1 + 16 * g + 4 * h);
+          acc[mt] = mfma_f32(av.x, w2[gg][0], acc[mt]);
+          acc[mt] = mfma_f32(av.y, w2[gg][1], acc[mt]);
+          acc[mt] = mfma_f32(av.z, w2[gg][2], acc[mt]);
+          acc[mt] = mfma_f32(av.w, w2[gg][3], acc[mt]);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc[mt];
+    }
+    lds_barrier();
+    if (tid < MT * 64) {
+      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
+      f32x4 s = sRed[mt * 64 + (tid & 63)];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      const float bias = sB2[cc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * mt + 4 * hh + i;
+        sH2[b * LD16 + cc] = b < rows ? fmaxf(s[i] + bias, 0.f) : 0.f;
+      }
+    }
+    lds_barrier();
+    // ---- partial logits of this slice (wave w < MT: rows 16w..16w+15; k order o2 = 4h + ks)
+    if (wave < MT) {
+      const float4 av = *reinterpret_cast<const float4*>(sH2 + (16 * wave + c) * LD16 + 4 * h);
+      const float4 bv = *reinterpret_cast<const float4*>(sW3 + c * LD16 + 4 * h);
+      f32x4 pl = mfma_f32(av.x, bv.x, zero4());
+      pl = mfma_f32(av.y, bv.y, pl);
+      pl = mfma_f32(av.z, bv.z, pl);
+      pl = mfma_f32(av.w, bv.w, pl);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st_wt32(pb.plx + (((int64_t)p * NH + hd) * BP + 16 * wave + 4 * h + i) * 16 + c, pl[i]);
+    }
+    persist::publish(pb.flags, FPP, p, F_PL + hd, (unsigned)(t + 1));
+
+    // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3
+    if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (tid < BP * 4) {
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16, NH * BP * 16 * 4);
+      float4 v[NH];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) v[k] = ld_sc1_16(r, (k * BP * 16 + 4 * tv) * 4);
+      float4 s = v[0];
+#pragma unroll
+      for (int k = 1; k < NH; ++k) {
+        s.x += v[k].x;
+        s.y += v[k].y;
+        s.z += v[k].z;
+        s.w += v[k].w;
+      }
+      *reinterpret_cast<float4*>(sLg + (tv >> 2) * LD16 + 4 * (tv & 3)) = s;
+    }
+    lds_barrier();
+    // ---- log-softmax + NLL + argmax + dlogits of the whole batch (wave w < MT: rows 16w..)
+    if (wave < MT) {
+      const float b3 = sB3[c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * wave + 4 * h + i;
+        const bool rvalid = b < rows;
+        const int y = rvalid ? a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b] : -1;
+        const float logit = cin ? sLg[b * LD16 + c] + b3 : -INFINITY;
+        const float mx = row_max16(logit);
+        const float se = row_sum16(cin ? expf(logit - mx) : 0.f);
+        const float logp = logit - (mx + logf(se));
+        const int cand = row_min16((cin && logit == mx) ? c : 16);
+        if (rvalid && c == y) loss_acc -= logp;
+        if (rvalid && c == 0) correct_acc += (cand == y) ? 1.f : 0.f;
+        // dlogits: p_c / rows, and for the true class −Σ_{c≠y} p_c / rows rather than (p_y − 1) / rows,
+        // which cancels catastrophically on confident rows (p_y → 1). This is the value the
+        // reference's fp32 autograd produces through its log_softmax + cross_entropy pair
+        // (lightning_model.py:178, :189): scripts/probes/f32_softmax_cancel.py.
+        const float pc = cin ? expf(logp) : 0.f;
+        const float others = row_sum16(c != y ? pc : 0.f);
+        sDlog[b * LD16 + c] = (rvalid && cin) ? (c == y ? -others : pc) / (float)rows : 0.f;
+      }
+    }
+    lds_barrier();
+    // ---- dH2 slice = dlogits · W3[:, slice] ⊙ [H2 > 0]  (K = classes, natural order)
+    if (wave < MT) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma_f32(sDlog[(16 * wave + c) * LD16 + 4 * ks + h], sW3[(4 * ks + h) * LD16 + c], acc);
+      float* dst = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * wave + 4 * h + i;
+        const float v = sH2[b * LD16 + c] > 0.f ? acc[i] : 0.f;
+        sDH2[b * LD16 + c] = v;
+        st_wt32(dst + b * PD2 + 16 * hd + c, v);
+      }
+    }
+    persist::publish(pb.flags, FPP, p, F_DH2 + hd, (unsigned)(t + 1));
+
+    // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
+    //      b2 (wave 1), b3 (wave 2, the same arithmetic in every head)
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+      const int g = 2 * wave + gg;
+      f32x4 acc = zero4();  // C[o1 = 16g + 4h + i][o2 = 16hd + c], k-ordered over the batch
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(sH1[(4 * kb + h) * LDH1 + 16 * g + c], sDH2[(4 * kb + h) * LD16 + c], acc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, acc[i], w2[gg][i], m2[gg][i], v2[gg][i], e2[gg][i], lr_t, inv_bc2, wdmu);
+    }
+    if (wave == 0) {
+      f32x4 acc = zero4();  // C[o2 = 16hd + 4h + i][class c]
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(sH2[(4 * kb + h) * LD16 + c], sDlog[(4 * kb + h) * LD16 + c], acc);
+      if (cin) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          upd32<ADAM, EXTRA>(o, acc[i], w3[i], m3[i], v3[i], e3[i], lr_t, inv_bc2, wdmu);
+          sW3[c * LD16 + 4 * h + i] = w3[i];
+        }
+      }
+    } else if (wave == 1) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(1.f, sDH2[(4 * kb + h) * LD16 + c], acc);
+      if (lane < 16) upd32<ADAM, EXTRA>(o, acc[0], sB2[c], sB2[16 + c], sB2[32 + c], sB2[48 + c], lr_t, inv_bc2, wdmu);
+    } else if (wave == 2) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(1.f, sDlog[(4 * kb + h) * LD16 + c], acc);
+      if (lane < 16 && cin) upd32<ADAM, EXTRA>(o, acc[0], sB3[c], sB3[16 + c], sB3[32 + c], sB3[48 + c], lr_t, inv_bc2, wdmu);
+    }
+    __syncthreads();
+  }
+
+  // ---- write back W2 rows, b2, the W3 slice, b3 (head 0) and the epoch's loss / accuracy sums
+#pragma unroll
+  for (int gg = 0; gg < 2; ++gg) {
+    const int64_t idx = pS + a.off_w2 + (int64_t)o2 * PD1 + 16 * (2 * wave + gg) + 4 * h;
+    *reinterpret_cast<float4*>(a.params + idx) = float4{w2[gg][0], w2[gg][1], w2[gg][2], w2[gg][3]};
+    *reinterpret_cast<float4*>(a.m + idx) = float4{m2[gg][0], m2[gg][1], m2[gg][2], m2[gg][3]};
+    if (ADAM) *reinterpret_cast<float4*>(a.v + idx) = float4{v2[gg][0], v2[gg][1], v2[gg][2], v2[gg][3]};
+  }
+  if (wave == 0 && cin) {
+    const int64_t idx = pS + a.off_w3 + (int64_t)c * PD2 + 16 * hd + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a.params[idx + i] = w3[i];
+      a.m[idx + i] = m3[i];
+      if (ADAM) a.v[idx + i] = v3[i];
+    }
+  }
+  if (tid < 16) {
+    const int64_t idx = pS + a.off_b2 + 16 * hd + tid;
+    a.params[idx] = sB2[tid];
+    a.m[idx] = sB2[16 + tid];
+    if (ADAM) a.v[idx] = sB2[32 + tid];
+  } else if (hd == 0 && tid >= 64 && tid < 64 + D3) {
+    const int k = tid - 64;
+    const int64_t idx = pS + a.off_b3 + k;
+    a.params[idx] = sB3[k];
+    a.m[idx] = sB3[16 + k];
+    if (ADAM) a.v[idx] = sB3[32 + k];
+  }
+  if (hd == 0 && wave < MT) {
+    const float l = wave_sum(loss_acc), cr = wave_sum(correct_acc);
+    if (lane == 0) {
+      atomicAdd(&a.loss_acc[p], l);
+      atomicAdd(&a.correct_acc[p], (int)(cr + 0.5f));
+    }
+  }
+}
+
+// grid = 8 * ROLES blocks per group of 8 peers: block b serves peer p_base + (b & 7) in role b >> 3,
+// so a peer's 24 workgroups share one XCD under round-robin dispatch (speed only).
+template <int BP, bool ADAM, bool EXTRA>
+__global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base) {
+  extern __shared__ __attribute__((aligned(16))) char smem_p32[];
+  const int b = blockIdx.x;
+  const int p = p_base + (b & 7);
+  const int role = b >> 3;
+  if (p >= a.P) return;
+  const int4 ctl = a.ctl[p];
+  if (!(ctl.x & 1) || ctl.y <= 0) return;
+  if (role < NG)
+    owner32<BP, ADAM, EXTRA>(a, pb, p, role, smem_p32);
+  else
+    head32<BP, ADAM, EXTRA>(a, pb, p, role - NG, smem_p32);
+}
+
+// =============================================================================================
+// fp32 evaluation: grid = (ceil(max_test_rows / 64), P), 512 threads; one 64-row chunk of one
+// peer's test split per workgroup: forward (layer 1 with the exact split, layers 2-3 on the f32
+// MFMA), log-softmax NLL sum, argmax, correct count and confusion counts.
+// =============================================================================================
+constexpr int EV_ROWS = 64;
+
+__host__ __device__ inline size_t eval_lds32(int D0) {
+  const int ks1 = (D0 + 31) / 32;
+  const size_t x = (size_t)EV_ROWS * (ks1 * 32 + 8) * 2;
+  const size_t hh = (size_t)EV_ROWS * LDH1 * 4 + (size_t)EV_ROWS * LDD * 4;  // H1 + H2 overlay the X tile
+  return al16(x > hh ? x : hh) + 16;
+}
+
+__global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_e32[];
+  const int p = blockIdx.y;
+  const int4 ctl = a.ctl[p];
+  if (!(ctl.x & 1)) return;
+  const int base = blockIdx.x * EV_ROWS;
+  const int rows = min(EV_ROWS, ctl.w - base);
+  if (rows <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, c = lane & 15;
+  const int D0 = a.D0, D3 = a.D3, KS1 = (D0 + 31) / 32, LDX = KS1 * 32 + 8;
+  constexpr int MT = EV_ROWS / 16;
+  bf16* sX = reinterpret_cast<bf16*>(smem_e32);
+  float* sH1 = reinterpret_cast<float*>(smem_e32);
+  float* sH2 = reinterpret_cast<float*>(smem_e32 + (size_t)EV_ROWS * LDH1 * 4);
+  const float* P = a.params + (int64_t)p * a.S;
+  const uint8_t* X = a.Xtp[p] + (int64_t)base * D0;
+  const int* Y = a.Ytp[p] + base;
+
+  // X chunk -> bf16 (exact), zero rows beyond the split and the K padding columns
+  const int c8 = KS1 * 4;  // 8-column groups per padded row
+  for (int e = tid; e < EV_ROWS * c8; e += NT) {
+    const int r = e / c8, col = 8 * (e % c8);
+    const bf16x8 v = (r < rows && col < D0) ? ld8_u8(X + (int64_t)r * D0 + col) : zero_bf16x8();
+    *reinterpret_cast<bf16x8*>(sX + r * LDX + col) = v;
+  }
+  __syncthreads();
+
+  // layer 1: wave w -> H1 columns 32w..32w+31 (two 16-column tiles), W1 split on the fly
+  f32x4 acc[2][MT];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = zero4();
+  for (int s = 0; s < KS1; ++s) {
+    const int col = 32 * s + 8 * h;
+    bf16x8 bh[2], bm[2], bl[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (col < D0) {
+        const float* wp = P + a.off_w1 + (int64_t)(32 * wave + 16 * nt + c) * D0 + col;
+        const float4 lo4 = *reinterpret_cast<const float4*>(wp), hi4 = *reinterpret_cast<const float4*>(wp + 4);
+        x[0] = lo4.x; x[1] = lo4.y; x[2] = lo4.z; x[3] = lo4.w;
+        x[4] = hi4.x; x[5] = hi4.y; x[6] = hi4.z; x[7] = hi4.w;
+      }
+      split3(x, bh[nt], bm[nt], bl[nt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x8 af = ld8(sX + (16 * mt + c) * LDX + 32 * s + 8 * h);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[nt][mt] = mfma3(af, bh[nt], bm[nt], bl[nt], acc[nt][mt]);
+    }
+  }
+  __syncthreads();  // the X tile is dead: H1 / H2 overlay it
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int o1 = 32 * wave + 16 * nt + c;
+    const float bias = P[a.off_b1 + o1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sH1[(16 * mt + 4 * h + i) * LDH1 + o1] = fmaxf(acc[nt][mt][i] + bias, 0.f);
+  }
+  __syncthreads();
+  // layer 2: wave w -> H2 columns 16w..16w+15 (k order 16q + 4h + i)
+  {
+    f32x4 a2[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) a2[mt] = zero4();
+    const float* w2row = P + a.off_w2 + (int64_t)(16 * wave + c) * PD1;
+    for (int q = 0; q < PD1 / 16; ++q) {
+      const float4 bv = *reinterpret_cast<const float4*>(w2row + 16 * q + 4 * h);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float4 av = *reinterpret_cast<const float4*>(sH1 + (16 * mt + c) * LDH1 + 16 * q + 4 * h);
+        a2[mt] = mfma_f32(av.x, bv.x, a2[mt]);
+        a2[mt] = mfma_f32(av.y, bv.y, a2[mt]);
+        a2[mt] = mfma_f32(av.z, bv.z, a2[mt]);
+        a2[mt] = mfma_f32(av.w, bv.w, a2[mt]);
+      }
+    }
+    const float bias = P[a.off_b2 + 16 * wave + c];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sH2[(16 * mt + 4 * h + i) * LDD + 16 * wave + c] = fmaxf(a2[mt][i] + bias, 0.f);
+  }
+  __syncthreads();
+  // layer 3 + loss / argmax / confusion: wave w < MT owns rows 16w..16w+15
+  if (wave < MT) {
+    const bool cin = c < D3;
+    f32x4 lg = zero4();
+    const float* w3row = P + a.off_w3 + (int64_t)(cin ? c : 0) * PD2;
+    for (int q = 0; q < PD2 / 16; ++q) {
+      float4 bv = *reinterpret_cast<const float4*>(w3row + 16 * q + 4 * h);
+      if (!cin) bv = float4{0.f, 0.f, 0.f, 0.f};
+      const float4 av = *reinterpret_cast<const float4*>(sH2 + (16 * wave + c) * LDD + 16 * q + 4 * h);
+      lg = mfma_f32(av.x, bv.x, lg);
+      lg = mfma_f32(av.y, bv.y, lg);
+      lg = mfma_f32(av.z, bv.z, lg);
+      lg = mfma_f32(av.w, bv.w, lg);
+    }
+    const float b3 = cin ? P[a.off_b3 + c] : 0.f;
+    float loss_part = 0.f, correct_part = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * wave + 4 * h + i;
+      const bool rvalid = r < rows;
+      const int y = rvalid ? Y[r] : -1;
+      const float logit = cin ? lg[i] + b3 : -INFINITY;
+      const float mx = row_max16(logit);
+      const float se = row_sum16(cin ? expf(logit - mx) : 0.f);
+      const float logp = logit - (mx + logf(se));
+      const int cand = row_min16((cin && logit == mx) ? c : 16);
+      if (rvalid && c == y) loss_part -= logp;
+      if (rvalid && c == 0) {
+        correct_part += (cand == y) ? 1.f : 0.f;
+        if (a.conf != nullptr && y >= 0 && y < 16 && cand < 16) atomicAdd(&a.conf[(p * 16 + y) * 16 + cand], 1);
+      }
+    }
+    loss_part = wave_sum(loss_part);
+    const float cp = wave_sum(correct_part);
+    if (lane == 0) {
+      atomicAdd(&a.loss_acc[p], loss_part);
+      atomicAdd(&a.correct_acc[p], (int)(cp + 0.5f));
+    }
+  }
+}
+
+size_t persistent_f32_lds(const MLPArgs& a) {
+  const size_t lo = owner_lds32(a.Bpad, a.D0).total, lh = head_lds32(a.Bpad).total;
+  return lo > lh ? lo : lh;
+}
+
+template <int BP, bool ADAM, bool EXTRA>
+hipError_t prepare_f32(int lds) {
+  return hipFuncSetAttribute((const void*)mlp_persistent_f32_epoch<BP, ADAM, EXTRA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+template <int BP>
+hipError_t prepare_f32_bp(int lds) {
+  hipError_t e;
+  if ((e = prepare_f32<BP, true, false>(lds)) != hipSuccess) return e;
+  if ((e = prepare_f32<BP, true, true>(lds)) != hipSuccess) return e;
+  if ((e = prepare_f32<BP, false, false>(lds)) != hipSuccess) return e;
+  return prepare_f32<BP, false, true>(lds);
+}
+template <int BP>
+void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds) {
+  const dim3 grid(8 * ROLES), block(NT);
+  const bool adam = a.opt.kind == 0;
+  const bool extra = a.anchor != nullptr || a.cg != nullptr;
+  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false>), grid, block, lds, s, a, pb, p_base);
+  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true>), grid, block, lds, s, a, pb, p_base);
+  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false>), grid, block, lds, s, a, pb, p_base);
+  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true>), grid, block, lds, s, a, pb, p_base);
+}
+
+}  // namespace
+
+bool mlp_persistent_f32_supported(const MLPArgs& a) {
+  if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
+  if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
+  if (a.Bpad != 32 && a.Bpad != 64) return false;
+  if ((a.cg == nullptr) != (a.cl == nullptr)) return false;
+  return persistent_f32_lds(a) <= 160 * 1024;
+}
+
+size_t mlp_persistent_f32_bytes(int P, int Bpad) {
+  return (size_t)P * ((size_t)Bpad * PD1 + (size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * sizeof(float);
+}
+size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
+int mlp_persistent_f32_gang() { return ROLES; }
+int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
+
+hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
+  const int lds = (int)persistent_f32_lds(a);
+  hipError_t e = a.Bpad == 64 ? prepare_f32_bp<64>(lds) : prepare_f32_bp<32>(lds);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)mlp_eval_f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds32(a.D0));
+}
+
+hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags) {
+  if (zero_flags) {
+    hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
+    if (e != hipSuccess) return e;
+  }
+  const size_t lds = persistent_f32_lds(a);
+  // groups of 8 peers: one launch each (a launch's gangs must all be co-resident: 192 CUs)
+  for (int p0 = 0; p0 < a.P; p0 += 8) {
+    if (a.Bpad == 64)
+      launch_f32_bp<64>(a, pb, s, p0, lds);
+    else
+      launch_f32_bp<32>(a, pb, s, p0, lds);
+  }
+  return hipGetLastError();
+}
+
+void mlp_launch_eval_f32(const MLPArgs& a, int max_rows, hipStream_t s) {
+  if (max_rows <= 0) return;
+  const dim3 grid((max_rows + EV_ROWS - 1) / EV_ROWS, a.P);
+  hipLaunchKernelGGL(mlp_eval_f32, grid, dim3(NT), eval_lds32(a.D0), s, a);
+}

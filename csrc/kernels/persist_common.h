@@ -1,0 +1,112 @@
+// Device helpers shared by the weight-stationary persistent epoch kernels (mlp_persistent.hip,
+// mlp_persistent_f32.hip): in-launch hand-offs between the workgroups of a peer's gang, Adam bias
+// correction, and 16-lane DPP row reductions.
+//
+// Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, valid form row 1 of
+// MI355X_MICROARCH.md's hand-off table): payload stored write-through (sc1), every storing wave
+// drains its stores, the workgroup meets, ONE lane stores a relaxed agent-scope flag = step + 1;
+// the consumer polls relaxed from one wave, meets its workgroup, and reads every payload byte with
+// sc1 loads (no acquire fence needed). Flags are monotone within a launch and zeroed per launch.
+#pragma once
+#include "common.h"
+
+namespace persist {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int FLAG_LINE = 32;                            // u32 per flag: one 128-byte line each
+constexpr unsigned long long SPIN_TICKS = 100000000ull;  // wall_clock64 runs at 100 MHz: 1 s
+
+__device__ __forceinline__ unsigned* flag_at(unsigned* flags, int flags_per_peer, int p, int idx) {
+  return flags + ((size_t)p * flags_per_peer + idx) * FLAG_LINE;
+}
+__device__ __forceinline__ void st_wt(void* ptr, unsigned long long v) {  // 8-byte write-through store
+  __hip_atomic_store((gu64*)ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt32(float* ptr, float v) {  // 4-byte write-through store
+  __hip_atomic_store((gu32*)ptr, __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
+  return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Producer side: every storing wave drains its write-through stores, the workgroup meets, ONE lane
+// stores the flag (sc1).
+__device__ __forceinline__ void publish(unsigned* flags, int fpp, int p, int idx, unsigned value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag_at(flags, fpp, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer side: wave 0 polls flags idx0..idx0+n-1 (one lane each, relaxed sc1 loads + s_sleep)
+// until all reach `target`, then the workgroup meets; every later load of the handed-off bytes is
+// an sc1 load. Bounded: gives up after `ticks` or when another workgroup gave up.
+__device__ __forceinline__ bool wg_wait(unsigned* flags, int fpp, int p, int idx0, int n, unsigned target, int* err, int* sOk,
+                                        unsigned long long ticks = SPIN_TICKS) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned* f = flag_at(flags, fpp, p, idx0 + (lane < n ? lane : 0));
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    for (;;) {
+      const unsigned v = lane < n ? __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__all(v >= target)) break;
+      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        ok = 0;
+        break;
+      }
+      if (wall_clock64() - t0 > ticks) {
+        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *sOk = ok;
+  }
+  __syncthreads();
+  const int ok = *sOk;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+  return ok != 0;
+}
+
+// Per-step optimizer constants: lr_t = lr / (1 - β1^k), inv = 1 / sqrt(1 - β2^k), k = t0 + t + 1.
+__device__ __forceinline__ void bias_corr(const OptParams& o, int t0, int t, float& lr_t, float& inv) {
+  const int k = t0 + t + 1;
+  lr_t = o.lr / (1.f - __powf(o.beta1, (float)k));
+  inv = 1.f / sqrtf(1.f - __powf(o.beta2, (float)k));
+}
+
+// 16-lane (one MFMA row group) butterfly reductions on DPP: quad_perm xor1, xor2, then
+// row_half_mirror and row_mirror — VALU-latency instead of ds_bpermute round trips.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ int row_min16(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  return min(v, dpp_i<0x140>(v));
+}
+
+__host__ __device__ inline size_t al16(size_t v) { return (v + 15) / 16 * 16; }
+
+}  // namespace persist

@@ -141,7 +141,11 @@ struct MLPEngine {
   ResultSlot ring[MLP_RING];  // pinned host result buffers + completion events
   // weight-stationary persistent epoch (mlp_persistent.hip): exchange buffers + mode
   MLPPersistBufs pb{};
+  MLPPersistF32Bufs pb32{};
   int persist_mode = -1;  // -1 auto (eligible configs), 0 off
+  // 1 = fp32 (the reference's precision: fp32 persistent epoch + fp32 evaluation; no bf16 fallback),
+  // 0 = bf16 MFMA operands with fp32 master weights (persistent or 3-launch step path)
+  int precision = 1;
   int num_cus = 0;
   bool graph_persistent = false;
   // deferred to the epoch's control upload on the persistent path (fewer tiny launches per round)
@@ -163,9 +167,39 @@ struct MLPEngine {
   int* d_correct_eval = nullptr;
 
   bool use_persistent() const {
+    if (precision == 1) return fp32_ready();
     if (persist_mode == 0 || pb.h1x == nullptr || a.Xb16 == nullptr) return false;
     if (a.P * 17 > num_cus) return false;  // every gang must be co-resident (one workgroup per CU)
     return mlp_persistent_supported(a);
+  }
+  // the fp32 path: every gang of a launch (8 peers x 24 workgroups) co-resident, one per CU
+  bool fp32_ready() const {
+    if (pb32.h1x == nullptr || a.Xb16 == nullptr) return false;
+    if (8 * mlp_persistent_f32_gang() > num_cus) return false;
+    return mlp_persistent_f32_supported(a);
+  }
+  int launch_epoch_kernel(hipStream_t s, bool zero_flags) {
+    const hipError_t le = precision == 1 ? mlp_launch_persistent_f32_epoch(a, pb32, s, zero_flags) : mlp_launch_persistent_epoch(a, pb, s, zero_flags);
+    if (le != hipSuccess) {
+      g_last_error = std::string("persistent epoch launch: ") + hipGetErrorString(le);
+      return 1;
+    }
+    return 0;
+  }
+  void set_flag_zeroing(MLPArgs& ga) const {
+    if (precision == 1) {
+      ga.flags_zero = pb32.flags;
+      ga.flags_per_peer = mlp_persistent_f32_flags_per_peer();
+    } else {
+      ga.flags_zero = pb.flags;
+      ga.flags_per_peer = (int)(pb.flag_bytes / sizeof(unsigned) / a.P);
+    }
+  }
+  void launch_eval(const MLPArgs& ea, hipStream_t s) const {
+    if (precision == 1)
+      mlp_launch_eval_f32(ea, max_test_rows, s);
+    else
+      for (int base = 0; base < max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(ea, base, s);
   }
 
   ~MLPEngine() {
@@ -284,19 +318,14 @@ struct MLPEngine {
     {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
-      if (graph_persistent) {  // ... which also zeroes the hand-off flags (no memset node)
-        ga.flags_zero = pb.flags;
-        ga.flags_per_peer = (int)(pb.flag_bytes / sizeof(unsigned) / a.P);
-      }
+      if (graph_persistent) set_flag_zeroing(ga);  // ... which also zeroes the hand-off flags (no memset node)
       mlp_launch_gather_epoch(ga, cap_stream);
     }
     if (graph_persistent) {
-      hipError_t le = mlp_launch_persistent_epoch(a, pb, cap_stream, false);
-      if (le != hipSuccess) {
+      if (launch_epoch_kernel(cap_stream, false)) {
         hipGraph_t g = nullptr;
         hipStreamEndCapture(cap_stream, &g);
         if (g) hipGraphDestroy(g);
-        g_last_error = std::string("persistent epoch launch: ") + hipGetErrorString(le);
         return 1;
       }
     } else {
@@ -502,6 +531,16 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
       rc |= e->alloc(&p, 16);
       e->pb.err = (int*)p;
       if (mlp_persistent_prepare(a) != hipSuccess) e->persist_mode = 0;
+      // fp32 exchange buffers + flags (err word shared)
+      rc |= e->alloc(&p, mlp_persistent_f32_bytes(P, a.Bpad));
+      e->pb32.h1x = (float*)p;
+      e->pb32.plx = e->pb32.h1x + (size_t)P * a.Bpad * 256;
+      e->pb32.dh2x = e->pb32.plx + (size_t)P * 8 * a.Bpad * 16;
+      e->pb32.flag_bytes = mlp_persistent_f32_flag_bytes(P);
+      rc |= e->alloc(&p, e->pb32.flag_bytes);
+      e->pb32.flags = (unsigned*)p;
+      e->pb32.err = e->pb.err;
+      if (mlp_persistent_f32_prepare(a) != hipSuccess) e->pb32.h1x = nullptr;
     }
   }
   if (rc) {
@@ -653,6 +692,41 @@ int mlp_engine_set_persistent(void* h, int mode) {
   return 0;
 }
 
+// Precision of the engine: 1 = fp32 (default), 0 = bf16 operands / fp32 master weights.
+int mlp_engine_set_precision(void* h, int precision) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (precision != e->precision) {
+    e->precision = precision;
+    e->invalidate();
+  }
+  return 0;
+}
+// 1 if the fp32 persistent epoch supports this shape and local batch on this device.
+int mlp_f32_ok(int D0, int D1, int D2, int D3, int B) {
+  if (!mlp_shape_supported(D0, D1, D2, D3) || B < 1) return 0;
+  MLPArgs a{};
+  a.D0 = D0; a.D1 = D1; a.D2 = D2; a.D3 = D3;
+  a.B = B;
+  a.Bpad = (B + 31) / 32 * 32;
+  int dev = 0, cus = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (8 * mlp_persistent_f32_gang() > cus) return 0;
+  return mlp_persistent_f32_supported(a) ? 1 : 0;
+}
+// Debug: the owners of the fp32 epoch write their W2 replica to `buf` ([P][D2][D1] fp32) after the
+// epoch (null = off), for the bitwise check against the heads' rows.
+int mlp_engine_set_w2chk(void* h, float* buf) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (buf != e->pb32.w2chk) {
+    e->pb32.w2chk = buf;
+    e->invalidate();
+  }
+  return 0;
+}
+
 // 1 if the next epoch runs as the persistent kernel.
 int mlp_engine_uses_persistent(void* h) { return ((MLPEngine*)h)->use_persistent() ? 1 : 0; }
 
@@ -662,6 +736,10 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   std::lock_guard<std::mutex> g(e->mu);
   hipStream_t s = (hipStream_t)stream;
   if (e->max_steps <= 0) return 0;
+  if (e->precision == 1 && !e->use_persistent()) {
+    g_last_error = "fp32 MLP engine: shape / batch / CU count not supported by the fp32 persistent epoch (no silent bf16 fallback)";
+    return 2;
+  }
   if (!e->exec || e->graph_steps != e->max_steps) {
     if (e->capture(e->max_steps)) return 1;
   }
@@ -682,13 +760,17 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
   const bool pa = pers && e->pending_zero_acc;
   if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, pers && e->pending_fresh)) return 1;
   if (pers) e->pending_zero_acc = e->pending_fresh = false;
+  if (e->precision == 1 && !pers) {
+    g_last_error = "fp32 MLP engine: shape / batch / CU count not supported by the fp32 persistent epoch";
+    return 2;
+  }
   {
     MLPArgs ga = e->a;
     if (!pers) ga.Xb16 = nullptr;
     mlp_launch_gather_epoch(ga, s);
   }
-  if (e->use_persistent()) {
-    CHECK_HIP(mlp_launch_persistent_epoch(e->a, e->pb, s));
+  if (pers) {
+    if (e->launch_epoch_kernel(s, true)) return 1;
   } else {
     for (int st = 0; st < e->max_steps; ++st) mlp_launch_train_step(e->a, st, s);
   }
@@ -752,7 +834,7 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
     CHECK_HIP(hipEventRecord(e->ev_snap, s));
     hipStream_t es = e->eval_stream;
     CHECK_HIP(hipStreamWaitEvent(es, e->ev_snap, 0));
-    for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(ea, base, es);
+    e->launch_eval(ea, es);
     CHECK_HIP(hipGetLastError());
     if (e->publish(es, r, e->d_loss_eval, e->d_correct_eval, nullptr, e->d_conf)) return 1;
     CHECK_HIP(hipEventRecord(r.ev, es));
@@ -765,8 +847,8 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_conf, 0, sizeof(int) * e->a.P * 256, s));
-  mlp_launch_sync_shadow(e->a, s);
-  for (int base = 0; base < e->max_test_rows; base += MLP_EVAL_CHUNK) mlp_launch_eval_chunk(e->a, base, s);
+  if (e->precision != 1) mlp_launch_sync_shadow(e->a, s);
+  e->launch_eval(e->a, s);
   CHECK_HIP(hipGetLastError());
   if (e->publish(s, r, e->d_loss, e->d_correct, nullptr, e->d_conf)) return 1;
   CHECK_HIP(hipEventRecord(r.ev, s));

@@ -108,7 +108,9 @@ class TorchLearner(Learner):
         from myfyp_amd.parallel.cnn_engine import CNNEngineHandle
         from myfyp_amd.parallel.mlp_engine import MLPEngineHandle
 
-        for handle in (MLPEngineHandle, CNNEngineHandle):
+        if MLPEngineHandle.supports(module, self.batch_size):
+            return MLPEngineHandle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
+        for handle in (CNNEngineHandle,):
             if handle.supports(module):
                 return handle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
         return None

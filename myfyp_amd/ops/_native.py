@@ -77,6 +77,9 @@ _SIGNATURES = {
     "myfyp_fedavg_stacked_local": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "myfyp_neighbor_mix_stacked": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "mlp_engine_uses_persistent": (c_int, [c_void_p]),
+    "mlp_engine_set_precision": (c_int, [c_void_p, c_int]),
+    "mlp_f32_ok": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "mlp_engine_set_w2chk": (c_int, [c_void_p, c_void_p]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
 }
 

@@ -12,8 +12,12 @@ the Ray actor pool (``simulation/actor_pool.py``) for ReLU MLPs on MI355X:
   engine (``csrc/runtime/engine.hip``) whose kernels cover all peers via ``grid.z``;
 * ``evaluate`` is ganged the same way (one forward sweep over every peer's test split).
 
-Numerics: bf16 MFMA operands, fp32 accumulation, fp32 master weights and optimizer state,
-``torch.optim.Adam``/``SGD`` update rules, fresh optimizer state per ``fit`` (Lightning semantics).
+Numerics (``Settings.MLP_PRECISION``): "fp32" (default, the reference's precision — Lightning's
+default fp32 Trainer, ``lightning_learner.py:82-89``) runs the fp32 persistent epoch
+(``csrc/kernels/mlp_persistent_f32.hip``: exact fp32 products, fp32 accumulation, fp32 weights and
+optimizer state) and the fp32 evaluation; "bf16" uses bf16 MFMA operands with fp32 accumulation,
+master weights and optimizer state. Both follow the ``torch.optim.Adam``/``SGD`` update rules with
+fresh optimizer state per ``fit`` (Lightning semantics).
 """
 
 from __future__ import annotations
@@ -110,12 +114,13 @@ class MLPGroup:
     _lock = threading.Lock()
 
     @classmethod
-    def get(cls, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int) -> "MLPGroup":
-        key = (str(device), dims, batch_size)
+    def get(cls, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, precision: Optional[str] = None) -> "MLPGroup":
+        precision = precision or Settings.MLP_PRECISION
+        key = (str(device), dims, batch_size, precision)
         with cls._lock:
             g = cls._groups.get(key)
             if g is None:
-                g = cls(device, dims, batch_size)
+                g = cls(device, dims, batch_size, precision=precision)
                 cls._groups[key] = g
             return g
 
@@ -126,7 +131,10 @@ class MLPGroup:
                 g.close()
             cls._groups.clear()
 
-    def __init__(self, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, capacity: int = 8) -> None:
+    def __init__(self, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, capacity: int = 8, precision: str = "fp32") -> None:
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"MLP precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
         self.device = device
         self.dims = dims
         self.B = batch_size
@@ -218,6 +226,7 @@ class MLPGroup:
             _native.check(
                 lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
             )
+        _native.check(lib.mlp_engine_set_precision(self._engine, 1 if self.precision == "fp32" else 0), "set_precision")
         if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
             _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
         if self._bound_version != self._data_version:
@@ -444,7 +453,7 @@ class MLPEngineHandle:
     """A learner's slot in an :class:`MLPGroup`."""
 
     @staticmethod
-    def supports(module: torch.nn.Module) -> bool:
+    def supports(module: torch.nn.Module, batch_size: Optional[int] = None) -> bool:
         dims = mlp_dims(module)
         if dims is None:
             return False
@@ -452,6 +461,9 @@ class MLPEngineHandle:
         if lib is None:
             # GPU + fused path requested but no library: fail loudly (no silent eager fallback)
             raise RuntimeError(f"MI355X fused engine requested but native library unavailable: {_native.error()}")
+        if Settings.MLP_PRECISION == "fp32":
+            # the fp32 engine has no bf16 fallback: shapes it cannot run stay on fp32 autograd
+            return bool(lib.mlp_f32_ok(*dims, int(batch_size or Settings.BATCH_SIZE)))
         return bool(lib.mlp_shape_ok(*dims))
 
     @classmethod

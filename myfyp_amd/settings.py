@@ -85,7 +85,10 @@ class Settings:
     # ---------------- DEVICE / ENGINE (new: MI355X data plane)
     DEVICE: str = "auto"  # "auto" -> cuda if available else cpu
     BATCH_SIZE: int = 1  # reference default (lightning_dataset.py:81); benchmarks override it
-    COMPUTE_DTYPE: str = "bf16"  # GEMM operand dtype on the GPU (fp32 master weights)
+    COMPUTE_DTYPE: str = "bf16"  # CNN engines' GEMM operand dtype (fp32 master weights; BASELINE config 4 is bf16)
+    # fused MLP engine precision: "fp32" = the reference's (Lightning default fp32 Trainer): exact
+    # fp32 products, fp32 accumulation / weights / optimizer state; "bf16" = bf16 MFMA operands
+    MLP_PRECISION: str = "fp32"
     USE_FUSED_KERNELS: bool = True  # hand-written HIP path when the extension is present
     GROUP_PEERS: bool = True  # train co-located peers in one grouped launch
     GANG_WINDOW: float = 0.05  # seconds a grouped fit waits for expected co-located peers
@@ -163,6 +166,7 @@ class Settings:
         {
             "DEVICE": "DEVICE",
             "COMPUTE_DTYPE": "COMPUTE_DTYPE",
+            "MLP_PRECISION": "MLP_PRECISION",
             "USE_FUSED_KERNELS": "USE_FUSED_KERNELS",
             "GROUP_PEERS": "GROUP_PEERS",
             "GANG_WINDOW": "GANG_WINDOW",

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Parameterised GPU entry point (replaces the one-off gpu_*.sh scripts):
+#   OUT=<dir under gpurun_out> bash scripts/gpu_run.sh <step> [<step> ...]
+# steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), smoke, bench (fp32 headline),
+#        bench_bf16, bench_cnn, prof (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
+#        gloo ranks on one GPU). Every GPU step runs under its own time limit; the script stops at
+#        the first failure, and at once after a timeout, abort or segfault.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${OUT:-run}
+mkdir -p "$O"
+fatal() { case "$1" in 124|134|137|139) echo "fatal rc=$1 in $2"; exit "$1";; esac; }
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -4 "$O/$name.log"
+  fatal $rc "$name"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+    f32tests) run f32_tests 400 python -u -m pytest tests/test_mlp_f32_gpu.py -v --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench_fp32 300 python bench.py ;;
+    bench_bf16) run bench_bf16 300 python bench.py --precision bf16 ;;
+    bench_cnn) run bench_cnn 600 python benchmarks/bench_cnn.py ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python bench.py --steps 40 --warmup 5 ;;
+    rehearsal)
+      for n in 2 4; do
+        MYFYP_DIST_BACKEND=gloo run rehearsal_gloo_n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port 2970$n bench.py --gpus $n --steps 10 --warmup 2
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -15,6 +15,17 @@ def dev():
     return torch.device("cuda")
 
 
+@pytest.fixture
+def bf16_engine():
+    """The bf16-operand MLP engine (persistent + 3-launch step paths); fp32 is tests/test_mlp_f32_gpu.py."""
+    from myfyp_amd.settings import Settings
+
+    old = Settings.MLP_PRECISION
+    Settings.MLP_PRECISION = "bf16"
+    yield
+    Settings.MLP_PRECISION = old
+
+
 def test_weighted_average(dev):
     from myfyp_amd import ops
 
@@ -194,7 +205,7 @@ def _reference_mlp_run(module, x, y, perm, B, lr, steps):
 
 @pytest.mark.parametrize("persistent", [None, False], ids=["persistent", "steps"])
 @pytest.mark.parametrize("B", [32, 48])
-def test_fused_mlp_engine_matches_autograd(dev, B, persistent):
+def test_fused_mlp_engine_matches_autograd(dev, B, persistent, bf16_engine):
     """One local epoch of the grouped engine (2 peers, SGD) vs per-peer fp32 autograd, on the
     weight-stationary persistent epoch kernel and on the 3-launch step path."""
     import copy
@@ -260,7 +271,7 @@ def test_fused_mlp_engine_matches_autograd(dev, B, persistent):
 
 
 @pytest.mark.parametrize("persistent", [None, False], ids=["persistent", "steps"])
-def test_fused_mlp_single_step_gradients(dev, persistent):
+def test_fused_mlp_single_step_gradients(dev, persistent, bf16_engine):
     """Per-parameter gradient of ONE fused step (SGD, grad = Δw/lr) vs autograd, 3 peers, B=40."""
     import copy
     import threading
@@ -313,7 +324,7 @@ def test_fused_mlp_single_step_gradients(dev, persistent):
 
 
 @pytest.mark.parametrize("B", [64, 32])
-def test_persistent_epoch_matches_step_path_adam(dev, B):
+def test_persistent_epoch_matches_step_path_adam(dev, B, bf16_engine):
     """Several Adam epochs on 3 peers: persistent epoch kernel vs 3-launch step path from identical
     weights and batch order (same bf16 rounding points; accumulation order and the epilogue's
     reciprocal differ)."""
