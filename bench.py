@@ -153,13 +153,10 @@ def main() -> None:
     wait_to_finish(nodes, timeout=3600)
     t0, t1 = marks.get("t0"), marks.get("t1")
     elapsed = (t1 - t0) if (t0 is not None and t1 is not None) else float("nan")
-    # max over ranks
+    # max over the (live) ranks
     if world > 1:
-        import torch.distributed as dist
-
-        dev = fed.device
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=fed.device)
+        fed.all_reduce_(tt, op="max")
         elapsed = float(tt.item())
 
     # accuracy curve of the local peers: test_metric logged at round r = model after round r-1

@@ -144,10 +144,8 @@ def main() -> None:
     wait_to_finish(nodes, timeout=7200)
     el = marks["t1"] - marks["t0"]
     if world > 1:
-        import torch.distributed as dist
-
         t = torch.tensor([el], dtype=torch.float64, device=fed.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fed.all_reduce_(t, op="max")
         el = float(t.item())
     logs = logger.get_global_logs().get("experiment", {})
     accs = [logs[n.addr]["test_metric"][-1][1] for n in nodes if logs.get(n.addr, {}).get("test_metric")]

@@ -16,6 +16,17 @@
 // Payloads larger than the slot publish an overflow marker; every rank then sees the overflow and
 // the caller falls back to the gloo path collectively (no rank can diverge).
 //
+// Membership (fault tolerance). Each rank's `status` word is either the last generation it
+// published or kGone | g, "gone from generation g on" (it published g - 1 and never joins g or
+// later). Both transitions are compare-and-swaps on that one word, so a rank that is evicted can
+// no longer publish, and every survivor computes the same participant set for a generation:
+// r participates in g  <=>  status_r >= g (not gone)  or  status_r == kGone | h with h > g.
+// A rank leaves on purpose (shmc_leave: its last local peer died, or the job ends) or is evicted
+// by a waiter once its heartbeat (shmc_heartbeat, CLOCK_MONOTONIC ns) is older than `fail_s`.
+// This replaces the reference's heartbeat eviction + "aggregate whatever arrived"
+// (p2pfl/communication/protocols/heartbeater.py:94-103, learning/aggregators/aggregator.py:190-208)
+// for the collective weights plane: the caller rebuilds its process groups over the survivors.
+//
 // Plain C ABI (ctypes), host-only: no GPU state is touched.
 #include <atomic>
 #include <cerrno>
@@ -32,6 +43,7 @@ namespace {
 
 constexpr uint64_t kMagic = 0x6d79667970736d63ull;  // "myfypsmc"
 constexpr uint64_t kOverflow = ~0ull;
+constexpr uint64_t kGone = 1ull << 63;
 
 struct Header {
   std::atomic<uint64_t> magic;
@@ -44,8 +56,9 @@ struct Header {
 static_assert(sizeof(Header) == 256, "header layout");
 
 struct alignas(128) RankCtl {
-  std::atomic<uint64_t> arrived;  // last published generation
+  std::atomic<uint64_t> status;   // last published generation, or kGone | first generation not joined
   uint64_t len[2];                // payload length per parity slot (kOverflow = too large)
+  std::atomic<uint64_t> beat_ns;  // heartbeat, CLOCK_MONOTONIC ns (0 = no heartbeat thread)
 };
 static_assert(sizeof(RankCtl) == 128, "rank ctl layout");
 
@@ -73,6 +86,17 @@ double now_s() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+}
+
+// 1: r took part in generation gen; 0: r never will (gone before it); -1: not decided yet
+int joined(uint64_t s, uint64_t gen) {
+  if (s & kGone) return (s & ~kGone) > gen ? 1 : 0;
+  return s >= gen ? 1 : -1;
 }
 
 inline void cpu_relax() {
@@ -104,7 +128,7 @@ int shmc_version() { return 1; }
 
 // Rank 0 creates (`create`=1) the segment, the others attach. Returns nullptr on failure (errno set).
 void* shmc_open(const char* name, int rank, int world, uint64_t slot_bytes, int create, double timeout_s) {
-  if (world < 1 || rank < 0 || rank >= world || slot_bytes < 64) {
+  if (world < 1 || world > 64 || rank < 0 || rank >= world || slot_bytes < 64) {
     errno = EINVAL;
     return nullptr;
   }
@@ -169,49 +193,117 @@ int shmc_unlink(const char* name) { return shm_unlink(name); }
 
 uint64_t shmc_slot_bytes(void* handle) { return static_cast<Handle*>(handle)->slot_bytes; }
 
-// All-gather of variable-length byte payloads.  `out` has room for world * slot_bytes; rank r's
-// payload lands at out + r * slot_bytes with its length in lens[r].
-// Returns 0 on success, 1 if some rank's payload overflowed its slot (all ranks return 1 for the
-// same generation), -1 on timeout (a rank died or stalled).
-int shmc_allgather(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, double timeout_s) {
+// Membership-aware all-gather of variable-length byte payloads. `out` has room for
+// world * slot_bytes; rank r's payload lands at out + r * slot_bytes with its length in lens[r]
+// (0 for a rank that did not take part). *members gets the participant bitmask (world <= 64).
+// A rank that has not arrived is evicted once its heartbeat is older than fail_s (fail_s <= 0:
+// never). Returns 0 ok, 1 if some participant's payload overflowed its slot (all participants
+// return 1 for the same generation), -1 timeout, -3 this rank was evicted (or left) already.
+int shmc_allgather_m(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, uint64_t* members, double timeout_s,
+                     double fail_s) {
   Handle* h = static_cast<Handle*>(handle);
   const uint64_t gen = ++h->gen;
   const int par = static_cast<int>(gen & 1);
   RankCtl* me = h->ctl(h->rank);
-  if (n <= h->slot_bytes) {
+  if (in != nullptr && n <= h->slot_bytes) {
     std::memcpy(h->slot(h->rank, par), in, n);
     me->len[par] = n;
   } else {
-    me->len[par] = kOverflow;
+    me->len[par] = in == nullptr ? 0 : kOverflow;
   }
-  me->arrived.store(gen, std::memory_order_release);
+  uint64_t expect = gen - 1;
+  if (!me->status.compare_exchange_strong(expect, gen, std::memory_order_acq_rel, std::memory_order_acquire)) return -3;
   int rc = 0;
+  uint64_t mask = 0;
+  const uint64_t fail_ns = fail_s > 0 ? static_cast<uint64_t>(fail_s * 1e9) : 0;
   for (int r = 0; r < h->world; ++r) {
     RankCtl* c = h->ctl(r);
-    if (!wait_until([&] { return c->arrived.load(std::memory_order_acquire) >= gen; }, timeout_s)) return -1;
+    int j = -1;
+    const double t0 = now_s();
+    bool ok = wait_until(
+        [&] {
+          uint64_t s = c->status.load(std::memory_order_acquire);
+          j = joined(s, gen);
+          if (j >= 0) return true;
+          if (fail_ns) {  // evict a rank whose heartbeat went stale (a crashed process)
+            const uint64_t beat = c->beat_ns.load(std::memory_order_acquire);
+            const bool stale = beat ? now_ns() - beat > fail_ns : now_s() - t0 > fail_s;
+            if (stale && c->status.compare_exchange_strong(s, kGone | gen, std::memory_order_acq_rel, std::memory_order_acquire)) {
+              j = 0;
+              return true;
+            }
+          }
+          return false;
+        },
+        timeout_s);
+    if (!ok) return -1;
+    if (j == 0) {
+      if (lens) lens[r] = 0;
+      continue;
+    }
+    mask |= 1ull << r;
     const uint64_t len = c->len[par];
     if (len == kOverflow) {
       rc = 1;
-      lens[r] = 0;
+      if (lens) lens[r] = 0;
       continue;
     }
-    lens[r] = len;
-    std::memcpy(static_cast<char*>(out) + static_cast<size_t>(r) * h->slot_bytes, h->slot(r, par), len);
+    if (lens) lens[r] = len;
+    if (out != nullptr && len) std::memcpy(static_cast<char*>(out) + static_cast<size_t>(r) * h->slot_bytes, h->slot(r, par), len);
   }
+  if (members) *members = mask;
   return rc;
 }
 
-// Barrier = all-gather of nothing.
+// All-gather over every rank (no eviction). Returns 0 / 1 (overflow) / -1 (timeout or a rank left).
+int shmc_allgather(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, double timeout_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  uint64_t mask = 0;
+  const int rc = shmc_allgather_m(handle, in, n, out, lens, &mask, timeout_s, 0.0);
+  if (rc < 0) return -1;
+  const uint64_t all = h->world >= 64 ? ~0ull : ((1ull << h->world) - 1);
+  return mask == all ? rc : -1;
+}
+
+// Barrier = all-gather of nothing (over the current participants).
 int shmc_barrier(void* handle, double timeout_s) {
   Handle* h = static_cast<Handle*>(handle);
-  const uint64_t gen = ++h->gen;
-  h->ctl(h->rank)->len[gen & 1] = 0;
-  h->ctl(h->rank)->arrived.store(gen, std::memory_order_release);
-  for (int r = 0; r < h->world; ++r) {
-    RankCtl* c = h->ctl(r);
-    if (!wait_until([&] { return c->arrived.load(std::memory_order_acquire) >= gen; }, timeout_s)) return -1;
+  uint64_t mask = 0;
+  const int rc = shmc_allgather_m(handle, nullptr, 0, nullptr, nullptr, &mask, timeout_s, 0.0);
+  (void)h;
+  return rc < 0 ? -1 : 0;
+}
+
+// This rank leaves: it never joins a later generation. 0 ok, 1 already gone.
+int shmc_leave(void* handle) {
+  Handle* h = static_cast<Handle*>(handle);
+  RankCtl* me = h->ctl(h->rank);
+  uint64_t s = me->status.load(std::memory_order_acquire);
+  while (!(s & kGone)) {
+    if (me->status.compare_exchange_weak(s, kGone | (s + 1), std::memory_order_acq_rel, std::memory_order_acquire)) return 0;
   }
-  return 0;
+  return 1;
+}
+
+void shmc_heartbeat(void* handle) {
+  Handle* h = static_cast<Handle*>(handle);
+  h->ctl(h->rank)->beat_ns.store(now_ns(), std::memory_order_release);
+}
+
+// Bitmask of the ranks that have not left (and were not evicted).
+uint64_t shmc_alive(void* handle) {
+  Handle* h = static_cast<Handle*>(handle);
+  uint64_t mask = 0;
+  for (int r = 0; r < h->world; ++r)
+    if (!(h->ctl(r)->status.load(std::memory_order_acquire) & kGone)) mask |= 1ull << r;
+  return mask;
+}
+
+// Wait until every rank left (job end: keeps the rendezvous host alive until the last rank is
+// done). 0 ok, -1 timeout.
+int shmc_wait_all_gone(void* handle, double timeout_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  return wait_until([&] { return shmc_alive(handle) == 0; }, timeout_s) ? 0 : -1;
 }
 
 // A second rank's handle onto the SAME mapping as `handle` (threads as ranks inside one process:

@@ -26,6 +26,10 @@ int shmc_unlink(const char* name);
 uint64_t shmc_slot_bytes(void* handle);
 int shmc_allgather(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, double timeout_s);
 int shmc_barrier(void* handle, double timeout_s);
+int shmc_allgather_m(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, uint64_t* members, double timeout_s, double fail_s);
+int shmc_leave(void* handle);
+uint64_t shmc_alive(void* handle);
+int shmc_wait_all_gone(void* handle, double timeout_s);
 void shmc_close(void* handle);
 }
 
@@ -87,6 +91,41 @@ int main(int argc, char** argv) {
   };
   std::vector<std::thread> threads;
   for (int r = 0; r < world; ++r) threads.emplace_back(rank_main, r);
+  for (auto& t : threads) t.join();
+
+  // membership phase: the last rank leaves after `leave_at` rounds; every survivor must see it in
+  // the participant mask until then and never after, with the same payloads; finally every rank
+  // leaves and waits for the others (the job-end protocol of Federation.shutdown)
+  const int rounds = 200, leave_at = 37;
+  const uint64_t all = (world >= 64) ? ~0ull : ((1ull << world) - 1), survivors = all & ~(1ull << (world - 1));
+  auto member_main = [&](int r) {
+    void* h = views[r];
+    std::vector<unsigned char> in(slot), out(static_cast<size_t>(world) * slot);
+    std::vector<uint64_t> lens(world);
+    for (int i = 0; i < rounds; ++i) {
+      if (r == world - 1 && i == leave_at) {
+        if (shmc_leave(h) != 0) errors.fetch_add(1);
+        break;
+      }
+      const uint64_t n = payload_len(r, i, slot - 1);
+      for (uint64_t k = 0; k < n; ++k) in[k] = payload_byte(r, i, k);
+      uint64_t mask = 0;
+      if (shmc_allgather_m(h, in.data(), n, out.data(), lens.data(), &mask, 30.0, 0.0) != 0) {
+        errors.fetch_add(1);
+        continue;
+      }
+      if (mask != (i < leave_at ? all : survivors)) errors.fetch_add(1);
+      for (int q = 0; q < world; ++q) {
+        if (!(mask >> q & 1)) continue;
+        const uint64_t m = payload_len(q, i, slot - 1);
+        if (lens[q] != m || (m && out[static_cast<size_t>(q) * slot + m - 1] != payload_byte(q, i, m - 1))) errors.fetch_add(1);
+      }
+    }
+    shmc_leave(h);
+    if (shmc_wait_all_gone(h, 30.0) != 0 || shmc_alive(h) != 0) errors.fetch_add(1);
+  };
+  threads.clear();
+  for (int r = 0; r < world; ++r) threads.emplace_back(member_main, r);
   for (auto& t : threads) t.join();
   for (int r = world - 1; r >= 0; --r) shmc_close(views[r]);  // views first, the owner unmaps last
   if (errors.load() != 0) {

@@ -55,7 +55,9 @@ class CollectiveCommunicationProtocol(InMemoryCommunicationProtocol):
     def stop(self) -> None:
         inst = Federation._instance
         if inst is not None:
-            inst.unregister_local(self.addr)
+            node = getattr(self, "node", None)
+            running = node is not None and getattr(node.state, "round", None) is not None
+            inst.unregister_local(self.addr, mid_experiment=running)
         super().stop()
 
     def handshake(self, addr: str) -> bool:

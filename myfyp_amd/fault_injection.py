@@ -15,6 +15,8 @@ it as soon as it unregisters (``Federation.unregister_local``).
 
 from __future__ import annotations
 
+import os
+import sys
 import threading
 import time
 from typing import Any, Callable, Dict, List, Optional
@@ -129,6 +131,20 @@ def kill_at(node, stage: str = "TrainStage", round: Optional[int] = 1) -> StageF
         logger.warning(n.addr, f"💥 fault injection: killing node at {stage} (round {n.state.round})")
         n.stop()
         raise _Crash(f"{n.addr} killed at {stage}")
+
+    return StageFault(node, stage, crash, round)
+
+
+def crash_process_at(node, stage: str = "TrainStage", round: Optional[int] = 1, code: int = 0) -> StageFault:
+    """Kill the whole PROCESS when ``node`` reaches ``stage`` of ``round`` — no shutdown, no
+    departure notice, heartbeats just stop (a crashed rank). The other ranks must evict it by
+    heartbeat staleness (``Settings.FAILURE_TIMEOUT``). ``code`` 0 keeps ``torchrun`` from tearing
+    down the surviving workers, as a node-level crash on another host would."""
+
+    def crash(n) -> None:
+        logger.warning(n.addr, f"💥 fault injection: process crash at {stage} (round {n.state.round})")
+        sys.stdout.flush()
+        os._exit(code)
 
     return StageFault(node, stage, crash, round)
 

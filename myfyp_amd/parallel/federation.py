@@ -13,8 +13,14 @@ the peers of all processes form one federation:
   over RCCL → scale → broadcast into every local peer's parameter row); the initial model is one
   broadcast from the initiator's rank;
 * **fault tolerance** — a gang waits at most ``Settings.AGGREGATION_TIMEOUT`` for a co-located peer
-  and then proceeds without it (the reference's "aggregate whatever arrived", ``aggregator.py:192-208``);
-  cross-rank collectives run under the process-group timeout (``Settings.COLLECTIVE_TIMEOUT``).
+  and then proceeds without it (the reference's "aggregate whatever arrived", ``aggregator.py:192-208``).
+  Across ranks, every control-plane gather is also a liveness agreement (shared-memory membership
+  protocol, ``csrc/host/shm_collective.cpp``): a rank whose last local peer stops mid-experiment
+  *departs* (it never joins another collective), a rank whose heartbeat goes stale for
+  ``Settings.FAILURE_TIMEOUT`` is evicted, and every survivor observes the same participant set at
+  the same gather; before each weight collective the survivors re-agree and, on a change, rebuild
+  their process groups over themselves (group-local rendezvous) — the reference's heartbeat
+  eviction (``heartbeater.py:94-103``) for the RCCL weights plane.
 """
 
 from __future__ import annotations
@@ -195,6 +201,12 @@ class Federation:
         self._cpu_pg = None
         self.shm = None  # node-local shared-memory control plane (single-node jobs)
         self._round_driver = None
+        # membership (fault tolerance): live ranks, device group over them (None = WORLD)
+        self.members: List[int] = list(range(world))
+        self.departed = False
+        self._pg = None
+        self._hb_stop = threading.Event()
+        self._hb_thread: Optional[threading.Thread] = None
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
@@ -257,10 +269,28 @@ class Federation:
         if any(self.store.get(f"fedhost/{r}").decode() != host for r in range(self.world)):
             return
         self.shm = ShmCollective.create(self.store, self.rank, self.world, timeout=float(Settings.COLLECTIVE_TIMEOUT))
+        if self.shm is not None:
+            self.shm.heartbeat()
+
+            def beat() -> None:
+                while not self._hb_stop.wait(0.1):
+                    shm = self.shm
+                    if shm is None:
+                        return
+                    shm.heartbeat()
+
+            self._hb_thread = threading.Thread(target=beat, name=f"fed-heartbeat-{self.rank}", daemon=True)
+            self._hb_thread.start()
 
     def shutdown(self) -> None:
-        """Stop the control bus and tear down the process group (call once, at exit)."""
+        """Leave the job, wait until every rank has left (the rendezvous store lives in rank 0's
+        process), stop the control bus and tear down the process groups (call once, at exit).
+        Departed ranks take the same path, so a job with a dead peer still ends cleanly."""
+        synced = False
         if self.shm is not None:
+            self.shm.leave()
+            synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT))
+            self._hb_stop.set()
             self.shm.close()
             self.shm = None
         if self.bus is not None:
@@ -270,7 +300,8 @@ class Federation:
             import torch.distributed as dist
 
             if dist.is_initialized():
-                dist.barrier()
+                if not synced and not self.departed:
+                    dist.barrier(group=self._pg)
                 dist.destroy_process_group()
         Federation._instance = None
 
@@ -279,6 +310,8 @@ class Federation:
         inst = cls._instance
         if inst is not None and inst.bus is not None:
             inst.bus.stop()
+        if inst is not None:
+            inst._hb_stop.set()
         if inst is not None and inst.shm is not None:
             inst.shm.close()
             inst.shm = None
@@ -355,26 +388,66 @@ class Federation:
 
         return self.gang.run(member, members, payload, fn, Settings.AGGREGATION_TIMEOUT if timeout is None else timeout)
 
-    def unregister_local(self, addr: str) -> None:
-        """A co-located peer stopped (or crashed): drop it from every future gang."""
+    def unregister_local(self, addr: str, mid_experiment: bool = False) -> None:
+        """A co-located peer stopped (or crashed): drop it from every future gang. If it was the
+        last live local peer and an experiment was running, this rank departs the federation."""
         with self._lock:
             self.local_nodes.pop(addr, None)
+            last = not self.local_nodes
         self.gang.poke()
+        if last and mid_experiment:
+            self.depart()
+
+    # ------------------------------------------------------------------ membership
+    def depart(self) -> None:
+        """This rank leaves the running experiment: it joins no further collective, and the other
+        ranks stop waiting for it at their next gather (shared-memory membership protocol)."""
+        if self.departed or self.world == 1:
+            return
+        self.departed = True
+        if self.shm is not None:
+            self.shm.leave()
+        logger.warning(f"rank{self.rank}", "last local peer stopped mid-experiment: rank departs the federation")
+
+    def _apply_members(self, ranks: List[int]) -> None:
+        """Every survivor calls this with the same participant set at the same gather."""
+        if ranks == self.members:
+            return
+        import torch.distributed as dist
+
+        gone = [r for r in self.members if r not in ranks]
+        logger.warning(f"rank{self.rank}", f"ranks {gone} left the federation; continuing over ranks {ranks}")
+        with self._lock:
+            self.members = list(ranks)
+            self.peers = {a: r for a, r in self.peers.items() if r in ranks}
+        # process groups over the survivors; group-local rendezvous (the departed ranks take no part)
+        self._pg = dist.new_group(ranks=ranks, use_local_synchronization=True)
+        self._cpu_pg = self._pg if dist.get_backend() == "gloo" else dist.new_group(ranks=ranks, backend="gloo", use_local_synchronization=True)
+        self.record("membership_change", float(len(gone)))
+
+    def sync_members(self) -> List[int]:
+        """Liveness agreement right before a weight collective (a peer may have died since the
+        round's vote gather): every survivor leaves with the same member list and process group."""
+        if self.world > 1 and not self.departed and self.shm is not None:
+            ranks, _ = self.shm.allgather_members(None, float(Settings.FAILURE_TIMEOUT))
+            self._apply_members(ranks)
+        return self.members
 
     def all_gather_object(self, obj: Any) -> List[Any]:
         """Control-plane gather (votes, wire models) over a CPU (gloo) group: an object gather on the
         RCCL group would pickle through device memory and synchronise the host with every queued
         kernel, stalling the asynchronous round pipeline."""
-        if self.world == 1:
+        if self.world == 1 or self.departed:
             return [obj]
         if self.shm is not None:
-            got = self.shm.allgather_object(obj)
+            ranks, got = self.shm.allgather_members(obj, float(Settings.FAILURE_TIMEOUT))
+            self._apply_members(ranks)
             if got is not None:
-                return got
-            # some rank's payload exceeded the shared slot: every rank takes the gloo path together
+                return [got[r] for r in ranks]
+            # some rank's payload exceeded the shared slot: every member takes the gloo path together
         import torch.distributed as dist
 
-        out: List[Any] = [None] * self.world
+        out: List[Any] = [None] * len(self.members)
         dist.all_gather_object(out, obj, group=self._cpu_group())
         return out
 
@@ -398,35 +471,50 @@ class Federation:
             self._cpu_pg = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
         return self._cpu_pg
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place SUM all-reduce over RCCL (bucketed for large buffers)."""
-        if self.world == 1:
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place all-reduce over RCCL among the live ranks (bucketed for large buffers)."""
+        if self.world == 1 or self.departed:
             return t
         import torch.distributed as dist
 
+        rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
         flat = t.view(-1)
         bucket = max(1, Settings.BUCKET_BYTES // flat.element_size())
         if flat.numel() <= bucket:
-            dist.all_reduce(flat)
+            dist.all_reduce(flat, op=rop, group=self._pg)
         else:
-            works = [dist.all_reduce(flat[i : i + bucket], async_op=True) for i in range(0, flat.numel(), bucket)]
+            works = [dist.all_reduce(flat[i : i + bucket], op=rop, group=self._pg, async_op=True) for i in range(0, flat.numel(), bucket)]
             for w in works:
                 w.wait()
         return t
 
     def broadcast_(self, t: torch.Tensor, src_rank: int) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 or self.departed:
             return t
         import torch.distributed as dist
 
-        dist.broadcast(t, src=src_rank)
+        dist.broadcast(t, src=src_rank, group=self._pg)
         return t
 
-    def barrier(self) -> None:
-        if self.world > 1:
-            import torch.distributed as dist
+    @property
+    def solo(self) -> bool:
+        """No other live rank to exchange weights with."""
+        return self.world == 1 or self.departed or self.members == [self.rank]
 
-            dist.barrier()
+    @property
+    def group(self):
+        """Device process group over the live ranks (None = the default group)."""
+        return self._pg
+
+    def barrier(self) -> None:
+        if self.world == 1 or self.departed:
+            return
+        if self.shm is not None:
+            self.sync_members()
+            return
+        import torch.distributed as dist
+
+        dist.barrier(group=self._pg)
 
     def record(self, name: str, seconds: float) -> None:
         self.stats.setdefault(name, []).append(seconds)

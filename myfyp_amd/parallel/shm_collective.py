@@ -16,7 +16,7 @@ import ctypes
 import os
 import pickle
 import secrets
-from typing import Any, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from myfyp_amd.management.logger import logger
 
@@ -50,6 +50,16 @@ def _load() -> Optional[ctypes.CDLL]:
     lib.shmc_allgather.argtypes = [vp, ctypes.c_char_p, u64, vp, ctypes.POINTER(u64), d]
     lib.shmc_barrier.restype = i
     lib.shmc_barrier.argtypes = [vp, d]
+    lib.shmc_allgather_m.restype = i
+    lib.shmc_allgather_m.argtypes = [vp, ctypes.c_char_p, u64, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), d, d]
+    lib.shmc_leave.restype = i
+    lib.shmc_leave.argtypes = [vp]
+    lib.shmc_heartbeat.restype = None
+    lib.shmc_heartbeat.argtypes = [vp]
+    lib.shmc_alive.restype = u64
+    lib.shmc_alive.argtypes = [vp]
+    lib.shmc_wait_all_gone.restype = i
+    lib.shmc_wait_all_gone.argtypes = [vp, d]
     lib.shmc_close.restype = None
     lib.shmc_close.argtypes = [vp]
     _LIB = lib
@@ -120,6 +130,38 @@ class ShmCollective:
         if parts is None:
             return None
         return [pickle.loads(p) for p in parts]  # payloads written by this job's own ranks
+
+    # ------------------------------------------------------------------ membership (fault tolerance)
+    def allgather_members(self, obj: Any, fail_s: float) -> Tuple[List[int], Optional[Dict[int, Any]]]:
+        """All-gather over the ranks still in the job: (participant ranks, {rank: payload}) — the
+        same participant set on every survivor. A rank whose heartbeat is older than ``fail_s`` is
+        evicted. Payload dict None (on every participant) if one payload overflowed its slot."""
+        mask = ctypes.c_uint64(0)
+        data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        rc = self._lib.shmc_allgather_m(self._h, data, len(data), ctypes.addressof(self._out), self._lens, ctypes.byref(mask), self.timeout, fail_s)
+        if rc == -3:
+            raise RuntimeError("this rank left the federation (or was evicted as unresponsive)")
+        if rc < 0:
+            raise TimeoutError(f"shared-memory all-gather timed out after {self.timeout}s")
+        ranks = [r for r in range(self.world) if mask.value >> r & 1]
+        if rc == 1:
+            return ranks, None
+        base = ctypes.addressof(self._out)
+        return ranks, {r: pickle.loads(ctypes.string_at(base + r * self.slot, int(self._lens[r]))) for r in ranks}
+
+    def leave(self) -> bool:
+        """Leave the job: later all-gathers of the other ranks no longer wait for this one."""
+        return self._lib.shmc_leave(self._h) == 0
+
+    def heartbeat(self) -> None:
+        self._lib.shmc_heartbeat(self._h)
+
+    def alive(self) -> List[int]:
+        m = int(self._lib.shmc_alive(self._h))
+        return [r for r in range(self.world) if m >> r & 1]
+
+    def wait_all_gone(self, timeout: float) -> bool:
+        return self._lib.shmc_wait_all_gone(self._h, timeout) == 0
 
     def barrier(self) -> None:
         if self._lib.shmc_barrier(self._h, self.timeout) != 0:

@@ -44,7 +44,8 @@ def _stacked_group(learners) -> Optional[Any]:
 def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str) -> None:
     """Every peer adopts the initiator's weights: local copy + one RCCL broadcast per tensor."""
     learners = {a: fed.local_nodes[a].learner for a in arrived if a in fed.local_nodes}
-    src_rank = fed.peers.get(initiator, 0)
+    fed.sync_members()
+    src_rank = fed.peers.get(initiator, min(fed.members))
     ref_addr = initiator if initiator in learners else next(iter(learners))
     src = state_tensors(learners[ref_addr])
     bufs = [t.detach().clone() for t in src]
@@ -74,6 +75,7 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     """Sample-weighted mean of the trainers' models (weight 0 for non-trainers), result into every
     local peer. One local weighted reduction kernel + one all-reduce + one broadcast kernel."""
     t0 = time.perf_counter()
+    fed.sync_members()  # a rank may have lost its last peer since the vote: agree on the survivors
     addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
     learners = [fed.local_nodes[a].learner for a in addrs]
     weights = [float(arrived[a][0]) for a in addrs]
@@ -92,7 +94,7 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
         n = group.numel
         fast = ops.fast_lib()
         stream = torch.cuda.current_stream(dev).cuda_stream
-        if fed.world == 1:  # nothing to all-reduce: weighted mean and write-back in one launch
+        if fed.solo:  # nothing to all-reduce: weighted mean and write-back in one launch
             ops.check(fast.myfyp_fedavg_stacked_local(group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, mask.ctypes.data, stream),
                       "fedavg_local")
         else:
@@ -156,6 +158,7 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
     grouped batch of point-to-point sends/receives (RCCL over xGMI; gloo on CPU). Every rank calls
     this with the same peer list, so the P2P pattern matches by construction."""
     t0 = time.perf_counter()
+    fed.sync_members()
     peers = fed.all_peers()
     index = {a: i for i, a in enumerate(peers)}
     w = aggregator.mixing_matrix(len(peers))
@@ -165,7 +168,7 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
         return []
     learners = [fed.local_nodes[a].learner for a in local]
     group = _stacked_group(learners)
-    if fed.world == 1 and group is not None and group.params.is_cuda and group.capacity <= 16 and group.S % 4 == 0:
+    if fed.solo and group is not None and group.params.is_cuda and group.capacity <= 16 and group.S % 4 == 0:
         # every neighbour is a row of the same stacked engine buffer: the whole mixing step is one
         # in-place kernel (row p <- Σ_q M[p, q] row q); no per-peer pack / average / unpack launches
         mix = np.zeros((group.capacity, group.capacity), dtype=np.float32)
@@ -200,8 +203,9 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
         import torch.distributed as dist
 
         # per rank pair, sends and receives are both ordered by the source peer's index (NCCL ignores tags)
-        ops_ = [dist.P2POp(dist.isend, t, rb, tag=index[a]) for (a, rb), t in sorted(sends.items(), key=lambda kv: (index[kv[0][0]], kv[0][1]))]
-        ops_ += [dist.P2POp(dist.irecv, t, fed.peers[b], tag=index[b]) for b, t in sorted(recvs.items(), key=lambda kv: index[kv[0]])]
+        pg = fed.group
+        ops_ = [dist.P2POp(dist.isend, t, rb, group=pg, tag=index[a]) for (a, rb), t in sorted(sends.items(), key=lambda kv: (index[kv[0][0]], kv[0][1]))]
+        ops_ += [dist.P2POp(dist.irecv, t, fed.peers[b], group=pg, tag=index[b]) for b, t in sorted(recvs.items(), key=lambda kv: index[kv[0]])]
         for req in dist.batch_isend_irecv(ops_):
             req.wait()
     src = dict(rows)

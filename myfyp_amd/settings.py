@@ -93,6 +93,8 @@ class Settings:
     GROUP_PEERS: bool = True  # train co-located peers in one grouped launch
     GANG_WINDOW: float = 0.05  # seconds a grouped fit waits for expected co-located peers
     COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
+    # a rank whose control-plane heartbeat is older than this is evicted from the federation (s)
+    FAILURE_TIMEOUT: float = 60
     BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
     SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
@@ -171,6 +173,7 @@ class Settings:
             "GROUP_PEERS": "GROUP_PEERS",
             "GANG_WINDOW": "GANG_WINDOW",
             "COLLECTIVE_TIMEOUT": "COLLECTIVE_TIMEOUT",
+            "FAILURE_TIMEOUT": "FAILURE_TIMEOUT",
             "BUCKET_BYTES": "BUCKET_BYTES",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",

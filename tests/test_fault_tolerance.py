@@ -1,0 +1,49 @@
+"""Cross-rank fault tolerance of the collective weights plane (BASELINE config 5
+"1-peer dropout" at one peer per rank): 3 ranks × 1 peer over gloo on the CPU; rank 2's only peer
+is killed at TrainStage of round 1. Rank 2 departs; ranks 0 and 1 agree on the survivors at their
+next gather, rebuild their process groups and finish every round with equal models, well before
+AGGREGATION_TIMEOUT / COLLECTIVE_TIMEOUT (300 s)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+def test_three_ranks_one_dies_survivors_finish():
+    env = dict(os.environ, ROUNDS="3", KILL_RANK="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+           "--master-port", str(29900 + os.getpid() % 90), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    outs = {o["rank"]: o for o in (json.loads(l) for l in res.stdout.splitlines() if l.startswith("{"))}
+    assert set(outs) == {0, 1, 2}, outs
+    assert outs[2]["killed"] and outs[2]["departed"]
+    for r in (0, 1):
+        o = outs[r]
+        assert o["finished_rounds"] == 3, o
+        assert o["members"] == [0, 1], o
+        assert o["elapsed"] < 60, o  # no aggregation / collective timeout was waited out
+    assert abs(outs[0]["checksum"] - outs[1]["checksum"]) < 1e-3 * max(1.0, abs(outs[0]["checksum"])), outs
+    assert abs(outs[0]["absmax"] - outs[1]["absmax"]) < 1e-6, outs
+
+
+@pytest.mark.slow
+def test_three_ranks_one_process_crashes_survivors_evict_it():
+    """Rank 2's PROCESS dies at TrainStage of round 1 without any notice: the survivors evict it
+    once its heartbeat is FAILURE_TIMEOUT (3 s) stale and finish every round."""
+    env = dict(os.environ, ROUNDS="3", KILL_RANK="2", KILL_MODE="crash", FAILURE_TIMEOUT="3", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+           "--master-port", str(29800 + os.getpid() % 90), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    outs = {o["rank"]: o for o in (json.loads(l) for l in res.stdout.splitlines() if l.startswith("{"))}
+    assert set(outs) == {0, 1}, outs  # the crashed rank printed nothing
+    for r in (0, 1):
+        assert outs[r]["finished_rounds"] == 3 and outs[r]["members"] == [0, 1], outs[r]
+        assert outs[r]["elapsed"] < 60, outs[r]
+    assert abs(outs[0]["absmax"] - outs[1]["absmax"]) < 1e-6, outs

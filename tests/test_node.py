@@ -70,9 +70,10 @@ def test_gossip_convergence(data, n, r):
         logs = logger.get_global_logs()[exp]
         for nd in nodes:
             acc = dict(logs[nd.addr]["test_metric"])
-            # reference bar: > 0.5 (test/node_test.py:128-132); synthetic data + raw 0..255 inputs
-            # learn slower than real MNIST at batch 1, so the bar is applied to the final model
-            assert acc[r] > 0.5 and acc[r] > acc[0], acc
+            # reference bar (test/node_test.py:128-132): test_metric logged at round index 1 — the
+            # model after the first aggregated round — above 0.5 on every node
+            assert acc[1] > 0.5, acc
+            assert acc[r] > acc[0], acc
     finally:
         for nd in nodes:
             nd.stop()
