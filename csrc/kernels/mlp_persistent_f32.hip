@@ -35,6 +35,23 @@
 #include "mlp_persistent.h"
 #include "persist_common.h"
 
+// Optional phase timestamps (build with -DMLP_STAMPS): peer 0's owner 0 (role 0) and head 0 (role 1),
+// steps < 32, read with mlp_debug_persistent_f32_stamps (wall_clock64 ticks, 100 MHz).
+#ifdef MLP_STAMPS
+__device__ unsigned long long g_p32_stamps[2][32][10];
+#define P32_STAMP(role, t, i)                                                                   \
+  do {                                                                                          \
+    if (p == 0 && threadIdx.x == 0 && (t) < 32) g_p32_stamps[role][t][i] = wall_clock64(); \
+  } while (0)
+extern "C" int mlp_debug_persistent_f32_stamps(void* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p32_stamps), sizeof(g_p32_stamps)) == hipSuccess ? 0 : 1;
+}
+#else
+#define P32_STAMP(role, t, i) \
+  do {                        \
+  } while (0)
+#endif
+
 namespace {
 
 using persist::al16;
@@ -319,6 +336,28 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
     for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, acc[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_p, inv_p, wdmu);
   };
+  // forward contribution of this wave's K step q (slot q) to the H1 slice, with the weights as they
+  // are now and the batch tile currently staged in LDS
+  auto fwd_kstep = [&](int q, f32x4(&acc)[MT]) {
+    const int s = wave + 8 * q;
+    if (s >= KS1) return;
+    // lane coordinates laundered per K step: the compiler would otherwise hoist every LDS address
+    // of the loop out of it and spill them
+    int lq = lane;
+    asm volatile("" : "+v"(lq));
+    const int hq = lq >> 4, cq = lq & 15;
+    float wq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wq[j] = q < RQ ? w1[q < RQ ? q : 0][j] : sW1x[cq * 32 + kappa(hq, j)];
+    bf16x8 bh, bm, bl;
+    split3(wq, bh, bm, bl);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * hq;
+      const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
+      acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
+    }
+  };
   __syncthreads();  // sW1x written
 
   for (int t = 0; t < nsteps; ++t) {
@@ -328,6 +367,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     float lr_t, inv_bc2;
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
     float* sH1c = sH1 + (t & 1) * BP * 16;
+    if (g == 0) P32_STAMP(0, t, 0);
 
     // ================= A: H1 slice = relu(X · W1sliceᵀ + b1), split-K over the 8 waves
     {
@@ -336,25 +376,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int s = wave + 8 * q;
-        if (s < KS1) {
-          // lane coordinates laundered per K step: the compiler would otherwise hoist every LDS
-          // address of the loop out of it and spill them
-          int lq = lane;
-          asm volatile("" : "+v"(lq));
-          const int hq = lq >> 4, cq = lq & 15;
-          float wq[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) wq[j] = q < RQ ? w1[q < RQ ? q : 0][j] : sW1x[cq * 32 + kappa(hq, j)];
-          bf16x8 bh, bm, bl;
-          split3(wq, bh, bm, bl);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * hq;
-            const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
-            acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
-          }
-        }
+        fwd_kstep(q, acc);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -374,10 +396,13 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         st_wt32(pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + cc, v);
       }
     }
+    if (g == 0) P32_STAMP(0, t, 1);
     persist::publish(pb.flags, FPP, p, F_H1 + g, (unsigned)(t + 1));
+    if (g == 0) P32_STAMP(0, t, 2);
 
     // the previous step's W2-replica update runs while the heads work on this step's H1
     if (t > 0) w2_replica_update(t - 1);
+    if (g == 0) P32_STAMP(0, t, 3);
 
     // next step's batch: pull this wave's columns into the XCD's L2 (staged after the dW1 MFMAs)
     const bool more = t + 1 < nsteps;
@@ -396,6 +421,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 
     // ================= C: backward of this slice
     if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (g == 0) P32_STAMP(0, t, 4);
     {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2, BP * PD2 * 4);
       float4 v[BP / 16];
@@ -446,6 +472,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       *reinterpret_cast<bf16x4*>(sD3 + 32 * LDT + off) = dl;
     }
     lds_barrier();
+    if (g == 0) P32_STAMP(0, t, 5);
     // C2 (every wave, its own K steps): dW1 rows (and db1, in the bias slot) against the exact
     // three-term split of dH1, W1 update, the next batch's columns staged right after this K
     // step's reads
@@ -468,7 +495,11 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
           for (int kk = 0; kk < XQ; ++kk) {
             const int idx = kk * 64 + lv;
             const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+#ifdef P32_EXP_NOX  // timing experiment: no next-batch staging loads
+            xq[kk] = uint4{(unsigned)lv, 0u, 0u, 0u};
+#else
             xq[kk] = (more && col < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + col)) : uint4{0u, 0u, 0u, 0u};
+#endif
           }
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt) {
@@ -479,9 +510,14 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
                           ld8(dfrag + 32 * LDT + 32 * kb), acc);
             if (q < RQ) {
               const int qq = q < RQ ? q : 0;
+#ifdef P32_EXP_NOADAM  // timing experiment: plain SGD in place of the Adam epilogue
+#pragma unroll
+              for (int i = 0; i < 4; ++i) w1[qq][4 * tt + i] -= 1e-9f * acc[i];
+#else
 #pragma unroll
               for (int i = 0; i < 4; ++i)
                 upd32<ADAM, EXTRA>(o, acc[i], w1[qq][4 * tt + i], m1[qq][4 * tt + i], v1[qq][4 * tt + i], e1[qq][4 * tt + i], lr_t, inv_bc2, wdmu);
+#endif
             } else {  // the LDS-resident K step
               const int off = (lq & 15) * 32 + 16 * tt + 4 * (lq >> 4);
               float4 w = *reinterpret_cast<float4*>(sW1x + off), m = *reinterpret_cast<float4*>(sW1x + 512 + off),
@@ -510,6 +546,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       }
     }
     __syncthreads();
+    if (g == 0) P32_STAMP(0, t, 6);
   }
 
   // ---- write the state back (fp32 master weights and moments; b1 from the bias slot)
@@ -650,7 +687,9 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
 
     // ---- H1(t) from the 16 owners -> LDS (16-byte sc1 loads)
+    if (hd == 0) P32_STAMP(1, t, 0);
     if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (hd == 0) P32_STAMP(1, t, 1);
     {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + (int64_t)p * BP * PD1, BP * PD1 * 4);
       float4 v[BP / 8];
@@ -663,6 +702,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       }
     }
     lds_barrier();
+    if (hd == 0) P32_STAMP(1, t, 2);
     // ---- H2 slice = relu(H1 · W2rowsᵀ + b2); wave w sums o1 in [32w, 32w+32) (k order 16g + 4h + i)
     {
       f32x4 acc[MT];
@@ -708,10 +748,13 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 #pragma unroll
       for (int i = 0; i < 4; ++i) st_wt32(pb.plx + (((int64_t)p * NH + hd) * BP + 16 * wave + 4 * h + i) * 16 + c, pl[i]);
     }
+    if (hd == 0) P32_STAMP(1, t, 3);
     persist::publish(pb.flags, FPP, p, F_PL + hd, (unsigned)(t + 1));
+    if (hd == 0) P32_STAMP(1, t, 4);
 
     // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3
     if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (hd == 0) P32_STAMP(1, t, 5);
     if (tid < BP * 4) {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16, NH * BP * 16 * 4);
       float4 v[NH];
@@ -753,6 +796,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       }
     }
     lds_barrier();
+    if (hd == 0) P32_STAMP(1, t, 6);
     // ---- dH2 slice = dlogits · W3[:, slice] ⊙ [H2 > 0]  (K = classes, natural order)
     if (wave < MT) {
       f32x4 acc = zero4();
@@ -768,6 +812,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       }
     }
     persist::publish(pb.flags, FPP, p, F_DH2 + hd, (unsigned)(t + 1));
+    if (hd == 0) P32_STAMP(1, t, 7);
 
     // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
     //      b2 (wave 1), b3 (wave 2, the same arithmetic in every head)
@@ -803,6 +848,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       if (lane < 16 && cin) upd32<ADAM, EXTRA>(o, acc[0], sB3[c], sB3[16 + c], sB3[32 + c], sB3[48 + c], lr_t, inv_bc2, wdmu);
     }
     __syncthreads();
+    if (hd == 0) P32_STAMP(1, t, 8);
   }
 
   // ---- write back W2 rows, b2, the W3 slice, b3 (head 0) and the epoch's loss / accuracy sums

@@ -61,10 +61,13 @@ def build(verbose: bool = False, jobs: int = 8, variant: str = "") -> str:
     ``MYFYP_NATIVE_LIB``)."""
     hipcc = _hipcc()
     obj_dir, lib, extra = OBJ_DIR, LIB, ()
-    if variant == "stamps":
-        obj_dir = os.path.join(ROOT, "build", "obj_stamps")
-        lib = os.path.join(ROOT, "build", "stamps", "libmyfyp_hip.so")
-        extra = ("-DMLP_STAMPS",)
+    if variant:
+        # "stamps" or "stamps+NAME=VAL+NAME2" (extra -D macros for timing-only experiment builds)
+        parts = variant.split("+")
+        tag = variant.replace("+", "_").replace("=", "")
+        obj_dir = os.path.join(ROOT, "build", f"obj_{tag}")
+        lib = os.path.join(ROOT, "build", tag, "libmyfyp_hip.so")
+        extra = tuple(["-DMLP_STAMPS"] if parts[0] == "stamps" else []) + tuple(f"-D{m}" for m in parts[1:])
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sources()
