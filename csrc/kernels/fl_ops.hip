@@ -228,39 +228,62 @@ void fl_neighbor_mix(float* stacked, int P, int64_t n, int64_t ld, const MixPlan
   }
 }
 
-// per-coordinate median of K ≤ 16 models: insertion sort in registers
-__global__ __launch_bounds__(FL_BLOCK) void k_coordinate_median(float* __restrict__ out, const uint64_t* __restrict__ srcs, int K, int64_t n) {
+// per-coordinate median of K ≤ 16 models: branch-free compare-exchange network over K registers,
+// the result stored into P destination rows (every peer that takes the aggregate). Row pointers
+// travel as kernel arguments (no pointer table on the device, no H2D copy); each thread loads its
+// coordinate from every row before storing, so destinations may alias sources.
+template <int K>
+__global__ __launch_bounds__(FL_BLOCK) void k_coordinate_median(OutPtrs outs, int P, RowPtrs rows, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
   for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
-    float v[16];
+    float v[K];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = k < K ? reinterpret_cast<const float*>(srcs[k])[i] : INFINITY;
-    // branch-free bubble network over 16 slots (padding = +inf sorts last)
+    for (int k = 0; k < K; ++k) v[k] = rows.p[k][i];
 #pragma unroll
-    for (int a = 0; a < 16; ++a) {
+    for (int a = 0; a < K; ++a) {
 #pragma unroll
-      for (int b = 0; b < 15 - a; ++b) {
+      for (int b = 0; b < K - 1 - a; ++b) {
         const float lo = fminf(v[b], v[b + 1]);
-        const float hi = fmaxf(v[b], v[b + 1]);
+        v[b + 1] = fmaxf(v[b], v[b + 1]);
         v[b] = lo;
-        v[b + 1] = hi;
       }
     }
-    float med;
-    if (K & 1) {
-      med = v[0];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) if (k == (K - 1) / 2) med = v[k];
-    } else {
-      float a0 = v[0], a1 = v[0];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (k == K / 2 - 1) a0 = v[k];
-        if (k == K / 2) a1 = v[k];
-      }
-      med = 0.5f * (a0 + a1);
+    const float med = (K & 1) ? v[(K - 1) / 2] : 0.5f * (v[K / 2 - 1] + v[K / 2]);
+    for (int p = 0; p < P; ++p) outs.p[p][i] = med;
+  }
+}
+
+// SCAFFOLD (Karimireddy et al.) server step in two launches around one all-reduce; float4 body,
+// scalar tail. Sums run in the same k order as the host reference.
+__global__ __launch_bounds__(FL_BLOCK) void k_scaffold_reduce(float* __restrict__ buf, RowPtrs dy, RowPtrs dc, RowW w, int K, int64_t n) {
+  const int64_t gid = (int64_t)blockIdx.x * FL_BLOCK + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = gid; i < n; i += stride) {
+    float sy = 0.f, sc = 0.f;
+    for (int k = 0; k < K; ++k) {
+      sy = fmaf(w.w[k], dy.p[k][i], sy);
+      sc += dc.p[k][i];
     }
-    out[i] = med;
+    buf[i] = sy;
+    buf[n + 1 + i] = sc;
+  }
+  if (gid == 0) {
+    float ws = 0.f;
+    for (int k = 0; k < K; ++k) ws += w.w[k];
+    buf[n] = ws;
+    buf[2 * n + 1] = (float)K;
+  }
+}
+
+__global__ __launch_bounds__(FL_BLOCK) void k_scaffold_apply(OutPtrs outs, int P, const float* __restrict__ x_start, const float* __restrict__ buf,
+                                                             float* __restrict__ c, int c_init, float glr, int64_t n) {
+  const float scale = glr / fmaxf(buf[n], 1e-12f);
+  const float inv_cnt = 1.f / fmaxf(buf[2 * n + 1], 1.f);
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = (int64_t)blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    const float x = fmaf(buf[i], scale, x_start[i]);
+    for (int p = 0; p < P; ++p) outs.p[p][i] = x;
+    c[i] = (c_init ? 0.f : c[i]) + buf[n + 1 + i] * inv_cnt;
   }
 }
 
@@ -315,8 +338,22 @@ void fl_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int64
   if (gx > 256) gx = 256;
   hipLaunchKernelGGL(k_broadcast_rows, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, src, P, n, ld, mask);
 }
-void fl_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(k_coordinate_median, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, out, srcs, K, n);
+void fl_coordinate_median(const OutPtrs& outs, int P, const RowPtrs& rows, int K, int64_t n, hipStream_t s) {
+  const dim3 g(grid_for(n)), b(FL_BLOCK);
+  switch (K) {
+#define MED_CASE(KK) \
+  case KK: hipLaunchKernelGGL(k_coordinate_median<KK>, g, b, 0, s, outs, P, rows, n); break;
+    MED_CASE(1) MED_CASE(2) MED_CASE(3) MED_CASE(4) MED_CASE(5) MED_CASE(6) MED_CASE(7) MED_CASE(8)
+    MED_CASE(9) MED_CASE(10) MED_CASE(11) MED_CASE(12) MED_CASE(13) MED_CASE(14) MED_CASE(15) MED_CASE(16)
+#undef MED_CASE
+    default: break;
+  }
+}
+void fl_scaffold_reduce(float* buf, const RowPtrs& dy, const RowPtrs& dc, const RowW& w, int K, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scaffold_reduce, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, buf, dy, dc, w, K, n);
+}
+void fl_scaffold_apply(const OutPtrs& outs, int P, const float* x_start, const float* buf, float* c, int c_init, float glr, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scaffold_apply, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, outs, P, x_start, buf, c, c_init, glr, n);
 }
 void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shadow, int64_t n, const OptParams& o, int step, const float* anchor,
                  const float* cg, const float* cl, hipStream_t s) {

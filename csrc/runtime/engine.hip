@@ -442,12 +442,46 @@ int myfyp_neighbor_mix_stacked(float* stacked, int P, int64_t n, int64_t ld, con
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+// Row-pointer arguments below are HOST arrays of device pointers; they travel as kernel arguments.
+static bool rows_ok(int k, const char* what) {
+  if (k >= 1 && k <= 16) return true;
+  g_last_error = std::string(what) + " supports 1..16 rows";
+  return false;
+}
+int myfyp_coordinate_median_multi(const uint64_t* outs, int P, const uint64_t* srcs, int K, int64_t n, void* stream) {
+  if (!rows_ok(K, "coordinate_median") || !rows_ok(P, "coordinate_median outputs")) return 2;
+  RowPtrs rows{};
+  OutPtrs o{};
+  for (int k = 0; k < K; ++k) rows.p[k] = reinterpret_cast<const float*>(srcs[k]);
+  for (int p = 0; p < P; ++p) o.p[p] = reinterpret_cast<float*>(outs[p]);
+  fl_coordinate_median(o, P, rows, K, n, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
 int myfyp_coordinate_median(float* out, const uint64_t* srcs, int K, int64_t n, void* stream) {
-  if (K < 1 || K > 16) {
-    g_last_error = "coordinate_median supports 1..16 models";
+  return myfyp_coordinate_median_multi((const uint64_t*)&out, 1, srcs, K, n, stream);
+}
+int myfyp_scaffold_reduce(float* buf, const uint64_t* dy, const uint64_t* dc, const float* w, int K, int64_t n, void* stream) {
+  if (K < 0 || K > 16) {
+    g_last_error = "scaffold_reduce supports 0..16 rows";
     return 2;
   }
-  fl_coordinate_median(out, srcs, K, n, (hipStream_t)stream);
+  RowPtrs y{}, c{};
+  RowW ww{};
+  for (int k = 0; k < K; ++k) {
+    y.p[k] = reinterpret_cast<const float*>(dy[k]);
+    c.p[k] = reinterpret_cast<const float*>(dc[k]);
+    ww.w[k] = w[k];
+  }
+  fl_scaffold_reduce(buf, y, c, ww, K, n, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int myfyp_scaffold_apply(const uint64_t* outs, int P, const float* x_start, const float* buf, float* c, int c_init, float glr, int64_t n, void* stream) {
+  if (!rows_ok(P, "scaffold_apply outputs")) return 2;
+  OutPtrs o{};
+  for (int p = 0; p < P; ++p) o.p[p] = reinterpret_cast<float*>(outs[p]);
+  fl_scaffold_apply(o, P, x_start, buf, c, c_init, glr, n, (hipStream_t)stream);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

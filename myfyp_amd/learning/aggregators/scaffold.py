@@ -21,6 +21,9 @@ class Scaffold(Aggregator):
     """Karimireddy et al., 2020 — https://arxiv.org/abs/1910.06378."""
 
     REQUIRED_INFO_KEYS = ["delta_y_i", "delta_c_i"]
+    # collective plane: two device all-reduces (n-weighted Δy, mean Δc) + axpy, no host copies
+    # (parallel/weights_plane.py: aggregate_scaffold)
+    collective_kind = "scaffold"
 
     def __init__(self, node_name: str = "unknown", global_lr: float = 0.1) -> None:
         super().__init__(node_name)

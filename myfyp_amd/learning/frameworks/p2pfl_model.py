@@ -45,6 +45,18 @@ def safe_loads(data: bytes) -> Any:
     return _SafeUnpickler(io.BytesIO(data)).load()
 
 
+def _to_host(obj: Any) -> Any:
+    """Callback info may hold device tensors (SCAFFOLD Δy/Δc stay on the GPU between rounds); the
+    wire/checkpoint format carries numpy arrays only — converted here, at the boundary."""
+    if isinstance(obj, dict):
+        return {k: _to_host(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_host(v) for v in obj)
+    if type(obj).__module__.startswith("torch") and hasattr(obj, "detach"):
+        return obj.detach().cpu().numpy()
+    return obj
+
+
 class P2PFLModel:
     """Holds parameters (as numpy on the wire), contributors, sample count and callback info."""
 
@@ -71,7 +83,7 @@ class P2PFLModel:
     def encode_parameters(self, params: Optional[List[np.ndarray]] = None) -> bytes:
         if params is None:
             params = self.get_parameters()
-        return pickle.dumps({"params": params, "additional_info": self.additional_info})
+        return pickle.dumps({"params": params, "additional_info": _to_host(self.additional_info)})
 
     def decode_parameters(self, data: bytes) -> Tuple[List[np.ndarray], Dict[str, Any]]:
         try:

@@ -37,6 +37,8 @@ def _flat_to_list(flat: torch.Tensor, learner) -> list:
 
 
 def _list_to_flat(arrs, like: torch.Tensor) -> torch.Tensor:
+    if len(arrs) and isinstance(arrs[0], torch.Tensor):  # device-resident (collective plane)
+        return torch.cat([a.detach().reshape(-1).to(device=like.device, dtype=torch.float32) for a in arrs])
     return torch.cat([torch.as_tensor(np.asarray(a), dtype=torch.float32).reshape(-1) for a in arrs]).to(like.device)
 
 
@@ -48,6 +50,8 @@ class SCAFFOLDCallback(TorchCallback):
         self.c_i: Optional[torch.Tensor] = None
         self.c: Optional[torch.Tensor] = None
         self.x0: Optional[torch.Tensor] = None
+        self.delta_y: Optional[torch.Tensor] = None
+        self.delta_c: Optional[torch.Tensor] = None
 
     @staticmethod
     def get_name() -> str:
@@ -71,10 +75,14 @@ class SCAFFOLDCallback(TorchCallback):
         y = learner.flat_params().detach()
         k = max(1, steps)
         c_new = self.c_i - self.c + (self.x0 - y) / (k * lr)
-        delta_c = c_new - self.c_i
+        # Δy / Δc stay device flats (one elementwise pass each, no host copy): the collective
+        # SCAFFOLD reduction (weights_plane.aggregate_scaffold) all-reduces them on the GPU; the
+        # per-layer entries are views of these flats, converted to numpy only at the wire boundary
+        self.delta_y = y - self.x0
+        self.delta_c = c_new - self.c_i
         self.c_i = c_new
-        self.additional_info["delta_y_i"] = _flat_to_list(y - self.x0, learner)
-        self.additional_info["delta_c_i"] = _flat_to_list(delta_c, learner)
+        self.additional_info["delta_y_i"] = learner.split_flat(self.delta_y)
+        self.additional_info["delta_c_i"] = learner.split_flat(self.delta_c)
 
     def state_dict(self) -> dict:
         return {} if self.c_i is None else {"c_i": self.c_i.detach().cpu().numpy()}

@@ -108,7 +108,9 @@ def save_checkpoint(learner, directory: str, exp_name: str, addr: str, round: in
 def _encode_with_info(model, info: Dict[str, Any]) -> bytes:
     import pickle
 
-    return pickle.dumps({"params": model.get_parameters(), "additional_info": info})
+    from myfyp_amd.learning.frameworks.p2pfl_model import _to_host
+
+    return pickle.dumps({"params": model.get_parameters(), "additional_info": _to_host(info)})
 
 
 def latest_checkpoint(directory: str, exp_name: str, addr: str) -> Optional[str]:

@@ -17,6 +17,7 @@ Ops
 
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Sequence
 
 import torch
@@ -127,14 +128,69 @@ def coordinate_median(param_lists: Sequence[Sequence[torch.Tensor]]) -> List[tor
             med = s[(k - 1) // 2] if k % 2 else 0.5 * (s[k // 2 - 1] + s[k // 2])
             out.append(med.to(param_lists[0][layer].dtype))
         return out
-    lib = _lib()
     for layer in range(len(param_lists[0])):
-        srcs = [p[layer].contiguous().float() for p in param_lists]
+        srcs = [p[layer].contiguous().float().reshape(-1) for p in param_lists]
         dst = torch.empty_like(srcs[0])
-        ptrs = torch.tensor([s.data_ptr() for s in srcs], dtype=torch.int64, device=dev)
-        _native.check(lib.myfyp_coordinate_median(dst.data_ptr(), ptrs.data_ptr(), k, dst.numel(), _stream()), "coordinate_median")
-        out.append(dst.to(param_lists[0][layer].dtype))
+        median_into(srcs, [dst])
+        out.append(dst.view_as(param_lists[0][layer]).to(param_lists[0][layer].dtype))
     return out
+
+
+def _host_ptrs(ts: Sequence[torch.Tensor]) -> ctypes.c_void_p:
+    """Host table of device row pointers (the native entry points pass it as a kernel argument)."""
+    arr = (ctypes.c_uint64 * max(1, len(ts)))(*[t.data_ptr() for t in ts])
+    return ctypes.cast(arr, ctypes.c_void_p), arr  # keep arr alive across the call
+
+
+def median_into(rows: Sequence[torch.Tensor], outs: Sequence[torch.Tensor]) -> None:
+    """``outs[p] = coordinate-wise median(rows)`` for 1-D fp32 rows; on the GPU one launch
+    (``k_coordinate_median<K>``) for K <= 16 rows and <= 16 outputs, which may alias the rows."""
+    k = len(rows)
+    if rows[0].device.type == "cuda" and k <= 16 and len(outs) <= 16 and all(t.is_contiguous() and t.dtype == torch.float32 for t in [*rows, *outs]):
+        src, keep_s = _host_ptrs(rows)
+        dst, keep_d = _host_ptrs(outs)
+        _native.check(_lib().myfyp_coordinate_median_multi(dst, len(outs), src, k, rows[0].numel(), _stream()), "coordinate_median_multi")
+        return
+    s, _ = torch.sort(torch.stack([r.float() for r in rows]), dim=0)
+    med = s[(k - 1) // 2] if k % 2 else 0.5 * (s[k // 2 - 1] + s[k // 2])
+    for o in outs:
+        o.copy_(med)
+
+
+def scaffold_reduce(buf: torch.Tensor, dys: Sequence[torch.Tensor], dcs: Sequence[torch.Tensor], weights: Sequence[float]) -> None:
+    """``buf = [Σ w_k Δy_k | Σ w_k | Σ Δc_k | K]`` (2n + 2 floats) from the local contributors."""
+    n = (buf.numel() - 2) // 2
+    k = len(dys)
+    if buf.device.type == "cuda" and k <= 16:
+        y, keep_y = _host_ptrs(dys)
+        c, keep_c = _host_ptrs(dcs)
+        w = (ctypes.c_float * max(1, k))(*weights)
+        _native.check(_lib().myfyp_scaffold_reduce(buf.data_ptr(), y, c, ctypes.cast(w, ctypes.c_void_p), k, n, _stream()), "scaffold_reduce")
+        return
+    buf.zero_()
+    for dy, dc, wt in zip(dys, dcs, weights):
+        buf[:n].add_(dy, alpha=wt)
+        buf[n + 1 : 2 * n + 1].add_(dc)
+    buf[n] = float(sum(weights))
+    buf[2 * n + 1] = float(k)
+
+
+def scaffold_apply(outs: Sequence[torch.Tensor], x_start: torch.Tensor, buf: torch.Tensor, c: torch.Tensor, c_init: bool, global_lr: float) -> None:
+    """``outs[p] = x_start + η_g · buf[:n] / buf[n]``; ``c = (0 if c_init else c) + buf[n+1:2n+1] / buf[2n+1]``."""
+    n = x_start.numel()
+    if buf.device.type == "cuda" and len(outs) <= 16:
+        o, keep = _host_ptrs(outs)
+        _native.check(_lib().myfyp_scaffold_apply(o, len(outs), x_start.data_ptr(), buf.data_ptr(), c.data_ptr(), int(c_init), float(global_lr), n, _stream()),
+                      "scaffold_apply")
+        return
+    x_new = torch.addcmul(x_start, buf[:n], global_lr / buf[n : n + 1].clamp_min(1e-12))
+    dc = buf[n + 1 : 2 * n + 1] / buf[2 * n + 1 : 2 * n + 2].clamp_min(1.0)
+    if c_init:
+        c.copy_(dc)
+    else:
+        c.add_(dc)
+    for t in outs:
+        t.copy_(x_new)
 
 
 # ---------------------------------------------------------------------------------------------

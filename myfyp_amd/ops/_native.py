@@ -39,6 +39,9 @@ _SIGNATURES = {
     "myfyp_stacked_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_float, c_void_p]),
     "myfyp_broadcast_rows": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_coordinate_median": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "myfyp_coordinate_median_multi": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
+    "myfyp_scaffold_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "myfyp_scaffold_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int64, c_void_p]),
     # optimizers over flat buffers
     "myfyp_adam_step": (
         c_int,

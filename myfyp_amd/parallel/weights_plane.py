@@ -223,6 +223,115 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
     return local
 
 
+# aggregator kinds reduced on the device (no wire models, no host copies)
+DEVICE_KINDS = ("mean", "neighbor", "scaffold", "median")
+
+
+def _scaffold_cb(learner):
+    for cb in getattr(learner, "callbacks", []):
+        if cb.get_name() == "scaffold":
+            return cb
+    raise ValueError("SCAFFOLD aggregation needs the 'scaffold' callback on every learner")
+
+
+@traced("aggregate_scaffold")
+def aggregate_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> None:
+    """SCAFFOLD server step on the device (reference math: ``p2pfl/learning/aggregators/
+    scaffold.py:76-111``): x ← x_start + η_g·Σ n_i Δy_i / Σ n_i, c ← c + mean(Δc_i).
+
+    One packed device buffer [Σ n_iΔy_i | Σ n_i | Σ Δc_i | count] reduced over the local trainers,
+    ONE all-reduce over the live ranks, then every local peer's flat parameters are set to the new
+    global model and its callbacks receive the new global control variate (a device tensor).
+    x_start is a trainer's round-start snapshot (the callback's x0) or a non-trainer's current
+    weights — identical on every rank, since every peer starts the round from the last aggregate."""
+    t0 = time.perf_counter()
+    fed.sync_members()
+    addrs = [a for a in arrived if a in fed.local_nodes]
+    learners = {a: fed.local_nodes[a].learner for a in addrs}
+    flats = [learners[a].flat_params() for a in addrs]
+    n = flats[0].numel()
+    dys, dcs, ws = [], [], []
+    x_start = None
+    for a in addrs:
+        w = float(arrived[a][0])
+        cb = _scaffold_cb(learners[a])
+        if w > 0 and cb.delta_y is not None:
+            dys.append(cb.delta_y)
+            dcs.append(cb.delta_c)
+            ws.append(w)
+            if x_start is None:
+                x_start = cb.x0
+    if x_start is None:  # no local trainer: this rank's peers still hold the round-start model
+        x_start = flats[0].detach().clone()
+    # one reduction launch -> ONE all-reduce of [Σ n_iΔy_i | Σ n_i | Σ Δc_i | count] -> one apply
+    # launch that writes the new model into every local peer and updates the control variate
+    buf = torch.empty(2 * n + 2, dtype=torch.float32, device=flats[0].device)
+    ops.scaffold_reduce(buf, dys, dcs, ws)
+    fed.all_reduce_(buf)
+    c_prev = getattr(aggregator, "_c_dev", None)
+    c_init = c_prev is None or c_prev.numel() != n
+    c_new = torch.empty(n, dtype=torch.float32, device=buf.device) if c_init else c_prev
+    with torch.no_grad():
+        ops.scaffold_apply(flats, x_start, buf, c_new, c_init, aggregator.global_lr)
+    gc = learners[addrs[0]].split_flat(c_new)  # same architecture on every peer: one set of views
+    for a in addrs:
+        lr = learners[a]
+        fed.local_nodes[a].aggregator._c_dev = c_new
+        lr.get_model().add_info("scaffold", {"global_c": gc})
+        lr.update_callbacks_with_model_info()
+    fed.record("aggregate", time.perf_counter() - t0)
+
+
+@traced("aggregate_median")
+def aggregate_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None:
+    """Coordinate-wise median of the trainers' models on the device (``fedmedian.py:56-62``):
+    the local trainers' flat rows are packed into a [k_max, n] buffer, ONE all-gather over the live
+    ranks (RCCL) collects every trainer's row, and ONE ``k_coordinate_median<K>`` launch (sorting
+    network in registers, <= 16 models) writes the result into every local peer. With a single
+    rank the kernel reads the live rows directly (no packing copy)."""
+    t0 = time.perf_counter()
+    fed.sync_members()
+    addrs = [a for a in arrived if a in fed.local_nodes]
+    learners = {a: fed.local_nodes[a].learner for a in addrs}
+    trainers = [a for a in addrs if float(arrived[a][0]) > 0]
+    counts = fed.all_gather_object(len(trainers))
+    kmax = max(1, max(counts))
+    flat_only = all(len(state_tensors(learners[a])) == 1 for a in addrs)  # no floating buffers
+    rows_of = (lambda a: learners[a].flat_params()) if flat_only else (lambda a: _pack(learners[a]))
+    if fed.solo:  # every trainer is local: median straight from the live rows into every peer
+        if not trainers:
+            return
+        if flat_only:
+            ops.median_into([rows_of(a) for a in trainers], [learners[a].flat_params() for a in addrs])
+        else:
+            med = torch.empty_like(_pack(learners[addrs[0]]))
+            ops.median_into([rows_of(a) for a in trainers], [med])
+            for a in addrs:
+                _unpack_into(learners[a], med)
+        fed.record("aggregate", time.perf_counter() - t0)
+        return
+    import torch.distributed as dist
+
+    ref = rows_of(addrs[0])
+    n = ref.numel()
+    send = torch.zeros(kmax, n, dtype=torch.float32, device=ref.device)
+    for i, a in enumerate(trainers):
+        send[i].copy_(rows_of(a))
+    recv = torch.empty(len(counts) * kmax, n, dtype=torch.float32, device=ref.device)
+    dist.all_gather_into_tensor(recv, send, group=fed.group)
+    rows = [recv[r * kmax + i] for r, c in enumerate(counts) for i in range(c)]
+    if not rows:
+        return
+    if flat_only:
+        ops.median_into(rows, [learners[a].flat_params() for a in addrs])
+    else:
+        med = torch.empty(n, dtype=torch.float32, device=ref.device)
+        ops.median_into(rows, [med])
+        for a in addrs:
+            _unpack_into(learners[a], med)
+    fed.record("aggregate", time.perf_counter() - t0)
+
+
 def aggregate_generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> Any:
     """Any aggregator: all-gather the trainers' wire models and reduce identically on every rank."""
     local_models = {a: p[1] for a, p in arrived.items() if p[1] is not None}

@@ -18,7 +18,8 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
     model = learner.get_model()
     n = model.num_samples if trainer else 0
     wire = None
-    if trainer and kind not in ("mean", "neighbor"):
+    on_device = kind in weights_plane.DEVICE_KINDS and hasattr(learner, "flat_params")
+    if trainer and not on_device:
         wire = model.build_copy(params=model.get_parameters(), num_samples=model.num_samples, contributors=list(model.contributors), additional_info=dict(model.additional_info))
     round_ = state.round
 
@@ -28,6 +29,12 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
             extra = getattr(aggregator, "proximal_mu", None)
         elif kind == "neighbor":
             weights_plane.aggregate_neighbors(f, arrived, aggregator)
+            extra = None
+        elif kind == "scaffold" and all(p[1] is None for p in arrived.values()):
+            weights_plane.aggregate_scaffold(f, arrived, aggregator)
+            extra = None
+        elif kind == "median" and all(p[1] is None for p in arrived.values()):
+            weights_plane.aggregate_median(f, arrived)
             extra = None
         else:
             weights_plane.aggregate_generic(f, arrived, aggregator)

@@ -10,6 +10,8 @@ import sys
 
 import pytest
 
+from _ports import free_port
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -17,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_three_ranks_one_dies_survivors_finish():
     env = dict(os.environ, ROUNDS="3", KILL_RANK="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
-           "--master-port", str(29900 + os.getpid() % 90), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     outs = {o["rank"]: o for o in (json.loads(l) for l in res.stdout.splitlines() if l.startswith("{"))}
@@ -38,7 +40,7 @@ def test_three_ranks_one_process_crashes_survivors_evict_it():
     once its heartbeat is FAILURE_TIMEOUT (3 s) stale and finish every round."""
     env = dict(os.environ, ROUNDS="3", KILL_RANK="2", KILL_MODE="crash", FAILURE_TIMEOUT="3", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
-           "--master-port", str(29800 + os.getpid() % 90), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "_mp_dropout_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     outs = {o["rank"]: o for o in (json.loads(l) for l in res.stdout.splitlines() if l.startswith("{"))}

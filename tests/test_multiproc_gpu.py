@@ -9,6 +9,8 @@ import sys
 
 import pytest
 
+from _ports import free_port
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_two_ranks_fused_engine_cross_rank_fedavg(precision):
     env = dict(os.environ, MYFYP_DIST_BACKEND="gloo", MP_PRECISION=precision, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(29400 + (os.getpid() % 300) + (0 if precision == "fp32" else 1)), os.path.join(ROOT, "tests", "_mp_fused_worker.py")]
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "_mp_fused_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert res.returncode == 0, res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])

@@ -7,6 +7,8 @@ import time
 
 import numpy as np
 import pytest
+
+from _ports import free_port
 import torch
 
 from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
@@ -93,7 +95,7 @@ def test_neighbor_avg_workflow_learns():
 @pytest.mark.slow
 def test_ring_p2p_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(29500 + os.getpid() % 150), os.path.join(ROOT, "tests", "workers", "neighbor_avg_worker.py")]
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "neighbor_avg_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert res.returncode == 0, res.stderr[-3000:]
     assert res.stdout.count("OK") == 2

@@ -13,6 +13,8 @@ import time
 import numpy as np
 import pytest
 
+from _ports import free_port
+
 from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
 from myfyp_amd.communication.protocols.memory.memory_communication_protocol import InMemoryCommunicationProtocol
 from myfyp_amd.exceptions import NodeRunningException, ZeroRoundsException
@@ -158,7 +160,7 @@ def test_collective_two_processes_gloo(tmp_path):
     """2 ranks × 2 peers over torch.distributed (gloo): identical models and a JSON result."""
     cmd = [
         sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-        "--master-port", str(29700 + os.getpid() % 200), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--peers", "4",
+        "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--peers", "4",
         "--steps", "2", "--warmup", "1", "--n-train", "2000", "--n-test", "400", "--batch-size", "32",
     ]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)

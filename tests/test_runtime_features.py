@@ -5,6 +5,8 @@ import time
 
 import numpy as np
 import pytest
+
+from _ports import free_port
 import torch
 
 from myfyp_amd import fault_injection
@@ -250,7 +252,7 @@ def test_yaml_runner_split_over_two_ranks():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(29700 + os.getpid() % 150), os.path.join(root, "tests", "workers", "runner_worker.py")]
+           "--master-port", str(free_port()), os.path.join(root, "tests", "workers", "runner_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert res.returncode == 0, res.stderr[-3000:] + res.stdout[-2000:]
     assert res.stdout.count(" OK ") == 2, res.stdout

@@ -6,6 +6,8 @@ import sys
 
 import pytest
 
+from _ports import free_port
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -18,7 +20,7 @@ def test_shm_library_builds_and_single_rank_roundtrip(tmp_path):
 @pytest.mark.slow
 def test_shm_allgather_three_ranks():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
-           "--master-port", str(29660 + os.getpid() % 150), os.path.join(ROOT, "tests", "workers", "shm_collective_worker.py")]
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "shm_collective_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert res.returncode == 0, res.stderr[-3000:] + res.stdout[-2000:]
     assert res.stdout.count(" OK ") == 3, res.stdout
