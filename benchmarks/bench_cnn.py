@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--n-test", type=int, default=10000)
     ap.add_argument("--torch-step", action="store_true")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--delayed-averaging", action="store_true", help="opt-in delayed averaging (numerics change; last round exact)")
+    ap.add_argument("--no-overlap", action="store_true", help="synchronous FedAvg (no side-stream bucket pipeline)")
+    ap.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = Settings.BUCKET_BYTES)")
     return ap.parse_args()
 
 
@@ -98,6 +101,10 @@ def main() -> None:
     Settings.VOTE_TIMEOUT = Settings.AGGREGATION_TIMEOUT = 3600
     Settings.BATCH_SIZE = B
     Settings.GANG_WINDOW = 30.0
+    Settings.DELAYED_AVERAGING = bool(args.delayed_averaging)
+    Settings.OVERLAP_COLLECTIVES = not args.no_overlap
+    if args.bucket_mb > 0:
+        Settings.BUCKET_BYTES = int(args.bucket_mb * (1 << 20))
     fed = Federation.init()
     world, rank = fed.world, fed.rank
     ppr = args.peers // world
@@ -168,6 +175,8 @@ def main() -> None:
         "partition": f"dirichlet({args.dirichlet})" if args.dirichlet else "iid", "dropout": args.dropout,
         "final_test_acc_mean": round(float(np.mean(accs)), 4) if accs else None,
         "engine_ms_per_grouped_step": step_ms_engine,
+        "collective": ("delayed-averaging" if args.delayed_averaging else ("synchronous" if args.no_overlap else "side-stream-bucketed"))
+        + f", bucket {Settings.BUCKET_BYTES >> 20} MiB",
     }
     if args.torch_step and rank == 0 and torch.cuda.is_available():
         t_ms = torch_step_ms(args.model, B)

@@ -11,8 +11,10 @@ struct FedAvgWeights {
   float w[FEDAVG_MAX_PEERS];
   float wsum;
 };
-void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
-void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
+void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
+void fl_fedavg_apply(float* stacked, const float* out, const float* wsum_slot, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
+void fl_fedavg_delayed_land(float* stacked, float* snap, int64_t ld_snap, const float* avg, const float* wsum_slot, int P, int64_t n, int64_t ld,
+                            unsigned long long mask, hipStream_t s);
 void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, unsigned long long mask, hipStream_t s);
 // Topology mixing of a stacked group in place: row p <- sum_k w[p][k] * row idx[p][k] (P <= 16 rows,
 // up to P sources per row; rows with nsrc == 0 are left alone).

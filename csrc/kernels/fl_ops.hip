@@ -79,13 +79,15 @@ __global__ __launch_bounds__(FL_BLOCK) void k_broadcast_rows(float* __restrict__
 
 // FedAvg over a stacked [P][ld] group with the per-peer weights / mask passed BY VALUE (kernel
 // arguments): no host→device copy, nothing for the host to wait on.
-//   reduce: out[i] = Σ_p w[p] · stacked[p*ld + i] (i < n), out[n] = wsum
-//   apply:  stacked[p*ld + i] = out[i] / max(out[n], 1e-12) for rows with mask bit p set
-__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ out, const float* __restrict__ stacked, int P, int64_t n, int64_t ld,
-                                                             FedAvgWeights w) {
+//   reduce: out[i] = Σ_p w[p] · stacked[p*ld + i] (i < n), *wsum_slot = wsum (when non-null)
+//   apply:  stacked[p*ld + i] = out[i] / max(*wsum_slot, 1e-12) for rows with mask bit p set
+// A bucketed all-reduce calls them per bucket (sub-ranges of out / stacked, bucket 0 carries the
+// weight sum in a slot in front of the data, so bucket k's apply only waits for buckets 0 and k).
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ out, float* __restrict__ wsum_slot, const float* __restrict__ stacked,
+                                                             int P, int64_t n, int64_t ld, FedAvgWeights w) {
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
   const int64_t t0 = blockIdx.x * FL_BLOCK + threadIdx.x;
-  if (t0 == 0) out[n] = w.wsum;
+  if (t0 == 0 && wsum_slot != nullptr) *wsum_slot = w.wsum;
   if ((ld % 4) == 0) {
     const int64_t n4 = n / 4;
     for (int64_t i = t0; i < n4; i += stride) {
@@ -112,11 +114,11 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_apply(float* __restrict__ stacked, const float* __restrict__ out, int P, int64_t n, int64_t ld,
-                                                            unsigned long long mask) {
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_apply(float* __restrict__ stacked, const float* __restrict__ out, const float* __restrict__ wsum_slot,
+                                                            int P, int64_t n, int64_t ld, unsigned long long mask) {
   const int p = blockIdx.y;
   if (!((mask >> p) & 1ull)) return;
-  const float inv = 1.f / fmaxf(out[n], 1e-12f);
+  const float inv = 1.f / fmaxf(*wsum_slot, 1e-12f);
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
   float* dst = stacked + p * ld;
   if ((ld % 4) == 0) {
@@ -172,14 +174,44 @@ void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgW
   hipLaunchKernelGGL(k_fedavg_local, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, stacked, P, n, ld, w, mask);
 }
 
-void fl_fedavg_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, stacked, P, n, ld, w);
+void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, wsum_slot, stacked, P, n, ld, w);
 }
 
-void fl_fedavg_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s) {
+void fl_fedavg_apply(float* stacked, const float* out, const float* wsum_slot, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s) {
   unsigned gx = grid_for((n + 3) / 4);
   if (gx > 256) gx = 256;
-  hipLaunchKernelGGL(k_fedavg_apply, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, out, P, n, ld, mask);
+  hipLaunchKernelGGL(k_fedavg_apply, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, out, wsum_slot, P, n, ld, mask);
+}
+
+// Delayed averaging (opt-in): land the previous round's average as a correction and take the new
+// snapshot in one pass, for every row with mask bit p set:
+//   x = stacked[p][i] + avg[i] / wsum - snap[p][i];  stacked[p][i] = x;  snap[p][i] = x
+// With avg == nullptr (nothing pending) it only snapshots.
+__global__ __launch_bounds__(FL_BLOCK) void k_fedavg_delayed_land(float* __restrict__ stacked, float* __restrict__ snap, int64_t ld_snap,
+                                                                   const float* __restrict__ avg, const float* __restrict__ wsum_slot, int P, int64_t n,
+                                                                   int64_t ld, unsigned long long mask) {
+  const int p = blockIdx.y;
+  if (!((mask >> p) & 1ull)) return;
+  const float inv = avg != nullptr ? 1.f / fmaxf(*wsum_slot, 1e-12f) : 0.f;
+  float* x = stacked + p * ld;
+  float* sp = snap + p * ld_snap;
+  const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
+  for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
+    float v = x[i];
+    if (avg != nullptr) {
+      v = v + (avg[i] * inv - sp[i]);
+      x[i] = v;
+    }
+    sp[i] = v;
+  }
+}
+
+void fl_fedavg_delayed_land(float* stacked, float* snap, int64_t ld_snap, const float* avg, const float* wsum_slot, int P, int64_t n, int64_t ld,
+                            unsigned long long mask, hipStream_t s) {
+  unsigned gx = grid_for(n);
+  if (gx > 512) gx = 512;
+  hipLaunchKernelGGL(k_fedavg_delayed_land, dim3(gx, P), dim3(FL_BLOCK), 0, s, stacked, snap, ld_snap, avg, wsum_slot, P, n, ld, mask);
 }
 
 // Gossip neighbour averaging of co-located peers (reference: aggregator over the neighbours'

@@ -367,11 +367,20 @@ int myfyp_broadcast_rows(float* stacked, const float* src, int P, int64_t n, int
   return 0;
 }
 // FedAvg of a stacked [P][ld] group: weights / mask by value (P <= 64); out has n + 1 floats.
-int myfyp_fedavg_stacked_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w_host, void* stream) {
-  if (P < 1 || P > FEDAVG_MAX_PEERS) {
-    g_last_error = "fedavg_stacked: 1..64 rows";
-    return 2;
-  }
+static bool fedavg_rows_ok(int P) {
+  if (P >= 1 && P <= FEDAVG_MAX_PEERS) return true;
+  g_last_error = "fedavg_stacked: 1..64 rows";
+  return false;
+}
+static unsigned long long mask_bits(const float* mask_host, int P) {
+  unsigned long long mask = 0;
+  for (int p = 0; p < P; ++p)
+    if (mask_host[p] != 0.f) mask |= 1ull << p;
+  return mask;
+}
+// wsum_slot: where the weight sum goes (nullptr: not written, e.g. buckets after the first)
+int myfyp_fedavg_bucket_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const float* w_host, void* stream) {
+  if (!fedavg_rows_ok(P)) return 2;
   FedAvgWeights w{};
   double sum = 0.0;
   for (int p = 0; p < P; ++p) {
@@ -379,19 +388,28 @@ int myfyp_fedavg_stacked_reduce(float* out, const float* stacked, int P, int64_t
     sum += w_host[p];
   }
   w.wsum = (float)sum;
-  fl_fedavg_reduce(out, stacked, P, n, ld, w, (hipStream_t)stream);
+  fl_fedavg_reduce(out, wsum_slot, stacked, P, n, ld, w, (hipStream_t)stream);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+int myfyp_fedavg_bucket_apply(float* stacked, const float* out, const float* wsum_slot, int P, int64_t n, int64_t ld, const float* mask_host, void* stream) {
+  if (!fedavg_rows_ok(P)) return 2;
+  fl_fedavg_apply(stacked, out, wsum_slot, P, n, ld, mask_bits(mask_host, P), (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// Unbucketed layout: out[0:n] | out[n] = weight sum.
+int myfyp_fedavg_stacked_reduce(float* out, const float* stacked, int P, int64_t n, int64_t ld, const float* w_host, void* stream) {
+  return myfyp_fedavg_bucket_reduce(out, out + n, stacked, P, n, ld, w_host, stream);
+}
 int myfyp_fedavg_stacked_apply(float* stacked, const float* out, int P, int64_t n, int64_t ld, const float* mask_host, void* stream) {
-  if (P < 1 || P > FEDAVG_MAX_PEERS) {
-    g_last_error = "fedavg_stacked: 1..64 rows";
-    return 2;
-  }
-  unsigned long long mask = 0;
-  for (int p = 0; p < P; ++p)
-    if (mask_host[p] != 0.f) mask |= 1ull << p;
-  fl_fedavg_apply(stacked, out, P, n, ld, mask, (hipStream_t)stream);
+  return myfyp_fedavg_bucket_apply(stacked, out, out + n, P, n, ld, mask_host, stream);
+}
+// Delayed averaging: rows in mask <- row + avg / *wsum_slot - snap, snap <- row (avg null: snapshot only)
+int myfyp_fedavg_delayed_land(float* stacked, float* snap, int64_t ld_snap, const float* avg, const float* wsum_slot, int P, int64_t n, int64_t ld,
+                              const float* mask_host, void* stream) {
+  if (!fedavg_rows_ok(P)) return 2;
+  fl_fedavg_delayed_land(stacked, snap, ld_snap, avg, wsum_slot, P, n, ld, mask_bits(mask_host, P), (hipStream_t)stream);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

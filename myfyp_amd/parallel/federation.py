@@ -488,6 +488,17 @@ class Federation:
                 w.wait()
         return t
 
+    def all_reduce_async(self, t: torch.Tensor):
+        """Start a sum all-reduce of ``t`` (one bucket) over the live ranks on the communicator's
+        stream, ordered after the work already queued on the CURRENT stream. Returns the work
+        handle (``wait()`` makes the current stream wait on it), or None when there is nobody to
+        reduce with."""
+        if self.solo:
+            return None
+        import torch.distributed as dist
+
+        return dist.all_reduce(t, group=self._pg, async_op=True)
+
     def broadcast_(self, t: torch.Tensor, src_rank: int) -> torch.Tensor:
         if self.world == 1 or self.departed:
             return t

@@ -70,10 +70,132 @@ def gather_votes(fed: Federation, arrived: Dict[str, Dict[str, int]]) -> Dict[st
 # ---------------------------------------------------------------------------------------------
 # aggregation
 # ---------------------------------------------------------------------------------------------
+_COMM_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def comm_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """The side HIP stream that carries the weight collectives of ``dev`` (one per device)."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _COMM_STREAMS.get(idx)
+    if st is None:
+        st = _COMM_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+def bucket_ranges(n: int, bucket_bytes: int) -> List[Tuple[int, int]]:
+    """[b0, b1) ranges over n floats; every b0 is a multiple of 4 (float4 kernels stay aligned)."""
+    step = max(4, (bucket_bytes // 4) // 4 * 4)
+    return [(b0, min(n, b0 + step)) for b0 in range(0, n, step)] or [(0, 0)]
+
+
+class _Delayed:
+    """Delayed-averaging state of one stacked group or of the generic per-learner path."""
+
+    def __init__(self) -> None:
+        self.snap: Optional[torch.Tensor] = None  # round-r local rows (stacked: [capacity, n])
+        self.snaps: Dict[str, torch.Tensor] = {}  # generic path: addr -> packed row
+        self.buf: Optional[torch.Tensor] = None  # [wsum, pad x3 | Σ w x_r] (stacked) / [Σ w x_r | Σ w] (generic)
+        self.done = None  # event on the side stream: the round-r all-reduce has landed in buf
+        self.pending = False
+
+
+def _delayed_state(fed: Federation, key) -> _Delayed:
+    table = fed.__dict__.setdefault("_delayed", {})
+    st = table.get(key)
+    if st is None:
+        st = table[key] = _Delayed()
+    return st
+
+
+def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, final: bool) -> None:
+    """FedAvg of a stacked ``[capacity, S]`` group on the GPU, host never waits.
+
+    * one rank: one ``k_fedavg_local`` launch (weighted mean written into every masked row);
+    * several ranks, ``OVERLAP_COLLECTIVES``: on the side stream, per bucket a reduce launch and an
+      async all-reduce (RCCL orders it after that launch), then per bucket wait + apply launch —
+      bucket k's all-reduce overlaps bucket k+1's reduce and bucket k-1's apply; the compute stream
+      waits on the side stream only at the point the next round touches the parameters;
+    * ``DELAYED_AVERAGING`` (opt-in, not on the last round): land the previous round's average as
+      ``x += avg - snap`` and take the new snapshot (one launch), then reduce + all-reduce the
+      snapshot on the side stream while the next round trains from the local weights.
+    """
+    from myfyp_amd.settings import Settings
+
+    fast = ops.fast_lib()
+    n, P, S = group.numel, group.capacity, group.S
+    dev = group.params.device
+    cur = torch.cuda.current_stream(dev)
+    wp, mp = w.ctypes.data, mask.ctypes.data
+    base = group.params.data_ptr()
+    delayed = bool(Settings.DELAYED_AVERAGING)
+    st = _delayed_state(fed, id(group)) if (delayed or getattr(fed, "_delayed", {}).get(id(group))) else None
+    landed = False
+    if st is not None and st.pending:  # land round r-1's average (and re-snapshot) in one launch
+        cur.wait_event(st.done)
+        ops.check(fast.myfyp_fedavg_delayed_land(base, st.snap.data_ptr(), n, st.buf.data_ptr() + 16, st.buf.data_ptr(), P, n, S, mp, cur.cuda_stream),
+                  "fedavg_delayed_land")
+        st.pending, landed = False, True
+    if delayed and not final:
+        if st.snap is None or tuple(st.snap.shape) != (P, n):
+            st.snap = torch.empty(P, n, dtype=torch.float32, device=dev)
+            st.buf = torch.empty(n + 4, dtype=torch.float32, device=dev)
+            landed = False
+        if not landed:  # first delayed round: snapshot only
+            ops.check(fast.myfyp_fedavg_delayed_land(base, st.snap.data_ptr(), n, None, None, P, n, S, mp, cur.cuda_stream), "fedavg_snapshot")
+        _bucketed_reduce(fed, fast, comm_stream(dev), cur, st.snap.data_ptr(), n, n, P, wp, st.buf, apply=None)
+        st.done = torch.cuda.Event()
+        st.done.record(comm_stream(dev))
+        st.pending = True
+        return
+    if fed.solo:  # nothing to all-reduce: weighted mean and write-back in one launch
+        ops.check(fast.myfyp_fedavg_stacked_local(base, P, n, S, wp, mp, cur.cuda_stream), "fedavg_local")
+        return
+    if not Settings.OVERLAP_COLLECTIVES:
+        buf = group.fedavg_buffer()
+        ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), base, P, n, S, wp, cur.cuda_stream), "fedavg_reduce")
+        fed.all_reduce_(buf)
+        ops.check(fast.myfyp_fedavg_stacked_apply(base, buf.data_ptr(), P, n, S, mp, cur.cuda_stream), "fedavg_apply")
+        return
+    buf = getattr(group, "_wp_bucket_buf", None)
+    if buf is None or buf.numel() != n + 4:
+        buf = group._wp_bucket_buf = torch.empty(n + 4, dtype=torch.float32, device=dev)
+    _bucketed_reduce(fed, fast, comm_stream(dev), cur, base, S, n, P, wp, buf, apply=(base, S, mp))
+
+
+def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, P: int, wp: int, buf: torch.Tensor, apply) -> None:
+    """Side-stream pipeline over ``bucket_ranges``: reduce launch + async all-reduce per bucket,
+    then (``apply`` = (dst, ld, mask)) per bucket wait + apply launch. ``buf`` = [wsum, pad x3 | data];
+    bucket 0's all-reduce carries the weight sum, so apply k needs only buckets 0 and k."""
+    from myfyp_amd.settings import Settings
+
+    cs.wait_stream(cur)  # the rows are final on the compute stream
+    bp = buf.data_ptr()
+    ranges = bucket_ranges(n, Settings.BUCKET_BYTES)
+    works = []
+    with torch.cuda.stream(cs):
+        for k, (b0, b1) in enumerate(ranges):
+            ops.check(fast.myfyp_fedavg_bucket_reduce(bp + 4 * (4 + b0), bp if k == 0 else None, src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream),
+                      "fedavg_bucket_reduce")
+            works.append(fed.all_reduce_async(buf[(0 if k == 0 else 4 + b0) : 4 + b1]))
+        for k, (b0, b1) in enumerate(ranges):
+            if works[k] is not None:
+                works[k].wait()
+            if apply is not None:
+                dst, dld, mp = apply
+                ops.check(fast.myfyp_fedavg_bucket_apply(dst + 4 * b0, bp + 4 * (4 + b0), bp, P, b1 - b0, dld, mp, cs.cuda_stream), "fedavg_bucket_apply")
+    buf.record_stream(cs)
+    if apply is not None:
+        cur.wait_stream(cs)  # stream-level: the next kernel on the compute stream sees the average
+
+
 @traced("aggregate_mean")
-def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tuple[float, List[str]]:
+def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final: bool = True) -> Tuple[float, List[str]]:
     """Sample-weighted mean of the trainers' models (weight 0 for non-trainers), result into every
-    local peer. One local weighted reduction kernel + one all-reduce + one broadcast kernel."""
+    local peer. Stacked groups on the GPU: see ``_stacked_mean_cuda`` (side-stream bucketed
+    pipeline, optional delayed averaging). ``final`` marks the experiment's last round (delayed
+    averaging flushes and aggregates exactly there)."""
+    from myfyp_amd.settings import Settings
+
     t0 = time.perf_counter()
     fed.sync_members()  # a rank may have lost its last peer since the vote: agree on the survivors
     addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
@@ -83,26 +205,13 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
     group = _stacked_group(learners)
     dev = learners[0].flat_params().device
     if group is not None and dev.type == "cuda":
-        # one native reduction kernel (weights as kernel arguments) -> RCCL all-reduce over the
-        # n + 1 floats (weighted sum | Σw) -> one native normalise-and-broadcast kernel; no host
-        # tensor traffic and nothing the host waits on
         w = np.zeros(group.capacity, dtype=np.float32)
         mask = np.zeros(group.capacity, dtype=np.float32)
         for lr, wt in zip(learners, weights):
             w[lr._engine.slot] = wt
             mask[lr._engine.slot] = 1.0
-        n = group.numel
-        fast = ops.fast_lib()
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        if fed.solo:  # nothing to all-reduce: weighted mean and write-back in one launch
-            ops.check(fast.myfyp_fedavg_stacked_local(group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, mask.ctypes.data, stream),
-                      "fedavg_local")
-        else:
-            buf = group.fedavg_buffer()
-            ops.check(fast.myfyp_fedavg_stacked_reduce(buf.data_ptr(), group.params.data_ptr(), group.capacity, n, group.S, w.ctypes.data, stream), "fedavg_reduce")
-            fed.all_reduce_(buf)
-            ops.check(fast.myfyp_fedavg_stacked_apply(group.params.data_ptr(), buf.data_ptr(), group.capacity, n, group.S, mask.ctypes.data, stream), "fedavg_apply")
-        total_w = float(sum(weights))  # local share; the global Σw stays on the device (buf[n])
+        _stacked_mean_cuda(fed, group, w, mask, final)
+        total_w = float(sum(weights))  # local share; the global Σw stays on the device
     elif group is not None:
         wm = torch.zeros(2, group.capacity, dtype=torch.float32)
         for lr, wt in zip(learners, weights):
@@ -118,25 +227,39 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> Tu
         ops.broadcast_rows(buf[:n], group.params[:, :n], wm[1])
         total_w = total
     else:
-        states = [state_tensors(lr) for lr in learners]
-        flat = torch.cat([torch.cat([t.reshape(-1).float() for t in st]) for st in states[:1]])
-        n = flat.numel()
-        acc = torch.zeros(n + 1, dtype=torch.float32, device=dev)
-        for st, wt in zip(states, weights):
-            if wt > 0:
-                acc[:n].add_(torch.cat([t.reshape(-1).float() for t in st]), alpha=wt)
-        acc[n] = sum(weights)
-        fed.all_reduce_(acc)
-        total_w = float(acc[n])
-        avg = acc[:n] / max(total_w, 1e-12)
-        with torch.no_grad():
-            for st in states:
-                off = 0
-                for t in st:
-                    t.copy_(avg[off : off + t.numel()].view_as(t).to(t.dtype))
-                    off += t.numel()
+        total_w = _generic_mean(fed, addrs, learners, weights, final, bool(Settings.DELAYED_AVERAGING))
     fed.record("aggregate", time.perf_counter() - t0)
     return total_w, contributors
+
+
+def _generic_mean(fed: Federation, addrs, learners, weights, final: bool, delayed: bool) -> float:
+    """Per-learner path (CPU, or models outside a stacked engine group); same delayed-averaging
+    semantics as the stacked kernels, in torch ops."""
+    st = _delayed_state(fed, "generic") if (delayed or getattr(fed, "_delayed", {}).get("generic")) else None
+    if st is not None and st.pending:  # land: x += avg_{r-1} - snap_{r-1}
+        avg = st.buf[:-1] / st.buf[-1].clamp_min(1e-12)
+        for a, lr in zip(addrs, learners):
+            if a in st.snaps:
+                _unpack_into(lr, _pack(lr) + (avg - st.snaps[a]))
+        st.pending = False
+    rows = [_pack(lr) for lr in learners]
+    n = rows[0].numel()
+    acc = torch.zeros(n + 1, dtype=torch.float32, device=rows[0].device)
+    for r, wt in zip(rows, weights):
+        if wt > 0:
+            acc[:n].add_(r, alpha=wt)
+    acc[n] = sum(weights)
+    fed.all_reduce_(acc)
+    total_w = float(acc[n])
+    if delayed and not final:  # keep the local weights; the average lands next round
+        st.snaps = dict(zip(addrs, rows))
+        st.buf = acc
+        st.pending = True
+        return total_w
+    avg = acc[:n] / max(total_w, 1e-12)
+    for lr in learners:
+        _unpack_into(lr, avg)
+    return total_w
 
 
 def _pack(learner) -> torch.Tensor:

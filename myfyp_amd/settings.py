@@ -95,7 +95,16 @@ class Settings:
     COLLECTIVE_TIMEOUT: float = 300  # RCCL watchdog (seconds)
     # a rank whose control-plane heartbeat is older than this is evicted from the federation (s)
     FAILURE_TIMEOUT: float = 60
-    BUCKET_BYTES: int = 64 << 20  # all-reduce bucket size (xGMI ring per-link bound)
+    # all-reduce bucket size: large enough that each ring step is bandwidth-bound on the xGMI links,
+    # small enough that a 45 MB ResNet-18 buffer pipelines (bucket k's all-reduce overlaps bucket
+    # k+1's reduce kernel and bucket k-1's apply kernel on the side stream)
+    BUCKET_BYTES: int = 16 << 20
+    # stacked-group FedAvg runs on a side HIP stream, bucketed and pipelined (exact numerics)
+    OVERLAP_COLLECTIVES: bool = True
+    # opt-in delayed averaging (SURVEY §7.4 hard part 4b): the next round trains from the local
+    # weights while the all-reduce runs; the averaged delta lands at the next aggregation
+    # (x += avg_r - x_r); the last round aggregates exactly. Changes numerics.
+    DELAYED_AVERAGING: bool = False
     SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
@@ -175,6 +184,8 @@ class Settings:
             "COLLECTIVE_TIMEOUT": "COLLECTIVE_TIMEOUT",
             "FAILURE_TIMEOUT": "FAILURE_TIMEOUT",
             "BUCKET_BYTES": "BUCKET_BYTES",
+            "OVERLAP_COLLECTIVES": "OVERLAP_COLLECTIVES",
+            "DELAYED_AVERAGING": "DELAYED_AVERAGING",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",

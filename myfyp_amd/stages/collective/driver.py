@@ -141,7 +141,8 @@ class RoundDriver:
                 evs = group._run_eval_batch({slot[a]: () for a in trainers if a in has_test})
                 fits = group._run_fit_batch({slot[a]: reqs[a] for a in trainers})
                 out = {a: (evs.get(slot[a]), fits[slot[a]]) for a in trainers}
-            weights_plane.aggregate_mean(f, {a: (n.get(a, 0), None) for a in cur})
+            total = next(iter(states.values())).total_rounds
+            weights_plane.aggregate_mean(f, {a: (n.get(a, 0), None) for a in cur}, final=total is None or round_ + 1 >= total)
             for hook in list(f.round_hooks):
                 hook(round_, f)
             for a, m in cur.items():

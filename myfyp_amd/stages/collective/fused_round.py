@@ -55,6 +55,7 @@ def join(state, learner, aggregator, trainer: bool) -> None:
     n = learner.num_train_samples() if trainer else 0
     has_test = trainer and learner.data is not None and learner.data.get_num_samples(train=False) > 0
     round_ = state.round
+    final = state.total_rounds is None or round_ + 1 >= state.total_rounds
 
     def leader(arrived):
         addrs = [a for a in arrived if a in f.local_nodes]  # a peer may die after arriving
@@ -67,7 +68,7 @@ def join(state, learner, aggregator, trainer: bool) -> None:
             fits = group._run_fit_batch({slot[a]: arrived[a][2] for a in trainers})
             for a in trainers:
                 out[a] = (evs.get(slot[a]), fits[slot[a]])
-        weights_plane.aggregate_mean(f, {a: (arrived[a][1], None) for a in addrs})
+        weights_plane.aggregate_mean(f, {a: (arrived[a][1], None) for a in addrs}, final=final)
         for hook in list(f.round_hooks):
             hook(round_, f)
         return out

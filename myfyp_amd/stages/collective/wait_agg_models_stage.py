@@ -22,10 +22,11 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
     if trainer and not on_device:
         wire = model.build_copy(params=model.get_parameters(), num_samples=model.num_samples, contributors=list(model.contributors), additional_info=dict(model.additional_info))
     round_ = state.round
+    final = state.total_rounds is None or round_ + 1 >= state.total_rounds
 
     def leader(arrived):
         if kind == "mean":
-            total, contributors = weights_plane.aggregate_mean(f, arrived)
+            total, contributors = weights_plane.aggregate_mean(f, arrived, final=final)
             extra = getattr(aggregator, "proximal_mu", None)
         elif kind == "neighbor":
             weights_plane.aggregate_neighbors(f, arrived, aggregator)

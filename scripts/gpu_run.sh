@@ -2,7 +2,8 @@
 # Parameterised GPU entry point (replaces the one-off gpu_*.sh scripts):
 #   OUT=<dir under gpurun_out> bash scripts/gpu_run.sh <step> [<step> ...]
 # steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), smoke, bench (fp32 headline),
-#        bench_bf16, bench_cnn, devagg (device SCAFFOLD/FedMedian tests + copy trace), prof (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
+#        bench_bf16, bench_cnn, devagg (device SCAFFOLD/FedMedian tests + copy trace),
+#        overlap (side-stream / delayed FedAvg tests, bench, kernel overlap trace), prof (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
 #        gloo ranks on one GPU). Every GPU step runs under its own time limit; the script stops at
 #        the first failure, and at once after a timeout, abort or segfault.
 set -o pipefail
@@ -34,6 +35,11 @@ for step in "$@"; do
       run devagg_prof 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$O/agg" -o run -- python3 scripts/probes/device_agg_copies.py
       mv gpurun_out/device_agg_windows.json "$O/" && python3 scripts/tools/copies_in_window.py "$O"/agg/run_results.db "$O/device_agg_windows.json" > "$O/devagg_windows.txt"
       cat "$O/devagg_windows.txt" ;;
+    overlap)
+      run overlap_tests 400 python -u -m pytest tests/test_overlap.py tests/test_cnn_engine_gpu.py -k "overlap or delayed or lenet_fused_epoch" -v -m gpu --timeout 120 --timeout-method thread
+      run bench_cnn_delayed 600 python benchmarks/bench_cnn.py --delayed-averaging
+      run overlap_prof 300 rocprofv3 --kernel-trace -d "$O/ovl" -o run -- python3 scripts/probes/overlap_probe.py
+      python3 scripts/tools/kernel_overlap.py "$O"/ovl/run_results.db fedavg > "$O/overlap.txt"; cat "$O/overlap.txt" ;;
     rehearsal)
       for n in 2 4; do
         MYFYP_DIST_BACKEND=gloo run rehearsal_gloo_n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \

@@ -183,19 +183,57 @@ def test_lenet_train_step_matches_torch(fused, monkeypatch):
     assert learners[0]._engine.group.lenet_fused == (fused == "1")
 
 
-def test_lenet_fused_epoch_matches_layerwise_path(monkeypatch):
-    """A whole epoch with a partial last batch and momentum: fused step vs the layer-by-layer path."""
+class _FixedCorrection:
+    """Stands in for the FedProx / SCAFFOLD callbacks: fixed optimizer extras for every fit."""
+
+    def __init__(self, extra):
+        self.extra = extra
+
+    @staticmethod
+    def get_name():
+        return "fixed_correction"
+
+    def get_info(self):
+        return {}
+
+    def set_info(self, info):
+        pass
+
+    def grad_correction(self):
+        return self.extra
+
+
+@pytest.mark.parametrize("mode", ["plain", "weight_decay", "fedprox", "scaffold"])
+def test_lenet_fused_epoch_matches_layerwise_path(monkeypatch, mode):
+    """A whole epoch with a partial last batch and momentum: fused step vs the layer-by-layer path
+    (``k_opt_step``), with weight decay, a FedProx anchor/mu or SCAFFOLD c_global/c_local — the
+    fused kernel reads those through its own index remaps (conv (co,ci,tap), fc1 e2t)."""
     import threading
 
     from myfyp_amd.models import LeNet5
 
     runs = []
+    extras = None
     for fused in ("1", "0"):
         monkeypatch.setenv("MYFYP_LENET_FUSED", fused)
-        learners, _, _ = _make_learners(lambda i: LeNet5(seed=50 + i), 3, 100, 40, 32, 0.05, momentum=0.9)
+        wd = 5e-3 if mode == "weight_decay" else 0.0
+        learners, _, _ = _make_learners(lambda i: LeNet5(seed=50 + i), 3, 100, 40, 32, 0.05, momentum=0.9, wd=wd)
         g = learners[0]._engine.group
         assert g.lenet_fused == (fused == "1")
         p0 = [lr_.flat_params().detach().clone() for lr_ in learners]
+        if extras is None:  # same extras (device tensors, generated once) for both runs
+            gen = torch.Generator(device="cuda").manual_seed(11)
+            extras = []
+            for q in p0:
+                if mode == "fedprox":
+                    extras.append({"anchor": q + 0.2 * torch.randn(q.shape, device="cuda", generator=gen), "mu": 1.0})
+                elif mode == "scaffold":
+                    extras.append({"c_global": 0.2 * torch.randn(q.shape, device="cuda", generator=gen),
+                                   "c_local": 0.2 * torch.randn(q.shape, device="cuda", generator=gen)})
+                else:
+                    extras.append({})
+        for lr_, ex in zip(learners, extras):
+            lr_.callbacks = [_FixedCorrection(ex)] if ex else []
         ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
         [t.start() for t in ths]
         [t.join() for t in ths]
@@ -206,7 +244,7 @@ def test_lenet_fused_epoch_matches_layerwise_path(monkeypatch):
     for a, b in zip(d_f, d_l):
         cos = F.cosine_similarity(a, b, dim=0)
         rel = (a - b).norm() / b.norm()
-        assert cos > 0.98 and rel < 0.2, (float(cos), float(rel))
+        assert cos > 0.98 and rel < 0.2, (mode, float(cos), float(rel))
     torch.testing.assert_close(l_f, l_l, rtol=3e-2, atol=1e-2)  # (loss sum, correct) per peer
     for a, b in zip(e_f, e_l):
         assert abs(a["test_loss"] - b["test_loss"]) < 0.05 * max(1.0, b["test_loss"]), (a, b)
