@@ -61,6 +61,7 @@ struct MLPArgs {
   int* correct_acc;  // [P]
   int* conf;         // [P][16][16] (eval) or null
   OptParams opt;
+  int debug_giveup;  // fp32 persistent epoch test hook: peer + 1 whose first attempt gives up (0 = none)
 };
 
 bool mlp_shape_supported(int D0, int D1, int D2, int D3);

@@ -30,14 +30,16 @@ struct MLPPersistF32Bufs {
   float* dh2x;      // [P][2][Bpad][128]   head hd -> owners: dH2 columns 16hd..16hd+15 (step parity)
   unsigned* flags;  // [P][32][32] one 128-B line per flag (16 H1, 8 PL, 8 dH2); zeroed per launch
   size_t flag_bytes;
-  int* err;         // sticky give-up word (shared with the bf16 path)
+  int* err;         // give-up words: [0,64) per peer first attempt (1 gave up, 2 recovered), [64,128) retry
+  unsigned fbase;   // hand-off flag base of the running attempt (set in the kernel)
   float* w2chk;     // debug: owners' W2 replica after the epoch [P][128][256], or null
 };
 
 bool mlp_persistent_f32_supported(const MLPArgs& a);
 size_t mlp_persistent_f32_bytes(int P, int Bpad);
 size_t mlp_persistent_f32_flag_bytes(int P);
-int mlp_persistent_f32_gang();             // workgroups (CUs) per peer
+int mlp_persistent_f32_gang();
+int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus);             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);

@@ -397,7 +397,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       }
     }
     if (g == 0) P32_STAMP(0, t, 1);
-    persist::publish(pb.flags, FPP, p, F_H1 + g, (unsigned)(t + 1));
+    persist::publish(pb.flags, FPP, p, F_H1 + g, pb.fbase + (unsigned)(t + 1));
     if (g == 0) P32_STAMP(0, t, 2);
 
     // the previous step's W2-replica update runs while the heads work on this step's H1
@@ -420,7 +420,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     }
 
     // ================= C: backward of this slice
-    if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (g == 0) P32_STAMP(0, t, 4);
     {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2, BP * PD2 * 4);
@@ -688,7 +688,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 
     // ---- H1(t) from the 16 owners -> LDS (16-byte sc1 loads)
     if (hd == 0) P32_STAMP(1, t, 0);
-    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 1);
     {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + (int64_t)p * BP * PD1, BP * PD1 * 4);
@@ -749,11 +749,11 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       for (int i = 0; i < 4; ++i) st_wt32(pb.plx + (((int64_t)p * NH + hd) * BP + 16 * wave + 4 * h + i) * 16 + c, pl[i]);
     }
     if (hd == 0) P32_STAMP(1, t, 3);
-    persist::publish(pb.flags, FPP, p, F_PL + hd, (unsigned)(t + 1));
+    persist::publish(pb.flags, FPP, p, F_PL + hd, pb.fbase + (unsigned)(t + 1));
     if (hd == 0) P32_STAMP(1, t, 4);
 
     // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3
-    if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, (unsigned)(t + 1), pb.err, sOk)) return;
+    if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 5);
     if (tid < BP * 4) {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16, NH * BP * 16 * 4);
@@ -811,7 +811,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         st_wt32(dst + b * PD2 + 16 * hd + c, v);
       }
     }
-    persist::publish(pb.flags, FPP, p, F_DH2 + hd, (unsigned)(t + 1));
+    persist::publish(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1));
     if (hd == 0) P32_STAMP(1, t, 7);
 
     // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
@@ -891,8 +891,19 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 
 // grid = 8 * ROLES blocks per group of 8 peers: block b serves peer p_base + (b & 7) in role b >> 3,
 // so a peer's 24 workgroups share one XCD under round-robin dispatch (speed only).
+//
+// Give-up recovery: a gang whose hand-off wait times out (a workgroup not resident, see
+// persist::wg_wait) stops without storing any parameter or optimizer state — every global write of
+// the epoch is in the final write-back — and marks err[p] = 1. The same stream then runs the
+// launch again as attempt 1: gangs with err[p] == 0 exit at once, a gang that gave up re-runs its
+// epoch from the untouched pre-epoch state with its own give-up word err[64 + p] and hand-off
+// flags offset by RETRY_BASE (the aborted attempt's flag values are all smaller), and on success
+// sets err[p] = 2 ("recovered"). Gangs are independent: one peer's give-up never aborts another.
+constexpr unsigned RETRY_BASE = 1u << 24;
+constexpr int ERR_RETRY = 64;  // err layout: [0, 64) first attempt, [64, 128) retry, per peer
+
 template <int BP, bool ADAM, bool EXTRA>
-__global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base) {
+__global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base, int attempt) {
   extern __shared__ __attribute__((aligned(16))) char smem_p32[];
   const int b = blockIdx.x;
   const int p = p_base + (b & 7);
@@ -900,10 +911,28 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
   if (p >= a.P) return;
   const int4 ctl = a.ctl[p];
   if (!(ctl.x & 1) || ctl.y <= 0) return;
+  int* err_first = pb.err + p;
+  if (attempt) {
+    if (__hip_atomic_load(err_first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    pb.err = pb.err + ERR_RETRY + p;
+    pb.fbase = RETRY_BASE;
+  } else {
+    if (a.debug_giveup == p + 1) {  // test hook: this peer's first attempt gives up at once
+      if (role == 0 && threadIdx.x == 0) __hip_atomic_store(err_first, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    pb.err = err_first;
+    pb.fbase = 0;
+  }
   if (role < NG)
     owner32<BP, ADAM, EXTRA>(a, pb, p, role, smem_p32);
   else
     head32<BP, ADAM, EXTRA>(a, pb, p, role - NG, smem_p32);
+  if (attempt && role == 0) {  // owner 0 completed the re-run: the gang recovered
+    __syncthreads();
+    if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      __hip_atomic_store(err_first, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // =============================================================================================
@@ -1070,14 +1099,14 @@ hipError_t prepare_f32_bp(int lds) {
   return prepare_f32<BP, false, true>(lds);
 }
 template <int BP>
-void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds) {
+void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds, int attempt) {
   const dim3 grid(8 * ROLES), block(NT);
   const bool adam = a.opt.kind == 0;
   const bool extra = a.anchor != nullptr || a.cg != nullptr;
-  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false>), grid, block, lds, s, a, pb, p_base);
-  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true>), grid, block, lds, s, a, pb, p_base);
-  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false>), grid, block, lds, s, a, pb, p_base);
-  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true>), grid, block, lds, s, a, pb, p_base);
+  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false>), grid, block, lds, s, a, pb, p_base, attempt);
+  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true>), grid, block, lds, s, a, pb, p_base, attempt);
 }
 
 }  // namespace
@@ -1095,6 +1124,16 @@ size_t mlp_persistent_f32_bytes(int P, int Bpad) {
 }
 size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
 int mlp_persistent_f32_gang() { return ROLES; }
+
+// Workgroups of one epoch launch (8 gangs) that the device can hold at once, from the occupancy
+// calculator for the instantiation the launch will use (registers, LDS, 512 threads).
+int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
+  int per_cu = 0;
+  const size_t lds = persistent_f32_lds(a);
+  const void* fn = a.Bpad == 64 ? (const void*)mlp_persistent_f32_epoch<64, true, false> : (const void*)mlp_persistent_f32_epoch<32, true, false>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
+  return per_cu * num_cus;
+}
 int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
 
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
@@ -1110,13 +1149,15 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
     if (e != hipSuccess) return e;
   }
   const size_t lds = persistent_f32_lds(a);
-  // groups of 8 peers: one launch each (a launch's gangs must all be co-resident: 192 CUs)
-  for (int p0 = 0; p0 < a.P; p0 += 8) {
-    if (a.Bpad == 64)
-      launch_f32_bp<64>(a, pb, s, p0, lds);
-    else
-      launch_f32_bp<32>(a, pb, s, p0, lds);
-  }
+  // groups of 8 peers: one launch each (a launch's gangs must all be co-resident: 192 CUs), then
+  // the recovery launches (attempt 1): a no-op exit for every gang that did not give up
+  for (int attempt = 0; attempt < 2; ++attempt)
+    for (int p0 = 0; p0 < a.P; p0 += 8) {
+      if (a.Bpad == 64)
+        launch_f32_bp<64>(a, pb, s, p0, lds, attempt);
+      else
+        launch_f32_bp<32>(a, pb, s, p0, lds, attempt);
+    }
   return hipGetLastError();
 }
 

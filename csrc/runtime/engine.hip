@@ -35,6 +35,9 @@ namespace {
 // Control words / active mask travel as kernel arguments (captured at launch), so the host never
 // enqueues a copy from pageable memory: nothing on the round's path blocks the host on the GPU.
 #define MLP_CTL_MAX 64
+// give-up words of a fit: [0, 64) per-peer first attempt (1 gave up, 2 recovered by the retry
+// launch), [64, 128) per-peer retry; the bf16 epoch uses word 0 for the whole launch
+#define MLP_ERR_WORDS 128
 struct CtlUpload {
   int4 ctl[MLP_CTL_MAX];
   int active[MLP_CTL_MAX];
@@ -58,10 +61,9 @@ __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long 
   }
   if (u.zero_conf)
     for (int q = p; q < u.P * 256; q += blockDim.x) u.zero_conf[q] = 0;
-  if (p == 0) {
-    *seed = u.seed;
-    if (u.zero_err) *u.zero_err = 0;
-  }
+  if (u.zero_err)
+    for (int q = p; q < MLP_ERR_WORDS; q += blockDim.x) u.zero_err[q] = 0;
+  if (p == 0) *seed = u.seed;
 }
 
 // Evaluation snapshot for the overlapped evaluation, in one launch: fp32 copy + bf16 shadow + W2T of
@@ -103,7 +105,16 @@ __global__ void k_publish(const float* loss, const int* correct, const int* err,
     o_loss[t] = loss[t];
     o_correct[t] = correct[t];
   }
-  if (t == 0) *o_err = err ? *err : 0;
+  // give-up status, bit 0: a give-up that was not recovered, bit 1: one recovered by the retry
+  __shared__ int st;
+  if (t == 0) st = 0;
+  __syncthreads();
+  if (err && t < MLP_ERR_WORDS) {
+    const int v = err[t];
+    if (v != 0) atomicOr(&st, (v == 2 && t < 64) ? 2 : 1);
+  }
+  __syncthreads();
+  if (t == 0) *o_err = st;
   if (conf && o_conf)
     for (int q = t; q < P * 256; q += blockDim.x) o_conf[q] = conf[q];
 }
@@ -173,11 +184,21 @@ struct MLPEngine {
     return mlp_persistent_supported(a);
   }
   // the fp32 path: every gang of a launch (8 peers x 24 workgroups) co-resident, one per CU
+  // Co-residency: the occupancy calculator (registers, LDS, 512 threads) must place the whole launch
+  // at once; epochs of every engine of the process run one after another (gang_order below), and
+  // the concurrent evaluation kernels are finite, so a launch is never starved for good — and a gang
+  // that still times out is re-run by the retry launch.
+  mutable int f32_cap_bpad = -1, f32_cap = 0;
   bool fp32_ready() const {
     if (pb32.h1x == nullptr || a.Xb16 == nullptr) return false;
-    if (8 * mlp_persistent_f32_gang() > num_cus) return false;
-    return mlp_persistent_f32_supported(a);
+    if (!mlp_persistent_f32_supported(a)) return false;
+    if (f32_cap_bpad != a.Bpad) {
+      f32_cap = mlp_persistent_f32_resident_capacity(a, num_cus);
+      f32_cap_bpad = a.Bpad;
+    }
+    return 8 * mlp_persistent_f32_gang() <= f32_cap;
   }
+  int recoveries = 0;
   int launch_epoch_kernel(hipStream_t s, bool zero_flags) {
     const hipError_t le = precision == 1 ? mlp_launch_persistent_f32_epoch(a, pb32, s, zero_flags) : mlp_launch_persistent_epoch(a, pb, s, zero_flags);
     if (le != hipSuccess) {
@@ -342,6 +363,19 @@ struct MLPEngine {
     return 0;
   }
 };
+
+// Persistent epochs of all engines in this process run in launch order (stream-ordered through
+// one event; the host never waits): two gangs' launches never compete for the same CUs. One
+// process per GPU is the deployment; ranks sharing a GPU are rehearsals.
+struct GangOrder {
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+  bool ev_ready = false;
+};
+GangOrder& gang_order() {
+  static GangOrder g;
+  return g;
+}
 
 }  // namespace
 
@@ -580,7 +614,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
       e->pb.flag_bytes = mlp_persistent_flag_bytes(P);
       rc |= e->alloc(&p, e->pb.flag_bytes);
       e->pb.flags = (unsigned*)p;
-      rc |= e->alloc(&p, 16);
+      rc |= e->alloc(&p, MLP_ERR_WORDS * sizeof(int));
       e->pb.err = (int*)p;
       if (mlp_persistent_prepare(a) != hipSuccess) e->persist_mode = 0;
       // fp32 exchange buffers + flags (err word shared)
@@ -697,7 +731,7 @@ int mlp_engine_begin(void* h, const int* active_host, void* stream) {
   if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
-  if (e->pb.err) CHECK_HIP(hipMemsetAsync(e->pb.err, 0, 16, s));
+  if (e->pb.err) CHECK_HIP(hipMemsetAsync(e->pb.err, 0, MLP_ERR_WORDS * sizeof(int), s));
   mlp_launch_sync_shadow(e->a, s);
   CHECK_HIP(hipGetLastError());
   return 0;
@@ -764,8 +798,8 @@ int mlp_f32_ok(int D0, int D1, int D2, int D3, int B) {
   int dev = 0, cus = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (8 * mlp_persistent_f32_gang() > cus) return 0;
-  return mlp_persistent_f32_supported(a) ? 1 : 0;
+  if (!mlp_persistent_f32_supported(a) || mlp_persistent_f32_prepare(a) != hipSuccess) return 0;
+  return 8 * mlp_persistent_f32_gang() <= mlp_persistent_f32_resident_capacity(a, cus) ? 1 : 0;
 }
 // Debug: the owners of the fp32 epoch write their W2 replica to `buf` ([P][D2][D1] fp32) after the
 // epoch (null = off), for the bitwise check against the heads' rows.
@@ -799,7 +833,17 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   const bool pa = e->graph_persistent && e->pending_zero_acc;
   if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh)) return 1;
   if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
-  CHECK_HIP(hipGraphLaunch(e->exec, s));
+  if (e->graph_persistent) {
+    GangOrder& go = gang_order();
+    std::lock_guard<std::mutex> og(go.mu);
+    if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
+    CHECK_HIP(hipGraphLaunch(e->exec, s));
+    if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
+    CHECK_HIP(hipEventRecord(go.ev, s));
+    go.ev_ready = true;
+  } else {
+    CHECK_HIP(hipGraphLaunch(e->exec, s));
+  }
   return 0;
 }
 
@@ -915,10 +959,24 @@ int mlp_engine_fetch(void* h, int slot, float* loss_host, int* correct_host, int
   memcpy(loss_host, r.loss, sizeof(float) * e->a.P);
   memcpy(correct_host, r.correct, sizeof(int) * e->a.P);
   if (conf_host) memcpy(conf_host, r.conf, sizeof(int) * e->a.P * 256);
-  if (*r.err != 0) {
-    g_last_error = "persistent MLP epoch gave up (a gang workgroup was not resident or a hand-off timed out)";
+  const int st = *r.err;
+  if (st & 2) e->recoveries++;
+  if (st & 1) {
+    g_last_error = "persistent MLP epoch gave up (a gang workgroup was not resident or a hand-off timed out) and its retry did not recover";
     return 3;
   }
+  return 0;
+}
+
+// Give-ups recovered by the retry launch so far (fetched results only).
+int mlp_engine_recoveries(void* h) { return ((MLPEngine*)h)->recoveries; }
+
+// Test hook: peer p's next fp32 epochs give up on their first attempt (p < 0: off). Re-captures.
+int mlp_engine_debug_giveup(void* h, int peer) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->a.debug_giveup = peer < 0 ? 0 : peer + 1;
+  e->invalidate();
   return 0;
 }
 

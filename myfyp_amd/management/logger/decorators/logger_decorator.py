@@ -44,6 +44,9 @@ class LoggerDecorator(P2PFLogger):
     def get_local_logs(self) -> LocalLogsType:
         return self._p2pflogger.get_local_logs()
 
+    def ingest_records(self, records) -> None:
+        self._p2pflogger.ingest_records(records)
+
     def get_global_logs(self) -> GlobalLogsType:
         return self._p2pflogger.get_global_logs()
 

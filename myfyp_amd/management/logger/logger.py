@@ -173,6 +173,17 @@ class P2PFLogger:
                             if (step, val) not in mine:
                                 self.local_metrics.add_log(exp, rnd, metric, node, val, step)
 
+    def ingest_records(self, records) -> None:
+        """Store metric records ``(addr, exp, round, metric, value, step)`` produced on another rank
+        (the live relay, ``management/logger/central.py``); no listener fires for them."""
+        for addr, exp, rnd, metric, value, step in records:
+            if step is None:
+                self.global_metrics.add_log(exp, rnd, metric, addr, value)
+            else:
+                mine = self.local_metrics.get_all_logs().get(exp, {}).get(rnd, {}).get(addr, {}).get(metric, [])
+                if (step, value) not in mine:
+                    self.local_metrics.add_log(exp, rnd, metric, addr, value, step)
+
     def get_local_logs(self) -> LocalLogsType:
         return self.local_metrics.get_all_logs()
 

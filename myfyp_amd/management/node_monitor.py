@@ -1,8 +1,14 @@
 """Resource monitor thread (parity: ``p2pfl/management/node_monitor.py:31-86``).
 
-Reports CPU %, RAM %, network MB/s like the reference and, new for MI355X, the GPU's allocated /
-reserved HBM (from the PyTorch-ROCm caching allocator, no extra tools needed). Fixes the
-reference's blocking ``.run()`` start: callers use ``.start()``.
+Reports CPU %, RAM % and network MB/s, like the reference. New for MI355X:
+- device telemetry through AMD SMI or sysfs (``device_telemetry.py``): power, GFX and HBM
+  activity, HBM used and total, temperature;
+- the caching allocator's allocated / reserved HBM;
+- weight-plane traffic from the federation's ``CommStats``: MB moved and MB/s per collective kind,
+  and the last latency in µs. The side-stream FedAvg pipeline is timed with HIP events.
+
+It also fixes the reference's blocking ``.run()`` start: callers use
+``.start()``.
 """
 
 from __future__ import annotations
@@ -25,6 +31,8 @@ class NodeMonitor(threading.Thread):
         self.period = Settings.RESOURCE_MONITOR_PERIOD
         self._stop_event = threading.Event()
         self._last_net = None
+        self._last_comm: Dict[str, tuple] = {}
+        self._telemetry = None
 
     def stop(self) -> None:
         self._stop_event.set()
@@ -58,6 +66,33 @@ class NodeMonitor(threading.Thread):
             if torch.cuda.is_available():
                 out["gpu_mem_allocated_gb"] = torch.cuda.memory_allocated() / 2**30
                 out["gpu_mem_reserved_gb"] = torch.cuda.memory_reserved() / 2**30
+                if self._telemetry is None:
+                    from myfyp_amd.management.device_telemetry import DeviceTelemetry
+
+                    self._telemetry = DeviceTelemetry(torch.cuda.current_device())
+                out.update(self._telemetry.sample())
         except Exception:
             pass
+        out.update(self.comm_sample())
+        return out
+
+    def comm_sample(self) -> Dict[str, float]:
+        """Per collective kind: cumulative MB, MB/s since the previous sample, last latency (µs)."""
+        from myfyp_amd.parallel.federation import Federation
+
+        fed = Federation._instance
+        if fed is None or getattr(fed, "comm", None) is None:
+            return {}
+        out: Dict[str, float] = {}
+        t = time.time()
+        snap = fed.comm.snapshot()
+        for kind, st in snap.items():
+            mb = st["bytes"] / 1e6
+            out[f"comm_{kind}_mb"] = mb
+            prev = self._last_comm.get(kind)
+            if prev is not None and t > prev[1]:
+                out[f"comm_{kind}_mb_s"] = (mb - prev[0]) / (t - prev[1])
+            self._last_comm[kind] = (mb, t)
+            if st["us_last"] is not None:
+                out[f"comm_{kind}_us"] = st["us_last"]
         return out

@@ -42,6 +42,64 @@ from myfyp_amd.utils.lockcheck import make_lock
 
 
 # ---------------------------------------------------------------------------------------------
+# communication statistics (node monitor: bytes moved, collective latency)
+# ---------------------------------------------------------------------------------------------
+class CommStats:
+    """Bytes and latency per collective kind. Host-timed calls record wall time; device-timed
+    ones (the side-stream FedAvg pipeline) record a pair of HIP events, resolved lazily when a
+    snapshot is taken, so recording never waits on the GPU."""
+
+    def __init__(self) -> None:
+        self._lock = threading.Lock()
+        self.bytes: Dict[str, int] = {}
+        self.calls: Dict[str, int] = {}
+        self.us_last: Dict[str, float] = {}
+        self.us_total: Dict[str, float] = {}
+        self._pending: List[tuple] = []
+
+    def _add(self, kind: str, nbytes: int, us: Optional[float]) -> None:
+        self.bytes[kind] = self.bytes.get(kind, 0) + int(nbytes)
+        self.calls[kind] = self.calls.get(kind, 0) + 1
+        if us is not None:
+            self.us_last[kind] = us
+            self.us_total[kind] = self.us_total.get(kind, 0.0) + us
+
+    def host(self, kind: str, nbytes: int, seconds: float) -> None:
+        with self._lock:
+            self._add(kind, nbytes, seconds * 1e6)
+
+    def device(self, kind: str, nbytes: int, ev0, ev1) -> None:
+        with self._lock:
+            self._pending.append((kind, int(nbytes), ev0, ev1))
+            if len(self._pending) > 256:  # never resolved (no snapshot taken): keep bytes, drop timing
+                k, b, _, _ = self._pending.pop(0)
+                self._add(k, b, None)
+
+    def snapshot(self) -> Dict[str, Dict[str, float]]:
+        with self._lock:
+            keep = []
+            for kind, nbytes, ev0, ev1 in self._pending:
+                try:
+                    done = ev1.query()
+                except Exception:
+                    done = True
+                    ev0 = None
+                if not done:
+                    keep.append((kind, nbytes, ev0, ev1))
+                    continue
+                us = None
+                if ev0 is not None:
+                    try:
+                        us = ev0.elapsed_time(ev1) * 1e3
+                    except Exception:
+                        us = None
+                self._add(kind, nbytes, us)
+            self._pending = keep
+            return {k: {"bytes": self.bytes[k], "calls": self.calls[k], "us_last": self.us_last.get(k), "us_total": self.us_total.get(k, 0.0)}
+                    for k in self.bytes}
+
+
+# ---------------------------------------------------------------------------------------------
 # cross-rank control bus
 # ---------------------------------------------------------------------------------------------
 class StoreBus:
@@ -63,9 +121,10 @@ class StoreBus:
     def _listen(self) -> None:
         # non-blocking counter poll with adaptive back-off: control messages are rare (start/stop,
         # heartbeats), and a blocking store.wait() would pin the store socket at shutdown
+        # after stop() one more pass delivers what is already queued (e.g. the relay's last metrics)
         seq = 1
         idle = 0.0005
-        while not self._stop.is_set():
+        while True:
             try:
                 ctr = self.store.add(f"mbox/{self.rank}/ctr", 0)
             except Exception:
@@ -73,11 +132,13 @@ class StoreBus:
                     return
                 continue
             if ctr < seq:
+                if self._stop.is_set():
+                    return
                 self._stop.wait(idle)
                 idle = min(idle * 2, 0.02)
                 continue
             idle = 0.0005
-            while seq <= ctr and not self._stop.is_set():
+            while seq <= ctr:
                 key = f"mbox/{self.rank}/{seq}"
                 try:
                     payload = self.store.get(key)
@@ -190,6 +251,8 @@ class Federation:
         self.device = device
         self.store = store
         self.bus: Optional[StoreBus] = None
+        self.central = None  # live metric relay to rank 0 (management/logger/central.py)
+        self.comm = CommStats()
         self.local_nodes: Dict[str, Any] = {}
         self.local_order: List[str] = []
         self.peers: Dict[str, int] = {}  # addr -> rank (all peers, after finalize)
@@ -287,6 +350,9 @@ class Federation:
         process), stop the control bus and tear down the process groups (call once, at exit).
         Departed ranks take the same path, so a job with a dead peer still ends cleanly."""
         synced = False
+        if self.central is not None:
+            self.central.stop()  # last flush to rank 0 while every rank is still here
+            self.central = None
         if self.shm is not None:
             self.shm.leave()
             synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT))
@@ -308,6 +374,9 @@ class Federation:
     @classmethod
     def reset(cls) -> None:
         inst = cls._instance
+        if inst is not None and inst.central is not None:
+            inst.central.stop()
+            inst.central = None
         if inst is not None and inst.bus is not None:
             inst.bus.stop()
         if inst is not None:
@@ -343,6 +412,11 @@ class Federation:
                 for other in self.peers:
                     if other != addr:
                         node.communication_protocol.connect(other)
+        if self.world > 1 and float(Settings.CENTRAL_LOG_PERIOD) > 0 and self.central is None:
+            from myfyp_amd.management.logger import logger
+            from myfyp_amd.management.logger.central import CentralLogRelay
+
+            self.central = CentralLogRelay(self, logger)
         self.finalized.set()
         return self.all_peers()
 
@@ -360,6 +434,16 @@ class Federation:
 
     def _deliver(self, dest: str, kind: str, msg: dict) -> None:
         from myfyp_amd.communication.protocols.memory.memory_communication_protocol import ServerRegistry
+        from myfyp_amd.management.logger.central import RELAY_ADDR, RELAY_KIND
+
+        if dest == RELAY_ADDR and kind == RELAY_KIND:  # live metrics of another rank (rank 0 only)
+            if self.central is not None:
+                self.central.ingest(msg)
+            else:
+                from myfyp_amd.management.logger import logger
+
+                logger.ingest_records([tuple(r) for r in msg.get("records") or []])
+            return
 
         server = ServerRegistry.get(dest)
         if server is None:
@@ -480,12 +564,14 @@ class Federation:
         rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
         flat = t.view(-1)
         bucket = max(1, Settings.BUCKET_BYTES // flat.element_size())
+        t0 = time.perf_counter()
         if flat.numel() <= bucket:
             dist.all_reduce(flat, op=rop, group=self._pg)
         else:
             works = [dist.all_reduce(flat[i : i + bucket], op=rop, group=self._pg, async_op=True) for i in range(0, flat.numel(), bucket)]
             for w in works:
                 w.wait()
+        self.comm.host("all_reduce", flat.numel() * flat.element_size(), time.perf_counter() - t0)
         return t
 
     def all_reduce_async(self, t: torch.Tensor):
@@ -497,6 +583,7 @@ class Federation:
             return None
         import torch.distributed as dist
 
+        self.comm.host("all_reduce_async", t.numel() * t.element_size(), 0.0)
         return dist.all_reduce(t, group=self._pg, async_op=True)
 
     def broadcast_(self, t: torch.Tensor, src_rank: int) -> torch.Tensor:
@@ -504,7 +591,9 @@ class Federation:
             return t
         import torch.distributed as dist
 
+        t0 = time.perf_counter()
         dist.broadcast(t, src=src_rank, group=self._pg)
+        self.comm.host("broadcast", t.numel() * t.element_size(), time.perf_counter() - t0)
         return t
 
     @property

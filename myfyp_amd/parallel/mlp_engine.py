@@ -368,11 +368,26 @@ class MLPGroup:
         loss = np.zeros(self.capacity, dtype=np.float32)
         correct = np.zeros(self.capacity, dtype=np.int32)
         conf = np.zeros((self.capacity, 16, 16), dtype=np.int32) if with_conf else None
+        before = self.recoveries()
         try:
             _native.check(lib.mlp_engine_fetch(self._engine, k, loss.ctypes.data, correct.ctypes.data, conf.ctypes.data if with_conf else None), "fetch")
         finally:
             self._slot_free[k].set()
+        if self.recoveries() != before:
+            from myfyp_amd.management.logger import logger
+
+            logger.warning("mlp-engine", "persistent epoch: a gang gave up (workgroup not resident) and was re-run by the retry launch")
         return loss, correct, conf
+
+    def recoveries(self) -> int:
+        """Give-ups of the persistent fp32 epoch that the in-stream retry launch recovered."""
+        return int(_native.load(required=True).mlp_engine_recoveries(self._engine)) if self._engine else 0
+
+    def debug_giveup(self, slot: Optional[int]) -> None:
+        """Test hook: the peer in ``slot`` gives up on the first attempt of every fp32 epoch."""
+        with self.lock:
+            self._ensure_engine()
+            _native.check(_native.load(required=True).mlp_engine_debug_giveup(self._engine, -1 if slot is None else int(slot)), "debug_giveup")
 
     def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)

@@ -172,6 +172,8 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
     bp = buf.data_ptr()
     ranges = bucket_ranges(n, Settings.BUCKET_BYTES)
     works = []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(cs)
     with torch.cuda.stream(cs):
         for k, (b0, b1) in enumerate(ranges):
             ops.check(fast.myfyp_fedavg_bucket_reduce(bp + 4 * (4 + b0), bp if k == 0 else None, src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream),
@@ -183,6 +185,8 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
             if apply is not None:
                 dst, dld, mp = apply
                 ops.check(fast.myfyp_fedavg_bucket_apply(dst + 4 * b0, bp + 4 * (4 + b0), bp, P, b1 - b0, dld, mp, cs.cuda_stream), "fedavg_bucket_apply")
+    ev1.record(cs)
+    fed.comm.device("fedavg_pipeline", 4 * (n + 1), ev0, ev1)  # resolved lazily by the node monitor
     buf.record_stream(cs)
     if apply is not None:
         cur.wait_stream(cs)  # stream-level: the next kernel on the compute stream sees the average

@@ -105,6 +105,8 @@ class Settings:
     # weights while the all-reduce runs; the averaged delta lands at the next aggregation
     # (x += avg_r - x_r); the last round aggregates exactly. Changes numerics.
     DELAYED_AVERAGING: bool = False
+    # ranks > 0 ship their metrics to rank 0 live, every this many seconds (0 disables the relay)
+    CENTRAL_LOG_PERIOD: float = 0.5
     SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
@@ -186,6 +188,7 @@ class Settings:
             "BUCKET_BYTES": "BUCKET_BYTES",
             "OVERLAP_COLLECTIVES": "OVERLAP_COLLECTIVES",
             "DELAYED_AVERAGING": "DELAYED_AVERAGING",
+            "CENTRAL_LOG_PERIOD": "CENTRAL_LOG_PERIOD",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",

@@ -254,3 +254,29 @@ def test_f32_partial_last_batch_and_bias(dev):
         for (name, pe), pr, pz in zip(l.model.get_model().named_parameters(), refs[i].parameters(), p0[i]):
             rel = _rel_update(pe, pr, pz)
             assert rel < 1e-4, f"peer {i} {name}: relative update error {rel:.2e}"
+
+
+def test_f32_giveup_recovered_by_retry_launch(dev):
+    """A gang that gives up (here: forced on its first attempt through the engine's test hook, as a
+    non-resident workgroup would) is re-run by the in-stream retry launch from the untouched
+    pre-epoch state: the epoch result is bit-identical to a run without the give-up, the other
+    peers are unaffected, and the engine counts one recovery per epoch."""
+    spec = {"name": "adam", "lr": 1e-3}
+    results = []
+    for forced in (False, True):
+        from myfyp_amd.parallel.mlp_engine import MLPGroup
+
+        MLPGroup.reset_all()
+        learners, refs, g, n = _setup(dev, 3, 64, 1500, 5, spec)
+        _pin_perms(dev, g, learners, n)
+        if forced:
+            g.debug_giveup(learners[1]._engine.slot)
+        _fit_all(learners)
+        _ = [l.evaluate() for l in learners]  # results fetched: give-up status checked
+        results.append(([l.flat_params().detach().clone() for l in learners], g.recoveries()))
+        if forced:
+            g.debug_giveup(None)
+    (p_ok, rec_ok), (p_rec, rec_rec) = results
+    assert rec_ok == 0 and rec_rec == 1, (rec_ok, rec_rec)
+    for a, b in zip(p_ok, p_rec):
+        assert torch.equal(a, b)

@@ -256,3 +256,50 @@ def test_yaml_runner_split_over_two_ranks():
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert res.returncode == 0, res.stderr[-3000:] + res.stdout[-2000:]
     assert res.stdout.count(" OK ") == 2, res.stdout
+
+
+@pytest.mark.slow
+def test_central_log_relay_two_ranks_gloo():
+    """Rank 0 sees the other rank's peers' metrics while the job runs (no end-of-run merge)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.join(root, "tests", "workers", "central_log_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert res.stdout.count("OK") == 2
+
+
+def test_node_monitor_reports_comm_stats():
+    """Weight-plane traffic shows up in the node monitor (bytes, rate, latency per kind)."""
+    from myfyp_amd.management.node_monitor import NodeMonitor
+    from myfyp_amd.parallel.federation import Federation
+
+    Federation.reset()
+    fed = Federation.init()
+    try:
+        mon = NodeMonitor("mon", lambda *a: None)
+        fed.comm.host("all_reduce", 4_000_000, 250e-6)
+        s1 = mon.sample()
+        assert s1["comm_all_reduce_mb"] == pytest.approx(4.0) and s1["comm_all_reduce_us"] == pytest.approx(250.0)
+        fed.comm.host("all_reduce", 6_000_000, 100e-6)
+        time.sleep(0.01)
+        s2 = mon.sample()
+        assert s2["comm_all_reduce_mb"] == pytest.approx(10.0) and s2["comm_all_reduce_mb_s"] > 0
+    finally:
+        Federation.reset()
+
+
+@pytest.mark.gpu
+def test_device_telemetry_reads_the_gpu():
+    """Power / HBM / activity of the training GPU through AMD SMI (or sysfs)."""
+    from myfyp_amd.management.device_telemetry import DeviceTelemetry
+
+    tel = DeviceTelemetry(0)
+    s = tel.sample()
+    print(tel.source, s)
+    assert tel.source in ("amdsmi", "sysfs"), "no telemetry source on the GPU box"
+    assert s.get("hbm_total_gb", 0) > 200  # MI355X: 288 GB HBM3E
+    assert "gpu_power_w" in s or "gpu_busy_pct" in s
