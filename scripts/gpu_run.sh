@@ -3,7 +3,8 @@
 #   OUT=<dir under gpurun_out> bash scripts/gpu_run.sh <step> [<step> ...]
 # steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), smoke, bench (fp32 headline),
 #        bench_bf16, bench_cnn, devagg (device SCAFFOLD/FedMedian tests + copy trace),
-#        overlap (side-stream / delayed FedAvg tests, bench, kernel overlap trace), prof (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
+#        overlap (side-stream / delayed FedAvg tests, bench, kernel overlap trace), prof, stamps,
+#        pmc (MLP counters), cnn_configs (BASELINE configs 3-5), cnn_prof (ResNet-18 kernel stats) (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
 #        gloo ranks on one GPU). Every GPU step runs under its own time limit; the script stops at
 #        the first failure, and at once after a timeout, abort or segfault.
 set -o pipefail
@@ -40,6 +41,20 @@ for step in "$@"; do
       run bench_cnn_delayed 600 python benchmarks/bench_cnn.py --delayed-averaging
       run overlap_prof 300 rocprofv3 --kernel-trace -d "$O/ovl" -o run -- python3 scripts/probes/overlap_probe.py
       python3 scripts/tools/kernel_overlap.py "$O"/ovl/run_results.db fedavg > "$O/overlap.txt"; cat "$O/overlap.txt" ;;
+    stamps)  # phase timestamps of the fp32 persistent epoch (library built with: python -m myfyp_amd.ops.build --stamps)
+      MYFYP_NATIVE_LIB=build/stamps/libmyfyp_hip.so run stamps_f32 200 python scripts/probes/stamps_f32.py ;;
+    pmc)  # counters of the MLP kernels, one pass per counter group (never with a trace domain)
+      run pmc_a 300 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+        --kernel-include-regex "mlp_" --output-format csv -d "$O/pmc_a" -o a -- python3 bench.py --steps 2 --warmup 1
+      run pmc_b 300 timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum \
+        --kernel-include-regex "mlp_" --output-format csv -d "$O/pmc_b" -o b -- python3 bench.py --steps 2 --warmup 1 ;;
+    cnn_configs)  # BASELINE configs 3, 4, 5
+      run lenet_ring 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 4
+      run resnet_fedavg 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      run resnet_fedprox_drop 400 python benchmarks/bench_cnn.py --model resnet18 --aggregator fedprox --dirichlet 0.5 --dropout --rounds 3 ;;
+    cnn_prof)  # kernel statistics of the ResNet-18 grouped step
+      run cnn_prof 400 rocprofv3 --kernel-trace --stats -d "$O/cnn_prof" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 1 \
+        --n-train 16384 --n-test 2048 ;;
     rehearsal)
       for n in 2 4; do
         MYFYP_DIST_BACKEND=gloo run rehearsal_gloo_n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
