@@ -59,6 +59,7 @@ using persist::gu32;
 using persist::row_max16;
 using persist::row_min16;
 using persist::row_sum16;
+using persist::st_wt128;
 using persist::st_wt32;
 
 constexpr int NT = 512;  // threads per workgroup (8 waves)
@@ -686,6 +687,15 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     float lr_t, inv_bc2;
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
 
+    // labels of this lane's softmax rows, loaded before the waits (off the critical path)
+    int yv[4] = {-1, -1, -1, -1};
+    if (wave < MT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 16 * wave + 4 * h + i;
+        if (b < rows) yv[i] = a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b];
+      }
+    }
     // ---- H1(t) from the 16 owners -> LDS (16-byte sc1 loads)
     if (hd == 0) P32_STAMP(1, t, 0);
     if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
@@ -745,41 +755,41 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       pl = mfma_f32(av.y, bv.y, pl);
       pl = mfma_f32(av.z, bv.z, pl);
       pl = mfma_f32(av.w, bv.w, pl);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) st_wt32(pb.plx + (((int64_t)p * NH + hd) * BP + 16 * wave + 4 * h + i) * 16 + c, pl[i]);
+      // plx[p][hd][wave][lane][i] = partial logit (row 16·wave + 4h + i, class c): the consuming lane
+      // of every head has the same (wave, h, c) and reads its four rows as one float4
+      const u32x4 pv = __builtin_bit_cast(u32x4, pl);
+      st_wt128(pb.plx + ((int64_t)p * NH + hd) * BP * 16, BP * 16 * 4, (wave * 64 + lane) * 16, pv);
     }
     if (hd == 0) P32_STAMP(1, t, 3);
     persist::publish(pb.flags, FPP, p, F_PL + hd, pb.fbase + (unsigned)(t + 1));
     if (hd == 0) P32_STAMP(1, t, 4);
 
-    // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3
+    // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3, straight
+    //      into the softmax lanes' registers
     if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 5);
-    if (tid < BP * 4) {
+    // ---- log-softmax + NLL + argmax + dlogits of the whole batch (wave w < MT: rows 16w..)
+    if (wave < MT) {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16, NH * BP * 16 * 4);
       float4 v[NH];
 #pragma unroll
-      for (int k = 0; k < NH; ++k) v[k] = ld_sc1_16(r, (k * BP * 16 + 4 * tv) * 4);
-      float4 s = v[0];
+      for (int k = 0; k < NH; ++k) v[k] = ld_sc1_16(r, (k * BP * 16 + (wave * 64 + lane) * 4) * 4);
+      float4 sl = v[0];
 #pragma unroll
       for (int k = 1; k < NH; ++k) {
-        s.x += v[k].x;
-        s.y += v[k].y;
-        s.z += v[k].z;
-        s.w += v[k].w;
+        sl.x += v[k].x;
+        sl.y += v[k].y;
+        sl.z += v[k].z;
+        sl.w += v[k].w;
       }
-      *reinterpret_cast<float4*>(sLg + (tv >> 2) * LD16 + 4 * (tv & 3)) = s;
-    }
-    lds_barrier();
-    // ---- log-softmax + NLL + argmax + dlogits of the whole batch (wave w < MT: rows 16w..)
-    if (wave < MT) {
+      const float lsum[4] = {sl.x, sl.y, sl.z, sl.w};
       const float b3 = sB3[c];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = 16 * wave + 4 * h + i;
         const bool rvalid = b < rows;
-        const int y = rvalid ? a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b] : -1;
-        const float logit = cin ? sLg[b * LD16 + c] + b3 : -INFINITY;
+        const int y = yv[i];
+        const float logit = cin ? lsum[i] + b3 : -INFINITY;
         const float mx = row_max16(logit);
         const float se = row_sum16(cin ? expf(logit - mx) : 0.f);
         const float logp = logit - (mx + logf(se));

@@ -27,6 +27,13 @@ __device__ __forceinline__ void st_wt(void* ptr, unsigned long long v) {  // 8-b
 __device__ __forceinline__ void st_wt32(float* ptr, float v) {  // 4-byte write-through store
   __hip_atomic_store((gu32*)ptr, __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+// 16-byte write-through (sc1) store at byte offset `off` (per lane) of a UNIFORM base: the buffer
+// resource must be wave-uniform (a per-lane base would be read from the first lane only)
+__device__ __forceinline__ void st_wt128(float* base, int bytes, int off, u32x4_t v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
 __device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
   return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
