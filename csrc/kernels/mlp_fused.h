@@ -62,6 +62,7 @@ struct MLPArgs {
   int* conf;         // [P][16][16] (eval) or null
   OptParams opt;
   int debug_giveup;  // fp32 persistent epoch test hook: peer + 1 whose first attempt gives up (0 = none)
+  int f32_ks;        // fp32 persistent epoch owner K split: 1, 2, or 0 = by P
 };
 
 bool mlp_shape_supported(int D0, int D1, int D2, int D3);

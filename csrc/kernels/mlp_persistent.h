@@ -39,7 +39,9 @@ bool mlp_persistent_f32_supported(const MLPArgs& a);
 size_t mlp_persistent_f32_bytes(int P, int Bpad);
 size_t mlp_persistent_f32_flag_bytes(int P);
 int mlp_persistent_f32_gang();
-int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus);             // workgroups (CUs) per peer
+int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus);
+int mlp_persistent_f32_launch_wgs(const MLPArgs& a);  // workgroups of one epoch launch
+int mlp_persistent_f32_ks(const MLPArgs& a);          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);

@@ -63,12 +63,19 @@ using persist::st_wt128;
 using persist::st_wt32;
 
 constexpr int NT = 512;  // threads per workgroup (8 waves)
-constexpr int NG = 16;   // owners per peer (D1 / 16)
+constexpr int NCG = 16;  // W1 column groups per peer (D1 / 16)
 constexpr int NH = 8;    // heads per peer (D2 / 16)
-constexpr int ROLES = NG + NH;
+constexpr int KSMAX = 2;
+// KS = K split of the owners: KS owners share a column group, each holding 1/KS of its K steps and
+// publishing a partial H1 slice (heads and the owner pair add the partials in kh order, so every
+// reader gets the same bits). KS = 1 when 8 peers share the GPU (8 x 24 workgroups); KS = 2 when at
+// most 4 do (4 x 40): the per-step owner work (forward, dW1, Adam, X staging) halves.
+__host__ __device__ constexpr int ng_of(int KS) { return NCG * KS; }         // owners per peer
+__host__ __device__ constexpr int roles_of(int KS) { return NCG * KS + NH; }  // workgroups per peer
+__host__ __device__ constexpr int ppl_of(int KS) { return KS == 1 ? 8 : 4; }  // peers per launch
 constexpr int PD1 = 256, PD2 = 128;
-constexpr int FPP = NG + 2 * NH;  // flags per peer
-constexpr int F_H1 = 0, F_PL = NG, F_DH2 = NG + NH;
+constexpr int FPP = NCG * KSMAX + 2 * NH;  // flags per peer (laid out for KSMAX)
+constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH;
 constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 799
 
 // K steps of the W1 GEMMs: D0 columns plus at least one padding column, column D0, which carries
@@ -164,10 +171,11 @@ struct OwnerLds32 {
   int ldt;  // bf16 row stride of the transposed dH1 split tiles [3][16][B]
   size_t x, red, h1, dh1s, w1x, ok, total;
 };
-__host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0) {
+// K steps of one owner: KH = ceil(KS1 / KS) (the last K-split owner may hold fewer)
+__host__ __device__ inline int kh_of(int D0, int KS) { return (ks1_of(D0) + KS - 1) / KS; }
+__host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0, int KS) {
   OwnerLds32 L;
-  const int ks1 = ks1_of(D0);
-  L.ldx = ks1 * 32 + 8;
+  L.ldx = kh_of(D0, KS) * 32 + 8;
   L.ldt = Bpad + 8;
   const int MT = Bpad / 16;
   const size_t red = (size_t)8 * MT * 64 * 16, dh2 = (size_t)Bpad * LDD * 4;
@@ -176,7 +184,7 @@ __host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0) {
   L.red = o;  o += al16(red > dh2 ? red : dh2);  // cross-wave partials, overlaid by the dH2 tile
   L.h1 = o;   o += al16((size_t)2 * Bpad * 16 * 4);  // own H1 slice, step-parity double buffer
   L.dh1s = o; o += al16((size_t)3 * 16 * L.ldt * 2);  // dH1ᵀ as hi / mid / lo bf16 (exact split)
-  L.w1x = o;  o += al16((size_t)4 * 16 * 32 * 4);     // W1 state of K step 24 (w, m, v, e)
+  L.w1x = o;  o += al16(KS == 1 ? (size_t)4 * 16 * 32 * 4 : 0);  // KS = 1: W1 state of K step 24 (w, m, v, e)
   L.ok = o;   o += 16;
   L.total = o;
   return L;
@@ -205,20 +213,27 @@ __host__ __device__ inline HeadLds32 head_lds32(int Bpad) {
 // =============================================================================================
 // owner workgroup
 // =============================================================================================
-// W1 state of one K step (16 rows × 32 columns, κ slot order) for the lanes of a wave, kept either in
-// registers (K steps < 24: three per wave) or, for K step 24 (wave 0, D0 > 767), in LDS: four
-// register slots per wave would not fit beside the working set of two waves per SIMD.
-constexpr int RQ = 3;  // register-resident K steps per wave
+// W1 state of one K step (16 rows × 32 columns, κ slot order) for the lanes of a wave, kept in
+// registers. KS = 1: K steps < 24 three per wave, and K step 24 (wave 0, D0 > 767) in LDS — four
+// register slots per wave would not fit beside the working set of two waves per SIMD. KS = 2: at
+// most 13 K steps per owner, two register slots per wave.
+__host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : 2; }
 
-template <int BP, bool ADAM, bool EXTRA>
+template <int BP, bool ADAM, bool EXTRA, int KS>
 __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem) {
   constexpr int MT = BP / 16;
+  constexpr int RQ = rq_of(KS);
   constexpr int XPT = BP / 4;  // 16-byte X chunks per lane: 4 K steps x BP rows x 4 chunks / 64 lanes
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, c = lane & 15;
-  const int D0 = a.D0, KS1 = ks1_of(D0);
-  const OwnerLds32 L = owner_lds32(BP, D0);
+  const int cg = g % NCG, kh = g / NCG;  // column group, K part
+  const int D0 = a.D0;
+  const int KH = kh_of(D0, KS);
+  const int s0 = kh * KH;  // first (global) K step of this owner; local K step j is global s0 + j
+  const int KS1 = (ks1_of(D0) - s0 < KH) ? ks1_of(D0) - s0 : KH;  // local K steps of this owner
+  const int C0 = 32 * s0;  // first global X column of the tile
+  const OwnerLds32 L = owner_lds32(BP, D0, KS);
   const int LDX = L.ldx, LDT = L.ldt;
   bf16* sX = reinterpret_cast<bf16*>(smem + L.x);
   f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
@@ -239,14 +254,14 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   // ---- resident W1 rows: wave w owns K steps w, w+8, w+16 (registers) and w+24 (LDS), κ slot
   //      order; the slot of column D0 holds b1
   float w1[RQ][8], m1[RQ][8], v1[RQ][8], e1[RQ][8];
-  const int orow = NG * g + c;
+  const int orow = NCG * cg + c;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < RQ + 1; ++q) {
     const int s = wave + 8 * q;
-    if (q == RQ && s >= KS1) break;
+    if (q == RQ && (KS != 1 || s >= KS1)) break;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const int k = 32 * s + 16 * half + 4 * h;
+      const int k = C0 + 32 * s + 16 * half + 4 * h;  // global W1 column
       float4 wv = {0.f, 0.f, 0.f, 0.f}, mv = wv, vv = wv, ev = wv;
       if (s < KS1 && k < D0) {
         const int64_t idx = pS + a.off_w1 + (int64_t)orow * D0 + k;
@@ -289,7 +304,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   float w2c[4], m2c[4], v2c[4], e2c[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t idx = pS + a.off_w2 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NG * g + c;
+    const int64_t idx = pS + a.off_w2 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NCG * cg + c;
     w2c[i] = a.params[idx];
     m2c[i] = fresh ? 0.f : a.m[idx];
     v2c[i] = (ADAM && !fresh) ? a.v[idx] : 0.f;
@@ -304,20 +319,25 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
       const int q = k / (BP / 16), kk = k % (BP / 16);
+      if (q > RQ || (q == RQ && KS != 1)) break;
       const int s = wave + 8 * q;
       const int idx = kk * 64 + lv;
-      const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
-      if (s < KS1 && col < D0) {
-        const bf16* src = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + col;
+      const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
+      if (s < KS1 && gcol < D0) {
+        const bf16* src = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + gcol;
         *reinterpret_cast<uint4*>(sX + r * LDX + col) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
-      } else if (s < KS1 && col == D0) {
+      } else if (s < KS1 && gcol == D0) {
         *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows);
       }
     }
   };
-  for (int e = tid; e < BP * (KS1 * 32 - D0); e += NT) {
-    const int r = e / (KS1 * 32 - D0), q = e % (KS1 * 32 - D0);
-    sX[r * LDX + D0 + q] = (bf16)0.f;
+  {  // columns past D0 (the bias column's K step) are zero for the whole epoch
+    const int z0 = D0 - C0, z1 = KS1 * 32;
+    if (z0 < z1)
+      for (int e = tid; e < BP * (z1 - z0); e += NT) {
+        const int r = e / (z1 - z0), q = e % (z1 - z0);
+        sX[r * LDX + z0 + q] = (bf16)0.f;
+      }
   }
   if (nsteps > 0) xw_stage(0, lane);
 
@@ -376,7 +396,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         fwd_kstep(q, acc);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -392,9 +412,10 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = 16 * mt + 4 * hh + i;
-        const float v = b < rows ? fmaxf(s[i], 0.f) : 0.f;  // b1 came in through the bias column
+        // b1 came in through the bias column; KS > 1: a partial sum (relu after the kh-ordered sum)
+        const float v = b < rows ? (KS == 1 ? fmaxf(s[i], 0.f) : s[i]) : 0.f;
         sH1c[b * 16 + cc] = v;
-        st_wt32(pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + cc, v);
+        st_wt32(pb.h1x + (((int64_t)p * KS + kh) * BP + b) * PD1 + NCG * cg + cc, v);
       }
     }
     if (g == 0) P32_STAMP(0, t, 1);
@@ -411,11 +432,11 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       const int rows_n = rows_at(a, n, t + 1);
       unsigned sink = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         const int s = wave + 8 * q;
         const int r = lane;
-        if (s < KS1 && 32 * s < D0 && r < rows_n && r < BP)
-          sink ^= *reinterpret_cast<const unsigned*>(a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B + r) * D0 + 32 * s);
+        if (s < KS1 && C0 + 32 * s < D0 && r < rows_n && r < BP)
+          sink ^= *reinterpret_cast<const unsigned*>(a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B + r) * D0 + C0 + 32 * s);
       }
       asm volatile("" ::"v"(sink));
     }
@@ -423,6 +444,29 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     // ================= C: backward of this slice
     if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (g == 0) P32_STAMP(0, t, 4);
+    if (KS > 1) {
+      // full H1 slice = the K parts' partials summed in kh order (the heads' order: same bits),
+      // relu; the other parts published theirs before the heads could produce this step's dH2
+      if (tid < BP * 4) {
+        const int b = tid >> 2, c4 = 4 * (tid & 3);
+        float4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k2 = 0; k2 < KS; ++k2) {
+          float4 v;
+          if (k2 == kh) {
+            v = *reinterpret_cast<const float4*>(sH1c + b * 16 + c4);
+          } else {
+            const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + ((int64_t)p * KS + k2) * BP * PD1, BP * PD1 * 4);
+            v = ld_sc1_16(r, (b * PD1 + NCG * cg + c4) * 4);
+          }
+          sum.x += v.x;
+          sum.y += v.y;
+          sum.z += v.z;
+          sum.w += v.w;
+        }
+        *reinterpret_cast<float4*>(sH1c + b * 16 + c4) = float4{fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f), fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)};
+      }
+    }
     {
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2, BP * PD2 * 4);
       float4 v[BP / 16];
@@ -483,7 +527,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       const int rows_next = more ? rows_at(a, n, t + 1) : 0;
       const bf16* xnext = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         const int s = wave + 8 * q;
         __builtin_amdgcn_sched_barrier(0);
         if (s < KS1) {
@@ -495,11 +539,11 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
           for (int kk = 0; kk < XQ; ++kk) {
             const int idx = kk * 64 + lv;
-            const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
+            const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
 #ifdef P32_EXP_NOX  // timing experiment: no next-batch staging loads
             xq[kk] = uint4{(unsigned)lv, 0u, 0u, 0u};
 #else
-            xq[kk] = (more && col < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + col)) : uint4{0u, 0u, 0u, 0u};
+            xq[kk] = (more && gcol < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + gcol)) : uint4{0u, 0u, 0u, 0u};
 #endif
           }
 #pragma unroll
@@ -536,10 +580,10 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
             for (int kk = 0; kk < XQ; ++kk) {
               const int idx = kk * 64 + lv;
-              const int r = idx >> 2, col = 32 * s + 8 * (idx & 3);
-              if (col < D0)
+              const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
+              if (gcol < D0)
                 *reinterpret_cast<uint4*>(sX + r * LDX + col) = xq[kk];
-              else if (col == D0)
+              else if (gcol == D0)
                 *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows_next);
             }
           }
@@ -555,11 +599,11 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   int64_t pS_w = pS;
   asm volatile("" : "+v"(orow_w), "+s"(pS_w));
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
     const int s = wave + 8 * q;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const int k = 32 * s + 16 * half + 4 * h;
+      const int k = C0 + 32 * s + 16 * half + 4 * h;  // global W1 column
       if (s >= KS1 || k > D0) continue;
       float4 w, m, v;
       if (q < RQ) {
@@ -590,14 +634,14 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   if (pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
     if (nsteps > 0) w2_replica_update(nsteps - 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NG * g + c] = w2c[i];
+    for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NCG * cg + c] = w2c[i];
   }
 }
 
 // =============================================================================================
 // head workgroup
 // =============================================================================================
-template <int BP, bool ADAM, bool EXTRA>
+template <int BP, bool ADAM, bool EXTRA, int KS>
 __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int hd, char* smem) {
   constexpr int MT = BP / 16;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -696,19 +740,33 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         if (b < rows) yv[i] = a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b];
       }
     }
-    // ---- H1(t) from the 16 owners -> LDS (16-byte sc1 loads)
+    // ---- H1(t) from the owners -> LDS (16-byte sc1 loads); KS > 1: the K parts' partials summed
+    //      in kh order (the owners' order: same bits), then relu
     if (hd == 0) P32_STAMP(1, t, 0);
-    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, NG, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, ng_of(KS), pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 1);
     {
-      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + (int64_t)p * BP * PD1, BP * PD1 * 4);
-      float4 v[BP / 8];
+      // every partial's loads issued before any is consumed (one L2 round trip, not KS)
+      float4 u[KS][BP / 8];
 #pragma unroll
-      for (int k = 0; k < BP / 8; ++k) v[k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 256 fp32 = BP*64 chunks
+      for (int k2 = 0; k2 < KS; ++k2) {
+        const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + ((int64_t)p * KS + k2) * BP * PD1, BP * PD1 * 4);
+#pragma unroll
+        for (int k = 0; k < BP / 8; ++k) u[k2][k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 256 fp32 = BP*64 chunks
+      }
 #pragma unroll
       for (int k = 0; k < BP / 8; ++k) {
+        float4 v = u[0][k];
+#pragma unroll
+        for (int k2 = 1; k2 < KS; ++k2) {
+          v.x += u[k2][k].x;
+          v.y += u[k2][k].y;
+          v.z += u[k2][k].z;
+          v.w += u[k2][k].w;
+        }
+        if (KS > 1) v = float4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
         const int e = tv + NT * k;
-        *reinterpret_cast<float4*>(sH1 + (e >> 6) * LDH1 + 4 * (e & 63)) = v[k];
+        *reinterpret_cast<float4*>(sH1 + (e >> 6) * LDH1 + 4 * (e & 63)) = v;
       }
     }
     lds_barrier();
@@ -899,8 +957,9 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
   }
 }
 
-// grid = 8 * ROLES blocks per group of 8 peers: block b serves peer p_base + (b & 7) in role b >> 3,
-// so a peer's 24 workgroups share one XCD under round-robin dispatch (speed only).
+// grid = ppl_of(KS) * roles_of(KS) blocks per group of peers: block b serves peer
+// p_base + b % ppl in role b / ppl, so a peer's workgroups share one XCD under round-robin dispatch
+// (speed only).
 //
 // Give-up recovery: a gang whose hand-off wait times out (a workgroup not resident, see
 // persist::wg_wait) stops without storing any parameter or optimizer state — every global write of
@@ -912,12 +971,13 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 constexpr unsigned RETRY_BASE = 1u << 24;
 constexpr int ERR_RETRY = 64;  // err layout: [0, 64) first attempt, [64, 128) retry, per peer
 
-template <int BP, bool ADAM, bool EXTRA>
+template <int BP, bool ADAM, bool EXTRA, int KS>
 __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base, int attempt) {
   extern __shared__ __attribute__((aligned(16))) char smem_p32[];
+  constexpr int PPL = ppl_of(KS);
   const int b = blockIdx.x;
-  const int p = p_base + (b & 7);
-  const int role = b >> 3;
+  const int p = p_base + b % PPL;
+  const int role = b / PPL;
   if (p >= a.P) return;
   const int4 ctl = a.ctl[p];
   if (!(ctl.x & 1) || ctl.y <= 0) return;
@@ -934,10 +994,10 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     pb.err = err_first;
     pb.fbase = 0;
   }
-  if (role < NG)
-    owner32<BP, ADAM, EXTRA>(a, pb, p, role, smem_p32);
+  if (role < ng_of(KS))
+    owner32<BP, ADAM, EXTRA, KS>(a, pb, p, role, smem_p32);
   else
-    head32<BP, ADAM, EXTRA>(a, pb, p, role - NG, smem_p32);
+    head32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32);
   if (attempt && role == 0) {  // owner 0 completed the re-run: the gang recovered
     __syncthreads();
     if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
@@ -1091,65 +1151,105 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
   }
 }
 
-size_t persistent_f32_lds(const MLPArgs& a) {
-  const size_t lo = owner_lds32(a.Bpad, a.D0).total, lh = head_lds32(a.Bpad).total;
+// K split of a launch: MYFYP_F32_KS=1|2 (tests), else the engine's choice (2 when every active peer
+// sits in the first ppl_of(2) slots: one launch of 40-workgroup gangs does all the work), else 2
+// when P <= ppl_of(2). The occupancy check below may still veto 2.
+int f32_ks_wanted(const MLPArgs& a) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("MYFYP_F32_KS");
+    env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+  }
+  if (env) return env;
+  if (a.f32_ks == 1 || a.f32_ks == 2) return a.f32_ks;  // the engine's choice (active peers)
+  return a.P <= ppl_of(2) ? 2 : 1;
+}
+
+size_t persistent_f32_lds_ks(const MLPArgs& a, int KS) {
+  const size_t lo = owner_lds32(a.Bpad, a.D0, KS).total, lh = head_lds32(a.Bpad).total;
   return lo > lh ? lo : lh;
 }
 
-template <int BP, bool ADAM, bool EXTRA>
-hipError_t prepare_f32(int lds) {
-  return hipFuncSetAttribute((const void*)mlp_persistent_f32_epoch<BP, ADAM, EXTRA>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+template <int BP, bool ADAM, bool EXTRA, int KS>
+const void* f32_fn() {
+  return (const void*)mlp_persistent_f32_epoch<BP, ADAM, EXTRA, KS>;
 }
-template <int BP>
+template <int BP, int KS>
 hipError_t prepare_f32_bp(int lds) {
-  hipError_t e;
-  if ((e = prepare_f32<BP, true, false>(lds)) != hipSuccess) return e;
-  if ((e = prepare_f32<BP, true, true>(lds)) != hipSuccess) return e;
-  if ((e = prepare_f32<BP, false, false>(lds)) != hipSuccess) return e;
-  return prepare_f32<BP, false, true>(lds);
+  const void* fns[4] = {f32_fn<BP, true, false, KS>(), f32_fn<BP, true, true, KS>(), f32_fn<BP, false, false, KS>(), f32_fn<BP, false, true, KS>()};
+  for (const void* fn : fns) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
-template <int BP>
+template <int BP, int KS>
 void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds, int attempt) {
-  const dim3 grid(8 * ROLES), block(NT);
+  const dim3 grid(ppl_of(KS) * roles_of(KS)), block(NT);
   const bool adam = a.opt.kind == 0;
   const bool extra = a.anchor != nullptr || a.cg != nullptr;
-  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false>), grid, block, lds, s, a, pb, p_base, attempt);
-  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true>), grid, block, lds, s, a, pb, p_base, attempt);
-  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false>), grid, block, lds, s, a, pb, p_base, attempt);
-  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true>), grid, block, lds, s, a, pb, p_base, attempt);
+  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false, KS>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true, KS>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false, KS>), grid, block, lds, s, a, pb, p_base, attempt);
+  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true, KS>), grid, block, lds, s, a, pb, p_base, attempt);
+}
+
+// Workgroups one launch of K split KS can have resident at once (occupancy calculator for the
+// instantiation: registers, LDS, 512 threads).
+int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS) {
+  int per_cu = 0;
+  const size_t lds = persistent_f32_lds_ks(a, KS);
+  const void* fn = KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2>() : f32_fn<32, true, false, 2>())
+                           : (a.Bpad == 64 ? f32_fn<64, true, false, 1>() : f32_fn<32, true, false, 1>());
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
+  return per_cu * num_cus;
+}
+
+// The K split actually used: the wanted one if its launch is co-resident, else 1.
+int f32_ks(const MLPArgs& a) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int want = f32_ks_wanted(a);
+  if (want == 2 && ppl_of(2) * roles_of(2) > resident_capacity_ks(a, cus, 2)) return 1;
+  return want;
 }
 
 }  // namespace
+
+size_t persistent_f32_lds(const MLPArgs& a) { return persistent_f32_lds_ks(a, f32_ks(a)); }
 
 bool mlp_persistent_f32_supported(const MLPArgs& a) {
   if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
   if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
   if (a.Bpad != 32 && a.Bpad != 64) return false;
   if ((a.cg == nullptr) != (a.cl == nullptr)) return false;
-  return persistent_f32_lds(a) <= 160 * 1024;
+  return persistent_f32_lds_ks(a, 1) <= 160 * 1024;
 }
 
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
-  return (size_t)P * ((size_t)Bpad * PD1 + (size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * sizeof(float);
+  return (size_t)P * ((size_t)KSMAX * Bpad * PD1 + (size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * sizeof(float);
 }
 size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
-int mlp_persistent_f32_gang() { return ROLES; }
+int mlp_persistent_f32_gang() { return roles_of(1); }
+int mlp_persistent_f32_ks(const MLPArgs& a) { return f32_ks(a); }
 
-// Workgroups of one epoch launch (8 gangs) that the device can hold at once, from the occupancy
-// calculator for the instantiation the launch will use (registers, LDS, 512 threads).
-int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
-  int per_cu = 0;
-  const size_t lds = persistent_f32_lds(a);
-  const void* fn = a.Bpad == 64 ? (const void*)mlp_persistent_f32_epoch<64, true, false> : (const void*)mlp_persistent_f32_epoch<32, true, false>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
-  return per_cu * num_cus;
-}
+// Workgroups one epoch launch needs (its peers' gangs) and how many the device holds at once.
+int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return ppl_of(f32_ks(a)) * roles_of(f32_ks(a)); }
+int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) { return resident_capacity_ks(a, num_cus, f32_ks(a)); }
 int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
 
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
-  const int lds = (int)persistent_f32_lds(a);
-  hipError_t e = a.Bpad == 64 ? prepare_f32_bp<64>(lds) : prepare_f32_bp<32>(lds);
-  if (e != hipSuccess) return e;
+  hipError_t e;
+  for (int KS = 1; KS <= KSMAX; ++KS) {
+    const int lds = (int)persistent_f32_lds_ks(a, KS);
+    e = KS == 1 ? (a.Bpad == 64 ? prepare_f32_bp<64, 1>(lds) : prepare_f32_bp<32, 1>(lds))
+                : (a.Bpad == 64 ? prepare_f32_bp<64, 2>(lds) : prepare_f32_bp<32, 2>(lds));
+    if (e != hipSuccess) return e;
+  }
   return hipFuncSetAttribute((const void*)mlp_eval_f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds32(a.D0));
 }
 
@@ -1158,15 +1258,20 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
     if (e != hipSuccess) return e;
   }
-  const size_t lds = persistent_f32_lds(a);
-  // groups of 8 peers: one launch each (a launch's gangs must all be co-resident: 192 CUs), then
-  // the recovery launches (attempt 1): a no-op exit for every gang that did not give up
+  const int KS = f32_ks(a);
+  const int ppl = ppl_of(KS);
+  const size_t lds = persistent_f32_lds_ks(a, KS);
+  // groups of ppl peers: one launch each (a launch's gangs must all be co-resident), then the
+  // recovery launches (attempt 1): a no-op exit for every gang that did not give up
   for (int attempt = 0; attempt < 2; ++attempt)
-    for (int p0 = 0; p0 < a.P; p0 += 8) {
-      if (a.Bpad == 64)
-        launch_f32_bp<64>(a, pb, s, p0, lds, attempt);
-      else
-        launch_f32_bp<32>(a, pb, s, p0, lds, attempt);
+    for (int p0 = 0; p0 < a.P; p0 += ppl) {
+      if (KS == 2) {
+        if (a.Bpad == 64) launch_f32_bp<64, 2>(a, pb, s, p0, lds, attempt);
+        else launch_f32_bp<32, 2>(a, pb, s, p0, lds, attempt);
+      } else {
+        if (a.Bpad == 64) launch_f32_bp<64, 1>(a, pb, s, p0, lds, attempt);
+        else launch_f32_bp<32, 1>(a, pb, s, p0, lds, attempt);
+      }
     }
   return hipGetLastError();
 }

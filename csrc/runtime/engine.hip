@@ -196,7 +196,7 @@ struct MLPEngine {
       f32_cap = mlp_persistent_f32_resident_capacity(a, num_cus);
       f32_cap_bpad = a.Bpad;
     }
-    return 8 * mlp_persistent_f32_gang() <= f32_cap;
+    return mlp_persistent_f32_launch_wgs(a) <= f32_cap;
   }
   int recoveries = 0;
   int launch_epoch_kernel(hipStream_t s, bool zero_flags) {
@@ -620,7 +620,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
       // fp32 exchange buffers + flags (err word shared)
       rc |= e->alloc(&p, mlp_persistent_f32_bytes(P, a.Bpad));
       e->pb32.h1x = (float*)p;
-      e->pb32.plx = e->pb32.h1x + (size_t)P * a.Bpad * 256;
+      e->pb32.plx = e->pb32.h1x + (size_t)2 * P * a.Bpad * 256;  // H1 partials of up to 2 K parts
       e->pb32.dh2x = e->pb32.plx + (size_t)P * 8 * a.Bpad * 16;
       e->pb32.flag_bytes = mlp_persistent_f32_flag_bytes(P);
       rc |= e->alloc(&p, e->pb32.flag_bytes);
@@ -799,7 +799,7 @@ int mlp_f32_ok(int D0, int D1, int D2, int D3, int B) {
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (!mlp_persistent_f32_supported(a) || mlp_persistent_f32_prepare(a) != hipSuccess) return 0;
-  return 8 * mlp_persistent_f32_gang() <= mlp_persistent_f32_resident_capacity(a, cus) ? 1 : 0;
+  return mlp_persistent_f32_launch_wgs(a) <= mlp_persistent_f32_resident_capacity(a, cus) ? 1 : 0;
 }
 // Debug: the owners of the fp32 epoch write their W2 replica to `buf` ([P][D2][D1] fp32) after the
 // epoch (null = off), for the bitwise check against the heads' rows.
@@ -970,6 +970,19 @@ int mlp_engine_fetch(void* h, int slot, float* loss_host, int* correct_host, int
 
 // Give-ups recovered by the retry launch so far (fetched results only).
 int mlp_engine_recoveries(void* h) { return ((MLPEngine*)h)->recoveries; }
+
+// fp32 persistent epoch: owner K split (1 or 2; 0 = by engine capacity). Re-captures on change.
+int mlp_engine_set_f32_ks(void* h, int ks) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (ks != e->a.f32_ks) {
+    e->a.f32_ks = ks;
+    e->f32_cap_bpad = -1;  // the co-resident capacity depends on the instantiation
+    e->invalidate();
+  }
+  return 0;
+}
+int mlp_engine_f32_ks(void* h) { return mlp_persistent_f32_ks(((MLPEngine*)h)->a); }
 
 // Test hook: peer p's next fp32 epochs give up on their first attempt (p < 0: off). Re-captures.
 int mlp_engine_debug_giveup(void* h, int peer) {

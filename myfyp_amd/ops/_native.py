@@ -87,6 +87,8 @@ _SIGNATURES = {
     "mlp_f32_ok": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "mlp_engine_set_w2chk": (c_int, [c_void_p, c_void_p]),
     "mlp_engine_recoveries": (c_int, [c_void_p]),
+    "mlp_engine_set_f32_ks": (c_int, [c_void_p, c_int]),
+    "mlp_engine_f32_ks": (c_int, [c_void_p]),
     "mlp_engine_debug_giveup": (c_int, [c_void_p, c_int]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
     "mlp_debug_persistent_f32_stamps": (c_int, [c_void_p]),  # likewise

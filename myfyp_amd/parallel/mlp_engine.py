@@ -151,6 +151,7 @@ class MLPGroup:
         self.extras: Dict[str, torch.Tensor] = {}
         self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
         self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
+        self.force_f32_ks: Optional[int] = None  # test hook: fp32 owner K split (1 or 2)
         # weight-stationary persistent epoch kernel (csrc/kernels/mlp_persistent.hip): None = auto
         # (used whenever the shape/optimizer is eligible), False = always the 3-launch step path
         self.persistent: Optional[bool] = None
@@ -227,6 +228,11 @@ class MLPGroup:
                 lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
             )
         _native.check(lib.mlp_engine_set_precision(self._engine, 1 if self.precision == "fp32" else 0), "set_precision")
+        # fp32 owner K split: 2 (40-workgroup gangs, half the owner work per step) when every
+        # attached peer sits in the first 4 slots, i.e. one launch covers them all — the case of
+        # one process per GPU with few peers each (N >= 2 GPUs in bench.py); 8 peers keep 1
+        ks = self.force_f32_ks or (2 if self.handles and max(self.handles) < 4 else 1)
+        _native.check(lib.mlp_engine_set_f32_ks(self._engine, ks), "set_f32_ks")
         if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
             _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
         if self._bound_version != self._data_version:
@@ -378,6 +384,12 @@ class MLPGroup:
 
             logger.warning("mlp-engine", "persistent epoch: a gang gave up (workgroup not resident) and was re-run by the retry launch")
         return loss, correct, conf
+
+    def f32_ks(self) -> int:
+        """Owner K split the fp32 persistent epoch uses (1 or 2)."""
+        with self.lock:
+            self._ensure_engine()
+            return int(_native.load(required=True).mlp_engine_f32_ks(self._engine))
 
     def recoveries(self) -> int:
         """Give-ups of the persistent fp32 epoch that the in-stream retry launch recovered."""

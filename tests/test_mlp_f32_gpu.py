@@ -121,13 +121,17 @@ def _rel_update(pe, pr, p0):
     return ((d_e - d_r).norm() / (d_r.norm() + 1e-30)).item()
 
 
+@pytest.mark.parametrize("ks", [1, 2])
 @pytest.mark.parametrize("B", [64, 32])
 @pytest.mark.parametrize("epochs", [1, 2])
-def test_f32_epoch_matches_torch_adam(dev, B, epochs):
+def test_f32_epoch_matches_torch_adam(dev, B, epochs, ks):
     """Whole local epochs of the fp32 persistent kernel (2 peers, Adam 1e-3, raw 0..255 inputs)
-    vs fp32 autograd + torch.optim.Adam on the same batches: relative update error < 1e-3."""
+    vs fp32 autograd + torch.optim.Adam on the same batches: relative update error < 1e-3. Both
+    owner K splits: 1 (24-workgroup gangs, the 8-peer layout) and 2 (40-workgroup gangs)."""
     spec = {"name": "adam", "lr": 1e-3}
     learners, refs, g, n = _setup(dev, 2, B, 1400, 3, spec)
+    g.force_f32_ks = ks
+    assert g.f32_ks() == ks
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     for l in learners:
