@@ -173,9 +173,11 @@ __global__ void k_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf1
 // ------------------------------------------------------------------------------------------------
 // BatchNorm backward: g = dz * [mask > 0]; partial (sum g, sum g*xhat) per block; optional g out
 // ------------------------------------------------------------------------------------------------
+// mss (optional, instead of mask): the ReLU mask is recomputed as y*sc + sh > 0 from this BN's
+// forward scale/shift — the activation relu(y*sc + sh) was never materialised
 __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps,
                                                        const float* ms, const int* nb, int hw, int Cp, float* part, int64_t part_ps, bf16* gout,
-                                                       int64_t gout_ps) {
+                                                       int64_t gout_ps, const float* mss) {
   const int peer = blockIdx.y;
   const int64_t rows = (int64_t)nb[peer] * hw;
   const int cpp = Cp / 8;
@@ -183,13 +185,15 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
   const int tid = threadIdx.x;
   const int c8 = tid % cpp, rr = tid / cpp;
   const float* mp = ms + peer * 2 * Cp;
-  float mean[8], inv[8], sg[8], sgx[8];
+  float mean[8], inv[8], sg[8], sgx[8], msc[8], msh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mean[j] = mp[c8 * 8 + j];
     inv[j] = mp[Cp + c8 * 8 + j];
     sg[j] = 0.f;
     sgx[j] = 0.f;
+    msc[j] = mss ? mss[peer * 2 * Cp + c8 * 8 + j] : 0.f;
+    msh[j] = mss ? mss[peer * 2 * Cp + Cp + c8 * 8 + j] : 0.f;
   }
   if (rr < rpp) {
     const int64_t per_blk = (rows + gridDim.x - 1) / gridDim.x;
@@ -215,9 +219,15 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
         if (r >= r1) break;
         float g[8], t[8];
         unpack8(vd[u], g);
-        unpack8(vm[u], t);
+        if (mss != nullptr) {
+          unpack8(vy[u], t);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+          for (int j = 0; j < 8; ++j) g[j] = fmaf(t[j], msc[j], msh[j]) > 0.f ? g[j] : 0.f;
+        } else {
+          unpack8(vm[u], t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = t[j] > 0.f ? g[j] : 0.f;
+        }
         if (gop != nullptr) *reinterpret_cast<uint4*>(gop + r * Cp) = pack8(g);
         unpack8(vy[u], t);
 #pragma unroll
@@ -279,7 +289,8 @@ __global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, 
 
 // dy = k1 * (g - mean_g - xhat * mean_gxhat), g recomputed from dz and mask
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps,
-                                                      const float* ms, const float* coef, const int* nb, int hw, int Cp, bf16* dy, int64_t dy_ps) {
+                                                      const float* ms, const float* coef, const int* nb, int hw, int Cp, bf16* dy, int64_t dy_ps,
+                                                      const float* mss) {
   const int peer = blockIdx.y;
   const int rows = nb[peer] * hw;
   const EwMap m(Cp);
@@ -287,9 +298,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz
   const int c0 = m.c8 * 8;
   const float* mp = ms + peer * 2 * Cp;
   const float* cp = coef + peer * 3 * Cp;
-  float mean[8], inv[8], k1[8], mg[8], mgx[8];
+  float mean[8], inv[8], k1[8], mg[8], mgx[8], msc[8], msh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    msc[j] = mss ? mss[peer * 2 * Cp + c0 + j] : 0.f;
+    msh[j] = mss ? mss[peer * 2 * Cp + Cp + c0 + j] : 0.f;
     mean[j] = mp[c0 + j];
     inv[j] = mp[Cp + c0 + j];
     k1[j] = cp[c0 + j];
@@ -322,7 +335,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz
       unpack8(vy[u], q);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float gg = t[j] > 0.f ? g[j] : 0.f;
+        const bool live = mss != nullptr ? fmaf(q[j], msc[j], msh[j]) > 0.f : t[j] > 0.f;
+        const float gg = live ? g[j] : 0.f;
         const float xh = (q[j] - mean[j]) * inv[j];
         g[j] = k1[j] * (gg - mg[j] - xh * mgx[j]);
       }
@@ -662,10 +676,10 @@ int cnn_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf16* res, in
   return ok();
 }
 int cnn_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms, const int* nb,
-                      int hw, int Cp, float* part, int64_t part_ps, int nblk, bf16* gout, int64_t gout_ps, int peers, void* s) {
+                      int hw, int Cp, float* part, int64_t part_ps, int nblk, bf16* gout, int64_t gout_ps, int peers, void* s, const float* mss) {
   if (Cp / 8 > 256 || (Cp & 7)) return 1;
   hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, y, y_ps, ms, nb, hw, Cp, part,
-                     part_ps, gout, gout_ps);
+                     part_ps, gout, gout_ps, mss);
   return ok();
 }
 int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps, const float* ms,
@@ -675,10 +689,10 @@ int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int*
   return ok();
 }
 int cnn_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms,
-                     const float* coef, const int* nb, int max_rows, int hw, int Cp, bf16* dy, int64_t dy_ps, int peers, void* s) {
+                     const float* coef, const int* nb, int max_rows, int hw, int Cp, bf16* dy, int64_t dy_ps, int peers, void* s, const float* mss) {
   if ((Cp & 7) || Cp / 8 > 256) return 1;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(ew_row_blocks(max_rows, Cp), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps,
-                     y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps);
+                     y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps, mss);
   return ok();
 }
 int cnn_relu_bwd(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const int* nb, int max_rows, int hw, int Cp, bf16* out,

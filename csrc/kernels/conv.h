@@ -34,6 +34,10 @@ struct ConvGemmArgs {
   // per-peer valid batch (rows = nb * out_h * out_w); nullptr = all max_batch rows
   const int* nbatch;
   int max_batch;
+  // MODE 0 prologue (optional): src holds a BatchNorm INPUT y; the A operand is relu(y*sc + sh)
+  // per channel ([sc | sh], 2*src_c floats per peer), padding taps stay 0 — the BN-apply + ReLU
+  // pass that would materialise it is skipped
+  const float* pro_ss; int64_t pro_ss_ps;
 };
 
 struct WgradArgs {
@@ -46,6 +50,8 @@ struct WgradArgs {
   int k_per_split;                      // rows of M per split (multiple of 64)
   const int* nbatch;
   int max_batch;
+  // optional prologue on x: relu(x*sc + sh) per channel (see ConvGemmArgs::pro_ss)
+  const float* pro_ss; int64_t pro_ss_ps;
 };
 
 extern "C" {

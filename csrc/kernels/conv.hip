@@ -46,6 +46,18 @@ __device__ __forceinline__ int fdiv(int x, int d, float inv) {
   return q;
 }
 
+// relu(v*sc + sh) on one 16-byte chunk of 8 bf16 channels (the k_bn_act arithmetic: fmaf, relu,
+// round to bf16 — bit-identical to the materialised activation)
+__device__ __forceinline__ uint4 bn_relu8(uint4 u, const float* sc, const float* sh) {
+  bf16 v[8];
+  __builtin_memcpy(v, &u, 16);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)fmaxf(fmaf((float)v[j], sc[j], sh[j]), 0.f);
+  uint4 r;
+  __builtin_memcpy(&r, v, 16);
+  return r;
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // [k][W] images read with ds_read_b64_tr_b16 (W = 64 or 128 bf16, unpadded rows): 8-byte granules
@@ -109,6 +121,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
+  const float* pro = (MODE == 0 && a.pro_ss != nullptr) ? a.pro_ss + peer * a.pro_ss_ps : nullptr;
   const int Ktot = (tR > 0 && tS > 0) ? tR * tS * a.src_c : 0;  // 0: a parity class no tap reaches (zeros + resid)
   const int nk = (Ktot + CG_BK - 1) / CG_BK;
   const int cc = tid & 7;            // this thread's 16-byte chunk within a K-step
@@ -192,6 +205,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
         pix = a_img[i] + h * a.src_w + w;
       }
       ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
+      if (MODE == 0 && pro != nullptr && ok) ra[i] = bn_relu8(ra[i], pro + c8 * 8, pro + a.src_c + c8 * 8);
     }
     // advance the A chunk by one K-step (8 chunks)
     ac8 += 8;
@@ -375,6 +389,14 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   }
   const int cca = tid % CA;
   const bool acol_ok = co0 + cca * 8 < a.dy_c;
+  // x prologue constants of this thread's fixed channel chunk (bci .. bci + 7)
+  const float* pro = a.pro_ss != nullptr ? a.pro_ss + peer * a.pro_ss_ps : nullptr;
+  float psc[8], psh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    psc[j] = (pro != nullptr && bcol_ok) ? pro[bci + j] : 1.f;
+    psh[j] = (pro != nullptr && bcol_ok) ? pro[a.x_c + bci + j] : 0.f;
+  }
 
   // per-row output coordinates (img, oh, ow) of this thread's B rows, advanced by +64 pixels per
   // K-step with carries (no per-step division)
@@ -402,6 +424,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
       const int h = b_oh[i] * a.stride + hb, w = b_ow[i] * a.stride + wb;
       const bool ok = bcol_ok && m < kend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) : make_uint4(0, 0, 0, 0);
+      if (pro != nullptr && ok) rb[i] = bn_relu8(rb[i], psc, psh);
       b_ow[i] += d_ow;
       if (b_ow[i] >= a.Wo) { b_ow[i] -= a.Wo; ++b_oh[i]; }
       b_oh[i] += d_oh;

@@ -47,7 +47,7 @@ class ConvGemmArgs(ctypes.Structure):
         ("wt", c_void_p), ("wt_ps", c_int64), ("ncol", c_int), ("ncol_valid", c_int),
         ("out", c_void_p), ("out_ps", c_int64), ("bias", c_void_p), ("bias_ps", c_int64),
         ("resid", c_void_p), ("resid_ps", c_int64), ("relu", c_int), ("stats", c_void_p), ("stats_ps", c_int64),
-        ("nbatch", c_void_p), ("max_batch", c_int),
+        ("nbatch", c_void_p), ("max_batch", c_int), ("pro_ss", c_void_p), ("pro_ss_ps", c_int64),
     ]
 
 
@@ -57,7 +57,7 @@ class WgradArgs(ctypes.Structure):
         ("H", c_int), ("W", c_int), ("x_c", c_int), ("Ho", c_int), ("Wo", c_int), ("dy_c", c_int),
         ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int),
         ("grad", c_void_p), ("grad_ps", c_int64), ("accumulate", c_int), ("k_per_split", c_int),
-        ("nbatch", c_void_p), ("max_batch", c_int),
+        ("nbatch", c_void_p), ("max_batch", c_int), ("pro_ss", c_void_p), ("pro_ss_ps", c_int64),
     ]
 
 
@@ -97,9 +97,9 @@ _SIGS = {
     "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_act": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
-    "cnn_bn_bwd_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_bn_bwd_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "cnn_bn_bwd_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
-    "cnn_bn_bwd_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
+    "cnn_bn_bwd_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "cnn_relu_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_colsum": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "cnn_maxpool2": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
@@ -214,6 +214,9 @@ class CNNGroup:
         self.extras: Dict[str, torch.Tensor] = {}
         self.perm_fn = None
         self.eager = False
+        # ResNet blocks: BN1-apply + ReLU folded into conv2's forward / wgrad operand prologues and
+        # its ReLU mask recomputed in the BN backward (MYFYP_CNN_FUSE_BN=0: the materialised a1 path)
+        self.fuse_bn1 = os.environ.get("MYFYP_CNN_FUSE_BN", "1") != "0"
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
         self._data_version = 0
@@ -448,7 +451,9 @@ class CNNGroup:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None) -> None:
+    def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None,
+             pro: Optional["BNL"] = None) -> None:
+        """``pro``: src holds that BatchNorm's input y; the conv reads relu(BN(y)) in its prologue."""
         lib, P = _lib(), self.capacity
         shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
@@ -473,6 +478,9 @@ class CNNGroup:
         if stats is not None:
             a.stats, a.stats_ps = stats.data_ptr(), stats.shape[1]
         a.nbatch, a.max_batch = self.nb.data_ptr(), self.B
+        if pro is not None:
+            ss = self.ss(pro)
+            a.pro_ss, a.pro_ss_ps = ss.data_ptr(), ss.shape[1]
         _chk(lib.conv_gemm_launch(mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
@@ -484,7 +492,7 @@ class CNNGroup:
         k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
         return k_per, (M + k_per - 1) // k_per
 
-    def wgrad(self, L: ConvL, dy: torch.Tensor, x: torch.Tensor) -> None:
+    def wgrad(self, L: ConvL, dy: torch.Tensor, x: torch.Tensor, pro: Optional["BNL"] = None) -> None:
         lib, P = _lib(), self.capacity
         a = WgradArgs()
         a.dy, a.dy_ps, a.x, a.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
@@ -494,6 +502,9 @@ class CNNGroup:
         k_per, splits = self._wgrad_split(L)
         a.accumulate = int(splits > 1)  # must match the segment's zero_after (the optimizer re-zeroes)
         a.k_per_split, a.nbatch, a.max_batch = k_per, self.nb.data_ptr(), self.B
+        if pro is not None:
+            ss = self.ss(pro)
+            a.pro_ss, a.pro_ss_ps = ss.data_ptr(), ss.shape[1]
         _chk(lib.conv_wgrad_launch(ctypes.byref(a), P, splits, self._stream()), f"wgrad {L.name}")
 
     def bn_fin(self, bn: BNL, stats: torch.Tensor, rows: int, hw: int, train: bool) -> None:
@@ -518,21 +529,23 @@ class CNNGroup:
                             y2.shape[1] if y2 is not None else 0, self.ss(bn2).data_ptr() if bn2 is not None else None, int(relu), self.nb.data_ptr(),
                             self.B * hw, hw, bn.Cp, out.data_ptr(), out.shape[1], P, self._stream()), f"bn_act {bn.name}")
 
-    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None) -> None:
+    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None, mask_from_y: bool = False) -> None:
+        """``mask_from_y``: the ReLU after this BN was never materialised; its mask is y*sc + sh > 0."""
         lib, P = _lib(), self.capacity
+        mss = self.ss(bn).data_ptr() if mask_from_y else None
         nblk = max(1, min(128, (self.B * hw + 255) // 256))
         part = self.fbuf(f"bnsum_{bn.name}", 2 * bn.Cp)  # atomically accumulated, re-zeroed by the finalize
         coef = self.fbuf(f"bncoef_{bn.name}", 3 * bn.Cp)
         _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
                                    self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
-                                   gout.shape[1] if gout is not None else 0, P, self._stream()), f"bn_bwd_reduce {bn.name}")
+                                   gout.shape[1] if gout is not None else 0, P, self._stream(), mss), f"bn_bwd_reduce {bn.name}")
         gbase = self.grad.data_ptr()
         _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nblk, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
                                      self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight), gbase + 4 * self._off(bn.module.bias),
                                      bn.C, bn.Cp, coef.data_ptr(), P, self._stream()), f"bn_bwd_finalize {bn.name}")
         _chk(lib.cnn_bn_bwd_apply(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
                                   self.ms(bn).data_ptr(), coef.data_ptr(), self.nb.data_ptr(), self.B * hw, hw, bn.Cp, dy_out.data_ptr(),
-                                  dy_out.shape[1], P, self._stream()), f"bn_bwd_apply {bn.name}")
+                                  dy_out.shape[1], P, self._stream(), mss), f"bn_bwd_apply {bn.name}")
 
     def relu_bwd(self, dz, mask, out, hw, cp) -> None:
         _chk(_lib().cnn_relu_bwd(dz.data_ptr(), dz.shape[1], mask.data_ptr(), mask.shape[1], self.nb.data_ptr(), self.B * hw, hw, cp, out.data_ptr(),
@@ -573,11 +586,14 @@ class CNNGroup:
             st1 = self.fbuf(f"st1_{bi}", rows1 * 2 * c1.cp_out) if train else None
             self.conv(c1, a_in, y1, stats=st1)
             self.bn_fin(bn1, st1, rows1, hw1, train)
-            a1 = self.act(f"a1_{bi}", B * hw1, c1.cp_out)
-            self.bn_act(bn1, y1, a1, hw1)
             y2 = self.act(f"y2_{bi}", B * hw1, c2.cp_out)
             st2 = self.fbuf(f"st2_{bi}", rows1 * 2 * c2.cp_out) if train else None
-            self.conv(c2, a1, y2, stats=st2)
+            if self.fuse_bn1:  # BN1-apply + ReLU in conv2's operand prologue (a1 never written)
+                self.conv(c2, y1, y2, stats=st2, pro=bn1)
+            else:
+                a1 = self.act(f"a1_{bi}", B * hw1, c1.cp_out)
+                self.bn_act(bn1, y1, a1, hw1)
+                self.conv(c2, a1, y2, stats=st2)
             self.bn_fin(bn2, st2, rows1, hw1, train)
             a = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
             if proj is not None:
@@ -615,7 +631,8 @@ class CNNGroup:
             hw1 = c1.ho * c1.wo
             a_out = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
             a_in = self.act(f"a2_{bi - 1}", B * c1.h * c1.w, c1.cp_in) if bi > 0 else self.act("a_stem", B * c1.h * c1.w, c1.cp_in)
-            y1, a1, y2 = self.act(f"y1_{bi}", B * hw1, c1.cp_out), self.act(f"a1_{bi}", B * hw1, c1.cp_out), self.act(f"y2_{bi}", B * hw1, c2.cp_out)
+            y1, y2 = self.act(f"y1_{bi}", B * hw1, c1.cp_out), self.act(f"y2_{bi}", B * hw1, c2.cp_out)
+            a1 = None if self.fuse_bn1 else self.act(f"a1_{bi}", B * hw1, c1.cp_out)
             dy2 = self.act(f"dy2_{bi}", B * hw1, c2.cp_out)
             d_in = self.act(f"d_out_{bi - 1}" if bi > 0 else "d_stem", B * c1.h * c1.w, c1.cp_in)
             if proj is not None:
@@ -634,9 +651,13 @@ class CNNGroup:
                 resid = g
             da1 = self.act(f"da1_{bi}", B * hw1, c1.cp_out)
             self.conv(c2, dy2, da1, mode=1)
-            self.wgrad(c2, dy2, a1)
             dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
-            self.bn_bwd(bn1, da1, a1, y1, dy1, hw1)
+            if self.fuse_bn1:
+                self.wgrad(c2, dy2, y1, pro=bn1)
+                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, mask_from_y=True)
+            else:
+                self.wgrad(c2, dy2, a1)
+                self.bn_bwd(bn1, da1, a1, y1, dy1, hw1)
             self.conv(c1, dy1, d_in, mode=1, resid=resid)
             self.wgrad(c1, dy1, a_in)
             d = d_in
