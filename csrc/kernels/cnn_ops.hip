@@ -175,6 +175,7 @@ __global__ void k_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf1
 // ------------------------------------------------------------------------------------------------
 // mss (optional, instead of mask): the ReLU mask is recomputed as y*sc + sh > 0 from this BN's
 // forward scale/shift — the activation relu(y*sc + sh) was never materialised
+template <bool MSS>
 __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps,
                                                        const float* ms, const int* nb, int hw, int Cp, float* part, int64_t part_ps, bf16* gout,
                                                        int64_t gout_ps, const float* mss) {
@@ -192,14 +193,14 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
     inv[j] = mp[Cp + c8 * 8 + j];
     sg[j] = 0.f;
     sgx[j] = 0.f;
-    msc[j] = mss ? mss[peer * 2 * Cp + c8 * 8 + j] : 0.f;
-    msh[j] = mss ? mss[peer * 2 * Cp + Cp + c8 * 8 + j] : 0.f;
+    msc[j] = MSS ? mss[peer * 2 * Cp + c8 * 8 + j] : 0.f;
+    msh[j] = MSS ? mss[peer * 2 * Cp + Cp + c8 * 8 + j] : 0.f;
   }
   if (rr < rpp) {
     const int64_t per_blk = (rows + gridDim.x - 1) / gridDim.x;
     const int64_t r0 = blockIdx.x * per_blk, r1 = min(rows, r0 + per_blk);
     const bf16* dzp = dz + peer * dz_ps + c8 * 8;
-    const bf16* mkp = mask ? mask + peer * mask_ps + c8 * 8 : nullptr;
+    const bf16* mkp = (!MSS && mask) ? mask + peer * mask_ps + c8 * 8 : nullptr;
     const bf16* yp = y + peer * y_ps + c8 * 8;
     bf16* gop = gout ? gout + peer * gout_ps + c8 * 8 : nullptr;
     for (int64_t rb = r0 + rr; rb < r1; rb += EW_RU * rpp) {
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
         if (r >= r1) break;
         float g[8], t[8];
         unpack8(vd[u], g);
-        if (mss != nullptr) {
+        if (MSS) {
           unpack8(vy[u], t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) g[j] = fmaf(t[j], msc[j], msh[j]) > 0.f ? g[j] : 0.f;
@@ -288,6 +289,7 @@ __global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, 
 }
 
 // dy = k1 * (g - mean_g - xhat * mean_gxhat), g recomputed from dz and mask
+template <bool MSS>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps,
                                                       const float* ms, const float* coef, const int* nb, int hw, int Cp, bf16* dy, int64_t dy_ps,
                                                       const float* mss) {
@@ -301,8 +303,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz
   float mean[8], inv[8], k1[8], mg[8], mgx[8], msc[8], msh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    msc[j] = mss ? mss[peer * 2 * Cp + c0 + j] : 0.f;
-    msh[j] = mss ? mss[peer * 2 * Cp + Cp + c0 + j] : 0.f;
+    msc[j] = MSS ? mss[peer * 2 * Cp + c0 + j] : 0.f;
+    msh[j] = MSS ? mss[peer * 2 * Cp + Cp + c0 + j] : 0.f;
     mean[j] = mp[c0 + j];
     inv[j] = mp[Cp + c0 + j];
     k1[j] = cp[c0 + j];
@@ -312,6 +314,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz
   dz += peer * dz_ps + c0;
   y += peer * y_ps + c0;
   dy += peer * dy_ps + c0;
+  if (MSS) mask = nullptr;
   if (mask) mask += peer * mask_ps + c0;
   const int step = gridDim.x * m.rpb;
   for (int r0 = blockIdx.x * m.rpb + m.r; r0 < rows; r0 += EW_RU * step) {
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const bf16* dz, int64_t dz
       unpack8(vy[u], q);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bool live = mss != nullptr ? fmaf(q[j], msc[j], msh[j]) > 0.f : t[j] > 0.f;
+        const bool live = MSS ? fmaf(q[j], msc[j], msh[j]) > 0.f : t[j] > 0.f;
         const float gg = live ? g[j] : 0.f;
         const float xh = (q[j] - mean[j]) * inv[j];
         g[j] = k1[j] * (gg - mg[j] - xh * mgx[j]);
@@ -678,8 +681,12 @@ int cnn_bn_act(const bf16* y, int64_t y_ps, const float* ss, const bf16* res, in
 int cnn_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms, const int* nb,
                       int hw, int Cp, float* part, int64_t part_ps, int nblk, bf16* gout, int64_t gout_ps, int peers, void* s, const float* mss) {
   if (Cp / 8 > 256 || (Cp & 7)) return 1;
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, y, y_ps, ms, nb, hw, Cp, part,
-                     part_ps, gout, gout_ps, mss);
+  if (mss != nullptr)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<true>, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, y, y_ps, ms, nb, hw, Cp,
+                       part, part_ps, gout, gout_ps, mss);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<false>, dim3(nblk, peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps, y, y_ps, ms, nb, hw, Cp,
+                       part, part_ps, gout, gout_ps, mss);
   return ok();
 }
 int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps, const float* ms,
@@ -691,8 +698,12 @@ int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int*
 int cnn_bn_bwd_apply(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const bf16* y, int64_t y_ps, const float* ms,
                      const float* coef, const int* nb, int max_rows, int hw, int Cp, bf16* dy, int64_t dy_ps, int peers, void* s, const float* mss) {
   if ((Cp & 7) || Cp / 8 > 256) return 1;
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(ew_row_blocks(max_rows, Cp), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps,
-                     y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps, mss);
+  if (mss != nullptr)
+    hipLaunchKernelGGL(k_bn_bwd_apply<true>, dim3(ew_row_blocks(max_rows, Cp), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps,
+                       y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps, mss);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<false>, dim3(ew_row_blocks(max_rows, Cp), peers), dim3(256), 0, (hipStream_t)s, dz, dz_ps, mask, mask_ps,
+                       y, y_ps, ms, coef, nb, hw, Cp, dy, dy_ps, mss);
   return ok();
 }
 int cnn_relu_bwd(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t mask_ps, const int* nb, int max_rows, int hw, int Cp, bf16* out,

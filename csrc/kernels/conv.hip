@@ -1,6 +1,6 @@
 // Implicit-GEMM convolutions on MFMA (gfx950, wave64), grouped over co-located peers.
 //
-// k_conv_gemm<MODE, BN>: C[M][Ncol] = A[M][K] · B[K][Ncol]
+// k_conv_gemm<MODE, BN, PRO>: C[M][Ncol] = A[M][K] · B[K][Ncol]
 //   MODE 0 (forward) : rows = output pixels, A = im2col(X) gathered on the fly, K = (r, s, ci),
 //                      B = Wf[co][r][s][ci] rows (K-contiguous), staged [n][k] XOR-swizzled
 //   MODE 1 (dgrad)   : rows = input pixels,  A = dY gathered at ((h+pad-r)/st, (w+pad-s)/st) when
@@ -15,7 +15,7 @@
 //   Fused epilogue: + bias, + residual, ReLU, zeroed channel padding, BatchNorm sums (atomics).
 //   XCD-aware bijective block remap so tiles sharing an operand panel land on one L2.
 //
-// k_conv_wgrad<BM, BN>: dW[co][(r,s,ci)] = sum_m dY[m][co] · im2col(X)[m][(r,s,ci)]
+// k_conv_wgrad<BM, BN, PRO>: dW[co][(r,s,ci)] = sum_m dY[m][co] · im2col(X)[m][(r,s,ci)]
 //   K = pixels (split over workgroups), both operands staged [m][channels] as loaded and read
 //   as MFMA fragments with the transposed LDS read. The gradient is written in the GEMM's own
 //   (Wf) layout [cp_out][R][S][cp_in] fp32: 16 lanes of a row write 64 contiguous bytes (plain
@@ -86,7 +86,7 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, in
   return __builtin_bit_cast(bf16x8, both);
 }
 
-template <int MODE, int BN>
+template <int MODE, int BN, bool PRO>
 __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
   // MODE 0 forward, MODE 1 dgrad (all taps), MODE 2 strided dgrad by output parity class
   // (blockIdx.y = class (ph, pw): rows are the dX pixels (2hh+ph, 2ww+pw), K walks only the taps
@@ -121,7 +121,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
-  const float* pro = (MODE == 0 && a.pro_ss != nullptr) ? a.pro_ss + peer * a.pro_ss_ps : nullptr;
+  // PRO (MODE 0): the source is a BN output y; the A operand is relu(y*sc + sh) of the previous
+  // BatchNorm, applied when the staged registers go to LDS (after this K-step's MFMAs, so the
+  // loads stay in flight across them; transforming at load time put a vmcnt(0) before the MFMAs)
+  const float* pro = PRO ? a.pro_ss + peer * a.pro_ss_ps : nullptr;
   const int Ktot = (tR > 0 && tS > 0) ? tR * tS * a.src_c : 0;  // 0: a parity class no tap reaches (zeros + resid)
   const int nk = (Ktot + CG_BK - 1) / CG_BK;
   const int cc = tid & 7;            // this thread's 16-byte chunk within a K-step
@@ -175,6 +178,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   }
   const int RS = a.R * a.S, TT = tR * tS;
   uint4 ra[AR], rb[NB];
+  float4 psc[2], psh[2];  // PRO: scale / shift of the staged chunk's 8 channels
+  unsigned aok = 0;       // PRO: staged A rows that are real pixels (padding stays 0, not relu(sh))
   auto load = [&](int kt) {
     const int k = kt * CG_BK + cc * 8;
     const bool kok = ar < tR;
@@ -205,7 +210,13 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
         pix = a_img[i] + h * a.src_w + w;
       }
       ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
-      if (MODE == 0 && pro != nullptr && ok) ra[i] = bn_relu8(ra[i], pro + c8 * 8, pro + a.src_c + c8 * 8);
+      if (PRO) aok = ok ? (aok | (1u << i)) : (aok & ~(1u << i));
+    }
+    if (PRO) {
+      const float4* p4 = reinterpret_cast<const float4*>(pro + c8 * 8);
+      const float4* q4 = reinterpret_cast<const float4*>(pro + a.src_c + c8 * 8);
+      psc[0] = p4[0]; psc[1] = p4[1];
+      psh[0] = q4[0]; psh[1] = q4[1];
     }
     // advance the A chunk by one K-step (8 chunks)
     ac8 += 8;
@@ -243,7 +254,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
     bf16* As = lds + buf * BUF;
     bf16* Bs = As + BM * CG_BK;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(As + swz((tid >> 3) + 32 * i, cc)) = ra[i];
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = ra[i];
+      if (PRO && ((aok >> i) & 1u)) v = bn_relu8(v, reinterpret_cast<const float*>(psc), reinterpret_cast<const float*>(psh));
+      *reinterpret_cast<uint4*>(As + swz((tid >> 3) + 32 * i, cc)) = v;
+    }
     if (!BT) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(Bs + swz((tid >> 3) + 32 * i, cc)) = rb[i];
@@ -348,7 +363,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 // ------------------------------------------------------------------------------------------------
 // weight gradient
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, bool PRO>
 __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, int tiles_n, int splits) {
   constexpr int FM = BM / 32, FN = BN / 32;       // fragments per wave
   constexpr int CA = BM / 8, CB = BN / 8;         // 16-byte chunks per staged row
@@ -389,13 +404,17 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   }
   const int cca = tid % CA;
   const bool acol_ok = co0 + cca * 8 < a.dy_c;
-  // x prologue constants of this thread's fixed channel chunk (bci .. bci + 7)
-  const float* pro = a.pro_ss != nullptr ? a.pro_ss + peer * a.pro_ss_ps : nullptr;
+  // PRO: x is a BN output y and the B operand is relu(y*sc + sh); constants of this thread's fixed
+  // channel chunk (bci .. bci + 7), applied at the LDS store (the loads stay in flight across the MFMAs)
   float psc[8], psh[8];
+  unsigned bok = 0;
+  if (PRO) {
+    const float* pro = a.pro_ss + peer * a.pro_ss_ps;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    psc[j] = (pro != nullptr && bcol_ok) ? pro[bci + j] : 1.f;
-    psh[j] = (pro != nullptr && bcol_ok) ? pro[a.x_c + bci + j] : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = bcol_ok ? pro[bci + j] : 1.f;
+      psh[j] = bcol_ok ? pro[a.x_c + bci + j] : 0.f;
+    }
   }
 
   // per-row output coordinates (img, oh, ow) of this thread's B rows, advanced by +64 pixels per
@@ -424,7 +443,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
       const int h = b_oh[i] * a.stride + hb, w = b_ow[i] * a.stride + wb;
       const bool ok = bcol_ok && m < kend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) : make_uint4(0, 0, 0, 0);
-      if (pro != nullptr && ok) rb[i] = bn_relu8(rb[i], psc, psh);
+      if (PRO) bok = ok ? (bok | (1u << i)) : (bok & ~(1u << i));
       b_ow[i] += d_ow;
       if (b_ow[i] >= a.Wo) { b_ow[i] -= a.Wo; ++b_oh[i]; }
       b_oh[i] += d_oh;
@@ -438,7 +457,11 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 #pragma unroll
     for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(As + tr_off<BM>(tid / CA + (256 / CA) * i, cca * 8)) = ra[i];
 #pragma unroll
-    for (int i = 0; i < NBr; ++i) *reinterpret_cast<uint4*>(Bs + tr_off<BN>(tid / CB + (256 / CB) * i, ccb * 8)) = rb[i];
+    for (int i = 0; i < NBr; ++i) {
+      uint4 v = rb[i];
+      if (PRO && ((bok >> i) & 1u)) v = bn_relu8(v, psc, psh);
+      *reinterpret_cast<uint4*>(Bs + tr_off<BN>(tid / CB + (256 / CB) * i, ccb * 8)) = v;
+    }
   };
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -506,16 +529,19 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   const int tiles_n = (a.ncol + (wide ? 127 : 63)) / (wide ? 128 : 64);
   dim3 grid(tiles_m * tiles_n, parity ? 4 : 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
-#define CG_LAUNCH(M_, BN_) hipLaunchKernelGGL((k_conv_gemm<M_, BN_>), grid, block, 0, s, a, tiles_m, tiles_n)
-  if (mode == 0) {
-    if (wide) CG_LAUNCH(0, 128);
-    else CG_LAUNCH(0, 64);
+#define CG_LAUNCH(M_, BN_, P_) hipLaunchKernelGGL((k_conv_gemm<M_, BN_, P_>), grid, block, 0, s, a, tiles_m, tiles_n)
+  if (mode == 0 && a.pro_ss != nullptr) {
+    if (wide) CG_LAUNCH(0, 128, true);
+    else CG_LAUNCH(0, 64, true);
+  } else if (mode == 0) {
+    if (wide) CG_LAUNCH(0, 128, false);
+    else CG_LAUNCH(0, 64, false);
   } else if (parity) {
-    if (wide) CG_LAUNCH(2, 128);
-    else CG_LAUNCH(2, 64);
+    if (wide) CG_LAUNCH(2, 128, false);
+    else CG_LAUNCH(2, 64, false);
   } else {
-    if (wide) CG_LAUNCH(1, 128);
-    else CG_LAUNCH(1, 64);
+    if (wide) CG_LAUNCH(1, 128, false);
+    else CG_LAUNCH(1, 64, false);
   }
 #undef CG_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
@@ -534,9 +560,15 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   const int tiles_m = (a.dy_c + BM - 1) / BM, tiles_n = (ncol + BN - 1) / BN;
   dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
-  if (wm && wn) hipLaunchKernelGGL((k_conv_wgrad<128, 128>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
-  else if (wm) hipLaunchKernelGGL((k_conv_wgrad<128, 64>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
-  else if (wn) hipLaunchKernelGGL((k_conv_wgrad<64, 128>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
-  else hipLaunchKernelGGL((k_conv_wgrad<64, 64>), grid, block, 0, s, a, tiles_m, tiles_n, splits);
+#define WG_LAUNCH(BM_, BN_)                                                                                      \
+  do {                                                                                                           \
+    if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad<BM_, BN_, true>), grid, block, 0, s, a, tiles_m, tiles_n, splits); \
+    else hipLaunchKernelGGL((k_conv_wgrad<BM_, BN_, false>), grid, block, 0, s, a, tiles_m, tiles_n, splits);  \
+  } while (0)
+  if (wm && wn) WG_LAUNCH(128, 128);
+  else if (wm) WG_LAUNCH(128, 64);
+  else if (wn) WG_LAUNCH(64, 128);
+  else WG_LAUNCH(64, 64);
+#undef WG_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -214,9 +214,12 @@ class CNNGroup:
         self.extras: Dict[str, torch.Tensor] = {}
         self.perm_fn = None
         self.eager = False
-        # ResNet blocks: BN1-apply + ReLU folded into conv2's forward / wgrad operand prologues and
-        # its ReLU mask recomputed in the BN backward (MYFYP_CNN_FUSE_BN=0: the materialised a1 path)
-        self.fuse_bn1 = os.environ.get("MYFYP_CNN_FUSE_BN", "1") != "0"
+        # ResNet blocks, opt-in (MYFYP_CNN_FUSE_BN=1): BN1-apply + ReLU folded into conv2's forward /
+        # wgrad operand prologues and its ReLU mask recomputed in the BN backward. Measured a net loss
+        # on MI355X (+14 ms of 441 ms GPU time per profile, profiles/r2j_bn_prologue): the transform
+        # is redone for each of the 9 im2col taps and every N tile, which costs more VALU in the
+        # latency-bound conv loops than the k_bn_act pass it removes. Off by default.
+        self.fuse_bn1 = os.environ.get("MYFYP_CNN_FUSE_BN", "0") == "1"
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
         self._data_version = 0

@@ -345,6 +345,12 @@ class Federation:
             self._hb_thread = threading.Thread(target=beat, name=f"fed-heartbeat-{self.rank}", daemon=True)
             self._hb_thread.start()
 
+    def _stop_heartbeat(self) -> None:
+        self._hb_stop.set()
+        t, self._hb_thread = self._hb_thread, None
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=5.0)
+
     def shutdown(self) -> None:
         """Leave the job, wait until every rank has left (the rendezvous store lives in rank 0's
         process), stop the control bus and tear down the process groups (call once, at exit).
@@ -356,7 +362,7 @@ class Federation:
         if self.shm is not None:
             self.shm.leave()
             synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT))
-            self._hb_stop.set()
+            self._stop_heartbeat()  # joined before the unmap: a beat in flight wrote into freed pages (SIGSEGV at exit)
             self.shm.close()
             self.shm = None
         if self.bus is not None:
@@ -380,7 +386,7 @@ class Federation:
         if inst is not None and inst.bus is not None:
             inst.bus.stop()
         if inst is not None:
-            inst._hb_stop.set()
+            inst._stop_heartbeat()
         if inst is not None and inst.shm is not None:
             inst.shm.close()
             inst.shm = None

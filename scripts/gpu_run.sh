@@ -1,7 +1,7 @@
 #!/bin/bash
 # Parameterised GPU entry point (replaces the one-off gpu_*.sh scripts):
 #   OUT=<dir under gpurun_out> bash scripts/gpu_run.sh <step> [<step> ...]
-# steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), smoke, bench (fp32 headline),
+# steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), cnntests (tests/test_cnn_engine_gpu.py), smoke, bench (fp32 headline),
 #        bench_bf16, bench_cnn, devagg (device SCAFFOLD/FedMedian tests + copy trace),
 #        overlap (side-stream / delayed FedAvg tests, bench, kernel overlap trace), prof, stamps,
 #        pmc (MLP counters), cnn_configs (BASELINE configs 3-5), cnn_prof (ResNet-18 kernel stats) (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
@@ -26,6 +26,7 @@ for step in "$@"; do
   case $step in
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     f32tests) run f32_tests 400 python -u -m pytest tests/test_mlp_f32_gpu.py -v --timeout 120 --timeout-method thread ;;
+    cnntests) run cnn_tests 500 python -u -m pytest tests/test_cnn_engine_gpu.py -v --timeout 150 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench_fp32 300 python bench.py ;;
     bench_bf16) run bench_bf16 300 python bench.py --precision bf16 ;;

@@ -322,27 +322,32 @@ def test_cnn_graph_replay_matches_eager():
 def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     """BN1-apply + ReLU folded into conv2's forward / wgrad prologues, with the ReLU mask recomputed
     from y1 in the BN backward, against the path that materialises a1 (k_bn_act). The prologue
-    rounds relu(y*sc + sh) to bf16 exactly like k_bn_act; the two runs still differ in the order
-    of the BN-statistics and split-K atomics, so one step is compared within that noise."""
+    rounds relu(y*sc + sh) to bf16 exactly like k_bn_act. The runs still differ in the order of
+    the BN-statistics and split-K fp32 atomics; at batch 16 with bf16 activations that order alone
+    moves one step's update by ~20 % (measured: two unfused runs give cos 0.977, rel 0.21 —
+    scripts/probes/cnn_fuse_noise.py). So the fused run is compared against the unfused
+    run-to-run noise floor, and the first step's loss (forward only) must agree tightly."""
     import threading
 
     from myfyp_amd.models import ResNet18
 
     runs = []
-    for fuse in ("1", "0"):
+    for fuse in ("0", "0", "1"):
         monkeypatch.setenv("MYFYP_CNN_FUSE_BN", fuse)
         learners, _, _ = _make_learners(lambda i: ResNet18(seed=70 + i), 2, 16, 16, 16, 0.05, momentum=0.9, wd=5e-4)
-        assert learners[0]._engine.group.fuse_bn1 == (fuse == "1")
+        g = learners[0]._engine.group
+        assert g.fuse_bn1 == (fuse == "1")
         p0 = [lr_.flat_params().detach().clone() for lr_ in learners]
         ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
         [t.start() for t in ths]
         [t.join() for t in ths]
-        ev = [lr_.evaluate() for lr_ in learners]
-        runs.append(([lr_.flat_params().detach().clone() - q for lr_, q in zip(learners, p0)], ev))
-    (d_f, e_f), (d_u, e_u) = runs
-    for a, b in zip(d_f, d_u):
-        cos = F.cosine_similarity(a, b, dim=0)
-        rel = (a - b).norm() / b.norm()
-        assert cos > 0.999 and rel < 0.03, (float(cos), float(rel))
-    for a, b in zip(e_f, e_u):
-        assert abs(a["test_loss"] - b["test_loss"]) < 0.02 * max(1.0, b["test_loss"]), (a, b)
+        loss = float(g.stat.view(g.capacity, 4)[0, 0])
+        runs.append(([lr_.flat_params().detach().clone() - q for lr_, q in zip(learners, p0)], loss))
+    (d_u1, l_u1), (d_u2, l_u2), (d_f, l_f) = runs
+
+    def dist(xs, ys):
+        return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
+
+    for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
+        assert c_f > c_n - 0.03 and r_f < 1.5 * r_n + 0.02, ((c_f, r_f), (c_n, r_n))
+    assert abs(l_f - l_u1) < 1e-2 * max(1.0, abs(l_u1)), (l_f, l_u1, l_u2)
