@@ -38,6 +38,17 @@ struct ConvGemmArgs {
   // per channel ([sc | sh], 2*src_c floats per peer), padding taps stay 0 — the BN-apply + ReLU
   // pass that would materialise it is skipped
   const float* pro_ss; int64_t pro_ss_ps;
+  // dgrad epilogue (optional, MODE 1/2): the output is the gradient dz of a ReLU(BatchNorm) output.
+  // out = g = bf16(acc + resid) * [mask > 0], and the BN-backward column sums (sum g, sum g*xhat)
+  // accumulate into bnb_part0/1 ([sum g | sum g*xhat] per channel, 2*ncol floats per peer) for up to
+  // two BatchNorms whose inputs y0/y1 share that gradient (a block's BN2 and its projection BN);
+  // xhat = (y - mean) * inv from bnb_ms0/1 ([mean | inv], 2*ncol per peer). Replaces the separate
+  // k_bn_bwd_reduce pass over (dz, mask, y).
+  const bf16* bnb_mask; int64_t bnb_mask_ps;
+  const bf16* bnb_y0; int64_t bnb_y0_ps;
+  const bf16* bnb_y1; int64_t bnb_y1_ps;
+  const float* bnb_ms0; const float* bnb_ms1;
+  float* bnb_part0; float* bnb_part1; int64_t bnb_part_ps;
 };
 
 struct WgradArgs {

@@ -25,6 +25,8 @@
 
 #include "conv.h"
 
+struct bf8 { bf16 v[8]; };
+
 #define CG_BK 64
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -305,9 +307,60 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   }
 
   // ---------------------------------------------------------------- epilogue
+  // The accumulator tile goes through LDS (fp32, the 64 KB / 48 KB operand buffers are free now) so
+  // that every thread then owns one 16-byte chunk (8 channels) of a row: bias, residual, mask and y
+  // operands are 16-byte loads and the output a 16-byte store. Straight from the MFMA layout a lane
+  // holds 1 column x 16 rows, i.e. 2-byte accesses (and 3-4x as many VMEM instructions again for
+  // the BN-backward operands).
+  // Staging layout: [BM][BN] fp32, column XOR-swizzled by bits 2-3 of the row — the four row groups
+  // of one MFMA write (rows 4q + e) land in four distinct 16-bank groups.
+  float* cst = reinterpret_cast<float*>(lds);
+  static_assert(BM * BN * 4 <= 2 * BUF * 2, "staging tile must fit the operand buffers");
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wr * 64 + i * 16 + 4 * (lane >> 4) + e;
+        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
+        cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
+      }
+  __syncthreads();
+
+  constexpr int CH = BN / 8, RP = 256 / CH, PASSES = BM / RP;
+  const int ch = tid % CH, rr = tid / CH;
+  const int col0 = n0 + ch * 8;
+  const bool chok = col0 < a.ncol;  // ncol is a multiple of 8
   bf16* out = a.out + peer * a.out_ps;
   const bf16* resid = a.resid ? a.resid + peer * a.resid_ps : nullptr;
-  const float* bias = a.bias ? a.bias + peer * a.bias_ps : nullptr;
+  // BN-backward epilogue (dgrad only)
+  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
+  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
+  const bf16* bmask = (bnb && a.bnb_mask) ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
+  const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
+  const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
+  const bool fstats = !bnb && a.stats != nullptr;
+  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], q0[8], q1[8], q2[8];
+  bool cval[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = col0 + j;
+    cval[j] = col < a.ncol_valid;
+    bv[j] = (a.bias != nullptr && cval[j]) ? a.bias[peer * a.bias_ps + col] : 0.f;
+    mean0[j] = inv0[j] = mean1[j] = inv1[j] = 0.f;
+    if (bnb && chok) {
+      const float* m0p = a.bnb_ms0 + peer * 2 * a.ncol;
+      mean0[j] = m0p[col];
+      inv0[j] = m0p[a.ncol + col];
+      if (bnb2) {
+        const float* m1p = a.bnb_ms1 + peer * 2 * a.ncol;
+        mean1[j] = m1p[col];
+        inv1[j] = m1p[a.ncol + col];
+      }
+    }
+    q0[j] = q1[j] = q2[j] = 0.f;
+  }
   // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
   auto out_row = [&](int m) -> int {
     if (MODE != 2) return m;
@@ -315,46 +368,95 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
     const int hh = rem / rw, ww = rem - hh * rw;
     return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
   };
-  int orow[4][4];
+  if (chok) {
+#pragma unroll 2
+    for (int p = 0; p < PASSES; ++p) {
+      const int row = rr + p * RP;
+      const int m = m0 + row;
+      if (m >= M) break;
+      const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
+      uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
+      if (resid != nullptr) ur = *reinterpret_cast<const uint4*>(resid + o);
+      if (bmask != nullptr) um = *reinterpret_cast<const uint4*>(bmask + o);
+      if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
+      if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
+      const int sw = ((row >> 2) & 3) << 4;
+      const float4 lo = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8) ^ sw));
+      const float4 hi = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8 + 4) ^ sw));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const bf8 br = __builtin_bit_cast(bf8, ur), bm = __builtin_bit_cast(bf8, um);
+      const bf8 b0 = __builtin_bit_cast(bf8, uy0), b1 = __builtin_bit_cast(bf8, uy1);
+      bf8 ob;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) orow[i][e] = out_row(m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + e);
-#pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
-    const bool cok = col < a.ncol;
-    const bool cvalid = col < a.ncol_valid;
-    const float bv = (bias != nullptr && cvalid) ? bias[col] : 0.f;
-    float s = 0.f, ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + e;
-        if (row < M && cok) {
-          const int64_t o = (int64_t)orow[i][e] * a.ncol + col;
-          float v = acc[i][j][e] + bv;
-          if (resid != nullptr) v += (float)resid[o];
-          if (a.relu) v = fmaxf(v, 0.f);
-          if (!cvalid) v = 0.f;
-          out[o] = (bf16)v;
-          s += v;
-          ss += v * v;
+      for (int j = 0; j < 8; ++j) {
+        float x = v[j] + bv[j];
+        if (resid != nullptr) x += (float)br.v[j];
+        if (a.relu) x = fmaxf(x, 0.f);
+        if (!cval[j]) x = 0.f;
+        if (bnb) {
+          if (bmask != nullptr && !((float)bm.v[j] > 0.f)) x = 0.f;
+          ob.v[j] = (bf16)x;
+          const float g = (float)ob.v[j];  // the sums see exactly the g the BN apply reads back
+          q0[j] += g;
+          q1[j] += g * ((float)b0.v[j] - mean0[j]) * inv0[j];
+          if (bnb2) q2[j] += g * ((float)b1.v[j] - mean1[j]) * inv1[j];
+        } else {
+          ob.v[j] = (bf16)x;
+          q0[j] += x;
+          q1[j] += x * x;
         }
       }
+      *reinterpret_cast<uint4*>(out + o) = __builtin_bit_cast(uint4, ob);
     }
-    if (a.stats != nullptr) {
-      // BatchNorm batch statistics: the wave's column sums go straight into the peer's [2][ncol]
-      // accumulator (no partial-row slab, no serial reduction kernel; bn_finalize reads and re-zeroes it)
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-      ss += __shfl_xor(ss, 16);
-      ss += __shfl_xor(ss, 32);
-      if ((lane >> 4) == 0 && cok) {
+  }
+  if (!bnb && !fstats) return;
+  // per-column sums: over the wave's rows (lanes of one chunk) by shuffles, over the 4 waves in LDS,
+  // then one atomic per column and statistic into the peer's accumulator
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int off = CH; off < 64; off <<= 1) {
+      q0[j] += __shfl_xor(q0[j], off);
+      q1[j] += __shfl_xor(q1[j], off);
+      if (bnb2) q2[j] += __shfl_xor(q2[j], off);
+    }
+  }
+  __syncthreads();  // staging tile no longer read
+  float* red = cst;  // [4 waves][3][BN]
+  if (lane < CH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wave * 3 + 0) * BN + ch * 8 + j] = q0[j];
+      red[(wave * 3 + 1) * BN + ch * 8 + j] = q1[j];
+      red[(wave * 3 + 2) * BN + ch * 8 + j] = q2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int col = n0 + tid;
+    if (col < a.ncol) {
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        t0 += red[(w * 3 + 0) * BN + tid];
+        t1 += red[(w * 3 + 1) * BN + tid];
+        t2 += red[(w * 3 + 2) * BN + tid];
+      }
+      if (bnb) {
+        float* p0 = a.bnb_part0 + peer * a.bnb_part_ps;
+        atomicAdd(p0 + col, t0);
+        atomicAdd(p0 + a.ncol + col, t1);
+        if (bnb2) {
+          float* p1 = a.bnb_part1 + peer * a.bnb_part_ps;
+          atomicAdd(p1 + col, t0);
+          atomicAdd(p1 + a.ncol + col, t2);
+        }
+      } else {
+        // BatchNorm batch statistics straight into the peer's [2][ncol] accumulator (bn_finalize
+        // reads and re-zeroes it)
         float* st = a.stats + peer * a.stats_ps;
-        atomicAdd(st + col, s);
-        atomicAdd(st + a.ncol + col, ss);
+        atomicAdd(st + col, t0);
+        atomicAdd(st + a.ncol + col, t1);
       }
     }
   }

@@ -48,6 +48,9 @@ class ConvGemmArgs(ctypes.Structure):
         ("out", c_void_p), ("out_ps", c_int64), ("bias", c_void_p), ("bias_ps", c_int64),
         ("resid", c_void_p), ("resid_ps", c_int64), ("relu", c_int), ("stats", c_void_p), ("stats_ps", c_int64),
         ("nbatch", c_void_p), ("max_batch", c_int), ("pro_ss", c_void_p), ("pro_ss_ps", c_int64),
+        ("bnb_mask", c_void_p), ("bnb_mask_ps", c_int64), ("bnb_y0", c_void_p), ("bnb_y0_ps", c_int64),
+        ("bnb_y1", c_void_p), ("bnb_y1_ps", c_int64), ("bnb_ms0", c_void_p), ("bnb_ms1", c_void_p),
+        ("bnb_part0", c_void_p), ("bnb_part1", c_void_p), ("bnb_part_ps", c_int64),
     ]
 
 
@@ -220,6 +223,10 @@ class CNNGroup:
         # is redone for each of the 9 im2col taps and every N tile, which costs more VALU in the
         # latency-bound conv loops than the k_bn_act pass it removes. Off by default.
         self.fuse_bn1 = os.environ.get("MYFYP_CNN_FUSE_BN", "0") == "1"
+        # ResNet backward: the BN-backward column sums of a ReLU(BN) output are accumulated in the
+        # epilogue of the dgrad that produces its gradient (k_bn_bwd_reduce skipped for those BNs;
+        # MYFYP_CNN_FOLD_BNB=0: the separate reduce pass)
+        self.fold_bnb = os.environ.get("MYFYP_CNN_FOLD_BNB", "1") != "0"
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
         self._data_version = 0
@@ -455,8 +462,11 @@ class CNNGroup:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None,
-             pro: Optional["BNL"] = None) -> None:
-        """``pro``: src holds that BatchNorm's input y; the conv reads relu(BN(y)) in its prologue."""
+             pro: Optional["BNL"] = None, bnb: Optional[tuple] = None) -> None:
+        """``pro``: src holds that BatchNorm's input y; the conv reads relu(BN(y)) in its prologue.
+        ``bnb`` (dgrad): ``(mask, [(bn, y), ...])`` — out is written as the ReLU-masked gradient g and
+        the BN-backward sums of each listed BatchNorm (input y) accumulate in the epilogue; follow
+        with ``bn_bwd(..., pre_reduced=True)``."""
         lib, P = _lib(), self.capacity
         shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
@@ -484,6 +494,18 @@ class CNNGroup:
         if pro is not None:
             ss = self.ss(pro)
             a.pro_ss, a.pro_ss_ps = ss.data_ptr(), ss.shape[1]
+        if bnb is not None:
+            mask, targets = bnb
+            assert mode == 1 and 1 <= len(targets) <= 2 and all(bn.Cp == a.ncol for bn, _ in targets)
+            if mask is not None:
+                a.bnb_mask, a.bnb_mask_ps = mask.data_ptr(), mask.shape[1]
+            (bn0, y0), rest = targets[0], targets[1:]
+            part0 = self.fbuf(f"bnsum_{bn0.name}", 2 * bn0.Cp)
+            a.bnb_y0, a.bnb_y0_ps, a.bnb_ms0, a.bnb_part0, a.bnb_part_ps = y0.data_ptr(), y0.shape[1], self.ms(bn0).data_ptr(), part0.data_ptr(), part0.shape[1]
+            if rest:
+                bn1_, y1_ = rest[0]
+                a.bnb_y1, a.bnb_y1_ps, a.bnb_ms1 = y1_.data_ptr(), y1_.shape[1], self.ms(bn1_).data_ptr()
+                a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", 2 * bn1_.Cp).data_ptr()
         _chk(lib.conv_gemm_launch(mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
@@ -532,16 +554,21 @@ class CNNGroup:
                             y2.shape[1] if y2 is not None else 0, self.ss(bn2).data_ptr() if bn2 is not None else None, int(relu), self.nb.data_ptr(),
                             self.B * hw, hw, bn.Cp, out.data_ptr(), out.shape[1], P, self._stream()), f"bn_act {bn.name}")
 
-    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None, mask_from_y: bool = False) -> None:
-        """``mask_from_y``: the ReLU after this BN was never materialised; its mask is y*sc + sh > 0."""
+    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None, mask_from_y: bool = False, pre_reduced: bool = False) -> None:
+        """``mask_from_y``: the ReLU after this BN was never materialised; its mask is y*sc + sh > 0.
+        ``pre_reduced``: dz is already the masked gradient g and its sums were accumulated by the
+        producing dgrad's epilogue (``conv(..., bnb=...)``): only finalize + apply run."""
         lib, P = _lib(), self.capacity
         mss = self.ss(bn).data_ptr() if mask_from_y else None
         nblk = max(1, min(128, (self.B * hw + 255) // 256))
         part = self.fbuf(f"bnsum_{bn.name}", 2 * bn.Cp)  # atomically accumulated, re-zeroed by the finalize
         coef = self.fbuf(f"bncoef_{bn.name}", 3 * bn.Cp)
-        _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
-                                   self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
-                                   gout.shape[1] if gout is not None else 0, P, self._stream(), mss), f"bn_bwd_reduce {bn.name}")
+        if pre_reduced:
+            assert mask is None and gout is None and not mask_from_y
+        else:
+            _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
+                                       self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
+                                       gout.shape[1] if gout is not None else 0, P, self._stream(), mss), f"bn_bwd_reduce {bn.name}")
         gbase = self.grad.data_ptr()
         _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nblk, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
                                      self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight), gbase + 4 * self._off(bn.module.bias),
@@ -629,6 +656,8 @@ class CNNGroup:
         d = self.act(f"d_out_{len(self.blocks) - 1}", B * hw, last.cp_out)
         _chk(lib.cnn_avgpool(1, dpooled.data_ptr(), dpooled.shape[1], self.nb.data_ptr(), B, self.final_hw, fc.cp_in, d.data_ptr(), d.shape[1],
                              self.capacity, self._stream()), "avgpool_bwd")
+        fold = self.fold_bnb
+        pre = False  # d is already the masked gradient of this block's output, its BN sums accumulated
         for bi in range(len(self.blocks) - 1, -1, -1):
             c1, bn1, c2, bn2, proj = self.blocks[bi]
             hw1 = c1.ho * c1.wo
@@ -638,36 +667,61 @@ class CNNGroup:
             a1 = None if self.fuse_bn1 else self.act(f"a1_{bi}", B * hw1, c1.cp_out)
             dy2 = self.act(f"dy2_{bi}", B * hw1, c2.cp_out)
             d_in = self.act(f"d_out_{bi - 1}" if bi > 0 else "d_stem", B * c1.h * c1.w, c1.cp_in)
+            mask_out = None if pre else a_out
             if proj is not None:
                 cs, bns = proj
                 ys = self.act(f"ys_{bi}", B * hw1, cs.cp_out)
-                self.bn_bwd(bn2, d, a_out, y2, dy2, hw1)
+                self.bn_bwd(bn2, d, mask_out, y2, dy2, hw1, pre_reduced=pre)
                 dys = self.act(f"dys_{bi}", B * hw1, cs.cp_out)
-                self.bn_bwd(bns, d, a_out, ys, dys, hw1)
+                self.bn_bwd(bns, d, mask_out, ys, dys, hw1, pre_reduced=pre)
                 dsc = self.act(f"dsc_{bi}", B * c1.h * c1.w, c1.cp_in)
                 self.conv(cs, dys, dsc, mode=1)
                 self.wgrad(cs, dys, a_in)
                 resid = dsc
+            elif pre:
+                self.bn_bwd(bn2, d, None, y2, dy2, hw1, pre_reduced=True)
+                resid = d  # already the masked gradient g
             else:
                 g = self.act(f"g_{bi}", B * hw1, c2.cp_out)
                 self.bn_bwd(bn2, d, a_out, y2, dy2, hw1, gout=g)
                 resid = g
             da1 = self.act(f"da1_{bi}", B * hw1, c1.cp_out)
-            self.conv(c2, dy2, da1, mode=1)
             dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
             if self.fuse_bn1:
+                self.conv(c2, dy2, da1, mode=1)
                 self.wgrad(c2, dy2, y1, pro=bn1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, mask_from_y=True)
+            elif fold:
+                self.conv(c2, dy2, da1, mode=1, bnb=(a1, [(bn1, y1)]))
+                self.wgrad(c2, dy2, a1)
+                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True)
             else:
+                self.conv(c2, dy2, da1, mode=1)
                 self.wgrad(c2, dy2, a1)
                 self.bn_bwd(bn1, da1, a1, y1, dy1, hw1)
-            self.conv(c1, dy1, d_in, mode=1, resid=resid)
+            bnb = None
+            if fold:  # d_in is the gradient of the previous block's (or the stem's) ReLU(BN) output
+                if bi > 0:
+                    pc1, _, pc2, pbn2, pproj = self.blocks[bi - 1]
+                    phw = pc1.ho * pc1.wo
+                    tg = [(pbn2, self.act(f"y2_{bi - 1}", B * phw, pc2.cp_out))]
+                    if pproj is not None:
+                        tg.append((pproj[1], self.act(f"ys_{bi - 1}", B * phw, pproj[0].cp_out)))
+                    bnb = (a_in, tg)
+                else:
+                    st = self.stem
+                    bnb = (a_in, [(self.stem_bn, self.act("y_stem", B * st.ho * st.wo, st.cp_out))])
+            self.conv(c1, dy1, d_in, mode=1, resid=resid, bnb=bnb)
             self.wgrad(c1, dy1, a_in)
             d = d_in
+            pre = bnb is not None
         L, bn = self.stem, self.stem_bn
         hw = L.ho * L.wo
         dys = self.act("dy_stem", B * hw, L.cp_out)
-        self.bn_bwd(bn, d, self.act("a_stem", B * hw, L.cp_out), self.act("y_stem", B * hw, L.cp_out), dys, hw)
+        if pre:
+            self.bn_bwd(bn, d, None, self.act("y_stem", B * hw, L.cp_out), dys, hw, pre_reduced=True)
+        else:
+            self.bn_bwd(bn, d, self.act("a_stem", B * hw, L.cp_out), self.act("y_stem", B * hw, L.cp_out), dys, hw)
         self.wgrad(L, dys, self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c)))
 
     def _forward_lenet(self, x0: torch.Tensor, train: bool) -> torch.Tensor:

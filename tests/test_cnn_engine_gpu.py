@@ -91,6 +91,55 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
         assert gw[cout:].abs().max().item() == 0 if cpo > cout else True
 
 
+@pytest.mark.parametrize("cin,cout,stride,h,n,two", [(64, 64, 1, 16, 3, False), (64, 128, 2, 16, 2, True), (128, 128, 1, 8, 4, True)])
+def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two):
+    """dgrad with the BN-backward epilogue: out = bf16(dX + resid) * [mask > 0] and per-channel
+    (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op."""
+    from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, _lib
+
+    lib = _lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    k, pad = 3, 1
+    ho = (h + 2 * pad - k) // stride + 1
+    w = _bf(torch.randn(cout, cin, k, k, device=dev) * (1.0 / (cin * k * k) ** 0.5))
+    wf = w.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
+    dy = _bf(torch.randn(n, cout, ho, ho, device=dev))
+    dx_ref = torch.nn.grad.conv2d_input((n, cin, h, h), w, dy, stride=stride, padding=pad)
+    resid = _bf(torch.randn(n, cin, h, h, device=dev))
+    mask = _bf(torch.relu(torch.randn(n, cin, h, h, device=dev)))
+    ys = [_bf(torch.randn(n, cin, h, h, device=dev) * 2 + 0.5) for _ in range(2 if two else 1)]
+    ms = [torch.stack([y.mean((0, 2, 3)), 1.0 / (y.var((0, 2, 3), unbiased=False) + 1e-5).sqrt()]).reshape(1, -1).contiguous() for y in ys]
+    nh = lambda t: _nhwc_pad(t, cin).reshape(1, -1).contiguous()
+    dyn, rn, mn = _nhwc_pad(dy, cout).reshape(1, -1).contiguous(), nh(resid), nh(mask)
+    yn = [nh(y) for y in ys]
+    out = torch.zeros(1, n * h * h * cin, device=dev, dtype=torch.bfloat16)
+    parts = [torch.zeros(1, 2 * cin, device=dev) for _ in ys]
+    b = ConvGemmArgs()
+    b.src, b.src_h, b.src_w, b.src_c = dyn.data_ptr(), ho, ho, cout
+    b.out_h, b.out_w, b.R, b.S, b.stride, b.pad = h, h, k, k, stride, pad
+    b.wt, b.ncol, b.ncol_valid = wf.data_ptr(), cin, cin
+    b.out, b.max_batch = out.data_ptr(), n
+    b.resid = rn.data_ptr()
+    b.bnb_mask, b.bnb_y0, b.bnb_ms0, b.bnb_part0 = mn.data_ptr(), yn[0].data_ptr(), ms[0].data_ptr(), parts[0].data_ptr()
+    if two:
+        b.bnb_y1, b.bnb_ms1, b.bnb_part1 = yn[1].data_ptr(), ms[1].data_ptr(), parts[1].data_ptr()
+    assert lib.conv_gemm_launch(1, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    g_ref = (dx_ref + resid) * (mask > 0)
+    g = out.view(n, h, h, cin).float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(g, g_ref, atol=3e-2, rtol=3e-2)
+    for y, m, part in zip(ys, ms, parts):
+        xhat = (y - m[0, :cin].view(1, -1, 1, 1)) * m[0, cin:].view(1, -1, 1, 1)
+        sg_ref, sgx_ref = g_ref.sum((0, 2, 3)), (g_ref * xhat).sum((0, 2, 3))
+        scale = g_ref.abs().sum((0, 2, 3)).max()
+        assert (part[0, :cin] - sg_ref).abs().max() < 1e-2 * scale, float((part[0, :cin] - sg_ref).abs().max())
+        # the kernel sums the bf16-rounded g it writes, exactly what the BN apply reads back
+        gx = (g * xhat).sum((0, 2, 3))
+        torch.testing.assert_close(part[0, cin:], gx, atol=1e-2 * float(scale), rtol=1e-3)
+        assert (part[0, cin:] - sgx_ref).abs().max() < 2e-2 * scale
+
+
 def _make_learners(model_fn, n_peers, n_train, n_test, batch, lr, momentum=0.0, wd=0.0):
     from myfyp_amd.learning.dataset.synthetic import synthetic_cifar10
     from myfyp_amd.learning.frameworks.torch import TorchModel
