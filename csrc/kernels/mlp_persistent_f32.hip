@@ -63,6 +63,9 @@ using persist::st_wt128;
 using persist::st_wt32;
 
 constexpr int NT = 512;  // threads per workgroup (8 waves)
+#ifndef P32_EXP_FUSE_FWD
+#define P32_EXP_FUSE_FWD 0  // experiment: next step's forward accumulated inside C2 — measured 16.8 us/step vs 15.7 (C2 4.6 -> 6.6 us, 14 more VGPR spills), not kept
+#endif
 constexpr int NCG = 16;  // W1 column groups per peer (D1 / 16)
 constexpr int NH = 8;    // heads per peer (D2 / 16)
 constexpr int KSMAX = 2;
@@ -391,7 +394,9 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (g == 0) P32_STAMP(0, t, 0);
 
     // ================= A: H1 slice = relu(X · W1sliceᵀ + b1), split-K over the 8 waves
-    {
+    // (P32_EXP_FUSE_FWD, t > 0: each wave's partials were accumulated in sRed during the previous
+    // step's C2, right after its K steps' W1 update and the staging of this batch's columns)
+    if (!P32_EXP_FUSE_FWD || t == 0) {
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
@@ -587,6 +592,21 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
                 *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows_next);
             }
           }
+          if (P32_EXP_FUSE_FWD && more) {
+            // next step's forward partial of this K step: its W1 columns are final for step t + 1
+            // and the batch columns were just staged by this wave (LDS is in order within a wave;
+            // the wait + memory clobber keeps the compiler from hoisting the reads above the writes)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            f32x4 accn[MT];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) accn[mt] = q == 0 ? zero4() : sRed[(wave * MT + mt) * 64 + lane];
+            fwd_kstep(q, accn);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = accn[mt];
+          }
+        } else if (P32_EXP_FUSE_FWD && more && q == 0) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = zero4();
         }
       }
     }
