@@ -227,6 +227,9 @@ class CNNGroup:
         # epilogue of the dgrad that produces its gradient (k_bn_bwd_reduce skipped for those BNs;
         # MYFYP_CNN_FOLD_BNB=0: the separate reduce pass)
         self.fold_bnb = os.environ.get("MYFYP_CNN_FOLD_BNB", "1") != "0"
+        # wgrad split-K target: workgroups per CU over all peers (more splits = more parallelism and
+        # more fp32 atomics on the gradient)
+        self.wgrad_tpc = int(os.environ.get("MYFYP_WGRAD_TPC", "2"))  # measured: 2 -> 75.6 ms wgrad, 4 -> 78.4, 8 -> 89.8 (scripts/probes/wgrad_tpc.sh)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
         self._data_version = 0
@@ -513,7 +516,7 @@ class CNNGroup:
         M = self.B * L.ho * L.wo
         ncol = L.R * L.S * L.cp_in
         tiles = ((L.cp_out + 127) // 128) * ((ncol + 127) // 128)
-        want = max(1, (4 * 256) // max(1, tiles * self.capacity))
+        want = max(1, (self.wgrad_tpc * 256) // max(1, tiles * self.capacity))
         k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
         return k_per, (M + k_per - 1) // k_per
 
