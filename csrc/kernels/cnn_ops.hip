@@ -611,33 +611,90 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
   const int co = wk.y;
   const int rsz = sg.R * sg.S, n = sg.cin * rsz, nf = rsz * sg.cp_in, ldg = sg.cp_in + 1;
   const int64_t row = sg.off + (int64_t)co * n;
+  // i / rsz and j / cp_in without integer division (exact: i, j < 2^22)
+  const float inv_rsz = 1.f / (float)rsz, inv_cp = 1.f / (float)sg.cp_in;
+  auto qdiv = [](int x, int d, float inv) {
+    int q = (int)((float)x * inv);
+    q -= (q * d > x) ? 1 : 0;
+    q += ((q + 1) * d <= x) ? 1 : 0;
+    return q;
+  };
+  float* grow = const_cast<float*>(gf) + peer * gf_ps + sg.wf_off + (int64_t)co * nf;
+  bf16* dst = shadow + peer * shadow_ps + sg.wf_off + (int64_t)co * nf;
+  // 16-byte passes when the row's addresses allow it (cp_in is a multiple of 8, so a 4- or
+  // 8-element group never straddles two taps); uniform per block
+  const bool vg = ((reinterpret_cast<uintptr_t>(grow) & 15) == 0);
+  const bool vw = ((reinterpret_cast<uintptr_t>(wp + row) & 15) == 0) && ((reinterpret_cast<uintptr_t>(mp + row) & 15) == 0) && (n & 3) == 0;
+  const bool vs = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
   if (update) {
-    float* grow = const_cast<float*>(gf) + peer * gf_ps + sg.wf_off + (int64_t)co * nf;
-    for (int j = tid; j < nf; j += 256) {
-      const int rs = j / sg.cp_in, ci = j - rs * sg.cp_in;
-      gl[rs * ldg + ci] = grow[j];
-      if (sg.zero_after) grow[j] = 0.f;
+    if (vg) {
+      for (int j = tid * 4; j < nf; j += 1024) {
+        const float4 v = *reinterpret_cast<const float4*>(grow + j);
+        const int rs = qdiv(j, sg.cp_in, inv_cp), ci = j - rs * sg.cp_in;
+        float* d = gl + rs * ldg + ci;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+        if (sg.zero_after) *reinterpret_cast<float4*>(grow + j) = float4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      for (int j = tid; j < nf; j += 256) {
+        const int rs = qdiv(j, sg.cp_in, inv_cp), ci = j - rs * sg.cp_in;
+        gl[rs * ldg + ci] = grow[j];
+        if (sg.zero_after) grow[j] = 0.f;
+      }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 256) {
-      const int ct = i / rsz, rs = i - ct * rsz;
-      const int ce = sg.t2e ? sg.t2e[ct] : ct;
-      const int64_t idx = row + i;
-      float wv = wp[idx], mv = mp[idx];
-      opt_update(o, gl[rs * ldg + ce], wv, mv, vdummy, 1.f, 1.f, ap, cgp, clp, idx);
-      wp[idx] = wv;
-      mp[idx] = mv;
-      wl[i] = wv;
+    if (vw) {
+      for (int i0 = tid * 4; i0 < n; i0 += 1024) {
+        float4 w4 = *reinterpret_cast<const float4*>(wp + row + i0), m4 = *reinterpret_cast<const float4*>(mp + row + i0);
+        float wv[4] = {w4.x, w4.y, w4.z, w4.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = i0 + e;
+          const int ct = qdiv(i, rsz, inv_rsz), rs = i - ct * rsz;
+          const int ce = sg.t2e ? sg.t2e[ct] : ct;
+          opt_update(o, gl[rs * ldg + ce], wv[e], mv[e], vdummy, 1.f, 1.f, ap, cgp, clp, row + i);
+          wl[i] = wv[e];
+        }
+        *reinterpret_cast<float4*>(wp + row + i0) = float4{wv[0], wv[1], wv[2], wv[3]};
+        *reinterpret_cast<float4*>(mp + row + i0) = float4{mv[0], mv[1], mv[2], mv[3]};
+      }
+    } else {
+      for (int i = tid; i < n; i += 256) {
+        const int ct = qdiv(i, rsz, inv_rsz), rs = i - ct * rsz;
+        const int ce = sg.t2e ? sg.t2e[ct] : ct;
+        const int64_t idx = row + i;
+        float wv = wp[idx], mv = mp[idx];
+        opt_update(o, gl[rs * ldg + ce], wv, mv, vdummy, 1.f, 1.f, ap, cgp, clp, idx);
+        wp[idx] = wv;
+        mp[idx] = mv;
+        wl[i] = wv;
+      }
     }
   } else {
     for (int i = tid; i < n; i += 256) wl[i] = wp[row + i];
   }
   __syncthreads();
-  bf16* dst = shadow + peer * shadow_ps + sg.wf_off + (int64_t)co * nf;
-  for (int j = tid; j < nf; j += 256) {
-    const int rs = j / sg.cp_in, ci = j - rs * sg.cp_in;
-    const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
-    dst[j] = (bf16)(tc >= 0 ? wl[tc * rsz + rs] : 0.f);
+  if (vs) {
+    for (int j = tid * 8; j < nf; j += 2048) {
+      const int rs = qdiv(j, sg.cp_in, inv_cp), ci0 = j - rs * sg.cp_in;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ci = ci0 + e;
+        const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
+        v[e] = tc >= 0 ? wl[tc * rsz + rs] : 0.f;
+      }
+      *reinterpret_cast<uint4*>(dst + j) = pack8(v);
+    }
+  } else {
+    for (int j = tid; j < nf; j += 256) {
+      const int rs = qdiv(j, sg.cp_in, inv_cp), ci = j - rs * sg.cp_in;
+      const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
+      dst[j] = (bf16)(tc >= 0 ? wl[tc * rsz + rs] : 0.f);
+    }
   }
 }
 
