@@ -577,8 +577,8 @@ struct Segment {
   const int* t2e;       // torch input column -> engine input channel, or null
 };
 
-#define SHADOW_MAX_ROW 4608  // cin * R * S floats of one output channel (512 * 3 * 3)
-#define GRAD_MAX_ROW (4608 + 16)
+#define SHADOW_MAX_ROW (4608 + 64)  // cin * R * S floats of one output channel (512 * 3 * 3) + cin / 8 pad
+#define GRAD_MAX_ROW (9 * (512 + 4))     // R * S rows of cp_in + 4 floats
 
 __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbuf, int64_t ps, const float* gf, int64_t gf_ps,
                                                   const Segment* segs, const int2* work, OptParams o, const float* anchor, const float* cg,
@@ -609,7 +609,12 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
   __shared__ float gl[GRAD_MAX_ROW];
   __shared__ float wl[SHADOW_MAX_ROW];
   const int co = wk.y;
-  const int rsz = sg.R * sg.S, n = sg.cin * rsz, nf = rsz * sg.cp_in, ldg = sg.cp_in + 1;
+  // LDS layouts (bank conflicts modelled per access pattern; the former +1 row pad gave 8-9-way
+  // conflicts on the column reads): gradient rows padded to cp_in + 4 (16-byte aligned, column reads
+  // <= 2-way), the torch-order master row padded by one float per 8 input channels (the shadow
+  // pass's 8-channel-per-lane reads become conflict-free)
+  const int rsz = sg.R * sg.S, n = sg.cin * rsz, nf = rsz * sg.cp_in, ldg = sg.cp_in + 4;
+  auto wli = [&](int ct, int rs) { return ct * rsz + rs + (ct >> 3); };
   const int64_t row = sg.off + (int64_t)co * n;
   // i / rsz and j / cp_in without integer division (exact: i, j < 2^22)
   const float inv_rsz = 1.f / (float)rsz, inv_cp = 1.f / (float)sg.cp_in;
@@ -631,11 +636,7 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
       for (int j = tid * 4; j < nf; j += 1024) {
         const float4 v = *reinterpret_cast<const float4*>(grow + j);
         const int rs = qdiv(j, sg.cp_in, inv_cp), ci = j - rs * sg.cp_in;
-        float* d = gl + rs * ldg + ci;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
+        *reinterpret_cast<float4*>(gl + rs * ldg + ci) = v;
         if (sg.zero_after) *reinterpret_cast<float4*>(grow + j) = float4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
@@ -656,7 +657,7 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
           const int ct = qdiv(i, rsz, inv_rsz), rs = i - ct * rsz;
           const int ce = sg.t2e ? sg.t2e[ct] : ct;
           opt_update(o, gl[rs * ldg + ce], wv[e], mv[e], vdummy, 1.f, 1.f, ap, cgp, clp, row + i);
-          wl[i] = wv[e];
+          wl[wli(ct, rs)] = wv[e];
         }
         *reinterpret_cast<float4*>(wp + row + i0) = float4{wv[0], wv[1], wv[2], wv[3]};
         *reinterpret_cast<float4*>(mp + row + i0) = float4{mv[0], mv[1], mv[2], mv[3]};
@@ -670,11 +671,14 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
         opt_update(o, gl[rs * ldg + ce], wv, mv, vdummy, 1.f, 1.f, ap, cgp, clp, idx);
         wp[idx] = wv;
         mp[idx] = mv;
-        wl[i] = wv;
+        wl[wli(ct, rs)] = wv;
       }
     }
   } else {
-    for (int i = tid; i < n; i += 256) wl[i] = wp[row + i];
+    for (int i = tid; i < n; i += 256) {
+      const int ct = qdiv(i, rsz, inv_rsz);
+      wl[wli(ct, i - ct * rsz)] = wp[row + i];
+    }
   }
   __syncthreads();
   if (vs) {
@@ -685,7 +689,7 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
       for (int e = 0; e < 8; ++e) {
         const int ci = ci0 + e;
         const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
-        v[e] = tc >= 0 ? wl[tc * rsz + rs] : 0.f;
+        v[e] = tc >= 0 ? wl[wli(tc, rs)] : 0.f;
       }
       *reinterpret_cast<uint4*>(dst + j) = pack8(v);
     }
@@ -693,7 +697,7 @@ __global__ __launch_bounds__(256) void k_opt_step(float* w, float* g, float* mbu
     for (int j = tid; j < nf; j += 256) {
       const int rs = qdiv(j, sg.cp_in, inv_cp), ci = j - rs * sg.cp_in;
       const int tc = sg.e2t ? sg.e2t[ci] : (ci < sg.cin ? ci : -1);
-      dst[j] = (bf16)(tc >= 0 ? wl[tc * rsz + rs] : 0.f);
+      dst[j] = (bf16)(tc >= 0 ? wl[wli(tc, rs)] : 0.f);
     }
   }
 }

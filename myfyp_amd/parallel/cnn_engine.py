@@ -367,7 +367,8 @@ class CNNGroup:
                 self._keep_colmaps += [te, tt]
                 e2t, t2e = te.data_ptr(), tt.data_ptr()
             cin_t = getattr(c, "cin_torch", c.cin)
-            if cin_t * c.R * c.S > 4608 or (c.cp_in + 1) * c.R * c.S > 4624:
+            # LDS rows of k_opt_step (cnn_ops.hip SHADOW_MAX_ROW / GRAD_MAX_ROW)
+            if cin_t * c.R * c.S + cin_t // 8 > 4608 + 64 or (c.cp_in + 4) * c.R * c.S > 9 * (512 + 4):
                 raise ValueError(f"conv layer {c.name} too wide for the optimizer kernel (cin * R * S > 4608)")
             accumulate = int(self._wgrad_split(c)[1] > 1)
             if getattr(self, "lenet_fused", False) and c.name in ("c1", "c2"):

@@ -4,7 +4,7 @@
 # steps: tests (pytest -m gpu), f32tests (tests/test_mlp_f32_gpu.py), cnntests (tests/test_cnn_engine_gpu.py), smoke, bench (fp32 headline),
 #        bench_bf16, bench_cnn, devagg (device SCAFFOLD/FedMedian tests + copy trace),
 #        overlap (side-stream / delayed FedAvg tests, bench, kernel overlap trace), prof, stamps,
-#        pmc (MLP counters), cnn_configs (BASELINE configs 3-5), cnn_prof (ResNet-18 kernel stats) (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
+#        pmc (MLP counters), cnn_configs (BASELINE configs 3-5), cnn_prof (ResNet-18 kernel stats), cnn_pmc (ResNet-18 counters) (rocprofv3 kernel stats of a short fp32 bench), rehearsal (2/4
 #        gloo ranks on one GPU). Every GPU step runs under its own time limit; the script stops at
 #        the first failure, and at once after a timeout, abort or segfault.
 set -o pipefail
@@ -53,6 +53,11 @@ for step in "$@"; do
       run lenet_ring 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 4
       run resnet_fedavg 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       run resnet_fedprox_drop 400 python benchmarks/bench_cnn.py --model resnet18 --aggregator fedprox --dirichlet 0.5 --dropout --rounds 3 ;;
+    cnn_pmc)  # counters of the ResNet-18 conv / BN / optimizer kernels, one pass per counter group
+      run cnn_pmc_a 300 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+        --kernel-include-regex "k_conv|k_bn|k_opt" --output-format csv -d "$O/cnn_pmc_a" -o a -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 0 --n-train 2048 --n-test 512
+      run cnn_pmc_b 300 timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU \
+        --kernel-include-regex "k_conv|k_bn|k_opt" --output-format csv -d "$O/cnn_pmc_b" -o b -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 0 --n-train 2048 --n-test 512 ;;
     cnn_prof)  # kernel statistics of the ResNet-18 grouped step
       run cnn_prof 400 rocprofv3 --kernel-trace --stats -d "$O/cnn_prof" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 1 \
         --n-train 16384 --n-test 2048 ;;
