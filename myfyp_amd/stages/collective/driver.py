@@ -3,7 +3,8 @@
 With the fused MLP engine a whole federated round costs the GPU ~2 ms, while eight co-located peer
 threads crossing two gang barriers per round spend comparable time just handing the GIL and the
 barrier locks to each other. When every co-located peer is a fused-engine learner of one group
-(no training callbacks, no workflow hooks) and the aggregator is sample-weighted averaging, the
+(no training callbacks, no workflow hooks) and the aggregator is sample-weighted averaging or
+topology neighbour mixing (``fused_round.eligible``), the
 peer threads therefore hand the remaining rounds to ONE driver thread (the last to arrive) and
 sleep until their experiment ends. The driver executes, per round and for all local peers, exactly
 what the collective stages would — Train/WaitAggregatedModels (one fused round: evaluation of every
@@ -34,8 +35,6 @@ from myfyp_amd.stages.collective import fused_round
 def eligible(f, aggregator) -> bool:
     """Decided by the vote leader (so every co-located peer takes the same path)."""
     if not Settings.ROUND_DRIVER or not fused_round.eligible(f, aggregator):
-        return False
-    if getattr(aggregator, "all_peers_train", False):
         return False
     for a in f.local_order:
         node = f.local_nodes.get(a)
@@ -142,7 +141,8 @@ class RoundDriver:
                 fits = group._run_fit_batch({slot[a]: reqs[a] for a in trainers})
                 out = {a: (evs.get(slot[a]), fits[slot[a]]) for a in trainers}
             total = next(iter(states.values())).total_rounds
-            weights_plane.aggregate_mean(f, {a: (n.get(a, 0), None) for a in cur}, final=total is None or round_ + 1 >= total)
+            aggregator = next(iter(cur.values())).kw["aggregator"]
+            fused_round.aggregate(f, {a: (n.get(a, 0), None) for a in cur}, aggregator, final=total is None or round_ + 1 >= total)
             for hook in list(f.round_hooks):
                 hook(round_, f)
             for a, m in cur.items():
@@ -185,7 +185,11 @@ class RoundDriver:
                 st = m.kw["state"]
                 logger.round_started(a, st.experiment)
                 votes[a] = make_votes(a, f.all_peers(), st.round)
-            train_set = tally_votes(weights_plane.gather_votes(f, votes))
+            allv = weights_plane.gather_votes(f, votes)
+            if getattr(aggregator, "all_peers_train", False):  # NeighborAvg: every live peer trains
+                train_set = sorted(allv, key=lambda a: f.all_peers().index(a))
+            else:
+                train_set = tally_votes(allv)
             for a, m in cur.items():
                 m.kw["state"].train_set = list(train_set)
 

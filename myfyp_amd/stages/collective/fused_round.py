@@ -3,9 +3,9 @@
 The collective workflow normally crosses three barriers per round after the vote (evaluation gang,
 fit gang, aggregation gang), each waking every co-located peer thread. When the vote leader finds
 that every local peer is a fused-engine learner of one group without training callbacks and the
-aggregator is sample-weighted averaging, the train / wait stages instead join ONE gang whose leader
-enqueues, in stream order, the evaluation of every trainer, the grouped local epoch(s) and the
-FedAvg collective. Each peer thread then only files its own results (metrics are logged when the
+aggregator is sample-weighted averaging or topology neighbour mixing, the train / wait stages instead
+join ONE gang whose leader enqueues, in stream order, the evaluation of every trainer, the grouped
+local epoch(s) and the weight collective (FedAvg, or the NeighborAvg mix). Each peer thread then only files its own results (metrics are logged when the
 device results land). Observable behaviour — stage history, metrics, contributions, the FedAvg
 result — is that of the three-gang path (``train_stage.py`` / ``wait_agg_models_stage.py``;
 reference ``stages/base_node/train_stage.py:44-100``).
@@ -32,7 +32,7 @@ def fit_result(fit):
 
 def eligible(f, aggregator) -> bool:
     """Decided once per round by the vote leader, so every co-located peer takes the same path."""
-    if not Settings.FUSED_ROUND or getattr(aggregator, "collective_kind", None) != "mean":
+    if not Settings.FUSED_ROUND or getattr(aggregator, "collective_kind", None) not in ("mean", "neighbor"):
         return False
     groups = set()
     for a in f.local_order:
@@ -45,6 +45,15 @@ def eligible(f, aggregator) -> bool:
             return False
         groups.add(id(eng.group))
     return len(groups) == 1
+
+
+def aggregate(f, arrived, aggregator, final: bool) -> None:
+    """The round's weight collective for an eligible aggregator: FedAvg (sample-weighted mean) or
+    topology neighbour mixing (``NeighborAvg``)."""
+    if getattr(aggregator, "collective_kind", None) == "neighbor":
+        weights_plane.aggregate_neighbors(f, arrived, aggregator)
+    else:
+        weights_plane.aggregate_mean(f, arrived, final=final)
 
 
 def join(state, learner, aggregator, trainer: bool) -> None:
@@ -68,7 +77,7 @@ def join(state, learner, aggregator, trainer: bool) -> None:
             fits = group._run_fit_batch({slot[a]: arrived[a][2] for a in trainers})
             for a in trainers:
                 out[a] = (evs.get(slot[a]), fits[slot[a]])
-        weights_plane.aggregate_mean(f, {a: (arrived[a][1], None) for a in addrs}, final=final)
+        aggregate(f, {a: (arrived[a][1], None) for a in addrs}, aggregator, final)
         for hook in list(f.round_hooks):
             hook(round_, f)
         return out

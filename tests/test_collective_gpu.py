@@ -77,3 +77,66 @@ def test_collective_fused_engine_modes(mode):
         Federation.reset()
         MLPGroup.reset_all()
         Settings.FUSED_ROUND, Settings.ROUND_DRIVER, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW = saved
+
+
+def test_neighbor_avg_fused_engine_modes_agree():
+    """NeighborAvg (ring) on the fused engine through the lock-step round driver, the fused round
+    and the threaded stages: same stage histories (everyone trains every round), learning, and the
+    same per-peer models — the topology mix replaces FedAvg in the one-gang-op round."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import numpy as np
+
+    from myfyp_amd.learning.aggregators import NeighborAvg
+    from myfyp_amd.utils.seed import set_seed
+
+    saved = (Settings.FUSED_ROUND, Settings.ROUND_DRIVER, Settings.BATCH_SIZE, Settings.GANG_WINDOW)
+    n, rounds = 4, 3
+    finals = {}
+    try:
+        for mode in ("driver", "fused_round", "threaded"):
+            Settings.FUSED_ROUND = mode != "threaded"
+            Settings.ROUND_DRIVER = mode == "driver"
+            Settings.BATCH_SIZE = 64
+            Settings.GANG_WINDOW = 5.0
+            set_seed(13)
+            MLPGroup.reset_all()
+            Federation.reset()
+            fed = Federation.init()
+            parts = synthetic_mnist(8000, 800, seed=5).generate_partitions(n, RandomIIDPartitionStrategy)
+            exp = f"nb-{mode}-{time.time_ns()}"
+            nodes = [
+                Node(TorchModel(MLP(seed=i)), parts[i], address=f"nb-{mode}-{i}", aggregator=NeighborAvg("ring"), protocol=CollectiveCommunicationProtocol,
+                     exp_name=exp)
+                for i in range(n)
+            ]
+            try:
+                for nd in nodes:
+                    nd.start()
+                assert all(nd.learner._engine is not None for nd in nodes)
+                fed.finalize()
+                nodes[0].set_start_learning(rounds=rounds, epochs=1)
+                wait_to_finish(nodes, timeout=120)
+                for nd in nodes:
+                    _history_ok(nd.learning_workflow.history, rounds)
+                    assert nd.learning_workflow.history.count("TrainStage") == rounds
+                logs = logger.get_global_logs()[exp]
+                assert min(dict(logs[nd.addr]["test_metric"])[rounds] for nd in nodes) > 0.8
+                timings = [logger.get_timings().get(nd.addr, {}) for nd in nodes]
+                assert any("driver_round" in t for t in timings) == (mode == "driver")
+                assert any("fused_round" in t for t in timings) == (mode == "fused_round")
+                finals[mode] = {nd.addr.split("-")[-1]: np.concatenate([a.ravel() for a in nd.learner.get_model().get_parameters()]) for nd in nodes}
+            finally:
+                for nd in nodes:
+                    nd.stop()
+                Federation.reset()
+                MLPGroup.reset_all()
+    finally:
+        Settings.FUSED_ROUND, Settings.ROUND_DRIVER, Settings.BATCH_SIZE, Settings.GANG_WINDOW = saved
+    ref = finals["threaded"]
+    for mode in ("driver", "fused_round"):
+        for k, v in finals[mode].items():
+            np.testing.assert_allclose(v, ref[k], atol=1e-4, rtol=1e-4, err_msg=f"{mode} peer {k}")
+    # peers are not averaged to one model (decentralised mixing), but their spread is bounded
+    spread = max(np.abs(ref[k] - ref["0"]).max() for k in ref)
+    assert 0.0 < spread < 1.0
