@@ -50,7 +50,7 @@ for step in "$@"; do
       run pmc_b 300 timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum \
         --kernel-include-regex "mlp_" --output-format csv -d "$O/pmc_b" -o b -- python3 bench.py --steps 2 --warmup 1 ;;
     cnn_configs)  # BASELINE configs 3, 4, 5
-      run lenet_ring 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 4
+      run lenet_ring 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 20
       run resnet_fedavg 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       run resnet_fedprox_drop 400 python benchmarks/bench_cnn.py --model resnet18 --aggregator fedprox --dirichlet 0.5 --dropout --rounds 3 ;;
     cnn_pmc)  # counters of the ResNet-18 conv / BN / optimizer kernels, one pass per counter group
