@@ -186,6 +186,9 @@ def main() -> None:
               f"p90 {np.percentile(d, 90):.3f} max {d.max():.3f}", file=sys.stderr, flush=True)
     print(f"[bench] rank {rank} median ms per call: {json.dumps(brk)} fed: "
           f"{ {k: round(1000 * float(np.median(v)), 3) for k, v in fed.stats.items()} }", file=sys.stderr, flush=True)
+    eng = getattr(nodes[0].learner, "_engine", None)
+    if eng is not None and hasattr(eng.group, "graph_launch_stats"):
+        print(f"[bench] rank {rank} epoch graph launches: {eng.group.graph_launch_stats()}", file=sys.stderr, flush=True)
     for n in nodes:
         n.stop()
 

@@ -36,6 +36,7 @@ struct MLPPersistF32Bufs {
 };
 
 bool mlp_persistent_f32_supported(const MLPArgs& a);
+size_t mlp_persistent_f32_h1x_floats(int P, int Bpad);  // H1-partial exchange region at the start of the buffer
 size_t mlp_persistent_f32_bytes(int P, int Bpad);
 size_t mlp_persistent_f32_flag_bytes(int P);
 int mlp_persistent_f32_gang();

@@ -163,6 +163,14 @@ __device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, flo
   }
 }
 
+// H1 partial of K part kh at step t: [P][KSMAX][2][BP][PD1], double-buffered by step parity. An
+// owner reads the other K part's partial of step t at the start of its C phase, while that part may
+// already publish step t + 1's; it cannot reach step t + 2 before every owner has published t + 1
+// (the heads' dH2(t + 1) waits for all of them), so two buffers suffice.
+__device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, int kh, int t, int BP) {
+  return pb.h1x + (((int64_t)p * KSMAX + kh) * 2 + (t & 1)) * BP * PD1;
+}
+
 __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
   const int r = n - t * a.B;
   return r < 0 ? 0 : (r > a.B ? a.B : r);
@@ -420,7 +428,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         // b1 came in through the bias column; KS > 1: a partial sum (relu after the kh-ordered sum)
         const float v = b < rows ? (KS == 1 ? fmaxf(s[i], 0.f) : s[i]) : 0.f;
         sH1c[b * 16 + cc] = v;
-        st_wt32(pb.h1x + (((int64_t)p * KS + kh) * BP + b) * PD1 + NCG * cg + cc, v);
+        st_wt32(h1x_part(pb, p, kh, t, BP) + (int64_t)b * PD1 + NCG * cg + cc, v);
       }
     }
     if (g == 0) P32_STAMP(0, t, 1);
@@ -461,7 +469,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
           if (k2 == kh) {
             v = *reinterpret_cast<const float4*>(sH1c + b * 16 + c4);
           } else {
-            const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + ((int64_t)p * KS + k2) * BP * PD1, BP * PD1 * 4);
+            const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 4);
             v = ld_sc1_16(r, (b * PD1 + NCG * cg + c4) * 4);
           }
           sum.x += v.x;
@@ -770,7 +778,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       float4 u[KS][BP / 8];
 #pragma unroll
       for (int k2 = 0; k2 < KS; ++k2) {
-        const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.h1x + ((int64_t)p * KS + k2) * BP * PD1, BP * PD1 * 4);
+        const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 4);
 #pragma unroll
         for (int k = 0; k < BP / 8; ++k) u[k2][k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 256 fp32 = BP*64 chunks
       }
@@ -1250,8 +1258,9 @@ bool mlp_persistent_f32_supported(const MLPArgs& a) {
   return persistent_f32_lds_ks(a, 1) <= 160 * 1024;
 }
 
+size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX * 2 * Bpad * PD1; }
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
-  return (size_t)P * ((size_t)KSMAX * Bpad * PD1 + (size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * sizeof(float);
+  return (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2)) * sizeof(float);
 }
 size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
 int mlp_persistent_f32_gang() { return roles_of(1); }

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -132,7 +133,15 @@ struct MLPEngine {
   MLPArgs a{};
   int max_steps = 0;
   hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  // Two executables of the same epoch graph, launched alternately, so a launch never reuses the
+  // launch state of an execution still on the GPU. Measured (profiles/r3_host_timeline): with one or
+  // two, hipGraphLaunch holds the host 4-8 us and the round rate is the same within noise (485-491
+  // rounds/s): the host already runs rounds ahead (it waits on the result ring, not on the GPU).
+  // Kept for the launch-time counters below; MYFYP_GRAPH_EXECS=1 selects one.
+  hipGraphExec_t execs[2] = {nullptr, nullptr};
+  hipGraphExec_t exec = nullptr;  // execs[0]: non-null once captured
+  int n_execs = 2;
+  unsigned long long launches = 0, launch_ns = 0, launch_max_ns = 0;
   int graph_steps = -1;
   hipStream_t cap_stream = nullptr;
   // engine-owned device buffers
@@ -233,7 +242,8 @@ struct MLPEngine {
     if (params_snap) hipFree(params_snap);
     if (shadow_snap) hipFree(shadow_snap);
     if (w2t_snap) hipFree(w2t_snap);
-    if (exec) hipGraphExecDestroy(exec);
+    for (auto& x : execs)
+      if (x) hipGraphExecDestroy(x);
     if (graph) hipGraphDestroy(graph);
     if (cap_stream) hipStreamDestroy(cap_stream);
     for (void* p : owned) hipFree(p);
@@ -317,7 +327,10 @@ struct MLPEngine {
   }
 
   void invalidate() {
-    if (exec) hipGraphExecDestroy(exec);
+    for (auto& x : execs) {
+      if (x) hipGraphExecDestroy(x);
+      x = nullptr;
+    }
     if (graph) hipGraphDestroy(graph);
     exec = nullptr;
     graph = nullptr;
@@ -328,6 +341,17 @@ struct MLPEngine {
     CHECK_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
     CHECK_HIP(hipMemset(*p, 0, bytes < 16 ? 16 : bytes));
     owned.push_back(*p);
+    return 0;
+  }
+
+  int launch_graph(hipStream_t s) {
+    hipGraphExec_t x = execs[n_execs > 1 ? (int)(launches & 1) : 0];
+    const auto t0 = std::chrono::steady_clock::now();
+    CHECK_HIP(hipGraphLaunch(x, s));
+    const unsigned long long ns = (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    ++launches;
+    launch_ns += ns;
+    if (ns > launch_max_ns) launch_max_ns = ns;
     return 0;
   }
 
@@ -358,7 +382,12 @@ struct MLPEngine {
       graph = nullptr;
       return 1;
     }
-    CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    {
+      const char* env = getenv("MYFYP_GRAPH_EXECS");
+      n_execs = (env != nullptr && atoi(env) == 1) ? 1 : 2;
+    }
+    for (int i = 0; i < n_execs; ++i) CHECK_HIP(hipGraphInstantiate(&execs[i], graph, nullptr, nullptr, 0));
+    exec = execs[0];
     graph_steps = steps;
     return 0;
   }
@@ -620,7 +649,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
       // fp32 exchange buffers + flags (err word shared)
       rc |= e->alloc(&p, mlp_persistent_f32_bytes(P, a.Bpad));
       e->pb32.h1x = (float*)p;
-      e->pb32.plx = e->pb32.h1x + (size_t)2 * P * a.Bpad * 256;  // H1 partials of up to 2 K parts
+      e->pb32.plx = e->pb32.h1x + mlp_persistent_f32_h1x_floats(P, a.Bpad);  // H1 partials: [P][KSMAX][parity]
       e->pb32.dh2x = e->pb32.plx + (size_t)P * 8 * a.Bpad * 16;
       e->pb32.flag_bytes = mlp_persistent_f32_flag_bytes(P);
       rc |= e->alloc(&p, e->pb32.flag_bytes);
@@ -837,14 +866,24 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
     GangOrder& go = gang_order();
     std::lock_guard<std::mutex> og(go.mu);
     if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
-    CHECK_HIP(hipGraphLaunch(e->exec, s));
+    if (e->launch_graph(s)) return 1;
     if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
     CHECK_HIP(hipEventRecord(go.ev, s));
     go.ev_ready = true;
   } else {
-    CHECK_HIP(hipGraphLaunch(e->exec, s));
+    if (e->launch_graph(s)) return 1;
   }
   return 0;
+}
+
+// Host time spent inside hipGraphLaunch: out[0] launches, out[1] total ns, out[2] max ns.
+int mlp_engine_graph_launch_stats(void* h, unsigned long long* out) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  out[0] = e->launches;
+  out[1] = e->launch_ns;
+  out[2] = e->launch_max_ns;
+  return e->n_execs;
 }
 
 // Same epoch without the graph (debug / profiling A-B).

@@ -391,6 +391,16 @@ class MLPGroup:
             self._ensure_engine()
             return int(_native.load(required=True).mlp_engine_f32_ks(self._engine))
 
+    def graph_launch_stats(self) -> dict:
+        """Host time inside hipGraphLaunch (launches, mean / max us) and the number of alternating
+        epoch-graph executables."""
+        if not self._engine:
+            return {}
+        out = np.zeros(3, dtype=np.uint64)
+        n = int(_native.load(required=True).mlp_engine_graph_launch_stats(self._engine, out.ctypes.data))
+        k = max(1, int(out[0]))
+        return {"execs": n, "launches": int(out[0]), "mean_us": round(float(out[1]) / k / 1e3, 2), "max_us": round(float(out[2]) / 1e3, 2)}
+
     def recoveries(self) -> int:
         """Give-ups of the persistent fp32 epoch that the in-stream retry launch recovered."""
         return int(_native.load(required=True).mlp_engine_recoveries(self._engine)) if self._engine else 0

@@ -30,7 +30,18 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench_fp32 300 python bench.py ;;
     bench_bf16) run bench_bf16 300 python bench.py --precision bf16 ;;
+    execab)  # A/B: one epoch-graph executable vs two launched alternately
+      MYFYP_GRAPH_EXECS=1 run execab_1a 300 python bench.py
+      run execab_2a 300 python bench.py
+      MYFYP_GRAPH_EXECS=1 run execab_1b 300 python bench.py
+      run execab_2b 300 python bench.py ;;
+    onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
+      run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
+      run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;
     bench_cnn) run bench_cnn 600 python benchmarks/bench_cnn.py ;;
+    apitrace)  # HIP API + kernel + copy trace of a short fp32 bench: GPU idle gaps and host-blocking calls
+      run apitrace 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d "$O/api" -o run -- python3 bench.py --steps 40 --warmup 5
+      python3 scripts/tools/api_blocking.py "$O"/api > "$O/api_blocking.txt" 2>&1; cat "$O/api_blocking.txt" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python bench.py --steps 40 --warmup 5 ;;
     devagg)
       run devagg_tests 300 python -u -m pytest tests/test_device_aggregators.py tests/test_kernels_gpu.py -k "device_plane or median" -v -m gpu --timeout 120 --timeout-method thread

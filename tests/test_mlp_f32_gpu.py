@@ -176,11 +176,21 @@ def test_f32_optimizers_match_torch(dev, spec):
                 assert rel < 1e-3, f"{spec} peer {i} {name}: relative update error {rel:.2e}"
 
 
+@pytest.mark.parametrize("ks", [1, 2])
 @pytest.mark.parametrize("kind", ["fedprox", "scaffold"])
-def test_f32_fedprox_scaffold_terms_match_torch(dev, kind):
-    """FedProx mu·(w − anchor) and SCAFFOLD (c − c_i) gradient terms in the fp32 epoch kernel."""
-    spec = {"name": "adam", "lr": 1e-3} if kind == "fedprox" else {"name": "sgd", "lr": 1e-4}
+def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, ks):
+    """FedProx mu·(w − anchor) and SCAFFOLD (c − c_i) gradient terms in the fp32 epoch kernel, at
+    both owner K splits.
+
+    The terms are checked under SGD (+ momentum for FedProx). Under Adam this setup is chaotic: the
+    prox term drives most W1 coordinates onto their anchor within the epoch, where Adam's normalised
+    step turns rounding-level differences into ±lr flips — torch fp32 itself, restarted from weights
+    one ulp away, moves by 1.5e-2 relative (scripts/probes/f32_ks_fedprox.py). The Adam update the
+    terms feed is the same register code and is pinned by test_f32_epoch_matches_torch_adam."""
+    spec = {"name": "sgd", "lr": 1e-3, "momentum": 0.9} if kind == "fedprox" else {"name": "sgd", "lr": 1e-4}
     learners, refs, g, n = _setup(dev, 2, 64, 900, 5, spec, scale=0.5)
+    g.force_f32_ks = ks
+    assert g.f32_ks() == ks
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     gen = torch.Generator(device="cpu").manual_seed(9)
