@@ -51,6 +51,8 @@ struct CtlUpload {
   int* zero_correct;
   int* zero_err;
   int* zero_conf;
+  unsigned* zero_flags;  // the persistent epoch's hand-off flags (prep-stream gather mode)
+  int n_flags;
 };
 __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long long* seed) {
   const int p = threadIdx.x;
@@ -64,6 +66,8 @@ __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long 
     for (int q = p; q < u.P * 256; q += blockDim.x) u.zero_conf[q] = 0;
   if (u.zero_err)
     for (int q = p; q < MLP_ERR_WORDS; q += blockDim.x) u.zero_err[q] = 0;
+  if (u.zero_flags)
+    for (int q = p; q < u.n_flags; q += blockDim.x) u.zero_flags[q] = 0u;
   if (p == 0) *seed = u.seed;
 }
 
@@ -133,6 +137,23 @@ struct MLPEngine {
   MLPArgs a{};
   int max_steps = 0;
   hipGraph_t graph = nullptr;
+  hipGraph_t graph_alt = nullptr;  // prep mode: the second executable's graph (other batch buffers)
+  // Prep-stream gather (persistent path with the in-kernel shuffle): the epoch's batch gather runs on
+  // its own stream into one of two batch buffers while the previous round's epoch still runs on the
+  // main stream (the gangs leave CUs free), so it is off the round's critical path. Executable i
+  // reads buffer i; the gather into buffer i waits only for the last epoch that read it.
+  // Opt-in (MYFYP_PREP_GATHER=1): measured round-rate neutral on the fp32 headline (488.2 / 500.7
+  // vs 498.0 / 501.7 rounds/s in-graph, profiles/r3_host_timeline) — the 28 us gather overlapped with
+  // the epoch costs the epoch about as much as it saves. Bit-identical to the in-graph gather (test).
+  bool prep_mode = false;
+  bf16* xb16_buf[2] = {nullptr, nullptr};
+  int* yb_buf[2] = {nullptr, nullptr};
+  hipStream_t prep_stream = nullptr;
+  hipEvent_t ev_gath[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  bool done_rec[2] = {false, false};
+  int4* d_ctl_prep = nullptr;
+  int* d_active_prep = nullptr;
+  unsigned long long* d_seed_prep = nullptr;
   // Two executables of the same epoch graph, launched alternately, so a launch never reuses the
   // launch state of an execution still on the GPU. Measured (profiles/r3_host_timeline): with one or
   // two, hipGraphLaunch holds the host 4-8 us and the round rate is the same within noise (485-491
@@ -233,6 +254,16 @@ struct MLPEngine {
   }
 
   ~MLPEngine() {
+    if (prep_stream) {
+      hipStreamSynchronize(prep_stream);
+      hipStreamDestroy(prep_stream);
+    }
+    for (int i = 0; i < 2; ++i) {
+      if (ev_gath[i]) hipEventDestroy(ev_gath[i]);
+      if (ev_done[i]) hipEventDestroy(ev_done[i]);
+    }
+    if (xb16_buf[1]) hipFree(xb16_buf[1]);
+    if (yb_buf[1]) hipFree(yb_buf[1]);
     if (eval_stream) {
       hipStreamSynchronize(eval_stream);
       hipStreamDestroy(eval_stream);
@@ -245,6 +276,7 @@ struct MLPEngine {
     for (auto& x : execs)
       if (x) hipGraphExecDestroy(x);
     if (graph) hipGraphDestroy(graph);
+    if (graph_alt) hipGraphDestroy(graph_alt);
     if (cap_stream) hipStreamDestroy(cap_stream);
     for (void* p : owned) hipFree(p);
     if (a.Xb) hipFree(a.Xb);
@@ -272,8 +304,18 @@ struct MLPEngine {
     return 0;
   }
 
-  int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false) {
+  void flag_words(unsigned** ptr, int* n) const {
+    if (precision == 1) {
+      *ptr = pb32.flags;
+      *n = a.P * mlp_persistent_f32_flags_per_peer();
+    } else {
+      *ptr = pb.flags;
+      *n = (int)(pb.flag_bytes / sizeof(unsigned));
+    }
+  }
+  int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false, bool zero_flags = false) {
     CtlUpload u{};
+    if (zero_flags) flag_words(&u.zero_flags, &u.n_flags);
     u.P = a.P;
     u.with_active = active_host != nullptr;
     u.seed = seed_host;
@@ -287,8 +329,28 @@ struct MLPEngine {
       u.zero_correct = d_correct;
       u.zero_err = pb.err;
     }
-    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(MLP_CTL_MAX), 0, s, u, d_ctl, d_active, d_seed);
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, s, u, d_ctl, d_active, d_seed);
     CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+  // Prep mode: the gather into batch buffer i on the prep stream, after the last epoch that read it;
+  // it gets its own copy of the control words and the shuffle key (nothing on the main stream).
+  int prep_gather(int i) {
+    if (done_rec[i]) CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_done[i], 0));
+    CtlUpload u{};
+    u.P = a.P;
+    u.seed = seed_host;
+    for (int p = 0; p < a.P; ++p) u.ctl[p] = ctl_host[p];
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, prep_stream, u, d_ctl_prep, d_active_prep, d_seed_prep);
+    MLPArgs ga = a;
+    ga.ctl = d_ctl_prep;
+    ga.seed = d_seed_prep;
+    ga.Xb16 = xb16_buf[i];
+    ga.Yb = yb_buf[i];
+    ga.flags_zero = nullptr;
+    mlp_launch_gather_epoch(ga, prep_stream);
+    CHECK_HIP(hipGetLastError());
+    CHECK_HIP(hipEventRecord(ev_gath[i], prep_stream));
     return 0;
   }
 
@@ -332,6 +394,8 @@ struct MLPEngine {
       x = nullptr;
     }
     if (graph) hipGraphDestroy(graph);
+    if (graph_alt) hipGraphDestroy(graph_alt);
+    graph_alt = nullptr;
     exec = nullptr;
     graph = nullptr;
     graph_steps = -1;
@@ -355,38 +419,77 @@ struct MLPEngine {
     return 0;
   }
 
-  int capture(int steps) {
-    invalidate();
-    if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+  // One epoch graph: [gather (unless prep mode), epoch kernel + retry launch] or the step chain;
+  // buf selects the batch buffers the epoch reads in prep mode.
+  int capture_one(int steps, int buf, hipGraph_t* out) {
+    const MLPArgs saved = a;
+    if (prep_mode) {
+      a.Xb16 = xb16_buf[buf];
+      a.Yb = yb_buf[buf];
+    }
     CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
-    graph_persistent = use_persistent();
-    {
+    if (!prep_mode) {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
       if (graph_persistent) set_flag_zeroing(ga);  // ... which also zeroes the hand-off flags (no memset node)
       mlp_launch_gather_epoch(ga, cap_stream);
     }
+    int rc = 0;
     if (graph_persistent) {
-      if (launch_epoch_kernel(cap_stream, false)) {
-        hipGraph_t g = nullptr;
-        hipStreamEndCapture(cap_stream, &g);
-        if (g) hipGraphDestroy(g);
-        return 1;
-      }
+      rc = launch_epoch_kernel(cap_stream, false);
     } else {
       for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
     }
-    hipError_t e = hipStreamEndCapture(cap_stream, &graph);
-    if (e != hipSuccess) {
-      g_last_error = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
-      graph = nullptr;
+    a = saved;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(cap_stream, &g);
+    if (rc || e != hipSuccess) {
+      if (g) hipGraphDestroy(g);
+      if (!rc) g_last_error = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
       return 1;
     }
-    {
-      const char* env = getenv("MYFYP_GRAPH_EXECS");
-      n_execs = (env != nullptr && atoi(env) == 1) ? 1 : 2;
+    *out = g;
+    return 0;
+  }
+
+  int ensure_prep() {
+    if (!prep_stream) {
+      CHECK_HIP(hipStreamCreateWithFlags(&prep_stream, hipStreamNonBlocking));
+      for (int i = 0; i < 2; ++i) {
+        CHECK_HIP(hipEventCreateWithFlags(&ev_gath[i], hipEventDisableTiming));
+        CHECK_HIP(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
+      }
+      void* p;
+      if (alloc(&p, (size_t)a.P * 16)) return 1;
+      d_ctl_prep = (int4*)p;
+      if (alloc(&p, (size_t)a.P * 4)) return 1;
+      d_active_prep = (int*)p;
+      if (alloc(&p, 8)) return 1;
+      d_seed_prep = (unsigned long long*)p;
     }
-    for (int i = 0; i < n_execs; ++i) CHECK_HIP(hipGraphInstantiate(&execs[i], graph, nullptr, nullptr, 0));
+    return 0;
+  }
+
+  int capture(int steps) {
+    invalidate();
+    if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    graph_persistent = use_persistent();
+    {
+      const char* env = getenv("MYFYP_PREP_GATHER");
+      prep_mode = graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && env != nullptr && atoi(env) == 1;
+      if (prep_mode && ensure_prep()) return 1;
+      if (prep_mode) {
+        // the batch buffers were (re)allocated or the graph changed: nothing in flight reads them
+        done_rec[0] = done_rec[1] = false;
+        xb16_buf[0] = a.Xb16;
+        yb_buf[0] = a.Yb;
+      }
+      const char* e2 = getenv("MYFYP_GRAPH_EXECS");
+      n_execs = (!prep_mode && e2 != nullptr && atoi(e2) == 1) ? 1 : 2;
+    }
+    if (capture_one(steps, 0, &graph)) return 1;
+    if (prep_mode && capture_one(steps, 1, &graph_alt)) return 1;
+    for (int i = 0; i < n_execs; ++i) CHECK_HIP(hipGraphInstantiate(&execs[i], (prep_mode && i == 1) ? graph_alt : graph, nullptr, nullptr, 0));
     exec = execs[0];
     graph_steps = steps;
     return 0;
@@ -695,9 +798,18 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
     CHECK_HIP(hipMalloc((void**)&e->a.Yb, (size_t)e->a.P * rows * sizeof(int)));
     CHECK_HIP(hipMemset(e->a.Xb, 0, (size_t)e->a.P * rows * e->a.D0));
     CHECK_HIP(hipMemset(e->a.Yb, 0, (size_t)e->a.P * rows * sizeof(int)));
+    if (e->xb16_buf[1]) hipFree(e->xb16_buf[1]);
+    if (e->yb_buf[1]) hipFree(e->yb_buf[1]);
+    e->xb16_buf[0] = e->xb16_buf[1] = nullptr;
+    e->yb_buf[0] = e->yb_buf[1] = nullptr;
     if (e->pb.h1x != nullptr) {
       CHECK_HIP(hipMalloc((void**)&e->a.Xb16, (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
       CHECK_HIP(hipMemset(e->a.Xb16, 0, (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
+      // second batch buffers for the prep-stream gather (288 GB of HBM: ~95 MB each is nothing)
+      CHECK_HIP(hipMalloc((void**)&e->xb16_buf[1], (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
+      CHECK_HIP(hipMemset(e->xb16_buf[1], 0, (size_t)e->a.P * rows * e->a.D0 * sizeof(bf16)));
+      CHECK_HIP(hipMalloc((void**)&e->yb_buf[1], (size_t)e->a.P * rows * sizeof(int)));
+      CHECK_HIP(hipMemset(e->yb_buf[1], 0, (size_t)e->a.P * rows * sizeof(int)));
     }
     e->a.xb_rows = rows;
   }
@@ -860,13 +972,22 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   }
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
   const bool pa = e->graph_persistent && e->pending_zero_acc;
-  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh)) return 1;
+  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh, e->prep_mode)) return 1;
   if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
+  const int buf = e->n_execs > 1 ? (int)(e->launches & 1) : 0;  // the executable launch_graph takes
+  if (e->prep_mode) {
+    if (e->prep_gather(buf)) return 1;
+    CHECK_HIP(hipStreamWaitEvent(s, e->ev_gath[buf], 0));
+  }
   if (e->graph_persistent) {
     GangOrder& go = gang_order();
     std::lock_guard<std::mutex> og(go.mu);
     if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
     if (e->launch_graph(s)) return 1;
+    if (e->prep_mode) {
+      CHECK_HIP(hipEventRecord(e->ev_done[buf], s));
+      e->done_rec[buf] = true;
+    }
     if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
     CHECK_HIP(hipEventRecord(go.ev, s));
     go.ev_ready = true;

@@ -35,6 +35,11 @@ for step in "$@"; do
       run execab_2a 300 python bench.py
       MYFYP_GRAPH_EXECS=1 run execab_1b 300 python bench.py
       run execab_2b 300 python bench.py ;;
+    prepab)  # A/B: epoch gather in the graph vs on the prep stream (overlapping the previous epoch)
+      MYFYP_PREP_GATHER=0 run prepab_0a 300 python bench.py
+      MYFYP_PREP_GATHER=1 run prepab_1a 300 python bench.py
+      MYFYP_PREP_GATHER=0 run prepab_0b 300 python bench.py
+      MYFYP_PREP_GATHER=1 run prepab_1b 300 python bench.py ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

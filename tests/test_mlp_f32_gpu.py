@@ -294,3 +294,25 @@ def test_f32_giveup_recovered_by_retry_launch(dev):
     assert rec_ok == 0 and rec_rec == 1, (rec_ok, rec_rec)
     for a, b in zip(p_ok, p_rec):
         assert torch.equal(a, b)
+
+
+def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch):
+    """The epoch batch gather on its own stream into alternating batch buffers (overlapping the
+    previous epoch) gives bit-identical training to the gather as the first node of the epoch
+    graph: three epochs (both buffers used, one reused) with the in-kernel shuffle of fixed keys."""
+    import random
+
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+
+    spec = {"name": "adam", "lr": 1e-3}
+    results = []
+    for prep in ("1", "0"):
+        monkeypatch.setenv("MYFYP_PREP_GATHER", prep)
+        MLPGroup.reset_all()
+        learners, refs, g, n = _setup(dev, 3, 64, 1500, 7, spec)
+        random.seed(4321)
+        for _ in range(3):
+            _fit_all(learners)
+        results.append([l.flat_params().detach().clone() for l in learners])
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
