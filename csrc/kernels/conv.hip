@@ -60,6 +60,21 @@ __device__ __forceinline__ uint4 bn_relu8(uint4 u, const float* sc, const float*
   return r;
 }
 
+// Operand gathers as raw buffer loads (CONV_BUFLOAD, default on): a 32-bit byte offset against a
+// per-peer resource, and an out-of-range offset for padding / masked chunks, which the buffer unit
+// returns as zeros — no 64-bit address arithmetic and no 4-way select per 16-byte chunk.
+#ifndef CONV_BUFLOAD
+#define CONV_BUFLOAD 1
+#endif
+typedef unsigned conv_u32x4 __attribute__((ext_vector_type(4)));
+constexpr int CONV_OOB = (int)0x80000000u;  // >= num_records: the load returns zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t conv_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ uint4 conv_ld16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(uint4, (conv_u32x4)__builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
 // [k][W] images read with ds_read_b64_tr_b16 (W = 64 or 128 bf16, unpadded rows): 8-byte granules
@@ -123,6 +138,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
+  const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(src), rs_wt = conv_rsrc(wt);
+  (void)rs_src;
+  (void)rs_wt;
   // PRO (MODE 0): the source is a BN output y; the A operand is relu(y*sc + sh) of the previous
   // BatchNorm, applied when the staged registers go to LDS (after this K-step's MFMAs, so the
   // loads stay in flight across them; transforming at load time put a vmcnt(0) before the MFMAs)
@@ -211,7 +229,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
         ok = ok && th >= 0 && tw >= 0 && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)a.src_w;
         pix = a_img[i] + h * a.src_w + w;
       }
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
+      if (CONV_BUFLOAD)
+        ra[i] = conv_ld16(rs_src, ok ? (pix * a.src_c + c8 * 8) * 2 : CONV_OOB);
+      else
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
       if (PRO) aok = ok ? (aok | (1u << i)) : (aok & ~(1u << i));
     }
     if (PRO) {
@@ -230,7 +251,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int n = n0 + (tid >> 3) + 32 * i;
-        rb[i] = (k < Ktot && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
+        if (CONV_BUFLOAD)
+          rb[i] = conv_ld16(rs_wt, (k < Ktot && n < a.ncol) ? (n * Ktot + k) * 2 : CONV_OOB);
+        else
+          rb[i] = (k < Ktot && n < a.ncol) ? *reinterpret_cast<const uint4*>(wt + (int64_t)n * Ktot + k) : make_uint4(0, 0, 0, 0);
       }
     } else {
       // k row = (tap, co): Wf[co][r][s][n0 + 8 * chunk ..] (ncol = Wf row length = cp_in)
@@ -243,7 +267,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
           const int ti = tS == 1 ? b_t[i] : b_t[i] / tS, tj = b_t[i] - ti * tS;
           rs = (r0 + 2 * ti) * a.S + s0 + 2 * tj;
         }
-        rb[i] = ok ? *reinterpret_cast<const uint4*>(wt + (b_co[i] * RS + rs) * a.ncol + n) : make_uint4(0, 0, 0, 0);
+        if (CONV_BUFLOAD)
+          rb[i] = conv_ld16(rs_wt, ok ? ((b_co[i] * RS + rs) * a.ncol + n) * 2 : CONV_OOB);
+        else
+          rb[i] = ok ? *reinterpret_cast<const uint4*>(wt + (b_co[i] * RS + rs) * a.ncol + n) : make_uint4(0, 0, 0, 0);
         b_co[i] += CG_BK;
         while (b_co[i] >= a.src_c) {
           b_co[i] -= a.src_c;
