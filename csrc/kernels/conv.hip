@@ -517,6 +517,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
   const int wr = wave >> 1, wc = wave & 1;
   const bf16* dy = a.dy + peer * a.dy_ps;
   const bf16* x = a.x + peer * a.x_ps;
+  const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(dy), rs_x = conv_rsrc(x);
+  (void)rs_dy;
+  (void)rs_x;
   const int hwo = a.Ho * a.Wo;
   const int ncol_tot = a.R * a.S * a.x_c;
 
@@ -564,14 +567,20 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = m_base + tid / CA + (256 / CA) * i;
-      ra[i] = (acol_ok && m < kend) ? *reinterpret_cast<const uint4*>(dy + (int64_t)m * a.dy_c + co0 + cca * 8) : make_uint4(0, 0, 0, 0);
+      if (CONV_BUFLOAD)
+        ra[i] = conv_ld16(rs_dy, (acol_ok && m < kend) ? (m * a.dy_c + co0 + cca * 8) * 2 : CONV_OOB);
+      else
+        ra[i] = (acol_ok && m < kend) ? *reinterpret_cast<const uint4*>(dy + (int64_t)m * a.dy_c + co0 + cca * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < NBr; ++i) {
       const int m = m_base + tid / CB + (256 / CB) * i;
       const int h = b_oh[i] * a.stride + hb, w = b_ow[i] * a.stride + wb;
       const bool ok = bcol_ok && m < kend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) : make_uint4(0, 0, 0, 0);
+      if (CONV_BUFLOAD)
+        rb[i] = conv_ld16(rs_x, ok ? (((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) * 2 : CONV_OOB);
+      else
+        rb[i] = ok ? *reinterpret_cast<const uint4*>(x + ((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) : make_uint4(0, 0, 0, 0);
       if (PRO) bok = ok ? (bok | (1u << i)) : (bok & ~(1u << i));
       b_ow[i] += d_ow;
       if (b_ow[i] >= a.Wo) { b_ow[i] -= a.Wo; ++b_oh[i]; }

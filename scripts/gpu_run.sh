@@ -44,7 +44,8 @@ for step in "$@"; do
       run conv_ab_buf 200 python scripts/probes/conv_ab.py
       MYFYP_NATIVE_LIB=build/base_CONV_BUFLOAD0/libmyfyp_hip.so run conv_ab_base 200 python scripts/probes/conv_ab.py
       run resnet_buf 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
-      MYFYP_NATIVE_LIB=build/base_CONV_BUFLOAD0/libmyfyp_hip.so run resnet_base 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
+      MYFYP_NATIVE_LIB=build/base_CONV_BUFLOAD0/libmyfyp_hip.so run resnet_base 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      run resnet_buf2 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;
