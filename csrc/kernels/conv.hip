@@ -105,7 +105,7 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, in
 
 template <int MODE, int BN, bool PRO>
 __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
-  // MODE 0 forward, MODE 1 dgrad (all taps), MODE 2 strided dgrad by output parity class
+  // MODE 0 forward, MODE 1 dgrad (all taps; MODE 3 = MODE 1 at stride 1), MODE 2 strided dgrad by output parity class
   // (blockIdx.y = class (ph, pw): rows are the dX pixels (2hh+ph, 2ww+pw), K walks only the taps
   // r = r0 + 2i, s = s0 + 2j that reach them — a plain stride-2 dgrad multiplies zeros for 3 of
   // every 4 (pixel, tap) pairs)
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
     if (MODE == 0) {
       a_bh[i] = oh * a.stride - a.pad;
       a_bw[i] = ow * a.stride - a.pad;
-    } else if (MODE == 1) {
+    } else if (MODE == 1 || MODE == 3) {
       a_bh[i] = oh + a.pad;
       a_bw[i] = ow + a.pad;
     } else {  // dY row of tap (r0, s0) for dX pixel (2oh+ph, 2ow+pw); tap i steps back one dY row
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
       } else {
         const int th = a_bh[i] - r, tw = a_bw[i] - s;
         int h, w;
-        if (a.stride == 1) {
+        if (MODE == 3 || a.stride == 1) {
           h = th;
           w = tw;
         } else {
@@ -677,6 +677,9 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   } else if (parity) {
     if (wide) CG_LAUNCH(2, 128, false);
     else CG_LAUNCH(2, 64, false);
+  } else if (a.stride == 1) {  // MODE 3: MODE 1 specialised to stride 1 (no divisibility test, no division)
+    if (wide) CG_LAUNCH(3, 128, false);
+    else CG_LAUNCH(3, 64, false);
   } else {
     if (wide) CG_LAUNCH(1, 128, false);
     else CG_LAUNCH(1, 64, false);
