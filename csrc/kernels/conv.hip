@@ -660,6 +660,10 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, void* stream) {
   const ConvGemmArgs& a = *pa;
   if ((a.src_c & 7) || (a.ncol & 7) || peers < 1 || mode < 0 || mode > 1) return 1;
+  // the buffer-load gathers form 32-bit byte offsets within one peer's source and weights
+  if (CONV_BUFLOAD && ((int64_t)a.max_batch * a.src_h * a.src_w * a.src_c * 2 >= INT32_MAX ||
+                       (int64_t)a.ncol * a.R * a.S * a.src_c * 2 >= INT32_MAX))
+    return 3;
   const bool wide = a.ncol > 64;
   const bool parity = mode == 1 && a.stride == 2;  // strided dgrad: one launch row per parity class
   const int rows = parity ? ((a.out_h + 1) >> 1) * ((a.out_w + 1) >> 1) : a.out_h * a.out_w;
@@ -695,6 +699,9 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   const WgradArgs& a = *pa;
   if ((a.x_c & 7) || (a.dy_c & 7) || (a.k_per_split & 63) || peers < 1 || splits < 1) return 1;
   if (splits > 1 && !a.accumulate) return 1;  // split-K partial sums must be added
+  if (CONV_BUFLOAD && ((int64_t)a.max_batch * a.H * a.W * a.x_c * 2 >= INT32_MAX ||
+                       (int64_t)a.max_batch * a.Ho * a.Wo * a.dy_c * 2 >= INT32_MAX))
+    return 3;  // 32-bit byte offsets of the buffer-load gathers
   const int ncol = a.R * a.S * a.x_c;
   const bool wm = a.dy_c > 64, wn = ncol > 64;
   const int BM = wm ? 128 : 64, BN = wn ? 128 : 64;
