@@ -185,6 +185,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   int a_pix[AR];  // MODE 0: pixel index of tap (0, 0)
 #pragma unroll
   for (int i = 0; i < AR; ++i) a_pix[i] = a_img[i] + a_bh[i] * a.src_w + a_bw[i];
+  // element offset of each row's tap-(0, 0) pixel: a K step adds (MODE 0) or subtracts (MODE 2 / 3)
+  // one per-thread tap offset, so the rows need no multiply in the K loop
+  int a_pixc[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) a_pixc[i] = a_pix[i] * a.src_c;
   constexpr int BCH = BN / 8;          // BT: 16-byte chunks per staged k row
   const int bt_c = tid % BCH, bt_r = tid / BCH;
   int b_t[NB], b_co[NB];
@@ -197,6 +202,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
     }
   }
   const int RS = a.R * a.S, TT = tR * tS;
+  const float inv_tS = 1.f / (float)(tS > 0 ? tS : 1);  // MODE 2: tap index -> (ti, tj) without an integer division
   uint4 ra[AR], rb[NB];
   float4 psc[2], psh[2];  // PRO: scale / shift of the staged chunk's 8 channels
   unsigned aok = 0;       // PRO: staged A rows that are real pixels (padding stays 0, not relu(sh))
@@ -204,17 +210,21 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
     const int k = kt * CG_BK + cc * 8;
     const bool kok = ar < tR;
     const int r = ar, s = as_, c8 = ac8;
+    const int tapc = (r * a.src_w + s) * a.src_c;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       bool ok = kok && a_ok[i];
       int pix;
+      int eoff = 0;  // element offset for the strength-reduced modes (0, 2, 3)
       if (MODE == 0) {
         ok = ok && (unsigned)(a_bh[i] + r) < (unsigned)a.src_h && (unsigned)(a_bw[i] + s) < (unsigned)a.src_w;
         pix = a_pix[i] + r * a.src_w + s;
+        eoff = a_pixc[i] + tapc + c8 * 8;
       } else if (MODE == 2) {
         const int h = a_bh[i] - r, w = a_bw[i] - s;
         ok = ok && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)a.src_w;
         pix = a_img[i] + h * a.src_w + w;
+        eoff = a_pixc[i] - tapc + c8 * 8;
       } else {
         const int th = a_bh[i] - r, tw = a_bw[i] - s;
         int h, w;
@@ -228,9 +238,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
         }
         ok = ok && th >= 0 && tw >= 0 && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)a.src_w;
         pix = a_img[i] + h * a.src_w + w;
+        eoff = MODE == 3 ? a_pixc[i] - tapc + c8 * 8 : pix * a.src_c + c8 * 8;
       }
       if (CONV_BUFLOAD)
-        ra[i] = conv_ld16(rs_src, ok ? (pix * a.src_c + c8 * 8) * 2 : CONV_OOB);
+        ra[i] = conv_ld16(rs_src, ok ? eoff * 2 : CONV_OOB);
       else
         ra[i] = ok ? *reinterpret_cast<const uint4*>(src + pix * a.src_c + c8 * 8) : make_uint4(0, 0, 0, 0);
       if (PRO) aok = ok ? (aok | (1u << i)) : (aok & ~(1u << i));
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
         const bool ok = b_t[i] < TT && n < a.ncol;
         int rs = b_t[i];
         if (MODE == 2) {
-          const int ti = tS == 1 ? b_t[i] : b_t[i] / tS, tj = b_t[i] - ti * tS;
+          const int ti = tS == 1 ? b_t[i] : fdiv(b_t[i], tS, inv_tS), tj = b_t[i] - ti * tS;
           rs = (r0 + 2 * ti) * a.S + s0 + 2 * tj;
         }
         if (CONV_BUFLOAD)
