@@ -58,6 +58,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--noise", type=float, default=1.0, help="synthetic stroke noise (difficulty)")
     ap.add_argument("--no-fused", action="store_true", help="autograd path instead of the fused HIP engine")
     ap.add_argument("--eager", action="store_true", help="fused kernels without hipGraph (A/B)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="one GPU: run FedAvg through a world-size-1 RCCL group (the multi-rank path: side-stream reduce -> RCCL all-reduce -> apply)")
+    ap.add_argument("--no-failover", action="store_true", help="skip the per-round confirmation of the weight collectives (fault tolerance off)")
     return ap.parse_args()
 
 
@@ -91,6 +94,8 @@ def main() -> None:
     Settings.USE_FUSED_KERNELS = not args.no_fused
     Settings.GANG_WINDOW = 5.0
     Settings.MLP_PRECISION = args.precision
+    Settings.FORCE_COLLECTIVE = bool(args.force_collective)
+    Settings.COLLECTIVE_FAILOVER = not args.no_failover
 
     fed = Federation.init()
     world, rank = fed.world, fed.rank
@@ -193,6 +198,12 @@ def main() -> None:
         n.stop()
 
     rps = args.steps / elapsed if elapsed == elapsed and elapsed > 0 else 0.0
+    coll = "none (one rank: local weighted-mean kernel)"
+    if fed.collective:
+        import torch.distributed as dist
+
+        be = dist.get_backend(fed.group)
+        coll = ("rccl" if be == "nccl" else be) + (" world-1 (forced)" if fed.forced else "") + (", failover" if fed._guarded() else "")
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -219,6 +230,7 @@ def main() -> None:
                 "epochs_per_round": args.epochs,
                 "optimizer": "adam lr=1e-3 (fresh per round)",
                 "aggregator": "FedAvg (weighted all-reduce)",
+                "collective": coll,
                 "engine": "fused-hip" + ("-eager" if args.eager else "-hipgraph") if fused else "autograd",
             },
             "time_to_target_s": None if t_target is None else round(t_target, 3),

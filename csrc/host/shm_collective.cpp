@@ -31,9 +31,11 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
@@ -59,6 +61,7 @@ struct alignas(128) RankCtl {
   std::atomic<uint64_t> status;   // last published generation, or kGone | first generation not joined
   uint64_t len[2];                // payload length per parity slot (kOverflow = too large)
   std::atomic<uint64_t> beat_ns;  // heartbeat, CLOCK_MONOTONIC ns (0 = no heartbeat thread)
+  std::atomic<int32_t> pid;       // the rank's process (single host): a vanished pid is a crash
 };
 static_assert(sizeof(RankCtl) == 128, "rank ctl layout");
 
@@ -97,6 +100,33 @@ uint64_t now_ns() {
 int joined(uint64_t s, uint64_t gen) {
   if (s & kGone) return (s & ~kGone) > gen ? 1 : 0;
   return s >= gen ? 1 : -1;
+}
+
+// The rank's process no longer exists (killed / crashed): no need to wait for its heartbeat to go
+// stale. All ranks of a job share the host (and the pid namespace) by construction of the segment.
+bool process_gone(const RankCtl* c) {
+  const int32_t pid = c->pid.load(std::memory_order_acquire);
+  if (pid <= 0) return false;
+  if (kill(pid, 0) != 0) return errno == ESRCH;
+  // exited but not yet reaped by its launcher (torchrun polls its workers): a zombie
+  char path[64], buf[256];
+  snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');
+  return rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X');
+}
+
+// r is still a member but unresponsive: its process is gone, or its heartbeat is older than fail_ns
+bool unresponsive(const RankCtl* c, uint64_t fail_ns) {
+  if (process_gone(c)) return true;
+  if (!fail_ns) return false;
+  const uint64_t beat = c->beat_ns.load(std::memory_order_acquire);
+  return beat && now_ns() - beat > fail_ns;
 }
 
 inline void cpu_relax() {
@@ -179,6 +209,7 @@ void* shmc_open(const char* name, int rank, int world, uint64_t slot_bytes, int 
       return nullptr;
     }
   }
+  h->ctl(rank)->pid.store(static_cast<int32_t>(getpid()), std::memory_order_release);
   hd->attached.fetch_add(1, std::memory_order_acq_rel);
   return h;
 }
@@ -225,9 +256,9 @@ int shmc_allgather_m(void* handle, const void* in, uint64_t n, void* out, uint64
           uint64_t s = c->status.load(std::memory_order_acquire);
           j = joined(s, gen);
           if (j >= 0) return true;
-          if (fail_ns) {  // evict a rank whose heartbeat went stale (a crashed process)
+          if (fail_ns) {  // evict a crashed rank: process gone, or heartbeat stale
             const uint64_t beat = c->beat_ns.load(std::memory_order_acquire);
-            const bool stale = beat ? now_ns() - beat > fail_ns : now_s() - t0 > fail_s;
+            const bool stale = process_gone(c) || (beat ? now_ns() - beat > fail_ns : now_s() - t0 > fail_s);
             if (stale && c->status.compare_exchange_strong(s, kGone | gen, std::memory_order_acq_rel, std::memory_order_acquire)) {
               j = 0;
               return true;
@@ -299,11 +330,39 @@ uint64_t shmc_alive(void* handle) {
   return mask;
 }
 
-// Wait until every rank left (job end: keeps the rendezvous host alive until the last rank is
-// done). 0 ok, -1 timeout.
-int shmc_wait_all_gone(void* handle, double timeout_s) {
+// Bitmask of the member ranks that are unresponsive right now (process gone, or heartbeat older
+// than fail_s; fail_s <= 0: process check only). Read-only: the collective watchdog uses it to
+// abort an in-flight weight collective; eviction itself stays with the all-gathers.
+uint64_t shmc_unresponsive(void* handle, double fail_s) {
   Handle* h = static_cast<Handle*>(handle);
-  return wait_until([&] { return shmc_alive(handle) == 0; }, timeout_s) ? 0 : -1;
+  const uint64_t fail_ns = fail_s > 0 ? static_cast<uint64_t>(fail_s * 1e9) : 0;
+  uint64_t mask = 0;
+  for (int r = 0; r < h->world; ++r) {
+    const RankCtl* c = h->ctl(r);
+    if (r == h->rank || (c->status.load(std::memory_order_acquire) & kGone)) continue;
+    if (unresponsive(c, fail_ns)) mask |= 1ull << r;
+  }
+  return mask;
+}
+
+// Wait until every rank left (job end: keeps the rendezvous host alive until the last rank is
+// done). A rank that crashed after its last gather never leaves by itself: it is evicted once it
+// is unresponsive (process gone, or heartbeat older than fail_s). 0 ok, -1 timeout.
+int shmc_wait_all_gone(void* handle, double timeout_s, double fail_s) {
+  Handle* h = static_cast<Handle*>(handle);
+  const uint64_t fail_ns = fail_s > 0 ? static_cast<uint64_t>(fail_s * 1e9) : 0;
+  return wait_until(
+             [&] {
+               for (int r = 0; r < h->world; ++r) {
+                 RankCtl* c = h->ctl(r);
+                 uint64_t s = c->status.load(std::memory_order_acquire);
+                 if (!(s & kGone) && unresponsive(c, fail_ns)) c->status.compare_exchange_strong(s, kGone | (s + 1), std::memory_order_acq_rel);
+               }
+               return shmc_alive(handle) == 0;
+             },
+             timeout_s)
+             ? 0
+             : -1;
 }
 
 // A second rank's handle onto the SAME mapping as `handle` (threads as ranks inside one process:

@@ -29,7 +29,7 @@ int shmc_barrier(void* handle, double timeout_s);
 int shmc_allgather_m(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, uint64_t* members, double timeout_s, double fail_s);
 int shmc_leave(void* handle);
 uint64_t shmc_alive(void* handle);
-int shmc_wait_all_gone(void* handle, double timeout_s);
+int shmc_wait_all_gone(void* handle, double timeout_s, double fail_s);
 void shmc_close(void* handle);
 }
 
@@ -122,7 +122,7 @@ int main(int argc, char** argv) {
       }
     }
     shmc_leave(h);
-    if (shmc_wait_all_gone(h, 30.0) != 0 || shmc_alive(h) != 0) errors.fetch_add(1);
+    if (shmc_wait_all_gone(h, 30.0, 0.0) != 0 || shmc_alive(h) != 0) errors.fetch_add(1);
   };
   threads.clear();
   for (int r = 0; r < world; ++r) threads.emplace_back(member_main, r);

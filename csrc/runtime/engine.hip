@@ -188,6 +188,9 @@ struct MLPEngine {
   // 0 = bf16 MFMA operands with fp32 master weights (persistent or 3-launch step path)
   int precision = 1;
   int num_cus = 0;
+  // CUs left to a concurrently running RCCL kernel (side-stream all-reduce / delayed averaging)
+  // when sizing the co-resident gangs: the persistent epoch needs every workgroup of a gang resident
+  int reserved_cus = 0;
   bool graph_persistent = false;
   // deferred to the epoch's control upload on the persistent path (fewer tiny launches per round)
   bool pending_zero_acc = false;  // zero loss / correct / give-up word
@@ -223,7 +226,7 @@ struct MLPEngine {
     if (pb32.h1x == nullptr || a.Xb16 == nullptr) return false;
     if (!mlp_persistent_f32_supported(a)) return false;
     if (f32_cap_bpad != a.Bpad) {
-      f32_cap = mlp_persistent_f32_resident_capacity(a, num_cus);
+      f32_cap = mlp_persistent_f32_resident_capacity(a, num_cus - reserved_cus > 0 ? num_cus - reserved_cus : 1);
       f32_cap_bpad = a.Bpad;
     }
     return mlp_persistent_f32_launch_wgs(a) <= f32_cap;
@@ -1138,6 +1141,18 @@ int mlp_engine_set_f32_ks(void* h, int ks) {
   if (ks != e->a.f32_ks) {
     e->a.f32_ks = ks;
     e->f32_cap_bpad = -1;  // the co-resident capacity depends on the instantiation
+    e->invalidate();
+  }
+  return 0;
+}
+// CUs reserved for a concurrent RCCL kernel in the co-residency capacity (0 = none). Re-captures.
+int mlp_engine_set_reserved_cus(void* h, int cus) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (cus < 0) cus = 0;
+  if (cus != e->reserved_cus) {
+    e->reserved_cus = cus;
+    e->f32_cap_bpad = -1;
     e->invalidate();
   }
   return 0;

@@ -149,6 +149,38 @@ def crash_process_at(node, stage: str = "TrainStage", round: Optional[int] = 1, 
     return StageFault(node, stage, crash, round)
 
 
+class CollectiveFault:
+    """Kill the whole PROCESS right before it issues a weight collective (after the reduce of its
+    local rows, after the pre-collective membership agreement) in ``round``: the other ranks are
+    already inside the collective — the case the collective guard (``Federation.await_works``)
+    must survive without waiting out ``COLLECTIVE_TIMEOUT``."""
+
+    def __init__(self, fed, node, round: Optional[int] = 1, kinds=("all_reduce", "all_reduce_async"), code: int = 0) -> None:
+        self.fed, self.node, self.round, self.kinds, self.code = fed, node, round, tuple(kinds), code
+        self.fired = threading.Event()
+        fed.pre_collective_hooks.append(self._hook)
+
+    def _hook(self, kind: str) -> None:
+        if self.fired.is_set() or kind not in self.kinds:
+            return
+        if self.round is not None and self.node.state.round != self.round:
+            return
+        self.fired.set()
+        logger.warning(self.node.addr, f"💥 fault injection: process crash inside {kind} (round {self.node.state.round})")
+        sys.stdout.flush()
+        os._exit(self.code)
+
+    def remove(self) -> None:
+        try:
+            self.fed.pre_collective_hooks.remove(self._hook)
+        except ValueError:
+            pass
+
+
+def crash_in_collective(fed, node, round: Optional[int] = 1, code: int = 0) -> CollectiveFault:
+    return CollectiveFault(fed, node, round, code=code)
+
+
 def delay_at(node, stage: str, seconds: float, round: Optional[int] = None) -> StageFault:
     """Stall ``node`` for ``seconds`` before ``stage`` (straggler injection)."""
     return StageFault(node, stage, lambda n: time.sleep(seconds), round)

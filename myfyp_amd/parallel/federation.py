@@ -20,11 +20,24 @@ the peers of all processes form one federation:
   ``Settings.FAILURE_TIMEOUT`` is evicted, and every survivor observes the same participant set at
   the same gather; before each weight collective the survivors re-agree and, on a change, rebuild
   their process groups over themselves (group-local rendezvous) — the reference's heartbeat
-  eviction (``heartbeater.py:94-103``) for the RCCL weights plane.
+  eviction (``heartbeater.py:94-103``) for the RCCL weights plane;
+* **in-flight failure** — a rank that dies *inside* a weight collective (after the pre-collective
+  agreement) is caught by the collective guard: every wait on a weight collective polls the
+  members' liveness (process gone / heartbeat stale, ``shmc_unresponsive``) and a watchdog thread
+  aborts the device group (``ncclCommAbort`` through ``_abort_process_group``) so no survivor
+  stays inside RCCL; the survivors agree on the outcome of every collective (one shared-memory
+  gather) before anything is written, rebuild their groups over themselves and re-run the
+  aggregation from the still-intact local rows (the reference's "aggregate whatever arrived",
+  ``aggregator.py:191-208``, and drop-on-send-failure, ``grpc_client.py:176-186``);
+* **forced collective** (``Settings.FORCE_COLLECTIVE`` / ``MYFYP_FORCE_COLLECTIVE=1``) — a
+  single-process job still initialises the ``nccl`` (RCCL) process group at world size 1 and takes
+  every multi-rank code path (bucketed side-stream FedAvg, broadcast, all-gather, group rebuild), so
+  the RCCL data plane runs and can be profiled on one GPU.
 """
 
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import sys
@@ -238,6 +251,11 @@ class LocalGang:
             return self._result[gen]
 
 
+class MembershipChanged(RuntimeError):
+    """A weight collective did not complete on every member (a rank died inside it). The groups
+    have been rebuilt over the survivors; the aggregation must be re-run from its inputs."""
+
+
 # ---------------------------------------------------------------------------------------------
 # federation
 # ---------------------------------------------------------------------------------------------
@@ -270,6 +288,26 @@ class Federation:
         self._pg = None
         self._hb_stop = threading.Event()
         self._hb_thread: Optional[threading.Thread] = None
+        # collective data plane active: several ranks, or a forced single-rank RCCL group
+        self.collective = world > 1
+        self.forced = False
+        # weights section (one aggregation): membership / departure frozen at entry
+        self._section_lock = threading.RLock()
+        self._frozen: Optional[Tuple[bool, List[int]]] = None
+        self._depart_deferred = False
+        # collective guard: watchdog state and the not-yet-confirmed device pipeline
+        self._inflight: Optional[Tuple[Any, List[int]]] = None  # (group, members) of the running collective
+        self._aborted: set = set()
+        self._pending: List[Tuple[List[Any], List[int], Callable[[], None], Any]] = []
+        # set by the round driver: deferred device collectives are confirmed at the top of the next
+        # round (before anything reads the rows); other callers confirm at the end of the section
+        self.async_confirm = False
+        self._wd_stop = threading.Event()
+        self._wd_thread: Optional[threading.Thread] = None
+        self.recoveries = 0
+        # fault injection (fault_injection.crash_in_collective): called right before a weight
+        # collective is issued, with its kind
+        self.pre_collective_hooks: List[Callable[[str], None]] = []
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
@@ -288,7 +326,18 @@ class Federation:
         else:
             device = torch.device("cpu")
         store = None
-        if world > 1:
+        forced = world == 1 and (bool(Settings.FORCE_COLLECTIVE) or os.environ.get("MYFYP_FORCE_COLLECTIVE", "0") not in ("", "0"))
+        if forced:  # a one-rank RCCL job: rendezvous on this host
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if world > 1 or forced:
             import torch.distributed as dist
 
             if not dist.is_initialized():
@@ -300,13 +349,21 @@ class Federation:
                     kw["device_id"] = device
                 dist.init_process_group(backend=be, **kw)
             store = _default_store()
-        cls._instance = cls(rank, world, local_rank, device, store)
-        if world > 1:
-            cls._instance._cpu_group()
-            cls._instance._init_shm()
-        if store is not None:
-            cls._instance.bus = StoreBus(store, rank, world, cls._instance._deliver)
-        return cls._instance
+        inst = cls._instance = cls(rank, world, local_rank, device, store)
+        inst.collective = world > 1 or forced
+        inst.forced = forced
+        if inst.collective:
+            import torch.distributed as dist
+
+            inst._cpu_group()
+            inst._init_shm()
+            # weight collectives run on their own group over the live ranks: the watchdog may abort
+            # it (ncclCommAbort) without touching WORLD, whose store later groups rendezvous on
+            inst._pg = dist.new_group(ranks=list(range(world)))
+            inst._start_watchdog()
+        if store is not None and world > 1:
+            inst.bus = StoreBus(store, rank, world, inst._deliver)
+        return inst
 
     @classmethod
     def get(cls) -> "Federation":
@@ -345,6 +402,12 @@ class Federation:
             self._hb_thread = threading.Thread(target=beat, name=f"fed-heartbeat-{self.rank}", daemon=True)
             self._hb_thread.start()
 
+    def _stop_watchdog(self) -> None:
+        self._wd_stop.set()
+        t, self._wd_thread = self._wd_thread, None
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=5.0)
+
     def _stop_heartbeat(self) -> None:
         self._hb_stop.set()
         t, self._hb_thread = self._hb_thread, None
@@ -359,20 +422,26 @@ class Federation:
         if self.central is not None:
             self.central.stop()  # last flush to rank 0 while every rank is still here
             self.central = None
+        try:
+            self.confirm_collectives()  # the last round's device collective (nothing to re-run after it)
+        except Exception as e:
+            logger.warning(f"rank{self.rank}", f"last collective unconfirmed at shutdown: {e}")
+        self._pending.clear()
+        self._stop_watchdog()
         if self.shm is not None:
             self.shm.leave()
-            synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT))
+            synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT), float(Settings.FAILURE_TIMEOUT))
             self._stop_heartbeat()  # joined before the unmap: a beat in flight wrote into freed pages (SIGSEGV at exit)
             self.shm.close()
             self.shm = None
         if self.bus is not None:
             self.bus.stop()
             self.bus = None
-        if self.world > 1:
+        if self.collective:
             import torch.distributed as dist
 
             if dist.is_initialized():
-                if not synced and not self.departed:
+                if not synced and not self.departed and self.members == list(range(self.world)) and not self._aborted:
                     dist.barrier(group=self._pg)
                 dist.destroy_process_group()
         Federation._instance = None
@@ -386,6 +455,7 @@ class Federation:
         if inst is not None and inst.bus is not None:
             inst.bus.stop()
         if inst is not None:
+            inst._stop_watchdog()
             inst._stop_heartbeat()
         if inst is not None and inst.shm is not None:
             inst.shm.close()
@@ -492,33 +562,44 @@ class Federation:
     def depart(self) -> None:
         """This rank leaves the running experiment: it joins no further collective, and the other
         ranks stop waiting for it at their next gather (shared-memory membership protocol)."""
-        if self.departed or self.world == 1:
+        if self.departed or not self.collective:
             return
         self.departed = True
-        if self.shm is not None:
+        if self._frozen is not None:
+            # inside a weights section this rank already agreed to take part: it completes the
+            # section's collectives and leaves at its exit (the others would wait for it otherwise)
+            self._depart_deferred = True
+        elif self.shm is not None:
             self.shm.leave()
         logger.warning(f"rank{self.rank}", "last local peer stopped mid-experiment: rank departs the federation")
 
-    def _apply_members(self, ranks: List[int]) -> None:
-        """Every survivor calls this with the same participant set at the same gather."""
-        if ranks == self.members:
+    def _apply_members(self, ranks: List[int], force: bool = False) -> None:
+        """Every survivor calls this with the same participant set at the same gather (``force``:
+        rebuild the groups even when nobody left, after a failed collective aborted them)."""
+        if ranks == self.members and not force:
             return
         import torch.distributed as dist
 
         gone = [r for r in self.members if r not in ranks]
-        logger.warning(f"rank{self.rank}", f"ranks {gone} left the federation; continuing over ranks {ranks}")
+        if gone:
+            logger.warning(f"rank{self.rank}", f"ranks {gone} left the federation; continuing over ranks {ranks}")
         with self._lock:
             self.members = list(ranks)
             self.peers = {a: r for a, r in self.peers.items() if r in ranks}
         # process groups over the survivors; group-local rendezvous (the departed ranks take no part)
+        old = (self._pg, self._cpu_pg)
         self._pg = dist.new_group(ranks=ranks, use_local_synchronization=True)
         self._cpu_pg = self._pg if dist.get_backend() == "gloo" else dist.new_group(ranks=ranks, backend="gloo", use_local_synchronization=True)
+        # the replaced groups include a rank that is gone: abort them (local, never blocks on the
+        # dead rank the way a destroy would) so their communicators and buffers are released
+        for g in {id(x): x for x in old if x is not None and x is not dist.group.WORLD}.values():
+            self._release_group(g)
         self.record("membership_change", float(len(gone)))
 
     def sync_members(self) -> List[int]:
         """Liveness agreement right before a weight collective (a peer may have died since the
         round's vote gather): every survivor leaves with the same member list and process group."""
-        if self.world > 1 and not self.departed and self.shm is not None:
+        if self.collective and not self.departed and self.shm is not None:
             ranks, _ = self.shm.allgather_members(None, float(Settings.FAILURE_TIMEOUT))
             self._apply_members(ranks)
         return self.members
@@ -527,7 +608,7 @@ class Federation:
         """Control-plane gather (votes, wire models) over a CPU (gloo) group: an object gather on the
         RCCL group would pickle through device memory and synchronise the host with every queued
         kernel, stalling the asynchronous round pipeline."""
-        if self.world == 1 or self.departed:
+        if not self.collective or self._is_departed():
             return [obj]
         if self.shm is not None:
             ranks, got = self.shm.allgather_members(obj, float(Settings.FAILURE_TIMEOUT))
@@ -545,7 +626,7 @@ class Federation:
         """Collective (every rank calls it): merge every rank's metric stores into every rank's
         logger, so ``logger.get_global_logs()`` shows all peers of the job (the reference's
         multi-process runs centralise logs in one Ray actor, ``ray_logger.py:32-250``)."""
-        if self.world == 1:
+        if not self.collective:
             return
         from myfyp_amd.management.logger import logger
 
@@ -562,21 +643,26 @@ class Federation:
         return self._cpu_pg
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        """In-place all-reduce over RCCL among the live ranks (bucketed for large buffers)."""
-        if self.world == 1 or self.departed:
+        """In-place all-reduce over RCCL among the live ranks (bucketed for large buffers). Guarded:
+        returns only once every member completed it; raises :class:`MembershipChanged` (groups
+        rebuilt, ``t`` restored to its input) when a member died inside it."""
+        if not self.collective or self._is_departed():
             return t
         import torch.distributed as dist
 
         rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
         flat = t.view(-1)
+        keep = flat.clone() if self._guarded() else None
+        self._pre_collective("all_reduce")
         bucket = max(1, Settings.BUCKET_BYTES // flat.element_size())
         t0 = time.perf_counter()
-        if flat.numel() <= bucket:
-            dist.all_reduce(flat, op=rop, group=self._pg)
-        else:
-            works = [dist.all_reduce(flat[i : i + bucket], op=rop, group=self._pg, async_op=True) for i in range(0, flat.numel(), bucket)]
-            for w in works:
-                w.wait()
+        works = [dist.all_reduce(flat[i : i + bucket], op=rop, group=self._pg, async_op=True) for i in range(0, flat.numel(), bucket)]
+        try:
+            self.await_works(works, "all_reduce")
+        except MembershipChanged:
+            if keep is not None:
+                flat.copy_(keep)
+            raise
         self.comm.host("all_reduce", flat.numel() * flat.element_size(), time.perf_counter() - t0)
         return t
 
@@ -589,23 +675,223 @@ class Federation:
             return None
         import torch.distributed as dist
 
+        self._pre_collective("all_reduce_async")
         self.comm.host("all_reduce_async", t.numel() * t.element_size(), 0.0)
         return dist.all_reduce(t, group=self._pg, async_op=True)
 
+    def all_gather_into_tensor_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """Guarded ``all_gather_into_tensor`` over the live ranks (same contract as ``all_reduce_``)."""
+        import torch.distributed as dist
+
+        t0 = time.perf_counter()
+        self._pre_collective("all_gather")
+        w = dist.all_gather_into_tensor(out, inp, group=self._pg, async_op=True)
+        self.await_works([w], "all_gather")
+        self.comm.host("all_gather", out.numel() * out.element_size(), time.perf_counter() - t0)
+        return out
+
+    def batch_p2p_(self, ops_: list) -> None:
+        """Guarded grouped point-to-point sends/receives (topology mixing)."""
+        import torch.distributed as dist
+
+        t0 = time.perf_counter()
+        # gloo's send/recv works only complete inside wait() (a dead peer's closed socket raises there)
+        self.await_works(dist.batch_isend_irecv(ops_), "p2p", poll=dist.get_backend(self._pg) != "gloo")
+        self.comm.host("p2p", 0, time.perf_counter() - t0)
+
     def broadcast_(self, t: torch.Tensor, src_rank: int) -> torch.Tensor:
-        if self.world == 1 or self.departed:
+        if not self.collective or self._is_departed():
             return t
         import torch.distributed as dist
 
         t0 = time.perf_counter()
-        dist.broadcast(t, src=src_rank, group=self._pg)
+        self._pre_collective("broadcast")
+        w = dist.broadcast(t, src=src_rank, group=self._pg, async_op=True)
+        self.await_works([w], "broadcast")
         self.comm.host("broadcast", t.numel() * t.element_size(), time.perf_counter() - t0)
         return t
 
     @property
     def solo(self) -> bool:
-        """No other live rank to exchange weights with."""
-        return self.world == 1 or self.departed or self.members == [self.rank]
+        """No other live rank to exchange weights with (a forced single-rank RCCL job is not solo:
+        its collectives run through RCCL)."""
+        if not self.collective or self._is_departed():
+            return True
+        return self.members == [self.rank] and not self.forced
+
+    # ------------------------------------------------------------------ collective guard
+    def _pre_collective(self, kind: str) -> None:
+        for hook in list(self.pre_collective_hooks):
+            hook(kind)
+
+    def _is_departed(self) -> bool:
+        fz = self._frozen
+        return fz[0] if fz is not None else self.departed
+
+    def _guarded(self) -> bool:
+        """Failure-aware collectives (liveness polling + agreement) need the shared-memory control
+        plane (single-node jobs); elsewhere collectives fall back to the RCCL/gloo timeouts."""
+        return bool(Settings.COLLECTIVE_FAILOVER) and self.shm is not None
+
+    @contextlib.contextmanager
+    def weights_section(self):
+        """One aggregation's weight collectives. Membership is agreed once at entry (one shm
+        gather) and frozen with this rank's departure state until exit, so a rank that agreed to
+        take part always completes the collectives it agreed to (a concurrent ``depart()`` takes
+        effect at exit). Nested sections reuse the outer agreement."""
+        with self._section_lock:
+            outer = self._frozen is not None
+            if not outer:
+                self.confirm_collectives()
+                self.sync_members()
+                self._frozen = (self.departed, list(self.members))
+            try:
+                yield self
+            finally:
+                if not outer:
+                    self._frozen = None
+                    if self._depart_deferred:
+                        self._depart_deferred = False
+                        if self.shm is not None:
+                            self.shm.leave()
+
+    def run_aggregation(self, fn: Callable[[], Any]) -> Any:
+        """Run ``fn`` (an aggregation: reads the local rows, weight collectives, then writes) in a
+        weights section; when a member died inside one of its collectives the groups are rebuilt
+        and ``fn`` is re-run over the survivors (its inputs are intact: nothing is written before
+        the last collective returned on every member)."""
+        for attempt in range(self.world + 1):
+            try:
+                with self.weights_section():
+                    return fn()
+            except MembershipChanged as e:
+                logger.warning(f"rank{self.rank}", f"re-running the aggregation over ranks {self.members} ({e})")
+        raise RuntimeError("aggregation did not complete after repeated membership changes")
+
+    def _members_alive(self, members: List[int]) -> List[int]:
+        """Members (other than this rank) that are unresponsive right now."""
+        if self.shm is None:
+            return []
+        bad = self.shm.unresponsive(float(Settings.FAILURE_TIMEOUT))
+        return [r for r in bad if r in members and r != self.rank]
+
+    def await_works(self, works: list, what: str, poll: bool = True) -> None:
+        """Wait for collective works while watching the members' liveness; then agree with the
+        other members that every one of them completed (one shm gather). On a failure anywhere:
+        abort the group, re-agree membership over the survivors and raise MembershipChanged."""
+        works = [w for w in works if w is not None]
+        if not self._guarded():
+            for w in works:
+                w.wait()
+            return
+        members = list(self._frozen[1]) if self._frozen is not None else list(self.members)
+        group = self._pg
+        ok = True
+        self._inflight = (group, members)
+        try:
+            spin = 0
+            for w in works:
+                while True:
+                    try:
+                        if not poll or w.is_completed():
+                            w.wait()  # surfaces an error; makes the current stream wait (nccl)
+                            break
+                    except Exception as e:  # connection closed by a dead peer (gloo), aborted comm (nccl)
+                        logger.warning(f"rank{self.rank}", f"{what} failed: {str(e)[:160]}")
+                        ok = False
+                        break
+                    if id(group) in self._aborted or self._members_alive(members):
+                        ok = False
+                        break
+                    spin += 1
+                    time.sleep(0 if spin < 200 else 0.0005)
+                if not ok:
+                    break
+        finally:
+            self._inflight = None
+        self._agree(ok, group, what)
+
+    def _agree(self, ok: bool, group, what: str) -> None:
+        """Every member reports whether its collective completed; unless all did and nobody left,
+        everyone aborts the group, rebuilds over the survivors and re-runs."""
+        ranks, got = self.shm.allgather_members(bool(ok), float(Settings.FAILURE_TIMEOUT))
+        frozen = self._frozen[1] if self._frozen is not None else self.members
+        all_ok = ok and got is not None and all(bool(got[r]) for r in ranks) and ranks == list(frozen)
+        if all_ok:
+            return
+        self.recoveries += 1
+        self.record("collective_recovery", 1.0)
+        self._release_group(group)
+        self._apply_members(ranks, force=True)
+        if self._frozen is not None:
+            self._frozen = (self._frozen[0], list(self.members))
+        raise MembershipChanged(f"{what}: members {list(frozen)} -> {ranks}")
+
+    def _release_group(self, g) -> None:
+        """Abort a replaced/failed device group (ncclCommAbort: local, never blocks on the dead
+        rank the way a destroy would, ends kernels still waiting on it, frees the communicator)."""
+        import torch.distributed as dist
+
+        if g is None or g is dist.group.WORLD or id(g) in self._aborted:
+            return
+        self._aborted.add(id(g))
+        try:
+            # gloo: a waiter on a dead peer already fails on its closed socket, and aborting a gloo
+            # group tears its worker threads down under the waiter (std::terminate): just drop it
+            if dist.get_backend(g) != "gloo":
+                dist.distributed_c10d._abort_process_group(g)
+        except Exception as e:  # best effort: the group is never used again
+            logger.debug(f"rank{self.rank}", f"group abort: {e}")
+
+    def _start_watchdog(self) -> None:
+        """Background watchdog: while a weight collective is in flight, a member that becomes
+        unresponsive gets the group aborted, so device kernels stuck on the dead peer end (the
+        host-side waits notice the abort and recover)."""
+        if not self._guarded() or self._wd_thread is not None:
+            return
+
+        def run() -> None:
+            while not self._wd_stop.wait(0.02):
+                inf = self._inflight
+                pend = self._pending
+                cands = [inf] if inf is not None else []
+                cands += [(g, m) for _, m, _, g in pend]
+                for g, members in cands:
+                    if g is not None and id(g) not in self._aborted and self._members_alive(members):
+                        logger.warning(f"rank{self.rank}", f"watchdog: member(s) {self._members_alive(members)} unresponsive inside a collective; aborting the group")
+                        self._release_group(g)
+
+        self._wd_thread = threading.Thread(target=run, name=f"fed-watchdog-{self.rank}", daemon=True)
+        self._wd_thread.start()
+
+    def defer_confirm(self, works: list, retry: Callable[[], None]) -> None:
+        """Register an asynchronous weight collective (device pipeline: apply kernels already
+        queued behind it) whose outcome is confirmed before the next aggregation or round —
+        ``retry`` re-runs it over the survivors from retained inputs."""
+        if not self._guarded():
+            return
+        members = list(self._frozen[1]) if self._frozen is not None else list(self.members)
+        self._pending.append((works, members, retry, self._pg))
+
+    def confirm_collectives(self) -> None:
+        """Confirm the deferred device collectives (every member completed them); on a failure
+        the groups are rebuilt and the retained-input retry runs (synchronously confirmed)."""
+        while self._pending:
+            works, members, retry, _ = self._pending.pop(0)
+            with self._section_lock:
+                saved = self._frozen
+                self._frozen = (False, members)
+                try:
+                    self.await_works(works, "deferred all_reduce")
+                    self._frozen = saved
+                except MembershipChanged as e:
+                    logger.warning(f"rank{self.rank}", f"re-running a deferred collective over ranks {self.members} ({e})")
+                    self._frozen = None
+                    self._pending.clear()
+                    self.run_aggregation(retry)
+                    self._frozen = saved
+                    self.confirm_collectives()
+                    return
 
     @property
     def group(self):
@@ -613,7 +899,7 @@ class Federation:
         return self._pg
 
     def barrier(self) -> None:
-        if self.world == 1 or self.departed:
+        if not self.collective or self.departed:
             return
         if self.shm is not None:
             self.sync_members()

@@ -233,6 +233,13 @@ class MLPGroup:
         # one process per GPU with few peers each (N >= 2 GPUs in bench.py); 8 peers keep 1
         ks = self.force_f32_ks or (2 if self.handles and max(self.handles) < 4 else 1)
         _native.check(lib.mlp_engine_set_f32_ks(self._engine, ks), "set_f32_ks")
+        # weight collectives on the comm stream may hold CUs while an epoch runs: size the
+        # co-resident gangs without them
+        from myfyp_amd.parallel.federation import Federation
+
+        fed = Federation._instance
+        reserve = int(Settings.RCCL_RESERVED_CUS) if fed is not None and not fed.solo else 0
+        _native.check(lib.mlp_engine_set_reserved_cus(self._engine, reserve), "set_reserved_cus")
         if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
             _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
         if self._bound_version != self._data_version:

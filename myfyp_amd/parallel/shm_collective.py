@@ -59,7 +59,9 @@ def _load() -> Optional[ctypes.CDLL]:
     lib.shmc_alive.restype = u64
     lib.shmc_alive.argtypes = [vp]
     lib.shmc_wait_all_gone.restype = i
-    lib.shmc_wait_all_gone.argtypes = [vp, d]
+    lib.shmc_wait_all_gone.argtypes = [vp, d, d]
+    lib.shmc_unresponsive.restype = u64
+    lib.shmc_unresponsive.argtypes = [vp, d]
     lib.shmc_close.restype = None
     lib.shmc_close.argtypes = [vp]
     _LIB = lib
@@ -160,8 +162,16 @@ class ShmCollective:
         m = int(self._lib.shmc_alive(self._h))
         return [r for r in range(self.world) if m >> r & 1]
 
-    def wait_all_gone(self, timeout: float) -> bool:
-        return self._lib.shmc_wait_all_gone(self._h, timeout) == 0
+    def unresponsive(self, fail_s: float) -> List[int]:
+        """Member ranks (other than this one) whose process is gone or whose heartbeat is older
+        than ``fail_s`` — read-only; the collective watchdog's trigger."""
+        m = int(self._lib.shmc_unresponsive(self._h, fail_s))
+        return [r for r in range(self.world) if m >> r & 1]
+
+    def wait_all_gone(self, timeout: float, fail_s: float = 0.0) -> bool:
+        """Job end: wait until every rank left; a crashed rank (process gone, or heartbeat older
+        than ``fail_s``) is evicted instead of waited for."""
+        return self._lib.shmc_wait_all_gone(self._h, timeout, fail_s) == 0
 
     def barrier(self) -> None:
         if self._lib.shmc_barrier(self._h, self.timeout) != 0:

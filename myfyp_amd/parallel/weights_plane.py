@@ -44,17 +44,23 @@ def _stacked_group(learners) -> Optional[Any]:
 def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str) -> None:
     """Every peer adopts the initiator's weights: local copy + one RCCL broadcast per tensor."""
     learners = {a: fed.local_nodes[a].learner for a in arrived if a in fed.local_nodes}
-    fed.sync_members()
-    src_rank = fed.peers.get(initiator, min(fed.members))
-    ref_addr = initiator if initiator in learners else next(iter(learners))
-    src = state_tensors(learners[ref_addr])
-    bufs = [t.detach().clone() for t in src]
-    for t in bufs:
-        fed.broadcast_(t, src_rank)
-    with torch.no_grad():
-        for a, lr in learners.items():
-            for dst, s in zip(state_tensors(lr), bufs):
-                dst.copy_(s)
+
+    def run() -> None:
+        # the initiator's rank, or (if it died) the lowest survivor: every survivor agrees on it
+        src_rank = fed.peers.get(initiator, min(fed.members))
+        if src_rank not in fed.members:
+            src_rank = min(fed.members)
+        ref_addr = initiator if initiator in learners else next(iter(learners))
+        src = state_tensors(learners[ref_addr])
+        bufs = [t.detach().clone() for t in src]
+        for t in bufs:
+            fed.broadcast_(t, src_rank)
+        with torch.no_grad():
+            for a, lr in learners.items():
+                for dst, s in zip(state_tensors(lr), bufs):
+                    dst.copy_(s)
+
+    fed.run_aggregation(run)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -137,15 +143,27 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
         st.pending, landed = False, True
     if delayed and not final:
         if st.snap is None or tuple(st.snap.shape) != (P, n):
-            st.snap = torch.empty(P, n, dtype=torch.float32, device=dev)
-            st.buf = torch.empty(n + 4, dtype=torch.float32, device=dev)
+            # zeros: rows of unused capacity slots are read (with weight 0) by the reduce
+            st.snap = torch.zeros(P, n, dtype=torch.float32, device=dev)
+            st.buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
             landed = False
         if not landed:  # first delayed round: snapshot only
             ops.check(fast.myfyp_fedavg_delayed_land(base, st.snap.data_ptr(), n, None, None, P, n, S, mp, cur.cuda_stream), "fedavg_snapshot")
-        _bucketed_reduce(fed, fast, comm_stream(dev), cur, st.snap.data_ptr(), n, n, P, wp, st.buf, apply=None)
+        snap_ptr, sbuf = st.snap.data_ptr(), st.buf
+        works = _bucketed_reduce(fed, fast, comm_stream(dev), cur, snap_ptr, n, n, P, wp, sbuf, apply=None)
         st.done = torch.cuda.Event()
         st.done.record(comm_stream(dev))
         st.pending = True
+
+        def retry() -> None:  # the snapshot rows are intact: reduce them again over the survivors
+            c = torch.cuda.current_stream(dev)
+            ops.check(fast.myfyp_fedavg_bucket_reduce(sbuf.data_ptr() + 16, sbuf.data_ptr(), snap_ptr, P, n, n, w.ctypes.data, c.cuda_stream),
+                      "fedavg_bucket_reduce")
+            fed.all_reduce_(sbuf)
+            st.done = torch.cuda.Event()
+            st.done.record(c)
+
+        fed.defer_confirm(works, retry)
         return
     if fed.solo:  # nothing to all-reduce: weighted mean and write-back in one launch
         ops.check(fast.myfyp_fedavg_stacked_local(base, P, n, S, wp, mp, cur.cuda_stream), "fedavg_local")
@@ -158,14 +176,32 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
         return
     buf = getattr(group, "_wp_bucket_buf", None)
     if buf is None or buf.numel() != n + 4:
-        buf = group._wp_bucket_buf = torch.empty(n + 4, dtype=torch.float32, device=dev)
-    _bucketed_reduce(fed, fast, comm_stream(dev), cur, base, S, n, P, wp, buf, apply=(base, S, mp))
+        buf = group._wp_bucket_buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
+    keep = None
+    if fed._guarded():  # retained local partial sums: a failed all-reduce is re-run from them
+        keep = getattr(group, "_wp_keep_buf", None)
+        if keep is None or keep.numel() != n + 4:
+            keep = group._wp_keep_buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
+    works = _bucketed_reduce(fed, fast, comm_stream(dev), cur, base, S, n, P, wp, buf, apply=(base, S, mp), keep=keep)
+    if keep is not None:
+
+        def retry() -> None:  # survivors: all-reduce the retained local partials, apply again
+            c = torch.cuda.current_stream(dev)
+            c.wait_stream(comm_stream(dev))
+            buf.copy_(keep)
+            fed.all_reduce_(buf)
+            ops.check(fast.myfyp_fedavg_bucket_apply(base, buf.data_ptr() + 16, buf.data_ptr(), P, n, S, mask.ctypes.data, c.cuda_stream),
+                      "fedavg_bucket_apply")
+
+        fed.defer_confirm(works, retry)
 
 
-def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, P: int, wp: int, buf: torch.Tensor, apply) -> None:
+def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, P: int, wp: int, buf: torch.Tensor, apply, keep=None) -> list:
     """Side-stream pipeline over ``bucket_ranges``: reduce launch + async all-reduce per bucket,
     then (``apply`` = (dst, ld, mask)) per bucket wait + apply launch. ``buf`` = [wsum, pad x3 | data];
-    bucket 0's all-reduce carries the weight sum, so apply k needs only buckets 0 and k."""
+    bucket 0's all-reduce carries the weight sum, so apply k needs only buckets 0 and k. ``keep``
+    (failover) receives a copy of each bucket's local partial sum before its all-reduce. Returns
+    the all-reduce works (confirmed later by the collective guard)."""
     from myfyp_amd.settings import Settings
 
     cs.wait_stream(cur)  # the rows are final on the compute stream
@@ -178,7 +214,10 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
         for k, (b0, b1) in enumerate(ranges):
             ops.check(fast.myfyp_fedavg_bucket_reduce(bp + 4 * (4 + b0), bp if k == 0 else None, src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream),
                       "fedavg_bucket_reduce")
-            works.append(fed.all_reduce_async(buf[(0 if k == 0 else 4 + b0) : 4 + b1]))
+            lo = 0 if k == 0 else 4 + b0
+            if keep is not None:
+                keep[lo : 4 + b1].copy_(buf[lo : 4 + b1])
+            works.append(fed.all_reduce_async(buf[lo : 4 + b1]))
         for k, (b0, b1) in enumerate(ranges):
             if works[k] is not None:
                 works[k].wait()
@@ -188,8 +227,11 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
     ev1.record(cs)
     fed.comm.device("fedavg_pipeline", 4 * (n + 1), ev0, ev1)  # resolved lazily by the node monitor
     buf.record_stream(cs)
+    if keep is not None:
+        keep.record_stream(cs)
     if apply is not None:
         cur.wait_stream(cs)  # stream-level: the next kernel on the compute stream sees the average
+    return works
 
 
 @traced("aggregate_mean")
@@ -201,37 +243,43 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
     from myfyp_amd.settings import Settings
 
     t0 = time.perf_counter()
-    fed.sync_members()  # a rank may have lost its last peer since the vote: agree on the survivors
-    addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
-    learners = [fed.local_nodes[a].learner for a in addrs]
-    weights = [float(arrived[a][0]) for a in addrs]
-    contributors = [a for a, w in zip(addrs, weights) if w > 0]
-    group = _stacked_group(learners)
-    dev = learners[0].flat_params().device
-    if group is not None and dev.type == "cuda":
-        w = np.zeros(group.capacity, dtype=np.float32)
-        mask = np.zeros(group.capacity, dtype=np.float32)
-        for lr, wt in zip(learners, weights):
-            w[lr._engine.slot] = wt
-            mask[lr._engine.slot] = 1.0
-        _stacked_mean_cuda(fed, group, w, mask, final)
-        total_w = float(sum(weights))  # local share; the global Σw stays on the device
-    elif group is not None:
-        wm = torch.zeros(2, group.capacity, dtype=torch.float32)
-        for lr, wt in zip(learners, weights):
-            wm[0, lr._engine.slot] = wt
-            wm[1, lr._engine.slot] = 1.0
-        n = group.numel
-        buf = torch.empty(n + 1, dtype=torch.float32, device=dev)
-        ops.stacked_weighted_sum(group.params[:, :n], wm[0], buf[:n], 1.0)
-        buf[n:].fill_(float(sum(weights)))
-        fed.all_reduce_(buf)
-        total = buf[n:].clone()
-        buf[:n].div_(total.clamp_min(1e-12))
-        ops.broadcast_rows(buf[:n], group.params[:, :n], wm[1])
-        total_w = total
-    else:
-        total_w = _generic_mean(fed, addrs, learners, weights, final, bool(Settings.DELAYED_AVERAGING))
+
+    def run() -> Tuple[float, List[str]]:
+        addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
+        learners = [fed.local_nodes[a].learner for a in addrs]
+        weights = [float(arrived[a][0]) for a in addrs]
+        contributors = [a for a, w in zip(addrs, weights) if w > 0]
+        group = _stacked_group(learners)
+        dev = learners[0].flat_params().device
+        if group is not None and dev.type == "cuda":
+            w = np.zeros(group.capacity, dtype=np.float32)
+            mask = np.zeros(group.capacity, dtype=np.float32)
+            for lr, wt in zip(learners, weights):
+                w[lr._engine.slot] = wt
+                mask[lr._engine.slot] = 1.0
+            _stacked_mean_cuda(fed, group, w, mask, final)
+            total_w = float(sum(weights))  # local share; the global Σw stays on the device
+        elif group is not None:
+            wm = torch.zeros(2, group.capacity, dtype=torch.float32)
+            for lr, wt in zip(learners, weights):
+                wm[0, lr._engine.slot] = wt
+                wm[1, lr._engine.slot] = 1.0
+            n = group.numel
+            buf = torch.empty(n + 1, dtype=torch.float32, device=dev)
+            ops.stacked_weighted_sum(group.params[:, :n], wm[0], buf[:n], 1.0)
+            buf[n:].fill_(float(sum(weights)))
+            fed.all_reduce_(buf)
+            total = buf[n:].clone()
+            buf[:n].div_(total.clamp_min(1e-12))
+            ops.broadcast_rows(buf[:n], group.params[:, :n], wm[1])
+            total_w = total
+        else:
+            total_w = _generic_mean(fed, addrs, learners, weights, final, bool(Settings.DELAYED_AVERAGING))
+        return total_w, contributors
+
+    total_w, contributors = fed.run_aggregation(run)
+    if not fed.async_confirm:  # nobody confirms at the next round top: confirm the device pipeline now
+        fed.confirm_collectives()
     fed.record("aggregate", time.perf_counter() - t0)
     return total_w, contributors
 
@@ -285,7 +333,10 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
     grouped batch of point-to-point sends/receives (RCCL over xGMI; gloo on CPU). Every rank calls
     this with the same peer list, so the P2P pattern matches by construction."""
     t0 = time.perf_counter()
-    fed.sync_members()
+    return fed.run_aggregation(lambda: _neighbors(fed, arrived, aggregator, t0))
+
+
+def _neighbors(fed: Federation, arrived: Dict[str, Any], aggregator, t0: float) -> List[str]:
     peers = fed.all_peers()
     index = {a: i for i, a in enumerate(peers)}
     w = aggregator.mixing_matrix(len(peers))
@@ -333,8 +384,7 @@ def aggregate_neighbors(fed: Federation, arrived: Dict[str, Any], aggregator) ->
         pg = fed.group
         ops_ = [dist.P2POp(dist.isend, t, rb, group=pg, tag=index[a]) for (a, rb), t in sorted(sends.items(), key=lambda kv: (index[kv[0][0]], kv[0][1]))]
         ops_ += [dist.P2POp(dist.irecv, t, fed.peers[b], group=pg, tag=index[b]) for b, t in sorted(recvs.items(), key=lambda kv: index[kv[0]])]
-        for req in dist.batch_isend_irecv(ops_):
-            req.wait()
+        fed.batch_p2p_(ops_)
     src = dict(rows)
     src.update(recvs)
     mixed = {}
@@ -372,7 +422,11 @@ def aggregate_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], a
     x_start is a trainer's round-start snapshot (the callback's x0) or a non-trainer's current
     weights — identical on every rank, since every peer starts the round from the last aggregate."""
     t0 = time.perf_counter()
-    fed.sync_members()
+    fed.run_aggregation(lambda: _scaffold(fed, arrived, aggregator))
+    fed.record("aggregate", time.perf_counter() - t0)
+
+
+def _scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> None:
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     flats = [learners[a].flat_params() for a in addrs]
@@ -406,7 +460,6 @@ def aggregate_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], a
         fed.local_nodes[a].aggregator._c_dev = c_new
         lr.get_model().add_info("scaffold", {"global_c": gc})
         lr.update_callbacks_with_model_info()
-    fed.record("aggregate", time.perf_counter() - t0)
 
 
 @traced("aggregate_median")
@@ -417,7 +470,11 @@ def aggregate_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> 
     network in registers, <= 16 models) writes the result into every local peer. With a single
     rank the kernel reads the live rows directly (no packing copy)."""
     t0 = time.perf_counter()
-    fed.sync_members()
+    fed.run_aggregation(lambda: _median(fed, arrived))
+    fed.record("aggregate", time.perf_counter() - t0)
+
+
+def _median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None:
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     trainers = [a for a in addrs if float(arrived[a][0]) > 0]
@@ -435,17 +492,14 @@ def aggregate_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> 
             ops.median_into([rows_of(a) for a in trainers], [med])
             for a in addrs:
                 _unpack_into(learners[a], med)
-        fed.record("aggregate", time.perf_counter() - t0)
         return
-    import torch.distributed as dist
-
     ref = rows_of(addrs[0])
     n = ref.numel()
     send = torch.zeros(kmax, n, dtype=torch.float32, device=ref.device)
     for i, a in enumerate(trainers):
         send[i].copy_(rows_of(a))
     recv = torch.empty(len(counts) * kmax, n, dtype=torch.float32, device=ref.device)
-    dist.all_gather_into_tensor(recv, send, group=fed.group)
+    fed.all_gather_into_tensor_(recv, send)
     rows = [recv[r * kmax + i] for r, c in enumerate(counts) for i in range(c)]
     if not rows:
         return
@@ -456,11 +510,14 @@ def aggregate_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> 
         ops.median_into(rows, [med])
         for a in addrs:
             _unpack_into(learners[a], med)
-    fed.record("aggregate", time.perf_counter() - t0)
 
 
 def aggregate_generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> Any:
     """Any aggregator: all-gather the trainers' wire models and reduce identically on every rank."""
+    return fed.run_aggregation(lambda: _generic(fed, arrived, aggregator))
+
+
+def _generic(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> Any:
     local_models = {a: p[1] for a, p in arrived.items() if p[1] is not None}
     everything: Dict[str, Any] = {}
     for part in fed.all_gather_object(local_models):

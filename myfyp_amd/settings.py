@@ -108,6 +108,15 @@ class Settings:
     # ranks > 0 ship their metrics to rank 0 live, every this many seconds (0 disables the relay)
     CENTRAL_LOG_PERIOD: float = 0.5
     SHM_CONTROL_PLANE: bool = True  # single-node jobs: control-plane gathers through shared memory
+    # a single-process job still runs its weight collectives through a world-size-1 RCCL group (the
+    # multi-rank code path on one GPU: profiling, tests); env MYFYP_FORCE_COLLECTIVE=1 does the same
+    FORCE_COLLECTIVE: bool = False
+    # failure-aware weight collectives (single-node shm control plane): liveness polled while
+    # waiting, watchdog abort, agreement on every collective, re-run over the survivors
+    COLLECTIVE_FAILOVER: bool = True
+    # CUs the fp32 MLP persistent epoch leaves to a concurrent RCCL kernel when collectives are
+    # active (co-residency: every workgroup of a gang must be resident at once)
+    RCCL_RESERVED_CUS: int = 32
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
     GIL_SWITCH_INTERVAL: float | None = 2e-4
@@ -190,6 +199,9 @@ class Settings:
             "DELAYED_AVERAGING": "DELAYED_AVERAGING",
             "CENTRAL_LOG_PERIOD": "CENTRAL_LOG_PERIOD",
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
+            "FORCE_COLLECTIVE": "FORCE_COLLECTIVE",
+            "COLLECTIVE_FAILOVER": "COLLECTIVE_FAILOVER",
+            "RCCL_RESERVED_CUS": "RCCL_RESERVED_CUS",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",
             "ROUND_DRIVER": "ROUND_DRIVER",

@@ -25,16 +25,19 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
     final = state.total_rounds is None or round_ + 1 >= state.total_rounds
 
     def leader(arrived):
+        device_path = kind in ("scaffold", "median") and _agree_device_path(f, kind, arrived)
+        if kind in ("scaffold", "median") and not device_path:
+            arrived = _with_wire_models(f, arrived)
         if kind == "mean":
             total, contributors = weights_plane.aggregate_mean(f, arrived, final=final)
             extra = getattr(aggregator, "proximal_mu", None)
         elif kind == "neighbor":
             weights_plane.aggregate_neighbors(f, arrived, aggregator)
             extra = None
-        elif kind == "scaffold" and all(p[1] is None for p in arrived.values()):
+        elif kind == "scaffold" and device_path:
             weights_plane.aggregate_scaffold(f, arrived, aggregator)
             extra = None
-        elif kind == "median" and all(p[1] is None for p in arrived.values()):
+        elif kind == "median" and device_path:
             weights_plane.aggregate_median(f, arrived)
             extra = None
         else:
@@ -49,6 +52,29 @@ def join_aggregation(state, learner, aggregator, trainer: bool) -> None:
         model.add_info("fedprox", {"mu": mu})
         learner.update_callbacks_with_model_info()
     model.set_contribution(list(state.train_set) or [state.addr], max(1, model.num_samples))
+
+
+def _agree_device_path(f, kind: str, arrived) -> bool:
+    """SCAFFOLD / FedMedian reduce on the device only when EVERY rank's peers are device learners
+    (flat parameter buffers): the ranks agree on it through one control-plane gather, so all of
+    them issue the same collectives (a rank whose local peers happen to be non-trainers cannot
+    tell from its own, empty, payloads)."""
+    local_ok = all(hasattr(f.local_nodes[a].learner, "flat_params") for a in arrived if a in f.local_nodes)
+    return all(f.all_gather_object(bool(local_ok)))
+
+
+def _with_wire_models(f, arrived):
+    """Generic path after the device path was voted down: local trainers that skipped building a
+    wire model (they expected the device path) build it now."""
+    out = {}
+    for a, p in arrived.items():
+        if p[0] and p[1] is None and a in f.local_nodes:
+            model = f.local_nodes[a].learner.get_model()
+            wire = model.build_copy(params=model.get_parameters(), num_samples=model.num_samples, contributors=list(model.contributors),
+                                    additional_info=dict(model.additional_info))
+            p = (p[0], wire)
+        out[a] = p
+    return out
 
 
 class WaitAggregatedModelsStage(Stage):

@@ -49,3 +49,35 @@ def test_three_ranks_one_process_crashes_survivors_evict_it():
         assert outs[r]["finished_rounds"] == 3 and outs[r]["members"] == [0, 1], outs[r]
         assert outs[r]["elapsed"] < 60, outs[r]
     assert abs(outs[0]["absmax"] - outs[1]["absmax"]) < 1e-6, outs
+
+
+@pytest.mark.slow
+def test_rank_dies_inside_the_all_reduce(tmp_path):
+    """Rank 2's process exits right before it issues round 1's FedAvg all-reduce — after the
+    pre-collective agreement, while ranks 0 and 1 are already inside the collective (VERDICT r2
+    item 3). The collective guard notices (closed connection / process gone), the survivors agree,
+    rebuild their groups and re-run the aggregation from their intact local rows: both finish every
+    round well inside COLLECTIVE_TIMEOUT, and round 1's result is the host FedAvg of the two
+    survivors' pre-aggregation rows (reference math: aggregator_test.py:68-113)."""
+    import numpy as np
+
+    env = dict(os.environ, ROUNDS="3", KILL_RANK="2", KILL_ROUND="1", FAILURE_TIMEOUT="20", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               OUT_DIR=str(tmp_path))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "collective_crash_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    outs = {}
+    for f in tmp_path.glob("rank*.json"):
+        o = json.loads(f.read_text())
+        outs[o["rank"]] = o
+    assert set(outs) == {0, 1}, res.stderr[-3000:]
+    for r in (0, 1):
+        o = outs[r]
+        assert o["finished_rounds"] == 3 and o["members"] == [0, 1], {k: v for k, v in o.items() if k != "trace"}
+        assert o["recoveries"] >= 1, o["recoveries"]
+        assert o["elapsed"] < 60, o["elapsed"]  # neither FAILURE_TIMEOUT (20 s) nor COLLECTIVE_TIMEOUT was waited out
+    t0, t1 = outs[0]["trace"]["1"], outs[1]["trace"]["1"]
+    expect = (np.array(t0["pre"]) * t0["w"] + np.array(t1["pre"]) * t1["w"]) / (t0["w"] + t1["w"])
+    for t in (t0, t1):
+        np.testing.assert_allclose(np.array(t["post"]), expect, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,59 @@
+"""The RCCL data plane on one MI355X. A single process runs every weight
+collective case twice — solo (single-rank fast paths: ``k_fedavg_local``, in-place median, no
+collective) and FORCED through a world-size-1 ``nccl`` (RCCL) process group
+(``MYFYP_FORCE_COLLECTIVE=1``): side-stream bucketed FedAvg (reduce kernel → RCCL all-reduce →
+apply kernel per bucket, several buckets), delayed averaging, the init-model broadcast, SCAFFOLD's
+all-reduce, FedMedian's all-gather, the group rebuild (``new_group`` + abort of the replaced RCCL
+communicator), on the fused fp32 MLP engine and the ResNet-18 CNN engine. The forced results must
+equal the solo ones: bit-equal for FedAvg / broadcast (same summation order, an identity
+all-reduce), 1e-6 for SCAFFOLD and the median. Each mode runs in its own process (started by
+subprocess from this test; never by exec from a GPU-initialised process)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(tmp_path, forced: bool):
+    out = str(tmp_path / f"out_{int(forced)}.pt")
+    env = dict(os.environ, MYFYP_FORCE_COLLECTIVE="1" if forced else "0", OUT=out, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("MASTER_PORT", None)
+    res = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "workers", "forced_collective_worker.py")], capture_output=True, text=True,
+                         timeout=420, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-5000:]
+    with open(out + ".json") as f:
+        info = json.load(f)
+    return torch.load(out, weights_only=True), info
+
+
+def test_forced_rccl_world1_matches_solo(tmp_path):
+    solo, info_s = _run(tmp_path, False)
+    forced, info_f = _run(tmp_path, True)
+    assert not info_s["forced"] and info_f["forced"]
+    assert info_f["backend"] == "nccl", info_f
+    for case, c in info_f["cases"].items():
+        assert not c["solo"], (case, c)  # every case took the multi-rank path
+    calls = info_f["cases"]
+    assert calls["mlp_fedavg"]["comm_calls"].get("all_reduce_async", 0) >= 3 * 2, calls["mlp_fedavg"]  # >= 2 buckets per round
+    assert calls["resnet_fedavg"]["comm_calls"].get("all_reduce_async", 0) >= 2, calls["resnet_fedavg"]
+    assert calls["init_broadcast"]["comm_calls"].get("broadcast", 0) >= 1
+    assert calls["median"]["comm_calls"].get("all_gather", 0) == 1
+    assert calls["scaffold"]["comm_calls"].get("all_reduce", 0) == 1
+    for case in ("init_broadcast", "mlp_fedavg", "mlp_delayed", "resnet_fedavg"):
+        a, b = solo[case], forced[case]
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b), f"{case}: max |solo - forced| = {(a - b).abs().max().item()}"
+    for case in ("scaffold", "median"):
+        torch.testing.assert_close(forced[case], solo[case], rtol=0, atol=1e-6)
+    # FedAvg peers agree with each other after the last round
+    for case in ("mlp_fedavg", "resnet_fedavg"):
+        f = forced[case]
+        assert (f - f[0]).abs().max().item() < 1e-6, case
