@@ -41,6 +41,13 @@ def parse():
     ap.add_argument("--delayed-averaging", action="store_true", help="opt-in delayed averaging (numerics change; last round exact)")
     ap.add_argument("--no-overlap", action="store_true", help="synchronous FedAvg (no side-stream bucket pipeline)")
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="all-reduce bucket size (0 = Settings.BUCKET_BYTES)")
+    # synthetic-data difficulty (so that time-to-accuracy measures something: the default CIFAR
+    # stand-in is learnt to ~100 % in one round by ResNet-18)
+    ap.add_argument("--similarity", type=float, default=0.9, help="class-prototype overlap")
+    ap.add_argument("--noise", type=float, default=1.5, help="per-pixel stroke noise")
+    ap.add_argument("--modes", type=int, default=8, help="prototypes per class")
+    ap.add_argument("--label-noise", type=float, default=0.2, help="fraction of training labels randomised")
+    ap.add_argument("--target-acc", type=float, default=0.8, help="time-to-accuracy target (mean test accuracy over the peers)")
     return ap.parse_args()
 
 
@@ -108,7 +115,7 @@ def main() -> None:
     fed = Federation.init()
     world, rank = fed.world, fed.rank
     ppr = args.peers // world
-    data = synthetic_cifar10(args.n_train, args.n_test, seed=7)
+    data = synthetic_cifar10(args.n_train, args.n_test, seed=7, similarity=args.similarity, noise=args.noise, modes=args.modes, label_noise=args.label_noise)
     if args.dirichlet > 0:
         parts = data.generate_partitions(args.peers, DirichletPartitionStrategy, alpha=args.dirichlet)
     else:
@@ -143,6 +150,14 @@ def main() -> None:
             marks["t1"] = time.perf_counter()
 
     fed.round_hooks.append(hook)
+    landed: dict = {}  # round -> [(acc, host time the evaluation landed)]
+    local_addrs = {n.addr for n in nodes}
+
+    def on_metric(addr, exp_name, rnd, metric, value, step):
+        if metric == "test_metric" and step is None and addr in local_addrs:
+            landed.setdefault(rnd, []).append((value, time.perf_counter()))
+
+    logger.add_metric_listener(on_metric)
     t_start = time.perf_counter()
     if args.warmup == 0:  # time from the start (includes graph capture)
         marks["t0"] = t_start
@@ -156,13 +171,24 @@ def main() -> None:
         el = float(t.item())
     logs = logger.get_global_logs().get("experiment", {})
     accs = [logs[n.addr]["test_metric"][-1][1] for n in nodes if logs.get(n.addr, {}).get("test_metric")]
+    # accuracy curve: test_metric logged at round r evaluates the model after round r - 1
+    by_round: dict = {}
+    for n in nodes:
+        for r, v in logs.get(n.addr, {}).get("test_metric", []):
+            by_round.setdefault(r, []).append(v)
+    curve = {r: float(np.mean(v)) for r, v in sorted(by_round.items())}
+    r_target = t_target = None
+    for r, a in curve.items():
+        if r >= 1 and a >= args.target_acc and r in landed:
+            r_target, t_target = r, max(t for _, t in landed[r]) - t_start
+            break
     tm = logger.get_timings().get(nodes[0].addr, {})
     brk = {k: round(1000 * float(np.median(v[args.warmup:] or v)), 2) for k, v in tm.items()}
     print(f"[bench_cnn] rank {rank} median ms per call: {json.dumps(brk)}", file=sys.stderr, flush=True)
-    step_ms_engine = None
-    if fused and "fit" in tm:
-        steps = (len(parts[gids[0]].column("label")) + B - 1) // B
-        step_ms_engine = round(1000 * float(np.median(tm["fit"][args.warmup:] or tm["fit"])) / steps, 3)
+    # grouped step time from the round time (the engine's fit only enqueues: its host time is not
+    # the device time any more)
+    steps = (len(parts[gids[0]].column("label")) + B - 1) // B
+    step_ms_engine = round(1000 * el / args.rounds / max(1, steps), 3) if fused else None
     for n in nodes:
         n.stop()
     out = {
@@ -174,7 +200,10 @@ def main() -> None:
         "dtype": "bf16" if fused else "fp32", "data": "synthetic CIFAR-10-shaped uint8", "local_batch": B,
         "partition": f"dirichlet({args.dirichlet})" if args.dirichlet else "iid", "dropout": args.dropout,
         "final_test_acc_mean": round(float(np.mean(accs)), 4) if accs else None,
-        "engine_ms_per_grouped_step": step_ms_engine,
+        "acc_curve": {int(r): round(a, 4) for r, a in curve.items()},
+        "target_acc": args.target_acc, "rounds_to_target": r_target, "time_to_target_s": None if t_target is None else round(t_target, 3),
+        "data_difficulty": {"similarity": args.similarity, "noise": args.noise, "modes": args.modes, "label_noise": args.label_noise},
+        "round_ms_per_local_step": step_ms_engine,
         "collective": ("delayed-averaging" if args.delayed_averaging else ("synchronous" if args.no_overlap else "side-stream-bucketed"))
         + f", bucket {Settings.BUCKET_BYTES >> 20} MiB",
     }

@@ -35,6 +35,7 @@ import torch
 
 from myfyp_amd.ops import _native
 from myfyp_amd.parallel.mlp_engine import _Gang
+from myfyp_amd.parallel.pending import Resolver
 from myfyp_amd.settings import Settings
 
 c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
@@ -212,6 +213,7 @@ class CNNGroup:
         self.B = batch_size
         self.arch = arch_of(template)
         self.lock = threading.RLock()
+        self.resolver: Optional[Resolver] = None  # created on first use (device result copies)
         self.handles: Dict[int, "CNNEngineHandle"] = {}
         self.capacity = 0
         self.extras: Dict[str, torch.Tensor] = {}
@@ -909,12 +911,12 @@ class CNNGroup:
                 opt["cg"], opt["cl"] = cg, cl
             self._opt = opt
             # inactive slots must not train: zero their sample count for this fit
-            n_active = torch.tensor([self.n_train[s] if s in batch else 0 for s in range(self.capacity)], dtype=torch.int32, device=self.device)
-            self.tab["n"].copy_(n_active)
+            n_host = [self.n_train[s] if s in batch else 0 for s in range(self.capacity)]
+            self._h2d(self.tab["n"], n_host)
             self.mom.zero_()
             self._shadow_sync()
             self.stat.zero_()
-            steps = (max(n_active.tolist()) + self.B - 1) // self.B
+            steps = (max(n_host) + self.B - 1) // self.B  # host copy: no device round trip
             key = ("fit", steps, tuple(sorted(opt)), opt.get("kind"))
             for ep in range(epochs):
                 if self.perm_fn is not None:
@@ -924,13 +926,38 @@ class CNNGroup:
                     keys.masked_fill_(self._perm_mask, 2.0)
                     self.perm.copy_(torch.argsort(keys, dim=1).to(torch.int32))
                 self._run_steps(key, steps, lambda: [self._train_step(t * self.B) for t in range(steps)], scalars=opt)
-            stat = self.stat.view(self.capacity, 4).cpu().numpy()
-            self.tab["n"].copy_(torch.tensor(self.n_train, dtype=torch.int32, device=self.device))
+            raw = self._d2h_async(self.stat.view(self.capacity, 4))
+            self._h2d(self.tab["n"], list(self.n_train))
+        # results resolve off-thread when the pinned copy lands (the round never waits for the GPU)
         out = {}
         for slot in batch:
             n = max(1, self.n_train[slot] * epochs)
-            out[slot] = (int((self.n_train[slot] + self.B - 1) // self.B) * epochs, float(stat[slot, 0]) / n, float(stat[slot, 1]) / n)
+            out[slot] = (int((self.n_train[slot] + self.B - 1) // self.B) * epochs,
+                         raw.map(lambda r, s=slot, n=n: (float(r[0][s, 0]) / n, float(r[0][s, 1]) / n)))
         return out
+
+    def _h2d(self, dst: torch.Tensor, values) -> None:
+        """Stream-ordered upload of a small host list (pinned staging; the caching host allocator
+        keeps the buffer alive until the copy ran)."""
+        src = torch.tensor(values, dtype=dst.dtype, pin_memory=True)
+        dst.copy_(src, non_blocking=True)
+
+    def _d2h_async(self, *tensors: torch.Tensor):
+        """Pinned device→host copies of ``tensors`` on the current stream and a Pending of their
+        numpy views, completed by the resolver thread once the copies landed."""
+        if self.resolver is None:
+            self.resolver = Resolver(f"cnn-results-{self.device}")
+        hosts = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in tensors]
+        for h, t in zip(hosts, tensors):
+            h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+
+        def fetch():
+            ev.synchronize()
+            return [h.numpy() for h in hosts]
+
+        return self.resolver.submit(fetch)
 
     def _run_steps(self, key, steps: int, body, scalars: Optional[dict] = None) -> None:
         """Run ``body`` (a whole epoch of steps). The first run of a key is eager (it allocates every
@@ -978,10 +1005,9 @@ class CNNGroup:
             self.stat.zero_()
             self.conf.zero_()
             self._eval_all()
-            stat = self.stat.view(self.capacity, 4).cpu().numpy()
-            conf = self.conf.view(self.capacity, 16, 16).cpu().numpy()
+            raw = self._d2h_async(self.stat.view(self.capacity, 4), self.conf.view(self.capacity, 16, 16))
         K = self.n_classes
-        return {slot: (float(stat[slot, 0]) / max(1, self.n_test[slot]), conf[slot, :K, :K].copy()) for slot in batch}
+        return {slot: raw.map(lambda r, s=slot: (float(r[0][s, 0]) / max(1, self.n_test[s]), r[1][s, :K, :K].copy())) for slot in batch}
 
     def expect(self, fit_slots: Optional[Set[int]] = None, eval_slots: Optional[Set[int]] = None) -> None:
         self.fit_gang.expected = fit_slots
@@ -1070,9 +1096,9 @@ class CNNEngineHandle:
 
     def fit(self, learner, spec: dict, extra: dict) -> Tuple[int, float]:
         self._sync_data(learner)
-        steps, loss, _acc = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
+        steps, raw = self.group.fit_gang.submit(self.slot, (spec, learner.epochs, extra), self.group.default_expected())
         learner.global_step += steps
-        return steps, loss
+        return steps, raw.map(lambda v: v[0])
 
     def evaluate(self, learner) -> Tuple[float, np.ndarray]:
         self._sync_data(learner)

@@ -277,9 +277,10 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
             total_w = _generic_mean(fed, addrs, learners, weights, final, bool(Settings.DELAYED_AVERAGING))
         return total_w, contributors
 
+    # the side-stream pipeline's all-reduces stay unconfirmed until the next weights section (or
+    # shutdown): by then the next local epoch is already queued behind them, so the host's wait for
+    # them never leaves the GPU idle (see Federation.confirm_collectives)
     total_w, contributors = fed.run_aggregation(run)
-    if not fed.async_confirm:  # nobody confirms at the next round top: confirm the device pipeline now
-        fed.confirm_collectives()
     fed.record("aggregate", time.perf_counter() - t0)
     return total_w, contributors
 

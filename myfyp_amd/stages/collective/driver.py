@@ -80,14 +80,12 @@ class RoundDriver:
         while not m.done.is_set():
             if self._claim():
                 members = dict(self.members)
-                self.f.async_confirm = True
                 try:
                     self._drive(members)
                 except BaseException as e:  # surfaced in every peer's learning thread
                     for mm in members.values():
                         mm.error = e
                 finally:
-                    self.f.async_confirm = False
                     for mm in members.values():
                         mm.done.set()
                     with self.lock:
@@ -118,9 +116,6 @@ class RoundDriver:
             cur = live()
             if not cur:
                 return
-            # the previous round's device collective is confirmed (every member completed it, or
-            # it is re-run over the survivors) before this round's evaluation / epoch read the rows
-            f.confirm_collectives()
             t0 = time.time()
             mark("driver_round")
             states = {a: m.kw["state"] for a, m in cur.items()}
@@ -203,7 +198,7 @@ class RoundDriver:
         from myfyp_amd.stages.collective._common import set_gang_expectations
 
         set_gang_expectations(self.f, set(), None)
-        self.f.confirm_collectives()
+        self.f.confirm_collectives()  # the last round's all-reduce, before the final evaluation reads the rows
         pend = {}
         first = next(iter(done.values())).kw["learner"]
         group = first._engine.group

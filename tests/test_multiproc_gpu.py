@@ -27,3 +27,6 @@ def test_two_ranks_fused_engine_cross_rank_fedavg(precision):
     assert out["world"] == 2 and out["peers"] == 4 and out["fused"], out
     assert out["max_diff"] < 1e-6, out  # every peer holds the same FedAvg model after the last round
     assert out["moved"] > 1e-3, out  # and it trained
+    # the last round's aggregate is the host float64 sample-weighted mean of the 4 trained rows
+    assert out["n_pre"] == 4 and out["wsum"] > 0, out
+    assert out["fedavg_err"] <= 1e-6 * max(1.0, out["fedavg_scale"]), out

@@ -44,6 +44,7 @@ def test_forced_rccl_world1_matches_solo(tmp_path):
     calls = info_f["cases"]
     assert calls["mlp_fedavg"]["comm_calls"].get("all_reduce_async", 0) >= 3 * 2, calls["mlp_fedavg"]  # >= 2 buckets per round
     assert calls["resnet_fedavg"]["comm_calls"].get("all_reduce_async", 0) >= 2, calls["resnet_fedavg"]
+    assert calls["resnet_train"]["comm_calls"].get("all_reduce_async", 0) >= 2, calls["resnet_train"]
     assert calls["init_broadcast"]["comm_calls"].get("broadcast", 0) >= 1
     assert calls["median"]["comm_calls"].get("all_gather", 0) == 1
     assert calls["scaffold"]["comm_calls"].get("all_reduce", 0) == 1
@@ -53,7 +54,12 @@ def test_forced_rccl_world1_matches_solo(tmp_path):
         assert torch.equal(a, b), f"{case}: max |solo - forced| = {(a - b).abs().max().item()}"
     for case in ("scaffold", "median"):
         torch.testing.assert_close(forced[case], solo[case], rtol=0, atol=1e-6)
-    # FedAvg peers agree with each other after the last round
-    for case in ("mlp_fedavg", "resnet_fedavg"):
-        f = forced[case]
-        assert (f - f[0]).abs().max().item() < 1e-6, case
+    # FedAvg peers agree with each other after the last round; ResNet training (not bit-reproducible
+    # run to run: atomics in the BN-backward sums) only has to agree within each run
+    for case in ("mlp_fedavg", "resnet_train"):
+        for res in (solo, forced):
+            f = res[case]
+            assert torch.isfinite(f).all() and (f - f[0]).abs().max().item() < 1e-6, case
+    # the weight-0 peer also receives the average (masked apply over every local row)
+    f = forced["resnet_fedavg"]
+    assert (f - f[0]).abs().max().item() == 0.0

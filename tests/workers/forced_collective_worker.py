@@ -101,9 +101,37 @@ def case_mlp_delayed(fed):
         Settings.DELAYED_AVERAGING = False
 
 
-def case_resnet_fedavg(fed):
+def case_resnet_train(fed):
+    """Two rounds of ResNet-18 training + FedAvg through the pipeline (training itself is not
+    bit-reproducible run to run: BN-backward sums use atomics, so only the peers' agreement is
+    compared)."""
     Settings.TRAIN_SET_SIZE = 2
-    return _experiment(fed, "resnet_fedavg", lambda i: ResNet18(seed=40 + i), synthetic_cifar10(256, 64, seed=3), 2, 2, 32)
+    return _experiment(fed, "resnet_train", lambda i: ResNet18(seed=40 + i), synthetic_cifar10(256, 64, seed=3), 2, 2, 32)
+
+
+def case_resnet_fedavg(fed):
+    """FedAvg of ResNet-18 engine rows (parameters + BN running statistics) set to seeded values:
+    bucketed side-stream pipeline (forced) vs the one-launch local mean (solo)."""
+    data = synthetic_cifar10(64, 16, seed=3)
+    nodes = [Node(TorchModel(ResNet18(seed=50 + i)), data, address=f"rf-{i}", aggregator=FedAvg(), protocol=CollectiveCommunicationProtocol,
+                  learner_kwargs={"batch_size": 32}) for i in range(3)]
+    try:
+        for nd in nodes:
+            nd.start()
+        fed.finalize()
+        g = torch.Generator().manual_seed(17)
+        with torch.no_grad():
+            for nd in nodes:
+                for t in weights_plane.state_tensors(nd.learner):
+                    t.copy_(torch.randn(t.shape, generator=g).to(t.dtype))
+        weights_plane.aggregate_mean(fed, {nd.addr: (w, None) for nd, w in zip(nodes, [3.0, 0.0, 5.0])}, final=True)
+        fed.confirm_collectives()
+        _sync()
+        _record(fed, "resnet_fedavg")
+        return _flats(nodes)
+    finally:
+        for nd in nodes:
+            nd.stop()
 
 
 def _direct_nodes(make_agg, k, tag):
@@ -185,6 +213,7 @@ CASES = {
     "scaffold": case_scaffold,
     "median": case_median,
     "resnet_fedavg": case_resnet_fedavg,
+    "resnet_train": case_resnet_train,
 }
 
 
@@ -192,7 +221,7 @@ def main() -> None:
     assert CPU or torch.cuda.is_available()
     if CPU:
         Settings.DEVICE = "cpu"
-        del CASES["resnet_fedavg"]
+        del CASES["resnet_fedavg"], CASES["resnet_train"]
     logger.set_level("WARNING")
     Settings.LOG_LEVEL = "WARNING"
     Settings.GANG_WINDOW = 5.0
