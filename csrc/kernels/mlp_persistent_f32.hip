@@ -63,9 +63,17 @@ using persist::st_wt128;
 using persist::st_wt32;
 
 constexpr int NT = 512;  // threads per workgroup (8 waves)
-#ifndef P32_EXP_FUSE_FWD
-#define P32_EXP_FUSE_FWD 0  // experiment: next step's forward accumulated inside C2 — measured 16.8 us/step vs 15.7 (C2 4.6 -> 6.6 us, 14 more VGPR spills), not kept
+// A/B switches for timing builds (build variant "stamps+P32_BALANCE=0" etc.): the LDS-resident K
+// step shared out over the waves (1) or carried whole by wave 0 (0); running f64 Adam bias
+// corrections (1) or two fp32 pow() per step (0)
+#ifndef P32_BALANCE
+#define P32_BALANCE 0  // measured: 489-492 vs 492-497 rounds/s (profiles/r3d_mlp_ab), not kept on
 #endif
+#ifndef P32_RUNNING_BC
+#define P32_RUNNING_BC 1
+#endif
+// (measured and not kept: the next step's forward accumulated inside C2 — 16.8 us/step vs 15.7,
+// C2 4.6 -> 6.6 us and 14 more VGPR spills)
 constexpr int NCG = 16;  // W1 column groups per peer (D1 / 16)
 constexpr int NH = 8;    // heads per peer (D2 / 16)
 constexpr int KSMAX = 2;
@@ -354,7 +362,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 
   // deferred W2-replica update of step tp: dW2[o2][16g + c] over the batch, with dH2(tp) re-read
   // (sc1) from the step-parity buffer and H1(tp) from this workgroup's LDS
-  auto w2_replica_update = [&](int tp) {
+  auto w2_replica_update = [&](int tp, float lr_p, float inv_p) {
     const float* dh2 = pb.dh2x + ((int64_t)p * 2 + (tp & 1)) * BP * PD2;
     const float* h1p = sH1 + (tp & 1) * BP * 16;
     float av[BP / 4];
@@ -363,16 +371,17 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     f32x4 acc = zero4();
 #pragma unroll
     for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(av[kb], h1p[(4 * kb + h) * 16 + c], acc);
-    float lr_p, inv_p;
-    persist::bias_corr(o, ctl.z, tp, lr_p, inv_p);
 #pragma unroll
     for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, acc[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_p, inv_p, wdmu);
   };
   // forward contribution of this wave's K step q (slot q) to the H1 slice, with the weights as they
-  // are now and the batch tile currently staged in LDS
+  // are now and the batch tile currently staged in LDS. The LDS-resident K step (q == RQ, KS = 1:
+  // K step 24, D0 > 767) is shared out by batch tile: wave w < MT adds only tile mt = w, so no wave
+  // carries a fourth whole K step (it made wave 0 the critical path of the forward).
   auto fwd_kstep = [&](int q, f32x4(&acc)[MT]) {
-    const int s = wave + 8 * q;
-    if (s >= KS1) return;
+    const bool lds_step = P32_BALANCE && KS == 1 && q == RQ;
+    const int s = lds_step ? 8 * RQ : wave + 8 * q;
+    if (s >= KS1 || (lds_step && wave >= MT)) return;
     // lane coordinates laundered per K step: the compiler would otherwise hoist every LDS address
     // of the loop out of it and spill them
     int lq = lane;
@@ -385,6 +394,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     split3(wq, bh, bm, bl);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+      if (lds_step && mt != wave) continue;  // wave-uniform
       const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * hq;
       const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
       acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
@@ -392,19 +402,24 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   };
   __syncthreads();  // sW1x written
 
+  persist::BiasCorr bc;
+  bc.init(o, ctl.z);
+  float lr_t = 0.f, inv_bc2 = 0.f;
   for (int t = 0; t < nsteps; ++t) {
     int tv = tid;  // per-iteration opaque thread index (addresses re-derived each step: VGPR pressure)
     asm volatile("" : "+v"(tv));
     const int rows = rows_at(a, n, t);
-    float lr_t, inv_bc2;
+    const float lr_prev = lr_t, inv_prev = inv_bc2;  // step t - 1 (the deferred W2-replica update)
+#if P32_RUNNING_BC
+    bc.next(o, lr_t, inv_bc2);
+#else
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
+#endif
     float* sH1c = sH1 + (t & 1) * BP * 16;
     if (g == 0) P32_STAMP(0, t, 0);
 
     // ================= A: H1 slice = relu(X · W1sliceᵀ + b1), split-K over the 8 waves
-    // (P32_EXP_FUSE_FWD, t > 0: each wave's partials were accumulated in sRed during the previous
-    // step's C2, right after its K steps' W1 update and the staging of this batch's columns)
-    if (!P32_EXP_FUSE_FWD || t == 0) {
+    {
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
@@ -436,7 +451,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (g == 0) P32_STAMP(0, t, 2);
 
     // the previous step's W2-replica update runs while the heads work on this step's H1
-    if (t > 0) w2_replica_update(t - 1);
+    if (t > 0) w2_replica_update(t - 1, lr_prev, inv_prev);
     if (g == 0) P32_STAMP(0, t, 3);
 
     // next step's batch: pull this wave's columns into the XCD's L2 (staged after the dW1 MFMAs)
@@ -541,13 +556,24 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       const bf16* xnext = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
 #pragma unroll
       for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
-        const int s = wave + 8 * q;
+        // register K steps: wave w owns K step w + 8q, both 16-column halves (tt = 0, 1). The
+        // LDS-resident K step (q == RQ, KS = 1) is shared out by half: wave NW-2 takes tt = 0
+        // (columns 768..783), wave NW-1 tt = 1 (the bias column and padding) — each reads, updates
+        // and restages only its own half of the tile, so the halves never race.
+        const bool lds_step = P32_BALANCE && KS == 1 && q == RQ;
+        constexpr int NW = NT / 64;
+        const int s = lds_step ? 8 * RQ : wave + 8 * q;
+        const int tt_lo = lds_step ? wave - (NW - 2) : 0;
+        const int tt_hi = lds_step ? tt_lo + 1 : 2;
         __builtin_amdgcn_sched_barrier(0);
-        if (s < KS1) {
+        if (s < KS1 && tt_lo >= 0) {
           int lq = lane;
           asm volatile("" : "+v"(lq));
           const bf16* dfrag = sD3 + (lq & 15) * LDT + 8 * (lq >> 4);
           constexpr int XQ = BP / 16;
+          // this lane's 16-byte chunks of the K step: chunk (lv & 3) of a row covers columns
+          // 32s + 8(lv & 3) .. +8, i.e. half tt = (lv & 3) >> 1
+          const bool xmine = !lds_step || ((lv & 3) >> 1) == tt_lo;
           uint4 xq[XQ];
 #pragma unroll
           for (int kk = 0; kk < XQ; ++kk) {
@@ -556,11 +582,12 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #ifdef P32_EXP_NOX  // timing experiment: no next-batch staging loads
             xq[kk] = uint4{(unsigned)lv, 0u, 0u, 0u};
 #else
-            xq[kk] = (more && gcol < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + gcol)) : uint4{0u, 0u, 0u, 0u};
+            xq[kk] = (more && xmine && gcol < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + gcol)) : uint4{0u, 0u, 0u, 0u};
 #endif
           }
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt) {
+            if (tt < tt_lo || tt >= tt_hi) continue;  // wave-uniform
             f32x4 acc = zero4();  // C[k = 32s + 16tt + 4h + i][o1 = c]
 #pragma unroll
             for (int kb = 0; kb < BP / 32; ++kb)
@@ -594,27 +621,13 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
             for (int kk = 0; kk < XQ; ++kk) {
               const int idx = kk * 64 + lv;
               const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
+              if (!xmine) continue;
               if (gcol < D0)
                 *reinterpret_cast<uint4*>(sX + r * LDX + col) = xq[kk];
               else if (gcol == D0)
                 *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows_next);
             }
           }
-          if (P32_EXP_FUSE_FWD && more) {
-            // next step's forward partial of this K step: its W1 columns are final for step t + 1
-            // and the batch columns were just staged by this wave (LDS is in order within a wave;
-            // the wait + memory clobber keeps the compiler from hoisting the reads above the writes)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            f32x4 accn[MT];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) accn[mt] = q == 0 ? zero4() : sRed[(wave * MT + mt) * 64 + lane];
-            fwd_kstep(q, accn);
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = accn[mt];
-          }
-        } else if (P32_EXP_FUSE_FWD && more && q == 0) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = zero4();
         }
       }
     }
@@ -622,16 +635,20 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (g == 0) P32_STAMP(0, t, 6);
   }
 
-  // ---- write the state back (fp32 master weights and moments; b1 from the bias slot)
-  int orow_w = orow;
+  // ---- write the state back (fp32 master weights and moments; b1 from the bias slot). Every
+  //      address is re-derived from laundered lane / row indices: the compiler would otherwise keep
+  //      the prologue's 64-bit load addresses alive across the whole epoch (VGPR spills)
+  int lw = lane;
   int64_t pS_w = pS;
-  asm volatile("" : "+v"(orow_w), "+s"(pS_w));
+  asm volatile("" : "+v"(lw), "+s"(pS_w));
+  const int hw = lw >> 4, cw = lw & 15;
+  const int orow_w = NCG * cg + cw;
 #pragma unroll
   for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
     const int s = wave + 8 * q;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const int k = C0 + 32 * s + 16 * half + 4 * h;  // global W1 column
+      const int k = C0 + 32 * s + 16 * half + 4 * hw;  // global W1 column
       if (s >= KS1 || k > D0) continue;
       float4 w, m, v;
       if (q < RQ) {
@@ -641,7 +658,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         m = float4{m1[qq][j0], m1[qq][j0 + 1], m1[qq][j0 + 2], m1[qq][j0 + 3]};
         v = float4{v1[qq][j0], v1[qq][j0 + 1], v1[qq][j0 + 2], v1[qq][j0 + 3]};
       } else {
-        const int off = c * 32 + 16 * half + 4 * h;
+        const int off = cw * 32 + 16 * half + 4 * hw;
         w = *reinterpret_cast<float4*>(sW1x + off);
         m = *reinterpret_cast<float4*>(sW1x + 512 + off);
         v = *reinterpret_cast<float4*>(sW1x + 1024 + off);
@@ -660,7 +677,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     }
   }
   if (pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
-    if (nsteps > 0) w2_replica_update(nsteps - 1);
+    if (nsteps > 0) w2_replica_update(nsteps - 1, lr_t, inv_bc2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NCG * cg + c] = w2c[i];
   }
@@ -752,12 +769,18 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
   __syncthreads();
   float loss_acc = 0.f, correct_acc = 0.f;
 
+  persist::BiasCorr bc;
+  bc.init(o, ctl.z);
   for (int t = 0; t < nsteps; ++t) {
     int tv = tid;
     asm volatile("" : "+v"(tv));
     const int rows = rows_at(a, n, t);
     float lr_t, inv_bc2;
+#if P32_RUNNING_BC
+    bc.next(o, lr_t, inv_bc2);
+#else
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
+#endif
 
     // labels of this lane's softmax rows, loaded before the waits (off the critical path)
     int yv[4] = {-1, -1, -1, -1};

@@ -224,12 +224,71 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0, noise_floo
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 def test_lenet_train_step_matches_torch(fused, monkeypatch):
-    """fused = the one-kernel LeNet step (lenet_fused.hip); 0 = the layer-by-layer conv kernels."""
+    """fused = the one-kernel LeNet step (lenet_fused.hip); 0 = the layer-by-layer conv kernels.
+    Tolerance: the bf16 noise floor (torch's own bf16-autocast step vs fp32), not a fixed bound."""
     from myfyp_amd.models import LeNet5
 
     monkeypatch.setenv("MYFYP_LENET_FUSED", fused)
-    learners, _ = _run_one_step(lambda i: LeNet5(seed=10 + i), n_peers=2, batch=32, lr=0.05, momentum=0.9)
+    learners, _ = _run_one_step(lambda i: LeNet5(seed=10 + i), n_peers=2, batch=32, lr=0.05, momentum=0.9, noise_floor=True)
     assert learners[0]._engine.group.lenet_fused == (fused == "1")
+
+
+def _torch_fit(ref, batches, lr, momentum, wd, bf16):
+    """One fit of the reference: a FRESH torch.optim.SGD (the engine also starts every fit with zero
+    momentum), one step per batch in order; returns the mean training loss."""
+    ref.train()
+    opt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=momentum, weight_decay=wd)
+    losses = []
+    for x, y in batches:
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            loss = F.cross_entropy(ref(x).float(), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    return sum(losses) / len(losses)
+
+
+def test_resnet_trajectory_matches_torch_within_bf16_floor():
+    """ResNet-18 over 20 local steps (4 fits of 5 steps: momentum, weight decay, BN running
+    statistics carried across fits) on the grouped engine vs torch fp32 and torch bf16 autocast on
+    the same batches in the same order. The engine's per-fit mean loss (the loss curve) and its final
+    per-tensor parameter deltas must stay within the bf16 noise floor that torch's own autocast run
+    shows against fp32 (one step only was pinned before)."""
+    from myfyp_amd.models import ResNet18
+
+    steps, fits, batch, lr, mom, wd = 5, 4, 16, 0.05, 0.9, 5e-4
+    learners, refs, _ = _make_learners(lambda i: ResNet18(seed=80 + i), 1, steps * batch, 16, batch, lr, mom, wd)
+    lr_ = learners[0]
+    g = lr_._engine.group
+    g.perm_fn = lambda ep: torch.arange(g.nmax, dtype=torch.int32, device="cuda").unsqueeze(0).repeat(g.capacity, 1)
+    x, y = lr_.device_data(True)
+    batches = [(x[i * batch:(i + 1) * batch], y[i * batch:(i + 1) * batch]) for i in range(steps)]
+    r32, r16 = refs[0], ResNet18(seed=80).cuda()
+    p0 = {n: p.detach().clone() for n, p in r32.named_parameters()}
+    from myfyp_amd.parallel.pending import resolve
+
+    curve = {"engine": [], "fp32": [], "bf16": []}
+    for f in range(fits):
+        n_steps, loss = lr_._engine.fit(lr_, lr_._optimizer_spec(), {})
+        assert n_steps == steps
+        curve["engine"].append(float(resolve(loss)))  # the engine's mean training loss of this fit
+        curve["fp32"].append(_torch_fit(r32, batches, lr, mom, wd, False))
+        curve["bf16"].append(_torch_fit(r16, batches, lr, mom, wd, True))
+    for f in range(fits):
+        floor = abs(curve["bf16"][f] - curve["fp32"][f])
+        assert abs(curve["engine"][f] - curve["fp32"][f]) <= max(0.03 * curve["fp32"][f], 3 * floor), (f, curve)
+    assert curve["engine"][-1] < curve["engine"][0], curve  # it learns
+    eng = dict(lr_.model.get_model().named_parameters())
+    for name, p in r32.named_parameters():
+        d32 = (p.detach() - p0[name]).flatten()
+        if d32.norm() < 1e-8:
+            continue
+        d16 = (dict(r16.named_parameters())[name].detach() - p0[name]).flatten()
+        de = (eng[name].detach() - p0[name]).flatten()
+        rel16 = float((d16 - d32).norm() / d32.norm())
+        rel = float((de - d32).norm() / d32.norm())
+        assert rel < max(0.1, 2.0 * rel16), (name, rel, rel16)
 
 
 class _FixedCorrection:
