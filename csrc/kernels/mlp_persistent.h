@@ -26,8 +26,9 @@ hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& p
 //      gangs of 16 owners + 8 heads, one launch per group of 8 peers.
 struct MLPPersistF32Bufs {
   float* h1x;       // [P][Bpad][256]      owner g -> heads: H1 columns 16g..16g+15
-  float* plx;       // [P][8][Bpad][16]    head hd -> heads: partial logits over its H2 slice
-  float* dh2x;      // [P][2][Bpad][128]   head hd -> owners: dH2 columns 16hd..16hd+15 (step parity)
+  float* plx;       // [P][8][Bpad*16][2]  head hd -> heads: partial logits over its H2 slice, LL (value, tag) pairs
+  float* dh2x;      // [P][2][Bpad][128][2] head hd -> owners: dH2 columns 16hd..16hd+15 (step parity), LL pairs
+  unsigned* gen;    // [P] epoch generation of the LL tags (advanced by every completed epoch)
   unsigned* flags;  // [P][32][32] one 128-B line per flag (16 H1, 8 PL, 8 dH2); zeroed per launch
   size_t flag_bytes;
   int* err;         // give-up words: [0,64) per peer first attempt (1 gave up, 2 recovered), [64,128) retry

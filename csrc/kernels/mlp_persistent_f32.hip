@@ -28,10 +28,11 @@
 // f32 MFMA chain over the batch as the head's, and the same optimizer code: it stays bit-identical
 // to the head's rows with no W2 traffic at all (checked by a GPU test through `w2chk`).
 //
-// Per step three hand-offs, all write-through (sc1) stores + drained flag + sc1 loads
-// (persist_common.h): H1 slices owners → heads (16 × 4 KB), partial logits head ↔ head (8 × 4 KB),
-// dH2 slices heads → owners (8 × 4 KB, double-buffered by step parity because the owners re-read
-// the previous step's tile for their deferred W2-replica update).
+// Per step three hand-offs (persist_common.h): H1 slices owners → heads (16 × 4 KB; write-through
+// stores + drained flag + sc1 loads), partial logits head ↔ head (8 × 4 KB) and dH2 slices heads →
+// owners (8 × 4 KB, double-buffered by step parity because the owners re-read the previous step's
+// tile for their deferred W2-replica update) — the last two as LL (value, tag) pairs: no producer
+// drain, workgroup meet or flag store, the consumer's data load is its readiness check.
 #include "mlp_persistent.h"
 #include "persist_common.h"
 
@@ -72,6 +73,17 @@ constexpr int NT = 512;  // threads per workgroup (8 waves)
 #ifndef P32_RUNNING_BC
 #define P32_RUNNING_BC 1
 #endif
+// LL (value, tag) hand-offs (1) or write-through stores + drained flag (0), per hand-off
+#ifndef P32_LL_H1
+#define P32_LL_H1 0
+#endif
+#ifndef P32_LL_PL
+#define P32_LL_PL 0
+#endif
+#ifndef P32_LL_DH2
+#define P32_LL_DH2 0
+#endif
+constexpr int H1W = P32_LL_H1 ? 2 : 1;  // floats per H1 exchange element (value, tag)
 // (measured and not kept: the next step's forward accumulated inside C2 — 16.8 us/step vs 15.7,
 // C2 4.6 -> 6.6 us and 14 more VGPR spills)
 constexpr int NCG = 16;  // W1 column groups per peer (D1 / 16)
@@ -176,7 +188,7 @@ __device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, flo
 // already publish step t + 1's; it cannot reach step t + 2 before every owner has published t + 1
 // (the heads' dH2(t + 1) waits for all of them), so two buffers suffice.
 __device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, int kh, int t, int BP) {
-  return pb.h1x + (((int64_t)p * KSMAX + kh) * 2 + (t & 1)) * BP * PD1;
+  return pb.h1x + (((int64_t)p * KSMAX + kh) * 2 + (t & 1)) * BP * PD1 * H1W;
 }
 
 __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
@@ -239,7 +251,7 @@ __host__ __device__ inline HeadLds32 head_lds32(int Bpad) {
 __host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : 2; }
 
 template <int BP, bool ADAM, bool EXTRA, int KS>
-__device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem) {
+__device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem, unsigned gen) {
   constexpr int MT = BP / 16;
   constexpr int RQ = rq_of(KS);
   constexpr int XPT = BP / 4;  // 16-byte X chunks per lane: 4 K steps x BP rows x 4 chunks / 64 lanes
@@ -363,11 +375,17 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   // deferred W2-replica update of step tp: dW2[o2][16g + c] over the batch, with dH2(tp) re-read
   // (sc1) from the step-parity buffer and H1(tp) from this workgroup's LDS
   auto w2_replica_update = [&](int tp, float lr_p, float inv_p) {
-    const float* dh2 = pb.dh2x + ((int64_t)p * 2 + (tp & 1)) * BP * PD2;
+    // dH2(tp): LL pairs, verified at step tp; read through a buffer resource with 32-bit offsets from
+    // a laundered lane (64-bit per-kb addresses hoisted out of the step loop would be spilled)
+    constexpr int DW = P32_LL_DH2 ? 2 : 1;  // floats per dH2 exchange element
+    const __amdgpu_buffer_rsrc_t rd = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (tp & 1)) * BP * PD2 * 2, BP * PD2 * 8);
+    int lr = lane;
+    asm volatile("" : "+v"(lr));
+    const int ro = 4 * DW * ((lr >> 4) * PD2 + 16 * wave + (lr & 15));
     const float* h1p = sH1 + (tp & 1) * BP * 16;
     float av[BP / 4];
 #pragma unroll
-    for (int kb = 0; kb < BP / 4; ++kb) av[kb] = ld_wt32(dh2 + (4 * kb + h) * PD2 + 16 * wave + c);
+    for (int kb = 0; kb < BP / 4; ++kb) av[kb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ro + 4 * DW * 4 * kb * PD2, 0, 16));
     f32x4 acc = zero4();
 #pragma unroll
     for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(av[kb], h1p[(4 * kb + h) * 16 + c], acc);
@@ -400,6 +418,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
     }
   };
+  if (tid == 0) sOk[1] = 1;  // LL bulk-load verdict (0: a wave gave up)
   __syncthreads();  // sW1x written
 
   persist::BiasCorr bc;
@@ -410,6 +429,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     asm volatile("" : "+v"(tv));
     const int rows = rows_at(a, n, t);
     const float lr_prev = lr_t, inv_prev = inv_bc2;  // step t - 1 (the deferred W2-replica update)
+    const unsigned tag = persist::ll_tag(gen, pb.fbase, t);
 #if P32_RUNNING_BC
     bc.next(o, lr_t, inv_bc2);
 #else
@@ -443,11 +463,17 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         // b1 came in through the bias column; KS > 1: a partial sum (relu after the kh-ordered sum)
         const float v = b < rows ? (KS == 1 ? fmaxf(s[i], 0.f) : s[i]) : 0.f;
         sH1c[b * 16 + cc] = v;
+#if P32_LL_H1
+        persist::ll_st1(h1x_part(pb, p, kh, t, BP) + 2 * ((int64_t)b * PD1 + NCG * cg + cc), v, tag);
+#else
         st_wt32(h1x_part(pb, p, kh, t, BP) + (int64_t)b * PD1 + NCG * cg + cc, v);
+#endif
       }
     }
     if (g == 0) P32_STAMP(0, t, 1);
+#if !P32_LL_H1
     persist::publish(pb.flags, FPP, p, F_H1 + g, pb.fbase + (unsigned)(t + 1));
+#endif
     if (g == 0) P32_STAMP(0, t, 2);
 
     // the previous step's W2-replica update runs while the heads work on this step's H1
@@ -470,7 +496,14 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     }
 
     // ================= C: backward of this slice
+    const float* dh2_t = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2 * 2;
+    const __amdgpu_buffer_rsrc_t r_dh2 = rsrc_of(dh2_t, BP * PD2 * 8);
+#if P32_LL_DH2
+    // representative wait (one chunk per head: its first two columns of row 0), then the bulk load
+    if (!persist::ll_wg_wait([&](int k) { return persist::ll_ld2(r_dh2, 16 * k * 8); }, NH, tag, pb.err, sOk)) return;
+#else
     if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+#endif
     if (g == 0) P32_STAMP(0, t, 4);
     if (KS > 1) {
       // full H1 slice = the K parts' partials summed in kh order (the heads' order: same bits),
@@ -484,8 +517,16 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
           if (k2 == kh) {
             v = *reinterpret_cast<const float4*>(sH1c + b * 16 + c4);
           } else {
+#if P32_LL_H1
+            const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 8);
+            persist::ll_u32x4 u2[2];
+            if (!persist::ll_wait(u2, [&](int k) { return persist::ll_ld2(r, 8 * (b * PD1 + NCG * cg + c4) + 16 * k); }, tag, pb.err)) sOk[1] = 0;
+            v = float4{__uint_as_float(u2[0][0]), __uint_as_float(u2[0][2]), __uint_as_float(u2[1][0]),
+                       __uint_as_float(u2[1][2])};
+#else
             const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 4);
             v = ld_sc1_16(r, (b * PD1 + NCG * cg + c4) * 4);
+#endif
           }
           sum.x += v.x;
           sum.y += v.y;
@@ -495,18 +536,32 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         *reinterpret_cast<float4*>(sH1c + b * 16 + c4) = float4{fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f), fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)};
       }
     }
+#if !P32_LL_DH2
     {
-      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2, BP * PD2 * 4);
       float4 v[BP / 16];
 #pragma unroll
-      for (int k = 0; k < BP / 16; ++k) v[k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 128 fp32 = BP*32 chunks
+      for (int k = 0; k < BP / 16; ++k) v[k] = ld_sc1_16(r_dh2, (tv + NT * k) * 16);  // BP x 128 fp32 = BP*32 chunks
 #pragma unroll
       for (int k = 0; k < BP / 16; ++k) {
         const int e = tv + NT * k;
         *reinterpret_cast<float4*>(sDH2 + (e >> 5) * LDD + 4 * (e & 31)) = v[k];
       }
     }
+#else
+    {
+      // BP x 128 LL pairs = BP*64 16-byte chunks (2 columns each), every tag verified
+      persist::ll_u32x4 v[BP / 8];
+      const bool ok = persist::ll_wait(v, [&](int k) { return persist::ll_ld2(r_dh2, (tv + NT * k) * 16); }, tag, pb.err);
+#pragma unroll
+      for (int k = 0; k < BP / 8; ++k) {
+        const int e = tv + NT * k;
+        *reinterpret_cast<float2*>(sDH2 + (e >> 6) * LDD + 2 * (e & 63)) = float2{__uint_as_float(v[k][0]), __uint_as_float(v[k][2])};
+      }
+      if (!ok) sOk[1] = 0;
+    }
+#endif
     lds_barrier();
+    if (sOk[1] == 0) return;
     // C1: dH1 partials — wave w sums its 16 o2 rows (k order o2 = 16w + 4h + ks)
     {
       f32x4 acc1[MT];
@@ -523,11 +578,11 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc1[mt];
     }
     lds_barrier();
-    if (tid < MT * 64) {
-      const int mt = tid >> 6, hh = (tid & 63) >> 4, cc = tid & 15;
-      f32x4 s = sRed[mt * 64 + (tid & 63)];
+    if (tv < MT * 64) {  // tv: the step's laundered thread index (a hoisted offset would be spilled)
+      const int mt = tv >> 6, hh = (tv & 63) >> 4, cc = tv & 15;
+      f32x4 s = sRed[mt * 64 + (tv & 63)];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tid & 63)];
+      for (int w = 1; w < 8; ++w) s += sRed[(w * MT + mt) * 64 + (tv & 63)];
       bf16x4 dh, dm, dl;  // exact three-term split of dH1 (the B operand of the dW1 MFMAs)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -687,7 +742,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 // head workgroup
 // =============================================================================================
 template <int BP, bool ADAM, bool EXTRA, int KS>
-__device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int hd, char* smem) {
+__device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int hd, char* smem, unsigned gen) {
   constexpr int MT = BP / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -766,6 +821,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     sB3[32 + k] = (kin && ADAM && !fresh) ? a.v[idx] : 0.f;
     sB3[48 + k] = (kin && EXTRA) ? extra_at(a, idx) : 0.f;
   }
+  if (tid == 0) sOk[1] = 1;  // LL verdict (0: a wave gave up)
   __syncthreads();
   float loss_acc = 0.f, correct_acc = 0.f;
 
@@ -781,6 +837,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 #else
     persist::bias_corr(o, ctl.z, t, lr_t, inv_bc2);
 #endif
+    const unsigned tag = persist::ll_tag(gen, pb.fbase, t);
 
     // labels of this lane's softmax rows, loaded before the waits (off the critical path)
     int yv[4] = {-1, -1, -1, -1};
@@ -794,6 +851,37 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     // ---- H1(t) from the owners -> LDS (16-byte sc1 loads); KS > 1: the K parts' partials summed
     //      in kh order (the owners' order: same bits), then relu
     if (hd == 0) P32_STAMP(1, t, 0);
+#if P32_LL_H1
+    {
+      // representative wait: lane k polls owner k's first two columns of row 0 (K part k / NCG)
+      const __amdgpu_buffer_rsrc_t r_all = rsrc_of(h1x_part(pb, p, 0, t, BP), KSMAX * 2 * BP * PD1 * 8);
+      if (!persist::ll_wg_wait([&](int k) { return persist::ll_ld2(r_all, ((k / NCG) * 2 * BP * PD1 + NCG * (k % NCG)) * 8); }, ng_of(KS), tag, pb.err, sOk))
+        return;
+    }
+    if (hd == 0) P32_STAMP(1, t, 1);
+    {
+      // BP x 256 pairs per K part = BP*128 chunks of 2 columns; parts summed in kh order
+      float2 sum[BP / 4];
+#pragma unroll
+      for (int k2 = 0; k2 < KS; ++k2) {
+        const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 8);
+        persist::ll_u32x4 u[BP / 4];
+        if (!persist::ll_wait(u, [&](int k) { return persist::ll_ld2(r, (tv + NT * k) * 16); }, tag, pb.err)) sOk[1] = 0;
+#pragma unroll
+        for (int k = 0; k < BP / 4; ++k) {
+          const float2 v = {__uint_as_float(u[k][0]), __uint_as_float(u[k][2])};
+          sum[k] = k2 == 0 ? v : float2{sum[k].x + v.x, sum[k].y + v.y};
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < BP / 4; ++k) {
+        float2 v = sum[k];
+        if (KS > 1) v = float2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+        const int e = tv + NT * k;
+        *reinterpret_cast<float2*>(sH1 + (e >> 7) * LDH1 + 2 * (e & 127)) = v;
+      }
+    }
+#else
     if (!persist::wg_wait(pb.flags, FPP, p, F_H1, ng_of(KS), pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 1);
     {
@@ -820,7 +908,11 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         *reinterpret_cast<float4*>(sH1 + (e >> 6) * LDH1 + 4 * (e & 63)) = v;
       }
     }
+#endif
     lds_barrier();
+#if P32_LL_H1
+    if (sOk[1] == 0) return;
+#endif
     if (hd == 0) P32_STAMP(1, t, 2);
     // ---- H2 slice = relu(H1 · W2rowsᵀ + b2); wave w sums o1 in [32w, 32w+32) (k order 16g + 4h + i)
     {
@@ -864,32 +956,55 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       pl = mfma_f32(av.y, bv.y, pl);
       pl = mfma_f32(av.z, bv.z, pl);
       pl = mfma_f32(av.w, bv.w, pl);
-      // plx[p][hd][wave][lane][i] = partial logit (row 16·wave + 4h + i, class c): the consuming lane
-      // of every head has the same (wave, h, c) and reads its four rows as one float4
-      const u32x4 pv = __builtin_bit_cast(u32x4, pl);
-      st_wt128(pb.plx + ((int64_t)p * NH + hd) * BP * 16, BP * 16 * 4, (wave * 64 + lane) * 16, pv);
+      // plx[p][hd][wave][lane] = 4 partial logits (rows 16·wave + 4h + i, class c) as two LL pair
+      // chunks: the consuming lane of every head has the same (wave, h, c) and reads its four rows
+#if P32_LL_PL
+      persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32, pl[0], pl[1], tag);
+      persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32 + 16, pl[2], pl[3], tag);
+#else
+      st_wt128(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 4, (wave * 64 + lane) * 16, __builtin_bit_cast(u32x4, pl));
+#endif
     }
     if (hd == 0) P32_STAMP(1, t, 3);
+#if !P32_LL_PL
     persist::publish(pb.flags, FPP, p, F_PL + hd, pb.fbase + (unsigned)(t + 1));
+    if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+#endif
     if (hd == 0) P32_STAMP(1, t, 4);
 
     // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3, straight
-    //      into the softmax lanes' registers
-    if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
-    if (hd == 0) P32_STAMP(1, t, 5);
+    //      into the softmax lanes' registers; each softmax wave polls its own LL chunks
     // ---- log-softmax + NLL + argmax + dlogits of the whole batch (wave w < MT: rows 16w..)
     if (wave < MT) {
-      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16, NH * BP * 16 * 4);
-      float4 v[NH];
+#if P32_LL_PL
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16 * 2, NH * BP * 16 * 8);
+      persist::ll_u32x4 u[2 * NH];
+      const bool ok = persist::ll_wait(u, [&](int k) { return persist::ll_ld2(r, (k >> 1) * BP * 16 * 8 + (wave * 64 + lane) * 32 + (k & 1) * 16); }, tag, pb.err);
+      if (!ok) sOk[1] = 0;
+#else
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16 * 2, NH * BP * 16 * 8);
+      float4 uf[NH];
 #pragma unroll
-      for (int k = 0; k < NH; ++k) v[k] = ld_sc1_16(r, (k * BP * 16 + (wave * 64 + lane) * 4) * 4);
-      float4 sl = v[0];
+      for (int k = 0; k < NH; ++k) uf[k] = ld_sc1_16(r, k * BP * 16 * 8 + (wave * 64 + lane) * 16);
+#endif
+      if (hd == 0) P32_STAMP(1, t, 5);
+      float4 sl = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 1; k < NH; ++k) {
-        sl.x += v[k].x;
-        sl.y += v[k].y;
-        sl.z += v[k].z;
-        sl.w += v[k].w;
+      for (int k = 0; k < NH; ++k) {
+#if P32_LL_PL
+        const float4 vk = {__uint_as_float(u[2 * k][0]), __uint_as_float(u[2 * k][2]), __uint_as_float(u[2 * k + 1][0]),
+                           __uint_as_float(u[2 * k + 1][2])};
+#else
+        const float4 vk = uf[k];
+#endif
+        if (k == 0) {
+          sl = vk;
+        } else {
+          sl.x += vk.x;
+          sl.y += vk.y;
+          sl.z += vk.z;
+          sl.w += vk.w;
+        }
       }
       const float lsum[4] = {sl.x, sl.y, sl.z, sl.w};
       const float b3 = sB3[c];
@@ -915,22 +1030,31 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       }
     }
     lds_barrier();
+    if (sOk[1] == 0) return;  // a softmax wave gave up on the partial logits
     if (hd == 0) P32_STAMP(1, t, 6);
     // ---- dH2 slice = dlogits · W3[:, slice] ⊙ [H2 > 0]  (K = classes, natural order)
     if (wave < MT) {
       f32x4 acc = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) acc = mfma_f32(sDlog[(16 * wave + c) * LD16 + 4 * ks + h], sW3[(4 * ks + h) * LD16 + c], acc);
-      float* dst = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2;
+      float* dst = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2 * 2;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = 16 * wave + 4 * h + i;
         const float v = sH2[b * LD16 + c] > 0.f ? acc[i] : 0.f;
         sDH2[b * LD16 + c] = v;
+#if P32_LL_DH2
+        persist::ll_st1(dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
+#else
         st_wt32(dst + b * PD2 + 16 * hd + c, v);
+#endif
       }
     }
+#if P32_LL_DH2
+    lds_barrier();  // sDH2 for the off-path updates (the LL stores need no drain or flag)
+#else
     persist::publish(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1));
+#endif
     if (hd == 0) P32_STAMP(1, t, 7);
 
     // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
@@ -1045,14 +1169,19 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     pb.err = err_first;
     pb.fbase = 0;
   }
+  const unsigned gen = __hip_atomic_load(pb.gen + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (role < ng_of(KS))
-    owner32<BP, ADAM, EXTRA, KS>(a, pb, p, role, smem_p32);
+    owner32<BP, ADAM, EXTRA, KS>(a, pb, p, role, smem_p32, gen);
   else
-    head32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32);
-  if (attempt && role == 0) {  // owner 0 completed the re-run: the gang recovered
+    head32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32, gen);
+  if (role == 0) {
     __syncthreads();
-    if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      __hip_atomic_store(err_first, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      // owner 0 finished every step: the next launch tags its LL pairs with the next generation (a
+      // gang that gave up keeps it; its retry differs by the attempt bit)
+      __hip_atomic_store(pb.gen + p, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (attempt) __hip_atomic_store(err_first, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the gang recovered
+    }
   }
 }
 
@@ -1281,9 +1410,10 @@ bool mlp_persistent_f32_supported(const MLPArgs& a) {
   return persistent_f32_lds_ks(a, 1) <= 160 * 1024;
 }
 
-size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX * 2 * Bpad * PD1; }
+size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX * 2 * Bpad * PD1 * H1W; }
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
-  return (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2)) * sizeof(float);
+  // H1 partials (fp32) + partial logits and dH2 as LL (value, tag) pairs
+  return (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * 2) * sizeof(float);
 }
 size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
 int mlp_persistent_f32_gang() { return roles_of(1); }

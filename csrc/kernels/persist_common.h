@@ -78,6 +78,94 @@ __device__ __forceinline__ bool wg_wait(unsigned* flags, int fpp, int p, int idx
   return ok != 0;
 }
 
+// ---- LL hand-off (the "low latency" protocol of RCCL): every 4-byte payload word travels with a
+// 4-byte tag in ONE naturally aligned 8-byte store, so the consumer's load of the data is its own
+// readiness check — no drain of the producer's stores, no workgroup meet and no flag store on the
+// producer side (the flag protocol above costs two L2 round trips more per hand-off). The tag is
+// unique per (epoch generation, attempt, step): stale pairs of an earlier step or launch never match.
+__device__ __forceinline__ unsigned ll_tag(unsigned gen, unsigned fbase, int t) {
+  return ((gen & 0xFFFu) << 20) | (fbase ? (1u << 19) : 0u) | (unsigned)(t + 1);
+}
+typedef unsigned ll_u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte write-through store of two LL pairs {v0, tag, v1, tag} at byte offset `off` of a uniform base
+__device__ __forceinline__ void ll_st2(float* base, int bytes, int off, float v0, float v1, unsigned tag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+  const ll_u32x4 v = {__builtin_bit_cast(unsigned, v0), tag, __builtin_bit_cast(unsigned, v1), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+// 8-byte write-through store of one LL pair
+__device__ __forceinline__ void ll_st1(float* pair, float v, unsigned tag) {
+  st_wt(pair, ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, v));
+}
+// 16-byte L1-bypassing load of two LL pairs
+__device__ __forceinline__ ll_u32x4 ll_ld2(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16); }
+__device__ __forceinline__ bool ll_ok2(const ll_u32x4& v, unsigned tag) { return v[1] == tag && v[3] == tag; }
+// Payload words of a received chunk: read them with __uint_as_float(v[i]). amdclang 22 (ROCm 7.2)
+// miscompiles __builtin_bit_cast(float, v[i]) on an ext-vector ELEMENT lvalue: it reads element 0
+// whatever i is (tests/test_kernel_lint.py rejects the pattern).
+
+// Consumer side of an LL hand-off with N 16-byte chunks per lane: `load(k)` issues chunk k's load;
+// spins (s_sleep between polls, chunks that already matched are not reloaded) until every chunk of
+// every lane of the wave carries `tag`. Bounded like wg_wait: false when the gang gave up (err set by
+// any workgroup) or after `ticks`.
+template <int N, class Load>
+__device__ __forceinline__ bool ll_wait(ll_u32x4 (&v)[N], Load load, unsigned tag, int* err, unsigned long long ticks = SPIN_TICKS) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = load(k);
+  unsigned long long t0 = 0;
+  for (;;) {
+    bool ready = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) ready = ready && ll_ok2(v[k], tag);
+    if (__all(ready)) return true;
+    if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+    const unsigned long long now = wall_clock64();
+    if (t0 == 0) {
+      t0 = now;
+    } else if (now - t0 > ticks) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (!ll_ok2(v[k], tag)) v[k] = load(k);
+  }
+}
+
+// Representative wait of an LL hand-off with n <= 64 producers (long waits: the consumer workgroup
+// must not hammer L2 with bulk polls): wave 0, lane k < n, polls one 16-byte chunk of producer k
+// (`probe(k)` issues its load) until its tags match, then the workgroup meets; the bulk loads that
+// follow still verify every tag (ll_wait), since a producer's other chunks may land later.
+template <class Probe>
+__device__ __forceinline__ bool ll_wg_wait(Probe probe, int n, unsigned tag, int* err, int* sOk, unsigned long long ticks = SPIN_TICKS) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int k = lane < n ? lane : 0;
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    for (;;) {
+      const bool ready = lane >= n || ll_ok2(probe(k), tag);
+      if (__all(ready)) break;
+      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        ok = 0;
+        break;
+      }
+      if (wall_clock64() - t0 > ticks) {
+        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *sOk = ok;
+  }
+  __syncthreads();
+  const int ok = *sOk;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok != 0;
+}
+
 // Per-step optimizer constants: lr_t = lr / (1 - β1^k), inv = 1 / sqrt(1 - β2^k), k = t0 + t + 1.
 __device__ __forceinline__ void bias_corr(const OptParams& o, int t0, int t, float& lr_t, float& inv) {
   const int k = t0 + t + 1;

@@ -756,7 +756,9 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
       rc |= e->alloc(&p, mlp_persistent_f32_bytes(P, a.Bpad));
       e->pb32.h1x = (float*)p;
       e->pb32.plx = e->pb32.h1x + mlp_persistent_f32_h1x_floats(P, a.Bpad);  // H1 partials: [P][KSMAX][parity]
-      e->pb32.dh2x = e->pb32.plx + (size_t)P * 8 * a.Bpad * 16;
+      e->pb32.dh2x = e->pb32.plx + (size_t)P * 8 * a.Bpad * 16 * 2;           // LL pairs
+      rc |= e->alloc(&p, (size_t)P * sizeof(unsigned));
+      e->pb32.gen = (unsigned*)p;
       e->pb32.flag_bytes = mlp_persistent_f32_flag_bytes(P);
       rc |= e->alloc(&p, e->pb32.flag_bytes);
       e->pb32.flags = (unsigned*)p;

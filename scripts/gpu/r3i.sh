@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3, call I: LL hand-offs after the bit_cast fix (partial logits, dH2) in the fp32 MLP epoch: numerics + bench + stamps
+set -o pipefail
+O=gpurun_out/r3x_i; mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_mlp_f32_gpu.py -x -q --timeout 240 --timeout-method thread > $O/mlp_f32_tests.log 2>&1 || { echo "mlp tests failed" >> $O/status; exit 1; }
+for i in 1 2; do timeout -k 10 120 python bench.py --steps 200 --warmup 10 > $O/bench_$i.log 2>&1 || exit 1; done
+MYFYP_NATIVE_LIB=build/stamps/libmyfyp_hip.so timeout -k 10 120 python scripts/probes/stamps_f32.py > $O/stamps.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_collective_gpu.py tests/test_multiproc_gpu.py tests/test_kernels_gpu.py -x -q --timeout 240 --timeout-method thread > $O/other_tests.log 2>&1; echo "other tests rc=$?" >> $O/status
