@@ -237,7 +237,7 @@ def main() -> None:
             "rounds_to_target": r_target,
             "target_acc": args.target_acc,
             "final_test_acc": None if final_acc is None else round(final_acc, 4),
-            "baseline_note": "vs_baseline = value / 1.20 rounds/s: measured proxy of the reference algorithm (gossip, batch-1 fp32 CPU learner, 8 nodes; BASELINE.md); the reference publishes no number",
+            "baseline_note": "vs_baseline = value / 1.20 rounds/s, the measured proxy of the reference algorithm (gossip, batch-1 fp32 CPU learner, 8 nodes; BASELINE.md; the reference publishes no number). Context, not parity: this run trains at local batch 64 on the GPU, the proxy at batch 1 on the CPU",
         }
         print(json.dumps(out), flush=True)
     fed.shutdown()

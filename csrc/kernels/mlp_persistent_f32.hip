@@ -734,7 +734,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   if (pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
     if (nsteps > 0) w2_replica_update(nsteps - 1, lr_t, inv_bc2);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * h + i) * PD1 + NCG * cg + c] = w2c[i];
+    for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * hw + i) * PD1 + NCG * cg + cw] = w2c[i];
   }
 }
 
@@ -1179,7 +1179,9 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       // owner 0 finished every step: the next launch tags its LL pairs with the next generation (a
       // gang that gave up keeps it; its retry differs by the attempt bit)
-      __hip_atomic_store(pb.gen + p, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // (re-read, not kept live in a VGPR across the epoch)
+      __hip_atomic_store(pb.gen + p, __hip_atomic_load(pb.gen + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
       if (attempt) __hip_atomic_store(err_first, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the gang recovered
     }
   }
