@@ -68,4 +68,5 @@ struct WgradArgs {
 extern "C" {
 int conv_gemm_launch(int mode, const ConvGemmArgs* a, int peers, void* stream);
 int conv_wgrad_launch(const WgradArgs* a, int peers, int splits, void* stream);
+int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int cout, int cin, int R, int S, int peers, void* stream);
 }

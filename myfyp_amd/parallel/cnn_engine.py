@@ -98,6 +98,7 @@ _SIGS = {
     "conv_gemm_launch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "conv_wt_flip_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_act": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
@@ -231,6 +232,8 @@ class CNNGroup:
         self.fold_bnb = os.environ.get("MYFYP_CNN_FOLD_BNB", "1") != "0"
         # wgrad split-K target: workgroups per CU over all peers (more splits = more parallelism and
         # more fp32 atomics on the gradient)
+        # stride-1 dgrad as a forward conv over dY with flipped weights (conv.hip MODE 4); 0 = MODE 3
+        self.dgrad_fwd = os.environ.get("MYFYP_DGRAD_FWD", "1") != "0"
         self.wgrad_tpc = int(os.environ.get("MYFYP_WGRAD_TPC", "2"))  # measured: 2 -> 75.6 ms wgrad, 4 -> 78.4, 8 -> 89.8 (scripts/probes/wgrad_tpc.sh)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
@@ -349,6 +352,7 @@ class CNNGroup:
         self.mom = torch.zeros_like(params)
         self.shadow = torch.zeros(capacity, self.shadow_numel, dtype=torch.bfloat16, device=dev)
         self.gradf = torch.zeros(capacity, self.shadow_numel, dtype=torch.float32, device=dev)
+        self.shadow_t = torch.zeros_like(self.shadow) if self.dgrad_fwd else None  # MODE 4 weights (k_conv_wt_flip)
         self.capacity = capacity
         for slot, h in self.handles.items():
             h.retarget()
@@ -476,7 +480,18 @@ class CNNGroup:
         lib, P = _lib(), self.capacity
         shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
-        if mode == 0:
+        # stride-1 dgrad as a forward conv over dY with flipped, transposed weights (conv.hip MODE 4):
+        # the forward's K-contiguous weight panel instead of the transposed LDS reads of MODE 3
+        fwd_dgrad = mode == 1 and L.stride == 1 and L.colmap is None and self.dgrad_fwd
+        if fwd_dgrad:
+            wt = self.shadow_t.data_ptr() + 2 * shadow_f
+            _chk(lib.conv_wt_flip_launch(self.shadow.data_ptr() + 2 * shadow_f, self.shadow.shape[1], wt, self.shadow_t.shape[1], L.cp_out, L.cp_in, L.R, L.S,
+                                         P, self._stream()), f"wt flip {L.name}")
+            a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.ho, L.wo, L.cp_out
+            a.out_h, a.out_w = L.h, L.w
+            a.wt = wt
+            a.ncol, a.ncol_valid = L.cp_in, L.cin
+        elif mode == 0:
             a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.h, L.w, L.cp_in
             a.out_h, a.out_w = L.ho, L.wo
             a.wt = self.shadow.data_ptr() + 2 * shadow_f
@@ -487,7 +502,7 @@ class CNNGroup:
             a.wt = self.shadow.data_ptr() + 2 * shadow_f
             a.ncol, a.ncol_valid = L.cp_in, (L.cin if L.colmap is None else L.cp_in)
         a.src_ps, a.wt_ps = src.shape[1], self.shadow.shape[1]
-        a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, L.pad
+        a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, (L.R - 1 - L.pad if fwd_dgrad else L.pad)
         a.out, a.out_ps = out.data_ptr(), out.shape[1]
         if bias and L.bias is not None:
             a.bias, a.bias_ps = self.params.data_ptr() + 4 * self._off(L.bias), self.params.shape[1]
@@ -512,7 +527,7 @@ class CNNGroup:
                 bn1_, y1_ = rest[0]
                 a.bnb_y1, a.bnb_y1_ps, a.bnb_ms1 = y1_.data_ptr(), y1_.shape[1], self.ms(bn1_).data_ptr()
                 a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", 2 * bn1_.Cp).data_ptr()
-        _chk(lib.conv_gemm_launch(mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
+        _chk(lib.conv_gemm_launch(4 if fwd_dgrad else mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
         """(pixels per split, splits): split the pixel (K) dimension only until ~4 tiles per CU exist."""

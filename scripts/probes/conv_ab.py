@@ -21,7 +21,10 @@ for name, cin, cout, h, st in shapes:
     dy = torch.randn(P, B * ho * ho * cout, device=dev).to(torch.bfloat16)
     dx = torch.empty(P, B * h * h * cin, device=dev, dtype=torch.bfloat16)
     flops = 2 * P * B * ho * ho * cout * 9 * cin
-    for mode in (0, 1):
+    wt = torch.empty_like(wf)
+    for mode in (0, 1, 4):
+        if mode == 4 and st != 1:
+            continue
         a = ConvGemmArgs()
         if mode == 0:
             a.src, a.src_ps, a.src_h, a.src_w, a.src_c = x.data_ptr(), x.shape[1], h, h, cin
@@ -35,12 +38,23 @@ for name, cin, cout, h, st in shapes:
         a.stride, a.pad = st, 1
         a.wt, a.wt_ps, a.max_batch = wf.data_ptr(), wf.shape[1], B
         s = torch.cuda.current_stream().cuda_stream
-        for _ in range(3):
+        if mode == 4:  # dgrad as a forward conv over dY: flipped weights (timed with the conv), pad R-1-pad
+            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
+            a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
+            a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
+            a.wt, a.pad = wt.data_ptr(), 1
+
+        def launch():
+            if mode == 4:
+                assert lib.conv_wt_flip_launch(wf.data_ptr(), wf.shape[1], wt.data_ptr(), wt.shape[1], cout, cin, 3, 3, P, s) == 0
             assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, s) == 0
+
+        for _ in range(3):
+            launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(20):
-            lib.conv_gemm_launch(mode, ctypes.byref(a), P, s)
+            launch()
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 20 * 1000

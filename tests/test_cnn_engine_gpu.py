@@ -70,6 +70,17 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
     assert lib.conv_gemm_launch(1, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     torch.testing.assert_close(dx.view(n, h, h, cpi)[..., :cin].float(), dx_ref.permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
+    if stride == 1:  # MODE 4: the same dgrad as a forward conv over dY with flipped, transposed weights
+        wt = torch.zeros_like(wf)
+        s_ = torch.cuda.current_stream().cuda_stream
+        assert lib.conv_wt_flip_launch(wf.data_ptr(), 0, wt.data_ptr(), 0, cpo, cpi, k, k, 1, s_) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(wt.view(cpi, k, k, cpo), wf.flip(1, 2).permute(3, 1, 2, 0))
+        dx4 = torch.zeros_like(dx)
+        b.wt, b.pad, b.out = wt.data_ptr(), k - 1 - pad, dx4.data_ptr()
+        assert lib.conv_gemm_launch(4, ctypes.byref(b), 1, s_) == 0
+        torch.cuda.synchronize()
+        torch.testing.assert_close(dx4.view(n, h, h, cpi)[..., :cin].float(), dx_ref.permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
 
     # wgrad
     dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
@@ -91,10 +102,12 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
         assert gw[cout:].abs().max().item() == 0 if cpo > cout else True
 
 
-@pytest.mark.parametrize("cin,cout,stride,h,n,two", [(64, 64, 1, 16, 3, False), (64, 128, 2, 16, 2, True), (128, 128, 1, 8, 4, True)])
-def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two):
+@pytest.mark.parametrize("cin,cout,stride,h,n,two,mode", [(64, 64, 1, 16, 3, False, 1), (64, 128, 2, 16, 2, True, 1), (128, 128, 1, 8, 4, True, 1),
+                                                          (64, 64, 1, 16, 3, False, 4), (128, 128, 1, 8, 4, True, 4), (64, 128, 1, 8, 2, True, 4)])
+def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode):
     """dgrad with the BN-backward epilogue: out = bf16(dX + resid) * [mask > 0] and per-channel
-    (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op."""
+    (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op. mode 4: the
+    stride-1 dgrad as a forward conv over dY with flipped weights (what the engine runs)."""
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, _lib
 
     lib = _lib()
@@ -124,7 +137,11 @@ def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two):
     b.bnb_mask, b.bnb_y0, b.bnb_ms0, b.bnb_part0 = mn.data_ptr(), yn[0].data_ptr(), ms[0].data_ptr(), parts[0].data_ptr()
     if two:
         b.bnb_y1, b.bnb_ms1, b.bnb_part1 = yn[1].data_ptr(), ms[1].data_ptr(), parts[1].data_ptr()
-    assert lib.conv_gemm_launch(1, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
+    if mode == 4:
+        wt = torch.zeros_like(wf)
+        assert lib.conv_wt_flip_launch(wf.data_ptr(), 0, wt.data_ptr(), 0, cout, cin, k, k, 1, torch.cuda.current_stream().cuda_stream) == 0
+        b.wt, b.pad = wt.data_ptr(), k - 1 - pad
+    assert lib.conv_gemm_launch(mode, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     g_ref = (dx_ref + resid) * (mask > 0)
     g = out.view(n, h, h, cin).float().permute(0, 3, 1, 2)
