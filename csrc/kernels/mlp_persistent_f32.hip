@@ -77,6 +77,15 @@ constexpr int NT = 512;  // threads per workgroup (8 waves)
 #ifndef P32_LL_H1
 #define P32_LL_H1 0
 #endif
+// scheduling fences between the K steps of the forward / of C2 (1) or free interleaving (0).
+// Measured (profiles/r3h_sched): C2 unfenced 532.6 / 535.0 vs 512.1 / 521.8 rounds/s fenced, no
+// spills; the forward's fence is neutral and stays
+#ifndef P32_SB_FWD
+#define P32_SB_FWD 1
+#endif
+#ifndef P32_SB_C2
+#define P32_SB_C2 0
+#endif
 #ifndef P32_LL_PL
 #define P32_LL_PL 0
 #endif
@@ -446,7 +455,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
       for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         fwd_kstep(q, acc);
-        __builtin_amdgcn_sched_barrier(0);
+        if (P32_SB_FWD) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc[mt];
@@ -620,7 +629,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         const int s = lds_step ? 8 * RQ : wave + 8 * q;
         const int tt_lo = lds_step ? wave - (NW - 2) : 0;
         const int tt_hi = lds_step ? tt_lo + 1 : 2;
-        __builtin_amdgcn_sched_barrier(0);
+        if (P32_SB_C2) __builtin_amdgcn_sched_barrier(0);
         if (s < KS1 && tt_lo >= 0) {
           int lq = lane;
           asm volatile("" : "+v"(lq));

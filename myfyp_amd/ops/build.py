@@ -64,10 +64,13 @@ def build(verbose: bool = False, jobs: int = 8, variant: str = "") -> str:
     if variant:
         # "stamps" or "stamps+NAME=VAL+NAME2" (extra -D macros for timing-only experiment builds)
         parts = variant.split("+")
-        tag = variant.replace("+", "_").replace("=", "")
+        tag = variant.replace("+", "_").replace("=", "").replace("mllvm:", "").replace("-", "")
         obj_dir = os.path.join(ROOT, "build", f"obj_{tag}")
         lib = os.path.join(ROOT, "build", tag, "libmyfyp_hip.so")
-        extra = tuple(["-DMLP_STAMPS"] if parts[0] == "stamps" else []) + tuple(f"-D{m}" for m in parts[1:])
+        # a part starting with "mllvm:" is a raw backend option (experiment builds: "-mllvm <opt>")
+        extra = tuple(["-DMLP_STAMPS"] if parts[0] == "stamps" else [])
+        for m in parts[1:]:
+            extra += ("-mllvm", m[len("mllvm:"):]) if m.startswith("mllvm:") else (f"-D{m}",)
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sources()
