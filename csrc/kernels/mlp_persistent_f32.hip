@@ -106,8 +106,9 @@ __host__ __device__ constexpr int ng_of(int KS) { return NCG * KS; }         // 
 __host__ __device__ constexpr int roles_of(int KS) { return NCG * KS + NH; }  // workgroups per peer
 __host__ __device__ constexpr int ppl_of(int KS) { return KS == 1 ? 8 : 4; }  // peers per launch
 constexpr int PD1 = 256, PD2 = 128;
-constexpr int FPP = NCG * KSMAX + 2 * NH;  // flags per peer (laid out for KSMAX)
-constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH;
+constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH, F_DONE = NCG * KSMAX + 2 * NH;
+constexpr int FPP = F_DONE + NCG * KSMAX + NH;  // flags per peer (laid out for KSMAX): + one commit flag per role
+constexpr unsigned DONE_MARK = 1u << 23;      // commit flag value (above every step's t + 1)
 constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 799
 
 // K steps of the W1 GEMMs: D0 columns plus at least one padding column, column D0, which carries
@@ -258,6 +259,22 @@ __host__ __device__ inline HeadLds32 head_lds32(int Bpad) {
 // register slots per wave would not fit beside the working set of two waves per SIMD. KS = 2: at
 // most 13 K steps per owner, two register slots per wave.
 __host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : 2; }
+
+// Gang commit: a role stores its state only after EVERY role of the gang finished every
+// step. Without it, heads that passed their last wait could write back while an owner still timed
+// out on the last dH2 hand-off, and the retry launch would re-run the epoch from half-updated
+// state. Each role publishes its commit flag and waits for all of them (bounded, like every other
+// hand-off); a gang that gave up anywhere stores nothing. Test hook: debug_giveup = p + 1 + 256
+// makes owner 0 of peer p give up right here on the first attempt.
+template <int KS>
+__device__ __forceinline__ bool gang_commit(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int role, int* sOk) {
+  if (pb.fbase == 0 && role == 0 && a.debug_giveup == p + 1 + 256) {
+    if (threadIdx.x == 0) __hip_atomic_store(pb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  persist::publish(pb.flags, FPP, p, F_DONE + role, pb.fbase + DONE_MARK);
+  return persist::wg_wait(pb.flags, FPP, p, F_DONE, roles_of(KS), pb.fbase + DONE_MARK, pb.err, sOk);
+}
 
 template <int BP, bool ADAM, bool EXTRA, int KS>
 __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem, unsigned gen) {
@@ -699,6 +716,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (g == 0) P32_STAMP(0, t, 6);
   }
 
+  if (!gang_commit<KS>(a, pb, p, g, sOk)) return;
   // ---- write the state back (fp32 master weights and moments; b1 from the bias slot). Every
   //      address is re-derived from laundered lane / row indices: the compiler would otherwise keep
   //      the prologue's 64-bit load addresses alive across the whole epoch (VGPR spills)
@@ -1103,6 +1121,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     if (hd == 0) P32_STAMP(1, t, 8);
   }
 
+  if (!gang_commit<KS>(a, pb, p, ng_of(KS) + hd, sOk)) return;
   // ---- write back W2 rows, b2, the W3 slice, b3 (head 0) and the epoch's loss / accuracy sums
 #pragma unroll
   for (int gg = 0; gg < 2; ++gg) {
@@ -1171,7 +1190,7 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     pb.err = pb.err + ERR_RETRY + p;
     pb.fbase = RETRY_BASE;
   } else {
-    if (a.debug_giveup == p + 1) {  // test hook: this peer's first attempt gives up at once
+    if (a.debug_giveup == p + 1) {  // test hook: this peer's first attempt gives up at once (p + 1 + 256: at the commit)
       if (role == 0 && threadIdx.x == 0) __hip_atomic_store(err_first, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }

@@ -1161,11 +1161,12 @@ int mlp_engine_set_reserved_cus(void* h, int cus) {
 }
 int mlp_engine_f32_ks(void* h) { return mlp_persistent_f32_ks(((MLPEngine*)h)->a); }
 
-// Test hook: peer p's next fp32 epochs give up on their first attempt (p < 0: off). Re-captures.
-int mlp_engine_debug_giveup(void* h, int peer) {
+// Test hook: peer p's next fp32 epochs give up on their first attempt (p < 0: off), at launch or
+// (at_end) at the gang commit after the last step. Re-captures.
+int mlp_engine_debug_giveup(void* h, int peer, int at_end) {
   auto* e = (MLPEngine*)h;
   std::lock_guard<std::mutex> g(e->mu);
-  e->a.debug_giveup = peer < 0 ? 0 : peer + 1;
+  e->a.debug_giveup = peer < 0 ? 0 : peer + 1 + (at_end ? 256 : 0);
   e->invalidate();
   return 0;
 }

@@ -412,11 +412,12 @@ class MLPGroup:
         """Give-ups of the persistent fp32 epoch that the in-stream retry launch recovered."""
         return int(_native.load(required=True).mlp_engine_recoveries(self._engine)) if self._engine else 0
 
-    def debug_giveup(self, slot: Optional[int]) -> None:
-        """Test hook: the peer in ``slot`` gives up on the first attempt of every fp32 epoch."""
+    def debug_giveup(self, slot: Optional[int], at_end: bool = False) -> None:
+        """Test hook: the peer in ``slot`` gives up on the first attempt of every fp32 epoch, at
+        launch or (``at_end``) at the gang commit after its last step."""
         with self.lock:
             self._ensure_engine()
-            _native.check(_native.load(required=True).mlp_engine_debug_giveup(self._engine, -1 if slot is None else int(slot)), "debug_giveup")
+            _native.check(_native.load(required=True).mlp_engine_debug_giveup(self._engine, -1 if slot is None else int(slot), int(at_end)), "debug_giveup")
 
     def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)

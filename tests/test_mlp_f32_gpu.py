@@ -270,11 +270,13 @@ def test_f32_partial_last_batch_and_bias(dev):
             assert rel < 1e-4, f"peer {i} {name}: relative update error {rel:.2e}"
 
 
-def test_f32_giveup_recovered_by_retry_launch(dev):
+@pytest.mark.parametrize("at_end", [False, True])
+def test_f32_giveup_recovered_by_retry_launch(dev, at_end):
     """A gang that gives up (here: forced on its first attempt through the engine's test hook, as a
     non-resident workgroup would) is re-run by the in-stream retry launch from the untouched
     pre-epoch state: the epoch result is bit-identical to a run without the give-up, the other
-    peers are unaffected, and the engine counts one recovery per epoch."""
+    peers are unaffected, and the engine counts one recovery per epoch. at_end: the give-up comes
+    after every step ran, at the gang commit — no role may have stored anything."""
     spec = {"name": "adam", "lr": 1e-3}
     results = []
     for forced in (False, True):
@@ -284,7 +286,7 @@ def test_f32_giveup_recovered_by_retry_launch(dev):
         learners, refs, g, n = _setup(dev, 3, 64, 1500, 5, spec)
         _pin_perms(dev, g, learners, n)
         if forced:
-            g.debug_giveup(learners[1]._engine.slot)
+            g.debug_giveup(learners[1]._engine.slot, at_end=at_end)
         _fit_all(learners)
         _ = [l.evaluate() for l in learners]  # results fetched: give-up status checked
         results.append(([l.flat_params().detach().clone() for l in learners], g.recoveries()))
