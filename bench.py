@@ -61,6 +61,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--force-collective", action="store_true",
                     help="one GPU: run FedAvg through a world-size-1 RCCL group (the multi-rank path: side-stream reduce -> RCCL all-reduce -> apply)")
     ap.add_argument("--no-failover", action="store_true", help="skip the per-round confirmation of the weight collectives (fault tolerance off)")
+    ap.add_argument("--no-prewarm", action="store_true", help="do not prepare the fused engine at Node.start (round 0 captures the epoch graph)")
     return ap.parse_args()
 
 
@@ -96,6 +97,7 @@ def main() -> None:
     Settings.MLP_PRECISION = args.precision
     Settings.FORCE_COLLECTIVE = bool(args.force_collective)
     Settings.COLLECTIVE_FAILOVER = not args.no_failover
+    Settings.ENGINE_PREWARM = not args.no_prewarm
 
     fed = Federation.init()
     world, rank = fed.world, fed.rank
@@ -109,8 +111,10 @@ def main() -> None:
         Node(TorchModel(MLP(seed=100 + g)), parts[g], address=f"peer-{g}", protocol=CollectiveCommunicationProtocol, learner_kwargs={"batch_size": args.batch_size})
         for g in gids
     ]
+    t_ns = time.perf_counter()
     for n in nodes:
-        n.start()
+        n.start()  # Settings.ENGINE_PREWARM: the fused engine captures its epoch graph here
+    node_start_s = time.perf_counter() - t_ns
     fed.finalize()
     if args.eager:
         for n in nodes:
@@ -184,6 +188,8 @@ def main() -> None:
         if "driver_round" in logger.get_timings().get(nd.addr, {}):
             tm["driver_round"] = logger.get_timings()[nd.addr]["driver_round"]
     brk = {k: round(1000 * float(np.median(v[args.warmup :] or v)), 3) for k, v in tm.items()}
+    first = [round(1000 * (round_end[r] - t_start), 2) for r in sorted(round_end)[:10]]
+    print(f"[bench] rank {rank} round-end times since set_start_learning (ms), rounds 0..9: {first}", file=sys.stderr, flush=True)
     ends = [round_end[r] for r in sorted(round_end) if r >= args.warmup - 1]
     if len(ends) > 2:
         d = np.diff(ends) * 1000.0
@@ -237,6 +243,8 @@ def main() -> None:
             "rounds_to_target": r_target,
             "target_acc": args.target_acc,
             "final_test_acc": None if final_acc is None else round(final_acc, 4),
+            "node_start_s": round(node_start_s, 4),
+            "node_start_note": "Node.start() of the local peers before set_start_learning, incl. the fused-engine prewarm (epoch-graph capture/upload, code-object load; no training work); time_to_target_s is clocked from set_start_learning",
             "baseline_note": "vs_baseline = value / 1.20 rounds/s, the measured proxy of the reference algorithm (gossip, batch-1 fp32 CPU learner, 8 nodes; BASELINE.md; the reference publishes no number). Context, not parity: this run trains at local batch 64 on the GPU, the proxy at batch 1 on the CPU",
         }
         print(json.dumps(out), flush=True)

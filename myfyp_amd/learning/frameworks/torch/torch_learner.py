@@ -175,6 +175,14 @@ class TorchLearner(Learner):
         return self.data.get_num_samples(train=True)
 
     # ------------------------------------------------------------------ train
+    def prewarm(self) -> None:
+        """One-time fused-engine setup before learning starts (graph capture and upload, code-object
+        load; no training work). Called by ``Node.start`` when ``Settings.ENGINE_PREWARM`` is set."""
+        eng = self._engine
+        group = getattr(eng, "group", None) if eng is not None else None
+        if group is not None and hasattr(group, "prewarm"):
+            group.prewarm(self._optimizer_spec())
+
     def _optimizer_spec(self) -> dict:
         module = self.model.get_model()
         spec = getattr(module, "optimizer_spec", None)

@@ -44,6 +44,7 @@ from myfyp_amd.learning.frameworks.p2pfl_model import P2PFLModel
 from myfyp_amd.learning.frameworks.simulation import try_init_learner_with_ray
 from myfyp_amd.management.logger import logger
 from myfyp_amd.node_state import NodeState
+from myfyp_amd.settings import Settings
 from myfyp_amd.stages.workflows import LearningWorkflow
 
 
@@ -121,6 +122,10 @@ class Node:
         self._running = True
         logger.register_node(self.addr, self.simulation)
         self._communication_protocol.start()
+        if Settings.ENGINE_PREWARM:
+            prewarm = getattr(self.learner, "prewarm", None)
+            if prewarm is not None:
+                prewarm()  # fused engine: capture the epoch graph now, not in round 0
         if wait:
             self._communication_protocol.wait_for_termination()
             logger.info(self.addr, "Protocol terminated.")

@@ -296,6 +296,30 @@ class MLPGroup:
             self.extras[name] = buf
         return buf
 
+    def _set_optimizer(self, lib, spec: dict, mu: float, anchor, cg, cl) -> None:
+        kind = 0 if spec.get("name", "adam") == "adam" else 1
+        _native.check(
+            lib.mlp_engine_set_optimizer(
+                self._engine, kind, float(spec.get("lr", 1e-3)), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
+                float(spec.get("eps", 1e-8)), float(spec.get("weight_decay", 0.0)), float(spec.get("momentum", 0.0)),
+                int(bool(spec.get("nesterov", False))), mu,
+            ),
+            "set_optimizer",
+        )
+        _native.check(lib.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
+
+    def prewarm(self, spec: dict) -> None:
+        """One-time engine setup before the first fit (node start): bind the data, capture and
+        upload the epoch graph for ``spec`` (no FedProx/SCAFFOLD extras: those re-capture on their
+        first fit), allocate the evaluation side and load the code object. Runs no training work;
+        a later change (another peer attaching, other optimizer settings) re-captures as before."""
+        lib = _native.load(required=True)
+        with self.lock:
+            self._ensure_engine()
+            self._set_optimizer(lib, spec, 0.0, None, None, None)
+            _native.check(lib.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
+            _native.check(lib.mlp_engine_prepare(self._engine, torch.cuda.current_stream(self.device).cuda_stream), "prepare")
+
     # ------------------------------------------------------------------ batched fit
     def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
@@ -304,7 +328,6 @@ class MLPGroup:
             stream = torch.cuda.current_stream(self.device).cuda_stream
             specs = list(batch.values())
             spec, epochs = specs[0][0], max(r[1] for r in specs)
-            kind = 0 if spec.get("name", "adam") == "adam" else 1
             extras_any = [r[2] for r in specs if r[2]]
             mu = 0.0
             anchor = cg = cl = None
@@ -324,15 +347,7 @@ class MLPGroup:
                         cg[slot].zero_()
                         cl[slot].zero_()
             fast = _native.load_fast()
-            _native.check(
-                fast.mlp_engine_set_optimizer(
-                    self._engine, kind, float(spec.get("lr", 1e-3)), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
-                    float(spec.get("eps", 1e-8)), float(spec.get("weight_decay", 0.0)), float(spec.get("momentum", 0.0)),
-                    int(bool(spec.get("nesterov", False))), mu,
-                ),
-                "set_optimizer",
-            )
-            _native.check(fast.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
+            self._set_optimizer(fast, spec, mu, anchor, cg, cl)
             active = np.zeros(self.capacity, dtype=np.int32)
             for slot in batch:
                 active[slot] = 1

@@ -117,6 +117,9 @@ class Settings:
     # CUs the fp32 MLP persistent epoch leaves to a concurrent RCCL kernel when collectives are
     # active (co-residency: every workgroup of a gang must be resident at once)
     RCCL_RESERVED_CUS: int = 32
+    # Node.start() prepares the fused engine (epoch-graph capture and upload, code-object load; no
+    # training work) so round 0 does not pay it — like building a compiled model at load time
+    ENGINE_PREWARM: bool = True
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
     GIL_SWITCH_INTERVAL: float | None = 2e-4
@@ -202,6 +205,7 @@ class Settings:
             "FORCE_COLLECTIVE": "FORCE_COLLECTIVE",
             "COLLECTIVE_FAILOVER": "COLLECTIVE_FAILOVER",
             "RCCL_RESERVED_CUS": "RCCL_RESERVED_CUS",
+            "ENGINE_PREWARM": "ENGINE_PREWARM",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",
             "ROUND_DRIVER": "ROUND_DRIVER",

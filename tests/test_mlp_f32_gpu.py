@@ -298,6 +298,27 @@ def test_f32_giveup_recovered_by_retry_launch(dev, at_end):
         assert torch.equal(a, b)
 
 
+def test_f32_prewarm_is_transparent(dev):
+    """Engine prewarm (Node.start: graph capture + upload, code-object load) runs no training work:
+    an epoch after prewarm is bit-identical to one without it."""
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+
+    spec = {"name": "adam", "lr": 1e-3}
+    results = []
+    for warm in (True, False):
+        MLPGroup.reset_all()
+        learners, refs, g, n = _setup(dev, 2, 64, 1400, 7, spec)
+        _pin_perms(dev, g, learners, n)
+        if warm:
+            for l in learners:
+                l.prewarm()
+            torch.cuda.synchronize()
+        _fit_all(learners)
+        results.append([l.flat_params().detach().clone() for l in learners])
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
+
+
 def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch):
     """The epoch batch gather on its own stream into alternating batch buffers (overlapping the
     previous epoch) gives bit-identical training to the gather as the first node of the epoch
