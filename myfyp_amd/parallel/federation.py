@@ -425,22 +425,27 @@ class Federation:
             logger.warning(f"rank{self.rank}", f"last collective unconfirmed at shutdown: {e}")
         self._pending.clear()
         self._stop_watchdog()
-        if self.shm is not None:
-            self.shm.leave()
-            synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT), float(Settings.FAILURE_TIMEOUT))
-            self._stop_heartbeat()  # joined before the unmap: a beat in flight wrote into freed pages (SIGSEGV at exit)
-            self.shm.close()
-            self.shm = None
         if self.bus is not None:
             self.bus.stop()
             self.bus = None
+        # Process groups go first and the shm "all gone" wait last: rank 0's process hosts the
+        # rendezvous store, so it must not exit while another rank is still tearing down its groups
+        # (a store that vanished under a peer's destroy_process_group aborted that peer at exit).
         if self.collective:
             import torch.distributed as dist
 
             if dist.is_initialized():
-                if not synced and not self.departed and self.members == list(range(self.world)) and not self._aborted:
+                if self.shm is None and not self.departed and self.members == list(range(self.world)) and not self._aborted:
                     dist.barrier(group=self._pg)
                 dist.destroy_process_group()
+        if self.shm is not None:
+            self.shm.leave()
+            synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT), float(Settings.FAILURE_TIMEOUT))
+            if not synced:
+                logger.warning(f"rank{self.rank}", "not every rank left within COLLECTIVE_TIMEOUT")
+            self._stop_heartbeat()  # joined before the unmap: a beat in flight wrote into freed pages (SIGSEGV at exit)
+            self.shm.close()
+            self.shm = None
         Federation._instance = None
 
     @classmethod
