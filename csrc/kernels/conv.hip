@@ -25,6 +25,8 @@
 
 #include "conv.h"
 
+#include <cstdlib>
+
 struct bf8 { bf16 v[8]; };
 
 #define CG_BK 64
@@ -101,6 +103,167 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, in
   // whole-vector bit cast (an element-wise short->bf16 cast miscompiles into lane-duplicating perms)
   const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, both);
+}
+
+// Epilogue shared by the conv GEMM kernels (BM x BN tile, NT threads, NT / 64 waves as
+// (BM / 64) x 2, each 64 x BN/2): the accumulator tile goes through LDS (fp32) so that every thread
+// then owns one 16-byte chunk (8 channels) of a row: bias, residual, mask and y operands are 16-byte
+// loads and the output a 16-byte store. Straight from the MFMA layout a lane holds 1 column x 16 rows,
+// i.e. 2-byte accesses (and 3-4x as many VMEM instructions again for the BN-backward operands).
+// Staging layout: [BM][BN] fp32, column XOR-swizzled by bits 2-3 of the row — the four row groups of
+// one MFMA write (rows 4q + e) land in four distinct 16-bank groups. The caller's operand buffers
+// must be idle (a barrier after the last K step's LDS reads).
+template <int MODE, int BM, int BN, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
+                                              int hw, int rw, int ph, int pw) {
+  constexpr int NF = BN / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  float* cst = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wr * 64 + i * 16 + 4 * (lane >> 4) + e;
+        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
+        cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
+      }
+  __syncthreads();
+
+  constexpr int CH = BN / 8, RP = NT / CH, PASSES = BM / RP, NW = NT / 64;
+  const int ch = tid % CH, rr = tid / CH;
+  const int col0 = n0 + ch * 8;
+  const bool chok = col0 < a.ncol;  // ncol is a multiple of 8
+  bf16* out = a.out + peer * a.out_ps;
+  const bf16* resid = a.resid ? a.resid + peer * a.resid_ps : nullptr;
+  // BN-backward epilogue (dgrad only)
+  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
+  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
+  const bf16* bmask = (bnb && a.bnb_mask) ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
+  const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
+  const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
+  const bool fstats = !bnb && a.stats != nullptr;
+  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], q0[8], q1[8], q2[8];
+  bool cval[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = col0 + j;
+    cval[j] = col < a.ncol_valid;
+    bv[j] = (a.bias != nullptr && cval[j]) ? a.bias[peer * a.bias_ps + col] : 0.f;
+    mean0[j] = inv0[j] = mean1[j] = inv1[j] = 0.f;
+    if (bnb && chok) {
+      const float* m0p = a.bnb_ms0 + peer * 2 * a.ncol;
+      mean0[j] = m0p[col];
+      inv0[j] = m0p[a.ncol + col];
+      if (bnb2) {
+        const float* m1p = a.bnb_ms1 + peer * 2 * a.ncol;
+        mean1[j] = m1p[col];
+        inv1[j] = m1p[a.ncol + col];
+      }
+    }
+    q0[j] = q1[j] = q2[j] = 0.f;
+  }
+  // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
+  auto out_row = [&](int m) -> int {
+    if (MODE != 2) return m;
+    const int img = m / hw, rem = m - img * hw;
+    const int hh = rem / rw, ww = rem - hh * rw;
+    return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
+  };
+  if (chok) {
+#pragma unroll 2
+    for (int p = 0; p < PASSES; ++p) {
+      const int row = rr + p * RP;
+      const int m = m0 + row;
+      if (m >= M) break;
+      const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
+      uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
+      if (resid != nullptr) ur = *reinterpret_cast<const uint4*>(resid + o);
+      if (bmask != nullptr) um = *reinterpret_cast<const uint4*>(bmask + o);
+      if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
+      if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
+      const int sw = ((row >> 2) & 3) << 4;
+      const float4 lo = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8) ^ sw));
+      const float4 hi = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8 + 4) ^ sw));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const bf8 br = __builtin_bit_cast(bf8, ur), bm = __builtin_bit_cast(bf8, um);
+      const bf8 b0 = __builtin_bit_cast(bf8, uy0), b1 = __builtin_bit_cast(bf8, uy1);
+      bf8 ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = v[j] + bv[j];
+        if (resid != nullptr) x += (float)br.v[j];
+        if (a.relu) x = fmaxf(x, 0.f);
+        if (!cval[j]) x = 0.f;
+        if (bnb) {
+          if (bmask != nullptr && !((float)bm.v[j] > 0.f)) x = 0.f;
+          ob.v[j] = (bf16)x;
+          const float g = (float)ob.v[j];  // the sums see exactly the g the BN apply reads back
+          q0[j] += g;
+          q1[j] += g * ((float)b0.v[j] - mean0[j]) * inv0[j];
+          if (bnb2) q2[j] += g * ((float)b1.v[j] - mean1[j]) * inv1[j];
+        } else {
+          ob.v[j] = (bf16)x;
+          q0[j] += x;
+          q1[j] += x * x;
+        }
+      }
+      *reinterpret_cast<uint4*>(out + o) = __builtin_bit_cast(uint4, ob);
+    }
+  }
+  if (!bnb && !fstats) return;
+  // per-column sums: over the wave's rows (lanes of one chunk) by shuffles, over the waves in LDS,
+  // then one atomic per column and statistic into the peer's accumulator
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int off = CH; off < 64; off <<= 1) {
+      q0[j] += __shfl_xor(q0[j], off);
+      q1[j] += __shfl_xor(q1[j], off);
+      if (bnb2) q2[j] += __shfl_xor(q2[j], off);
+    }
+  }
+  __syncthreads();  // staging tile no longer read
+  float* red = cst;  // [NW waves][3][BN]
+  if (lane < CH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wave * 3 + 0) * BN + ch * 8 + j] = q0[j];
+      red[(wave * 3 + 1) * BN + ch * 8 + j] = q1[j];
+      red[(wave * 3 + 2) * BN + ch * 8 + j] = q2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int col = n0 + tid;
+    if (col < a.ncol) {
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        t0 += red[(w * 3 + 0) * BN + tid];
+        t1 += red[(w * 3 + 1) * BN + tid];
+        t2 += red[(w * 3 + 2) * BN + tid];
+      }
+      if (bnb) {
+        float* p0 = a.bnb_part0 + peer * a.bnb_part_ps;
+        atomicAdd(p0 + col, t0);
+        atomicAdd(p0 + a.ncol + col, t1);
+        if (bnb2) {
+          float* p1 = a.bnb_part1 + peer * a.bnb_part_ps;
+          atomicAdd(p1 + col, t0);
+          atomicAdd(p1 + a.ncol + col, t2);
+        }
+      } else {
+        // BatchNorm batch statistics straight into the peer's [2][ncol] accumulator (bn_finalize
+        // reads and re-zeroes it)
+        float* st = a.stats + peer * a.stats_ps;
+        atomicAdd(st + col, t0);
+        atomicAdd(st + a.ncol + col, t1);
+      }
+    }
+  }
 }
 
 template <int MODE, int BN, bool PRO>
@@ -317,6 +480,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
 
+  static_assert(BM * BN * 4 <= 2 * BUF * 2, "staging tile must fit the operand buffers");
   // one register stage (loads of K-step kt+1 in flight during kt's MFMAs); measured: a second
   // register stage with LDS-only barriers is 20-60 % slower here (VGPR pressure, occupancy)
   if (nk > 0) {
@@ -349,159 +513,158 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   }
 
   // ---------------------------------------------------------------- epilogue
-  // The accumulator tile goes through LDS (fp32, the 64 KB / 48 KB operand buffers are free now) so
-  // that every thread then owns one 16-byte chunk (8 channels) of a row: bias, residual, mask and y
-  // operands are 16-byte loads and the output a 16-byte store. Straight from the MFMA layout a lane
-  // holds 1 column x 16 rows, i.e. 2-byte accesses (and 3-4x as many VMEM instructions again for
-  // the BN-backward operands).
-  // Staging layout: [BM][BN] fp32, column XOR-swizzled by bits 2-3 of the row — the four row groups
-  // of one MFMA write (rows 4q + e) land in four distinct 16-bank groups.
-  float* cst = reinterpret_cast<float*>(lds);
-  static_assert(BM * BN * 4 <= 2 * BUF * 2, "staging tile must fit the operand buffers");
+  conv_epilogue<MODE, BM, BN, 256>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw);
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward-shaped convs (MODE 0 without the BN prologue, MODE 4) through an LDS-DMA stage ring
+// ------------------------------------------------------------------------------------------------
+// k_conv_fwd_dma<MODE, BM, BN, NS, MINB>: the same implicit GEMM as k_conv_gemm's forward gathers,
+// restructured around gfx950 direct-to-LDS loads (buffer_load_dwordx4 ... lds):
+//   BM x BN tiles, 2 BM threads (BM / 32 waves as (BM / 64) x 2, each 64 x BN/2 — the same per-wave
+//   MFMA block as k_conv_gemm), NS LDS stages of [BM][64] A + [BN][64] B, MINB workgroups per CU.
+//   Every operand chunk goes HBM/L2 -> LDS with no VGPR destination: the K loop keeps NS - 1 stages
+//   in flight across its barriers (counted vmcnt, raw s_barrier — __syncthreads() would drain them),
+//   instead of the register stage of k_conv_gemm, which covers one K step of MFMAs (the convs were
+//   latency-bound: 43-58 % of wave cycles waiting, profiles/r2l_cnn_pmc).
+//   LDS-DMA writes lane l of a wave instruction at base + 16 l, so a wave instruction fills 8
+//   contiguous 128-byte rows; the XOR chunk swizzle of swz() is applied on the SOURCE side: lane l
+//   loads logical chunk (l & 7) ^ ((row >> 1) & 7), which for rows 8 (w + NW i) + (l >> 3) (NW waves,
+//   even) is the same chunk cc for all of a thread's rows — so one incremental (r, s, c8) tap walk
+//   per thread serves every A row, and the B rows (K-contiguous weight rows) use the same chunk.
+//   Padding taps, rows past the batch and K past R*S*C load through an out-of-range offset: the
+//   buffer unit writes zeros.
+// Configurations (conv_gemm_launch, measured on the ResNet-18 shapes, profiles/r3z_conv_dma): two
+// stages and more workgroups per CU beat a deeper ring — 128 x 128 / 2 stages / 2 per CU for the wide
+// layers and 128 x 64 / 2 stages / 3 per CU for the 64-channel ones are 10-15 % faster than the
+// register stage on every forward and MODE 4 shape (layer-4 forward 90.0 -> 76.1 us, 1016 TF/s;
+// layer-1 forward 159.1 -> 135.5 us); 256 x 128 / 3 stages / 1 per CU is 12 % faster on layers 3-4
+// only, and 3-stage 64-channel tiles are slower than the register stage (short K: 9 K steps).
+// The epilogue (bias, residual, ReLU, BN sums / BN-backward sums) is conv_epilogue.
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void conv_dma16(__amdgpu_buffer_rsrc_t r, bf16* lds_wave_base, int byte_off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, byte_off, 0, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int MODE, int BM, int BN, int NS, int MINB>
+__global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, int tiles_m, int tiles_n) {
+  static_assert(MODE == 0 || MODE == 4, "forward-shaped gathers only");
+  constexpr int NT = 2 * BM, NW = NT / 64;
+  constexpr int AR = BM * 8 / NT;  // A 16-byte chunks per thread per K step (4)
+  constexpr int NB = BN * 8 / NT;  // B chunks per thread per K step
+  static_assert(NB >= 1 && NW % 2 == 0, "tile shape");
+  constexpr int G = AR + NB;       // LDS-DMA instructions per thread per stage
+  constexpr int NF = BN / 32;
+  constexpr int STAGE = (BM + BN) * CG_BK;
+  constexpr int OPER = NS * STAGE, EPI = BM * BN * 2;  // bf16 units (the epilogue stages fp32)
+  static_assert(NS >= 2 && NS <= 4, "stage ring depth");
+  // one LDS object only: a second one makes hipcc wait vmcnt(0) before the K loop's LDS reads
+  __shared__ __attribute__((aligned(16))) bf16 lds[OPER > EPI ? OPER : EPI];
+
+  const int peer = blockIdx.z;
+  const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
+  const int hw = a.out_h * a.out_w;
+  const int M = nb * hw;
+  const int wgid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= M) return;  // tile past this peer's batch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(a.src + peer * a.src_ps), rs_wt = conv_rsrc(a.wt + peer * a.wt_ps);
+  const int Ktot = a.R * a.S * a.src_c;
+  const int nk = (Ktot + CG_BK - 1) / CG_BK;
+  const int cc = (lane & 7) ^ (((wave & 1) << 2) | (lane >> 4));  // this thread's logical 16-byte chunk
+  const int cpp = a.src_c >> 3;
+
+  // A rows 8 (wave + NW i) + (lane >> 3): source coordinate of tap (0, 0) and its element offset
+  int a_bh[AR], a_bw[AR], a_pixc[AR];
+  bool a_ok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + 8 * (wave + NW * i) + (lane >> 3);
+    a_ok[i] = m < M;
+    const int mm = a_ok[i] ? m : 0;
+    const int img = mm / hw, rem = mm - img * hw;
+    const int oh = rem / a.out_w, ow = rem - oh * a.out_w;
+    a_bh[i] = oh * a.stride - a.pad;
+    a_bw[i] = ow * a.stride - a.pad;
+    a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
+  }
+  int b_off[NB];  // element offset of this thread's weight rows (K-contiguous), -1: past ncol
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + 8 * (wave + NW * i) + (lane >> 3);
+    b_off[i] = n < a.ncol ? n * Ktot : -1;
+  }
+  // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
+  int ar = 0, as_ = 0, ac8 = cc, kk = cc * 8;
+  while (ac8 >= cpp) {
+    ac8 -= cpp;
+    if (++as_ == a.S) { as_ = 0; ++ar; }
+  }
+  auto issue = [&](int buf) {
+    bf16* As = lds + buf * STAGE;
+    bf16* Bs = As + BM * CG_BK;
+    const bool kok = ar < a.R;
+    const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const bool ok = kok && a_ok[i] && (unsigned)(a_bh[i] + ar) < (unsigned)a.src_h && (unsigned)(a_bw[i] + as_) < (unsigned)a.src_w;
+      conv_dma16(rs_src, As + 8 * (wave + NW * i) * CG_BK, ok ? (a_pixc[i] + tapc) * 2 : CONV_OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) conv_dma16(rs_wt, Bs + 8 * (wave + NW * i) * CG_BK, (kk < Ktot && b_off[i] >= 0) ? (b_off[i] + kk) * 2 : CONV_OOB);
+    ac8 += 8;
+    kk += CG_BK;
+    while (ac8 >= cpp) {
+      ac8 -= cpp;
+      if (++as_ == a.S) { as_ = 0; ++ar; }
+    }
+  };
+  f32x4 acc[4][NF];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NF; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wr * 64 + i * 16 + 4 * (lane >> 4) + e;
-        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
-        cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
-      }
-  __syncthreads();
+    for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
 
-  constexpr int CH = BN / 8, RP = 256 / CH, PASSES = BM / RP;
-  const int ch = tid % CH, rr = tid / CH;
-  const int col0 = n0 + ch * 8;
-  const bool chok = col0 < a.ncol;  // ncol is a multiple of 8
-  bf16* out = a.out + peer * a.out_ps;
-  const bf16* resid = a.resid ? a.resid + peer * a.resid_ps : nullptr;
-  // BN-backward epilogue (dgrad only)
-  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
-  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
-  const bf16* bmask = (bnb && a.bnb_mask) ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
-  const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
-  const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
-  const bool fstats = !bnb && a.stats != nullptr;
-  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], q0[8], q1[8], q2[8];
-  bool cval[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = col0 + j;
-    cval[j] = col < a.ncol_valid;
-    bv[j] = (a.bias != nullptr && cval[j]) ? a.bias[peer * a.bias_ps + col] : 0.f;
-    mean0[j] = inv0[j] = mean1[j] = inv1[j] = 0.f;
-    if (bnb && chok) {
-      const float* m0p = a.bnb_ms0 + peer * 2 * a.ncol;
-      mean0[j] = m0p[col];
-      inv0[j] = m0p[a.ncol + col];
-      if (bnb2) {
-        const float* m1p = a.bnb_ms1 + peer * 2 * a.ncol;
-        mean1[j] = m1p[col];
-        inv1[j] = m1p[a.ncol + col];
-      }
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
+  int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
+  for (int kt = 0; kt < nk; ++kt) {
+    // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
+    const int ahead = nk - 1 - kt;
+    if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G>();
+    else if (NS >= 3 && ahead >= 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
+    if (kt + NS - 1 < nk) issue(wb);
+    const bf16* As = lds + rd * STAGE;
+    const bf16* Bs = As + BM * CG_BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = h * 4 + (lane >> 4);
+      bf16x8 af[4], bfr[NF];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
     }
-    q0[j] = q1[j] = q2[j] = 0.f;
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    wb = wb + 1 == NS ? 0 : wb + 1;
   }
-  // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
-  auto out_row = [&](int m) -> int {
-    if (MODE != 2) return m;
-    const int img = m / hw, rem = m - img * hw;
-    const int hh = rem / rw, ww = rem - hh * rw;
-    return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
-  };
-  if (chok) {
-#pragma unroll 2
-    for (int p = 0; p < PASSES; ++p) {
-      const int row = rr + p * RP;
-      const int m = m0 + row;
-      if (m >= M) break;
-      const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
-      uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
-      if (resid != nullptr) ur = *reinterpret_cast<const uint4*>(resid + o);
-      if (bmask != nullptr) um = *reinterpret_cast<const uint4*>(bmask + o);
-      if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
-      if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
-      const int sw = ((row >> 2) & 3) << 4;
-      const float4 lo = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8) ^ sw));
-      const float4 hi = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8 + 4) ^ sw));
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const bf8 br = __builtin_bit_cast(bf8, ur), bm = __builtin_bit_cast(bf8, um);
-      const bf8 b0 = __builtin_bit_cast(bf8, uy0), b1 = __builtin_bit_cast(bf8, uy1);
-      bf8 ob;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x = v[j] + bv[j];
-        if (resid != nullptr) x += (float)br.v[j];
-        if (a.relu) x = fmaxf(x, 0.f);
-        if (!cval[j]) x = 0.f;
-        if (bnb) {
-          if (bmask != nullptr && !((float)bm.v[j] > 0.f)) x = 0.f;
-          ob.v[j] = (bf16)x;
-          const float g = (float)ob.v[j];  // the sums see exactly the g the BN apply reads back
-          q0[j] += g;
-          q1[j] += g * ((float)b0.v[j] - mean0[j]) * inv0[j];
-          if (bnb2) q2[j] += g * ((float)b1.v[j] - mean1[j]) * inv1[j];
-        } else {
-          ob.v[j] = (bf16)x;
-          q0[j] += x;
-          q1[j] += x * x;
-        }
-      }
-      *reinterpret_cast<uint4*>(out + o) = __builtin_bit_cast(uint4, ob);
-    }
-  }
-  if (!bnb && !fstats) return;
-  // per-column sums: over the wave's rows (lanes of one chunk) by shuffles, over the 4 waves in LDS,
-  // then one atomic per column and statistic into the peer's accumulator
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int off = CH; off < 64; off <<= 1) {
-      q0[j] += __shfl_xor(q0[j], off);
-      q1[j] += __shfl_xor(q1[j], off);
-      if (bnb2) q2[j] += __shfl_xor(q2[j], off);
-    }
-  }
-  __syncthreads();  // staging tile no longer read
-  float* red = cst;  // [4 waves][3][BN]
-  if (lane < CH) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[(wave * 3 + 0) * BN + ch * 8 + j] = q0[j];
-      red[(wave * 3 + 1) * BN + ch * 8 + j] = q1[j];
-      red[(wave * 3 + 2) * BN + ch * 8 + j] = q2[j];
-    }
-  }
-  __syncthreads();
-  if (tid < BN) {
-    const int col = n0 + tid;
-    if (col < a.ncol) {
-      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        t0 += red[(w * 3 + 0) * BN + tid];
-        t1 += red[(w * 3 + 1) * BN + tid];
-        t2 += red[(w * 3 + 2) * BN + tid];
-      }
-      if (bnb) {
-        float* p0 = a.bnb_part0 + peer * a.bnb_part_ps;
-        atomicAdd(p0 + col, t0);
-        atomicAdd(p0 + a.ncol + col, t1);
-        if (bnb2) {
-          float* p1 = a.bnb_part1 + peer * a.bnb_part_ps;
-          atomicAdd(p1 + col, t0);
-          atomicAdd(p1 + a.ncol + col, t2);
-        }
-      } else {
-        // BatchNorm batch statistics straight into the peer's [2][ncol] accumulator (bn_finalize
-        // reads and re-zeroes it)
-        float* st = a.stats + peer * a.stats_ps;
-        atomicAdd(st + col, t0);
-        atomicAdd(st + a.ncol + col, t1);
-      }
-    }
-  }
+  __syncthreads();  // operand stages idle: the epilogue stages the tile over them
+  conv_epilogue<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, a.out_w, 0, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -672,6 +835,23 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+// forward-shaped convs through k_conv_fwd_dma (default) or k_conv_gemm's register stage
+// (MYFYP_CONV_DMA=0, or conv_set_dma(0): the A/B switch)
+static int g_conv_dma = -1;
+static bool conv_dma_enabled() {
+  if (g_conv_dma < 0) {
+    const char* e = getenv("MYFYP_CONV_DMA");
+    g_conv_dma = e != nullptr ? atoi(e) : 1;
+  }
+  return g_conv_dma != 0;
+}
+extern "C" int conv_set_dma(int v) {
+  conv_dma_enabled();
+  const int old = g_conv_dma;
+  if (v >= 0) g_conv_dma = v;
+  return old;
+}
+
 extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, void* stream) {
   const ConvGemmArgs& a = *pa;
   // mode 0 forward, 1 dgrad, 4 stride-1 dgrad as a forward conv over dY with k_conv_wt_flip weights
@@ -683,12 +863,41 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
                        (int64_t)a.ncol * a.R * a.S * a.src_c * 2 >= INT32_MAX))
     return 3;
   const bool wide = a.ncol > 64;
+  hipStream_t s = (hipStream_t)stream;
+  if ((mode == 4 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
+    // variant code (conv_set_dma / MYFYP_CONV_DMA): 1 = the measured defaults below; otherwise bits
+    // 1-2 pick the 64-channel tile (0 register stage, 1 128x64/3 stages/2 per CU, 2 128x64/2/3,
+    // 3 256x64/3/1) and bits 3-4 the wide one (0 register stage, 1 256x128/3/1, 2 128x128/2/2)
+    int v = g_conv_dma;
+    if (v == 1) v = (2 << 1) | (2 << 3);  // measured best for every ResNet-18 shape (profiles/r3z_conv_dma)
+    const int var = wide ? (v >> 3) & 3 : (v >> 1) & 3;
+    if (var != 0) {
+      const int bm = (wide ? var == 1 : var == 3) ? 256 : 128, bn = wide ? 128 : 64;
+      const int tiles_m = (a.max_batch * a.out_h * a.out_w + bm - 1) / bm;
+      const int tiles_n = (a.ncol + bn - 1) / bn;
+      dim3 grid(tiles_m * tiles_n, 1, peers), block(2 * bm);
+#define DMA_LAUNCH(BM_, BN_, NS_, MB_)                                                                                   \
+  do {                                                                                                                   \
+    if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_dma<4, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n); \
+    else hipLaunchKernelGGL((k_conv_fwd_dma<0, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n);          \
+  } while (0)
+      if (wide) {
+        if (var == 1) DMA_LAUNCH(256, 128, 3, 1);
+        else DMA_LAUNCH(128, 128, 2, 2);
+      } else {
+        if (var == 1) DMA_LAUNCH(128, 64, 3, 2);
+        else if (var == 2) DMA_LAUNCH(128, 64, 2, 3);
+        else DMA_LAUNCH(256, 64, 3, 1);
+      }
+#undef DMA_LAUNCH
+      return hipGetLastError() == hipSuccess ? 0 : 2;
+    }
+  }
   const bool parity = mode == 1 && a.stride == 2;  // strided dgrad: one launch row per parity class
   const int rows = parity ? ((a.out_h + 1) >> 1) * ((a.out_w + 1) >> 1) : a.out_h * a.out_w;
   const int tiles_m = (a.max_batch * rows + 127) / 128;
   const int tiles_n = (a.ncol + (wide ? 127 : 63)) / (wide ? 128 : 64);
   dim3 grid(tiles_m * tiles_n, parity ? 4 : 1, peers), block(256);
-  hipStream_t s = (hipStream_t)stream;
 #define CG_LAUNCH(M_, BN_, P_) hipLaunchKernelGGL((k_conv_gemm<M_, BN_, P_>), grid, block, 0, s, a, tiles_m, tiles_n)
   if (mode == 4) {
     if (wide) CG_LAUNCH(4, 128, false);

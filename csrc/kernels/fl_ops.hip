@@ -102,13 +102,15 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ 
     }
     for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
       float acc = 0.f;
-      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       out[i] = acc;
     }
   } else {
     for (int64_t i = t0; i < n; i += stride) {
       float acc = 0.f;
-      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       out[i] = acc;
     }
   }
@@ -156,14 +158,16 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_local(float* __restrict__ s
     }
     for (int64_t i = n4 * 4 + blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
       float acc = 0.f;
-      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       for (int p = 0; p < P; ++p)
         if ((mask >> p) & 1ull) stacked[p * ld + i] = acc * inv;
     }
   } else {
     for (int64_t i = blockIdx.x * FL_BLOCK + threadIdx.x; i < n; i += stride) {
       float acc = 0.f;
-      for (int p = 0; p < P; ++p) acc += w.w[p] * stacked[p * ld + i];
+      for (int p = 0; p < P; ++p)
+        if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       for (int p = 0; p < P; ++p)
         if ((mask >> p) & 1ull) stacked[p * ld + i] = acc * inv;
     }

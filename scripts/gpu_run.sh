@@ -46,6 +46,11 @@ for step in "$@"; do
       run resnet_buf 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       MYFYP_NATIVE_LIB=build/base_CONV_BUFLOAD0/libmyfyp_hip.so run resnet_base 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       run resnet_buf2 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
+    dmaab)  # forward-shaped convs: LDS-DMA stage ring (default) vs register stage (MYFYP_CONV_DMA=0)
+      run conv_ab_dma 300 python scripts/probes/conv_ab.py
+      run resnet_dma 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      MYFYP_CONV_DMA=0 run resnet_reg 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      run resnet_dma2 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

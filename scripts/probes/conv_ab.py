@@ -1,4 +1,5 @@
-"""Time the conv GEMM (forward / dgrad) on ResNet-18 CIFAR shapes, 8 peers, batch 128 (TF/s per shape)."""
+"""Time the conv GEMM (forward / dgrad) on ResNet-18 CIFAR shapes, 8 peers, batch 128 (TF/s per shape);
+forward-shaped modes 0 / 4 through the LDS-DMA kernel (dma) and the register-staged one (reg)."""
 import ctypes
 import sys
 import os
@@ -22,41 +23,49 @@ for name, cin, cout, h, st in shapes:
     dx = torch.empty(P, B * h * h * cin, device=dev, dtype=torch.bfloat16)
     flops = 2 * P * B * ho * ho * cout * 9 * cin
     wt = torch.empty_like(wf)
+    # conv_set_dma variant codes: 0 register stage; narrow (64 channels) 3 / 5 / 7 = 128x64 3 stages 2 per CU /
+    # 128x64 2 stages 3 per CU / 256x64 3 stages 1 per CU; wide 9 / 17 = 256x128 3 stages / 128x128 2 stages 2 per CU
+    VARIANTS = {3: "128x64/3", 5: "128x64/2", 7: "256x64/3", 9: "256x128/3", 17: "128x128/2", 0: "reg"}
     for mode in (0, 1, 4):
         if mode == 4 and st != 1:
             continue
-        a = ConvGemmArgs()
-        if mode == 0:
-            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = x.data_ptr(), x.shape[1], h, h, cin
-            a.out_h, a.out_w, a.ncol, a.ncol_valid = ho, ho, cout, cout
-            a.out, a.out_ps = y.data_ptr(), y.shape[1]
-        else:
-            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
-            a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
-            a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
-        a.R = a.S = 3
-        a.stride, a.pad = st, 1
-        a.wt, a.wt_ps, a.max_batch = wf.data_ptr(), wf.shape[1], B
-        s = torch.cuda.current_stream().cuda_stream
-        if mode == 4:  # dgrad as a forward conv over dY: flipped weights (timed with the conv), pad R-1-pad
-            a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
-            a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
-            a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
-            a.wt, a.pad = wt.data_ptr(), 1
+        narrow = (cout if mode == 0 else cin) <= 64
+        codes = [0] if mode == 1 else ([0, 3, 5, 7] if narrow else [0, 9, 17])
+        for dma in codes:
+            lib.conv_set_dma(dma)
+            a = ConvGemmArgs()
+            if mode == 0:
+                a.src, a.src_ps, a.src_h, a.src_w, a.src_c = x.data_ptr(), x.shape[1], h, h, cin
+                a.out_h, a.out_w, a.ncol, a.ncol_valid = ho, ho, cout, cout
+                a.out, a.out_ps = y.data_ptr(), y.shape[1]
+            else:
+                a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
+                a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
+                a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
+            a.R = a.S = 3
+            a.stride, a.pad = st, 1
+            a.wt, a.wt_ps, a.max_batch = wf.data_ptr(), wf.shape[1], B
+            s = torch.cuda.current_stream().cuda_stream
+            if mode == 4:  # dgrad as a forward conv over dY: flipped weights (timed with the conv), pad R-1-pad
+                a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
+                a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
+                a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
+                a.wt, a.pad = wt.data_ptr(), 1
 
-        def launch():
-            if mode == 4:
-                assert lib.conv_wt_flip_launch(wf.data_ptr(), wf.shape[1], wt.data_ptr(), wt.shape[1], cout, cin, 3, 3, P, s) == 0
-            assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, s) == 0
+            def launch():
+                if mode == 4:
+                    assert lib.conv_wt_flip_launch(wf.data_ptr(), wf.shape[1], wt.data_ptr(), wt.shape[1], cout, cin, 3, 3, P, s) == 0
+                assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, s) == 0
 
-        for _ in range(3):
-            launch()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(20):
-            launch()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / 20 * 1000
-        useful = flops if mode == 0 or st == 1 else flops  # dgrad useful work = forward FLOPs
-        print(f"{name:18s} mode {mode}: {us:8.1f} us ({useful / us / 1e6:6.0f} TF/s useful)", flush=True)
+            for _ in range(3):
+                launch()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                launch()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / 20 * 1000
+            useful = flops if mode == 0 or st == 1 else flops  # dgrad useful work = forward FLOPs
+            print(f"{name:18s} mode {mode} {VARIANTS[dma]:10s}: {us:8.1f} us ({useful / us / 1e6:6.0f} TF/s useful)", flush=True)
+lib.conv_set_dma(1)

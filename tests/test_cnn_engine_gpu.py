@@ -26,8 +26,21 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
+@pytest.fixture(params=[1, 0, 3, 7, 9], ids=["dma", "regstage", "dma128x64s3", "dma256x64s3", "dma256x128s3"])
+def conv_dma(request):
+    """Forward-shaped convs (mode 0, mode 4) through the LDS-DMA stage-ring kernel (1: the default
+    tiles, 128x64 / 128x128 with 2 stages; 3 / 7 / 9: the 3-stage variants, see conv_gemm_launch) or
+    the register-staged k_conv_gemm (0); restored afterwards."""
+    from myfyp_amd.parallel.cnn_engine import _lib
+
+    lib = _lib()
+    old = lib.conv_set_dma(request.param)
+    yield request.param
+    lib.conv_set_dma(old)
+
+
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3)])
-def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
+def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma):
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
 
     lib = _lib()
@@ -104,7 +117,7 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n):
 
 @pytest.mark.parametrize("cin,cout,stride,h,n,two,mode", [(64, 64, 1, 16, 3, False, 1), (64, 128, 2, 16, 2, True, 1), (128, 128, 1, 8, 4, True, 1),
                                                           (64, 64, 1, 16, 3, False, 4), (128, 128, 1, 8, 4, True, 4), (64, 128, 1, 8, 2, True, 4)])
-def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode):
+def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode, conv_dma):
     """dgrad with the BN-backward epilogue: out = bf16(dX + resid) * [mask > 0] and per-channel
     (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op. mode 4: the
     stride-1 dgrad as a forward conv over dY with flipped weights (what the engine runs)."""
