@@ -272,9 +272,13 @@ __global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, 
   if (c >= Cp) return;
   float* cp = coef + peer * 3 * Cp;
   float* pp = const_cast<float*>(part) + peer * part_ps;
-  const float sg = pp[c], sgx = pp[Cp + c];
-  pp[c] = 0.f;
-  pp[Cp + c] = 0.f;
+  float sg = 0.f, sgx = 0.f;  // nblk accumulator rows [nblk][2][Cp] (spread atomics), re-armed
+  for (int r = 0; r < nblk; ++r) {
+    sg += pp[r * 2 * Cp + c];
+    sgx += pp[r * 2 * Cp + Cp + c];
+    pp[r * 2 * Cp + c] = 0.f;
+    pp[r * 2 * Cp + Cp + c] = 0.f;
+  }
   if (c >= C) {
     cp[c] = 0.f; cp[Cp + c] = 0.f; cp[2 * Cp + c] = 0.f;
     return;

@@ -49,6 +49,10 @@ struct ConvGemmArgs {
   const bf16* bnb_y1; int64_t bnb_y1_ps;
   const float* bnb_ms0; const float* bnb_ms1;
   float* bnb_part0; float* bnb_part1; int64_t bnb_part_ps;
+  // accumulator rows of `stats` ([rows][2][ncol] per peer; 0 = 1): the epilogue of M tile t adds
+  // into row t % rows, so the tiles' fp32 atomics spread over `rows` addresses per column
+  int stats_rows;
+  int bnb_rows;  // same for the BN-backward partials bnb_part0/1 ([rows][2][ncol] per peer)
 };
 
 struct WgradArgs {

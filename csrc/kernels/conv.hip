@@ -247,18 +247,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
         t2 += red[(w * 3 + 2) * BN + tid];
       }
       if (bnb) {
-        float* p0 = a.bnb_part0 + peer * a.bnb_part_ps;
+        const int prow = (m0 >> 7) % (a.bnb_rows > 1 ? a.bnb_rows : 1);
+        float* p0 = a.bnb_part0 + peer * a.bnb_part_ps + prow * 2 * a.ncol;
         atomicAdd(p0 + col, t0);
         atomicAdd(p0 + a.ncol + col, t1);
         if (bnb2) {
-          float* p1 = a.bnb_part1 + peer * a.bnb_part_ps;
+          float* p1 = a.bnb_part1 + peer * a.bnb_part_ps + prow * 2 * a.ncol;
           atomicAdd(p1 + col, t0);
           atomicAdd(p1 + a.ncol + col, t2);
         }
       } else {
         // BatchNorm batch statistics straight into the peer's [2][ncol] accumulator (bn_finalize
         // reads and re-zeroes it)
-        float* st = a.stats + peer * a.stats_ps;
+        float* st = a.stats + peer * a.stats_ps + ((m0 >> 7) % (a.stats_rows > 1 ? a.stats_rows : 1)) * 2 * a.ncol;
         atomicAdd(st + col, t0);
         atomicAdd(st + a.ncol + col, t1);
       }
@@ -670,6 +671,33 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
 // ------------------------------------------------------------------------------------------------
 // weight gradient
 // ------------------------------------------------------------------------------------------------
+// Wf-layout gradient [dy_c][ncol_tot] of one wgrad tile: lanes 0..15 of a row group write 16
+// consecutive floats (fp32 atomics when the pixel dimension is split)
+template <int BM, int BN>
+__device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&acc)[BM / 32][BN / 32], int peer, int co0, int n0, int ncol_tot) {
+  constexpr int FM = BM / 32, FN = BN / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  float* grad = a.grad + peer * a.grad_ps;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+    if (n >= ncol_tot) continue;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
+        if (co < a.dy_c) {
+          float* dst = grad + (int64_t)co * ncol_tot + n;
+          if (a.accumulate) atomicAdd(dst, acc[i][j][e]);
+          else *dst = acc[i][j][e];
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN, bool PRO>
 __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, int tiles_n, int splits) {
   constexpr int FM = BM / 32, FN = BN / 32;       // fragments per wave
@@ -811,25 +839,126 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(WgradArgs a, int tiles_m, in
     cur ^= 1;
   }
 
-  // Wf-layout gradient [dy_c][ncol_tot]: lanes 0..15 of a row group write 16 consecutive floats
-  float* grad = a.grad + peer * a.grad_ps;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
-    if (n >= ncol_tot) continue;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
-        if (co < a.dy_c) {
-          float* dst = grad + (int64_t)co * ncol_tot + n;
-          if (a.accumulate) atomicAdd(dst, acc[i][j][e]);
-          else *dst = acc[i][j][e];
-        }
-      }
-    }
+  wgrad_store<BM, BN>(a, acc, peer, co0, n0, ncol_tot);
+}
+
+// k_conv_wgrad_dma<BM, BN, NS, MINB>: k_conv_wgrad with its operands staged by LDS-DMA into an
+// NS-stage ring (no register stage, counted vmcnt + raw barriers; see k_conv_fwd_dma). A thread
+// keeps the rows of the register-staged kernel (a wave instruction fills 64 / CW consecutive rows of
+// the [64][W] image, W / 8 = CW chunks per row); the transposed-read layout tr_off<W> permutes 16-byte
+// chunks by trf<W>(row) / 2, which is the same for all of a thread's rows, so the thread loads the
+// fixed logical chunk (lane % CW) ^ (trf(row) / 2) — one (r, s, ci) column per thread as before.
+// No BN prologue (PRO launches take k_conv_wgrad).
+template <int BM, int BN, int NS, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_conv_wgrad_dma(WgradArgs a, int tiles_m, int tiles_n, int splits) {
+  constexpr int FM = BM / 32, FN = BN / 32;
+  constexpr int CA = BM / 8, CB = BN / 8;
+  constexpr int NA = 64 * CA / 256, NBr = 64 * CB / 256;
+  constexpr int G = NA + NBr;  // LDS-DMA instructions per thread per stage
+  constexpr int STAGE = 64 * (BM + BN);
+  static_assert(NS >= 2 && NS <= 3, "stage ring depth");
+  __shared__ __attribute__((aligned(16))) bf16 lds[NS * STAGE];  // the only LDS object (see k_conv_fwd_dma)
+
+  const int peer = blockIdx.z;
+  const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
+  const int M = nb * a.Ho * a.Wo;
+  const int ntile = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, ntile * splits);
+  const int split = wgid / ntile, tile = wgid - split * ntile;
+  const int kbeg = split * a.k_per_split;
+  const int kend = min(M, kbeg + a.k_per_split);
+  if (kbeg >= kend) return;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(a.dy + peer * a.dy_ps), rs_x = conv_rsrc(a.x + peer * a.x_ps);
+  const int hwo = a.Ho * a.Wo;
+  const int ncol_tot = a.R * a.S * a.x_c;
+
+  // logical chunks of this thread (source-side swizzle), fixed for the whole loop
+  const int cca = (lane % CA) ^ (trf<BM>(tid / CA) >> 1);
+  const int ccb = (lane % CB) ^ (trf<BN>(tid / CB) >> 1);
+  const int nb0 = n0 + ccb * 8;
+  const bool bcol_ok = nb0 < ncol_tot;
+  int br = 0, bs = 0, bci = 0;
+  if (bcol_ok) {
+    const int rs = nb0 / a.x_c;
+    bci = nb0 - rs * a.x_c;
+    br = rs / a.S;
+    bs = rs - br * a.S;
   }
+  const bool acol_ok = co0 + cca * 8 < a.dy_c;
+  int b_img[NBr], b_oh[NBr], b_ow[NBr];
+#pragma unroll
+  for (int i = 0; i < NBr; ++i) {
+    const int m = kbeg + tid / CB + (256 / CB) * i;
+    b_img[i] = m / hwo;
+    const int rem = m - b_img[i] * hwo;
+    b_oh[i] = rem / a.Wo;
+    b_ow[i] = rem - b_oh[i] * a.Wo;
+  }
+  const int d_img = 64 / hwo, d_rem = 64 - d_img * hwo, d_oh = d_rem / a.Wo, d_ow = d_rem - d_oh * a.Wo;
+  const int hb = br - a.pad, wb0 = bs - a.pad;
+  int m_next = kbeg;  // first pixel of the next K step to issue
+  auto issue = [&](int buf) {
+    bf16* As = lds + buf * STAGE;
+    bf16* Bs = As + 64 * BM;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = m_next + tid / CA + (256 / CA) * i;
+      conv_dma16(rs_dy, As + ((64 / CA) * wave + (256 / CA) * i) * BM, (acol_ok && m < kend) ? (m * a.dy_c + co0 + cca * 8) * 2 : CONV_OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < NBr; ++i) {
+      const int m = m_next + tid / CB + (256 / CB) * i;
+      const int h = b_oh[i] * a.stride + hb, w = b_ow[i] * a.stride + wb0;
+      const bool ok = bcol_ok && m < kend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      conv_dma16(rs_x, Bs + ((64 / CB) * wave + (256 / CB) * i) * BN, ok ? (((b_img[i] * a.H + h) * a.W + w) * a.x_c + bci) * 2 : CONV_OOB);
+      b_ow[i] += d_ow;
+      if (b_ow[i] >= a.Wo) { b_ow[i] -= a.Wo; ++b_oh[i]; }
+      b_oh[i] += d_oh;
+      if (b_oh[i] >= a.Ho) { b_oh[i] -= a.Ho; ++b_img[i]; }
+      b_img[i] += d_img;
+    }
+    m_next += 64;
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = zero4();
+
+  const int nk = (kend - kbeg + 63) / 64;
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) issue(st);
+  int rd = 0, wbuf = NS - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt;
+    if (NS >= 3 && ahead >= 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
+    if (kt + NS - 1 < nk) issue(wbuf);
+    const bf16* As = lds + rd * STAGE;
+    const bf16* Bs = As + 64 * BM;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag_tr<BM>(As, wr * (BM / 2) + i * 16, h * 32, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag_tr<BN>(Bs, wc * (BN / 2) + j * 16, h * 32, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+    }
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    wbuf = wbuf + 1 == NS ? 0 : wbuf + 1;
+  }
+  wgrad_store<BM, BN>(a, acc, peer, co0, n0, ncol_tot);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -867,7 +996,8 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   if ((mode == 4 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
     // variant code (conv_set_dma / MYFYP_CONV_DMA): 1 = the measured defaults below; otherwise bits
     // 1-2 pick the 64-channel tile (0 register stage, 1 128x64/3 stages/2 per CU, 2 128x64/2/3,
-    // 3 256x64/3/1) and bits 3-4 the wide one (0 register stage, 1 256x128/3/1, 2 128x128/2/2)
+    // 3 256x64/3/1), bits 3-4 the wide one (0 register stage, 1 256x128/3/1, 2 128x128/2/2) and
+    // bits 5-6 the weight gradient's (conv_wgrad_launch)
     int v = g_conv_dma;
     if (v == 1) v = (2 << 1) | (2 << 3);  // measured best for every ResNet-18 shape (profiles/r3z_conv_dma)
     const int var = wide ? (v >> 3) & 3 : (v >> 1) & 3;
@@ -967,7 +1097,27 @@ extern "C" int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, lo
 }
 
 // rows of the BN statistics buffer a conv epilogue writes: one (sum, sumsq) accumulator row
-extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) { return 1; }
+// (MYFYP_BN_STAT_ROWS, default 16: the 64-channel forward convs were bound by 1024 workgroups per
+// peer adding into the same 128 addresses — 144 -> 122 us per conv with 16 rows, profiles/r3z_conv_dma)
+extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) {
+  static int rows = -1;
+  if (rows < 0) {
+    const char* e = getenv("MYFYP_BN_STAT_ROWS");
+    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 16;
+  }
+  const int tiles = (max_batch * out_h * out_w + 127) / 128;
+  return rows < tiles ? rows : (tiles > 0 ? tiles : 1);
+}
+// rows of the BN-backward partial-sum buffers (MYFYP_BNB_ROWS, default 16; conv epilogues and
+// k_bn_bwd_reduce accumulate into them, k_bn_bwd_finalize sums and re-zeroes every row)
+extern "C" int conv_bnb_rows() {
+  static int rows = -1;
+  if (rows < 0) {
+    const char* e = getenv("MYFYP_BNB_ROWS");
+    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 16;
+  }
+  return rows;
+}
 
 extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, void* stream) {
   const WgradArgs& a = *pa;
@@ -982,6 +1132,27 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   const int tiles_m = (a.dy_c + BM - 1) / BM, tiles_n = (ncol + BN - 1) / BN;
   dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
+  // LDS-DMA stage ring (conv_set_dma variant bits 5-6: 0 register stage, 1 two stages, 2 three
+  // stages). The default code 1 keeps the register stage: in the engine the two-stage ring measured
+  // 3-10 % slower per wgrad shape (same-box kernel traces, profiles/r3z_conv_dma), although the
+  // isolated probe put it within 3 % either way.
+  const int wv = conv_dma_enabled() && g_conv_dma != 1 ? (g_conv_dma >> 5) & 3 : 0;
+  if (a.pro_ss == nullptr && wv != 0) {
+#define WGD_LAUNCH(BM_, BN_, NS_, MB_) hipLaunchKernelGGL((k_conv_wgrad_dma<BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n, splits)
+    if (wv == 1) {
+      if (wm && wn) WGD_LAUNCH(128, 128, 2, 2);
+      else if (wm) WGD_LAUNCH(128, 64, 2, 3);
+      else if (wn) WGD_LAUNCH(64, 128, 2, 3);
+      else WGD_LAUNCH(64, 64, 2, 4);
+    } else {
+      if (wm && wn) WGD_LAUNCH(128, 128, 3, 1);
+      else if (wm) WGD_LAUNCH(128, 64, 3, 2);
+      else if (wn) WGD_LAUNCH(64, 128, 3, 2);
+      else WGD_LAUNCH(64, 64, 3, 3);
+    }
+#undef WGD_LAUNCH
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
 #define WG_LAUNCH(BM_, BN_)                                                                                      \
   do {                                                                                                           \
     if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad<BM_, BN_, true>), grid, block, 0, s, a, tiles_m, tiles_n, splits); \

@@ -51,7 +51,8 @@ class ConvGemmArgs(ctypes.Structure):
         ("nbatch", c_void_p), ("max_batch", c_int), ("pro_ss", c_void_p), ("pro_ss_ps", c_int64),
         ("bnb_mask", c_void_p), ("bnb_mask_ps", c_int64), ("bnb_y0", c_void_p), ("bnb_y0_ps", c_int64),
         ("bnb_y1", c_void_p), ("bnb_y1_ps", c_int64), ("bnb_ms0", c_void_p), ("bnb_ms1", c_void_p),
-        ("bnb_part0", c_void_p), ("bnb_part1", c_void_p), ("bnb_part_ps", c_int64),
+        ("bnb_part0", c_void_p), ("bnb_part1", c_void_p), ("bnb_part_ps", c_int64), ("stats_rows", c_int),
+        ("bnb_rows", c_int),
     ]
 
 
@@ -98,6 +99,7 @@ _SIGS = {
     "conv_gemm_launch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "conv_set_dma": (c_int, [c_int]),
     "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
+    "conv_bnb_rows": (c_int, []),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "conv_wt_flip_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
@@ -512,6 +514,7 @@ class CNNGroup:
         a.relu = int(relu)
         if stats is not None:
             a.stats, a.stats_ps = stats.data_ptr(), stats.shape[1]
+            a.stats_rows = stats.shape[1] // (2 * a.ncol)
         a.nbatch, a.max_batch = self.nb.data_ptr(), self.B
         if pro is not None:
             ss = self.ss(pro)
@@ -522,12 +525,14 @@ class CNNGroup:
             if mask is not None:
                 a.bnb_mask, a.bnb_mask_ps = mask.data_ptr(), mask.shape[1]
             (bn0, y0), rest = targets[0], targets[1:]
-            part0 = self.fbuf(f"bnsum_{bn0.name}", 2 * bn0.Cp)
+            nr = lib.conv_bnb_rows()
+            a.bnb_rows = nr
+            part0 = self.fbuf(f"bnsum_{bn0.name}", nr * 2 * bn0.Cp)
             a.bnb_y0, a.bnb_y0_ps, a.bnb_ms0, a.bnb_part0, a.bnb_part_ps = y0.data_ptr(), y0.shape[1], self.ms(bn0).data_ptr(), part0.data_ptr(), part0.shape[1]
             if rest:
                 bn1_, y1_ = rest[0]
                 a.bnb_y1, a.bnb_y1_ps, a.bnb_ms1 = y1_.data_ptr(), y1_.shape[1], self.ms(bn1_).data_ptr()
-                a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", 2 * bn1_.Cp).data_ptr()
+                a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", nr * 2 * bn1_.Cp).data_ptr()
         _chk(lib.conv_gemm_launch(4 if fwd_dgrad else mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
@@ -583,7 +588,8 @@ class CNNGroup:
         lib, P = _lib(), self.capacity
         mss = self.ss(bn).data_ptr() if mask_from_y else None
         nblk = max(1, min(128, (self.B * hw + 255) // 256))
-        part = self.fbuf(f"bnsum_{bn.name}", 2 * bn.Cp)  # atomically accumulated, re-zeroed by the finalize
+        nr = lib.conv_bnb_rows()  # accumulator rows (spread atomics), summed and re-zeroed by the finalize
+        part = self.fbuf(f"bnsum_{bn.name}", nr * 2 * bn.Cp)
         coef = self.fbuf(f"bncoef_{bn.name}", 3 * bn.Cp)
         if pre_reduced:
             assert mask is None and gout is None and not mask_from_y
@@ -592,7 +598,7 @@ class CNNGroup:
                                        self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
                                        gout.shape[1] if gout is not None else 0, P, self._stream(), mss), f"bn_bwd_reduce {bn.name}")
         gbase = self.grad.data_ptr()
-        _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nblk, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
+        _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nr, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
                                      self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight), gbase + 4 * self._off(bn.module.bias),
                                      bn.C, bn.Cp, coef.data_ptr(), P, self._stream()), f"bn_bwd_finalize {bn.name}")
         _chk(lib.cnn_bn_bwd_apply(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],

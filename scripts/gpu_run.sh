@@ -51,6 +51,23 @@ for step in "$@"; do
       run resnet_dma 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       MYFYP_CONV_DMA=0 run resnet_reg 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       run resnet_dma2 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
+    dmaprof)  # same-box kernel stats of the ResNet-18 step: register stage (0), DMA forward only (20), DMA forward + wgrad (1)
+      for v in 0 20 1; do
+        MYFYP_CONV_DMA=$v run cnn_prof_v$v 400 rocprofv3 --kernel-trace --stats -d "$O/cnn_prof_v$v" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 1 \
+          --n-train 16384 --n-test 2048
+      done
+      for v in 0 20 1; do MYFYP_CONV_DMA=$v run resnet_v$v 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3; done ;;
+    statrows)  # BN-statistics atomics spread over 16 accumulator rows vs one (same box, alternating)
+      for i in 1 2; do
+        MYFYP_BN_STAT_ROWS=1 run resnet_rows1_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        MYFYP_BN_STAT_ROWS=16 run resnet_rows16_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done
+      MYFYP_BN_STAT_ROWS=16 run cnn_prof_rows16 400 rocprofv3 --kernel-trace --stats -d "$O/cnn_prof_rows16" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 1 \
+          --n-train 16384 --n-test 2048 ;;
+    rowsab)  # spread accumulators (BN forward stats / BN-backward partials): 1 / 16 / 64 rows, alternating
+      for i in 1 2; do
+        for r in 1 16 64; do MYFYP_BN_STAT_ROWS=$r MYFYP_BNB_ROWS=$r run resnet_r${r}_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3; done
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

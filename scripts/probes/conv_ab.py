@@ -68,4 +68,43 @@ for name, cin, cout, h, st in shapes:
             us = e0.elapsed_time(e1) / 20 * 1000
             useful = flops if mode == 0 or st == 1 else flops  # dgrad useful work = forward FLOPs
             print(f"{name:18s} mode {mode} {VARIANTS[dma]:10s}: {us:8.1f} us ({useful / us / 1e6:6.0f} TF/s useful)", flush=True)
+
+# weight gradients: register stage (0) vs LDS-DMA ring with 2 (32) / 3 (64) stages, split-K as the
+# engine sizes it (MYFYP_WGRAD_TPC = 2 workgroups per CU over all peers)
+from myfyp_amd.parallel.cnn_engine import WgradArgs
+
+for name, cin, cout, h, st in shapes:
+    ho = (h + 2 - 3) // st + 1
+    x = torch.randn(P, B * h * h * cin, device=dev).to(torch.bfloat16)
+    dy = torch.randn(P, B * ho * ho * cout, device=dev).to(torch.bfloat16)
+    ncol = 9 * cin
+    grad = torch.zeros(P, cout * ncol, device=dev)
+    M = B * ho * ho
+    tiles = ((cout + 127) // 128) * ((ncol + 127) // 128)
+    want = max(1, (2 * 256) // max(1, tiles * P))
+    k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
+    splits = (M + k_per - 1) // k_per
+    flops = 2 * P * M * cout * ncol
+    for code, lab in ((0, "reg"), (32, "dma/2"), (64, "dma/3")):
+        lib.conv_set_dma(code)
+        c = WgradArgs()
+        c.dy, c.dy_ps, c.x, c.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
+        c.H, c.W, c.x_c, c.Ho, c.Wo, c.dy_c = h, h, cin, ho, ho, cout
+        c.R, c.S, c.stride, c.pad = 3, 3, st, 1
+        c.grad, c.grad_ps, c.accumulate, c.k_per_split, c.max_batch = grad.data_ptr(), grad.shape[1], int(splits > 1), k_per, B
+        s = torch.cuda.current_stream().cuda_stream
+
+        def launch():
+            assert lib.conv_wgrad_launch(ctypes.byref(c), P, splits, s) == 0
+
+        for _ in range(3):
+            launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            launch()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1000
+        print(f"{name:18s} wgrad {lab:6s} (splits {splits:2d}): {us:8.1f} us ({flops / us / 1e6:6.0f} TF/s)", flush=True)
 lib.conv_set_dma(1)

@@ -26,11 +26,12 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
-@pytest.fixture(params=[1, 0, 3, 7, 9], ids=["dma", "regstage", "dma128x64s3", "dma256x64s3", "dma256x128s3"])
+@pytest.fixture(params=[1, 0, 3, 7, 9, 32, 64], ids=["dma", "regstage", "dma128x64s3", "dma256x64s3", "dma256x128s3", "wgrad2", "wgrad3"])
 def conv_dma(request):
     """Forward-shaped convs (mode 0, mode 4) through the LDS-DMA stage-ring kernel (1: the default
-    tiles, 128x64 / 128x128 with 2 stages; 3 / 7 / 9: the 3-stage variants, see conv_gemm_launch) or
-    the register-staged k_conv_gemm (0); restored afterwards."""
+    tiles, 128x64 / 128x128 with 2 stages, register-staged wgrad; 3 / 7 / 9: the 3-stage forward
+    variants, 32 / 64: the 2- / 3-stage DMA wgrad, see conv_gemm_launch) or the register-staged
+    kernels (0); restored afterwards."""
     from myfyp_amd.parallel.cnn_engine import _lib
 
     lib = _lib()
@@ -55,12 +56,14 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
     wf = torch.zeros(cpo, k, k, cpi, device=dev, dtype=torch.bfloat16)
     wf[:cout, :, :, :cin] = w.permute(0, 2, 3, 1).to(torch.bfloat16)
     y = torch.zeros(1, n * ho * ho * cpo, device=dev, dtype=torch.bfloat16)
-    stats = torch.zeros(1, lib.conv_gemm_stats_rows(n, ho, ho) * 2 * cpo, device=dev)
+    srows = lib.conv_gemm_stats_rows(n, ho, ho)  # spread accumulator rows (summed below)
+    stats = torch.zeros(1, srows * 2 * cpo, device=dev)
     a = ConvGemmArgs()
     a.src, a.src_ps, a.src_h, a.src_w, a.src_c = xn.data_ptr(), 0, h, h, cpi
     a.out_h, a.out_w, a.R, a.S, a.stride, a.pad = ho, ho, k, k, stride, pad
     a.wt, a.wt_ps, a.ncol, a.ncol_valid = wf.data_ptr(), 0, cpo, cout
     a.out, a.out_ps, a.relu, a.stats, a.stats_ps, a.max_batch = y.data_ptr(), 0, 0, stats.data_ptr(), 0, n
+    a.stats_rows = srows
     assert lib.conv_gemm_launch(0, ctypes.byref(a), 1, torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     y_nhwc = y.view(n, ho, ho, cpo)[..., :cout].float()
@@ -140,13 +143,15 @@ def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode,
     dyn, rn, mn = _nhwc_pad(dy, cout).reshape(1, -1).contiguous(), nh(resid), nh(mask)
     yn = [nh(y) for y in ys]
     out = torch.zeros(1, n * h * h * cin, device=dev, dtype=torch.bfloat16)
-    parts = [torch.zeros(1, 2 * cin, device=dev) for _ in ys]
+    nr = lib.conv_bnb_rows()  # spread accumulator rows of the BN-backward sums
+    parts = [torch.zeros(1, nr * 2 * cin, device=dev) for _ in ys]
     b = ConvGemmArgs()
     b.src, b.src_h, b.src_w, b.src_c = dyn.data_ptr(), ho, ho, cout
     b.out_h, b.out_w, b.R, b.S, b.stride, b.pad = h, h, k, k, stride, pad
     b.wt, b.ncol, b.ncol_valid = wf.data_ptr(), cin, cin
     b.out, b.max_batch = out.data_ptr(), n
     b.resid = rn.data_ptr()
+    b.bnb_rows = nr
     b.bnb_mask, b.bnb_y0, b.bnb_ms0, b.bnb_part0 = mn.data_ptr(), yn[0].data_ptr(), ms[0].data_ptr(), parts[0].data_ptr()
     if two:
         b.bnb_y1, b.bnb_ms1, b.bnb_part1 = yn[1].data_ptr(), ms[1].data_ptr(), parts[1].data_ptr()
@@ -159,6 +164,7 @@ def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode,
     g_ref = (dx_ref + resid) * (mask > 0)
     g = out.view(n, h, h, cin).float().permute(0, 3, 1, 2)
     torch.testing.assert_close(g, g_ref, atol=3e-2, rtol=3e-2)
+    parts = [p_.view(nr, 2 * cin).sum(0, keepdim=True) for p_ in parts]
     for y, m, part in zip(ys, ms, parts):
         xhat = (y - m[0, :cin].view(1, -1, 1, 1)) * m[0, cin:].view(1, -1, 1, 1)
         sg_ref, sgx_ref = g_ref.sum((0, 2, 3)), (g_ref * xhat).sum((0, 2, 3))
