@@ -113,9 +113,20 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, in
 // Staging layout: [BM][BN] fp32, column XOR-swizzled by bits 2-3 of the row — the four row groups of
 // one MFMA write (rows 4q + e) land in four distinct 16-bank groups. The caller's operand buffers
 // must be idle (a barrier after the last K step's LDS reads).
+// per-thread column sums of the epilogue (8 channels): BN statistics (q0 = sum x, q1 = sum x^2) or
+// BN-backward sums (q0 = sum g, q1 / q2 = sum g * xhat of the one / two BatchNorms)
+struct EpiSums {
+  float q0[8], q1[8], q2[8];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q0[j] = q1[j] = q2[j] = 0.f;
+  }
+};
+
+// One tile: stage, apply, store, and add this thread's rows into q (no reduction: see conv_epilogue_sums).
 template <int MODE, int BM, int BN, int NT>
-__device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
-                                              int hw, int rw, int ph, int pw) {
+__device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
+                                                   int hw, int rw, int ph, int pw, EpiSums& q) {
   constexpr int NF = BN / 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -145,7 +156,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
   const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
   const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
   const bool fstats = !bnb && a.stats != nullptr;
-  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], q0[8], q1[8], q2[8];
+  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8];
+  float(&q0)[8] = q.q0;
+  float(&q1)[8] = q.q1;
+  float(&q2)[8] = q.q2;
   bool cval[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -163,7 +177,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
         inv1[j] = m1p[a.ncol + col];
       }
     }
-    q0[j] = q1[j] = q2[j] = 0.f;
   }
   // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
   auto out_row = [&](int m) -> int {
@@ -213,9 +226,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
       *reinterpret_cast<uint4*>(out + o) = __builtin_bit_cast(uint4, ob);
     }
   }
+}
+
+// The column sums of one or more tiles (q) -> one atomic per column and statistic into accumulator
+// row `srow` of the peer (rows spread the atomics of many workgroups over several addresses). Over
+// the wave's rows (lanes of one chunk) by shuffles, over the waves in LDS (the staging tile must no
+// longer be read: this starts with a barrier).
+template <int MODE, int BN, int NT>
+__device__ __forceinline__ void conv_epilogue_sums(const ConvGemmArgs& a, bf16* lds, int peer, int n0, int srow, EpiSums& q) {
+  constexpr int CH = BN / 8, NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid % CH;
+  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
+  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
+  const bool fstats = !bnb && a.stats != nullptr;
   if (!bnb && !fstats) return;
-  // per-column sums: over the wave's rows (lanes of one chunk) by shuffles, over the waves in LDS,
-  // then one atomic per column and statistic into the peer's accumulator
+  float(&q0)[8] = q.q0;
+  float(&q1)[8] = q.q1;
+  float(&q2)[8] = q.q2;
+  float* cst = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
 #pragma unroll
@@ -247,7 +276,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
         t2 += red[(w * 3 + 2) * BN + tid];
       }
       if (bnb) {
-        const int prow = (m0 >> 7) % (a.bnb_rows > 1 ? a.bnb_rows : 1);
+        const int prow = srow % (a.bnb_rows > 1 ? a.bnb_rows : 1);
         float* p0 = a.bnb_part0 + peer * a.bnb_part_ps + prow * 2 * a.ncol;
         atomicAdd(p0 + col, t0);
         atomicAdd(p0 + a.ncol + col, t1);
@@ -259,12 +288,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
       } else {
         // BatchNorm batch statistics straight into the peer's [2][ncol] accumulator (bn_finalize
         // reads and re-zeroes it)
-        float* st = a.stats + peer * a.stats_ps + ((m0 >> 7) % (a.stats_rows > 1 ? a.stats_rows : 1)) * 2 * a.ncol;
+        float* st = a.stats + peer * a.stats_ps + (srow % (a.stats_rows > 1 ? a.stats_rows : 1)) * 2 * a.ncol;
         atomicAdd(st + col, t0);
         atomicAdd(st + a.ncol + col, t1);
       }
     }
   }
+}
+
+// one tile's whole epilogue (its sums into accumulator row m0 / 128)
+template <int MODE, int BM, int BN, int NT>
+__device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
+                                              int hw, int rw, int ph, int pw) {
+  EpiSums q;
+  q.zero();
+  conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw, q);
+  conv_epilogue_sums<MODE, BN, NT>(a, lds, peer, n0, m0 >> 7, q);
 }
 
 template <int MODE, int BN, bool PRO>
@@ -558,7 +597,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   constexpr int AR = BM * 8 / NT;  // A 16-byte chunks per thread per K step (4)
   constexpr int NB = BN * 8 / NT;  // B chunks per thread per K step
   static_assert(NB >= 1 && NW % 2 == 0, "tile shape");
-  constexpr int G = AR + NB;       // LDS-DMA instructions per thread per stage
+  constexpr int G_ = AR + NB;      // LDS-DMA instructions per thread per stage
   constexpr int NF = BN / 32;
   constexpr int STAGE = (BM + BN) * CG_BK;
   constexpr int OPER = NS * STAGE, EPI = BM * BN * 2;  // bf16 units (the epilogue stages fp32)
@@ -566,14 +605,21 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   // one LDS object only: a second one makes hipcc wait vmcnt(0) before the K loop's LDS reads
   __shared__ __attribute__((aligned(16))) bf16 lds[OPER > EPI ? OPER : EPI];
 
+  // Persistent over M tiles: gridDim.x = G * tiles_n workgroups per peer; workgroup (g, tn) runs
+  // the tiles tm = g, g + G, ... of column tile tn and keeps the epilogue's column sums (BN
+  // statistics / BN-backward sums) in registers across them, so a conv issues one set of atomics
+  // per workgroup instead of per tile (the 64-channel layers have 1024 tiles per peer adding into
+  // the same columns).
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
   const int hw = a.out_h * a.out_w;
   const int M = nb * hw;
-  const int wgid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  if (m0 >= M) return;  // tile past this peer's batch
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int G = gridDim.x / tiles_n;
+  const int tn = wgid % tiles_n, g0 = wgid / tiles_n;
+  const int n0 = tn * BN;
+  const int tiles_mp = (M + BM - 1) / BM;  // this peer's M tiles
+  if (g0 >= tiles_mp) return;  // uniform: no tile for this workgroup
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -582,90 +628,98 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   const int nk = (Ktot + CG_BK - 1) / CG_BK;
   const int cc = (lane & 7) ^ (((wave & 1) << 2) | (lane >> 4));  // this thread's logical 16-byte chunk
   const int cpp = a.src_c >> 3;
-
-  // A rows 8 (wave + NW i) + (lane >> 3): source coordinate of tap (0, 0) and its element offset
-  int a_bh[AR], a_bw[AR], a_pixc[AR];
-  bool a_ok[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + 8 * (wave + NW * i) + (lane >> 3);
-    a_ok[i] = m < M;
-    const int mm = a_ok[i] ? m : 0;
-    const int img = mm / hw, rem = mm - img * hw;
-    const int oh = rem / a.out_w, ow = rem - oh * a.out_w;
-    a_bh[i] = oh * a.stride - a.pad;
-    a_bw[i] = ow * a.stride - a.pad;
-    a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
-  }
   int b_off[NB];  // element offset of this thread's weight rows (K-contiguous), -1: past ncol
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int n = n0 + 8 * (wave + NW * i) + (lane >> 3);
     b_off[i] = n < a.ncol ? n * Ktot : -1;
   }
-  // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
-  int ar = 0, as_ = 0, ac8 = cc, kk = cc * 8;
-  while (ac8 >= cpp) {
-    ac8 -= cpp;
-    if (++as_ == a.S) { as_ = 0; ++ar; }
+  // the K walk's start (chunk cc of K step 0)
+  int ar0 = 0, as0 = 0, ac80 = cc;
+  while (ac80 >= cpp) {
+    ac80 -= cpp;
+    if (++as0 == a.S) { as0 = 0; ++ar0; }
   }
-  auto issue = [&](int buf) {
-    bf16* As = lds + buf * STAGE;
-    bf16* Bs = As + BM * CG_BK;
-    const bool kok = ar < a.R;
-    const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
+  EpiSums q;
+  q.zero();
+  for (int tm = g0; tm < tiles_mp; tm += G) {
+    const int m0 = tm * BM;
+    // A rows 8 (wave + NW i) + (lane >> 3): source coordinate of tap (0, 0) and its element offset
+    int a_bh[AR], a_bw[AR], a_pixc[AR];
+    bool a_ok[AR];
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const bool ok = kok && a_ok[i] && (unsigned)(a_bh[i] + ar) < (unsigned)a.src_h && (unsigned)(a_bw[i] + as_) < (unsigned)a.src_w;
-      conv_dma16(rs_src, As + 8 * (wave + NW * i) * CG_BK, ok ? (a_pixc[i] + tapc) * 2 : CONV_OOB);
+      const int m = m0 + 8 * (wave + NW * i) + (lane >> 3);
+      a_ok[i] = m < M;
+      const int mm = a_ok[i] ? m : 0;
+      const int img = mm / hw, rem = mm - img * hw;
+      const int oh = rem / a.out_w, ow = rem - oh * a.out_w;
+      a_bh[i] = oh * a.stride - a.pad;
+      a_bw[i] = ow * a.stride - a.pad;
+      a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
     }
+    // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
+    int ar = ar0, as_ = as0, ac8 = ac80, kk = cc * 8;
+    auto issue = [&](int buf) {
+      bf16* As = lds + buf * STAGE;
+      bf16* Bs = As + BM * CG_BK;
+      const bool kok = ar < a.R;
+      const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) conv_dma16(rs_wt, Bs + 8 * (wave + NW * i) * CG_BK, (kk < Ktot && b_off[i] >= 0) ? (b_off[i] + kk) * 2 : CONV_OOB);
-    ac8 += 8;
-    kk += CG_BK;
-    while (ac8 >= cpp) {
-      ac8 -= cpp;
-      if (++as_ == a.S) { as_ = 0; ++ar; }
-    }
-  };
-  f32x4 acc[4][NF];
+      for (int i = 0; i < AR; ++i) {
+        const bool ok = kok && a_ok[i] && (unsigned)(a_bh[i] + ar) < (unsigned)a.src_h && (unsigned)(a_bw[i] + as_) < (unsigned)a.src_w;
+        conv_dma16(rs_src, As + 8 * (wave + NW * i) * CG_BK, ok ? (a_pixc[i] + tapc) * 2 : CONV_OOB);
+      }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NB; ++i) conv_dma16(rs_wt, Bs + 8 * (wave + NW * i) * CG_BK, (kk < Ktot && b_off[i] >= 0) ? (b_off[i] + kk) * 2 : CONV_OOB);
+      ac8 += 8;
+      kk += CG_BK;
+      while (ac8 >= cpp) {
+        ac8 -= cpp;
+        if (++as_ == a.S) { as_ = 0; ++ar; }
+      }
+    };
+    f32x4 acc[4][NF];
 #pragma unroll
-    for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
 
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s);
-  int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
-  for (int kt = 0; kt < nk; ++kt) {
-    // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
-    const int ahead = nk - 1 - kt;
-    if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G>();
-    else if (NS >= 3 && ahead >= 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-    lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
-    if (kt + NS - 1 < nk) issue(wb);
-    const bf16* As = lds + rd * STAGE;
-    const bf16* Bs = As + BM * CG_BK;
+    for (int st = 0; st < NS - 1; ++st)
+      if (st < nk) issue(st);
+    int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
+    for (int kt = 0; kt < nk; ++kt) {
+      // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
+      const int ahead = nk - 1 - kt;
+      if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G_>();
+      else if (NS >= 3 && ahead >= 1) wait_vmcnt<G_>();
+      else wait_vmcnt<0>();
+      lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
+      if (kt + NS - 1 < nk) issue(wb);
+      const bf16* As = lds + rd * STAGE;
+      const bf16* Bs = As + BM * CG_BK;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = h * 4 + (lane >> 4);
-      bf16x8 af[4], bfr[NF];
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + (lane >> 4);
+        bf16x8 af[4], bfr[NF];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
+        for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+        for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+          for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+      }
+      rd = rd + 1 == NS ? 0 : rd + 1;
+      wb = wb + 1 == NS ? 0 : wb + 1;
     }
-    rd = rd + 1 == NS ? 0 : rd + 1;
-    wb = wb + 1 == NS ? 0 : wb + 1;
+    __syncthreads();  // operand stages idle: the epilogue stages the tile over them
+    conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, a.out_w, 0, 0, q);
+    __syncthreads();  // staging tile read: the next tile's DMA may overwrite it
   }
-  __syncthreads();  // operand stages idle: the epilogue stages the tile over them
-  conv_epilogue<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, a.out_w, 0, 0);
+  conv_epilogue_sums<MODE, BN, NT>(a, lds, peer, n0, g0, q);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -964,6 +1018,24 @@ __global__ __launch_bounds__(256, MINB) void k_conv_wgrad_dma(WgradArgs a, int t
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+// workgroups of a persistent DMA conv launch over all column tiles and peers (0 = one resident wave;
+// tests set a small count so that every workgroup runs many M tiles)
+static int g_conv_dma_wgs = 0;
+extern "C" int conv_set_dma_wgs(int n) {
+  const int old = g_conv_dma_wgs;
+  g_conv_dma_wgs = n > 0 ? n : 0;
+  return old;
+}
+static int conv_num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
 // forward-shaped convs through k_conv_fwd_dma (default) or k_conv_gemm's register stage
 // (MYFYP_CONV_DMA=0, or conv_set_dma(0): the A/B switch)
 static int g_conv_dma = -1;
@@ -1005,7 +1077,12 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
       const int bm = (wide ? var == 1 : var == 3) ? 256 : 128, bn = wide ? 128 : 64;
       const int tiles_m = (a.max_batch * a.out_h * a.out_w + bm - 1) / bm;
       const int tiles_n = (a.ncol + bn - 1) / bn;
-      dim3 grid(tiles_m * tiles_n, 1, peers), block(2 * bm);
+      // persistent over M tiles: about one resident wave of workgroups (occupancy x CUs) in all
+      const int per_cu = (wide ? var == 1 : var == 3) ? 1 : (wide ? 2 : (var == 1 ? 2 : 3));
+      const int want = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : conv_num_cus() * per_cu;
+      int G = (want + tiles_n * peers - 1) / (tiles_n * peers);
+      G = G < 1 ? 1 : (G > tiles_m ? tiles_m : G);
+      dim3 grid(G * tiles_n, 1, peers), block(2 * bm);
 #define DMA_LAUNCH(BM_, BN_, NS_, MB_)                                                                                   \
   do {                                                                                                                   \
     if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_dma<4, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n); \

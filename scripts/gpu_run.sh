@@ -68,6 +68,10 @@ for step in "$@"; do
       for i in 1 2; do
         for r in 1 16 64; do MYFYP_BN_STAT_ROWS=$r MYFYP_BNB_ROWS=$r run resnet_r${r}_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3; done
       done ;;
+    epiprobe) run conv_epi 300 python scripts/probes/conv_epi_probe.py ;;
+    resnet2)
+      run resnet_a 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      run resnet_b 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

@@ -26,18 +26,21 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
-@pytest.fixture(params=[1, 0, 3, 7, 9, 32, 64], ids=["dma", "regstage", "dma128x64s3", "dma256x64s3", "dma256x128s3", "wgrad2", "wgrad3"])
+@pytest.fixture(params=[1, -1, 0, 3, 7, 9, 32, 64], ids=["dma", "dma_persist", "regstage", "dma128x64s3", "dma256x64s3", "dma256x128s3", "wgrad2", "wgrad3"])
 def conv_dma(request):
     """Forward-shaped convs (mode 0, mode 4) through the LDS-DMA stage-ring kernel (1: the default
     tiles, 128x64 / 128x128 with 2 stages, register-staged wgrad; 3 / 7 / 9: the 3-stage forward
     variants, 32 / 64: the 2- / 3-stage DMA wgrad, see conv_gemm_launch) or the register-staged
-    kernels (0); restored afterwards."""
+    kernels (0); -1: the default tiles with 3 workgroups per launch, so each runs many M tiles and
+    carries its column sums across them; restored afterwards."""
     from myfyp_amd.parallel.cnn_engine import _lib
 
     lib = _lib()
-    old = lib.conv_set_dma(request.param)
+    old = lib.conv_set_dma(1 if request.param == -1 else request.param)
+    old_wgs = lib.conv_set_dma_wgs(3 if request.param == -1 else 0)  # dma_persist: 3 workgroups run every M tile
     yield request.param
     lib.conv_set_dma(old)
+    lib.conv_set_dma_wgs(old_wgs)
 
 
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3)])
