@@ -264,21 +264,34 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const bf16* dz, int64_t d
   }
 }
 
-// sum partials -> dgamma/dbeta (accumulated into the flat grad) + apply coefficients
+// sum partials -> dgamma/dbeta (accumulated into the flat grad) + apply coefficients; the nblk
+// accumulator rows [nblk][2][Cp] (spread atomics) are summed by 4 row groups of 64 channels per
+// block (as k_bn_finalize) and re-armed
 __global__ void k_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps,
                                   const float* ms, float* dgamma, float* dbeta, int C, int Cp, float* coef) {
   const int peer = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cp) return;
-  float* cp = coef + peer * 3 * Cp;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  __shared__ float red[2][4][64];
+  float sg = 0.f, sgx = 0.f;
   float* pp = const_cast<float*>(part) + peer * part_ps;
-  float sg = 0.f, sgx = 0.f;  // nblk accumulator rows [nblk][2][Cp] (spread atomics), re-armed
-  for (int r = 0; r < nblk; ++r) {
-    sg += pp[r * 2 * Cp + c];
-    sgx += pp[r * 2 * Cp + Cp + c];
-    pp[r * 2 * Cp + c] = 0.f;
-    pp[r * 2 * Cp + Cp + c] = 0.f;
+  if (c < Cp) {
+    for (int r = rg; r < nblk; r += 4) {
+      sg += pp[r * 2 * Cp + c];
+      sgx += pp[r * 2 * Cp + Cp + c];
+    }
+    for (int r = rg; r < nblk; r += 4) {
+      pp[r * 2 * Cp + c] = 0.f;
+      pp[r * 2 * Cp + Cp + c] = 0.f;
+    }
   }
+  red[0][rg][threadIdx.x & 63] = sg;
+  red[1][rg][threadIdx.x & 63] = sgx;
+  __syncthreads();
+  if (rg != 0 || c >= Cp) return;
+  sg = red[0][0][c & 63] + red[0][1][c & 63] + red[0][2][c & 63] + red[0][3][c & 63];
+  sgx = red[1][0][c & 63] + red[1][1][c & 63] + red[1][2][c & 63] + red[1][3][c & 63];
+  float* cp = coef + peer * 3 * Cp;
   if (c >= C) {
     cp[c] = 0.f; cp[Cp + c] = 0.f; cp[2 * Cp + c] = 0.f;
     return;
@@ -756,7 +769,7 @@ int cnn_bn_bwd_reduce(const bf16* dz, int64_t dz_ps, const bf16* mask, int64_t m
 }
 int cnn_bn_bwd_finalize(const float* part, int64_t part_ps, int nblk, const int* nb, int hw, const float* gamma, int64_t param_ps, const float* ms,
                         float* dgamma, float* dbeta, int C, int Cp, float* coef, int peers, void* s) {
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((Cp + 255) / 256, peers), dim3(256), 0, (hipStream_t)s, part, part_ps, nblk, nb, hw, gamma, param_ps,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((Cp + 63) / 64, peers), dim3(256), 0, (hipStream_t)s, part, part_ps, nblk, nb, hw, gamma, param_ps,
                      ms, dgamma, dbeta, C, Cp, coef);
   return ok();
 }

@@ -582,6 +582,17 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 // only, and 3-stage 64-channel tiles are slower than the register stage (short K: 9 K steps).
 // The epilogue (bias, residual, ReLU, BN sums / BN-backward sums) is conv_epilogue.
 typedef __attribute__((address_space(3))) void lds_void;
+// stride-2 dgrad parity classes (ph, pw) = (c >> 1, c & 1): taps of the classes before class c
+// (their weights come first in the parity-flipped layout)
+__host__ __device__ __forceinline__ int conv_parity_taps(int R, int S, int pad, int c) {
+  const int r0 = ((c >> 1) + pad) & 1, s0 = ((c & 1) + pad) & 1;
+  return ((R - r0 + 1) >> 1) * ((S - s0 + 1) >> 1);
+}
+__host__ __device__ __forceinline__ int conv_parity_taps_before(int R, int S, int pad, int c) {
+  int t = 0;
+  for (int k = 0; k < c; ++k) t += conv_parity_taps(R, S, pad, k);
+  return t;
+}
 __device__ __forceinline__ void conv_dma16(__amdgpu_buffer_rsrc_t r, bf16* lds_wave_base, int byte_off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, byte_off, 0, 0, 0);
 }
@@ -592,7 +603,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int MODE, int BM, int BN, int NS, int MINB>
 __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, int tiles_m, int tiles_n) {
-  static_assert(MODE == 0 || MODE == 4, "forward-shaped gathers only");
+  static_assert(MODE == 0 || MODE == 4 || MODE == 5, "forward-shaped gathers only");
+  constexpr int EMODE = MODE == 5 ? 2 : MODE;  // epilogue: MODE 5 writes MODE 2's class rows
   constexpr int NT = 2 * BM, NW = NT / 64;
   constexpr int AR = BM * 8 / NT;  // A 16-byte chunks per thread per K step (4)
   constexpr int NB = BN * 8 / NT;  // B chunks per thread per K step
@@ -610,9 +622,30 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   // statistics / BN-backward sums) in registers across them, so a conv issues one set of atomics
   // per workgroup instead of per tile (the 64-channel layers have 1024 tiles per peer adding into
   // the same columns).
+  //
+  // MODE 5: the stride-2 dgrad of parity class blockIdx.y = (ph, pw) — rows are the dX pixels
+  // (2hh + ph, 2ww + pw), reached by the taps r = r0 + 2i, s = s0 + 2j only — run as a stride-1
+  // forward conv over dY with the class's tR x tS taps flipped (tap i' = tR-1-i reads dY row
+  // hh - pad' + i', pad' = tR - 1 - (ph + pad - r0) / 2) and the class weights written by
+  // k_conv_wt_flip (parity layout: classes in order, each [ci][tR][tS][co]).
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
-  const int hw = a.out_h * a.out_w;
+  int gh = a.out_h, gw = a.out_w, kR = a.R, kS = a.S, kst = a.stride, pad_h = a.pad, pad_w = a.pad, ph = 0, pw = 0;
+  int woff = 0;  // element offset of the class's weights
+  if (MODE == 5) {
+    ph = (int)blockIdx.y >> 1;
+    pw = (int)blockIdx.y & 1;
+    const int r0 = (ph + a.pad) & 1, s0 = (pw + a.pad) & 1;
+    kR = (a.R - r0 + 1) >> 1;
+    kS = (a.S - s0 + 1) >> 1;
+    gh = (a.out_h - ph + 1) >> 1;
+    gw = (a.out_w - pw + 1) >> 1;
+    pad_h = kR - 1 - ((ph + a.pad - r0) >> 1);
+    pad_w = kS - 1 - ((pw + a.pad - s0) >> 1);
+    kst = 1;
+    woff = conv_parity_taps_before(a.R, a.S, a.pad, (int)blockIdx.y) * a.src_c * a.ncol;
+  }
+  const int hw = gh * gw;
   const int M = nb * hw;
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int G = gridDim.x / tiles_n;
@@ -623,8 +656,8 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(a.src + peer * a.src_ps), rs_wt = conv_rsrc(a.wt + peer * a.wt_ps);
-  const int Ktot = a.R * a.S * a.src_c;
+  const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(a.src + peer * a.src_ps), rs_wt = conv_rsrc(a.wt + peer * a.wt_ps + woff);
+  const int Ktot = kR * kS * a.src_c;  // 0: a parity class no tap reaches (zeros + the epilogue's residual)
   const int nk = (Ktot + CG_BK - 1) / CG_BK;
   const int cc = (lane & 7) ^ (((wave & 1) << 2) | (lane >> 4));  // this thread's logical 16-byte chunk
   const int cpp = a.src_c >> 3;
@@ -638,7 +671,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   int ar0 = 0, as0 = 0, ac80 = cc;
   while (ac80 >= cpp) {
     ac80 -= cpp;
-    if (++as0 == a.S) { as0 = 0; ++ar0; }
+    if (++as0 == kS) { as0 = 0; ++ar0; }
   }
   EpiSums q;
   q.zero();
@@ -653,9 +686,9 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
       a_ok[i] = m < M;
       const int mm = a_ok[i] ? m : 0;
       const int img = mm / hw, rem = mm - img * hw;
-      const int oh = rem / a.out_w, ow = rem - oh * a.out_w;
-      a_bh[i] = oh * a.stride - a.pad;
-      a_bw[i] = ow * a.stride - a.pad;
+      const int oh = rem / gw, ow = rem - oh * gw;
+      a_bh[i] = oh * kst - pad_h;
+      a_bw[i] = ow * kst - pad_w;
       a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
     }
     // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
@@ -663,7 +696,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
     auto issue = [&](int buf) {
       bf16* As = lds + buf * STAGE;
       bf16* Bs = As + BM * CG_BK;
-      const bool kok = ar < a.R;
+      const bool kok = ar < kR;
       const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
@@ -676,7 +709,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
       kk += CG_BK;
       while (ac8 >= cpp) {
         ac8 -= cpp;
-        if (++as_ == a.S) { as_ = 0; ++ar; }
+        if (++as_ == kS) { as_ = 0; ++ar; }
       }
     };
     f32x4 acc[4][NF];
@@ -716,10 +749,10 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
       wb = wb + 1 == NS ? 0 : wb + 1;
     }
     __syncthreads();  // operand stages idle: the epilogue stages the tile over them
-    conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, a.out_w, 0, 0, q);
+    conv_epilogue_tile<EMODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, gw, ph, pw, q);
     __syncthreads();  // staging tile read: the next tile's DMA may overwrite it
   }
-  conv_epilogue_sums<MODE, BN, NT>(a, lds, peer, n0, g0, q);
+  conv_epilogue_sums<EMODE, BN, NT>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1057,35 +1090,42 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   const ConvGemmArgs& a = *pa;
   // mode 0 forward, 1 dgrad, 4 stride-1 dgrad as a forward conv over dY with k_conv_wt_flip weights
   // (the caller passes the forward-shaped arguments: src = dY, pad = R-1-pad, ncol = cin)
-  if ((a.src_c & 7) || (a.ncol & 7) || peers < 1 || !(mode == 0 || mode == 1 || mode == 4)) return 1;
-  if (mode == 4 && (a.stride != 1 || a.pro_ss != nullptr)) return 1;
+  // mode 5: stride-2 dgrad by parity class as forward convs over dY with conv_wt_flip_parity_launch's
+  // weights (dgrad-shaped arguments: src = dY, out = dX, the conv's R, S, pad; LDS-DMA kernel only)
+  if ((a.src_c & 7) || (a.ncol & 7) || peers < 1 || !(mode == 0 || mode == 1 || mode == 4 || mode == 5)) return 1;
+  if ((mode == 4 || mode == 5) && a.pro_ss != nullptr) return 1;
+  if ((mode == 4 && a.stride != 1) || (mode == 5 && (a.stride != 2 || !conv_dma_enabled()))) return 1;
   // the buffer-load gathers form 32-bit byte offsets within one peer's source and weights
   if (CONV_BUFLOAD && ((int64_t)a.max_batch * a.src_h * a.src_w * a.src_c * 2 >= INT32_MAX ||
                        (int64_t)a.ncol * a.R * a.S * a.src_c * 2 >= INT32_MAX))
     return 3;
   const bool wide = a.ncol > 64;
   hipStream_t s = (hipStream_t)stream;
-  if ((mode == 4 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
+  if ((mode == 4 || mode == 5 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
     // variant code (conv_set_dma / MYFYP_CONV_DMA): 1 = the measured defaults below; otherwise bits
     // 1-2 pick the 64-channel tile (0 register stage, 1 128x64/3 stages/2 per CU, 2 128x64/2/3,
     // 3 256x64/3/1), bits 3-4 the wide one (0 register stage, 1 256x128/3/1, 2 128x128/2/2) and
     // bits 5-6 the weight gradient's (conv_wgrad_launch)
     int v = g_conv_dma;
     if (v == 1) v = (2 << 1) | (2 << 3);  // measured best for every ResNet-18 shape (profiles/r3z_conv_dma)
-    const int var = wide ? (v >> 3) & 3 : (v >> 1) & 3;
+    int var = wide ? (v >> 3) & 3 : (v >> 1) & 3;
+    if (mode == 5 && var == 0) var = 2;  // no register-staged MODE 5
     if (var != 0) {
       const int bm = (wide ? var == 1 : var == 3) ? 256 : 128, bn = wide ? 128 : 64;
-      const int tiles_m = (a.max_batch * a.out_h * a.out_w + bm - 1) / bm;
+      const int rows = mode == 5 ? ((a.out_h + 1) >> 1) * ((a.out_w + 1) >> 1) : a.out_h * a.out_w;  // largest class
+      const int tiles_m = (a.max_batch * rows + bm - 1) / bm;
       const int tiles_n = (a.ncol + bn - 1) / bn;
       // persistent over M tiles: about one resident wave of workgroups (occupancy x CUs) in all
       const int per_cu = (wide ? var == 1 : var == 3) ? 1 : (wide ? 2 : (var == 1 ? 2 : 3));
       const int want = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : conv_num_cus() * per_cu;
       int G = (want + tiles_n * peers - 1) / (tiles_n * peers);
       G = G < 1 ? 1 : (G > tiles_m ? tiles_m : G);
-      dim3 grid(G * tiles_n, 1, peers), block(2 * bm);
+      if (mode == 5) G = (G + 3) / 4;  // four classes share the resident wave
+      dim3 grid(G * tiles_n, mode == 5 ? 4 : 1, peers), block(2 * bm);
 #define DMA_LAUNCH(BM_, BN_, NS_, MB_)                                                                                   \
   do {                                                                                                                   \
     if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_dma<4, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n); \
+    else if (mode == 5) hipLaunchKernelGGL((k_conv_fwd_dma<5, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n); \
     else hipLaunchKernelGGL((k_conv_fwd_dma<0, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n);          \
   } while (0)
       if (wide) {
@@ -1132,17 +1172,36 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
 // Flipped, transposed weights for MODE 4: Wt[ci][r][s][co] = Wf[co][R-1-r][S-1-s][ci] per peer (both
 // channel counts padded to multiples of 8). Per tap it is a [co][ci] -> [ci][co] transpose: 64 x 64
 // tiles through LDS, 16-byte coalesced loads along ci and stores along co.
+// parity_pad >= 0 (MODE 5, stride-2 dgrad with that padding): the four parity classes' weights in
+// class order, class c = (ph, pw) as [ci][i'][j'][co] over its tR x tS taps r = r0 + 2 (tR-1-i'),
+// s = s0 + 2 (tS-1-j') (flipped, so the class runs as a forward conv over dY).
 // grid = (ceil(ci / 64) * ceil(co / 64), R * S, peers), block 256.
 __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ wf, int64_t wf_ps, bf16* __restrict__ wt, int64_t wt_ps, int cout,
-                                                      int cin, int R, int S) {
+                                                      int cin, int R, int S, int parity_pad) {
   __shared__ bf16 tile[64][64 + 8];
-  const int peer = blockIdx.z, tap = blockIdx.y;  // destination tap (r, s)
+  const int peer = blockIdx.z, tap = blockIdx.y;  // destination tap (all classes, in class order)
   const int tci = (cin + 63) / 64;
   const int ci0 = (blockIdx.x % tci) * 64, co0 = (blockIdx.x / tci) * 64;
-  const int rs_src = (R - 1 - tap / S) * S + (S - 1 - tap % S);
-  const bf16* src = wf + peer * wf_ps;
-  bf16* dst = wt + peer * wt_ps;
   const int RS = R * S;
+  int rs_src, taps, dtap, base_taps;  // source tap, taps of the destination block, tap within it, taps before it
+  if (parity_pad < 0) {
+    rs_src = (R - 1 - tap / S) * S + (S - 1 - tap % S);
+    taps = RS;
+    dtap = tap;
+    base_taps = 0;
+  } else {
+    int c = 0, t = tap;
+    while (c < 3 && t >= conv_parity_taps(R, S, parity_pad, c)) t -= conv_parity_taps(R, S, parity_pad, c++);
+    const int r0 = ((c >> 1) + parity_pad) & 1, s0 = ((c & 1) + parity_pad) & 1;
+    const int tR = (R - r0 + 1) >> 1, tS = (S - s0 + 1) >> 1;
+    const int ip = t / tS, jp = t - ip * tS;
+    rs_src = (r0 + 2 * (tR - 1 - ip)) * S + s0 + 2 * (tS - 1 - jp);
+    taps = tR * tS;
+    dtap = t;
+    base_taps = tap - t;
+  }
+  const bf16* src = wf + peer * wf_ps;
+  bf16* dst = wt + peer * wt_ps + (int64_t)base_taps * cin * cout;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {  // 64 co rows x 8 chunks of 8 ci
     const int q = threadIdx.x + 256 * k, row = q >> 3, ch = q & 7;
@@ -1161,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ w
     bf8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v.v[j] = tile[ch * 8 + j][row];
-    *reinterpret_cast<bf8*>(dst + ((int64_t)ci * RS + tap) * cout + co) = v;
+    *reinterpret_cast<bf8*>(dst + ((int64_t)ci * taps + dtap) * cout + co) = v;
   }
 }
 
@@ -1169,7 +1228,16 @@ extern "C" int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, lo
   if ((cout & 7) || (cin & 7) || peers < 1) return 1;
   const unsigned tiles = (unsigned)(((cin + 63) / 64) * ((cout + 63) / 64));
   hipLaunchKernelGGL(k_conv_wt_flip, dim3(tiles, (unsigned)(R * S), (unsigned)peers), dim3(256), 0, (hipStream_t)stream, (const bf16*)wf, (int64_t)wf_ps,
-                     (bf16*)wt, (int64_t)wt_ps, cout, cin, R, S);
+                     (bf16*)wt, (int64_t)wt_ps, cout, cin, R, S, -1);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+// MODE 5's parity-class weights (stride-2 dgrad with padding `pad`)
+extern "C" int conv_wt_flip_parity_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int cout, int cin, int R, int S, int pad, int peers,
+                                          void* stream) {
+  if ((cout & 7) || (cin & 7) || peers < 1 || pad < 0) return 1;
+  const unsigned tiles = (unsigned)(((cin + 63) / 64) * ((cout + 63) / 64));
+  hipLaunchKernelGGL(k_conv_wt_flip, dim3(tiles, (unsigned)(R * S), (unsigned)peers), dim3(256), 0, (hipStream_t)stream, (const bf16*)wf, (int64_t)wf_ps,
+                     (bf16*)wt, (int64_t)wt_ps, cout, cin, R, S, pad);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -103,6 +103,7 @@ _SIGS = {
     "conv_bnb_rows": (c_int, []),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "conv_wt_flip_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "conv_wt_flip_parity_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_act": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
@@ -357,6 +358,7 @@ class CNNGroup:
         self.shadow = torch.zeros(capacity, self.shadow_numel, dtype=torch.bfloat16, device=dev)
         self.gradf = torch.zeros(capacity, self.shadow_numel, dtype=torch.float32, device=dev)
         self.shadow_t = torch.zeros_like(self.shadow) if self.dgrad_fwd else None  # MODE 4 weights (k_conv_wt_flip)
+        self.s2_fwd = os.environ.get("MYFYP_CNN_S2_FWD", "0") == "1"  # MODE 5 stride-2 dgrads (see conv())
         self.capacity = capacity
         for slot, h in self.handles.items():
             h.retarget()
@@ -487,7 +489,20 @@ class CNNGroup:
         # stride-1 dgrad as a forward conv over dY with flipped, transposed weights (conv.hip MODE 4):
         # the forward's K-contiguous weight panel instead of the transposed LDS reads of MODE 3
         fwd_dgrad = mode == 1 and L.stride == 1 and L.colmap is None and self.dgrad_fwd
-        if fwd_dgrad:
+        # stride-2 dgrad by parity class, each class a forward conv over dY with its flipped taps
+        # (conv.hip MODE 5, LDS-DMA kernel only). Opt-in (MYFYP_CNN_S2_FWD=1): measured neutral — the
+        # classes' K loops are 1-4 taps long, and the flip costs more than the gather it saves
+        # (stride-2 dgrads 21.7 vs 20.3-22.1 ms per profiled run, profiles/r3z_conv_dma)
+        par_dgrad = mode == 1 and L.stride == 2 and L.colmap is None and self.dgrad_fwd and self.s2_fwd and lib.conv_set_dma(-1) != 0
+        if par_dgrad:
+            wt = self.shadow_t.data_ptr() + 2 * shadow_f
+            _chk(lib.conv_wt_flip_parity_launch(self.shadow.data_ptr() + 2 * shadow_f, self.shadow.shape[1], wt, self.shadow_t.shape[1], L.cp_out, L.cp_in,
+                                                L.R, L.S, L.pad, P, self._stream()), f"wt parity flip {L.name}")
+            a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.ho, L.wo, L.cp_out
+            a.out_h, a.out_w = L.h, L.w
+            a.wt = wt
+            a.ncol, a.ncol_valid = L.cp_in, L.cin
+        elif fwd_dgrad:
             wt = self.shadow_t.data_ptr() + 2 * shadow_f
             _chk(lib.conv_wt_flip_launch(self.shadow.data_ptr() + 2 * shadow_f, self.shadow.shape[1], wt, self.shadow_t.shape[1], L.cp_out, L.cp_in, L.R, L.S,
                                          P, self._stream()), f"wt flip {L.name}")
@@ -534,7 +549,7 @@ class CNNGroup:
                 bn1_, y1_ = rest[0]
                 a.bnb_y1, a.bnb_y1_ps, a.bnb_ms1 = y1_.data_ptr(), y1_.shape[1], self.ms(bn1_).data_ptr()
                 a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", nr * 2 * bn1_.Cp).data_ptr()
-        _chk(lib.conv_gemm_launch(4 if fwd_dgrad else mode, ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
+        _chk(lib.conv_gemm_launch(5 if par_dgrad else (4 if fwd_dgrad else mode), ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
         """(pixels per split, splits): split the pixel (K) dimension only until ~4 tiles per CU exist."""

@@ -25,12 +25,12 @@ for name, cin, cout, h, st in shapes:
     wt = torch.empty_like(wf)
     # conv_set_dma variant codes: 0 register stage; narrow (64 channels) 3 / 5 / 7 = 128x64 3 stages 2 per CU /
     # 128x64 2 stages 3 per CU / 256x64 3 stages 1 per CU; wide 9 / 17 = 256x128 3 stages / 128x128 2 stages 2 per CU
-    VARIANTS = {3: "128x64/3", 5: "128x64/2", 7: "256x64/3", 9: "256x128/3", 17: "128x128/2", 0: "reg"}
-    for mode in (0, 1, 4):
-        if mode == 4 and st != 1:
+    VARIANTS = {3: "128x64/3", 5: "128x64/2", 7: "256x64/3", 9: "256x128/3", 17: "128x128/2", 0: "reg", 1: "default"}
+    for mode in (0, 1, 4, 5):
+        if (mode == 4 and st != 1) or (mode == 5 and st != 2):
             continue
         narrow = (cout if mode == 0 else cin) <= 64
-        codes = [0] if mode == 1 else ([0, 3, 5, 7] if narrow else [0, 9, 17])
+        codes = [0] if mode == 1 else ([1] if mode == 5 else ([0, 3, 5, 7] if narrow else [0, 9, 17]))
         for dma in codes:
             lib.conv_set_dma(dma)
             a = ConvGemmArgs()
@@ -46,15 +46,17 @@ for name, cin, cout, h, st in shapes:
             a.stride, a.pad = st, 1
             a.wt, a.wt_ps, a.max_batch = wf.data_ptr(), wf.shape[1], B
             s = torch.cuda.current_stream().cuda_stream
-            if mode == 4:  # dgrad as a forward conv over dY: flipped weights (timed with the conv), pad R-1-pad
+            if mode in (4, 5):  # dgrad as forward conv(s) over dY: flipped weights (timed with the conv)
                 a.src, a.src_ps, a.src_h, a.src_w, a.src_c = dy.data_ptr(), dy.shape[1], ho, ho, cout
                 a.out_h, a.out_w, a.ncol, a.ncol_valid = h, h, cin, cin
                 a.out, a.out_ps = dx.data_ptr(), dx.shape[1]
-                a.wt, a.pad = wt.data_ptr(), 1
+                a.wt, a.pad = wt.data_ptr(), (1 if mode == 4 else 1)
 
             def launch():
                 if mode == 4:
                     assert lib.conv_wt_flip_launch(wf.data_ptr(), wf.shape[1], wt.data_ptr(), wt.shape[1], cout, cin, 3, 3, P, s) == 0
+                if mode == 5:
+                    assert lib.conv_wt_flip_parity_launch(wf.data_ptr(), wf.shape[1], wt.data_ptr(), wt.shape[1], cout, cin, 3, 3, 1, P, s) == 0
                 assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, s) == 0
 
             for _ in range(3):

@@ -101,6 +101,26 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
         torch.cuda.synchronize()
         torch.testing.assert_close(dx4.view(n, h, h, cpi)[..., :cin].float(), dx_ref.permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
 
+    if stride == 2 and conv_dma != 0:  # MODE 5: parity classes as forward convs with class-flipped weights
+        wt = torch.zeros_like(wf)
+        s_ = torch.cuda.current_stream().cuda_stream
+        assert lib.conv_wt_flip_parity_launch(wf.data_ptr(), 0, wt.data_ptr(), 0, cpo, cpi, k, k, pad, 1, s_) == 0
+        torch.cuda.synchronize()
+        blocks, off = [], 0
+        for c in range(4):  # class c = (ph, pw): taps r0 + 2i, flipped, as [ci][tR][tS][co]
+            r0, s0 = ((c >> 1) + pad) & 1, ((c & 1) + pad) & 1
+            rr, ss = list(range(r0, k, 2))[::-1], list(range(s0, k, 2))[::-1]
+            if rr and ss:
+                blk = wf[:, rr][:, :, ss].permute(3, 1, 2, 0).reshape(-1)
+                blocks.append(blk)
+                off += blk.numel()
+        assert torch.equal(wt.view(-1)[:off], torch.cat(blocks))
+        dx5 = torch.full_like(dx, float("nan"))  # every dX pixel belongs to one class: all are written
+        b.wt, b.pad, b.out = wt.data_ptr(), pad, dx5.data_ptr()
+        assert lib.conv_gemm_launch(5, ctypes.byref(b), 1, s_) == 0
+        torch.cuda.synchronize()
+        torch.testing.assert_close(dx5.view(n, h, h, cpi)[..., :cin].float(), dx_ref.permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
+
     # wgrad
     dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
     M = n * ho * ho
@@ -122,11 +142,13 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
 
 
 @pytest.mark.parametrize("cin,cout,stride,h,n,two,mode", [(64, 64, 1, 16, 3, False, 1), (64, 128, 2, 16, 2, True, 1), (128, 128, 1, 8, 4, True, 1),
-                                                          (64, 64, 1, 16, 3, False, 4), (128, 128, 1, 8, 4, True, 4), (64, 128, 1, 8, 2, True, 4)])
+                                                          (64, 64, 1, 16, 3, False, 4), (128, 128, 1, 8, 4, True, 4), (64, 128, 1, 8, 2, True, 4),
+                                                          (64, 128, 2, 16, 2, True, 5), (128, 256, 2, 9, 3, False, 5)])
 def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode, conv_dma):
     """dgrad with the BN-backward epilogue: out = bf16(dX + resid) * [mask > 0] and per-channel
     (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op. mode 4: the
-    stride-1 dgrad as a forward conv over dY with flipped weights (what the engine runs)."""
+    stride-1 dgrad as a forward conv over dY with flipped weights (what the engine runs); mode 5: the
+    stride-2 dgrad by parity class, each class a forward conv with its flipped taps."""
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, _lib
 
     lib = _lib()
@@ -162,6 +184,12 @@ def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode,
         wt = torch.zeros_like(wf)
         assert lib.conv_wt_flip_launch(wf.data_ptr(), 0, wt.data_ptr(), 0, cout, cin, k, k, 1, torch.cuda.current_stream().cuda_stream) == 0
         b.wt, b.pad = wt.data_ptr(), k - 1 - pad
+    if mode == 5:
+        if conv_dma == 0:
+            pytest.skip("MODE 5 runs on the LDS-DMA kernel only")
+        wt = torch.zeros_like(wf)
+        assert lib.conv_wt_flip_parity_launch(wf.data_ptr(), 0, wt.data_ptr(), 0, cout, cin, k, k, pad, 1, torch.cuda.current_stream().cuda_stream) == 0
+        b.wt = wt.data_ptr()
     assert lib.conv_gemm_launch(mode, ctypes.byref(b), 1, torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     g_ref = (dx_ref + resid) * (mask > 0)
@@ -502,3 +530,31 @@ def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
         assert c_f > c_n - 0.03 and r_f < 1.5 * r_n + 0.02, ((c_f, r_f), (c_n, r_n))
     assert abs(l_f - l_u1) < 1e-2 * max(1.0, abs(l_u1)), (l_f, l_u1, l_u2)
+
+
+def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
+    """MYFYP_CNN_S2_FWD=1 (stride-2 dgrads as four parity-class forward convs, conv.hip MODE 5) against
+    the default MODE 2 path, over one local epoch of two peers: the update must sit within the
+    default path's own run-to-run noise floor (fp32 atomics reorder between runs; see the BN1 test)."""
+    import threading
+
+    from myfyp_amd.models import ResNet18
+
+    runs = []
+    for flag in ("0", "0", "1"):
+        monkeypatch.setenv("MYFYP_CNN_S2_FWD", flag)
+        learners, _, _ = _make_learners(lambda i: ResNet18(seed=90 + i), 2, 16, 16, 16, 0.05, momentum=0.9, wd=5e-4)
+        g = learners[0]._engine.group
+        assert g.s2_fwd == (flag == "1")
+        p0 = [lr_.flat_params().detach().clone() for lr_ in learners]
+        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        runs.append([lr_.flat_params().detach().clone() - q for lr_, q in zip(learners, p0)])
+    d_u1, d_u2, d_f = runs
+
+    def dist(xs, ys):
+        return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
+
+    for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
+        assert c_f > c_n - 0.03 and r_f < 1.5 * r_n + 0.02, ((c_f, r_f), (c_n, r_n))
