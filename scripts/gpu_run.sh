@@ -72,6 +72,20 @@ for step in "$@"; do
     resnet2)
       run resnet_a 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       run resnet_b 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3 ;;
+    lenet30)  # config 3 at 30 rounds (the r3b measurement length), twice
+      run lenet_ring30_a 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 30
+      run lenet_ring30_b 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 30 ;;
+    lenetab)  # config 3: DMA forward convs (eval path) vs register stage, alternating
+      for i in 1 2; do
+        MYFYP_CONV_DMA=0 run lenet_reg_$i 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 30
+        MYFYP_CONV_DMA=1 run lenet_dma_$i 400 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 30
+      done ;;
+    lenetold)  # config 3: the r3b tree (build/r3b_tree, commit 52fcf80) vs this tree, same data flags, alternating
+      D="--model lenet5 --aggregator neighbor --rounds 30 --similarity 0.8 --noise 1.2 --modes 4 --label-noise 0.1 --target-acc 0.8"
+      for i in 1 2; do
+        (cd build/r3b_tree && timeout -k 10 400 python benchmarks/bench_cnn.py $D) > "$O/lenet_old_$i.log" 2>&1 || exit 1
+        run lenet_new_$i 400 python benchmarks/bench_cnn.py $D
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;
