@@ -221,6 +221,9 @@ def main() -> None:
         "collective": ("delayed-averaging" if args.delayed_averaging else ("synchronous" if args.no_overlap else "side-stream-bucketed"))
         + f", bucket {Settings.BUCKET_BYTES >> 20} MiB",
     }
+    grp = getattr(engines[0], "group", None) if engines and engines[0] is not None else None
+    if grp is not None and getattr(grp, "_wsplit", None):
+        out["wgrad_splits"] = {k: v[1] for k, v in grp._wsplit.items()}  # device-tuned split-K per conv layer
     if args.torch_step and rank == 0 and torch.cuda.is_available():
         t_ms = torch_step_ms(args.model, B)
         out["torch_bf16_ms_per_peer_step"] = round(t_ms, 3)

@@ -240,6 +240,7 @@ class CNNGroup:
         # stride-1 dgrad as a forward conv over dY with flipped weights (conv.hip MODE 4); 0 = MODE 3
         self.dgrad_fwd = os.environ.get("MYFYP_DGRAD_FWD", "1") != "0"
         self.wgrad_tpc = int(os.environ.get("MYFYP_WGRAD_TPC", "2"))  # measured: 2 -> 75.6 ms wgrad, 4 -> 78.4, 8 -> 89.8 (scripts/probes/wgrad_tpc.sh)
+        self.wgrad_tune = os.environ.get("MYFYP_WGRAD_TUNE", "1") != "0"  # per-layer split-K timed on the device (_tune_wgrad)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._seen: set = set()
         self._data_version = 0
@@ -365,7 +366,62 @@ class CNNGroup:
         self._acts: Dict[str, torch.Tensor] = {}
         self._graphs.clear()
         self._seen = set()
+        self._tune_wgrad()
         self._build_segments()
+
+    def _tune_wgrad(self) -> None:
+        """Pick each ResNet wgrad layer's split-K count on the device (before the optimizer segments,
+        whose zero-after flags follow it, and before any graph capture). The best split depends on
+        the shape's workgroup count against the resident slots (a second, partial wave of workgroups
+        nearly doubles a launch) and on the K-loop length per workgroup, in ways a formula tracked
+        poorly: a sweep of the ResNet-18 shapes (profiles/r3z_wsplit) put the round-2 rule 1-18 %
+        off the best per layer (layer-3 wgrad 155 us at 1 split, 132 us at 3). Candidates around
+        that rule are timed on scratch operands of the layer's shape; MYFYP_WGRAD_TUNE=0 keeps the rule."""
+        self._wsplit: Dict[str, Tuple[int, int]] = {}
+        if not (self.wgrad_tune and self.arch == "resnet18" and self.device.type == "cuda" and Settings.USE_FUSED_KERNELS):
+            return
+        lib, P = _lib(), self.capacity
+        s = torch.cuda.current_stream(self.device)
+        cache: Dict[tuple, Tuple[int, int]] = {}
+        for L in self.convs:
+            if L.colmap is not None:
+                continue
+            key = (L.h, L.w, L.cp_in, L.cp_out, L.R, L.S, L.stride, L.pad)
+            if key in cache:
+                self._wsplit[L.name] = cache[key]
+                continue
+            M = self.B * L.ho * L.wo
+            base = self._wgrad_split_rule(L)[1]
+            cands = sorted({max(1, min(64, int(round(base * f)))) for f in (0.5, 1, 1.5, 2, 3, 4)} | {1})
+            x = torch.zeros(P, self.B * L.h * L.w * L.cp_in, dtype=torch.bfloat16, device=self.device)
+            dy = torch.zeros(P, M * L.cp_out, dtype=torch.bfloat16, device=self.device)
+            grad = torch.zeros(P, L.cp_out * L.R * L.S * L.cp_in, dtype=torch.float32, device=self.device)
+            best, seen = None, set()
+            for want in cands:
+                k_per = max(64, ((M + want - 1) // want + 63) // 64 * 64)
+                splits = (M + k_per - 1) // k_per
+                if splits in seen:
+                    continue
+                seen.add(splits)
+                a = WgradArgs()
+                a.dy, a.dy_ps, a.x, a.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
+                a.H, a.W, a.x_c, a.Ho, a.Wo, a.dy_c = L.h, L.w, L.cp_in, L.ho, L.wo, L.cp_out
+                a.R, a.S, a.stride, a.pad = L.R, L.S, L.stride, L.pad
+                a.grad, a.grad_ps, a.accumulate, a.k_per_split, a.max_batch = grad.data_ptr(), grad.shape[1], int(splits > 1), k_per, self.B
+                for _ in range(2):
+                    _chk(lib.conv_wgrad_launch(ctypes.byref(a), P, splits, s.cuda_stream), "wgrad tune")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(5):
+                    _chk(lib.conv_wgrad_launch(ctypes.byref(a), P, splits, s.cuda_stream), "wgrad tune")
+                e1.record(s)
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+                if best is None or t < best[0]:
+                    best = (t, (k_per, splits))
+            cache[key] = best[1]
+            self._wsplit[L.name] = best[1]
+            del x, dy, grad
 
     def _build_segments(self) -> None:
         segs, work = [], []
@@ -552,7 +608,12 @@ class CNNGroup:
         _chk(lib.conv_gemm_launch(5 if par_dgrad else (4 if fwd_dgrad else mode), ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
-        """(pixels per split, splits): split the pixel (K) dimension only until ~4 tiles per CU exist."""
+        """(pixels per split, splits): the device-tuned choice (``_tune_wgrad``) or the rule."""
+        tuned = getattr(self, "_wsplit", {}).get(L.name)
+        return tuned if tuned is not None else self._wgrad_split_rule(L)
+
+    def _wgrad_split_rule(self, L: ConvL) -> Tuple[int, int]:
+        """(pixels per split, splits): split the pixel (K) dimension only until ~wgrad_tpc tiles per CU exist."""
         M = self.B * L.ho * L.wo
         ncol = L.R * L.S * L.cp_in
         tiles = ((L.cp_out + 127) // 128) * ((ncol + 127) // 128)

@@ -86,6 +86,12 @@ for step in "$@"; do
         (cd build/r3b_tree && timeout -k 10 400 python benchmarks/bench_cnn.py $D) > "$O/lenet_old_$i.log" 2>&1 || exit 1
         run lenet_new_$i 400 python benchmarks/bench_cnn.py $D
       done ;;
+    wsplit) run wgrad_split 400 python scripts/probes/wgrad_split_sweep.py ;;
+    tuneab)  # device-tuned wgrad split-K vs the rule (MYFYP_WGRAD_TUNE=0), alternating
+      for i in 1 2; do
+        MYFYP_WGRAD_TUNE=0 run resnet_rule_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        run resnet_tuned_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;
