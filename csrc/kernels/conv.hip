@@ -124,26 +124,20 @@ struct EpiSums {
 };
 
 // One tile: stage, apply, store, and add this thread's rows into q (no reduction: see conv_epilogue_sums).
-template <int MODE, int BM, int BN, int NT>
-__device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
+// PARTS > 1: the tile goes through a staging area of BM / PARTS rows (`stg`, fp32) in PARTS rounds,
+// row slab by row slab (the waves of a slab stage, everyone applies), so that the rest of LDS can
+// take the next tile's first operand stage meanwhile (k_conv_fwd_dma).
+template <int MODE, int BM, int BN, int NT, int PARTS = 1>
+__device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], float* stg, int peer, int m0, int n0, int M,
                                                    int hw, int rw, int ph, int pw, EpiSums& q) {
   constexpr int NF = BN / 32;
+  constexpr int SR = BM / PARTS;  // staged rows per round (a multiple of the 64 rows of a wave)
+  static_assert(SR % 64 == 0, "staging rounds hold whole wave rows");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  float* cst = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NF; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wr * 64 + i * 16 + 4 * (lane >> 4) + e;
-        const int col = wc * (BN / 2) + j * 16 + (lane & 15);
-        cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
-      }
-  __syncthreads();
+  float* cst = stg;
 
-  constexpr int CH = BN / 8, RP = NT / CH, PASSES = BM / RP, NW = NT / 64;
+  constexpr int CH = BN / 8, RP = NT / CH, PASSES = SR / RP, NW = NT / 64;
   const int ch = tid % CH, rr = tid / CH;
   const int col0 = n0 + ch * 8;
   const bool chok = col0 < a.ncol;  // ncol is a multiple of 8
@@ -185,11 +179,25 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
     const int hh = rem / rw, ww = rem - hh * rw;
     return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
   };
+  for (int part = 0; part < PARTS; ++part) {
+  if (wr * 64 / SR == part) {  // this wave's rows are in the slab: stage them
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = wr * 64 - part * SR + i * 16 + 4 * (lane >> 4) + e;
+          const int col = wc * (BN / 2) + j * 16 + (lane & 15);
+          cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
+        }
+  }
+  __syncthreads();
   if (chok) {
 #pragma unroll 2
     for (int p = 0; p < PASSES; ++p) {
-      const int row = rr + p * RP;
-      const int m = m0 + row;
+      const int row = rr + p * RP;  // row within the slab
+      const int m = m0 + part * SR + row;
       if (m >= M) break;
       const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
       uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
@@ -225,6 +233,8 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       }
       *reinterpret_cast<uint4*>(out + o) = __builtin_bit_cast(uint4, ob);
     }
+  }
+  if (PARTS > 1) __syncthreads();  // the slab is read: the next round may restage
   }
 }
 
@@ -302,7 +312,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
                                               int hw, int rw, int ph, int pw) {
   EpiSums q;
   q.zero();
-  conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw, q);
+  conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, rw, ph, pw, q);
   conv_epilogue_sums<MODE, BN, NT>(a, lds, peer, n0, m0 >> 7, q);
 }
 
@@ -581,6 +591,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 // layer-1 forward 159.1 -> 135.5 us); 256 x 128 / 3 stages / 1 per CU is 12 % faster on layers 3-4
 // only, and 3-stage 64-channel tiles are slower than the register stage (short K: 9 K steps).
 // The epilogue (bias, residual, ReLU, BN sums / BN-backward sums) is conv_epilogue.
+#ifndef CONV_XT
+// k_conv_fwd_dma forward: the next tile's first stage under the epilogue. Measured neutral (layer-1
+// forward with statistics 161 vs 158 us, ResNet-18 2.199 / 2.199 vs 2.211 / 2.195 rounds/s,
+// profiles/r3z_conv_dma/xtab): the slab-staged epilogue's extra barriers eat the overlap. Off.
+#define CONV_XT 0
+#endif
 typedef __attribute__((address_space(3))) void lds_void;
 // stride-2 dgrad parity classes (ph, pw) = (c >> 1, c & 1): taps of the classes before class c
 // (their weights come first in the parity-flipped layout)
@@ -675,35 +691,47 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   }
   EpiSums q;
   q.zero();
-  for (int tm = g0; tm < tiles_mp; tm += G) {
-    const int m0 = tm * BM;
+  // Two-stage rings overlap tiles: once a tile's K loop is done, the next tile's first operand
+  // stage is issued into stage 0 and the epilogue stages the accumulators in two 64-row slabs
+  // through stage 1, so that DMA (and the next tile's row setup) runs under the epilogue instead of
+  // after it (the persistent loop otherwise serialises every tile's pipeline fill; separate
+  // workgroups per tile overlapped it across the CU's slots).
+  // (The dgrad modes spill or lose occupancy with it: forward only, and off by default — CONV_XT.)
+  constexpr bool XT = CONV_XT && MODE == 0 && NS == 2 && BM == 128 && BM / 2 * BN * 4 <= STAGE * 2;
+  if constexpr (XT) {
     // A rows 8 (wave + NW i) + (lane >> 3): source coordinate of tap (0, 0) and its element offset
     int a_bh[AR], a_bw[AR], a_pixc[AR];
     bool a_ok[AR];
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int m = m0 + 8 * (wave + NW * i) + (lane >> 3);
-      a_ok[i] = m < M;
-      const int mm = a_ok[i] ? m : 0;
-      const int img = mm / hw, rem = mm - img * hw;
-      const int oh = rem / gw, ow = rem - oh * gw;
-      a_bh[i] = oh * kst - pad_h;
-      a_bw[i] = ow * kst - pad_w;
-      a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
-    }
-    // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
-    int ar = ar0, as_ = as0, ac8 = ac80, kk = cc * 8;
+    int ar = ar0, as_ = as0, ac8 = ac80, kk = cc * 8;  // K walk of this thread's chunk: k = 64 kt + 8 cc = (r, s, c8)
+    auto setup = [&](int tm_) {
+      const int mb = tm_ * BM;
+  #pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int m = mb + 8 * (wave + NW * i) + (lane >> 3);
+        a_ok[i] = m < M;
+        const int mm = a_ok[i] ? m : 0;
+        const int img = mm / hw, rem = mm - img * hw;
+        const int oh = rem / gw, ow = rem - oh * gw;
+        a_bh[i] = oh * kst - pad_h;
+        a_bw[i] = ow * kst - pad_w;
+        a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
+      }
+      ar = ar0;
+      as_ = as0;
+      ac8 = ac80;
+      kk = cc * 8;
+    };
     auto issue = [&](int buf) {
       bf16* As = lds + buf * STAGE;
       bf16* Bs = As + BM * CG_BK;
       const bool kok = ar < kR;
       const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
-#pragma unroll
+  #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bool ok = kok && a_ok[i] && (unsigned)(a_bh[i] + ar) < (unsigned)a.src_h && (unsigned)(a_bw[i] + as_) < (unsigned)a.src_w;
         conv_dma16(rs_src, As + 8 * (wave + NW * i) * CG_BK, ok ? (a_pixc[i] + tapc) * 2 : CONV_OOB);
       }
-#pragma unroll
+  #pragma unroll
       for (int i = 0; i < NB; ++i) conv_dma16(rs_wt, Bs + 8 * (wave + NW * i) * CG_BK, (kk < Ktot && b_off[i] >= 0) ? (b_off[i] + kk) * 2 : CONV_OOB);
       ac8 += 8;
       kk += CG_BK;
@@ -712,45 +740,131 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
         if (++as_ == kS) { as_ = 0; ++ar; }
       }
     };
-    f32x4 acc[4][NF];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
-
-#pragma unroll
+    setup(g0);
+  #pragma unroll
     for (int st = 0; st < NS - 1; ++st)
       if (st < nk) issue(st);
-    int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
-    for (int kt = 0; kt < nk; ++kt) {
-      // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
-      const int ahead = nk - 1 - kt;
-      if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G_>();
-      else if (NS >= 3 && ahead >= 1) wait_vmcnt<G_>();
-      else wait_vmcnt<0>();
-      lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
-      if (kt + NS - 1 < nk) issue(wb);
-      const bf16* As = lds + rd * STAGE;
-      const bf16* Bs = As + BM * CG_BK;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ch = h * 4 + (lane >> 4);
-        bf16x8 af[4], bfr[NF];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+    for (int tm = g0; tm < tiles_mp; tm += G) {
+      const int m0 = tm * BM;
+      f32x4 acc[4][NF];
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+  #pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
+
+      int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
+      for (int kt = 0; kt < nk; ++kt) {
+        // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
+        const int ahead = nk - 1 - kt;
+        if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G_>();
+        else if (NS >= 3 && ahead >= 1) wait_vmcnt<G_>();
+        else wait_vmcnt<0>();
+        lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
+        if (kt + NS - 1 < nk) issue(wb);
+        const bf16* As = lds + rd * STAGE;
+        const bf16* Bs = As + BM * CG_BK;
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = h * 4 + (lane >> 4);
+          bf16x8 af[4], bfr[NF];
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
+  #pragma unroll
+          for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+  #pragma unroll
+          for (int i = 0; i < 4; ++i)
+  #pragma unroll
+            for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+        }
+        rd = rd + 1 == NS ? 0 : rd + 1;
+        wb = wb + 1 == NS ? 0 : wb + 1;
       }
-      rd = rd + 1 == NS ? 0 : rd + 1;
-      wb = wb + 1 == NS ? 0 : wb + 1;
+      __syncthreads();  // operand stages idle
+      const bool more = tm + G < tiles_mp;
+      if (more) {
+        setup(tm + G);
+        if (nk > 0) issue(0);  // the next tile's first stage lands under this epilogue
+      }
+      conv_epilogue_tile<EMODE, BM, BN, NT, 2>(a, acc, reinterpret_cast<float*>(lds + STAGE), peer, m0, n0, M, hw, gw, ph, pw, q);
     }
-    __syncthreads();  // operand stages idle: the epilogue stages the tile over them
-    conv_epilogue_tile<EMODE, BM, BN, NT>(a, acc, lds, peer, m0, n0, M, hw, gw, ph, pw, q);
-    __syncthreads();  // staging tile read: the next tile's DMA may overwrite it
+  } else {
+    for (int tm = g0; tm < tiles_mp; tm += G) {
+      const int m0 = tm * BM;
+      // A rows 8 (wave + NW i) + (lane >> 3): source coordinate of tap (0, 0) and its element offset
+      int a_bh[AR], a_bw[AR], a_pixc[AR];
+      bool a_ok[AR];
+  #pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int m = m0 + 8 * (wave + NW * i) + (lane >> 3);
+        a_ok[i] = m < M;
+        const int mm = a_ok[i] ? m : 0;
+        const int img = mm / hw, rem = mm - img * hw;
+        const int oh = rem / gw, ow = rem - oh * gw;
+        a_bh[i] = oh * kst - pad_h;
+        a_bw[i] = ow * kst - pad_w;
+        a_pixc[i] = ((img * a.src_h + a_bh[i]) * a.src_w + a_bw[i]) * a.src_c;
+      }
+      // K walk of this thread's chunk: K step kt covers k = 64 kt + 8 cc = (tap r, tap s, channel chunk c8)
+      int ar = ar0, as_ = as0, ac8 = ac80, kk = cc * 8;
+      auto issue = [&](int buf) {
+        bf16* As = lds + buf * STAGE;
+        bf16* Bs = As + BM * CG_BK;
+        const bool kok = ar < kR;
+        const int tapc = (ar * a.src_w + as_) * a.src_c + ac8 * 8;
+  #pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const bool ok = kok && a_ok[i] && (unsigned)(a_bh[i] + ar) < (unsigned)a.src_h && (unsigned)(a_bw[i] + as_) < (unsigned)a.src_w;
+          conv_dma16(rs_src, As + 8 * (wave + NW * i) * CG_BK, ok ? (a_pixc[i] + tapc) * 2 : CONV_OOB);
+        }
+  #pragma unroll
+        for (int i = 0; i < NB; ++i) conv_dma16(rs_wt, Bs + 8 * (wave + NW * i) * CG_BK, (kk < Ktot && b_off[i] >= 0) ? (b_off[i] + kk) * 2 : CONV_OOB);
+        ac8 += 8;
+        kk += CG_BK;
+        while (ac8 >= cpp) {
+          ac8 -= cpp;
+          if (++as_ == kS) { as_ = 0; ++ar; }
+        }
+      };
+      f32x4 acc[4][NF];
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+  #pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = zero4();
+
+  #pragma unroll
+      for (int st = 0; st < NS - 1; ++st)
+        if (st < nk) issue(st);
+      int rd = 0, wb = NS - 1;  // stage read this K step, stage the next issue writes
+      for (int kt = 0; kt < nk; ++kt) {
+        // this thread's DMA of stage kt has landed; the stages issued after it stay in flight
+        const int ahead = nk - 1 - kt;
+        if (NS >= 4 && ahead >= 2) wait_vmcnt<2 * G_>();
+        else if (NS >= 3 && ahead >= 1) wait_vmcnt<G_>();
+        else wait_vmcnt<0>();
+        lds_barrier();  // every wave's DMA of stage kt landed; every wave is done reading stage kt - 1
+        if (kt + NS - 1 < nk) issue(wb);
+        const bf16* As = lds + rd * STAGE;
+        const bf16* Bs = As + BM * CG_BK;
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = h * 4 + (lane >> 4);
+          bf16x8 af[4], bfr[NF];
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) af[i] = ld8(As + swz(wr * 64 + i * 16 + (lane & 15), ch));
+  #pragma unroll
+          for (int j = 0; j < NF; ++j) bfr[j] = ld8(Bs + swz(wc * (BN / 2) + j * 16 + (lane & 15), ch));
+  #pragma unroll
+          for (int i = 0; i < 4; ++i)
+  #pragma unroll
+            for (int j = 0; j < NF; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+        }
+        rd = rd + 1 == NS ? 0 : rd + 1;
+        wb = wb + 1 == NS ? 0 : wb + 1;
+      }
+      __syncthreads();  // operand stages idle: the epilogue stages the tile over them
+      conv_epilogue_tile<EMODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, gw, ph, pw, q);
+      __syncthreads();  // staging tile read: the next tile's DMA may overwrite it
+    }
   }
   conv_epilogue_sums<EMODE, BN, NT>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
 }

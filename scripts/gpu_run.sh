@@ -92,6 +92,14 @@ for step in "$@"; do
         MYFYP_WGRAD_TUNE=0 run resnet_rule_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
         run resnet_tuned_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       done ;;
+    xtab)  # cross-tile DMA prefetch in the forward conv (default) vs one tile at a time (build/base_CONV_XT0), alternating
+      L0=build/base_CONV_XT0/libmyfyp_hip.so
+      run epi_xt1 300 python scripts/probes/conv_epi_probe.py
+      MYFYP_NATIVE_LIB=$L0 run epi_xt0 300 python scripts/probes/conv_epi_probe.py
+      for i in 1 2; do
+        run resnet_xt1_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        MYFYP_NATIVE_LIB=$L0 run resnet_xt0_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

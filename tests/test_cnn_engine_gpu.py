@@ -558,3 +558,55 @@ def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
 
     for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
         assert c_f > c_n - 0.03 and r_f < 1.5 * r_n + 0.02, ((c_f, r_f), (c_n, r_n))
+
+
+@pytest.mark.parametrize("mode", [0, 4])
+def test_conv_grouped_peers_with_uneven_batches(mode, conv_dma):
+    """Three peers in one launch (grid.z) with per-peer valid batches 5 / 1 / 3 (``nbatch``), forward
+    with BN statistics (mode 0) and the stride-1 dgrad as a forward conv (mode 4): every peer's rows
+    match torch and rows past a peer's batch are left untouched (the persistent DMA kernel sizes its
+    M tiles per peer)."""
+    from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, _lib
+
+    lib = _lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    P, nmax, cin, cout, h, k = 3, 5, 64, 128, 12, 3
+    nbs = [5, 1, 3]
+    cpi, cpo = _cp(cin), _cp(cout)
+    xs = [_bf(torch.randn(nmax, cin, h, h, device=dev)) for _ in range(P)]
+    ws = [_bf(torch.randn(cout, cin, k, k, device=dev) * (1.0 / (cin * k * k) ** 0.5)) for _ in range(P)]
+    if mode == 0:
+        src = torch.stack([_nhwc_pad(x, cpi).reshape(-1) for x in xs]).contiguous()
+        wf = torch.stack([w.permute(0, 2, 3, 1).to(torch.bfloat16).reshape(-1) for w in ws]).contiguous()
+        ncol, c_src, refs = cpo, cpi, [F.conv2d(x, w, padding=1) for x, w in zip(xs, ws)]
+    else:  # dY of the conv cin -> cout; dX = conv_transpose, weights flipped per peer
+        dys = [_bf(torch.randn(nmax, cout, h, h, device=dev)) for _ in range(P)]
+        src = torch.stack([_nhwc_pad(d, cpo).reshape(-1) for d in dys]).contiguous()
+        wf0 = torch.stack([w.permute(0, 2, 3, 1).to(torch.bfloat16).reshape(-1) for w in ws]).contiguous()
+        wf = torch.zeros_like(wf0)
+        assert lib.conv_wt_flip_launch(wf0.data_ptr(), wf0.shape[1], wf.data_ptr(), wf.shape[1], cpo, cpi, k, k, P, torch.cuda.current_stream().cuda_stream) == 0
+        ncol, c_src = cpi, cpo
+        refs = [torch.nn.grad.conv2d_input((nmax, cin, h, h), w, d, padding=1) for w, d in zip(ws, dys)]
+    out = torch.full((P, nmax * h * h * ncol), 7.0, device=dev, dtype=torch.bfloat16)
+    nb = torch.tensor(nbs, dtype=torch.int32, device=dev)
+    rows = lib.conv_gemm_stats_rows(nmax, h, h)
+    stats = torch.zeros(P, rows * 2 * ncol, device=dev)
+    a = ConvGemmArgs()
+    a.src, a.src_ps, a.src_h, a.src_w, a.src_c = src.data_ptr(), src.shape[1], h, h, c_src
+    a.out_h, a.out_w, a.R, a.S, a.stride, a.pad = h, h, k, k, 1, 1
+    a.wt, a.wt_ps, a.ncol, a.ncol_valid = wf.data_ptr(), wf.shape[1], ncol, (cout if mode == 0 else cin)
+    a.out, a.out_ps, a.nbatch, a.max_batch = out.data_ptr(), out.shape[1], nb.data_ptr(), nmax
+    if mode == 0:
+        a.stats, a.stats_ps, a.stats_rows = stats.data_ptr(), stats.shape[1], rows
+    assert lib.conv_gemm_launch(mode, ctypes.byref(a), P, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    for p in range(P):
+        o = out[p].view(nmax, h, h, ncol)
+        n = nbs[p]
+        c = cout if mode == 0 else cin
+        torch.testing.assert_close(o[:n, ..., :c].float(), refs[p][:n].permute(0, 2, 3, 1), atol=3e-2, rtol=3e-2)
+        assert bool((o[n:] == 7.0).all()), f"peer {p}: rows past its batch were written"
+        if mode == 0:
+            st = stats[p].view(rows, 2, ncol).sum(0)
+            torch.testing.assert_close(st[0, :cout], refs[p][:n].sum((0, 2, 3)), atol=0.5, rtol=2e-2)
