@@ -1292,7 +1292,9 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
 // grid = (ceil(ci / 64) * ceil(co / 64), R * S, peers), block 256.
 __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ wf, int64_t wf_ps, bf16* __restrict__ wt, int64_t wt_ps, int cout,
                                                       int cin, int R, int S, int parity_pad) {
-  __shared__ bf16 tile[64][64 + 8];
+  // row pad 2: the transposed reads (column of 8 rows per 8-lane group, 8 groups) hit 32 distinct
+  // banks; a +8 pad put the groups 32 banks apart (12.4 conflicts per LDS instruction, profiles/r3z_pmc)
+  __shared__ bf16 tile[64][64 + 2];
   const int peer = blockIdx.z, tap = blockIdx.y;  // destination tap (all classes, in class order)
   const int tci = (cin + 63) / 64;
   const int ci0 = (blockIdx.x % tci) * 64, co0 = (blockIdx.x / tci) * 64;
