@@ -1162,6 +1162,132 @@ __global__ __launch_bounds__(256, MINB) void k_conv_wgrad_dma(WgradArgs a, int t
   wgrad_store<BM, BN>(a, acc, peer, co0, n0, ncol_tot);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// k_conv_wgrad_halo<W>: weight gradient of a 3x3 / stride-1 / pad-1 conv with 64 input and 64
+// output channels (ResNet-18 layer 1), from ONE staged X patch per K step instead of nine gathers.
+//   A K step is 64 pixels = 64 / W complete image rows (H * W % 64 == 0). Its nine im2col taps are
+//   shifted windows of the (64 / W + 2) x (W + 2) x 64 patch around those rows (zero padding
+//   outside the image), so the patch is staged once (17 KB at W = 32) where the generic wgrad
+//   gathers 9 x 8 KB. Each B fragment reads its tap's window through the transposed LDS read with
+//   per-lane patch rows: the 8 pixels of a lane group are consecutive within one image row, so
+//   they are 8 consecutive patch rows.
+//   One workgroup computes the whole 64 x 576 gradient of its pixel range: 8 waves as 2 (co halves)
+//   x 4 (column quarters of 144 = 9 fragments), fp32 accumulators, split-K over pixel ranges with
+//   fp32 atomics (as k_conv_wgrad). Register-staged, double-buffered.
+// ------------------------------------------------------------------------------------------------
+// transposed MFMA B fragment whose 8 k rows of lane group g start at patch row rb (per lane)
+__device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int rb, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rb + q, col0 + 4 * p)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rb + q + 4, col0 + 4 * p)));
+  const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, both);
+}
+
+template <int W>
+__global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits) {
+  constexpr int C = 64, RPS = 64 / W, PW = W + 2, PROWS = (RPS + 2) * PW;
+  constexpr int DYE = 64 * C, PE = PROWS * C, STG = DYE + PE;  // bf16 elements per stage
+  constexpr int PCH = PROWS * 8;                                // 16-byte patch chunks per K step
+  constexpr int PPT = (PCH + 511) / 512;                        // patch chunks per thread
+  static_assert(W >= 8 && W <= 64 && (64 % W) == 0, "image width");
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * STG];
+
+  const int peer = blockIdx.z;
+  const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
+  const int HW = a.H * W;
+  const int M = nb * HW;
+  const int split = xcd_remap(blockIdx.x, splits);
+  const int kbeg = split * a.k_per_split;
+  const int kend = min(M, kbeg + a.k_per_split);
+  if (kbeg >= kend) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave & 1, wn = wave >> 1;
+  const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(a.dy + peer * a.dy_ps), rs_x = conv_rsrc(a.x + peer * a.x_ps);
+
+  uint4 rdy, rp[PPT];
+  auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows)
+    {
+      const int row = tid >> 3, ch = tid & 7;
+      rdy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * C + ch * 8) * 2 : CONV_OOB);
+    }
+    const int img = m0 / HW, h0 = (m0 - img * HW) / W;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + 512 * i;
+      const int kp = e >> 3, ch = e & 7;
+      const int pr = kp / PW, pc = kp - pr * PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W;
+      rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * C + ch * 8) * 2 : CONV_OOB);
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* dys = lds + buf * STG;
+    bf16* pat = dys + DYE;
+    *reinterpret_cast<uint4*>(dys + tr_off<64>(tid >> 3, (tid & 7) * 8)) = rdy;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + 512 * i;
+      if (e < PCH) *reinterpret_cast<uint4*>(pat + tr_off<64>(e >> 3, (e & 7) * 8)) = rp[i];
+    }
+  };
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int f = 0; f < 9; ++f) acc[i][f] = zero4();
+
+  const int nk = (kend - kbeg + 63) / 64;
+  load(kbeg);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  const int g = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * 64);
+    const bf16* dys = lds + cur * STG;
+    const bf16* pat = dys + DYE;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = frag_tr<64>(dys, wco * 32 + i * 16, hh * 32, lane);
+      // this lane group's 8 pixels: 32 hh + 8 g .. +7, image row (32 hh + 8 g) / W of the step
+      const int k8 = hh * 32 + 8 * g;
+      const int pbase = (k8 / W) * PW + (k8 % W);  // patch row of tap (0, 0)
+#pragma unroll
+      for (int f = 0; f < 9; ++f) {
+        const int col = wn * 144 + f * 16;  // gradient column (tap, ci): 16 columns within one tap
+        const int tap = col >> 6, ci0 = col & 63;
+        const int r = tap / 3, s_ = tap - 3 * r;
+        const bf16x8 b = frag_tr_rows(pat, ci0, pbase + r * PW + s_, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][f] = mfma_bf16(af[i], b, acc[i][f]);
+      }
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // Wf-layout gradient [64 co][576]: column = tap * 64 + ci
+  float* grad = a.grad + peer * a.grad_ps;
+#pragma unroll
+  for (int f = 0; f < 9; ++f) {
+    const int n = wn * 144 + f * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = wco * 32 + i * 16 + 4 * (lane >> 4) + e;
+        float* dst = grad + (int64_t)co * 576 + n;
+        if (a.accumulate) atomicAdd(dst, acc[i][f][e]);
+        else *dst = acc[i][f][e];
+      }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
@@ -1171,6 +1297,16 @@ static int g_conv_dma_wgs = 0;
 extern "C" int conv_set_dma_wgs(int n) {
   const int old = g_conv_dma_wgs;
   g_conv_dma_wgs = n > 0 ? n : 0;
+  return old;
+}
+// 64-channel 3x3 weight gradients through k_conv_wgrad_halo (MYFYP_WGRAD_HALO=0: the generic kernel)
+static int g_wgrad_halo = [] {
+  const char* e = getenv("MYFYP_WGRAD_HALO");
+  return (e != nullptr && atoi(e) == 0) ? 0 : 1;
+}();
+extern "C" int conv_set_wgrad_halo(int on) {
+  const int old = g_wgrad_halo;
+  if (on >= 0) g_wgrad_halo = on ? 1 : 0;
   return old;
 }
 static int conv_num_cus() {
@@ -1393,6 +1529,16 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   const int tiles_m = (a.dy_c + BM - 1) / BM, tiles_n = (ncol + BN - 1) / BN;
   dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
+  // 64 -> 64 channel 3x3 stride-1 convs (ResNet-18 layer 1): all nine taps from one staged X patch
+  if (g_wgrad_halo && a.pro_ss == nullptr && a.x_c == 64 && a.dy_c == 64 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.Ho == a.H &&
+      a.Wo == a.W && (a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64)) {
+    dim3 hg(splits, 1, peers), hb(512);
+    if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8>), hg, hb, 0, s, a, splits);
+    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16>), hg, hb, 0, s, a, splits);
+    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32>), hg, hb, 0, s, a, splits);
+    else hipLaunchKernelGGL((k_conv_wgrad_halo<64>), hg, hb, 0, s, a, splits);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   // LDS-DMA stage ring (conv_set_dma variant bits 5-6: 0 register stage, 1 two stages, 2 three
   // stages). The default code 1 keeps the register stage: in the engine the two-stage ring measured
   // 3-10 % slower per wgrad shape (same-box kernel traces, profiles/r3z_conv_dma), although the

@@ -99,6 +99,7 @@ _SIGS = {
     "conv_gemm_launch": (c_int, [c_int, c_void_p, c_int, c_void_p]),
     "conv_set_dma": (c_int, [c_int]),
     "conv_set_dma_wgs": (c_int, [c_int]),
+    "conv_set_wgrad_halo": (c_int, [c_int]),
     "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
     "conv_bnb_rows": (c_int, []),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
@@ -392,7 +393,9 @@ class CNNGroup:
                 continue
             M = self.B * L.ho * L.wo
             base = self._wgrad_split_rule(L)[1]
-            cands = sorted({max(1, min(64, int(round(base * f)))) for f in (0.5, 1, 1.5, 2, 3, 4)} | {1})
+            # around the rule, plus a ladder up to 64 (the halo wgrad of the 64-channel layers wants one
+            # workgroup per CU: 32 splits x 8 peers, off the rule's multiples)
+            cands = sorted({max(1, min(64, int(round(base * f)))) for f in (0.5, 1, 1.5, 2, 3, 4)} | {1, 2, 4, 8, 16, 32, 64})
             x = torch.zeros(P, self.B * L.h * L.w * L.cp_in, dtype=torch.bfloat16, device=self.device)
             dy = torch.zeros(P, M * L.cp_out, dtype=torch.bfloat16, device=self.device)
             grad = torch.zeros(P, L.cp_out * L.R * L.S * L.cp_in, dtype=torch.float32, device=self.device)

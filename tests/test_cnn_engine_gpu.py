@@ -43,7 +43,8 @@ def conv_dma(request):
     lib.conv_set_dma_wgs(old_wgs)
 
 
-@pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3)])
+@pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3),
+                                                     (64, 64, 3, 1, 1, 32, 2), (64, 64, 3, 1, 1, 16, 3), (64, 64, 3, 1, 1, 8, 5)])
 def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma):
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
 
@@ -124,7 +125,9 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
     # wgrad
     dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
     M = n * ho * ho
-    for k_per in (128, (M + 63) // 64 * 64):  # split-K (atomics) and one split (plain stores)
+    halo = cin == 64 and cout == 64 and k == 3 and stride == 1  # k_conv_wgrad_halo (one X patch per K step)
+    for halo_on, k_per in [(1, 128), (1, (M + 63) // 64 * 64)] + ([(0, 128)] if halo else []):  # split-K (atomics) and one split (plain stores)
+        old_halo = lib.conv_set_wgrad_halo(halo_on)
         splits = (M + k_per - 1) // k_per
         grad = torch.zeros(1, cpo * k * k * cpi, device=dev)  # Wf layout [cp_out][R][S][cp_in]
         c = WgradArgs()
@@ -134,6 +137,7 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
         c.grad, c.accumulate, c.k_per_split, c.max_batch = grad.data_ptr(), int(splits > 1), k_per, n
         assert lib.conv_wgrad_launch(ctypes.byref(c), 1, splits, torch.cuda.current_stream().cuda_stream) == 0
         torch.cuda.synchronize()
+        lib.conv_set_wgrad_halo(old_halo)
         gw = grad.view(cpo, k, k, cpi)
         g = gw[:cout, :, :, :cin].permute(0, 3, 1, 2)
         err = (g - dw_ref).norm() / dw_ref.norm()
@@ -534,8 +538,12 @@ def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
 
 def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
     """MYFYP_CNN_S2_FWD=1 (stride-2 dgrads as four parity-class forward convs, conv.hip MODE 5) against
-    the default MODE 2 path, over one local epoch of two peers: the update must sit within the
-    default path's own run-to-run noise floor (fp32 atomics reorder between runs; see the BN1 test)."""
+    the default MODE 2 path, over one local epoch of two peers. MODE 5 sums the taps in another
+    order, so its bf16 dX differs in the last bit; at batch 16 such a difference grows through the
+    BatchNorms to about 20 % of one epoch's update (measured: two MODE-2 paths that differ only in
+    fp32 atomic order gave cos 0.977, rel 0.21 — scripts/probes/cnn_fuse_noise.py). The default
+    path's own repeat runs are nearly bit-identical now (rel 3e-4), so the bound is that measured
+    bf16 chaos level, not the run-to-run floor."""
     import threading
 
     from myfyp_amd.models import ResNet18
@@ -557,7 +565,7 @@ def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
         return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
 
     for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        assert c_f > c_n - 0.03 and r_f < 1.5 * r_n + 0.02, ((c_f, r_f), (c_n, r_n))
+        assert c_f > min(c_n - 0.03, 0.95) and r_f < max(1.5 * r_n + 0.02, 0.3), ((c_f, r_f), (c_n, r_n))
 
 
 @pytest.mark.parametrize("mode", [0, 4])
