@@ -1164,8 +1164,9 @@ __global__ __launch_bounds__(256, MINB) void k_conv_wgrad_dma(WgradArgs a, int t
 
 
 // ------------------------------------------------------------------------------------------------
-// k_conv_wgrad_halo<W>: weight gradient of a 3x3 / stride-1 / pad-1 conv with 64 input and 64
-// output channels (ResNet-18 layer 1), from ONE staged X patch per K step instead of nine gathers.
+// k_conv_wgrad_halo<W>: weight gradient of a 3x3 / stride-1 / pad-1 conv (channel counts multiples
+// of 64; ResNet-18 layers 1-3), from ONE staged X patch per K step instead of nine gathers. A
+// workgroup owns a 64-output x 64-input channel block (all nine taps: 64 x 576 gradient columns).
 //   A K step is 64 pixels = 64 / W complete image rows (H * W % 64 == 0). Its nine im2col taps are
 //   shifted windows of the (64 / W + 2) x (W + 2) x 64 patch around those rows (zero padding
 //   outside the image), so the patch is staged once (17 KB at W = 32) where the generic wgrad
@@ -1186,19 +1187,25 @@ __device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int r
 }
 
 template <int W>
-__global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits) {
+__global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits, int tiles_co, int tiles_ci) {
   constexpr int C = 64, RPS = 64 / W, PW = W + 2, PROWS = (RPS + 2) * PW;
   constexpr int DYE = 64 * C, PE = PROWS * C, STG = DYE + PE;  // bf16 elements per stage
   constexpr int PCH = PROWS * 8;                                // 16-byte patch chunks per K step
   constexpr int PPT = (PCH + 511) / 512;                        // patch chunks per thread
   static_assert(W >= 8 && W <= 64 && (64 % W) == 0, "image width");
+  // (C: the 64-channel blocks of dY and X this workgroup stages)
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * STG];
 
   const int peer = blockIdx.z;
   const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
   const int HW = a.H * W;
   const int M = nb * HW;
-  const int split = xcd_remap(blockIdx.x, splits);
+  // consecutive remapped ids (one XCD) share a split, i.e. the same pixels (dY rows and X patch)
+  const int ntile = tiles_co * tiles_ci;
+  const int wgid = xcd_remap(blockIdx.x, ntile * splits);
+  const int split = wgid / ntile, tile = wgid - split * ntile;
+  const int co0 = (tile / tiles_ci) * 64, ci0 = (tile % tiles_ci) * 64;
+  const int ncol = 9 * a.x_c;
   const int kbeg = split * a.k_per_split;
   const int kend = min(M, kbeg + a.k_per_split);
   if (kbeg >= kend) return;
@@ -1210,7 +1217,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
   auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows)
     {
       const int row = tid >> 3, ch = tid & 7;
-      rdy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * C + ch * 8) * 2 : CONV_OOB);
+      rdy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * a.dy_c + co0 + ch * 8) * 2 : CONV_OOB);
     }
     const int img = m0 / HW, h0 = (m0 - img * HW) / W;
 #pragma unroll
@@ -1220,7 +1227,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       const int pr = kp / PW, pc = kp - pr * PW;
       const int h = h0 - 1 + pr, w = pc - 1;
       const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W;
-      rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * C + ch * 8) * 2 : CONV_OOB);
+      rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * a.x_c + ci0 + ch * 8) * 2 : CONV_OOB);
     }
   };
   auto store = [&](int buf) {
@@ -1271,17 +1278,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
     __syncthreads();
     cur ^= 1;
   }
-  // Wf-layout gradient [64 co][576]: column = tap * 64 + ci
+  // Wf-layout gradient [co][tap][ci]: block column n = tap * 64 + local ci
   float* grad = a.grad + peer * a.grad_ps;
 #pragma unroll
   for (int f = 0; f < 9; ++f) {
-    const int n = wn * 144 + f * 16 + (lane & 15);
+    const int nl = wn * 144 + f * 16 + (lane & 15);
+    const int n = (nl >> 6) * a.x_c + ci0 + (nl & 63);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = wco * 32 + i * 16 + 4 * (lane >> 4) + e;
-        float* dst = grad + (int64_t)co * 576 + n;
+        const int co = co0 + wco * 32 + i * 16 + 4 * (lane >> 4) + e;
+        float* dst = grad + (int64_t)co * ncol + n;
         if (a.accumulate) atomicAdd(dst, acc[i][f][e]);
         else *dst = acc[i][f][e];
       }
@@ -1309,6 +1317,11 @@ extern "C" int conv_set_wgrad_halo(int on) {
   if (on >= 0) g_wgrad_halo = on ? 1 : 0;
   return old;
 }
+// widest channel count the halo wgrad takes (0 = any multiple of 64; MYFYP_WGRAD_HALO_MAXC, the A/B knob)
+static int g_wgrad_halo_max_c = [] {
+  const char* e = getenv("MYFYP_WGRAD_HALO_MAXC");
+  return e != nullptr ? atoi(e) : 0;
+}();
 static int conv_num_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -1530,13 +1543,15 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
   // 64 -> 64 channel 3x3 stride-1 convs (ResNet-18 layer 1): all nine taps from one staged X patch
-  if (g_wgrad_halo && a.pro_ss == nullptr && a.x_c == 64 && a.dy_c == 64 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.Ho == a.H &&
-      a.Wo == a.W && (a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64)) {
-    dim3 hg(splits, 1, peers), hb(512);
-    if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8>), hg, hb, 0, s, a, splits);
-    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16>), hg, hb, 0, s, a, splits);
-    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32>), hg, hb, 0, s, a, splits);
-    else hipLaunchKernelGGL((k_conv_wgrad_halo<64>), hg, hb, 0, s, a, splits);
+  if (g_wgrad_halo && a.pro_ss == nullptr && a.x_c % 64 == 0 && a.dy_c % 64 == 0 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 &&
+      a.Ho == a.H && a.Wo == a.W && (a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64) &&
+      (g_wgrad_halo_max_c == 0 || (a.x_c <= g_wgrad_halo_max_c && a.dy_c <= g_wgrad_halo_max_c))) {
+    const int tco = a.dy_c / 64, tci = a.x_c / 64;
+    dim3 hg(splits * tco * tci, 1, peers), hb(512);
+    if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8>), hg, hb, 0, s, a, splits, tco, tci);
+    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16>), hg, hb, 0, s, a, splits, tco, tci);
+    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32>), hg, hb, 0, s, a, splits, tco, tci);
+    else hipLaunchKernelGGL((k_conv_wgrad_halo<64>), hg, hb, 0, s, a, splits, tco, tci);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   // LDS-DMA stage ring (conv_set_dma variant bits 5-6: 0 register stage, 1 two stages, 2 three

@@ -100,6 +100,11 @@ for step in "$@"; do
         run resnet_xt1_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
         MYFYP_NATIVE_LIB=$L0 run resnet_xt0_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       done ;;
+    haloab)  # halo wgrad on 64-channel layers only (MAXC=64) vs all 64-multiples (default), alternating
+      for i in 1 2; do
+        MYFYP_WGRAD_HALO_MAXC=64 run resnet_halo64_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        run resnet_haloall_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

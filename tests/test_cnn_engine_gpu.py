@@ -44,7 +44,8 @@ def conv_dma(request):
 
 
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3),
-                                                     (64, 64, 3, 1, 1, 32, 2), (64, 64, 3, 1, 1, 16, 3), (64, 64, 3, 1, 1, 8, 5)])
+                                                     (64, 64, 3, 1, 1, 32, 2), (64, 64, 3, 1, 1, 16, 3), (64, 64, 3, 1, 1, 8, 5), (128, 128, 3, 1, 1, 16, 2),
+                                                     (256, 128, 3, 1, 1, 8, 3)])
 def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma):
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
 
@@ -125,7 +126,7 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
     # wgrad
     dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride=stride, padding=pad)
     M = n * ho * ho
-    halo = cin == 64 and cout == 64 and k == 3 and stride == 1  # k_conv_wgrad_halo (one X patch per K step)
+    halo = cin % 64 == 0 and cout % 64 == 0 and k == 3 and stride == 1  # k_conv_wgrad_halo (one X patch per K step)
     for halo_on, k_per in [(1, 128), (1, (M + 63) // 64 * 64)] + ([(0, 128)] if halo else []):  # split-K (atomics) and one split (plain stores)
         old_halo = lib.conv_set_wgrad_halo(halo_on)
         splits = (M + k_per - 1) // k_per
