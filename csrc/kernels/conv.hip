@@ -1177,22 +1177,28 @@ __global__ __launch_bounds__(256, MINB) void k_conv_wgrad_dma(WgradArgs a, int t
 //   x 4 (column quarters of 144 = 9 fragments), fp32 accumulators, split-K over pixel ranges with
 //   fp32 atomics (as k_conv_wgrad). Register-staged, double-buffered.
 // ------------------------------------------------------------------------------------------------
-// transposed MFMA B fragment whose 8 k rows of lane group g start at patch row rb (per lane)
-__device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int rb, int lane) {
+// transposed MFMA B fragment whose 8 k rows of lane group g are patch rows rlo + 0..3 and rhi + 0..3
+// (per lane: the two 4-pixel halves of the group, each within one image row)
+__device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int rlo, int rhi, int lane) {
   const int q = (lane & 15) >> 2, p = lane & 3;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rb + q, col0 + 4 * p)));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rb + q + 4, col0 + 4 * p)));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rlo + q, col0 + 4 * p)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + tr_off<64>(rhi + q, col0 + 4 * p)));
   const s16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, both);
 }
 
-template <int W>
+// W: image width; HI: image height when a K step spans several whole images (H * W < 64: one
+// padded patch per image, NI images per step), 0 when it is 64 / W rows of one image
+template <int W, int HI>
 __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits, int tiles_co, int tiles_ci) {
-  constexpr int C = 64, RPS = 64 / W, PW = W + 2, PROWS = (RPS + 2) * PW;
+  constexpr int C = 64;
+  constexpr int NI = HI ? 64 / (HI * W) : 1;    // images per K step
+  constexpr int RR = HI ? HI : 64 / W;          // image rows per K step and image
+  constexpr int PW = W + 2, PIMG = (RR + 2) * PW, PROWS = NI * PIMG;
   constexpr int DYE = 64 * C, PE = PROWS * C, STG = DYE + PE;  // bf16 elements per stage
   constexpr int PCH = PROWS * 8;                                // 16-byte patch chunks per K step
   constexpr int PPT = (PCH + 511) / 512;                        // patch chunks per thread
-  static_assert(W >= 8 && W <= 64 && (64 % W) == 0, "image width");
+  static_assert(W >= 4 && W <= 64 && (HI ? 64 % (HI * W) == 0 : 64 % W == 0), "image shape");
   // (C: the 64-channel blocks of dY and X this workgroup stages)
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * STG];
 
@@ -1214,19 +1220,21 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
   const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(a.dy + peer * a.dy_ps), rs_x = conv_rsrc(a.x + peer * a.x_ps);
 
   uint4 rdy, rp[PPT];
-  auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows)
+  auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows / images)
     {
       const int row = tid >> 3, ch = tid & 7;
       rdy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * a.dy_c + co0 + ch * 8) * 2 : CONV_OOB);
     }
-    const int img = m0 / HW, h0 = (m0 - img * HW) / W;
+    const int img0 = m0 / HW, h0 = HI ? 0 : (m0 - img0 * HW) / W;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int e = tid + 512 * i;
       const int kp = e >> 3, ch = e & 7;
-      const int pr = kp / PW, pc = kp - pr * PW;
-      const int h = h0 - 1 + pr, w = pc - 1;
-      const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W;
+      const int il = kp / PIMG, rem = kp - il * PIMG;
+      const int pr = rem / PW, pc = rem - pr * PW;
+      const int h = h0 - 1 + pr, w = pc - 1, img = img0 + il;
+      // images past the peer's batch (the last step of a multi-image K loop) load zeros
+      const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W && img < nb;
       rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * a.x_c + ci0 + ch * 8) * 2 : CONV_OOB);
     }
   };
@@ -1240,6 +1248,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       if (e < PCH) *reinterpret_cast<uint4*>(pat + tr_off<64>(e >> 3, (e & 7) * 8)) = rp[i];
     }
   };
+  // patch row of tap (0, 0) for pixel p of a K step
+  auto prow = [](int p) { return (p / (RR * W)) * PIMG + ((p % (RR * W)) / W) * PW + (p % W); };
   f32x4 acc[2][9];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1261,15 +1271,15 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = frag_tr<64>(dys, wco * 32 + i * 16, hh * 32, lane);
-      // this lane group's 8 pixels: 32 hh + 8 g .. +7, image row (32 hh + 8 g) / W of the step
+      // this lane group's 8 pixels 32 hh + 8 g .. +7, as two 4-pixel halves within one image row
       const int k8 = hh * 32 + 8 * g;
-      const int pbase = (k8 / W) * PW + (k8 % W);  // patch row of tap (0, 0)
+      const int plo = prow(k8), phi = prow(k8 + 4);
 #pragma unroll
       for (int f = 0; f < 9; ++f) {
         const int col = wn * 144 + f * 16;  // gradient column (tap, ci): 16 columns within one tap
         const int tap = col >> 6, ci0 = col & 63;
         const int r = tap / 3, s_ = tap - 3 * r;
-        const bf16x8 b = frag_tr_rows(pat, ci0, pbase + r * PW + s_, lane);
+        const bf16x8 b = frag_tr_rows(pat, ci0, plo + r * PW + s_, phi + r * PW + s_, lane);
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][f] = mfma_bf16(af[i], b, acc[i][f]);
       }
@@ -1543,15 +1553,16 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   dim3 grid(tiles_m * tiles_n * splits, 1, peers), block(256);
   hipStream_t s = (hipStream_t)stream;
   // 64 -> 64 channel 3x3 stride-1 convs (ResNet-18 layer 1): all nine taps from one staged X patch
+  const bool halo_shape = ((a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64)) || (a.H == 4 && a.W == 4);
   if (g_wgrad_halo && a.pro_ss == nullptr && a.x_c % 64 == 0 && a.dy_c % 64 == 0 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 &&
-      a.Ho == a.H && a.Wo == a.W && (a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64) &&
-      (g_wgrad_halo_max_c == 0 || (a.x_c <= g_wgrad_halo_max_c && a.dy_c <= g_wgrad_halo_max_c))) {
+      a.Ho == a.H && a.Wo == a.W && halo_shape && (g_wgrad_halo_max_c == 0 || (a.x_c <= g_wgrad_halo_max_c && a.dy_c <= g_wgrad_halo_max_c))) {
     const int tco = a.dy_c / 64, tci = a.x_c / 64;
     dim3 hg(splits * tco * tci, 1, peers), hb(512);
-    if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8>), hg, hb, 0, s, a, splits, tco, tci);
-    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16>), hg, hb, 0, s, a, splits, tco, tci);
-    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32>), hg, hb, 0, s, a, splits, tco, tci);
-    else hipLaunchKernelGGL((k_conv_wgrad_halo<64>), hg, hb, 0, s, a, splits, tco, tci);
+    if (a.W == 4) hipLaunchKernelGGL((k_conv_wgrad_halo<4, 4>), hg, hb, 0, s, a, splits, tco, tci);  // 4 images per K step
+    else if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8, 0>), hg, hb, 0, s, a, splits, tco, tci);
+    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16, 0>), hg, hb, 0, s, a, splits, tco, tci);
+    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32, 0>), hg, hb, 0, s, a, splits, tco, tci);
+    else hipLaunchKernelGGL((k_conv_wgrad_halo<64, 0>), hg, hb, 0, s, a, splits, tco, tci);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   // LDS-DMA stage ring (conv_set_dma variant bits 5-6: 0 register stage, 1 two stages, 2 three

@@ -105,6 +105,11 @@ for step in "$@"; do
         MYFYP_WGRAD_HALO_MAXC=64 run resnet_halo64_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
         run resnet_haloall_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       done ;;
+    halo4ab)  # halo wgrad incl. the 4x4-image layer 4 (default) vs without it (MYFYP_WGRAD_HALO_MAXC=256), alternating
+      for i in 1 2; do
+        MYFYP_WGRAD_HALO_MAXC=256 run resnet_h256_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        run resnet_hall_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

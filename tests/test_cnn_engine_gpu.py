@@ -45,7 +45,7 @@ def conv_dma(request):
 
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3),
                                                      (64, 64, 3, 1, 1, 32, 2), (64, 64, 3, 1, 1, 16, 3), (64, 64, 3, 1, 1, 8, 5), (128, 128, 3, 1, 1, 16, 2),
-                                                     (256, 128, 3, 1, 1, 8, 3)])
+                                                     (256, 128, 3, 1, 1, 8, 3), (128, 128, 3, 1, 1, 4, 5), (64, 192, 3, 1, 1, 4, 3)])
 def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma):
     from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
 
