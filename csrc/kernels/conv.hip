@@ -869,6 +869,119 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   conv_epilogue_sums<EMODE, BN, NT>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// k_conv_fwd_halo<MODE>: forward-shaped 3x3 / stride-1 / pad-1 conv with 64 input and 64 output
+// channels on 32-wide images (ResNet-18 layer 1: forward, MODE 0, and the stride-1 dgrad as a
+// forward conv, MODE 4), with the im2col operand read out of ONE staged patch per tile.
+//   A 256-pixel M tile is 8 image rows; its nine taps are shifted windows of the 10 x 34 x 64 patch
+//   around them (43.5 KB, zero padding outside the image) — the LDS-DMA kernel fetches 9 x 32 KB of
+//   im2col rows per tile instead. A fragments are plain 16-byte LDS reads at per-lane patch rows.
+//   The 64 x 576 weights stay in LDS for the whole (persistent) workgroup: nine [64 co][64 k]
+//   tap blocks. 8 waves as 4 x 2 (64 rows x 32 columns each), the shared epilogue
+//   (conv_epilogue_tile / conv_epilogue_sums) with column sums carried across the workgroup's tiles.
+//   The forward prefetches the next tile's patch into registers while the current one is multiplied.
+// ------------------------------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int tiles_m) {
+  static_assert(MODE == 0 || MODE == 4, "forward-shaped convs");
+  constexpr int W = 32, C = 64, BM = 256, BN = 64, NT = 512;
+  constexpr int TR = BM / W, PW = W + 2, PROWS = (TR + 2) * PW;  // tile rows, patch width / rows
+  constexpr int PCH = PROWS * 8, PPT = (PCH + NT - 1) / NT;       // 16-byte patch chunks (per thread)
+  constexpr int WE = 9 * C * BN;                                  // weight elements (bf16)
+  constexpr int PE = PROWS * C;
+  constexpr int EPI = BM * BN * 2;                                // fp32 staging, in bf16 units
+  __shared__ __attribute__((aligned(16))) bf16 lds[WE + (PE > EPI ? PE : EPI)];
+  bf16* wl = lds;       // [tap][64 n][64 k] (swz rows)
+  bf16* pat = lds + WE;  // [patch row][64 ci] (swz rows); the epilogue stages over it
+  const int peer = blockIdx.z;
+  const int nb = a.nbatch ? a.nbatch[peer] : a.max_batch;
+  const int HW = a.src_h * W;
+  const int M = nb * HW;
+  const int tiles_mp = (M + BM - 1) / BM;
+  const int G = gridDim.x;
+  const int g0 = xcd_remap(blockIdx.x, G);
+  if (g0 >= tiles_mp) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(a.src + peer * a.src_ps), rs_wt = conv_rsrc(a.wt + peer * a.wt_ps);
+  // weights once: 9 taps x 64 rows x 8 chunks = 4608 chunks, 9 per thread
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int e = tid + NT * i;
+    const int t = e >> 9, n = (e >> 3) & 63, ch = e & 7;
+    const uint4 v = conv_ld16(rs_wt, n < a.ncol ? (n * 9 * C + t * C + ch * 8) * 2 : CONV_OOB);
+    *reinterpret_cast<uint4*>(wl + t * C * BN + swz(n, ch)) = v;
+  }
+  uint4 rp[PPT];
+  auto load_patch = [&](int tm) {
+    const int m0 = tm * BM;
+    const int img = m0 / HW, h0 = (m0 - img * HW) / W;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + NT * i;
+      const int kp = e >> 3, ch = e & 7;
+      const int pr = kp / PW, pc = kp - pr * PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool ok = e < PCH && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)W && img < nb;
+      rp[i] = conv_ld16(rs_src, ok ? (((img * a.src_h + h) * W + w) * C + ch * 8) * 2 : CONV_OOB);
+    }
+  };
+  auto store_patch = [&]() {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + NT * i;
+      if (e < PCH) *reinterpret_cast<uint4*>(pat + swz(e >> 3, e & 7)) = rp[i];
+    }
+  };
+  // patch row of tap (0, 0) for this lane's A rows (row = wr * 64 + i * 16 + (lane & 15) of the tile)
+  int prow0[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = wr * 64 + i * 16 + (lane & 15);
+    prow0[i] = (p / W) * PW + (p % W);
+  }
+  // MODE 0 prefetches the next tile's patch into registers under the MFMAs; MODE 4's heavier
+  // (BN-backward) epilogue leaves no room for them (27 VGPRs spilled), so it loads after the epilogue
+  constexpr bool PREF = MODE == 0;
+  EpiSums q;
+  q.zero();
+  if (PREF) load_patch(g0);
+  for (int tm = g0; tm < tiles_mp; tm += G) {
+    if (!PREF) load_patch(tm);
+    store_patch();
+    __syncthreads();  // patch (and, the first time, the weights) staged
+    if (PREF && tm + G < tiles_mp) load_patch(tm + G);  // next tile's patch in flight under the MFMAs
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * PW + (t % 3);
+      const bf16* wt_t = wl + t * C * BN;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + (lane >> 4);
+        bf16x8 af[4], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = ld8(pat + swz(prow0[i] + toff, ch));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = ld8(wt_t + swz(wc * 32 + j * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // patch reads done: the epilogue stages over it
+    conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(pat), peer, tm * BM, 0, M, HW, W, 0, 0, q);
+    __syncthreads();  // staging read: the next patch may be stored
+  }
+  conv_epilogue_sums<MODE, BN, NT>(a, pat, peer, 0, g0, q);
+}
+
 // ------------------------------------------------------------------------------------------------
 // weight gradient
 // ------------------------------------------------------------------------------------------------
@@ -1317,6 +1430,16 @@ extern "C" int conv_set_dma_wgs(int n) {
   g_conv_dma_wgs = n > 0 ? n : 0;
   return old;
 }
+// 64-channel 3x3 convs on 32-wide images through k_conv_fwd_halo (MYFYP_FWD_HALO=0: the DMA kernel)
+static int g_fwd_halo = [] {
+  const char* e = getenv("MYFYP_FWD_HALO");
+  return (e != nullptr && atoi(e) == 0) ? 0 : 1;
+}();
+extern "C" int conv_set_fwd_halo(int on) {
+  const int old = g_fwd_halo;
+  if (on >= 0) g_fwd_halo = on ? 1 : 0;
+  return old;
+}
 // 64-channel 3x3 weight gradients through k_conv_wgrad_halo (MYFYP_WGRAD_HALO=0: the generic kernel)
 static int g_wgrad_halo = [] {
   const char* e = getenv("MYFYP_WGRAD_HALO");
@@ -1374,6 +1497,17 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     return 3;
   const bool wide = a.ncol > 64;
   hipStream_t s = (hipStream_t)stream;
+  // 64 -> 64 channel 3x3 convs on 32-wide images (ResNet-18 layer 1): im2col from one staged patch.
+  // Not for the two-BN dgrad epilogue: its extra registers spill here (252 vs 238 us on the DMA kernel)
+  if (((mode == 4 && a.bnb_y1 == nullptr) || (mode == 0 && a.pro_ss == nullptr)) && g_fwd_halo && a.src_c == 64 && a.ncol == 64 && a.R == 3 && a.S == 3 && a.stride == 1 &&
+      a.pad == 1 && a.src_w == 32 && a.out_w == 32 && a.out_h == a.src_h && (a.src_h * 32) % 256 == 0) {
+    const int tiles_m = (a.max_batch * a.out_h * 32 + 255) / 256;
+    int G = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : (conv_num_cus() + peers - 1) / peers;  // one workgroup per CU
+    G = G < 1 ? 1 : (G > tiles_m ? tiles_m : G);
+    if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else hipLaunchKernelGGL((k_conv_fwd_halo<0>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
   if ((mode == 4 || mode == 5 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
     // variant code (conv_set_dma / MYFYP_CONV_DMA): 1 = the measured defaults below; otherwise bits
     // 1-2 pick the 64-channel tile (0 register stage, 1 128x64/3 stages/2 per CU, 2 128x64/2/3,

@@ -100,6 +100,7 @@ _SIGS = {
     "conv_set_dma": (c_int, [c_int]),
     "conv_set_dma_wgs": (c_int, [c_int]),
     "conv_set_wgrad_halo": (c_int, [c_int]),
+    "conv_set_fwd_halo": (c_int, [c_int]),
     "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
     "conv_bnb_rows": (c_int, []),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),

@@ -110,6 +110,13 @@ for step in "$@"; do
         MYFYP_WGRAD_HALO_MAXC=256 run resnet_h256_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
         run resnet_hall_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       done ;;
+    fhaloab)  # layer-1 forward / stride-1 dgrad from one staged patch (default) vs the LDS-DMA kernel (MYFYP_FWD_HALO=0)
+      run epi_fh1 300 python scripts/probes/conv_epi_probe.py
+      MYFYP_FWD_HALO=0 run epi_fh0 300 python scripts/probes/conv_epi_probe.py
+      for i in 1 2; do
+        MYFYP_FWD_HALO=0 run resnet_fh0_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        run resnet_fh1_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;

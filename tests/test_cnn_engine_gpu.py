@@ -38,9 +38,11 @@ def conv_dma(request):
     lib = _lib()
     old = lib.conv_set_dma(1 if request.param == -1 else request.param)
     old_wgs = lib.conv_set_dma_wgs(3 if request.param == -1 else 0)  # dma_persist: 3 workgroups run every M tile
+    old_halo = lib.conv_set_fwd_halo(0 if request.param == 0 else 1)  # regstage: the register-staged kernel everywhere
     yield request.param
     lib.conv_set_dma(old)
     lib.conv_set_dma_wgs(old_wgs)
+    lib.conv_set_fwd_halo(old_halo)
 
 
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h,n", [(3, 64, 3, 1, 1, 32, 4), (64, 128, 3, 2, 1, 16, 3), (64, 128, 1, 2, 0, 16, 2), (6, 16, 5, 1, 0, 14, 5), (256, 512, 3, 2, 1, 8, 2), (16, 24, 3, 2, 1, 7, 2), (8, 16, 1, 2, 0, 9, 3),
@@ -148,7 +150,8 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(cin, cout, k, stride, pad, h, n, conv_dma
 
 @pytest.mark.parametrize("cin,cout,stride,h,n,two,mode", [(64, 64, 1, 16, 3, False, 1), (64, 128, 2, 16, 2, True, 1), (128, 128, 1, 8, 4, True, 1),
                                                           (64, 64, 1, 16, 3, False, 4), (128, 128, 1, 8, 4, True, 4), (64, 128, 1, 8, 2, True, 4),
-                                                          (64, 128, 2, 16, 2, True, 5), (128, 256, 2, 9, 3, False, 5)])
+                                                          (64, 128, 2, 16, 2, True, 5), (128, 256, 2, 9, 3, False, 5),
+                                                          (64, 64, 1, 32, 2, True, 4), (64, 64, 1, 32, 3, False, 4)])
 def test_dgrad_bn_backward_epilogue_vs_torch(cin, cout, stride, h, n, two, mode, conv_dma):
     """dgrad with the BN-backward epilogue: out = bf16(dX + resid) * [mask > 0] and per-channel
     (sum g, sum g*xhat) for one or two BatchNorms, against torch fp32 of the same op. mode 4: the
@@ -570,7 +573,8 @@ def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
 
 
 @pytest.mark.parametrize("mode", [0, 4])
-def test_conv_grouped_peers_with_uneven_batches(mode, conv_dma):
+@pytest.mark.parametrize("cout,h", [(128, 12), (64, 32)])
+def test_conv_grouped_peers_with_uneven_batches(mode, conv_dma, cout, h):
     """Three peers in one launch (grid.z) with per-peer valid batches 5 / 1 / 3 (``nbatch``), forward
     with BN statistics (mode 0) and the stride-1 dgrad as a forward conv (mode 4): every peer's rows
     match torch and rows past a peer's batch are left untouched (the persistent DMA kernel sizes its
@@ -580,7 +584,7 @@ def test_conv_grouped_peers_with_uneven_batches(mode, conv_dma):
     lib = _lib()
     dev = torch.device("cuda")
     torch.manual_seed(5)
-    P, nmax, cin, cout, h, k = 3, 5, 64, 128, 12, 3
+    P, nmax, cin, k = 3, 5, 64, 3  # (64, 32): the halo forward (k_conv_fwd_halo) on layer-1 shapes
     nbs = [5, 1, 3]
     cpi, cpo = _cp(cin), _cp(cout)
     xs = [_bf(torch.randn(nmax, cin, h, h, device=dev)) for _ in range(P)]
