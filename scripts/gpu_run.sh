@@ -154,6 +154,8 @@ for step in "$@"; do
     cnn_prof)  # kernel statistics of the ResNet-18 grouped step
       run cnn_prof 400 rocprofv3 --kernel-trace --stats -d "$O/cnn_prof" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 1 --warmup 1 \
         --n-train 16384 --n-test 2048 ;;
+    cnn_round_prof)  # kernel trace of full-size config-4 rounds (round boundary: evaluation, FedAvg, host gaps)
+      run cnn_round_prof 400 rocprofv3 --kernel-trace -d "$O/cnn_round_prof" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 2 --warmup 1 ;;
     rehearsal)
       for n in 2 4; do
         MYFYP_DIST_BACKEND=gloo run rehearsal_gloo_n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
