@@ -1064,27 +1064,36 @@ class CNNGroup:
 
     def _run_steps(self, key, steps: int, body, scalars: Optional[dict] = None) -> None:
         """Run ``body`` (a whole epoch of steps). The first run of a key is eager (it allocates every
-        buffer); later runs capture it once into a HIP graph and replay it. The graph bakes the
-        optimizer scalars and step offsets in, so they are part of the key."""
+        buffer) and is captured into a HIP graph right after it ran; later runs replay the graph.
+        Capturing in the first round keeps the capture's host time (the GPU idles through it) out
+        of every later round (``MYFYP_CNN_CAPTURE_LATE=1``: capture on the second run instead).
+        The graph bakes the optimizer scalars and step offsets in, so they are part of the key."""
         if self.eager or steps == 0:
             body()
             return
         gkey = key + tuple(sorted((k, v) for k, v in (scalars or {}).items() if isinstance(v, (int, float))))
         g = self._graphs.get(gkey)
         if g is None:
+            late = os.environ.get("MYFYP_CNN_CAPTURE_LATE", "0") == "1"
             if gkey not in self._seen:
                 self._seen.add(gkey)
                 body()
+                if late:
+                    return
+                self._graphs[gkey] = self._capture(body)
                 return
-            cur = torch.cuda.current_stream(self.device)
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(cur)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                body()
-            cur.wait_stream(s)
-            self._graphs[gkey] = g
+            g = self._graphs[gkey] = self._capture(body)
         g.replay()
+
+    def _capture(self, body) -> "torch.cuda.CUDAGraph":
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            body()
+        cur.wait_stream(s)
+        return g
 
     def _eval_all(self) -> None:
         steps = (self.ntmax + self.B - 1) // self.B

@@ -117,6 +117,13 @@ for step in "$@"; do
         MYFYP_FWD_HALO=0 run resnet_fh0_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
         run resnet_fh1_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
       done ;;
+    captab)  # CNN epoch graphs captured in the round that first runs them (default) vs one round later (MYFYP_CNN_CAPTURE_LATE=1)
+      for i in 1 2; do
+        MYFYP_CNN_CAPTURE_LATE=1 run resnet_late_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+        run resnet_early_$i 400 python benchmarks/bench_cnn.py --model resnet18 --rounds 3
+      done
+      MYFYP_CNN_CAPTURE_LATE=1 run lenet_late 300 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 20
+      run lenet_early 300 python benchmarks/bench_cnn.py --model lenet5 --aggregator neighbor --rounds 20 ;;
     onepeer)  # the device work of one rank of the N=8 / N=4 runs: 1 / 2 peers of 7.5k samples each on one GPU (no RCCL)
       run onepeer_p1 300 python bench.py --peers 1 --n-train 7500 --n-test 1250
       run onepeer_p2 300 python bench.py --peers 2 --n-train 15000 --n-test 2500 ;;
