@@ -506,6 +506,29 @@ def test_cnn_graph_replay_matches_eager():
     torch.testing.assert_close(p_e, p_g, atol=2e-3, rtol=2e-2)
 
 
+@pytest.mark.parametrize("late", [False, True])
+def test_cnn_epoch_graph_captured_after_first_run(monkeypatch, late):
+    """The first fit of an epoch shape runs eagerly and is captured right after it (so round 1
+    replays a ready graph); MYFYP_CNN_CAPTURE_LATE=1 captures on the second fit instead. Both
+    placements train (finite losses)."""
+    import threading
+
+    from myfyp_amd.models import LeNet5
+
+    monkeypatch.setenv("MYFYP_CNN_CAPTURE_LATE", "1" if late else "0")
+    learners, _, _ = _make_learners(lambda i: LeNet5(seed=40 + i), 2, 512, 256, 64, 0.05, momentum=0.9)
+    g = learners[0]._engine.group
+    counts, losses = [], []
+    for _ in range(2):
+        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        counts.append(len(g._graphs))
+        losses.append(float(g.stat.view(g.capacity, 4)[0, 0]))
+    assert counts == ([0, 1] if late else [1, 1]), counts
+    assert np.isfinite(losses).all(), losses
+
+
 def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     """BN1-apply + ReLU folded into conv2's forward / wgrad prologues, with the ReLU mask recomputed
     from y1 in the BN backward, against the path that materialises a1 (k_bn_act). The prologue
