@@ -111,7 +111,9 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* base, int col0, int k0, in
 // loads and the output a 16-byte store. Straight from the MFMA layout a lane holds 1 column x 16 rows,
 // i.e. 2-byte accesses (and 3-4x as many VMEM instructions again for the BN-backward operands).
 // Staging layout: [BM][BN] fp32, column XOR-swizzled by bits 2-3 of the row — the four row groups of
-// one MFMA write (rows 4q + e) land in four distinct 16-bank groups. The caller's operand buffers
+// one MFMA write (rows 4q + e) land in four distinct 16-bank groups — and by bit 0 of the row into
+// the other 16-byte half of each 32-byte chunk, so that at BN = 64 the two rows of a 16-lane read
+// phase (8 chunks each) hit disjoint banks. The caller's operand buffers
 // must be idle (a barrier after the last K step's LDS reads).
 // per-thread column sums of the epilogue (8 channels): BN statistics (q0 = sum x, q1 = sum x^2) or
 // BN-backward sums (q0 = sum g, q1 / q2 = sum g * xhat of the one / two BatchNorms)
@@ -189,7 +191,7 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
         for (int e = 0; e < 4; ++e) {
           const int row = wr * 64 - part * SR + i * 16 + 4 * (lane >> 4) + e;
           const int col = wc * (BN / 2) + j * 16 + (lane & 15);
-          cst[row * BN + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
+          cst[row * BN + (col ^ (((row >> 2) & 3) << 4) ^ ((row & 1) << 2))] = acc[i][j][e];
         }
   }
   __syncthreads();
@@ -205,7 +207,7 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       if (bmask != nullptr) um = *reinterpret_cast<const uint4*>(bmask + o);
       if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
       if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
-      const int sw = ((row >> 2) & 3) << 4;
+      const int sw = (((row >> 2) & 3) << 4) ^ ((row & 1) << 2);
       const float4 lo = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8) ^ sw));
       const float4 hi = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8 + 4) ^ sw));
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
