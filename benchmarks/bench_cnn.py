@@ -29,11 +29,13 @@ def parse():
     ap.add_argument("--model", choices=["lenet5", "resnet18"], default="resnet18")
     ap.add_argument("--peers", type=int, default=8)
     ap.add_argument("--batch-size", type=int, default=0, help="0 = 128 for resnet18, 64 for lenet5")
-    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--aggregator", choices=["fedavg", "neighbor", "fedprox"], default="fedavg")
     ap.add_argument("--dirichlet", type=float, default=0.0, help="non-IID Dirichlet alpha (0 = IID)")
     ap.add_argument("--dropout", action="store_true", help="kill one peer at round 1 (fault tolerance)")
+    ap.add_argument("--mu", type=float, default=0.01, help="FedProx proximal coefficient")
+    ap.add_argument("--no-fused", action="store_true", help="torch autograd learner instead of the HIP engine (A/B oracle)")
     ap.add_argument("--n-train", type=int, default=50000)
     ap.add_argument("--n-test", type=int, default=10000)
     ap.add_argument("--torch-step", action="store_true")
@@ -121,6 +123,8 @@ def main() -> None:
     Settings.TRAIN_SET_SIZE = args.peers
     Settings.VOTE_TIMEOUT = Settings.AGGREGATION_TIMEOUT = 3600
     Settings.BATCH_SIZE = B
+    if args.no_fused:
+        Settings.USE_FUSED_KERNELS = False
     Settings.GANG_WINDOW = 30.0
     Settings.DELAYED_AVERAGING = bool(args.delayed_averaging)
     Settings.OVERLAP_COLLECTIVES = not args.no_overlap
@@ -134,7 +138,7 @@ def main() -> None:
         parts = data.generate_partitions(args.peers, DirichletPartitionStrategy, alpha=args.dirichlet)
     else:
         parts = data.generate_partitions(args.peers, RandomIIDPartitionStrategy)
-    mk = {"fedavg": FedAvg, "fedprox": lambda: FedProx(proximal_mu=0.01), "neighbor": lambda: NeighborAvg("ring")}[args.aggregator]
+    mk = {"fedavg": FedAvg, "fedprox": lambda: FedProx(proximal_mu=args.mu), "neighbor": lambda: NeighborAvg("ring")}[args.aggregator]
     model_cls = ResNet18 if args.model == "resnet18" else LeNet5
     gids = [rank * ppr + j for j in range(ppr)]
     nodes = [Node(TorchModel(model_cls(seed=100 + g)), parts[g], address=f"cnn-{g}", protocol=CollectiveCommunicationProtocol, aggregator=mk(),
@@ -191,6 +195,12 @@ def main() -> None:
         for r, v in logs.get(n.addr, {}).get("test_metric", []):
             by_round.setdefault(r, []).append(v)
     curve = {r: float(np.mean(v)) for r, v in sorted(by_round.items())}
+    # local training loss per round (mean over the local peers of their last logged value)
+    loss_curve: dict = {}
+    for r, per_node in sorted(logger.get_local_logs().get("experiment", {}).items()):
+        vals = [v["train_loss"][-1][1] for a, v in per_node.items() if a in local_addrs and v.get("train_loss")]
+        if vals:
+            loss_curve[int(r)] = round(float(np.mean(vals)), 4)
     r_target = t_target = None
     for r, a in curve.items():
         if r >= 1 and a >= args.target_acc and r in landed:
@@ -215,6 +225,7 @@ def main() -> None:
         "partition": f"dirichlet({args.dirichlet})" if args.dirichlet else "iid", "dropout": args.dropout,
         "final_test_acc_mean": round(float(np.mean(accs)), 4) if accs else None,
         "acc_curve": {int(r): round(a, 4) for r, a in curve.items()},
+        "train_loss_curve": loss_curve,
         "target_acc": args.target_acc, "rounds_to_target": r_target, "time_to_target_s": None if t_target is None else round(t_target, 3),
         "data_difficulty": {"similarity": args.similarity, "noise": args.noise, "modes": args.modes, "label_noise": args.label_noise},
         "round_ms_per_local_step": step_ms_engine,

@@ -46,6 +46,8 @@ namespace {
 constexpr uint64_t kMagic = 0x6d79667970736d63ull;  // "myfypsmc"
 constexpr uint64_t kOverflow = ~0ull;
 constexpr uint64_t kGone = 1ull << 63;
+constexpr uint64_t kLeft = 1ull << 62;  // with kGone: the rank left on purpose (shmc_leave), not evicted
+constexpr uint64_t kGenMask = kLeft - 1;
 
 struct Header {
   std::atomic<uint64_t> magic;
@@ -98,7 +100,7 @@ uint64_t now_ns() {
 
 // 1: r took part in generation gen; 0: r never will (gone before it); -1: not decided yet
 int joined(uint64_t s, uint64_t gen) {
-  if (s & kGone) return (s & ~kGone) > gen ? 1 : 0;
+  if (s & kGone) return (s & kGenMask) > gen ? 1 : 0;
   return s >= gen ? 1 : -1;
 }
 
@@ -305,15 +307,28 @@ int shmc_barrier(void* handle, double timeout_s) {
   return rc < 0 ? -1 : 0;
 }
 
-// This rank leaves: it never joins a later generation. 0 ok, 1 already gone.
+// This rank leaves: it never joins a later generation. 0 ok, 1 already gone. The kLeft bit tells
+// the others it left on purpose (after completing every collective it had joined), as opposed to
+// an eviction of an unresponsive rank (shmc_left_clean).
 int shmc_leave(void* handle) {
   Handle* h = static_cast<Handle*>(handle);
   RankCtl* me = h->ctl(h->rank);
   uint64_t s = me->status.load(std::memory_order_acquire);
   while (!(s & kGone)) {
-    if (me->status.compare_exchange_weak(s, kGone | (s + 1), std::memory_order_acq_rel, std::memory_order_acquire)) return 0;
+    if (me->status.compare_exchange_weak(s, kGone | kLeft | (s + 1), std::memory_order_acq_rel, std::memory_order_acquire)) return 0;
   }
   return 1;
+}
+
+// Bitmask of the ranks that left on purpose (shmc_leave), not by eviction.
+uint64_t shmc_left_clean(void* handle) {
+  Handle* h = static_cast<Handle*>(handle);
+  uint64_t mask = 0;
+  for (int r = 0; r < h->world; ++r) {
+    const uint64_t s = h->ctl(r)->status.load(std::memory_order_acquire);
+    if ((s & kGone) && (s & kLeft)) mask |= 1ull << r;
+  }
+  return mask;
 }
 
 void shmc_heartbeat(void* handle) {

@@ -572,8 +572,26 @@ class Federation:
             # section's collectives and leaves at its exit (the others would wait for it otherwise)
             self._depart_deferred = True
         elif self.shm is not None:
-            self.shm.leave()
+            self._leave_clean()
         logger.warning(f"rank{self.rank}", "last local peer stopped mid-experiment: rank departs the federation")
+
+    def _leave_clean(self) -> None:
+        """Leave the shm membership on purpose. The deferred device collectives this rank joined
+        are completed locally first, so the others, when they confirm them, see a rank that left
+        after finishing them (``left_clean``) rather than one that failed inside them: no recovery,
+        and the confirmed round result keeps the leaver's share."""
+        deadline = time.perf_counter() + float(Settings.COLLECTIVE_TIMEOUT)
+        for works, _, _, _ in self._pending:
+            for w in works:
+                while w is not None and time.perf_counter() < deadline:
+                    try:
+                        if w.is_completed():
+                            break
+                    except Exception:
+                        break
+                    time.sleep(0.0005)
+        self._pending.clear()
+        self.shm.leave()
 
     def _apply_members(self, ranks: List[int], force: bool = False) -> None:
         """Every survivor calls this with the same participant set at the same gather (``force``:
@@ -755,7 +773,7 @@ class Federation:
                     if self._depart_deferred:
                         self._depart_deferred = False
                         if self.shm is not None:
-                            self.shm.leave()
+                            self._leave_clean()
 
     def run_aggregation(self, fn: Callable[[], Any]) -> Any:
         """Run ``fn`` (an aggregation: reads the local rows, weight collectives, then writes) in a
@@ -818,8 +836,14 @@ class Federation:
         everyone aborts the group, rebuilds over the survivors and re-runs."""
         ranks, got = self.shm.allgather_members(bool(ok), float(Settings.FAILURE_TIMEOUT))
         frozen = self._frozen[1] if self._frozen is not None else self.members
-        all_ok = ok and got is not None and all(bool(got[r]) for r in ranks) and ranks == list(frozen)
+        # a member missing from the gather is fine only if it left on purpose: it completed the
+        # collectives it had joined before leaving (depart / _leave_clean); an evicted one did not
+        missing = [r for r in frozen if r not in ranks]
+        clean = set(self.shm.left_clean()) if missing else set()
+        all_ok = ok and got is not None and all(bool(got[r]) for r in ranks) and set(ranks) <= set(frozen) and all(r in clean for r in missing)
         if all_ok:
+            if missing:
+                logger.info(f"rank{self.rank}", f"{what}: ranks {missing} left after completing it")
             return
         self.recoveries += 1
         self.record("collective_recovery", 1.0)
@@ -893,15 +917,20 @@ class Federation:
                 self._frozen = (False, members)
                 try:
                     self.await_works(works, "deferred all_reduce")
-                    self._frozen = saved
                 except MembershipChanged as e:
                     logger.warning(f"rank{self.rank}", f"re-running a deferred collective over ranks {self.members} ({e})")
                     self._frozen = None
                     self._pending.clear()
-                    self.run_aggregation(retry)
-                    self._frozen = saved
+                    try:
+                        self.run_aggregation(retry)
+                    finally:
+                        self._frozen = saved
                     self.confirm_collectives()
                     return
+                finally:
+                    # restored on every exit (a gather timeout or a failed retry included): a stale
+                    # frozen state would make every later weights section look nested
+                    self._frozen = saved
 
     @property
     def group(self):

@@ -58,6 +58,8 @@ def _load() -> Optional[ctypes.CDLL]:
     lib.shmc_heartbeat.argtypes = [vp]
     lib.shmc_alive.restype = u64
     lib.shmc_alive.argtypes = [vp]
+    lib.shmc_left_clean.restype = u64
+    lib.shmc_left_clean.argtypes = [vp]
     lib.shmc_wait_all_gone.restype = i
     lib.shmc_wait_all_gone.argtypes = [vp, d, d]
     lib.shmc_unresponsive.restype = u64
@@ -160,6 +162,11 @@ class ShmCollective:
 
     def alive(self) -> List[int]:
         m = int(self._lib.shmc_alive(self._h))
+        return [r for r in range(self.world) if m >> r & 1]
+
+    def left_clean(self) -> List[int]:
+        """Ranks that left on purpose (``leave``) — as opposed to evicted as unresponsive."""
+        m = int(self._lib.shmc_left_clean(self._h))
         return [r for r in range(self.world) if m >> r & 1]
 
     def unresponsive(self, fail_s: float) -> List[int]:

@@ -561,7 +561,9 @@ def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     # the unfused path's repeats are nearly bit-identical since the patch-staged wgrad (no split-K
     # atomics at these shapes), so the floor is also bounded by the measured bf16 chaos level
     for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        assert c_f > min(c_n - 0.03, 0.95) and r_f < max(1.5 * r_n + 0.02, 0.3), ((c_f, r_f), (c_n, r_n))
+        # bounded by the run-to-run floor or, where that floor is ~0, by the measured bf16 chaos
+        # level (cos 0.977, rel 0.21) plus a ~20 % margin — no wider
+        assert c_f > min(c_n - 0.03, 0.965) and r_f < max(1.5 * r_n + 0.02, 0.25), ((c_f, r_f), (c_n, r_n))
     assert abs(l_f - l_u1) < 1e-2 * max(1.0, abs(l_u1)), (l_f, l_u1, l_u2)
 
 
@@ -594,7 +596,9 @@ def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
         return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
 
     for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        assert c_f > min(c_n - 0.03, 0.95) and r_f < max(1.5 * r_n + 0.02, 0.3), ((c_f, r_f), (c_n, r_n))
+        # bounded by the run-to-run floor or, where that floor is ~0, by the measured bf16 chaos
+        # level (cos 0.977, rel 0.21) plus a ~20 % margin — no wider
+        assert c_f > min(c_n - 0.03, 0.965) and r_f < max(1.5 * r_n + 0.02, 0.25), ((c_f, r_f), (c_n, r_n))
 
 
 @pytest.mark.parametrize("mode", [0, 4])

@@ -82,3 +82,22 @@ def test_rank_dies_inside_the_all_reduce(tmp_path):
     expect = (np.array(t0["pre"]) * t0["w"] + np.array(t1["pre"]) * t1["w"]) / (t0["w"] + t1["w"])
     for t in (t0, t1):
         np.testing.assert_allclose(np.array(t["post"]), expect, rtol=1e-5, atol=1e-6)
+
+
+def test_clean_leave_with_a_deferred_all_reduce(tmp_path):
+    """a rank that leaves cleanly while a deferred all-reduce is pending is not
+    a failed collective — the survivors confirm it without a recovery or a retry, and the confirmed
+    round result keeps the departed rank's share (1 + 2 + 3)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OUT_DIR=str(tmp_path))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "clean_leave_worker.py")]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    outs = {int(f.stem[4:]): json.loads(f.read_text()) for f in tmp_path.glob("rank*.json")}
+    assert set(outs) == {0, 1}, res.stderr[-3000:]
+    for r in (0, 1):
+        o = outs[r]
+        assert o["recoveries"] == 0 and o["retried"] == 0, o
+        assert o["result"] == [6.0] * 8, o
+        assert o["members"] == [0, 1], o
+        assert o["next"] == [3.0] * 4, o

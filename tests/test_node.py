@@ -81,6 +81,50 @@ def test_gossip_convergence(data, n, r):
             nd.stop()
 
 
+@pytest.mark.parametrize("seed", range(5))
+def test_gossip_convergence_with_non_trainers(seed):
+    """The reference's (n, r) = (6, 3) case (test/node_test.py:79-132): six nodes connected as a line,
+    TRAIN_SET_SIZE = 4, so every round two nodes sit in WaitAggregatedModelsStage and receive the
+    full model by gossip while the trainers exchange partial aggregates
+    (p2pfl/stages/base_node/train_stage.py:120-176, wait_agg_models_stage.py:40-67). Reference bar
+    as written: stage history, equal models, and test_metric > 0.5 at round index 1 on every node
+    that logs it — over five seeds. The data is synthetic MNIST at stroke noise 0.6, the level at
+    which one node's local model learns this stand-in about as fast as the reference's MLP learns
+    real MNIST (at the default noise 1.0 the first aggregated round lands at 0.40-0.65)."""
+    from myfyp_amd.utils.seed import set_seed
+
+    set_seed(seed)
+    Settings.BATCH_SIZE = 16
+    Settings.TRAIN_SET_SIZE = 4
+    n, r = 6, 3
+    data = synthetic_mnist(6000, 600, seed=3, similarity=0.3, noise=0.6)
+    parts = data.generate_partitions(n, RandomIIDPartitionStrategy, seed=seed)
+    exp = f"gossip63-{seed}-{time.time_ns()}"
+    nodes = [Node(TorchModel(MLP(seed=10 * seed + i)), parts[i], address=f"g63-{seed}-{i}-{time.time_ns()}", exp_name=exp) for i in range(n)]
+    for nd in nodes:
+        nd.start()
+    try:
+        for i in range(n - 1):
+            nodes[i + 1].connect(nodes[i].addr)
+            time.sleep(0.01)
+        wait_convergence(nodes, n - 1, only_direct=False, wait=10)
+        t0 = time.time()
+        _run(nodes, r, timeout=240)
+        assert time.time() - t0 < 240  # reference bound (test/node_test.py:105)
+        for nd in nodes:
+            _history_ok(nd.learning_workflow.history, r)
+        waits = sum(nd.learning_workflow.history.count("WaitAggregatedModelsStage") for nd in nodes)
+        assert waits == (n - Settings.TRAIN_SET_SIZE) * r, waits  # two non-trainers every round
+        check_equal_models(nodes)
+        logs = logger.get_global_logs()[exp]
+        acc1 = [dict(logs[nd.addr]["test_metric"])[1] for nd in nodes if 1 in dict(logs[nd.addr]["test_metric"])]
+        assert len(acc1) == Settings.TRAIN_SET_SIZE, acc1  # the round-1 trainers evaluate the first aggregate
+        assert all(a > 0.5 for a in acc1), acc1
+    finally:
+        for nd in nodes:
+            nd.stop()
+
+
 @pytest.mark.parametrize("aggregator", [FedAvg, FedMedian, lambda: Scaffold(global_lr=1.0), FedProx], ids=["fedavg", "fedmedian", "scaffold", "fedprox"])
 def test_collective_workflow_aggregators(data, aggregator):
     Settings.BATCH_SIZE = 16
