@@ -188,7 +188,10 @@ def main() -> None:
         fed.all_reduce_(t, op="max")
         el = float(t.item())
     logs = logger.get_global_logs().get("experiment", {})
-    accs = [logs[n.addr]["test_metric"][-1][1] for n in nodes if logs.get(n.addr, {}).get("test_metric")]
+    # final accuracy: the peers that evaluated the last round (a peer killed by --dropout stopped
+    # logging at its death; its stale last value is not the federation's final accuracy)
+    last_r = max((r for n in nodes for r, _ in logs.get(n.addr, {}).get("test_metric", [])), default=None)
+    accs = [v for n in nodes for r, v in logs.get(n.addr, {}).get("test_metric", []) if r == last_r]
     # accuracy curve: test_metric logged at round r evaluates the model after round r - 1
     by_round: dict = {}
     for n in nodes:

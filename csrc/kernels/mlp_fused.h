@@ -63,6 +63,7 @@ struct MLPArgs {
   OptParams opt;
   int debug_giveup;  // fp32 persistent epoch test hook: peer + 1 whose first attempt gives up (0 = none)
   int f32_ks;        // fp32 persistent epoch owner K split: 1, 2, or 0 = by P
+  int f32_variant;   // fp32 persistent epoch gang layout: 1 owners + heads, 2 owners only, 0 = default
 };
 
 bool mlp_shape_supported(int D0, int D1, int D2, int D3);

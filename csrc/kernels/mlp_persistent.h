@@ -43,7 +43,8 @@ size_t mlp_persistent_f32_flag_bytes(int P);
 int mlp_persistent_f32_gang();
 int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus);
 int mlp_persistent_f32_launch_wgs(const MLPArgs& a);  // workgroups of one epoch launch
-int mlp_persistent_f32_ks(const MLPArgs& a);          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
+int mlp_persistent_f32_ks(const MLPArgs& a);
+int mlp_persistent_f32_variant(const MLPArgs& a);  // gang layout: 1 owners + heads, 2 owners only          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);

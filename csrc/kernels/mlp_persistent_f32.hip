@@ -35,6 +35,16 @@
 // drain, workgroup meet or flag store, the consumer's data load is its readiness check.
 #include "mlp_persistent.h"
 #include "persist_common.h"
+#include "mlp_f32_common.h"
+
+// gang layout 2 (owners only, two hand-offs per step): mlp_persistent_f32v2.hip
+bool mlp_f32v2_supported(const MLPArgs& a);
+size_t mlp_f32v2_lds(const MLPArgs& a);
+size_t mlp_f32v2_bytes(int P, int Bpad);
+int mlp_f32v2_launch_wgs();
+int mlp_f32v2_resident_capacity(const MLPArgs& a, int num_cus);
+hipError_t mlp_f32v2_prepare(const MLPArgs& a);
+void mlp_f32v2_launch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s);
 
 // Optional phase timestamps (build with -DMLP_STAMPS): peer 0's owner 0 (role 0) and head 0 (role 1),
 // steps < 32, read with mlp_debug_persistent_f32_stamps (wall_clock64 ticks, 100 MHz).
@@ -62,8 +72,8 @@ using persist::row_min16;
 using persist::row_sum16;
 using persist::st_wt128;
 using persist::st_wt32;
+using namespace f32k;
 
-constexpr int NT = 512;  // threads per workgroup (8 waves)
 // A/B switches for timing builds (build variant "stamps+P32_BALANCE=0" etc.): the LDS-resident K
 // step shared out over the waves (1) or carried whole by wave 0 (0); running f64 Adam bias
 // corrections (1) or two fp32 pow() per step (0)
@@ -105,93 +115,11 @@ constexpr int KSMAX = 2;
 __host__ __device__ constexpr int ng_of(int KS) { return NCG * KS; }         // owners per peer
 __host__ __device__ constexpr int roles_of(int KS) { return NCG * KS + NH; }  // workgroups per peer
 __host__ __device__ constexpr int ppl_of(int KS) { return KS == 1 ? 8 : 4; }  // peers per launch
-constexpr int PD1 = 256, PD2 = 128;
 constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH, F_DONE = NCG * KSMAX + 2 * NH;
 constexpr int FPP = F_DONE + NCG * KSMAX + NH;  // flags per peer (laid out for KSMAX): + one commit flag per role
-constexpr unsigned DONE_MARK = 1u << 23;      // commit flag value (above every step's t + 1)
+static_assert(FPP == F32_FPP, "flag block layout shared with mlp_persistent_f32v2.hip");
 constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 799
 
-// K steps of the W1 GEMMs: D0 columns plus at least one padding column, column D0, which carries
-// b1: the X tile holds 1 there for valid rows, so the forward MFMAs add b1 and the dW1 MFMAs
-// produce db1 in the register slot that holds b1 (no separate bias add, sum or update).
-__host__ __device__ inline int ks1_of(int D0) { return D0 / 32 + 1; }
-constexpr int LDD = PD2 + 4;   // fp32 row stride of the owner's dH2 tile [B][128]
-constexpr int LDH1 = PD1 + 4;  // fp32 row stride of the head's H1 tile [B][256]
-constexpr int LD16 = 20;       // fp32 row stride of [*][16] tiles
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 mfma_f32(float a, float b, const f32x4& c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-__device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }
-__device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
-__device__ __forceinline__ float ld_wt32(const float* p) {  // 4-byte L1-bypassing (sc1) load
-  return __builtin_bit_cast(float, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ float4 as_f4(const u32x4& v) { return __builtin_bit_cast(float4, v); }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-}
-// 16-byte sc1 load (L1 bypass) of a handed-off tile
-__device__ __forceinline__ float4 ld_sc1_16(__amdgpu_buffer_rsrc_t r, int byte_off) { return as_f4(__builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16)); }
-
-// frag_b_tr (common.h) with the lane index passed in (a per-step laundered copy)
-__device__ __forceinline__ bf16x8 frag_b_tr_l(const bf16* base, int ld, int k0, int n0, int lane) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const bf16* p0 = base + (k0 + 8 * g + q) * ld + n0 + 4 * pp;
-  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
-  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0 + 4 * ld));
-  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// Exact split of fp32 values into three bf16 terms: x == hi + mid + lo. hi = RNE(x) leaves a
-// remainder that is a multiple of x's 24-bit ulp below 2^16 ulps, mid takes its top 8 bits and lo
-// the last <= 8 (both subtractions are exact), so the three terms carry all 24 significand bits.
-__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bf16 a = (bf16)x[j];
-    const float r = x[j] - (float)a;
-    const bf16 b = (bf16)r;
-    hi[j] = a;
-    mid[j] = b;
-    lo[j] = (bf16)(r - (float)b);
-  }
-}
-// acc += A · (hi + mid + lo), smallest terms first
-__device__ __forceinline__ f32x4 mfma3(const bf16x8& a, const bf16x8& hi, const bf16x8& mid, const bf16x8& lo, f32x4 acc) {
-  acc = mfma_bf16(a, lo, acc);
-  acc = mfma_bf16(a, mid, acc);
-  return mfma_bf16(a, hi, acc);
-}
-
-// Per-element constant of the FedProx / SCAFFOLD gradient terms: g += mu·(w − anchor) + (c − c_i)
-// is g += mu·w + e with e = (c − c_i) − mu·anchor (the mu·w part is folded into weight decay).
-__device__ __forceinline__ float extra_at(const MLPArgs& a, int64_t idx) {
-  float e = 0.f;
-  if (a.cg != nullptr) e = a.cg[idx] - a.cl[idx];
-  if (a.anchor != nullptr) e = fmaf(-a.opt.mu, a.anchor[idx], e);
-  return e;
-}
-
-// torch.optim.Adam / SGD(+momentum, nesterov) update of one register-resident element. The same
-// code updates the head's W2 rows and the owners' W2 replica: identical inputs give identical bits.
-template <bool ADAM, bool EXTRA>
-__device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, float& m, float& v, float e, float lr_t, float inv, float wdmu) {
-  g = fmaf(wdmu, w, g);  // weight decay (+ FedProx mu); 0: exact no-op
-  if (EXTRA) g += e;
-  if (ADAM) {
-    m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
-    v = fmaf(o.beta2, v, (1.f - o.beta2) * (g * g));
-    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv, o.eps);
-    w = fmaf(-lr_t, m * __builtin_amdgcn_rcpf(denom), w);
-  } else {
-    if (o.momentum != 0.f) {
-      m = fmaf(o.momentum, m, g);
-      g = o.nesterov ? fmaf(o.momentum, m, g) : m;
-    }
-    w = fmaf(-o.lr, g, w);
-  }
-}
 
 // H1 partial of K part kh at step t: [P][KSMAX][2][BP][PD1], double-buffered by step parity. An
 // owner reads the other K part's partial of step t at the start of its C phase, while that part may
@@ -201,10 +129,6 @@ __device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, i
   return pb.h1x + (((int64_t)p * KSMAX + kh) * 2 + (t & 1)) * BP * PD1 * H1W;
 }
 
-__device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {
-  const int r = n - t * a.B;
-  return r < 0 ? 0 : (r > a.B ? a.B : r);
-}
 
 // ---- LDS carving (16-byte aligned offsets)
 struct OwnerLds32 {
@@ -1171,8 +1095,6 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 // epoch from the untouched pre-epoch state with its own give-up word err[64 + p] and hand-off
 // flags offset by RETRY_BASE (the aborted attempt's flag values are all smaller), and on success
 // sets err[p] = 2 ("recovered"). Gangs are independent: one peer's give-up never aborts another.
-constexpr unsigned RETRY_BASE = 1u << 24;
-constexpr int ERR_RETRY = 64;  // err layout: [0, 64) first attempt, [64, 128) retry, per peer
 
 template <int BP, bool ADAM, bool EXTRA, int KS>
 __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base, int attempt) {
@@ -1364,6 +1286,22 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
 // K split of a launch: MYFYP_F32_KS=1|2 (tests), else the engine's choice (2 when every active peer
 // sits in the first ppl_of(2) slots: one launch of 40-workgroup gangs does all the work), else 2
 // when P <= ppl_of(2). The occupancy check below may still veto 2.
+// Gang layout: MYFYP_F32_VARIANT=1|2 (A/B runs), else the engine's choice (a.f32_variant), else
+// F32_DEFAULT_VARIANT where it applies.
+#ifndef F32_DEFAULT_VARIANT
+#define F32_DEFAULT_VARIANT 1
+#endif
+int f32_variant(const MLPArgs& a) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("MYFYP_F32_VARIANT");
+    env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+  }
+  int v = env ? env : (a.f32_variant == 1 || a.f32_variant == 2 ? a.f32_variant : F32_DEFAULT_VARIANT);
+  if (v == 2 && !mlp_f32v2_supported(a)) v = 1;
+  return v;
+}
+
 int f32_ks_wanted(const MLPArgs& a) {
   static int env = -1;
   if (env < 0) {
@@ -1417,6 +1355,7 @@ int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS) {
 
 // The K split actually used: the wanted one if its launch is co-resident, else 1.
 int f32_ks(const MLPArgs& a) {
+  if (f32_variant(a) == 2) return 1;
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -1430,9 +1369,10 @@ int f32_ks(const MLPArgs& a) {
 
 }  // namespace
 
-size_t persistent_f32_lds(const MLPArgs& a) { return persistent_f32_lds_ks(a, f32_ks(a)); }
+size_t persistent_f32_lds(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_lds(a) : persistent_f32_lds_ks(a, f32_ks(a)); }
 
 bool mlp_persistent_f32_supported(const MLPArgs& a) {
+  if (f32_variant(a) == 2) return true;  // (layout 2's own shape check passed in f32_variant)
   if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
   if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
   if (a.Bpad != 32 && a.Bpad != 64) return false;
@@ -1442,16 +1382,22 @@ bool mlp_persistent_f32_supported(const MLPArgs& a) {
 
 size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX * 2 * Bpad * PD1 * H1W; }
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
-  // H1 partials (fp32) + partial logits and dH2 as LL (value, tag) pairs
-  return (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * 2) * sizeof(float);
+  // layout 1: H1 partials (fp32) + partial logits and dH2 as LL (value, tag) pairs; layout 2 carves
+  // its own regions from the same allocation
+  const size_t v1 = (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * 2) * sizeof(float);
+  const size_t v2 = mlp_f32v2_bytes(P, Bpad);
+  return v1 > v2 ? v1 : v2;
 }
 size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::FLAG_LINE * sizeof(unsigned); }
 int mlp_persistent_f32_gang() { return roles_of(1); }
 int mlp_persistent_f32_ks(const MLPArgs& a) { return f32_ks(a); }
+int mlp_persistent_f32_variant(const MLPArgs& a) { return f32_variant(a); }
 
 // Workgroups one epoch launch needs (its peers' gangs) and how many the device holds at once.
-int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return ppl_of(f32_ks(a)) * roles_of(f32_ks(a)); }
-int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) { return resident_capacity_ks(a, num_cus, f32_ks(a)); }
+int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_launch_wgs() : ppl_of(f32_ks(a)) * roles_of(f32_ks(a)); }
+int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
+  return f32_variant(a) == 2 ? mlp_f32v2_resident_capacity(a, num_cus) : resident_capacity_ks(a, num_cus, f32_ks(a));
+}
 int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
 
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
@@ -1462,6 +1408,10 @@ hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
                 : (a.Bpad == 64 ? prepare_f32_bp<64, 2>(lds) : prepare_f32_bp<32, 2>(lds));
     if (e != hipSuccess) return e;
   }
+  if (mlp_f32v2_supported(a)) {
+    e = mlp_f32v2_prepare(a);
+    if (e != hipSuccess) return e;
+  }
   return hipFuncSetAttribute((const void*)mlp_eval_f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds32(a.D0));
 }
 
@@ -1469,6 +1419,10 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
     if (e != hipSuccess) return e;
+  }
+  if (f32_variant(a) == 2) {
+    mlp_f32v2_launch(a, pb, s);
+    return hipGetLastError();
   }
   const int KS = f32_ks(a);
   const int ppl = ppl_of(KS);

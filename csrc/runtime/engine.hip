@@ -1185,6 +1185,18 @@ int mlp_engine_set_reserved_cus(void* h, int cus) {
   return 0;
 }
 int mlp_engine_f32_ks(void* h) { return mlp_persistent_f32_ks(((MLPEngine*)h)->a); }
+// fp32 persistent epoch gang layout (1 owners + heads, 2 owners only; 0 = default). Re-captures.
+int mlp_engine_set_f32_variant(void* h, int v) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (v != e->a.f32_variant) {
+    e->a.f32_variant = v;
+    e->f32_cap_bpad = -1;
+    e->invalidate();
+  }
+  return 0;
+}
+int mlp_engine_f32_variant(void* h) { return mlp_persistent_f32_variant(((MLPEngine*)h)->a); }
 
 // Test hook: peer p's next fp32 epochs give up on their first attempt (p < 0: off), at launch or
 // (at_end) at the gang commit after the last step. Re-captures.

@@ -91,6 +91,8 @@ _SIGNATURES = {
     "mlp_engine_set_f32_ks": (c_int, [c_void_p, c_int]),
     "mlp_engine_set_reserved_cus": (c_int, [c_void_p, c_int]),
     "mlp_engine_f32_ks": (c_int, [c_void_p]),
+    "mlp_engine_set_f32_variant": (c_int, [c_void_p, c_int]),
+    "mlp_engine_f32_variant": (c_int, [c_void_p]),
     "mlp_engine_debug_giveup": (c_int, [c_void_p, c_int, c_int]),
     "mlp_engine_prepare": (c_int, [c_void_p, c_void_p]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build

@@ -344,6 +344,10 @@ class Federation:
                 kw = {"timeout": datetime.timedelta(seconds=Settings.COLLECTIVE_TIMEOUT)}
                 if be == "nccl":
                     kw["device_id"] = device
+                    # RCCL's channel cap (one workgroup per channel): the CUs an RCCL kernel can
+                    # hold beside a persistent epoch (rccl_reserved_cus)
+                    os.environ.setdefault("NCCL_MAX_NCHANNELS", str(int(Settings.RCCL_MAX_CHANNELS)))
+                    os.environ.setdefault("NCCL_MAX_CTAS", os.environ["NCCL_MAX_NCHANNELS"])
                 dist.init_process_group(backend=be, **kw)
             store = _default_store()
         inst = cls._instance = cls(rank, world, local_rank, device, store)
@@ -620,7 +624,9 @@ class Federation:
         """Liveness agreement right before a weight collective (a peer may have died since the
         round's vote gather): every survivor leaves with the same member list and process group."""
         if self.collective and not self.departed and self.shm is not None:
+            t0 = time.perf_counter()
             ranks, _ = self.shm.allgather_members(None, float(Settings.FAILURE_TIMEOUT))
+            self.record("cp_sync_members", time.perf_counter() - t0)
             self._apply_members(ranks)
         return self.members
 
@@ -631,7 +637,9 @@ class Federation:
         if not self.collective or self._is_departed():
             return [obj]
         if self.shm is not None:
+            t0 = time.perf_counter()
             ranks, got = self.shm.allgather_members(obj, float(Settings.FAILURE_TIMEOUT))
+            self.record("cp_gather", time.perf_counter() - t0)
             self._apply_members(ranks)
             if got is not None:
                 return [got[r] for r in ranks]
@@ -762,8 +770,10 @@ class Federation:
         with self._section_lock:
             outer = self._frozen is not None
             if not outer:
-                self.confirm_collectives()
-                self.sync_members()
+                # a confirmation that ended in an agreement gather already agreed on the members
+                # (every member took part in it): no second membership gather right after it
+                if not self.confirm_collectives():
+                    self.sync_members()
                 self._frozen = (self.departed, list(self.members))
             try:
                 yield self
@@ -834,7 +844,9 @@ class Federation:
     def _agree(self, ok: bool, group, what: str) -> None:
         """Every member reports whether its collective completed; unless all did and nobody left,
         everyone aborts the group, rebuilds over the survivors and re-runs."""
+        t0 = time.perf_counter()
         ranks, got = self.shm.allgather_members(bool(ok), float(Settings.FAILURE_TIMEOUT))
+        self.record("cp_agree", time.perf_counter() - t0)
         frozen = self._frozen[1] if self._frozen is not None else self.members
         # a member missing from the gather is fine only if it left on purpose: it completed the
         # collectives it had joined before leaving (depart / _leave_clean); an evicted one did not
@@ -844,6 +856,11 @@ class Federation:
         if all_ok:
             if missing:
                 logger.info(f"rank{self.rank}", f"{what}: ranks {missing} left after completing it")
+                # the gather agreed the new member set (every member took part): adopt it, also
+                # for the frozen view of a deferred confirmation
+                self._apply_members(ranks)
+                if self._frozen is not None:
+                    self._frozen = (self._frozen[0], list(self.members))
             return
         self.recoveries += 1
         self.record("collective_recovery", 1.0)
@@ -899,7 +916,7 @@ class Federation:
         members = list(self._frozen[1]) if self._frozen is not None else list(self.members)
         self._pending.append((works, members, retry, self._pg))
 
-    def confirm_collectives(self) -> None:
+    def confirm_collectives(self) -> bool:
         """Confirm the deferred device collectives (every member completed them); on a failure
         the groups are rebuilt and the retained-input retry runs (synchronously confirmed).
 
@@ -910,6 +927,16 @@ class Federation:
         from rows the failed all-reduce left behind; the retry writes the survivors' average of
         round r over them, so round r+1's local progress is discarded and every survivor continues
         from the same, correct, round-r model."""
+        if not self._pending:
+            return False
+        t0 = time.perf_counter()
+        try:
+            self._confirm_pending()
+        finally:
+            self.record("cp_confirm", time.perf_counter() - t0)
+        return self._guarded() and not self._is_departed()
+
+    def _confirm_pending(self) -> None:
         while self._pending:
             works, members, retry, _ = self._pending.pop(0)
             with self._section_lock:
@@ -949,6 +976,16 @@ class Federation:
 
     def record(self, name: str, seconds: float) -> None:
         self.stats.setdefault(name, []).append(seconds)
+
+
+def rccl_reserved_cus() -> int:
+    """CUs a concurrent RCCL collective can occupy: ``Settings.RCCL_RESERVED_CUS`` if set, else the
+    RCCL channel cap in force (NCCL_MAX_NCHANNELS / NCCL_MAX_CTAS, RCCL's own knobs; RCCL launches
+    one workgroup per channel), else ``Settings.RCCL_MAX_CHANNELS``."""
+    if Settings.RCCL_RESERVED_CUS is not None:
+        return int(Settings.RCCL_RESERVED_CUS)
+    caps = [int(os.environ[k]) for k in ("NCCL_MAX_NCHANNELS", "NCCL_MAX_CTAS") if os.environ.get(k, "").isdigit()]
+    return min(caps) if caps else int(Settings.RCCL_MAX_CHANNELS)
 
 
 def _default_store():

@@ -152,6 +152,8 @@ class MLPGroup:
         self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
         self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
         self.force_f32_ks: Optional[int] = None  # test hook: fp32 owner K split (1 or 2)
+        # test / A-B hook: fp32 gang layout (1 owners + heads, 2 owners only; None = default)
+        self.force_f32_variant: Optional[int] = None
         # weight-stationary persistent epoch kernel (csrc/kernels/mlp_persistent.hip): None = auto
         # (used whenever the shape/optimizer is eligible), False = always the 3-launch step path
         self.persistent: Optional[bool] = None
@@ -233,12 +235,15 @@ class MLPGroup:
         # one process per GPU with few peers each (N >= 2 GPUs in bench.py); 8 peers keep 1
         ks = self.force_f32_ks or (2 if self.handles and max(self.handles) < 4 else 1)
         _native.check(lib.mlp_engine_set_f32_ks(self._engine, ks), "set_f32_ks")
+        # a forced K split of 2 is a layout-1 configuration
+        var = self.force_f32_variant or (1 if self.force_f32_ks == 2 else 0)
+        _native.check(lib.mlp_engine_set_f32_variant(self._engine, var), "set_f32_variant")
         # weight collectives on the comm stream may hold CUs while an epoch runs: size the
         # co-resident gangs without them
-        from myfyp_amd.parallel.federation import Federation
+        from myfyp_amd.parallel.federation import Federation, rccl_reserved_cus
 
         fed = Federation._instance
-        reserve = int(Settings.RCCL_RESERVED_CUS) if fed is not None and not fed.solo else 0
+        reserve = rccl_reserved_cus() if fed is not None and not fed.solo else 0
         _native.check(lib.mlp_engine_set_reserved_cus(self._engine, reserve), "set_reserved_cus")
         if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
             _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
@@ -406,6 +411,12 @@ class MLPGroup:
 
             logger.warning("mlp-engine", "persistent epoch: a gang gave up (workgroup not resident) and was re-run by the retry launch")
         return loss, correct, conf
+
+    def f32_variant(self) -> int:
+        """Gang layout the fp32 persistent epoch uses (1 owners + heads, 2 owners only)."""
+        with self.lock:
+            self._ensure_engine()
+            return int(_native.load(required=True).mlp_engine_f32_variant(self._engine))
 
     def f32_ks(self) -> int:
         """Owner K split the fp32 persistent epoch uses (1 or 2)."""

@@ -14,7 +14,7 @@ Additions (MI355X-first):
 from __future__ import annotations
 
 import os
-from typing import Any, Dict
+from typing import Optional, Any, Dict
 
 _CERT_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "certificates")
 
@@ -114,9 +114,16 @@ class Settings:
     # failure-aware weight collectives (single-node shm control plane): liveness polled while
     # waiting, watchdog abort, agreement on every collective, re-run over the survivors
     COLLECTIVE_FAILOVER: bool = True
+    # Channels RCCL may use per collective. RCCL launches one workgroup per channel, so this is also
+    # the number of CUs a concurrent RCCL kernel can hold. Federation.init exports it as RCCL's own
+    # NCCL_MAX_NCHANNELS / NCCL_MAX_CTAS caps unless the environment already sets them; the cap
+    # the process ends up with is what the persistent epoch reserves (rccl_reserved_cus). 32
+    # channels is ample for the latency-bound 0.94 MB MLP all-reduce and for ResNet-18's 22 MB.
+    RCCL_MAX_CHANNELS: int = 32
     # CUs the fp32 MLP persistent epoch leaves to a concurrent RCCL kernel when collectives are
-    # active (co-residency: every workgroup of a gang must be resident at once)
-    RCCL_RESERVED_CUS: int = 32
+    # active (co-residency: every workgroup of a gang must be resident at once). None: derived from
+    # the RCCL channel cap in force (see RCCL_MAX_CHANNELS)
+    RCCL_RESERVED_CUS: Optional[int] = None
     # Node.start() prepares the fused engine (epoch-graph capture and upload, code-object load; no
     # training work) so round 0 does not pay it — like building a compiled model at load time
     ENGINE_PREWARM: bool = True
@@ -205,6 +212,7 @@ class Settings:
             "FORCE_COLLECTIVE": "FORCE_COLLECTIVE",
             "COLLECTIVE_FAILOVER": "COLLECTIVE_FAILOVER",
             "RCCL_RESERVED_CUS": "RCCL_RESERVED_CUS",
+            "RCCL_MAX_CHANNELS": "RCCL_MAX_CHANNELS",
             "ENGINE_PREWARM": "ENGINE_PREWARM",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",

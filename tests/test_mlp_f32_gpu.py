@@ -121,17 +121,20 @@ def _rel_update(pe, pr, p0):
     return ((d_e - d_r).norm() / (d_r.norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize("ks", [1, 2])
+@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2"])
 @pytest.mark.parametrize("B", [64, 32])
 @pytest.mark.parametrize("epochs", [1, 2])
-def test_f32_epoch_matches_torch_adam(dev, B, epochs, ks):
+def test_f32_epoch_matches_torch_adam(dev, B, epochs, layout):
     """Whole local epochs of the fp32 persistent kernel (2 peers, Adam 1e-3, raw 0..255 inputs)
-    vs fp32 autograd + torch.optim.Adam on the same batches: relative update error < 1e-3. Both
-    owner K splits: 1 (24-workgroup gangs, the 8-peer layout) and 2 (40-workgroup gangs)."""
+    vs fp32 autograd + torch.optim.Adam on the same batches: relative update error < 1e-3. Every gang
+    layout: 2 (16 owners, two hand-offs per step: mlp_persistent_f32v2.hip), and layout 1 (owners +
+    heads) at both owner K splits: 1 (24-workgroup gangs) and 2 (40-workgroup gangs)."""
     spec = {"name": "adam", "lr": 1e-3}
     learners, refs, g, n = _setup(dev, 2, B, 1400, 3, spec)
+    ks = 2 if layout == "v1ks2" else 1
     g.force_f32_ks = ks
-    assert g.f32_ks() == ks
+    g.force_f32_variant = 2 if layout == "v2" else 1
+    assert g.f32_ks() == ks and g.f32_variant() == (2 if layout == "v2" else 1)
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     for l in learners:
@@ -176,9 +179,9 @@ def test_f32_optimizers_match_torch(dev, spec):
                 assert rel < 1e-3, f"{spec} peer {i} {name}: relative update error {rel:.2e}"
 
 
-@pytest.mark.parametrize("ks", [1, 2])
+@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2"])
 @pytest.mark.parametrize("kind", ["fedprox", "scaffold"])
-def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, ks):
+def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
     """FedProx mu·(w − anchor) and SCAFFOLD (c − c_i) gradient terms in the fp32 epoch kernel, at
     both owner K splits.
 
@@ -189,8 +192,10 @@ def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, ks):
     terms feed is the same register code and is pinned by test_f32_epoch_matches_torch_adam."""
     spec = {"name": "sgd", "lr": 1e-3, "momentum": 0.9} if kind == "fedprox" else {"name": "sgd", "lr": 1e-4}
     learners, refs, g, n = _setup(dev, 2, 64, 900, 5, spec, scale=0.5)
+    ks = 2 if layout == "v1ks2" else 1
     g.force_f32_ks = ks
-    assert g.f32_ks() == ks
+    g.force_f32_variant = 2 if layout == "v2" else 1
+    assert g.f32_ks() == ks and g.f32_variant() == (2 if layout == "v2" else 1)
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     gen = torch.Generator(device="cpu").manual_seed(9)
@@ -211,11 +216,14 @@ def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, ks):
 
 
 def test_f32_w2_replica_is_bit_identical(dev):
-    """The owners' W2 replica (updated from their own dW2 tile) equals the heads' W2 rows bit for bit."""
+    """Layout 1: the owners' W2 replica (updated from their own dW2 tile) equals the heads' W2 rows
+    bit for bit."""
     from myfyp_amd.ops import _native
 
     spec = {"name": "adam", "lr": 1e-3}
     learners, refs, g, n = _setup(dev, 3, 64, 1500, 6, spec)
+    g.force_f32_variant = 1
+    assert g.f32_variant() == 1
     _pin_perms(dev, g, learners, n)
     chk = torch.full((g.capacity, 128, 256), float("nan"), device=dev)
     lib = _native.load(required=True)
@@ -270,8 +278,9 @@ def test_f32_partial_last_batch_and_bias(dev):
             assert rel < 1e-4, f"peer {i} {name}: relative update error {rel:.2e}"
 
 
+@pytest.mark.parametrize("layout", [2, 1])
 @pytest.mark.parametrize("at_end", [False, True])
-def test_f32_giveup_recovered_by_retry_launch(dev, at_end):
+def test_f32_giveup_recovered_by_retry_launch(dev, at_end, layout):
     """A gang that gives up (here: forced on its first attempt through the engine's test hook, as a
     non-resident workgroup would) is re-run by the in-stream retry launch from the untouched
     pre-epoch state: the epoch result is bit-identical to a run without the give-up, the other
@@ -284,6 +293,8 @@ def test_f32_giveup_recovered_by_retry_launch(dev, at_end):
 
         MLPGroup.reset_all()
         learners, refs, g, n = _setup(dev, 3, 64, 1500, 5, spec)
+        g.force_f32_variant = layout
+        assert g.f32_variant() == layout
         _pin_perms(dev, g, learners, n)
         if forced:
             g.debug_giveup(learners[1]._engine.slot, at_end=at_end)
