@@ -239,12 +239,16 @@ def main() -> None:
                 "collective": coll,
                 "engine": "fused-hip" + ("-eager" if args.eager else "-hipgraph") if fused else "autograd",
             },
-            "time_to_target_s": None if t_target is None else round(t_target, 3),
+            # headline time-to-target: Node.start() (incl. the engine prewarm) + set_start_learning
+            # -> the evaluation that reaches the target (the prewarm moved setup out of
+            # the set_start_learning window; the sum is the honest wall-clock)
+            "time_to_target_s": None if t_target is None else round(node_start_s + t_target, 3),
+            "time_to_target_from_start_learning_s": None if t_target is None else round(t_target, 3),
             "rounds_to_target": r_target,
             "target_acc": args.target_acc,
             "final_test_acc": None if final_acc is None else round(final_acc, 4),
             "node_start_s": round(node_start_s, 4),
-            "node_start_note": "Node.start() of the local peers before set_start_learning, incl. the fused-engine prewarm (epoch-graph capture/upload, code-object load; no training work); time_to_target_s is clocked from set_start_learning",
+            "node_start_note": "Node.start() of the local peers before set_start_learning, incl. the fused-engine prewarm (epoch-graph capture/upload, code-object load; no training work); time_to_target_s = node_start_s + time_to_target_from_start_learning_s",
             "baseline_note": "vs_baseline = value / 1.20 rounds/s, the measured proxy of the reference algorithm (gossip, batch-1 fp32 CPU learner, 8 nodes; BASELINE.md; the reference publishes no number). Context, not parity: this run trains at local batch 64 on the GPU, the proxy at batch 1 on the CPU",
         }
         print(json.dumps(out), flush=True)

@@ -53,6 +53,10 @@ struct ConvGemmArgs {
   // into row t % rows, so the tiles' fp32 atomics spread over `rows` addresses per column
   int stats_rows;
   int bnb_rows;  // same for the BN-backward partials bnb_part0/1 ([rows][2][ncol] per peer)
+  // dgrad epilogue: the ReLU mask of the output comes from y0 itself, mask = (y0*sc + sh > 0) with
+  // this [sc | sh] (2*ncol floats per peer) — the activation relu(BN(y0)) was never materialised
+  // (its consumers read y0 through a BN prologue). Used when bnb_mask is null.
+  const float* bnb_mask_ss; int64_t bnb_mask_ss_ps;
 };
 
 struct WgradArgs {

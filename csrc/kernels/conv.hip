@@ -149,10 +149,11 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
   const bool bnb2 = bnb && a.bnb_part1 != nullptr;
   const bf16* bmask = (bnb && a.bnb_mask) ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
+  const bool ymask = bnb && bmask == nullptr && a.bnb_mask_ss != nullptr;  // mask = relu(BN(y0)) > 0
   const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
   const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
   const bool fstats = !bnb && a.stats != nullptr;
-  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8];
+  float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], msc[8], msh[8];
   float(&q0)[8] = q.q0;
   float(&q1)[8] = q.q1;
   float(&q2)[8] = q.q2;
@@ -162,7 +163,12 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
     const int col = col0 + j;
     cval[j] = col < a.ncol_valid;
     bv[j] = (a.bias != nullptr && cval[j]) ? a.bias[peer * a.bias_ps + col] : 0.f;
-    mean0[j] = inv0[j] = mean1[j] = inv1[j] = 0.f;
+    mean0[j] = inv0[j] = mean1[j] = inv1[j] = msc[j] = msh[j] = 0.f;
+    if (ymask && chok) {
+      const float* ssp = a.bnb_mask_ss + peer * a.bnb_mask_ss_ps;
+      msc[j] = ssp[col];
+      msh[j] = ssp[a.ncol + col];
+    }
     if (bnb && chok) {
       const float* m0p = a.bnb_ms0 + peer * 2 * a.ncol;
       mean0[j] = m0p[col];
@@ -222,6 +228,8 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
         if (!cval[j]) x = 0.f;
         if (bnb) {
           if (bmask != nullptr && !((float)bm.v[j] > 0.f)) x = 0.f;
+          // the bf16 activation relu(y*sc + sh) (bn_relu8) is > 0 exactly when y*sc + sh > 0
+          if (ymask && !(fmaf((float)b0.v[j], msc[j], msh[j]) > 0.f)) x = 0.f;
           ob.v[j] = (bf16)x;
           const float g = (float)ob.v[j];  // the sums see exactly the g the BN apply reads back
           q0[j] += g;
@@ -884,9 +892,10 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
 //   (conv_epilogue_tile / conv_epilogue_sums) with column sums carried across the workgroup's tiles.
 //   The forward prefetches the next tile's patch into registers while the current one is multiplied.
 // ------------------------------------------------------------------------------------------------
-template <int MODE>
+template <int MODE, bool PRO>
 __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int tiles_m) {
   static_assert(MODE == 0 || MODE == 4, "forward-shaped convs");
+  static_assert(!PRO || MODE == 0, "BN prologue on the forward only");
   constexpr int W = 32, C = 64, BM = 256, BN = 64, NT = 512;
   constexpr int TR = BM / W, PW = W + 2, PROWS = (TR + 2) * PW;  // tile rows, patch width / rows
   constexpr int PCH = PROWS * 8, PPT = (PCH + NT - 1) / NT;       // 16-byte patch chunks (per thread)
@@ -916,6 +925,22 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
     *reinterpret_cast<uint4*>(wl + t * C * BN + swz(n, ch)) = v;
   }
   uint4 rp[PPT];
+  // PRO: src is a BatchNorm input y and the operand is relu(y*sc + sh) (bn_relu8, bit-identical to
+  // k_bn_act), applied once per staged pixel as the patch goes to LDS — the patch holds each pixel
+  // once for all nine taps, so the fold costs one transform per element, not nine (the register
+  // stage's prologue fold, MYFYP_CNN_FUSE_BN, repeats it per tap). This thread's chunks are always
+  // channels 8 (tid & 7) .. +7 (NT is a multiple of 8): 16 scale / shift registers. Padding taps
+  // stay 0 (not relu(sh)): `pok` marks the chunks that are real pixels.
+  float psc[8], psh[8];
+  unsigned pok = 0;
+  if (PRO) {
+    const float* pro = a.pro_ss + peer * a.pro_ss_ps;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = pro[(tid & 7) * 8 + j];
+      psh[j] = pro[a.src_c + (tid & 7) * 8 + j];
+    }
+  }
   auto load_patch = [&](int tm) {
     const int m0 = tm * BM;
     const int img = m0 / HW, h0 = (m0 - img * HW) / W;
@@ -927,13 +952,16 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
       const int h = h0 - 1 + pr, w = pc - 1;
       const bool ok = e < PCH && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)W && img < nb;
       rp[i] = conv_ld16(rs_src, ok ? (((img * a.src_h + h) * W + w) * C + ch * 8) * 2 : CONV_OOB);
+      if (PRO) pok = ok ? (pok | (1u << i)) : (pok & ~(1u << i));
     }
   };
   auto store_patch = [&]() {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int e = tid + NT * i;
-      if (e < PCH) *reinterpret_cast<uint4*>(pat + swz(e >> 3, e & 7)) = rp[i];
+      uint4 v = rp[i];
+      if (PRO && ((pok >> i) & 1u)) v = bn_relu8(v, psc, psh);
+      if (e < PCH) *reinterpret_cast<uint4*>(pat + swz(e >> 3, e & 7)) = v;
     }
   };
   // patch row of tap (0, 0) for this lane's A rows (row = wr * 64 + i * 16 + (lane & 15) of the tile)
@@ -1304,7 +1332,7 @@ __device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int r
 
 // W: image width; HI: image height when a K step spans several whole images (H * W < 64: one
 // padded patch per image, NI images per step), 0 when it is 64 / W rows of one image
-template <int W, int HI>
+template <int W, int HI, bool PRO>
 __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits, int tiles_co, int tiles_ci) {
   constexpr int C = 64;
   constexpr int NI = HI ? 64 / (HI * W) : 1;    // images per K step
@@ -1335,6 +1363,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
   const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(a.dy + peer * a.dy_ps), rs_x = conv_rsrc(a.x + peer * a.x_ps);
 
   uint4 rdy, rp[PPT];
+  // PRO: x is a BatchNorm input y and the B operand is relu(y*sc + sh), applied once per staged X
+  // pixel (as k_conv_fwd_halo); this thread's chunks are channels ci0 + 8 (tid & 7) .. +7
+  float psc[8], psh[8];
+  unsigned pok = 0;
+  if (PRO) {
+    const float* pro = a.pro_ss + peer * a.pro_ss_ps;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = pro[ci0 + (tid & 7) * 8 + j];
+      psh[j] = pro[a.x_c + ci0 + (tid & 7) * 8 + j];
+    }
+  }
   auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows / images)
     {
       const int row = tid >> 3, ch = tid & 7;
@@ -1351,6 +1391,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       // images past the peer's batch (the last step of a multi-image K loop) load zeros
       const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W && img < nb;
       rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * a.x_c + ci0 + ch * 8) * 2 : CONV_OOB);
+      if (PRO) pok = ok ? (pok | (1u << i)) : (pok & ~(1u << i));
     }
   };
   auto store = [&](int buf) {
@@ -1360,7 +1401,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int e = tid + 512 * i;
-      if (e < PCH) *reinterpret_cast<uint4*>(pat + tr_off<64>(e >> 3, (e & 7) * 8)) = rp[i];
+      uint4 v = rp[i];
+      if (PRO && ((pok >> i) & 1u)) v = bn_relu8(v, psc, psh);
+      if (e < PCH) *reinterpret_cast<uint4*>(pat + tr_off<64>(e >> 3, (e & 7) * 8)) = v;
     }
   };
   // patch row of tap (0, 0) for pixel p of a K step
@@ -1501,13 +1544,14 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   hipStream_t s = (hipStream_t)stream;
   // 64 -> 64 channel 3x3 convs on 32-wide images (ResNet-18 layer 1): im2col from one staged patch.
   // Not for the two-BN dgrad epilogue: its extra registers spill here (252 vs 238 us on the DMA kernel)
-  if (((mode == 4 && a.bnb_y1 == nullptr) || (mode == 0 && a.pro_ss == nullptr)) && g_fwd_halo && a.src_c == 64 && a.ncol == 64 && a.R == 3 && a.S == 3 && a.stride == 1 &&
+  if (((mode == 4 && a.bnb_y1 == nullptr) || mode == 0) && g_fwd_halo && a.src_c == 64 && a.ncol == 64 && a.R == 3 && a.S == 3 && a.stride == 1 &&
       a.pad == 1 && a.src_w == 32 && a.out_w == 32 && a.out_h == a.src_h && (a.src_h * 32) % 256 == 0) {
     const int tiles_m = (a.max_batch * a.out_h * 32 + 255) / 256;
     int G = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : (conv_num_cus() + peers - 1) / peers;  // one workgroup per CU
     G = G < 1 ? 1 : (G > tiles_m ? tiles_m : G);
-    if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
-    else hipLaunchKernelGGL((k_conv_fwd_halo<0>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_fwd_halo<0, true>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else hipLaunchKernelGGL((k_conv_fwd_halo<0, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   if ((mode == 4 || mode == 5 || (mode == 0 && a.pro_ss == nullptr)) && conv_dma_enabled()) {
@@ -1690,15 +1734,21 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
   hipStream_t s = (hipStream_t)stream;
   // 64 -> 64 channel 3x3 stride-1 convs (ResNet-18 layer 1): all nine taps from one staged X patch
   const bool halo_shape = ((a.H * a.W) % 64 == 0 && (a.W == 8 || a.W == 16 || a.W == 32 || a.W == 64)) || (a.H == 4 && a.W == 4);
-  if (g_wgrad_halo && a.pro_ss == nullptr && a.x_c % 64 == 0 && a.dy_c % 64 == 0 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 &&
+  if (g_wgrad_halo && a.x_c % 64 == 0 && a.dy_c % 64 == 0 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 &&
       a.Ho == a.H && a.Wo == a.W && halo_shape && (g_wgrad_halo_max_c == 0 || (a.x_c <= g_wgrad_halo_max_c && a.dy_c <= g_wgrad_halo_max_c))) {
     const int tco = a.dy_c / 64, tci = a.x_c / 64;
     dim3 hg(splits * tco * tci, 1, peers), hb(512);
-    if (a.W == 4) hipLaunchKernelGGL((k_conv_wgrad_halo<4, 4>), hg, hb, 0, s, a, splits, tco, tci);  // 4 images per K step
-    else if (a.W == 8) hipLaunchKernelGGL((k_conv_wgrad_halo<8, 0>), hg, hb, 0, s, a, splits, tco, tci);
-    else if (a.W == 16) hipLaunchKernelGGL((k_conv_wgrad_halo<16, 0>), hg, hb, 0, s, a, splits, tco, tci);
-    else if (a.W == 32) hipLaunchKernelGGL((k_conv_wgrad_halo<32, 0>), hg, hb, 0, s, a, splits, tco, tci);
-    else hipLaunchKernelGGL((k_conv_wgrad_halo<64, 0>), hg, hb, 0, s, a, splits, tco, tci);
+#define WH_LAUNCH(W_, HI_)                                                                                          \
+  do {                                                                                                               \
+    if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, true>), hg, hb, 0, s, a, splits, tco, tci); \
+    else hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, false>), hg, hb, 0, s, a, splits, tco, tci);                  \
+  } while (0)
+    if (a.W == 4) WH_LAUNCH(4, 4);  // 4 images per K step
+    else if (a.W == 8) WH_LAUNCH(8, 0);
+    else if (a.W == 16) WH_LAUNCH(16, 0);
+    else if (a.W == 32) WH_LAUNCH(32, 0);
+    else WH_LAUNCH(64, 0);
+#undef WH_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   // LDS-DMA stage ring (conv_set_dma variant bits 5-6: 0 register stage, 1 two stages, 2 three

@@ -33,7 +33,7 @@
 #include "mlp_persistent.h"
 
 #ifdef MLP_STAMPS
-__device__ unsigned long long g_p32v2_stamps[32][10];
+__device__ unsigned long long g_p32v2_stamps[32][16];
 #define V2_STAMP(t, i)                                                                         \
   do {                                                                                         \
     if (p == 0 && g == 0 && threadIdx.x == 0 && (t) < 32) g_p32v2_stamps[t][i] = wall_clock64(); \
@@ -62,10 +62,11 @@ constexpr int PPL = 8;  // peers per launch (8 x 16 workgroups)
 constexpr int F1 = 0, F2 = NG, FDONE = 2 * NG;  // flag lines of a peer (within the shared F32_FPP block)
 constexpr int RQ = 3;                           // register-resident W1 K steps per wave (K step 24 in LDS)
 constexpr int W3LD = PD2 + 4;                   // fp32 row stride of the gathered W3 [16][128]
+constexpr int DW3P = (PD2 + 1) * 16;            // floats of one reducer's dW3 partial: [o2][class] + the db3 row
 
 // ---- exchange buffer (floats, from pb.h1x), region-major over peers
 struct V2Layout {
-  int64_t h2p, w3s, dh2r, h2r, dlr, lossp, total;
+  int64_t h2p, w3s, dh2r, dw3p, lossp, total;
 };
 __host__ __device__ inline V2Layout v2_layout(int P, int BP) {
   V2Layout L;
@@ -73,8 +74,7 @@ __host__ __device__ inline V2Layout v2_layout(int P, int BP) {
   L.h2p = o;   o += (int64_t)P * 2 * NG * BP * PD2;  // [P][2][g][mt][w][lane][4]: H2 partials in MFMA C order
   L.w3s = o;   o += (int64_t)P * 2 * NG * 16 * 8;    // [P][2][g][class][8]: W3 columns 8g..8g+7
   L.dh2r = o;  o += (int64_t)P * 2 * BP * PD2;       // [P][2][BP][128]: dH2 rows
-  L.h2r = o;   o += (int64_t)P * 2 * BP * PD2;       // [P][2][BP][128]: H2 rows (post-relu)
-  L.dlr = o;   o += (int64_t)P * 2 * BP * 16;        // [P][2][BP][16]: dlogits rows
+  L.dw3p = o;  o += (int64_t)P * 2 * NG * DW3P;      // [P][2][reducer][129][16]: dW3ᵀ partial over its rows + db3 partial
   L.lossp = o; o += (int64_t)P * NG * 8;             // [P][g][reducer row][2]: epoch loss / correct partials
   L.total = o;
   return L;
@@ -417,6 +417,7 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       *reinterpret_cast<float4*>(sW3 + ((tv & 31) >> 1) * W3LD + 8 * (tv >> 5) + 4 * (tv & 1)) = wv;
     }
     lds_barrier();
+    V2_STAMP(t, 11);
     if (tv < 128) {  // fixed-order sum of the four producer groups, + b2, relu
       f32x4 s = sPart[tv];
 #pragma unroll
@@ -426,6 +427,7 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       for (int i = 0; i < RPO; ++i) sH2r[i * PD2 + tv] = R0 + i < rows ? fmaxf(s[i0_r + i] + b2v, 0.f) : 0.f;
     }
     lds_barrier();
+    V2_STAMP(t, 12);
     if (wave < RPO) {  // row R0 + wave: logits (lane: class c, part h of 32 o2), softmax, NLL, dlogits
       const int i = wave, b = R0 + i;
       const bool cin = c < D3;
@@ -458,7 +460,8 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       if (h == 0) sDl[i * 16 + c] = (rvalid && cin) ? (c == y ? -others : pc) / (float)rows : 0.f;
     }
     lds_barrier();
-    {  // dH2 rows = dlogits · W3 ⊙ [H2 > 0]; publish dH2, H2 and dlogits rows
+    V2_STAMP(t, 13);
+    {  // dH2 rows = dlogits · W3 ⊙ [H2 > 0], and this reducer's share of dW3 / db3; publish both
       const int i = tv >> 7, o2 = tv & 127;
       const int64_t rbase = ((int64_t)p * 2 + par) * BP;
       if (i < RPO) {
@@ -466,9 +469,20 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
         for (int k = 0; k < D3; ++k) acc = fmaf(sDl[i * 16 + k], sW3[k * W3LD + o2], acc);
         const float hv = sH2r[i * PD2 + o2];
         st_wt32(xbase + XL.dh2r + (rbase + R0 + i) * PD2 + o2, hv > 0.f ? acc : 0.f);
-        st_wt32(xbase + XL.h2r + (rbase + R0 + i) * PD2 + o2, hv);
       }
-      if (tv < RPO * 16) st_wt32(xbase + XL.dlr + (rbase + R0 + (tv >> 4)) * 16 + (tv & 15), sDl[tv]);
+      // dW3ᵀ partial over the reducer rows: one MFMA per wave, A = dlogᵀ[class = c][row = h],
+      // B = H2[row = h][o2 = 16w + c] -> C[class 4h + i][o2 16w + c], stored [o2][class]
+      float* dst = xbase + XL.dw3p + (((int64_t)p * 2 + par) * NG + g) * DW3P;
+      const float av = h < RPO ? sDl[h * 16 + c] : 0.f;
+      const float bv = h < RPO ? sH2r[h * PD2 + 16 * wave + c] : 0.f;
+      const f32x4 pw = mfma_f32(av, bv, zero4());
+      st_wt128(dst, DW3P * 4, ((16 * wave + c) * 16 + 4 * h) * 4, __builtin_bit_cast(u32x4, pw));
+      if (tv < 16) {  // db3 partial: Σ over the reducer rows of dlogits
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < RPO; ++r) d += sDl[r * 16 + tv];
+        st_wt32(dst + PD2 * 16 + tv, d);
+      }
     }
     persist::publish(pb.flags, F32_FPP, p, F2 + g, target);
     V2_STAMP(t, 4);
@@ -476,6 +490,17 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
     // ================= C: backward of this slice
     if (!persist::wg_wait(pb.flags, F32_FPP, p, F2, NG, target, pb.err, sOk)) return;
     V2_STAMP(t, 5);
+    // dW3 columns 8g..8g+7 and db3 from the reducers' partials: lane (row r = tv & 15 of a DPP row)
+    // loads reducer r's chunk e = tv >> 4 (o2 = 8g + (e >> 2), classes 4 (e & 3)..+3), the 16 lanes of
+    // a row add their chunks (a fixed butterfly: the same bits in every run); tv < 64 do the same
+    // for db3 (row 128 of every partial; replicated in every owner)
+    float4 w3g, b3g;
+    {
+      const __amdgpu_buffer_rsrc_t rw = rsrc_of(xbase + XL.dw3p + ((int64_t)p * 2 + par) * NG * DW3P, NG * DW3P * 4);
+      const int r = tv & 15, e = tv >> 4;
+      w3g = ld_sc1_16(rw, (r * DW3P + (8 * g + (e >> 2)) * 16 + 4 * (e & 3)) * 4);
+      b3g = ld_sc1_16(rw, (r * DW3P + PD2 * 16 + 4 * (e & 3)) * 4);
+    }
     {
       const __amdgpu_buffer_rsrc_t rd = rsrc_of(xbase + XL.dh2r + ((int64_t)p * 2 + par) * BP * PD2, BP * PD2 * 4);
       float4 v[BP / 16];
@@ -487,21 +512,61 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
         *reinterpret_cast<float4*>(sDH2 + (e >> 5) * LDD + 4 * (e & 31)) = v[k];
       }
     }
+    {
+      const int r = tv & 15, e = tv >> 4;
+      const float s0 = row_sum16(w3g.x), s1 = row_sum16(w3g.y), s2 = row_sum16(w3g.z), s3 = row_sum16(w3g.w);
+      if (r == 0) {
+        const float sv[4] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cls = 4 * (e & 3) + j;
+          if (cls < D3) {
+            const int k = cls * 8 + (e >> 2);
+            upd32<ADAM, EXTRA>(o, sv[j], sW3s[k], sW3s[128 + k], sW3s[256 + k], sW3s[384 + k], lr_t, inv_bc2, wdmu);
+          }
+        }
+      }
+      if (tv < 64) {  // waves 0's four rows: classes 4 (e & 3)..+3 (e = 0..3)
+        const float t0 = row_sum16(b3g.x), t1 = row_sum16(b3g.y), t2 = row_sum16(b3g.z), t3 = row_sum16(b3g.w);
+        if (r == 0) {
+          const float tvv[4] = {t0, t1, t2, t3};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cls = 4 * e + j;
+            if (cls < D3) upd32<ADAM, EXTRA>(o, tvv[j], sB3[cls], sB3[16 + cls], sB3[32 + cls], sB3[48 + cls], lr_t, inv_bc2, wdmu);
+          }
+        }
+      }
+    }
     lds_barrier();
+    V2_STAMP(t, 6);
     // dH2 fragments of this wave's 16 W2 rows, read before the C1 partials overwrite the tile:
     //   C1 (dH1):  A = dH2[16mt + c][16w + 4h + ks]
     //   dW2:       A = dH2ᵀ[o2 = 16w + c][b = 4kb + h]
     float4 av1[MT];
-    float dv[BP / 4];
+    f32x4 gw2;      // dW2[o2 = 16w + 4h + i][k = c] over the batch (two interleaved MFMA chains)
+    float db2s;     // db2[16w + c] partial over rows 4kb + h
     {
       int lq = lane;
       asm volatile("" : "+v"(lq));
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) av1[mt] = *reinterpret_cast<const float4*>(sDH2 + (16 * mt + (lq & 15)) * LDD + 16 * wave + 4 * (lq >> 4));
+      float dv[BP / 4];
 #pragma unroll
       for (int kb = 0; kb < BP / 4; ++kb) dv[kb] = sDH2[(4 * kb + (lq >> 4)) * LDD + 16 * wave + (lq & 15)];
+      f32x4 g0 = zero4(), g1 = zero4();
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; kb += 2) {
+        g0 = mfma_f32(dv[kb], sH1[(4 * kb + (lq >> 4)) * LD16 + (lq & 15)], g0);
+        g1 = mfma_f32(dv[kb + 1], sH1[(4 * kb + 4 + (lq >> 4)) * LD16 + (lq & 15)], g1);
+      }
+      gw2 = g0 + g1;
+      db2s = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < BP / 4; ++kb) db2s += dv[kb];
     }
     lds_barrier();  // every wave holds its fragments: the tile region is free for the partials
+    V2_STAMP(t, 7);
     // C1: dH1 partials — wave w sums its 16 o2 rows (k order o2 = 16w + 4h + ks) with the OLD W2
     {
       f32x4 acc1[MT];
@@ -516,6 +581,7 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc1[mt];
     }
     lds_barrier();
+    V2_STAMP(t, 8);
     if (tv < MT * 64) {
       const int mt = tv >> 6, hh = (tv & 63) >> 4, cc = tv & 15;
       f32x4 s = sRed[mt * 64 + (tv & 63)];
@@ -537,19 +603,14 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       *reinterpret_cast<bf16x4*>(sD3 + 16 * LDT + off) = dm;
       *reinterpret_cast<bf16x4*>(sD3 + 32 * LDT + off) = dl;
     }
-    // W2 columns: dW2[o2 = 16w + 4h + i][k = c] over the batch, update, transposed copy; db2
+    // W2 columns: update from dW2, transposed copy; db2 (rows 4kb + h summed above, then across h)
     {
       int lq = lane;
       asm volatile("" : "+v"(lq));
-      f32x4 acc = zero4();
 #pragma unroll
-      for (int kb = 0; kb < BP / 4; ++kb) acc = mfma_f32(dv[kb], sH1[(4 * kb + (lq >> 4)) * LD16 + (lq & 15)], acc);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, acc[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_t, inv_bc2, wdmu);
+      for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, gw2[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_t, inv_bc2, wdmu);
       w2_transpose(w2c, w2f, lq);
-      float s = 0.f;  // db2[16w + c]: rows 4kb + h here, then across h
-#pragma unroll
-      for (int kb = 0; kb < BP / 4; ++kb) s += dv[kb];
+      float s = db2s;
       s += __shfl_xor(s, 16);
       s += __shfl_xor(s, 32);
       if (lq < 16) {
@@ -557,44 +618,8 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
         upd32<ADAM, EXTRA>(o, s, sB2[k], sB2[128 + k], sB2[256 + k], sB2[384 + k], lr_t, inv_bc2, wdmu);
       }
     }
-    if (wave == NT / 64 - 1) {
-      // W3 columns 8g..8g+7: dW3[class = 4h + i][8g + c] = Σ_b dlog[b][class] · H2[b][8g + c]
-      // (A = dlogᵀ, B = H2 columns), + db3 (replicated): one wave, fragments straight from the
-      // published rows (sc1 loads)
-      int lq = lane;
-      asm volatile("" : "+v"(lq));
-      const int hq = lq >> 4, cq = lq & 15;
-      const __amdgpu_buffer_rsrc_t rl = rsrc_of(xbase + XL.dlr + ((int64_t)p * 2 + par) * BP * 16, BP * 16 * 4);
-      const __amdgpu_buffer_rsrc_t rh = rsrc_of(xbase + XL.h2r + ((int64_t)p * 2 + par) * BP * PD2, BP * PD2 * 4);
-      float dl[BP / 4], hc[BP / 4];
-#pragma unroll
-      for (int ks = 0; ks < BP / 4; ++ks) {
-        dl[ks] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ((4 * ks + hq) * 16 + cq) * 4, 0, 16));
-        hc[ks] = cq < 8 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, ((4 * ks + hq) * PD2 + 8 * g + cq) * 4, 0, 16)) : 0.f;
-      }
-      f32x4 acc = zero4();
-      float s3 = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < BP / 4; ++ks) {
-        acc = mfma_f32(dl[ks], hc[ks], acc);
-        s3 += dl[ks];
-      }
-      s3 += __shfl_xor(s3, 16);
-      s3 += __shfl_xor(s3, 32);
-      if (cq < 8) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int cls = 4 * hq + i;
-          if (cls < D3) {
-            const int e = cls * 8 + cq;
-            upd32<ADAM, EXTRA>(o, acc[i], sW3s[e], sW3s[128 + e], sW3s[256 + e], sW3s[384 + e], lr_t, inv_bc2, wdmu);
-          }
-        }
-      }
-      if (lq < 16 && cq < D3) upd32<ADAM, EXTRA>(o, s3, sB3[cq], sB3[16 + cq], sB3[32 + cq], sB3[48 + cq], lr_t, inv_bc2, wdmu);
-    }
     lds_barrier();
-    V2_STAMP(t, 6);
+    V2_STAMP(t, 9);
     // C2 (every wave, its own K steps): dW1 rows (and db1, in the bias slot) against the exact
     // three-term split of dH1, W1 update, the next batch's columns staged right after this K step's
     // reads (as layout 1, KS = 1)
@@ -658,7 +683,7 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       }
     }
     __syncthreads();
-    V2_STAMP(t, 7);
+    V2_STAMP(t, 10);
   }
 
   // ---- epoch loss / correct partials of this owner's reducer rows (published before the commit)

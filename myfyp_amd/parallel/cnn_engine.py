@@ -52,7 +52,7 @@ class ConvGemmArgs(ctypes.Structure):
         ("bnb_mask", c_void_p), ("bnb_mask_ps", c_int64), ("bnb_y0", c_void_p), ("bnb_y0_ps", c_int64),
         ("bnb_y1", c_void_p), ("bnb_y1_ps", c_int64), ("bnb_ms0", c_void_p), ("bnb_ms1", c_void_p),
         ("bnb_part0", c_void_p), ("bnb_part1", c_void_p), ("bnb_part_ps", c_int64), ("stats_rows", c_int),
-        ("bnb_rows", c_int),
+        ("bnb_rows", c_int), ("bnb_mask_ss", c_void_p), ("bnb_mask_ss_ps", c_int64),
     ]
 
 
@@ -237,6 +237,11 @@ class CNNGroup:
         # epilogue of the dgrad that produces its gradient (k_bn_bwd_reduce skipped for those BNs;
         # MYFYP_CNN_FOLD_BNB=0: the separate reduce pass)
         self.fold_bnb = os.environ.get("MYFYP_CNN_FOLD_BNB", "1") != "0"
+        # ResNet blocks whose conv2 runs on the patch-staged kernels (64 -> 64 channels, 3x3, stride
+        # 1, 32-wide images: layer 1): BN1-apply + ReLU folded into conv2's forward / weight-gradient
+        # patch staging (one transform per staged pixel, not per tap) and the dgrad's ReLU mask taken
+        # from y1 — a1 is never written (MYFYP_CNN_HALO_BN1=0: materialise it as before)
+        self.halo_bn1 = os.environ.get("MYFYP_CNN_HALO_BN1", "1") != "0"
         # wgrad split-K target: workgroups per CU over all peers (more splits = more parallelism and
         # more fp32 atomics on the gradient)
         # stride-1 dgrad as a forward conv over dY with flipped weights (conv.hip MODE 4); 0 = MODE 3
@@ -538,11 +543,13 @@ class CNNGroup:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None,
-             pro: Optional["BNL"] = None, bnb: Optional[tuple] = None) -> None:
+             pro: Optional["BNL"] = None, bnb: Optional[tuple] = None, bnb_mask_bn: Optional["BNL"] = None) -> None:
         """``pro``: src holds that BatchNorm's input y; the conv reads relu(BN(y)) in its prologue.
         ``bnb`` (dgrad): ``(mask, [(bn, y), ...])`` — out is written as the ReLU-masked gradient g and
         the BN-backward sums of each listed BatchNorm (input y) accumulate in the epilogue; follow
-        with ``bn_bwd(..., pre_reduced=True)``."""
+        with ``bn_bwd(..., pre_reduced=True)``. ``bnb_mask_bn`` (with a None mask): the ReLU mask is
+        relu(BN(y0)) > 0 of that BatchNorm, computed from y0 in the epilogue (the activation was
+        never materialised)."""
         lib, P = _lib(), self.capacity
         shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
@@ -600,6 +607,9 @@ class CNNGroup:
             assert mode == 1 and 1 <= len(targets) <= 2 and all(bn.Cp == a.ncol for bn, _ in targets)
             if mask is not None:
                 a.bnb_mask, a.bnb_mask_ps = mask.data_ptr(), mask.shape[1]
+            elif bnb_mask_bn is not None:
+                mss = self.ss(bnb_mask_bn)
+                a.bnb_mask_ss, a.bnb_mask_ss_ps = mss.data_ptr(), mss.shape[1]
             (bn0, y0), rest = targets[0], targets[1:]
             nr = lib.conv_bnb_rows()
             a.bnb_rows = nr
@@ -649,6 +659,16 @@ class CNNGroup:
             _p(stats) if stats is not None else None, stats.shape[1] if stats is not None else 0, rows, self.nb.data_ptr(), hw,
             base + 4 * self._off(g), base + 4 * self._off(b), self.params.shape[1], base + 4 * ro, base + 4 * (ro + self.bn_total), self.params.shape[1],
             bn.C, bn.Cp, bn.eps, bn.momentum, int(train), self.ss(bn).data_ptr(), self.ms(bn).data_ptr(), P, self._stream()), f"bn_fin {bn.name}")
+
+    def _bn1_in_halo(self, c2: "ConvL") -> bool:
+        """conv2 of this block takes BN1 + ReLU in its patch staging (k_conv_fwd_halo /
+        k_conv_wgrad_halo shapes; the halo kernels must be on)."""
+        if not (self.halo_bn1 and not self.fuse_bn1 and self.device.type == "cuda"):
+            return False
+        lib = _lib()
+        on = lib.conv_set_fwd_halo(-1) != 0 and lib.conv_set_wgrad_halo(-1) != 0
+        return (on and c2.cp_in == 64 and c2.cp_out == 64 and c2.R == 3 and c2.S == 3 and c2.stride == 1 and c2.pad == 1 and c2.w == 32
+                and c2.h * 32 % 256 == 0 and c2.colmap is None)
 
     def ss(self, bn: BNL) -> torch.Tensor:
         return self.fbuf(f"ss_{bn.name}", 2 * bn.Cp)
@@ -727,7 +747,7 @@ class CNNGroup:
             self.bn_fin(bn1, st1, rows1, hw1, train)
             y2 = self.act(f"y2_{bi}", B * hw1, c2.cp_out)
             st2 = self.fbuf(f"st2_{bi}", rows1 * 2 * c2.cp_out) if train else None
-            if self.fuse_bn1:  # BN1-apply + ReLU in conv2's operand prologue (a1 never written)
+            if self.fuse_bn1 or self._bn1_in_halo(c2):  # BN1-apply + ReLU in conv2's operand prologue (a1 never written)
                 self.conv(c2, y1, y2, stats=st2, pro=bn1)
             else:
                 a1 = self.act(f"a1_{bi}", B * hw1, c1.cp_out)
@@ -773,7 +793,8 @@ class CNNGroup:
             a_out = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
             a_in = self.act(f"a2_{bi - 1}", B * c1.h * c1.w, c1.cp_in) if bi > 0 else self.act("a_stem", B * c1.h * c1.w, c1.cp_in)
             y1, y2 = self.act(f"y1_{bi}", B * hw1, c1.cp_out), self.act(f"y2_{bi}", B * hw1, c2.cp_out)
-            a1 = None if self.fuse_bn1 else self.act(f"a1_{bi}", B * hw1, c1.cp_out)
+            halo1 = self._bn1_in_halo(c2)
+            a1 = None if (self.fuse_bn1 or halo1) else self.act(f"a1_{bi}", B * hw1, c1.cp_out)
             dy2 = self.act(f"dy2_{bi}", B * hw1, c2.cp_out)
             d_in = self.act(f"d_out_{bi - 1}" if bi > 0 else "d_stem", B * c1.h * c1.w, c1.cp_in)
             mask_out = None if pre else a_out
@@ -796,7 +817,11 @@ class CNNGroup:
                 resid = g
             da1 = self.act(f"da1_{bi}", B * hw1, c1.cp_out)
             dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
-            if self.fuse_bn1:
+            if halo1 and fold:  # a1 never written: mask from y1 in the dgrad epilogue, BN1 in the wgrad staging
+                self.conv(c2, dy2, da1, mode=1, bnb=(None, [(bn1, y1)]), bnb_mask_bn=bn1)
+                self.wgrad(c2, dy2, y1, pro=bn1)
+                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True)
+            elif self.fuse_bn1 or halo1:
                 self.conv(c2, dy2, da1, mode=1)
                 self.wgrad(c2, dy2, y1, pro=bn1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, mask_from_y=True)

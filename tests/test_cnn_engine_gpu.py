@@ -652,3 +652,91 @@ def test_conv_grouped_peers_with_uneven_batches(mode, conv_dma, cout, h):
         if mode == 0:
             st = stats[p].view(rows, 2, ncol).sum(0)
             torch.testing.assert_close(st[0, :cout], refs[p][:n].sum((0, 2, 3)), atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("h,n", [(32, 2), (32, 3)])
+def test_bn_prologue_in_patch_kernels_matches_materialised(h, n):
+    """BN1-apply + ReLU folded into the patch-staged kernels (ResNet-18 layer-1 conv2): the forward
+    (k_conv_fwd_halo with pro_ss) and the weight gradient (k_conv_wgrad_halo with pro_ss) read the
+    BatchNorm input y and transform each staged pixel once; the stride-1 dgrad's BN-backward epilogue
+    takes its ReLU mask from y (bnb_mask_ss). Against the same kernels on the materialised
+    activation a = k_bn_act(y): outputs and weight gradients bit-identical (same bf16 operands, same
+    MFMA order), BatchNorm column sums equal up to their fp32 atomic order."""
+    from myfyp_amd.parallel.cnn_engine import ConvGemmArgs, WgradArgs, _lib
+
+    lib = _lib()
+    dev = torch.device("cuda")
+    s_ = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(5)
+    C, k, pad = 64, 3, 1
+    rows = n * h * h
+    y = (torch.randn(1, rows * C, device=dev) * 2 + 0.3).to(torch.bfloat16)
+    ss = torch.cat([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.5]).view(1, -1).contiguous()
+    a_mat = torch.zeros_like(y)
+    nb = torch.full((1,), n, dtype=torch.int32, device=dev)
+    assert lib.cnn_bn_act(y.data_ptr(), 0, ss.data_ptr(), None, 0, None, 0, None, 1, nb.data_ptr(), rows, h * h, C, a_mat.data_ptr(), 0, 1, s_) == 0
+    w = (torch.randn(C, k, k, C, device=dev) * (1.0 / (C * 9) ** 0.5)).to(torch.bfloat16)  # Wf [co][r][s][ci]
+    srows = lib.conv_gemm_stats_rows(n, h, h)
+
+    def fwd(src, pro):
+        out = torch.zeros_like(y)
+        st = torch.zeros(1, srows * 2 * C, device=dev)
+        a = ConvGemmArgs()
+        a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), h, h, C
+        a.out_h, a.out_w, a.R, a.S, a.stride, a.pad = h, h, k, k, 1, pad
+        a.wt, a.ncol, a.ncol_valid = w.data_ptr(), C, C
+        a.out, a.stats, a.stats_rows, a.max_batch = out.data_ptr(), st.data_ptr(), srows, n
+        if pro:
+            a.pro_ss = ss.data_ptr()
+        assert lib.conv_gemm_launch(0, ctypes.byref(a), 1, s_) == 0
+        torch.cuda.synchronize()
+        return out, st.view(srows, 2, C).sum(0)
+
+    (o_f, st_f), (o_m, st_m) = fwd(y, True), fwd(a_mat, False)
+    assert torch.equal(o_f, o_m)
+    torch.testing.assert_close(st_f, st_m, rtol=1e-5, atol=1e-3)
+
+    dy = torch.randn(1, rows * C, device=dev).to(torch.bfloat16)
+
+    def wgrad(x, pro):
+        grad = torch.zeros(1, C * 9 * C, device=dev)
+        c = WgradArgs()
+        c.dy, c.x = dy.data_ptr(), x.data_ptr()
+        c.H, c.W, c.x_c, c.Ho, c.Wo, c.dy_c = h, h, C, h, h, C
+        c.R, c.S, c.stride, c.pad = k, k, 1, pad
+        c.grad, c.accumulate, c.k_per_split, c.max_batch = grad.data_ptr(), 0, (rows + 63) // 64 * 64, n
+        if pro:
+            c.pro_ss = ss.data_ptr()
+        assert lib.conv_wgrad_launch(ctypes.byref(c), 1, 1, s_) == 0
+        torch.cuda.synchronize()
+        return grad
+
+    assert torch.equal(wgrad(y, True), wgrad(a_mat, False))
+
+    # stride-1 dgrad (MODE 4, flipped weights) with the BN-backward epilogue of this BN: mask from a
+    # (materialised) vs mask from y
+    wt = torch.zeros_like(w)
+    assert lib.conv_wt_flip_launch(w.data_ptr(), 0, wt.data_ptr(), 0, C, C, k, k, 1, s_) == 0
+    ms = torch.cat([torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5]).view(1, -1).contiguous()
+    nr = lib.conv_bnb_rows()
+
+    def dgrad(mask_mat):
+        out = torch.zeros_like(y)
+        part = torch.zeros(1, nr * 2 * C, device=dev)
+        b = ConvGemmArgs()
+        b.src, b.src_h, b.src_w, b.src_c = dy.data_ptr(), h, h, C
+        b.out_h, b.out_w, b.R, b.S, b.stride, b.pad = h, h, k, k, 1, k - 1 - pad
+        b.wt, b.ncol, b.ncol_valid = wt.data_ptr(), C, C
+        b.out, b.max_batch, b.bnb_rows = out.data_ptr(), n, nr
+        b.bnb_y0, b.bnb_ms0, b.bnb_part0 = y.data_ptr(), ms.data_ptr(), part.data_ptr()
+        if mask_mat:
+            b.bnb_mask = a_mat.data_ptr()
+        else:
+            b.bnb_mask_ss = ss.data_ptr()
+        assert lib.conv_gemm_launch(4, ctypes.byref(b), 1, s_) == 0
+        torch.cuda.synchronize()
+        return out, part.view(nr, 2 * C).sum(0)
+
+    (g_m, p_m), (g_y, p_y) = dgrad(True), dgrad(False)
+    assert torch.equal(g_m, g_y)
+    torch.testing.assert_close(p_y, p_m, rtol=1e-5, atol=1e-3)
