@@ -513,29 +513,21 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       }
     }
     {
+      // after the butterfly every lane of the row holds the four sums: lane r < 4 updates class
+      // 4 (e & 3) + r (one optimizer update per lane, not four in a row)
       const int r = tv & 15, e = tv >> 4;
       const float s0 = row_sum16(w3g.x), s1 = row_sum16(w3g.y), s2 = row_sum16(w3g.z), s3 = row_sum16(w3g.w);
-      if (r == 0) {
-        const float sv[4] = {s0, s1, s2, s3};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cls = 4 * (e & 3) + j;
-          if (cls < D3) {
-            const int k = cls * 8 + (e >> 2);
-            upd32<ADAM, EXTRA>(o, sv[j], sW3s[k], sW3s[128 + k], sW3s[256 + k], sW3s[384 + k], lr_t, inv_bc2, wdmu);
-          }
-        }
+      const float sv = r == 0 ? s0 : (r == 1 ? s1 : (r == 2 ? s2 : s3));
+      const int cls = 4 * (e & 3) + r;
+      if (r < 4 && cls < D3) {
+        const int k = cls * 8 + (e >> 2);
+        upd32<ADAM, EXTRA>(o, sv, sW3s[k], sW3s[128 + k], sW3s[256 + k], sW3s[384 + k], lr_t, inv_bc2, wdmu);
       }
-      if (tv < 64) {  // waves 0's four rows: classes 4 (e & 3)..+3 (e = 0..3)
+      if (tv < 64) {  // wave 0's four rows: classes 4e + r (e = 0..3)
         const float t0 = row_sum16(b3g.x), t1 = row_sum16(b3g.y), t2 = row_sum16(b3g.z), t3 = row_sum16(b3g.w);
-        if (r == 0) {
-          const float tvv[4] = {t0, t1, t2, t3};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int cls = 4 * e + j;
-            if (cls < D3) upd32<ADAM, EXTRA>(o, tvv[j], sB3[cls], sB3[16 + cls], sB3[32 + cls], sB3[48 + cls], lr_t, inv_bc2, wdmu);
-          }
-        }
+        const float tsv = r == 0 ? t0 : (r == 1 ? t1 : (r == 2 ? t2 : t3));
+        const int cb = 4 * e + r;
+        if (r < 4 && cb < D3) upd32<ADAM, EXTRA>(o, tsv, sB3[cb], sB3[16 + cb], sB3[32 + cb], sB3[48 + cb], lr_t, inv_bc2, wdmu);
       }
     }
     lds_barrier();
