@@ -24,6 +24,7 @@ constexpr unsigned RETRY_BASE = 1u << 24;  // hand-off flag base of the retry at
 constexpr int ERR_RETRY = 64;              // err layout: [0, 64) first attempt, [64, 128) retry, per peer
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x4 mfma_f32(float a, float b, const f32x4& c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ int kappa(int h, int j) { return j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4); }

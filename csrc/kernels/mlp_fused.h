@@ -70,4 +70,5 @@ bool mlp_shape_supported(int D0, int D1, int D2, int D3);
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s);
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s);
 void mlp_launch_sync_shadow(const MLPArgs& a, hipStream_t s);
-void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s);
+// max_wgs > 0 caps the grid (at least one workgroup per peer); rows are grid-strided
+void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s, int max_wgs = 0);

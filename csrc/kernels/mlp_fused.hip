@@ -653,7 +653,11 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   if (a.flags_zero != nullptr && blockIdx.x == 0)  // the persistent epoch's flags start at 0 (replaces a memset node)
     for (int q = threadIdx.x; q < a.flags_per_peer; q += 256) a.flags_zero[(int64_t)p * a.flags_per_peer + q] = 0u;
   if (!a.ctl[p].x) return;
-  const int i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GATHER_RPW;
+  const int nblk = (a.xb_rows + 4 * GATHER_RPW - 1) / (4 * GATHER_RPW);
+  // grid-stride over the row blocks: a capped grid (the gather ahead of an epoch) leaves the CUs
+  // the running epoch's gangs hold alone
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  const int i0 = (blk * 4 + (threadIdx.x >> 6)) * GATHER_RPW;
   const uint8_t* xp = a.Xp[p];
   const int* yp = a.Yp[p];
   constexpr int QPL = 4;  // uint2 pieces per lane per row (D0 <= 2048)
@@ -696,11 +700,17 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
     }
     if (lane == 0) a.Yb[row] = yp[src[r]];
   }
+  }
 }
 
-void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s) {
+void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s, int max_wgs) {
   const int64_t waves = (a.xb_rows + GATHER_RPW - 1) / GATHER_RPW;
-  hipLaunchKernelGGL(mlp_gather_epoch, dim3((unsigned)((waves + 3) / 4), 1, a.P), dim3(256), 0, s, a);
+  int64_t gx = (waves + 3) / 4;
+  if (max_wgs > 0) {
+    const int64_t cap = max_wgs / a.P > 0 ? max_wgs / a.P : 1;
+    if (gx > cap) gx = cap;
+  }
+  hipLaunchKernelGGL(mlp_gather_epoch, dim3((unsigned)gx, 1, a.P), dim3(256), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -99,6 +99,13 @@ using namespace f32k;
 #ifndef P32_LL_PL
 #define P32_LL_PL 0
 #endif
+// heads' log-softmax over 2 x MT waves, two rows per lane (1), or MT waves, four rows per lane (0):
+// the per-row DPP reductions and exp / log chains are the critical path between the partial-logit
+// hand-off and dH2; the sums over the heads are taken in the same order either way (same bits)
+#ifndef P32_SM8
+#define P32_SM8 1
+#endif
+constexpr int SMR = (P32_SM8 && !P32_LL_PL) ? 2 : 4;  // softmax rows per lane
 #ifndef P32_LL_DH2
 #define P32_LL_DH2 0
 #endif
@@ -791,11 +798,16 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     const unsigned tag = persist::ll_tag(gen, pb.fbase, t);
 
     // labels of this lane's softmax rows, loaded before the waits (off the critical path)
-    int yv[4] = {-1, -1, -1, -1};
-    if (wave < MT) {
+    // softmax wave w: rows 16 (w / (4 / SMR)) + 4h + SMR (w % (4 / SMR)) + i, i < SMR
+    constexpr int SMW = MT * (4 / SMR);  // softmax waves
+    const int sm_mt = wave / (4 / SMR), sm_i0 = SMR * (wave % (4 / SMR));
+    int yv[SMR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = 16 * wave + 4 * h + i;
+    for (int i = 0; i < SMR; ++i) yv[i] = -1;
+    if (wave < SMW) {
+#pragma unroll
+      for (int i = 0; i < SMR; ++i) {
+        const int b = 16 * sm_mt + 4 * h + sm_i0 + i;
         if (b < rows) yv[i] = a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b];
       }
     }
@@ -926,28 +938,19 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     // ---- logits = Σ_heads partials (fixed order: every head gets the same bits) + b3, straight
     //      into the softmax lanes' registers; each softmax wave polls its own LL chunks
     // ---- log-softmax + NLL + argmax + dlogits of the whole batch (wave w < MT: rows 16w..)
-    if (wave < MT) {
+    if (wave < SMW) {
+      float lsum[SMR];
 #if P32_LL_PL
       const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16 * 2, NH * BP * 16 * 8);
       persist::ll_u32x4 u[2 * NH];
       const bool ok = persist::ll_wait(u, [&](int k) { return persist::ll_ld2(r, (k >> 1) * BP * 16 * 8 + (wave * 64 + lane) * 32 + (k & 1) * 16); }, tag, pb.err);
       if (!ok) sOk[1] = 0;
-#else
-      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16 * 2, NH * BP * 16 * 8);
-      float4 uf[NH];
-#pragma unroll
-      for (int k = 0; k < NH; ++k) uf[k] = ld_sc1_16(r, k * BP * 16 * 8 + (wave * 64 + lane) * 16);
-#endif
       if (hd == 0) P32_STAMP(1, t, 5);
       float4 sl = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < NH; ++k) {
-#if P32_LL_PL
         const float4 vk = {__uint_as_float(u[2 * k][0]), __uint_as_float(u[2 * k][2]), __uint_as_float(u[2 * k + 1][0]),
                            __uint_as_float(u[2 * k + 1][2])};
-#else
-        const float4 vk = uf[k];
-#endif
         if (k == 0) {
           sl = vk;
         } else {
@@ -957,11 +960,42 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
           sl.w += vk.w;
         }
       }
-      const float lsum[4] = {sl.x, sl.y, sl.z, sl.w};
+      lsum[0] = sl.x;
+      lsum[1] = sl.y;
+      lsum[2] = sl.z;
+      lsum[3] = sl.w;
+#else
+      // this lane's SMR rows of every head's partial-logit chunk (MFMA C order [mt][lane][4 rows])
+      const __amdgpu_buffer_rsrc_t r = rsrc_of(pb.plx + (int64_t)p * NH * BP * 16 * 2, NH * BP * 16 * 8);
+      float uf[NH][SMR];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) {
+        const int off = k * BP * 16 * 8 + (sm_mt * 64 + lane) * 16 + sm_i0 * 4;
+        if (SMR == 4) {
+          const float4 v = ld_sc1_16(r, off);
+          uf[k][0] = v.x;
+          uf[k][1] = v.y;
+          uf[k][SMR > 2 ? 2 : 0] = v.z;
+          uf[k][SMR > 3 ? 3 : 0] = v.w;
+        } else {
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16);
+          uf[k][0] = __uint_as_float(v[0]);
+          uf[k][1] = __uint_as_float(v[1]);
+        }
+      }
+      if (hd == 0) P32_STAMP(1, t, 5);
+#pragma unroll
+      for (int i = 0; i < SMR; ++i) {
+        float sv = uf[0][i];
+#pragma unroll
+        for (int k = 1; k < NH; ++k) sv += uf[k][i];
+        lsum[i] = sv;
+      }
+#endif
       const float b3 = sB3[c];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = 16 * wave + 4 * h + i;
+      for (int i = 0; i < SMR; ++i) {
+        const int b = 16 * sm_mt + 4 * h + sm_i0 + i;
         const bool rvalid = b < rows;
         const int y = yv[i];
         const float logit = cin ? lsum[i] + b3 : -INFINITY;
@@ -1075,7 +1109,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     a.m[idx] = sB3[16 + k];
     if (ADAM) a.v[idx] = sB3[32 + k];
   }
-  if (hd == 0 && wave < MT) {
+  if (hd == 0 && wave < MT * (4 / SMR)) {
     const float l = wave_sum(loss_acc), cr = wave_sum(correct_acc);
     if (lane == 0) {
       atomicAdd(&a.loss_acc[p], l);
@@ -1287,17 +1321,26 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
 // sits in the first ppl_of(2) slots: one launch of 40-workgroup gangs does all the work), else 2
 // when P <= ppl_of(2). The occupancy check below may still veto 2.
 // Gang layout: MYFYP_F32_VARIANT=1|2 (A/B runs), else the engine's choice (a.f32_variant), else
-// F32_DEFAULT_VARIANT where it applies.
+// F32_DEFAULT_VARIANT, except for the Adam + FedProx/SCAFFOLD epoch at K split 1: layout 1's
+// instantiation spills VGPRs there (W1's register-resident Adam state plus the per-weight extra
+// term, with LDS full), layout 2's does not, so that one defaults to layout 2.
 #ifndef F32_DEFAULT_VARIANT
 #define F32_DEFAULT_VARIANT 1
 #endif
+int f32_ks_v1(const MLPArgs& a);
+
 int f32_variant(const MLPArgs& a) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("MYFYP_F32_VARIANT");
     env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }
-  int v = env ? env : (a.f32_variant == 1 || a.f32_variant == 2 ? a.f32_variant : F32_DEFAULT_VARIANT);
+  int v = env;
+  if (!v && (a.f32_variant == 1 || a.f32_variant == 2)) v = a.f32_variant;
+  if (!v) {
+    const bool adam_extra = a.opt.kind == 0 && (a.anchor != nullptr || a.cg != nullptr);
+    v = (adam_extra && f32_ks_v1(a) == 1) ? 2 : F32_DEFAULT_VARIANT;
+  }
   if (v == 2 && !mlp_f32v2_supported(a)) v = 1;
   return v;
 }
@@ -1353,9 +1396,8 @@ int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS) {
   return per_cu * num_cus;
 }
 
-// The K split actually used: the wanted one if its launch is co-resident, else 1.
-int f32_ks(const MLPArgs& a) {
-  if (f32_variant(a) == 2) return 1;
+// The K split layout 1 uses: the wanted one if its launch is co-resident, else 1.
+int f32_ks_v1(const MLPArgs& a) {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -1366,6 +1408,7 @@ int f32_ks(const MLPArgs& a) {
   if (want == 2 && ppl_of(2) * roles_of(2) > resident_capacity_ks(a, cus, 2)) return 1;
   return want;
 }
+int f32_ks(const MLPArgs& a) { return f32_variant(a) == 2 ? 1 : f32_ks_v1(a); }
 
 }  // namespace
 

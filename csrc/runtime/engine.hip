@@ -145,7 +145,15 @@ struct MLPEngine {
   // Opt-in (MYFYP_PREP_GATHER=1): measured round-rate neutral on the fp32 headline (488.2 / 500.7
   // vs 498.0 / 501.7 rounds/s in-graph, profiles/r3_host_timeline) — the 28 us gather overlapped with
   // the epoch costs the epoch about as much as it saves. Bit-identical to the in-graph gather (test).
+  // MYFYP_PREP_GATHER=2 (ahead): the gather of epoch r waits for the START of epoch r-1 (an event
+  // recorded on the main stream right before its graph launch; epoch r-2, the last reader of the
+  // buffer, is then done) and runs on a capped grid (MYFYP_PREP_GATHER_WGS, default 64) beside it,
+  // instead of at the round boundary (its earliest start in mode 1), where it slowed the FedAvg.
   bool prep_mode = false;
+  int prep_level = 0;
+  int prep_wgs = 64;
+  hipEvent_t ev_start = nullptr;
+  bool start_rec = false;
   bf16* xb16_buf[2] = {nullptr, nullptr};
   int* yb_buf[2] = {nullptr, nullptr};
   hipStream_t prep_stream = nullptr;
@@ -338,8 +346,15 @@ struct MLPEngine {
   }
   // Prep mode: the gather into batch buffer i on the prep stream, after the last epoch that read it;
   // it gets its own copy of the control words and the shuffle key (nothing on the main stream).
-  int prep_gather(int i) {
-    if (done_rec[i]) CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_done[i], 0));
+  int prep_gather(int i, hipStream_t main) {
+    if (prep_level == 2 && start_rec) {
+      CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_start, 0));
+    } else if (done_rec[i]) {
+      CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_done[i], 0));
+    } else {  // first gather after a (re)capture: behind everything already on the main stream
+      CHECK_HIP(hipEventRecord(ev_start, main));
+      CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_start, 0));
+    }
     CtlUpload u{};
     u.P = a.P;
     u.seed = seed_host;
@@ -351,7 +366,7 @@ struct MLPEngine {
     ga.Xb16 = xb16_buf[i];
     ga.Yb = yb_buf[i];
     ga.flags_zero = nullptr;
-    mlp_launch_gather_epoch(ga, prep_stream);
+    mlp_launch_gather_epoch(ga, prep_stream, prep_level == 2 ? prep_wgs : 0);
     CHECK_HIP(hipGetLastError());
     CHECK_HIP(hipEventRecord(ev_gath[i], prep_stream));
     return 0;
@@ -458,6 +473,7 @@ struct MLPEngine {
   int ensure_prep() {
     if (!prep_stream) {
       CHECK_HIP(hipStreamCreateWithFlags(&prep_stream, hipStreamNonBlocking));
+      CHECK_HIP(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
       for (int i = 0; i < 2; ++i) {
         CHECK_HIP(hipEventCreateWithFlags(&ev_gath[i], hipEventDisableTiming));
         CHECK_HIP(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
@@ -479,11 +495,14 @@ struct MLPEngine {
     graph_persistent = use_persistent();
     {
       const char* env = getenv("MYFYP_PREP_GATHER");
-      prep_mode = graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && env != nullptr && atoi(env) == 1;
+      prep_level = env != nullptr ? atoi(env) : 0;
+      prep_mode = graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && (prep_level == 1 || prep_level == 2);
+      if (const char* w = getenv("MYFYP_PREP_GATHER_WGS")) prep_wgs = atoi(w);
       if (prep_mode && ensure_prep()) return 1;
       if (prep_mode) {
         // the batch buffers were (re)allocated or the graph changed: nothing in flight reads them
         done_rec[0] = done_rec[1] = false;
+        start_rec = false;
         xb16_buf[0] = a.Xb16;
         yb_buf[0] = a.Yb;
       }
@@ -981,13 +1000,17 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
   const int buf = e->n_execs > 1 ? (int)(e->launches & 1) : 0;  // the executable launch_graph takes
   if (e->prep_mode) {
-    if (e->prep_gather(buf)) return 1;
+    if (e->prep_gather(buf, s)) return 1;
     CHECK_HIP(hipStreamWaitEvent(s, e->ev_gath[buf], 0));
   }
   if (e->graph_persistent) {
     GangOrder& go = gang_order();
     std::lock_guard<std::mutex> og(go.mu);
     if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
+    if (e->prep_mode && e->prep_level == 2) {
+      CHECK_HIP(hipEventRecord(e->ev_start, s));
+      e->start_rec = true;
+    }
     if (e->launch_graph(s)) return 1;
     if (e->prep_mode) {
       CHECK_HIP(hipEventRecord(e->ev_done[buf], s));

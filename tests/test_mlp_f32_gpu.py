@@ -330,17 +330,20 @@ def test_f32_prewarm_is_transparent(dev):
         assert torch.equal(a, b)
 
 
-def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch):
-    """The epoch batch gather on its own stream into alternating batch buffers (overlapping the
-    previous epoch) gives bit-identical training to the gather as the first node of the epoch
-    graph: three epochs (both buffers used, one reused) with the in-kernel shuffle of fixed keys."""
+@pytest.mark.parametrize("prep_mode", ["1", "2"])
+def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch, prep_mode):
+    """The epoch batch gather on its own stream into alternating batch buffers (mode 1: after the
+    last epoch that read the buffer; mode 2: beside the previous epoch, on a capped grid-strided
+    grid) gives bit-identical training to the gather as the first node of the epoch graph: three
+    epochs (both buffers used, one reused) with the in-kernel shuffle of fixed keys."""
     import random
 
     from myfyp_amd.parallel.mlp_engine import MLPGroup
 
     spec = {"name": "adam", "lr": 1e-3}
     results = []
-    for prep in ("1", "0"):
+    monkeypatch.setenv("MYFYP_PREP_GATHER_WGS", "6")  # fewer workgroups than row blocks: the stride loop runs
+    for prep in (prep_mode, "0"):
         monkeypatch.setenv("MYFYP_PREP_GATHER", prep)
         MLPGroup.reset_all()
         learners, refs, g, n = _setup(dev, 3, 64, 1500, 7, spec)
