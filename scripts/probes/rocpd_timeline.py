@@ -1,7 +1,10 @@
 """Per-period device timeline of a rocprofv3 run (rocpd SQLite, ROCm 7): busy time, idle gaps and
 the kernels of one steady-state period, where a period starts at each dispatch of a marker kernel.
 
-    python scripts/probes/rocpd_timeline.py <run_results.db> <marker substring> [period index]
+    python scripts/probes/rocpd_timeline.py <run_results.db> <marker substring> [period index] [seq]
+
+With a fourth argument ``seq`` it also lists the period's dispatches in start order: start and end
+offsets from the period start (us), stream id and kernel.
 """
 
 import sqlite3
@@ -40,6 +43,9 @@ def main() -> None:
     print(f"period {k}: {span:.1f} us, device busy (any stream) {busy:.1f} us, idle {gaps:.1f} us, {b - a} dispatches")
     for name, (n, us) in sorted(per.items(), key=lambda kv: -kv[1][1])[:30]:
         print(f"  {us:9.1f} us  {n:4d}x  {name[:110]}")
+    if len(sys.argv) > 4 and sys.argv[4] == "seq":
+        for r in rows[a : b + 1]:
+            print(f"  {(r[0] - t0) / 1e3:9.1f} {(r[1] - t0) / 1e3:9.1f}  s{r[2]}  {r[3].split('(')[0][:90]}")
 
 
 if __name__ == "__main__":

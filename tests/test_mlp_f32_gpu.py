@@ -215,6 +215,28 @@ def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
             assert rel < 1e-3, f"{kind} peer {i} {name}: relative update error {rel:.2e}"
 
 
+@pytest.mark.parametrize("kind", ["fedprox", "scaffold"])
+def test_f32_adam_extra_defaults_to_spill_free_layout(dev, kind):
+    """Adam + FedProx/SCAFFOLD at owner K split 1 runs layout 2 unless a layout is forced: layout 1's
+    instantiation spills VGPRs there, layout 2's does not (kernel-resource-usage remarks). Layout 2's
+    numerics with these terms are pinned by test_f32_fedprox_scaffold_terms_match_torch."""
+    spec = {"name": "adam", "lr": 1e-3}
+    learners, refs, g, n = _setup(dev, 2, 64, 900, 6, spec, scale=0.5)
+    g.force_f32_ks = 1
+    g.force_f32_variant = 0
+    assert g.f32_variant() == 1  # no extra term yet
+    flat = [l.flat_params().detach().clone() for l in learners]
+    if kind == "fedprox":
+        extras = [{"anchor": f.contiguous(), "mu": 0.01} for f in flat]
+    else:
+        extras = [{"c_global": torch.zeros_like(f), "c_local": torch.zeros_like(f)} for f in flat]
+    _fit_all(learners, extras)
+    assert g.f32_variant() == 2 and g.f32_ks() == 1
+    for l, f in zip(learners, flat):
+        d = l.flat_params().detach() - f
+        assert torch.isfinite(d).all() and d.abs().max() > 0
+
+
 def test_f32_w2_replica_is_bit_identical(dev):
     """Layout 1: the owners' W2 replica (updated from their own dW2 tile) equals the heads' W2 rows
     bit for bit."""
