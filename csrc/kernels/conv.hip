@@ -153,6 +153,12 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
   const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
   const bool fstats = !bnb && a.stats != nullptr;
+  // the per-column constants are re-read for every tile (pointers laundered through an empty asm):
+  // hoisted out of a persistent kernel's tile loop they would hold 56 VGPRs across the MFMAs
+  auto fresh = [](const float* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+  };
   float bv[8], mean0[8], inv0[8], mean1[8], inv1[8], msc[8], msh[8];
   float(&q0)[8] = q.q0;
   float(&q1)[8] = q.q1;
@@ -162,19 +168,19 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   for (int j = 0; j < 8; ++j) {
     const int col = col0 + j;
     cval[j] = col < a.ncol_valid;
-    bv[j] = (a.bias != nullptr && cval[j]) ? a.bias[peer * a.bias_ps + col] : 0.f;
+    bv[j] = (a.bias != nullptr && cval[j]) ? fresh(a.bias + peer * a.bias_ps)[col] : 0.f;
     mean0[j] = inv0[j] = mean1[j] = inv1[j] = msc[j] = msh[j] = 0.f;
     if (ymask && chok) {
-      const float* ssp = a.bnb_mask_ss + peer * a.bnb_mask_ss_ps;
+      const float* ssp = fresh(a.bnb_mask_ss + peer * a.bnb_mask_ss_ps);
       msc[j] = ssp[col];
       msh[j] = ssp[a.ncol + col];
     }
     if (bnb && chok) {
-      const float* m0p = a.bnb_ms0 + peer * 2 * a.ncol;
+      const float* m0p = fresh(a.bnb_ms0 + peer * 2 * a.ncol);
       mean0[j] = m0p[col];
       inv0[j] = m0p[a.ncol + col];
       if (bnb2) {
-        const float* m1p = a.bnb_ms1 + peer * 2 * a.ncol;
+        const float* m1p = fresh(a.bnb_ms1 + peer * 2 * a.ncol);
         mean1[j] = m1p[col];
         inv1[j] = m1p[a.ncol + col];
       }
@@ -892,6 +898,19 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
 //   (conv_epilogue_tile / conv_epilogue_sums) with column sums carried across the workgroup's tiles.
 //   The forward prefetches the next tile's patch into registers while the current one is multiplied.
 // ------------------------------------------------------------------------------------------------
+// MODE 4 (and MODE 0 without the BN prologue when HALO_DMA0 is set) stage the patch by LDS DMA
+// (buffer_load ... lds) into two patch buffers: the next tile's patch lands under this tile's MFMAs
+// and epilogue without a register round trip. MODE 4's BN-backward epilogue left no registers for
+// the register prefetch, so it used to load each patch after the previous epilogue, exposed
+// (237 us per layer-1 dgrad vs 110 us for the same-shape forward, profiles/r4i_resnet_window).
+// Two 344-row patch buffers + the weights fill 158 KB of the 160 KB; the epilogue stages in two
+// 128-row slabs over the patch just read.
+#ifndef HALO_DMA0
+#define HALO_DMA0 0
+#endif
+#ifndef HALO_DMA4
+#define HALO_DMA4 1
+#endif
 template <int MODE, bool PRO>
 __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int tiles_m) {
   static_assert(MODE == 0 || MODE == 4, "forward-shaped convs");
@@ -902,7 +921,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
   constexpr int WE = 9 * C * BN;                                  // weight elements (bf16)
   constexpr int PE = PROWS * C;
   constexpr int EPI = BM * BN * 2;                                // fp32 staging, in bf16 units
-  __shared__ __attribute__((aligned(16))) bf16 lds[WE + (PE > EPI ? PE : EPI)];
+  constexpr bool DMA = (MODE == 4 && HALO_DMA4) || (MODE == 0 && HALO_DMA0 && !PRO);
+  constexpr int PROWS8 = (PROWS + 7) / 8 * 8;  // DMA writes whole 8-row blocks (the tail gets zeros)
+  constexpr int PEP = PROWS8 * C;
+  static_assert(!DMA || (PEP >= BM / 2 * BN * 2 && PEP >= 8 * 3 * BN * 2), "a patch buffer holds a staging slab / the sums");
+  static_assert(!DMA || (WE + 2 * PEP) * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16 lds[DMA ? WE + 2 * PEP : WE + (PE > EPI ? PE : EPI)];
   bf16* wl = lds;       // [tap][64 n][64 k] (swz rows)
   bf16* pat = lds + WE;  // [patch row][64 ci] (swz rows); the epilogue stages over it
   const int peer = blockIdx.z;
@@ -971,11 +995,75 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
     const int p = wr * 64 + i * 16 + (lane & 15);
     prow0[i] = (p / W) * PW + (p % W);
   }
-  // MODE 0 prefetches the next tile's patch into registers under the MFMAs; MODE 4's heavier
-  // (BN-backward) epilogue leaves no room for them (27 VGPRs spilled), so it loads after the epilogue
-  constexpr bool PREF = MODE == 0;
   EpiSums q;
   q.zero();
+  if constexpr (DMA) {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    // physical 8-row block blk of the patch: lane L writes row 8 blk + L / 8, physical chunk L % 8,
+    // i.e. logical chunk (L % 8) ^ ((row >> 1) & 7) of swz's layout; rows past the patch, padding
+    // pixels and rows of a missing image read the zero page (CONV_OOB)
+    auto dma_patch = [&](int tm, bf16* dst) {
+      const int m0 = tm * BM;
+      const int img = m0 / HW, h0 = (m0 - img * HW) / W;
+#pragma unroll
+      for (int i = 0; i < (PROWS8 / 8 + 7) / 8; ++i) {
+        const int blk = wv + 8 * i;
+        if (blk * 8 >= PROWS) break;
+        const int R = blk * 8 + (lane >> 3);
+        const int chl = (lane & 7) ^ ((R >> 1) & 7);
+        const int pr = R / PW, pc = R - pr * PW;
+        const int h = h0 - 1 + pr, w = pc - 1;
+        const bool ok = R < PROWS && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)W && img < nb;
+        conv_dma16(rs_src, dst + blk * 8 * C, ok ? (((img * a.src_h + h) * W + w) * C + chl * 8) * 2 : CONV_OOB);
+      }
+    };
+    int cur = 0;
+    dma_patch(g0, pat);
+    for (int tm = g0; tm < tiles_mp; tm += G) {
+      bf16* pc = pat + cur * PEP;
+      wait_vmcnt<0>();
+      __syncthreads();  // every wave's patch DMA landed (and the weights, the first time); the other buffer is free
+      if (tm + G < tiles_mp) dma_patch(tm + G, pat + (cur ^ 1) * PEP);  // lands under this tile's MFMAs + epilogue
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
+      // the 72 A / 36 B LDS addresses of the nine taps are recomputed per tile (laundered rows):
+      // hoisted out of the tile loop they held ~100 VGPRs and spilled
+      int pr0[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pr0[i] = prow0[i];
+        asm volatile("" : "+v"(pr0[i]));
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * PW + (t % 3);
+        const bf16* wt_t = wl + t * C * BN;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = h * 4 + (lane >> 4);
+          bf16x8 af[4], bfr[2];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) af[i] = ld8(pc + swz(pr0[i] + toff, ch));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bfr[j] = ld8(wt_t + swz(wc * 32 + j * 16 + (lane & 15), ch));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(af[i], bfr[j], acc[i][j]);
+        }
+      }
+      __syncthreads();  // patch reads done: the epilogue stages over it, two 128-row slabs
+      conv_epilogue_tile<MODE, BM, BN, NT, 2>(a, acc, reinterpret_cast<float*>(pc), peer, tm * BM, 0, M, HW, W, 0, 0, q);
+      cur ^= 1;
+    }
+    conv_epilogue_sums<MODE, BN, NT>(a, pat, peer, 0, g0, q);
+    return;
+  }
+  // MODE 0 prefetches the next tile's patch into registers under the MFMAs
+  constexpr bool PREF = MODE == 0;
   if (PREF) load_patch(g0);
   for (int tm = g0; tm < tiles_mp; tm += G) {
     if (!PREF) load_patch(tm);
@@ -1543,8 +1631,9 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   const bool wide = a.ncol > 64;
   hipStream_t s = (hipStream_t)stream;
   // 64 -> 64 channel 3x3 convs on 32-wide images (ResNet-18 layer 1): im2col from one staged patch.
-  // Not for the two-BN dgrad epilogue: its extra registers spill here (252 vs 238 us on the DMA kernel)
-  if (((mode == 4 && a.bnb_y1 == nullptr) || mode == 0) && g_fwd_halo && a.src_c == 64 && a.ncol == 64 && a.R == 3 && a.S == 3 && a.stride == 1 &&
+  // The two-BN dgrad epilogue spilled in the register-staged version (252 vs 238 us on the DMA
+  // kernel); the DMA-staged one (HALO_DMA4) has 0 spills with it
+  if (((mode == 4 && (HALO_DMA4 || a.bnb_y1 == nullptr)) || mode == 0) && g_fwd_halo && a.src_c == 64 && a.ncol == 64 && a.R == 3 && a.S == 3 && a.stride == 1 &&
       a.pad == 1 && a.src_w == 32 && a.out_w == 32 && a.out_h == a.src_h && (a.src_h * 32) % 256 == 0) {
     const int tiles_m = (a.max_batch * a.out_h * 32 + 255) / 256;
     int G = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : (conv_num_cus() + peers - 1) / peers;  // one workgroup per CU
