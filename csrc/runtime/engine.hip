@@ -11,7 +11,9 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -53,9 +55,20 @@ struct CtlUpload {
   int* zero_conf;
   unsigned* zero_flags;  // the persistent epoch's hand-off flags (prep-stream gather mode)
   int n_flags;
+  // where the epoch graph's last node publishes the fit's results (null loss: nowhere — an earlier
+  // epoch of a multi-epoch fit, or stats published by a separate launch)
+  struct PubDst {
+    float* loss;
+    int* correct;
+    int* err;
+    unsigned* seq;
+    unsigned gen;
+  } pub;
 };
-__global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long long* seed) {
+using PubDst = CtlUpload::PubDst;
+__global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long long* seed, PubDst* pub) {
   const int p = threadIdx.x;
+  if (pub != nullptr && p == 0) *pub = u.pub;
   if (p < u.P) {
     ctl[p] = u.ctl[p];
     if (u.with_active) active[p] = u.active[p];
@@ -102,9 +115,12 @@ __global__ __launch_bounds__(256) void k_eval_snapshot(MLPArgs a, float* params_
   }
 }
 
-// Results -> pinned, host-mapped ring slot in ONE launch (instead of one copy per buffer).
-__global__ void k_publish(const float* loss, const int* correct, const int* err, const int* conf, int P, float* o_loss, int* o_correct,
-                          int* o_err, int* o_conf) {
+// Results -> pinned, host-mapped ring slot in ONE launch (instead of one copy per buffer). The slot's
+// sequence word is stored last, with system-scope release: the host polls it (mlp_engine_fetch)
+// instead of waiting on an event recorded behind this launch — an event record on the main stream
+// costs the GPU a 6-14 us idle gap before the next kernel (profiles/r4i_*/timeline_prep0.txt).
+__device__ __forceinline__ void publish_body(const float* loss, const int* correct, const int* err, const int* conf, int P, float* o_loss,
+                                             int* o_correct, int* o_err, int* o_conf, unsigned* o_seq, unsigned seq) {
   const int t = threadIdx.x;
   if (t < P) {
     o_loss[t] = loss[t];
@@ -122,6 +138,23 @@ __global__ void k_publish(const float* loss, const int* correct, const int* err,
   if (t == 0) *o_err = st;
   if (conf && o_conf)
     for (int q = t; q < P * 256; q += blockDim.x) o_conf[q] = conf[q];
+  if (o_seq) {
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(o_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+__global__ void k_publish(const float* loss, const int* correct, const int* err, const int* conf, int P, float* o_loss, int* o_correct,
+                          int* o_err, int* o_conf, unsigned* o_seq, unsigned seq) {
+  publish_body(loss, correct, err, conf, P, o_loss, o_correct, o_err, o_conf, o_seq, seq);
+}
+// The epoch graph's last node: the fit's results to the ring slot the epoch's control upload named
+// (the graph is fixed, the slot is not); a separate publish launch after the graph left the main
+// stream idle ~10 us behind the graph (profiles/r4j_*/timeline.txt).
+__global__ void k_publish_dev(const float* loss, const int* correct, const int* err, int P, const PubDst* pd) {
+  const PubDst d = *pd;
+  if (d.loss == nullptr) return;
+  publish_body(loss, correct, err, nullptr, P, d.loss, d.correct, d.err, nullptr, d.seq, d.gen);
 }
 
 #define MLP_RING 16
@@ -130,8 +163,26 @@ struct ResultSlot {
   int* correct = nullptr;
   int* conf = nullptr;
   int* err = nullptr;
-  hipEvent_t ev = nullptr;
+  unsigned* seq = nullptr;  // k_publish stores `gen` here last
+  std::atomic<unsigned> gen{0};
+  hipStream_t stream = nullptr;  // where the publish was enqueued (fault check while polling)
+  hipEvent_t ev = nullptr;       // MYFYP_RING_EVENTS=1: completion event instead of the sequence word
 };
+// MYFYP_GRAPH_PUBLISH=0: the fit's results by a separate launch after the epoch graph
+static bool graph_publish() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_GRAPH_PUBLISH");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+static bool ring_events() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_RING_EVENTS");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return v != 0;
+}
 
 struct MLPEngine {
   MLPArgs a{};
@@ -145,7 +196,8 @@ struct MLPEngine {
   // Opt-in (MYFYP_PREP_GATHER=1): measured round-rate neutral on the fp32 headline (488.2 / 500.7
   // vs 498.0 / 501.7 rounds/s in-graph, profiles/r3_host_timeline) — the 28 us gather overlapped with
   // the epoch costs the epoch about as much as it saves. Bit-identical to the in-graph gather (test).
-  // MYFYP_PREP_GATHER=2 (ahead): the gather of epoch r waits for the START of epoch r-1 (an event
+  // MYFYP_PREP_GATHER=2 (ahead, the default; 0 = the gather as the first node of the epoch graph):
+  // the gather of epoch r waits for the START of epoch r-1 (an event
   // recorded on the main stream right before its graph launch; epoch r-2, the last reader of the
   // buffer, is then done) and runs on a capped grid (MYFYP_PREP_GATHER_WGS, default 64) beside it,
   // instead of at the round boundary (its earliest start in mode 1), where it slowed the FedAvg.
@@ -180,6 +232,9 @@ struct MLPEngine {
   int4* d_ctl = nullptr;
   unsigned long long* d_seed = nullptr;
   unsigned long long seed_host = 0;
+  PubDst* d_pub = nullptr;      // the graph's publish destination (written by the control upload)
+  int graph_pub_slot = -1;      // ring slot the last epoch graph published into (stats_async skips it)
+  bool graph_has_pub = false;   // the captured graph ends with k_publish_dev
   std::vector<int4> ctl_host;
   float* d_loss = nullptr;
   int* d_correct = nullptr;
@@ -206,17 +261,26 @@ struct MLPEngine {
   std::vector<int> active_host_cache;
   // evaluation overlapped with the epoch (persistent path): it reads a snapshot of the parameters
   // taken on the main stream and runs on its own stream on the CUs the epoch's gangs leave free
+  // Two evaluation sides, used alternately: the snapshot for evaluation r overwrites the side that
+  // evaluation r-2 read, and the host (not the main stream) waits for that one — a stream wait on
+  // the previous evaluation cost the main stream a 6-7 us idle gap every round
+  // (profiles/r4j_*/timeline.txt); evaluation r-2 ends about a round before the host gets here.
   hipStream_t eval_stream = nullptr;
-  hipEvent_t ev_snap = nullptr, ev_eval_done = nullptr;
-  bool eval_pending = false;
-  float* params_snap = nullptr;
-  bf16* shadow_snap = nullptr;
-  bf16* w2t_snap = nullptr;
+  hipEvent_t ev_snap = nullptr;
+  struct EvalSide {
+    float* params = nullptr;
+    bf16* shadow = nullptr;
+    bf16* w2t = nullptr;
+    int4* ctl = nullptr;
+    int* active = nullptr;
+    float* loss = nullptr;
+    int* correct = nullptr;
+    int* conf = nullptr;
+    hipEvent_t done = nullptr;
+    bool rec = false;
+  } eside[2];
+  int eval_idx = 0;
   int64_t snap_S = 0;
-  int4* d_ctl_eval = nullptr;
-  int* d_active_eval = nullptr;
-  float* d_loss_eval = nullptr;
-  int* d_correct_eval = nullptr;
 
   bool use_persistent() const {
     if (precision == 1) return fp32_ready();
@@ -280,10 +344,12 @@ struct MLPEngine {
       hipStreamDestroy(eval_stream);
     }
     if (ev_snap) hipEventDestroy(ev_snap);
-    if (ev_eval_done) hipEventDestroy(ev_eval_done);
-    if (params_snap) hipFree(params_snap);
-    if (shadow_snap) hipFree(shadow_snap);
-    if (w2t_snap) hipFree(w2t_snap);
+    for (auto& es : eside) {
+      if (es.done) hipEventDestroy(es.done);
+      if (es.params) hipFree(es.params);
+      if (es.shadow) hipFree(es.shadow);
+      if (es.w2t) hipFree(es.w2t);
+    }
     for (auto& x : execs)
       if (x) hipGraphExecDestroy(x);
     if (graph) hipGraphDestroy(graph);
@@ -299,6 +365,7 @@ struct MLPEngine {
       if (r.correct) hipHostFree(r.correct);
       if (r.conf) hipHostFree(r.conf);
       if (r.err) hipHostFree(r.err);
+      if (r.seq) hipHostFree(r.seq);
     }
   }
 
@@ -310,6 +377,9 @@ struct MLPEngine {
       CHECK_HIP(hipHostMalloc((void**)&r.conf, sizeof(int) * a.P * 256, fl));
       CHECK_HIP(hipHostMalloc((void**)&r.err, sizeof(int), fl));
       *r.err = 0;
+      CHECK_HIP(hipHostMalloc((void**)&r.seq, sizeof(unsigned), fl));
+      *r.seq = 0;
+      r.gen = 0;
       CHECK_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     }
     return 0;
@@ -324,8 +394,9 @@ struct MLPEngine {
       *n = (int)(pb.flag_bytes / sizeof(unsigned));
     }
   }
-  int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false, bool zero_flags = false) {
+  int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false, bool zero_flags = false, const PubDst* pub = nullptr) {
     CtlUpload u{};
+    if (pub) u.pub = *pub;  // else null: the graph's publish node does nothing
     if (zero_flags) flag_words(&u.zero_flags, &u.n_flags);
     u.P = a.P;
     u.with_active = active_host != nullptr;
@@ -340,7 +411,7 @@ struct MLPEngine {
       u.zero_correct = d_correct;
       u.zero_err = pb.err;
     }
-    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, s, u, d_ctl, d_active, d_seed);
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, s, u, d_ctl, d_active, d_seed, d_pub);
     CHECK_HIP(hipGetLastError());
     return 0;
   }
@@ -359,7 +430,7 @@ struct MLPEngine {
     u.P = a.P;
     u.seed = seed_host;
     for (int p = 0; p < a.P; ++p) u.ctl[p] = ctl_host[p];
-    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, prep_stream, u, d_ctl_prep, d_active_prep, d_seed_prep);
+    hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, prep_stream, u, d_ctl_prep, d_active_prep, d_seed_prep, (PubDst*)nullptr);
     MLPArgs ga = a;
     ga.ctl = d_ctl_prep;
     ga.seed = d_seed_prep;
@@ -372,9 +443,15 @@ struct MLPEngine {
     return 0;
   }
 
+  // publish into ring slot r; completion: the slot's sequence word (or its event, MYFYP_RING_EVENTS=1)
   int publish(hipStream_t s, ResultSlot& r, const float* loss, const int* correct, const int* err, const int* conf) {
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, loss, correct, err, conf, a.P, r.loss, r.correct, r.err, conf ? r.conf : nullptr);
+    const unsigned g = r.gen.load() + 1;
+    r.stream = s;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, loss, correct, err, conf, a.P, r.loss, r.correct, r.err, conf ? r.conf : nullptr,
+                       ring_events() ? nullptr : r.seq, g);
     CHECK_HIP(hipGetLastError());
+    if (ring_events()) CHECK_HIP(hipEventRecord(r.ev, s));
+    r.gen.store(g);
     return 0;
   }
 
@@ -383,26 +460,39 @@ struct MLPEngine {
     if (!eval_stream) {
       CHECK_HIP(hipStreamCreateWithFlags(&eval_stream, hipStreamNonBlocking));
       CHECK_HIP(hipEventCreateWithFlags(&ev_snap, hipEventDisableTiming));
-      CHECK_HIP(hipEventCreateWithFlags(&ev_eval_done, hipEventDisableTiming));
-      void* p;
-      if (alloc(&p, (size_t)a.P * 16)) return 1;
-      d_ctl_eval = (int4*)p;
-      if (alloc(&p, (size_t)a.P * 4)) return 1;
-      d_active_eval = (int*)p;
-      if (alloc(&p, (size_t)a.P * 4)) return 1;
-      d_loss_eval = (float*)p;
-      if (alloc(&p, (size_t)a.P * 4)) return 1;
-      d_correct_eval = (int*)p;
+      for (auto& es : eside) {
+        CHECK_HIP(hipEventCreateWithFlags(&es.done, hipEventDisableTiming));
+        void* p;
+        if (alloc(&p, (size_t)a.P * 16)) return 1;
+        es.ctl = (int4*)p;
+        if (alloc(&p, (size_t)a.P * 4)) return 1;
+        es.active = (int*)p;
+        if (alloc(&p, (size_t)a.P * 4)) return 1;
+        es.loss = (float*)p;
+        if (alloc(&p, (size_t)a.P * 4)) return 1;
+        es.correct = (int*)p;
+        if (alloc(&p, (size_t)a.P * 256 * 4)) return 1;
+        es.conf = (int*)p;
+      }
     }
     if (snap_S != a.S) {
-      if (params_snap) hipFree(params_snap);
-      if (shadow_snap) hipFree(shadow_snap);
-      if (w2t_snap) hipFree(w2t_snap);
-      CHECK_HIP(hipMalloc((void**)&params_snap, (size_t)a.P * a.S * sizeof(float)));
-      CHECK_HIP(hipMalloc((void**)&shadow_snap, (size_t)a.P * a.S * sizeof(bf16)));
-      CHECK_HIP(hipMalloc((void**)&w2t_snap, (size_t)a.P * a.D1 * a.D2 * sizeof(bf16)));
+      for (auto& es : eside) {
+        if (es.params) hipFree(es.params);
+        if (es.shadow) hipFree(es.shadow);
+        if (es.w2t) hipFree(es.w2t);
+        CHECK_HIP(hipMalloc((void**)&es.params, (size_t)a.P * a.S * sizeof(float)));
+        CHECK_HIP(hipMalloc((void**)&es.shadow, (size_t)a.P * a.S * sizeof(bf16)));
+        CHECK_HIP(hipMalloc((void**)&es.w2t, (size_t)a.P * a.D1 * a.D2 * sizeof(bf16)));
+      }
       snap_S = a.S;
     }
+    return 0;
+  }
+  // the main stream must not run ahead of an overlapped evaluation that reads what it is about to
+  // change (a non-persistent evaluation on the main stream, a re-snapshot of the same side)
+  int wait_evals(hipStream_t s) {
+    for (auto& es : eside)
+      if (es.rec) CHECK_HIP(hipStreamWaitEvent(s, es.done, 0));
     return 0;
   }
 
@@ -458,6 +548,8 @@ struct MLPEngine {
     } else {
       for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
     }
+    graph_has_pub = graph_publish() && !ring_events() && d_pub != nullptr;
+    if (graph_has_pub) hipLaunchKernelGGL(k_publish_dev, dim3(1), dim3(256), 0, cap_stream, d_loss, d_correct, pb.err, a.P, (const PubDst*)d_pub);
     a = saved;
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(cap_stream, &g);
@@ -495,7 +587,7 @@ struct MLPEngine {
     graph_persistent = use_persistent();
     {
       const char* env = getenv("MYFYP_PREP_GATHER");
-      prep_level = env != nullptr ? atoi(env) : 0;
+      prep_level = env != nullptr ? atoi(env) : 2;  // default: ahead (+0.5-1 %, profiles/r4h_*, r4j_*)
       prep_mode = graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && (prep_level == 1 || prep_level == 2);
       if (const char* w = getenv("MYFYP_PREP_GATHER_WGS")) prep_wgs = atoi(w);
       if (prep_mode && ensure_prep()) return 1;
@@ -521,11 +613,25 @@ struct MLPEngine {
 // Persistent epochs of all engines in this process run in launch order (stream-ordered through
 // one event; the host never waits): two gangs' launches never compete for the same CUs. One
 // process per GPU is the deployment; ranks sharing a GPU are rehearsals.
+// The event is recorded lazily, only when an epoch is launched on a stream other than the last one
+// (recorded then on that stream: a superset of its last epoch, so still a safe order); an engine
+// that stays on one stream never records it — an event record behind every epoch cost a 14 us idle
+// gap before the next kernel (profiles/r4i_*/timeline_prep0.txt). MYFYP_GANG_EVENT=1: the old
+// record-after-every-epoch.
 struct GangOrder {
   std::mutex mu;
   hipEvent_t ev = nullptr;
   bool ev_ready = false;
+  bool has_last = false;
+  hipStream_t last = nullptr;
 };
+static bool gang_event_always() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_GANG_EVENT");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return v != 0;
+}
 GangOrder& gang_order() {
   static GangOrder g;
   return g;
@@ -748,6 +854,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
   rc |= e->alloc(&p, (size_t)P * 4); e->d_t0 = (int*)p; a.t0 = e->d_t0;
   rc |= e->alloc(&p, (size_t)P * 16); e->d_ctl = (int4*)p; a.ctl = e->d_ctl;
   rc |= e->alloc(&p, 16); e->d_seed = (unsigned long long*)p; a.seed = e->d_seed;
+  rc |= e->alloc(&p, sizeof(PubDst)); e->d_pub = (PubDst*)p;
   e->ctl_host.assign(P, int4{0, 0, 0, 0});
   rc |= e->alloc(&p, (size_t)P * 4); e->d_loss = (float*)p; a.loss_acc = e->d_loss;
   rc |= e->alloc(&p, (size_t)P * 4); e->d_correct = (int*)p; a.correct_acc = e->d_correct;
@@ -981,11 +1088,17 @@ int mlp_engine_set_w2chk(void* h, float* buf) {
 // 1 if the next epoch runs as the persistent kernel.
 int mlp_engine_uses_persistent(void* h) { return ((MLPEngine*)h)->use_persistent() ? 1 : 0; }
 
-// One local epoch for every active peer: a single graph replay (captured on first use).
-int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
-  auto* e = (MLPEngine*)h;
+// One local epoch for every active peer: a single graph replay (captured on first use). slot >= 0:
+// the graph's last node publishes the fit's results into that ring slot (mlp_engine_stats_async
+// for the slot is then a no-op); -1: nothing (earlier epochs of a multi-epoch fit, or the caller
+// publishes with mlp_engine_stats_async).
+static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_t s);
+int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) { return run_epoch_impl((MLPEngine*)h, t0_host, -1, (hipStream_t)stream); }
+int mlp_engine_run_epoch_pub(void* h, const int* t0_host, int slot, void* stream) {
+  return run_epoch_impl((MLPEngine*)h, t0_host, slot, (hipStream_t)stream);
+}
+static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_t s) {
   std::lock_guard<std::mutex> g(e->mu);
-  hipStream_t s = (hipStream_t)stream;
   if (e->max_steps <= 0) return 0;
   if (e->precision == 1 && !e->use_persistent()) {
     g_last_error = "fp32 MLP engine: shape / batch / CU count not supported by the fp32 persistent epoch (no silent bf16 fallback)";
@@ -996,7 +1109,13 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   }
   for (int p = 0; p < e->a.P; ++p) e->ctl_host[p].z = t0_host[p];
   const bool pa = e->graph_persistent && e->pending_zero_acc;
-  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh, e->prep_mode)) return 1;
+  PubDst pd{};
+  ResultSlot* pr = nullptr;
+  if (slot >= 0 && e->graph_has_pub) {
+    pr = &e->ring[slot % MLP_RING];
+    pd = PubDst{pr->loss, pr->correct, pr->err, pr->seq, pr->gen.load() + 1};
+  }
+  if (e->upload(s, pa ? e->active_host_cache.data() : nullptr, pa, e->graph_persistent && e->pending_fresh, e->prep_mode, &pd)) return 1;
   if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
   const int buf = e->n_execs > 1 ? (int)(e->launches & 1) : 0;  // the executable launch_graph takes
   if (e->prep_mode) {
@@ -1006,21 +1125,35 @@ int mlp_engine_run_epoch(void* h, const int* t0_host, void* stream) {
   if (e->graph_persistent) {
     GangOrder& go = gang_order();
     std::lock_guard<std::mutex> og(go.mu);
-    if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
+    if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
+    if (gang_event_always()) {
+      if (go.ev_ready) CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
+    } else if (go.has_last && go.last != s) {
+      CHECK_HIP(hipEventRecord(go.ev, go.last));
+      CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
+    }
     if (e->prep_mode && e->prep_level == 2) {
       CHECK_HIP(hipEventRecord(e->ev_start, s));
       e->start_rec = true;
     }
     if (e->launch_graph(s)) return 1;
-    if (e->prep_mode) {
+    if (e->prep_mode && e->prep_level == 1) {  // (mode 2 orders its gathers by ev_start)
       CHECK_HIP(hipEventRecord(e->ev_done[buf], s));
       e->done_rec[buf] = true;
     }
-    if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
-    CHECK_HIP(hipEventRecord(go.ev, s));
-    go.ev_ready = true;
+    if (gang_event_always()) {
+      CHECK_HIP(hipEventRecord(go.ev, s));
+      go.ev_ready = true;
+    }
+    go.has_last = true;
+    go.last = s;
   } else {
     if (e->launch_graph(s)) return 1;
+  }
+  if (pr != nullptr) {
+    pr->stream = s;
+    pr->gen.store(pd.gen);
+    e->graph_pub_slot = slot;
   }
   return 0;
 }
@@ -1045,7 +1178,7 @@ int mlp_engine_prepare(void* h, void* stream) {
   // code-object load: a publish of zero peers (its only store zeroes d_correct[0], which every fit
   // re-zeroes before accumulating; no ring slot is touched)
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, e->d_loss, e->d_correct, (const int*)nullptr, (const int*)nullptr, 0, e->d_loss,
-                     e->d_correct, e->d_correct, (int*)nullptr);
+                     e->d_correct, e->d_correct, (int*)nullptr, (unsigned*)nullptr, 0u);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -1092,12 +1225,16 @@ int mlp_engine_stats_async(void* h, int slot, void* stream) {
   auto* e = (MLPEngine*)h;
   hipStream_t s = (hipStream_t)stream;
   ResultSlot& r = e->ring[slot % MLP_RING];
+  if (e->graph_pub_slot == slot) {  // the epoch graph already published into this slot
+    e->graph_pub_slot = -1;
+    return 0;
+  }
+  e->graph_pub_slot = -1;
   if (e->pending_zero_acc) {  // a fit with no epoch launched: zero what it would have zeroed
     if (e->upload(s, e->active_host_cache.data(), true, false)) return 1;
     e->pending_zero_acc = false;
   }
   if (e->publish(s, r, e->d_loss, e->d_correct, e->pb.err, nullptr)) return 1;
-  CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
 
@@ -1110,11 +1247,22 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   if (e->use_persistent()) {
     // Overlapped evaluation: snapshot the parameters on the main stream (one launch: control words,
     // accumulators, fp32 + bf16 + W2T copies), then evaluate the snapshot on the side stream while
-    // the main stream goes on to the epoch, whose gangs leave ~half of the CUs free. The previous
-    // evaluation must be done with the snapshot buffers before they are overwritten.
+    // the main stream goes on to the epoch, whose gangs leave ~half of the CUs free. The evaluation
+    // that last used this side (two evaluations back) must be done with it before it is overwritten.
     std::lock_guard<std::mutex> g(e->mu);
     if (e->ensure_eval_side()) return 1;
-    if (e->eval_pending) CHECK_HIP(hipStreamWaitEvent(s, e->ev_eval_done, 0));
+    auto& es = e->eside[e->eval_idx];
+    e->eval_idx ^= 1;
+    // evaluation r-2 (a host wait, not a stream wait), polled: a blocking hipEventSynchronize
+    // sleeps until an interrupt and stalled the round driver up to 11 ms (profiles/r4l_*)
+    if (es.rec) {
+      for (long it = 0;; ++it) {
+        const hipError_t q = hipEventQuery(es.done);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) CHECK_HIP(q);
+        if (it >= 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
     CtlUpload u{};
     u.P = e->a.P;
     u.with_active = 1;
@@ -1123,35 +1271,35 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
       u.ctl[p] = e->ctl_host[p];
       u.active[p] = active_host[p];
     }
-    u.zero_loss = e->d_loss_eval;
-    u.zero_correct = e->d_correct_eval;
-    u.zero_conf = e->d_conf;
+    u.zero_loss = es.loss;
+    u.zero_correct = es.correct;
+    u.zero_conf = es.conf;
     MLPArgs ea = e->a;
-    ea.params = e->params_snap;
-    ea.shadow = e->shadow_snap;
-    ea.w2t = e->w2t_snap;
-    ea.ctl = e->d_ctl_eval;
-    ea.active = e->d_active_eval;
-    ea.loss_acc = e->d_loss_eval;
-    ea.correct_acc = e->d_correct_eval;
+    ea.params = es.params;
+    ea.shadow = es.shadow;
+    ea.w2t = es.w2t;
+    ea.ctl = es.ctl;
+    ea.active = es.active;
+    ea.loss_acc = es.loss;
+    ea.correct_acc = es.correct;
+    ea.conf = es.conf;
     {
       const int64_t blocks = (e->a.numel + 255) / 256;
-      hipLaunchKernelGGL(k_eval_snapshot, dim3((unsigned)(blocks < 1024 ? blocks : 1024), e->a.P), dim3(256), 0, s, e->a, e->params_snap,
-                         e->shadow_snap, e->w2t_snap, u, e->d_ctl_eval, e->d_active_eval);
+      hipLaunchKernelGGL(k_eval_snapshot, dim3((unsigned)(blocks < 1024 ? blocks : 1024), e->a.P), dim3(256), 0, s, e->a, es.params,
+                         es.shadow, es.w2t, u, es.ctl, es.active);
       CHECK_HIP(hipGetLastError());
     }
     CHECK_HIP(hipEventRecord(e->ev_snap, s));
-    hipStream_t es = e->eval_stream;
-    CHECK_HIP(hipStreamWaitEvent(es, e->ev_snap, 0));
-    e->launch_eval(ea, es);
+    hipStream_t xs = e->eval_stream;
+    CHECK_HIP(hipStreamWaitEvent(xs, e->ev_snap, 0));
+    e->launch_eval(ea, xs);
     CHECK_HIP(hipGetLastError());
-    if (e->publish(es, r, e->d_loss_eval, e->d_correct_eval, nullptr, e->d_conf)) return 1;
-    CHECK_HIP(hipEventRecord(r.ev, es));
-    CHECK_HIP(hipEventRecord(e->ev_eval_done, es));
-    e->eval_pending = true;
+    if (e->publish(xs, r, es.loss, es.correct, nullptr, es.conf)) return 1;
+    CHECK_HIP(hipEventRecord(es.done, xs));
+    es.rec = true;
     return 0;
   }
-  if (e->eval_pending) CHECK_HIP(hipStreamWaitEvent(s, e->ev_eval_done, 0));
+  if (e->wait_evals(s)) return 1;
   if (e->upload(s, active_host)) return 1;
   CHECK_HIP(hipMemsetAsync(e->d_loss, 0, sizeof(float) * e->a.P, s));
   CHECK_HIP(hipMemsetAsync(e->d_correct, 0, sizeof(int) * e->a.P, s));
@@ -1160,7 +1308,6 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
   e->launch_eval(e->a, s);
   CHECK_HIP(hipGetLastError());
   if (e->publish(s, r, e->d_loss, e->d_correct, nullptr, e->d_conf)) return 1;
-  CHECK_HIP(hipEventRecord(r.ev, s));
   return 0;
 }
 
@@ -1168,7 +1315,29 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
 int mlp_engine_fetch(void* h, int slot, float* loss_host, int* correct_host, int* conf_host) {
   auto* e = (MLPEngine*)h;
   ResultSlot& r = e->ring[slot % MLP_RING];
-  CHECK_HIP(hipEventSynchronize(r.ev));
+  if (ring_events()) {
+    CHECK_HIP(hipEventSynchronize(r.ev));
+  } else {
+    // poll the slot's sequence word: spin briefly, then sleep in 20 us steps; every ~0.5 s ask the
+    // publishing stream for a fault (a faulted stream reports it; an idle one must have published)
+    const unsigned want = r.gen.load();
+    for (long it = 0;; ++it) {
+      if (__atomic_load_n(r.seq, __ATOMIC_ACQUIRE) == want) break;
+      if (it < 256) continue;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if ((it & 16383) == 0) {
+        const hipError_t q = hipStreamQuery(r.stream);
+        if (q != hipSuccess && q != hipErrorNotReady) {
+          g_last_error = std::string("result publish: ") + hipGetErrorString(q);
+          return 1;
+        }
+        if (q == hipSuccess && __atomic_load_n(r.seq, __ATOMIC_ACQUIRE) != want) {
+          g_last_error = "result publish: stream idle but the slot's sequence word was not written";
+          return 1;
+        }
+      }
+    }
+  }
   memcpy(loss_host, r.loss, sizeof(float) * e->a.P);
   memcpy(correct_host, r.correct, sizeof(int) * e->a.P);
   if (conf_host) memcpy(conf_host, r.conf, sizeof(int) * e->a.P * 256);

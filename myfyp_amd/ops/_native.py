@@ -64,6 +64,7 @@ _SIGNATURES = {
     "mlp_engine_set_extras": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_begin": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mlp_engine_run_epoch": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mlp_engine_run_epoch_pub": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "mlp_engine_run_epoch_eager": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mlp_engine_read_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlp_engine_eval": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -364,15 +364,19 @@ class MLPGroup:
             # epoch order: drawn on the device inside the gather kernel (keyed Feistel permutation
             # per peer, key from the seeded Python RNG) unless a test pins explicit permutations
             _native.check(fast.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
-            run = fast.mlp_engine_run_epoch_eager if self.eager else fast.mlp_engine_run_epoch
+            # the result slot is taken first: the last epoch's graph publishes into it itself (its
+            # last node), so stats_async is then a no-op — no separate launch behind the graph
+            k = self._take_slot()
             for ep in range(epochs):
                 if self.perm_fn is not None:
                     self.perm.copy_(self.perm_fn(ep))
                 else:
                     _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
                 t0 = (steps_pe * ep).astype(np.int32)
-                _native.check(run(self._engine, t0.ctypes.data, stream), "run_epoch")
-            k = self._take_slot()
+                if self.eager:
+                    _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
+                else:
+                    _native.check(fast.mlp_engine_run_epoch_pub(self._engine, t0.ctypes.data, k if ep == epochs - 1 else -1, stream), "run_epoch")
             _native.check(fast.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=False))
         out = {}
@@ -454,7 +458,9 @@ class MLPGroup:
             for slot in batch:
                 active[slot] = 1
             k = self._take_slot()
-            _native.check(_native.load_fast().mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
+            # the GIL-releasing binding: on the overlapped path the call may wait (host side) for the
+            # evaluation two rounds back to release its snapshot side
+            _native.check(lib.mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=True))
         D3 = self.dims[3]
         return {slot: raw.map(lambda r, s=slot: (float(r[0][s]) / max(1, self.n_test[s]), r[2][s, :D3, :D3].copy())) for slot in batch}
