@@ -78,6 +78,15 @@ __device__ __forceinline__ uint4 conv_ld16(__amdgpu_buffer_rsrc_t r, int byte_of
 }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * CG_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+// Patch rows (the halo kernels' staged 64-channel patch): the MFMA A reads of a tap start at ANY
+// patch row, and a ds_read_b128 lane group ({0-3,12-15,20-27}, ...) takes 8 rows at chunk c and the
+// other 8 of the 16 at chunk c + 1; with swz's key (row >> 1) & 7 that was 2-way conflicted for
+// half the start rows (1.41 conflicts per LDS instruction, profiles/r4n_*). Key row & 6 is
+// conflict-free for every start row (exhaustive check over the lane groups and 16-byte bank units).
+#ifndef HALO_SWZP
+#define HALO_SWZP 1
+#endif
+__device__ __forceinline__ int swzp(int row, int chunk) { return HALO_SWZP ? row * CG_BK + ((chunk ^ (row & 6)) << 3) : swz(row, chunk); }
 
 // [k][W] images read with ds_read_b64_tr_b16 (W = 64 or 128 bf16, unpadded rows): 8-byte granules
 // XOR-permuted by a row function so that the 32 lanes of a half-wave (rows 8g+q, g = 0/1, q = 0..3,
@@ -985,7 +994,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
       const int e = tid + NT * i;
       uint4 v = rp[i];
       if (PRO && ((pok >> i) & 1u)) v = bn_relu8(v, psc, psh);
-      if (e < PCH) *reinterpret_cast<uint4*>(pat + swz(e >> 3, e & 7)) = v;
+      if (e < PCH) *reinterpret_cast<uint4*>(pat + swzp(e >> 3, e & 7)) = v;
     }
   };
   // patch row of tap (0, 0) for this lane's A rows (row = wr * 64 + i * 16 + (lane & 15) of the tile)
@@ -1000,7 +1009,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
   if constexpr (DMA) {
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     // physical 8-row block blk of the patch: lane L writes row 8 blk + L / 8, physical chunk L % 8,
-    // i.e. logical chunk (L % 8) ^ ((row >> 1) & 7) of swz's layout; rows past the patch, padding
+    // i.e. logical chunk (L % 8) ^ (row & 6) of swzp's layout; rows past the patch, padding
     // pixels and rows of a missing image read the zero page (CONV_OOB)
     auto dma_patch = [&](int tm, bf16* dst) {
       const int m0 = tm * BM;
@@ -1010,7 +1019,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
         const int blk = wv + 8 * i;
         if (blk * 8 >= PROWS) break;
         const int R = blk * 8 + (lane >> 3);
-        const int chl = (lane & 7) ^ ((R >> 1) & 7);
+        const int chl = (lane & 7) ^ (HALO_SWZP ? (R & 6) : ((R >> 1) & 7));
         const int pr = R / PW, pc = R - pr * PW;
         const int h = h0 - 1 + pr, w = pc - 1;
         const bool ok = R < PROWS && (unsigned)h < (unsigned)a.src_h && (unsigned)w < (unsigned)W && img < nb;
@@ -1046,7 +1055,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
           const int ch = h * 4 + (lane >> 4);
           bf16x8 af[4], bfr[2];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) af[i] = ld8(pc + swz(pr0[i] + toff, ch));
+          for (int i = 0; i < 4; ++i) af[i] = ld8(pc + swzp(pr0[i] + toff, ch));
 #pragma unroll
           for (int j = 0; j < 2; ++j) bfr[j] = ld8(wt_t + swz(wc * 32 + j * 16 + (lane & 15), ch));
 #pragma unroll
@@ -1084,7 +1093,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
         const int ch = h * 4 + (lane >> 4);
         bf16x8 af[4], bfr[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = ld8(pat + swz(prow0[i] + toff, ch));
+        for (int i = 0; i < 4; ++i) af[i] = ld8(pat + swzp(prow0[i] + toff, ch));
 #pragma unroll
         for (int j = 0; j < 2; ++j) bfr[j] = ld8(wt_t + swz(wc * 32 + j * 16 + (lane & 15), ch));
 #pragma unroll
