@@ -288,6 +288,14 @@ int shmc_allgather_m(void* handle, const void* in, uint64_t n, void* out, uint64
   return rc;
 }
 
+// Diagnostics: out[0] = this handle's generation, out[1 + r] = rank r's status word.
+int shmc_state(void* handle, uint64_t* out) {
+  Handle* h = static_cast<Handle*>(handle);
+  out[0] = h->gen;
+  for (int r = 0; r < h->world; ++r) out[1 + r] = h->ctl(r)->status.load(std::memory_order_acquire);
+  return h->world;
+}
+
 // All-gather over every rank (no eviction). Returns 0 / 1 (overflow) / -1 (timeout or a rank left).
 int shmc_allgather(void* handle, const void* in, uint64_t n, void* out, uint64_t* lens, double timeout_s) {
   Handle* h = static_cast<Handle*>(handle);

@@ -799,11 +799,20 @@ class Federation:
         raise RuntimeError("aggregation did not complete after repeated membership changes")
 
     def _members_alive(self, members: List[int]) -> List[int]:
-        """Members (other than this rank) that are unresponsive right now."""
+        """Members (other than this rank) that are unresponsive right now, or already evicted by
+        another rank's gather. The evicted ones matter to a rank still waiting inside the
+        collective: the faster survivors evicted the dead rank and moved on to the agreement, so
+        neither its heartbeat nor the others' progress would ever end this rank's wait (the 8-rank
+        rehearsal hung this way about once in ten runs). A member that left on purpose completed
+        the collectives it had joined and does not count."""
         if self.shm is None:
             return []
-        bad = self.shm.unresponsive(float(Settings.FAILURE_TIMEOUT))
-        return [r for r in bad if r in members and r != self.rank]
+        bad = set(self.shm.unresponsive(float(Settings.FAILURE_TIMEOUT)))
+        alive = set(self.shm.alive())
+        if len(alive) < self.world:
+            clean = set(self.shm.left_clean())
+            bad |= {r for r in members if r not in alive and r not in clean}
+        return [r for r in sorted(bad) if r in members and r != self.rank]
 
     def await_works(self, works: list, what: str, poll: bool = True) -> None:
         """Wait for collective works while watching the members' liveness; then agree with the

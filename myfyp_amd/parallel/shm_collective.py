@@ -60,6 +60,8 @@ def _load() -> Optional[ctypes.CDLL]:
     lib.shmc_alive.argtypes = [vp]
     lib.shmc_left_clean.restype = u64
     lib.shmc_left_clean.argtypes = [vp]
+    lib.shmc_state.restype = ctypes.c_int
+    lib.shmc_state.argtypes = [vp, vp]
     lib.shmc_wait_all_gone.restype = i
     lib.shmc_wait_all_gone.argtypes = [vp, d, d]
     lib.shmc_unresponsive.restype = u64
@@ -163,6 +165,16 @@ class ShmCollective:
     def alive(self) -> List[int]:
         m = int(self._lib.shmc_alive(self._h))
         return [r for r in range(self.world) if m >> r & 1]
+
+    def state(self) -> Tuple[int, List[str]]:
+        """Diagnostics: (this rank's generation, every rank's status word; G = gone, L = left clean)."""
+        buf = (ctypes.c_uint64 * (self.world + 1))()
+        self._lib.shmc_state(self._h, ctypes.addressof(buf))
+        out = []
+        for r in range(self.world):
+            s = int(buf[1 + r])
+            out.append(("G" + ("L" if s >> 62 & 1 else "") + str(s & ((1 << 62) - 1))) if s >> 63 else str(s))
+        return int(buf[0]), out
 
     def left_clean(self) -> List[int]:
         """Ranks that left on purpose (``leave``) — as opposed to evicted as unresponsive."""

@@ -19,7 +19,17 @@ def _launch(tmp_path, **env_extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr", "127.0.0.1",
            "--master-port", str(free_port()), os.path.join(ROOT, "tests", "workers", "rehearsal8_worker.py")]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    hung = [f for f in sorted(tmp_path.glob("hang_*.txt")) if f.stat().st_size]
+
+    def learning_stack(text: str) -> str:  # control-plane state + the learning thread's innermost frames
+        head = "".join(l + "\n" for l in text.splitlines() if l.startswith("shm gen"))
+        for block in text.split("\n\n"):
+            if "_start_learning" in block:
+                return head + "\n".join(block.splitlines()[:6])
+        return head + text[:600]
+
+    hangs = "".join(f"--- {f.name}\n{learning_stack(f.read_text())}\n" for f in hung)
+    assert res.returncode == 0, hangs + res.stdout[-2000:] + res.stderr[-2000:]
     return {json.loads(f.read_text())["rank"]: json.loads(f.read_text()) for f in tmp_path.glob("rank*.json")}
 
 

@@ -11,6 +11,7 @@ and the deferred-collective confirmation."""
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,6 +19,12 @@ sys.path.insert(0, ROOT)
 
 
 def main() -> None:
+    import faulthandler
+
+    # a rank stuck for 90 s prints every thread's stack and exits (a test failure with a diagnosis,
+    # not a 300 s subprocess timeout)
+    hang = open(os.path.join(os.environ["OUT_DIR"], f"hang_{os.environ.get('LOCAL_RANK', '0')}.txt"), "w")
+    faulthandler.dump_traceback_later(float(os.environ.get("HANG_DUMP_S", "90")), exit=True, file=hang)
     import numpy as np
     import torch
 
@@ -47,6 +54,16 @@ def main() -> None:
                 learner_kwargs={"batch_size": 32})
     node.start()
     fed.finalize()
+
+    def dump_shm_state() -> None:  # diagnostics of a stuck run: control-plane generations
+        if fed.shm is not None:
+            gen, st = fed.shm.state()
+            hang.write(f"shm gen {gen} status {st} members {fed.members}\n")
+            hang.flush()
+
+    t_dump = threading.Timer(float(os.environ.get("HANG_DUMP_S", "90")) - 5, dump_shm_state)
+    t_dump.daemon = True
+    t_dump.start()
     if rank == kill_rank:
         fault_injection.crash_in_collective(fed, node, round=kill_round)
     t0 = time.time()
