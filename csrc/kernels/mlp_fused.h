@@ -35,6 +35,12 @@ struct MLPArgs {
   bf16* Xb16;       // same batches as bf16 (persistent path; null otherwise)
   int* Yb;          // [P][xb_rows]
   int64_t xb_rows;  // max_steps * B
+  // direct-X epochs (fp32 layout 1): the kernel reads each batch row from a static exact-bf16 copy of
+  // the peer's images through the epoch's sample index (xidx), so no per-epoch image gather runs;
+  // the epoch's index / label kernel (mlp_index_epoch) writes xidx and Yb
+  const bf16* const* Xp16;  // [P] device pointers to [n_p][D0] bf16 images (or null)
+  int* xidx;                // [P][xb_rows] sample index of each epoch position
+  int x_direct;             // 1: the fp32 layout-1 epoch reads X through xidx / Xp16
   unsigned* flags_zero;  // persistent epoch: hand-off flag lines zeroed by the gather kernel (or null)
   int flags_per_peer;    // u32 words per peer
   // test data
@@ -70,5 +76,7 @@ bool mlp_shape_supported(int D0, int D1, int D2, int D3);
 void mlp_launch_train_step(const MLPArgs& a, int step, hipStream_t s);
 void mlp_launch_eval_chunk(const MLPArgs& a, int base, hipStream_t s);
 void mlp_launch_sync_shadow(const MLPArgs& a, hipStream_t s);
+// the epoch's sample index and labels (direct-X epochs); zeroes the hand-off flags like the gather
+void mlp_launch_index_epoch(const MLPArgs& a, hipStream_t s);
 // max_wgs > 0 caps the grid (at least one workgroup per peer); rows are grid-strided
 void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s, int max_wgs = 0);

@@ -703,6 +703,27 @@ __global__ __launch_bounds__(256) void mlp_gather_epoch(MLPArgs a) {
   }
 }
 
+// direct-X epochs: xidx[p][i] = perm_p(i) and Yb[p][i] = Y_p[perm_p(i)] (no image rows move: the
+// fp32 epoch kernel reads them from the static bf16 copy through xidx). grid = (ceil(xb_rows / 256),
+// 1, P), block 256.
+__global__ __launch_bounds__(256) void mlp_index_epoch(MLPArgs a) {
+  const int p = blockIdx.z;
+  const int n = a.ctl[p].y;
+  if (a.flags_zero != nullptr && blockIdx.x == 0)
+    for (int q = threadIdx.x; q < a.flags_per_peer; q += 256) a.flags_zero[(int64_t)p * a.flags_per_peer + q] = 0u;
+  if (!a.ctl[p].x) return;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || i >= a.xb_rows) return;
+  const int src = a.shuffle_native ? (int)feistel_perm((unsigned)i, (unsigned)n, *a.seed ^ (0x9e3779b97f4a7c15ull * (unsigned long long)(p + 1)))
+                                   : a.perm[(int64_t)p * a.perm_stride + i];
+  a.xidx[(int64_t)p * a.xb_rows + i] = src;
+  a.Yb[(int64_t)p * a.xb_rows + i] = a.Yp[p][src];
+}
+
+void mlp_launch_index_epoch(const MLPArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_index_epoch, dim3((unsigned)((a.xb_rows + 255) / 256), 1, a.P), dim3(256), 0, s, a);
+}
+
 void mlp_launch_gather_epoch(const MLPArgs& a, hipStream_t s, int max_wgs) {
   const int64_t waves = (a.xb_rows + GATHER_RPW - 1) / GATHER_RPW;
   int64_t gx = (waves + 3) / 4;

@@ -44,7 +44,10 @@ int mlp_persistent_f32_gang();
 int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus);
 int mlp_persistent_f32_launch_wgs(const MLPArgs& a);  // workgroups of one epoch launch
 int mlp_persistent_f32_ks(const MLPArgs& a);
-int mlp_persistent_f32_variant(const MLPArgs& a);  // gang layout: 1 owners + heads, 2 owners only          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
+int mlp_persistent_f32_variant(const MLPArgs& a);
+// 1: this build's fp32 epoch for `a` reads X directly (needs a.Xp16 and the index kernel's xidx / Yb)
+int mlp_persistent_f32_x_direct(const MLPArgs& a);
+int mlp_persistent_f32_x_direct_build();  // the build's P32_XDIRECT  // gang layout: 1 owners + heads, 2 owners only          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);

@@ -105,6 +105,15 @@ using namespace f32k;
 #ifndef P32_SM8
 #define P32_SM8 1
 #endif
+// direct-X epochs (layout 1, opt-in build -DP32_XDIRECT=1): batch rows read from the static bf16 copy
+// of the peer's images through the epoch index (MLPArgs::Xp16 / xidx, written by mlp_index_epoch)
+// instead of a per-epoch gathered copy. Measured slower (profiles/r4p_direct_x): the round boundary
+// loses the gather (an 8 x 7.5k index kernel replaces it) but C2's next-batch staging now waits on
+// the row index before its loads, 3.72 -> 4.28 us per step (519.4 / 524.8 vs 532.2 / 532.4
+// rounds/s). The engine asks mlp_persistent_f32_x_direct() which one the build expects.
+#ifndef P32_XDIRECT
+#define P32_XDIRECT 0
+#endif
 constexpr int SMR = (P32_SM8 && !P32_LL_PL) ? 2 : 4;  // softmax rows per lane
 #ifndef P32_LL_DH2
 #define P32_LL_DH2 0
@@ -141,7 +150,7 @@ __device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, i
 struct OwnerLds32 {
   int ldx;  // bf16 row stride of the X tile
   int ldt;  // bf16 row stride of the transposed dH1 split tiles [3][16][B]
-  size_t x, red, h1, dh1s, w1x, ok, total;
+  size_t x, red, h1, dh1s, w1x, rows, ok, total;
 };
 // K steps of one owner: KH = ceil(KS1 / KS) (the last K-split owner may hold fewer)
 __host__ __device__ inline int kh_of(int D0, int KS) { return (ks1_of(D0) + KS - 1) / KS; }
@@ -157,6 +166,7 @@ __host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0, int KS) {
   L.h1 = o;   o += al16((size_t)2 * Bpad * 16 * 4);  // own H1 slice, step-parity double buffer
   L.dh1s = o; o += al16((size_t)3 * 16 * L.ldt * 2);  // dH1ᵀ as hi / mid / lo bf16 (exact split)
   L.w1x = o;  o += al16(KS == 1 ? (size_t)4 * 16 * 32 * 4 : 0);  // KS = 1: W1 state of K step 24 (w, m, v, e)
+  L.rows = o; o += al16((size_t)Bpad * 4);  // direct-X epochs: the next batch's sample indices
   L.ok = o;   o += 16;
   L.total = o;
   return L;
@@ -229,7 +239,13 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   float* sH1 = reinterpret_cast<float*>(smem + L.h1);
   bf16* sD3 = reinterpret_cast<bf16*>(smem + L.dh1s);  // [hi, mid, lo][o1 local][b]
   float* sW1x = reinterpret_cast<float*>(smem + L.w1x);  // [w, m, v, e][16][32]: K step 24
+  int* sRowN = reinterpret_cast<int*>(smem + L.rows);     // direct X: sample index of next-batch row r
   int* sOk = reinterpret_cast<int*>(smem + L.ok);
+  // direct-X epoch (a.x_direct): batch row r of step t is image xidx[p][tB + r] of the peer's static
+  // bf16 copy (no per-epoch gather of the images; the index kernel wrote xidx)
+  constexpr bool xd = P32_XDIRECT != 0;
+  const bf16* xp16 = xd ? a.Xp16[p] : nullptr;
+  const int* xidx_p = xd ? a.xidx + (int64_t)p * a.xb_rows : nullptr;
 
   const OptParams& o = a.opt;
   const int4 ctl = a.ctl[p];
@@ -312,7 +328,8 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       const int idx = kk * 64 + lv;
       const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
       if (s < KS1 && gcol < D0) {
-        const bf16* src = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + gcol;
+        const bf16* src = xd ? (r < rows ? xp16 + (int64_t)xidx_p[t * a.B + r] * D0 + gcol : xp16)
+                             : a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + gcol;
         *reinterpret_cast<uint4*>(sX + r * LDX + col) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
       } else if (s < KS1 && gcol == D0) {
         *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows);
@@ -442,12 +459,23 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (more) {
       const int rows_n = rows_at(a, n, t + 1);
       unsigned sink = 0;
+      // direct X: this lane's next-batch row (lane < BP) through the epoch index; wave 0 leaves the
+      // indices in LDS for C2's staging (read after the dH2 barriers below)
+      int xi = lane;
+      if (xd) {
+        xi = (lane < rows_n && lane < BP) ? xidx_p[(t + 1) * a.B + lane] : 0;
+        int ln = lane;  // laundered: a hoisted LDS address was the bench instantiation's one VGPR spill
+        asm volatile("" : "+v"(ln));
+        if (wave == 0 && ln < BP) sRowN[ln] = xi;
+      }
+      const bf16* xbase = xd ? xp16 : a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
+      const bf16* xrow = xbase + (unsigned)(xi * D0);
 #pragma unroll
       for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         const int s = wave + 8 * q;
         const int r = lane;
         if (s < KS1 && C0 + 32 * s < D0 && r < rows_n && r < BP)
-          sink ^= *reinterpret_cast<const unsigned*>(a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B + r) * D0 + C0 + 32 * s);
+          sink ^= *reinterpret_cast<const unsigned*>(xrow + C0 + 32 * s);
       }
       asm volatile("" ::"v"(sink));
     }
@@ -565,7 +593,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       int lv = lane;
       asm volatile("" : "+v"(lv));
       const int rows_next = more ? rows_at(a, n, t + 1) : 0;
-      const bf16* xnext = a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
+      const bf16* xnext = xd ? xp16 : a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)(t + 1) * a.B) * D0;
 #pragma unroll
       for (int q = 0; q < (KS == 1 ? RQ + 1 : RQ); ++q) {
         // register K steps: wave w owns K step w + 8q, both 16-column halves (tt = 0, 1). The
@@ -594,7 +622,13 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #ifdef P32_EXP_NOX  // timing experiment: no next-batch staging loads
             xq[kk] = uint4{(unsigned)lv, 0u, 0u, 0u};
 #else
-            xq[kk] = (more && xmine && gcol < D0 && r < rows_next) ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(r * D0 + gcol)) : uint4{0u, 0u, 0u, 0u};
+            const bool xl = more && xmine && gcol < D0 && r < rows_next;
+            // row of the next batch: static-copy image (direct X; re-read from LDS per K step — four
+            // indices held across C2 cost the bench instantiation a VGPR spill) or batch row
+            int rr = r;
+            if (xd) asm volatile("" : "+v"(rr));
+            const int rid = xd ? sRowN[rr] : r;
+            xq[kk] = xl ? *reinterpret_cast<const uint4*>(xnext + (unsigned)(rid * D0 + gcol)) : uint4{0u, 0u, 0u, 0u};
 #endif
           }
 #pragma unroll
@@ -1435,6 +1469,8 @@ size_t mlp_persistent_f32_flag_bytes(int P) { return (size_t)P * FPP * persist::
 int mlp_persistent_f32_gang() { return roles_of(1); }
 int mlp_persistent_f32_ks(const MLPArgs& a) { return f32_ks(a); }
 int mlp_persistent_f32_variant(const MLPArgs& a) { return f32_variant(a); }
+int mlp_persistent_f32_x_direct(const MLPArgs& a) { return P32_XDIRECT && f32_variant(a) == 1 ? 1 : 0; }
+int mlp_persistent_f32_x_direct_build() { return P32_XDIRECT; }
 
 // Workgroups one epoch launch needs (its peers' gangs) and how many the device holds at once.
 int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_launch_wgs() : ppl_of(f32_ks(a)) * roles_of(f32_ks(a)); }

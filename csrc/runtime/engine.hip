@@ -201,6 +201,9 @@ struct MLPEngine {
   // recorded on the main stream right before its graph launch; epoch r-2, the last reader of the
   // buffer, is then done) and runs on a capped grid (MYFYP_PREP_GATHER_WGS, default 64) beside it,
   // instead of at the round boundary (its earliest start in mode 1), where it slowed the FedAvg.
+  // direct-X fp32 epochs (mlp_persistent_f32_x_direct): the graph's first node is the index / label
+  // kernel (8 x 7.5k indices) instead of the image gather, and no prep stream is used
+  bool x_direct = false;
   bool prep_mode = false;
   int prep_level = 0;
   int prep_wgs = 64;
@@ -359,6 +362,7 @@ struct MLPEngine {
     if (a.Xb) hipFree(a.Xb);
     if (a.Xb16) hipFree(a.Xb16);
     if (a.Yb) hipFree(a.Yb);
+    if (a.xidx) hipFree(a.xidx);
     for (auto& r : ring) {
       if (r.ev) hipEventDestroy(r.ev);
       if (r.loss) hipHostFree(r.loss);
@@ -536,7 +540,11 @@ struct MLPEngine {
       a.Yb = yb_buf[buf];
     }
     CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
-    if (!prep_mode) {
+    if (x_direct) {
+      MLPArgs ga = a;
+      set_flag_zeroing(ga);  // the index kernel zeroes the hand-off flags (no memset node)
+      mlp_launch_index_epoch(ga, cap_stream);
+    } else if (!prep_mode) {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
       if (graph_persistent) set_flag_zeroing(ga);  // ... which also zeroes the hand-off flags (no memset node)
@@ -585,10 +593,16 @@ struct MLPEngine {
     invalidate();
     if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
     graph_persistent = use_persistent();
+    x_direct = graph_persistent && precision == 1 && mlp_persistent_f32_x_direct(a);
+    if (x_direct && (a.Xp16 == nullptr || a.xidx == nullptr)) {
+      g_last_error = "fp32 direct-X epoch: no bf16 image table bound (mlp_engine_set_train_x16)";
+      return 1;
+    }
+    a.x_direct = x_direct ? 1 : 0;
     {
       const char* env = getenv("MYFYP_PREP_GATHER");
       prep_level = env != nullptr ? atoi(env) : 2;  // default: ahead (+0.5-1 %, profiles/r4h_*, r4j_*)
-      prep_mode = graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && (prep_level == 1 || prep_level == 2);
+      prep_mode = !x_direct && graph_persistent && a.shuffle_native && xb16_buf[1] != nullptr && (prep_level == 1 || prep_level == 2);
       if (const char* w = getenv("MYFYP_PREP_GATHER_WGS")) prep_wgs = atoi(w);
       if (prep_mode && ensure_prep()) return 1;
       if (prep_mode) {
@@ -929,6 +943,9 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
     CHECK_HIP(hipMalloc((void**)&e->a.Yb, (size_t)e->a.P * rows * sizeof(int)));
     CHECK_HIP(hipMemset(e->a.Xb, 0, (size_t)e->a.P * rows * e->a.D0));
     CHECK_HIP(hipMemset(e->a.Yb, 0, (size_t)e->a.P * rows * sizeof(int)));
+    if (e->a.xidx) hipFree(e->a.xidx);
+    CHECK_HIP(hipMalloc((void**)&e->a.xidx, (size_t)e->a.P * rows * sizeof(int)));
+    CHECK_HIP(hipMemset(e->a.xidx, 0, (size_t)e->a.P * rows * sizeof(int)));
     if (e->xb16_buf[1]) hipFree(e->xb16_buf[1]);
     if (e->yb_buf[1]) hipFree(e->yb_buf[1]);
     e->xb16_buf[0] = e->xb16_buf[1] = nullptr;
@@ -946,6 +963,23 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
   }
   e->invalidate();
   return 0;
+}
+
+// Direct-X fp32 epochs: per-peer device pointers to exact-bf16 copies of the training images ([n_p][D0],
+// the caller keeps them alive and rebinds when the data changes). Re-captures.
+int mlp_engine_set_train_x16(void* h, const uint64_t* Xp16) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->a.Xp16 = (const bf16* const*)Xp16;
+  e->invalidate();
+  return 0;
+}
+// 1 if this build's fp32 layout-1 epoch reads X directly (the caller then binds the bf16 images)
+int mlp_engine_x_direct_build() { return mlp_persistent_f32_x_direct_build(); }
+// 1 if the fp32 epoch of this engine's current configuration reads X directly (needs set_train_x16)
+int mlp_engine_x_direct(void* h) {
+  auto* e = (MLPEngine*)h;
+  return e->precision == 1 && mlp_persistent_f32_x_direct(e->a) ? 1 : 0;
 }
 
 // host copies of the per-peer sample counts (packed into the control words)
@@ -1206,7 +1240,14 @@ int mlp_engine_run_epoch_eager(void* h, const int* t0_host, void* stream) {
     g_last_error = "fp32 MLP engine: shape / batch / CU count not supported by the fp32 persistent epoch";
     return 2;
   }
-  {
+  if (pers && e->precision == 1 && mlp_persistent_f32_x_direct(e->a)) {
+    if (e->a.Xp16 == nullptr || e->a.xidx == nullptr) {
+      g_last_error = "fp32 direct-X epoch: no bf16 image table bound (mlp_engine_set_train_x16)";
+      return 1;
+    }
+    e->a.x_direct = 1;
+    mlp_launch_index_epoch(e->a, s);
+  } else {
     MLPArgs ga = e->a;
     if (!pers) ga.Xb16 = nullptr;
     mlp_launch_gather_epoch(ga, s);

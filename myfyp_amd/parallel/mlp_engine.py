@@ -276,6 +276,17 @@ class MLPGroup:
             self._keep += [x, y, xt, yt]
         self.n_train = ns
         self.n_test = nts
+        # builds with direct-X fp32 epochs (opt-in, -DP32_XDIRECT=1) read every batch row from an
+        # exact bf16 copy of the peer's uint8 images (made once per data binding): [n_p][D0] per slot
+        # (built whatever the precision: a later switch to fp32 must not find a missing table)
+        x16s = [0] * cap
+        want_x16 = bool(lib.mlp_engine_x_direct_build())
+        for slot, h in (self.handles.items() if want_x16 else ()):
+            x = h.device_split(True)[0]
+            if x.shape[0] > 0:
+                x16 = x.to(torch.bfloat16)
+                x16s[slot] = x16.data_ptr()
+                self._keep.append(x16)
         self._tables = {
             "Xp": torch.tensor(xs, dtype=torch.int64, device=dev),
             "Yp": torch.tensor(ys, dtype=torch.int64, device=dev),
@@ -283,6 +294,7 @@ class MLPGroup:
             "Xtp": torch.tensor(xts, dtype=torch.int64, device=dev),
             "Ytp": torch.tensor(yts, dtype=torch.int64, device=dev),
             "nt": torch.tensor(nts, dtype=torch.int32, device=dev),
+            "Xp16": torch.tensor(x16s, dtype=torch.int64, device=dev),
         }
         self.nmax = max(1, max(ns) if ns else 1)
         self.max_steps = (self.nmax + self.B - 1) // self.B
@@ -290,6 +302,7 @@ class MLPGroup:
         t = self._tables
         _native.check(lib.mlp_engine_set_train_data(self._engine, _p(t["Xp"]), _p(t["Yp"]), _p(t["n"]), _p(self.perm), self.nmax, self.max_steps), "set_train_data")
         _native.check(lib.mlp_engine_set_test_data(self._engine, _p(t["Xtp"]), _p(t["Ytp"]), _p(t["nt"]), max(nts) if nts else 0), "set_test_data")
+        _native.check(lib.mlp_engine_set_train_x16(self._engine, _p(t["Xp16"]) if want_x16 else None), "set_train_x16")
         n_host = np.asarray(ns, dtype=np.int32)
         nt_host = np.asarray(nts, dtype=np.int32)
         _native.check(lib.mlp_engine_set_counts(self._engine, n_host.ctypes.data, nt_host.ctypes.data), "set_counts")
