@@ -138,9 +138,15 @@ struct EpiSums {
 // PARTS > 1: the tile goes through a staging area of BM / PARTS rows (`stg`, fp32) in PARTS rounds,
 // row slab by row slab (the waves of a slab stage, everyone applies), so that the rest of LDS can
 // take the next tile's first operand stage meanwhile (k_conv_fwd_dma).
-template <int MODE, int BM, int BN, int NT, int PARTS = 1>
+// SPEC >= 0: the epilogue's operand set fixed at compile time (bit 0 residual, 1 BN-backward sums,
+// 2 a second BN, 3 ReLU mask from a materialised activation, 4 ReLU mask from y0 and the BN's
+// scale / shift; no bias, no ReLU, every column valid) — the runtime-flag epilogue keeps every
+// variant's registers and branches live in the persistent halo dgrad (11.7 VALU per MFMA); -1: flags
+// from the arguments.
+template <int MODE, int BM, int BN, int NT, int PARTS = 1, int SPEC = -1>
 __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], float* stg, int peer, int m0, int n0, int M,
                                                    int hw, int rw, int ph, int pw, EpiSums& q) {
+  constexpr bool SP = SPEC >= 0;
   constexpr int NF = BN / 32;
   constexpr int SR = BM / PARTS;  // staged rows per round (a multiple of the 64 rows of a wave)
   static_assert(SR % 64 == 0, "staging rounds hold whole wave rows");
@@ -153,12 +159,16 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   const int col0 = n0 + ch * 8;
   const bool chok = col0 < a.ncol;  // ncol is a multiple of 8
   bf16* out = a.out + peer * a.out_ps;
-  const bf16* resid = a.resid ? a.resid + peer * a.resid_ps : nullptr;
+  const bool resid_on = SP ? (SPEC & 1) != 0 : a.resid != nullptr;
+  const bf16* resid = resid_on ? a.resid + peer * a.resid_ps : nullptr;
   // BN-backward epilogue (dgrad only)
-  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
-  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
-  const bf16* bmask = (bnb && a.bnb_mask) ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
-  const bool ymask = bnb && bmask == nullptr && a.bnb_mask_ss != nullptr;  // mask = relu(BN(y0)) > 0
+  const bool bnb = MODE != 0 && (SP ? (SPEC & 2) != 0 : a.bnb_part0 != nullptr);
+  const bool bnb2 = bnb && (SP ? (SPEC & 4) != 0 : a.bnb_part1 != nullptr);
+  const bool bmask_on = bnb && (SP ? (SPEC & 8) != 0 : a.bnb_mask != nullptr);
+  const bf16* bmask = bmask_on ? a.bnb_mask + peer * a.bnb_mask_ps : nullptr;
+  const bool ymask = bnb && !bmask_on && (SP ? (SPEC & 16) != 0 : a.bnb_mask_ss != nullptr);  // mask = relu(BN(y0)) > 0
+  const bool bias_on = !SP && a.bias != nullptr;
+  const bool relu_on = !SP && a.relu;
   const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
   const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
   const bool fstats = !bnb && a.stats != nullptr;
@@ -176,8 +186,8 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int col = col0 + j;
-    cval[j] = col < a.ncol_valid;
-    bv[j] = (a.bias != nullptr && cval[j]) ? fresh(a.bias + peer * a.bias_ps)[col] : 0.f;
+    cval[j] = SP || col < a.ncol_valid;
+    bv[j] = (bias_on && cval[j]) ? fresh(a.bias + peer * a.bias_ps)[col] : 0.f;
     mean0[j] = inv0[j] = mean1[j] = inv1[j] = msc[j] = msh[j] = 0.f;
     if (ymask && chok) {
       const float* ssp = fresh(a.bnb_mask_ss + peer * a.bnb_mask_ss_ps);
@@ -224,8 +234,8 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       if (m >= M) break;
       const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
       uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
-      if (resid != nullptr) ur = *reinterpret_cast<const uint4*>(resid + o);
-      if (bmask != nullptr) um = *reinterpret_cast<const uint4*>(bmask + o);
+      if (resid_on) ur = *reinterpret_cast<const uint4*>(resid + o);
+      if (bmask_on) um = *reinterpret_cast<const uint4*>(bmask + o);
       if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
       if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
       const int sw = (((row >> 2) & 3) << 4) ^ ((row & 1) << 2);
@@ -237,12 +247,12 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       bf8 ob;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float x = v[j] + bv[j];
-        if (resid != nullptr) x += (float)br.v[j];
-        if (a.relu) x = fmaxf(x, 0.f);
+        float x = bias_on ? v[j] + bv[j] : v[j];
+        if (resid_on) x += (float)br.v[j];
+        if (relu_on) x = fmaxf(x, 0.f);
         if (!cval[j]) x = 0.f;
         if (bnb) {
-          if (bmask != nullptr && !((float)bm.v[j] > 0.f)) x = 0.f;
+          if (bmask_on && !((float)bm.v[j] > 0.f)) x = 0.f;
           // the bf16 activation relu(y*sc + sh) (bn_relu8) is > 0 exactly when y*sc + sh > 0
           if (ymask && !(fmaf((float)b0.v[j], msc[j], msh[j]) > 0.f)) x = 0.f;
           ob.v[j] = (bf16)x;
@@ -267,14 +277,14 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
 // row `srow` of the peer (rows spread the atomics of many workgroups over several addresses). Over
 // the wave's rows (lanes of one chunk) by shuffles, over the waves in LDS (the staging tile must no
 // longer be read: this starts with a barrier).
-template <int MODE, int BN, int NT>
+template <int MODE, int BN, int NT, int SPEC = -1>
 __device__ __forceinline__ void conv_epilogue_sums(const ConvGemmArgs& a, bf16* lds, int peer, int n0, int srow, EpiSums& q) {
   constexpr int CH = BN / 8, NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid % CH;
-  const bool bnb = MODE != 0 && a.bnb_part0 != nullptr;
-  const bool bnb2 = bnb && a.bnb_part1 != nullptr;
-  const bool fstats = !bnb && a.stats != nullptr;
+  const bool bnb = MODE != 0 && (SPEC >= 0 ? (SPEC & 2) != 0 : a.bnb_part0 != nullptr);
+  const bool bnb2 = bnb && (SPEC >= 0 ? (SPEC & 4) != 0 : a.bnb_part1 != nullptr);
+  const bool fstats = !bnb && SPEC < 0 && a.stats != nullptr;
   if (!bnb && !fstats) return;
   float(&q0)[8] = q.q0;
   float(&q1)[8] = q.q1;
@@ -920,7 +930,10 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
 #ifndef HALO_DMA4
 #define HALO_DMA4 1
 #endif
-template <int MODE, bool PRO>
+#ifndef HALO_SPEC  // the layer-1 dgrads with compile-time epilogue operand sets (conv_epilogue_tile SPEC)
+#define HALO_SPEC 1
+#endif
+template <int MODE, bool PRO, int SPEC = -1>
 __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int tiles_m) {
   static_assert(MODE == 0 || MODE == 4, "forward-shaped convs");
   static_assert(!PRO || MODE == 0, "BN prologue on the forward only");
@@ -1065,10 +1078,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
         }
       }
       __syncthreads();  // patch reads done: the epilogue stages over it, two 128-row slabs
-      conv_epilogue_tile<MODE, BM, BN, NT, 2>(a, acc, reinterpret_cast<float*>(pc), peer, tm * BM, 0, M, HW, W, 0, 0, q);
+      conv_epilogue_tile<MODE, BM, BN, NT, 2, SPEC>(a, acc, reinterpret_cast<float*>(pc), peer, tm * BM, 0, M, HW, W, 0, 0, q);
       cur ^= 1;
     }
-    conv_epilogue_sums<MODE, BN, NT>(a, pat, peer, 0, g0, q);
+    conv_epilogue_sums<MODE, BN, NT, SPEC>(a, pat, peer, 0, g0, q);
     return;
   }
   // MODE 0 prefetches the next tile's patch into registers under the MFMAs
@@ -1647,7 +1660,17 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     const int tiles_m = (a.max_batch * a.out_h * 32 + 255) / 256;
     int G = g_conv_dma_wgs > 0 ? g_conv_dma_wgs : (conv_num_cus() + peers - 1) / peers;  // one workgroup per CU
     G = G < 1 ? 1 : (G > tiles_m ? tiles_m : G);
-    if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    // the layer-1 dgrads' two epilogue operand sets, compiled specialised (conv_epilogue_tile SPEC):
+    // conv2 (BN1-backward sums, ReLU mask from y1) and conv1 (skip gradient, BN-backward sums of the
+    // previous block's BN2, mask from the block input)
+    int spec = -1;
+    if (mode == 4 && HALO_DMA4 && HALO_SPEC && a.bias == nullptr && !a.relu && a.ncol_valid == a.ncol && a.bnb_part0 != nullptr && a.bnb_part1 == nullptr) {
+      const int sp = (a.resid ? 1 : 0) | 2 | (a.bnb_mask ? 8 : (a.bnb_mask_ss ? 16 : 0));
+      if (sp == 11 || sp == 18) spec = sp;
+    }
+    if (mode == 4 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_halo<4, false, 11>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (mode == 4 && spec == 18) hipLaunchKernelGGL((k_conv_fwd_halo<4, false, 18>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_fwd_halo<0, true>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else hipLaunchKernelGGL((k_conv_fwd_halo<0, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     return hipGetLastError() == hipSuccess ? 0 : 2;
