@@ -140,7 +140,7 @@ struct EpiSums {
 // take the next tile's first operand stage meanwhile (k_conv_fwd_dma).
 // SPEC >= 0: the epilogue's operand set fixed at compile time (bit 0 residual, 1 BN-backward sums,
 // 2 a second BN, 3 ReLU mask from a materialised activation, 4 ReLU mask from y0 and the BN's
-// scale / shift; no bias, no ReLU, every column valid) — the runtime-flag epilogue keeps every
+// scale / shift, 5 forward BN statistics; no bias, no ReLU, every column valid) — the runtime-flag epilogue keeps every
 // variant's registers and branches live in the persistent halo dgrad (11.7 VALU per MFMA); -1: flags
 // from the arguments.
 template <int MODE, int BM, int BN, int NT, int PARTS = 1, int SPEC = -1>
@@ -171,7 +171,7 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   const bool relu_on = !SP && a.relu;
   const bf16* by0 = bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : nullptr;
   const bf16* by1 = bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : nullptr;
-  const bool fstats = !bnb && a.stats != nullptr;
+  const bool fstats = !bnb && (SP ? (SPEC & 32) != 0 : a.stats != nullptr);
   // the per-column constants are re-read for every tile (pointers laundered through an empty asm):
   // hoisted out of a persistent kernel's tile loop they would hold 56 VGPRs across the MFMAs
   auto fresh = [](const float* p) {
@@ -284,7 +284,7 @@ __device__ __forceinline__ void conv_epilogue_sums(const ConvGemmArgs& a, bf16* 
   const int ch = tid % CH;
   const bool bnb = MODE != 0 && (SPEC >= 0 ? (SPEC & 2) != 0 : a.bnb_part0 != nullptr);
   const bool bnb2 = bnb && (SPEC >= 0 ? (SPEC & 4) != 0 : a.bnb_part1 != nullptr);
-  const bool fstats = !bnb && SPEC < 0 && a.stats != nullptr;
+  const bool fstats = !bnb && (SPEC >= 0 ? (SPEC & 32) != 0 : a.stats != nullptr);
   if (!bnb && !fstats) return;
   float(&q0)[8] = q.q0;
   float(&q1)[8] = q.q1;
@@ -652,7 +652,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-template <int MODE, int BM, int BN, int NS, int MINB>
+template <int MODE, int BM, int BN, int NS, int MINB, int SPEC = -1>
 __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, int tiles_m, int tiles_n) {
   static_assert(MODE == 0 || MODE == 4 || MODE == 5, "forward-shaped gathers only");
   constexpr int EMODE = MODE == 5 ? 2 : MODE;  // epilogue: MODE 5 writes MODE 2's class rows
@@ -820,7 +820,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
         setup(tm + G);
         if (nk > 0) issue(0);  // the next tile's first stage lands under this epilogue
       }
-      conv_epilogue_tile<EMODE, BM, BN, NT, 2>(a, acc, reinterpret_cast<float*>(lds + STAGE), peer, m0, n0, M, hw, gw, ph, pw, q);
+      conv_epilogue_tile<EMODE, BM, BN, NT, 2, SPEC>(a, acc, reinterpret_cast<float*>(lds + STAGE), peer, m0, n0, M, hw, gw, ph, pw, q);
     }
   } else {
     for (int tm = g0; tm < tiles_mp; tm += G) {
@@ -897,11 +897,11 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
         wb = wb + 1 == NS ? 0 : wb + 1;
       }
       __syncthreads();  // operand stages idle: the epilogue stages the tile over them
-      conv_epilogue_tile<EMODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, gw, ph, pw, q);
+      conv_epilogue_tile<EMODE, BM, BN, NT, 1, SPEC>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, gw, ph, pw, q);
       __syncthreads();  // staging tile read: the next tile's DMA may overwrite it
     }
   }
-  conv_epilogue_sums<EMODE, BN, NT>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
+  conv_epilogue_sums<EMODE, BN, NT, SPEC>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
 }
 
 
@@ -1116,10 +1116,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
       }
     }
     __syncthreads();  // patch reads done: the epilogue stages over it
-    conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(pat), peer, tm * BM, 0, M, HW, W, 0, 0, q);
+    conv_epilogue_tile<MODE, BM, BN, NT, 1, SPEC>(a, acc, reinterpret_cast<float*>(pat), peer, tm * BM, 0, M, HW, W, 0, 0, q);
     __syncthreads();  // staging read: the next patch may be stored
   }
-  conv_epilogue_sums<MODE, BN, NT>(a, pat, peer, 0, g0, q);
+  conv_epilogue_sums<MODE, BN, NT, SPEC>(a, pat, peer, 0, g0, q);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1637,6 +1637,14 @@ extern "C" int conv_set_dma(int v) {
   return old;
 }
 
+// compile-time epilogue operand set of a launch (conv_epilogue_tile SPEC), -1 = runtime flags
+static int conv_spec(const ConvGemmArgs& a, int mode) {
+  if (!HALO_SPEC || a.bias != nullptr || a.relu || a.ncol_valid != a.ncol) return -1;
+  if (mode == 0) return (a.resid == nullptr && a.stats != nullptr && a.pro_ss == nullptr) ? 32 : -1;
+  if (a.bnb_part0 == nullptr) return -1;
+  return (a.resid ? 1 : 0) | 2 | (a.bnb_part1 ? 4 : 0) | (a.bnb_mask ? 8 : (a.bnb_mask_ss ? 16 : 0));
+}
+
 extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, void* stream) {
   const ConvGemmArgs& a = *pa;
   // mode 0 forward, 1 dgrad, 4 stride-1 dgrad as a forward conv over dY with k_conv_wt_flip weights
@@ -1663,15 +1671,18 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     // the layer-1 dgrads' two epilogue operand sets, compiled specialised (conv_epilogue_tile SPEC):
     // conv2 (BN1-backward sums, ReLU mask from y1) and conv1 (skip gradient, BN-backward sums of the
     // previous block's BN2, mask from the block input)
-    int spec = -1;
-    if (mode == 4 && HALO_DMA4 && HALO_SPEC && a.bias == nullptr && !a.relu && a.ncol_valid == a.ncol && a.bnb_part0 != nullptr && a.bnb_part1 == nullptr) {
-      const int sp = (a.resid ? 1 : 0) | 2 | (a.bnb_mask ? 8 : (a.bnb_mask_ss ? 16 : 0));
-      if (sp == 11 || sp == 18) spec = sp;
-    }
+    // (the forward with the BN1 prologue counts as stats-only: the prologue is on the operand side)
+    const int spec = mode == 4 ? (HALO_DMA4 ? conv_spec(a, 4) : -1) : (a.pro_ss ? [&] {
+      ConvGemmArgs b = a;
+      b.pro_ss = nullptr;
+      return conv_spec(b, 0);
+    }() : conv_spec(a, 0));
     if (mode == 4 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_halo<4, false, 11>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (mode == 4 && spec == 18) hipLaunchKernelGGL((k_conv_fwd_halo<4, false, 18>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (a.pro_ss != nullptr && spec == 32) hipLaunchKernelGGL((k_conv_fwd_halo<0, true, 32>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_fwd_halo<0, true>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (spec == 32) hipLaunchKernelGGL((k_conv_fwd_halo<0, false, 32>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else hipLaunchKernelGGL((k_conv_fwd_halo<0, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
@@ -1702,7 +1713,15 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     else if (mode == 5) hipLaunchKernelGGL((k_conv_fwd_dma<5, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n); \
     else hipLaunchKernelGGL((k_conv_fwd_dma<0, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n);          \
   } while (0)
-      if (wide) {
+      // the default wide tile with the layers 2-4 operand sets compiled in (conv_epilogue_tile SPEC):
+      // forward (BN statistics only) and the stride-1 dgrads (conv2: BN1-backward, mask from a1;
+      // conv1: skip gradient, previous BN2, mask from the block input; with a projection BN too it
+      // spilled 22 VGPRs, so that one keeps the runtime flags)
+      const int spec = (mode == 0 || mode == 4) ? conv_spec(a, mode) : -1;
+      if (wide && var != 1 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (wide && var != 1 && mode == 4 && spec == 10) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 10>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (wide && var != 1 && mode == 4 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (wide) {
         if (var == 1) DMA_LAUNCH(256, 128, 3, 1);
         else DMA_LAUNCH(128, 128, 2, 2);
       } else {
