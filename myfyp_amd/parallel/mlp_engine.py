@@ -380,17 +380,21 @@ class MLPGroup:
             # the result slot is taken first: the last epoch's graph publishes into it itself (its
             # last node), so stats_async is then a no-op — no separate launch behind the graph
             k = self._take_slot()
-            for ep in range(epochs):
-                if self.perm_fn is not None:
-                    self.perm.copy_(self.perm_fn(ep))
-                else:
-                    _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
-                t0 = (steps_pe * ep).astype(np.int32)
-                if self.eager:
-                    _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
-                else:
-                    _native.check(fast.mlp_engine_run_epoch_pub(self._engine, t0.ctypes.data, k if ep == epochs - 1 else -1, stream), "run_epoch")
-            _native.check(fast.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
+            try:
+                for ep in range(epochs):
+                    if self.perm_fn is not None:
+                        self.perm.copy_(self.perm_fn(ep))
+                    else:
+                        _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
+                    t0 = (steps_pe * ep).astype(np.int32)
+                    if self.eager:
+                        _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
+                    else:
+                        _native.check(fast.mlp_engine_run_epoch_pub(self._engine, t0.ctypes.data, k if ep == epochs - 1 else -1, stream), "run_epoch")
+                _native.check(fast.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
+            except BaseException:
+                self._slot_free[k].set()  # nothing will fetch this slot: give it back to the ring
+                raise
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=False))
         out = {}
         for slot in batch:
