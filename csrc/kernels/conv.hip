@@ -342,16 +342,16 @@ __device__ __forceinline__ void conv_epilogue_sums(const ConvGemmArgs& a, bf16* 
 }
 
 // one tile's whole epilogue (its sums into accumulator row m0 / 128)
-template <int MODE, int BM, int BN, int NT>
+template <int MODE, int BM, int BN, int NT, int SPEC = -1>
 __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], bf16* lds, int peer, int m0, int n0, int M,
                                               int hw, int rw, int ph, int pw) {
   EpiSums q;
   q.zero();
-  conv_epilogue_tile<MODE, BM, BN, NT>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, rw, ph, pw, q);
-  conv_epilogue_sums<MODE, BN, NT>(a, lds, peer, n0, m0 >> 7, q);
+  conv_epilogue_tile<MODE, BM, BN, NT, 1, SPEC>(a, acc, reinterpret_cast<float*>(lds), peer, m0, n0, M, hw, rw, ph, pw, q);
+  conv_epilogue_sums<MODE, BN, NT, SPEC>(a, lds, peer, n0, m0 >> 7, q);
 }
 
-template <int MODE, int BN, bool PRO>
+template <int MODE, int BN, bool PRO, int SPEC = -1>
 __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
   // MODE 0 forward, MODE 1 dgrad (all taps; MODE 3 = MODE 1 at stride 1), MODE 2 strided dgrad by output parity class,
   // MODE 4 stride-1 dgrad run as a forward conv over dY (pad R-1-pad) with the flipped, transposed
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   }
 
   // ---------------------------------------------------------------- epilogue
-  conv_epilogue<MODE, BM, BN, 256>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw);
+  conv_epilogue<MODE, BM, BN, 256, SPEC>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1640,8 +1640,8 @@ extern "C" int conv_set_dma(int v) {
 // compile-time epilogue operand set of a launch (conv_epilogue_tile SPEC), -1 = runtime flags
 static int conv_spec(const ConvGemmArgs& a, int mode) {
   if (!HALO_SPEC || a.bias != nullptr || a.relu || a.ncol_valid != a.ncol) return -1;
-  if (mode == 0) return (a.resid == nullptr && a.stats != nullptr && a.pro_ss == nullptr) ? 32 : -1;
-  if (a.bnb_part0 == nullptr) return -1;
+  if (mode == 0) return (a.resid == nullptr && a.pro_ss == nullptr) ? (a.stats != nullptr ? 32 : 0) : -1;
+  if (a.bnb_part0 == nullptr) return (a.resid == nullptr && a.stats == nullptr) ? 0 : -1;  // a plain dgrad
   return (a.resid ? 1 : 0) | 2 | (a.bnb_part1 ? 4 : 0) | (a.bnb_mask ? 8 : (a.bnb_mask_ss ? 16 : 0));
 }
 
@@ -1681,8 +1681,10 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     else if (mode == 4 && spec == 18) hipLaunchKernelGGL((k_conv_fwd_halo<4, false, 18>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (mode == 4) hipLaunchKernelGGL((k_conv_fwd_halo<4, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (a.pro_ss != nullptr && spec == 32) hipLaunchKernelGGL((k_conv_fwd_halo<0, true, 32>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (a.pro_ss != nullptr && spec == 0) hipLaunchKernelGGL((k_conv_fwd_halo<0, true, 0>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_fwd_halo<0, true>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else if (spec == 32) hipLaunchKernelGGL((k_conv_fwd_halo<0, false, 32>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
+    else if (spec == 0) hipLaunchKernelGGL((k_conv_fwd_halo<0, false, 0>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     else hipLaunchKernelGGL((k_conv_fwd_halo<0, false>), dim3(G, 1, peers), dim3(512), 0, s, a, tiles_m);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
@@ -1714,11 +1716,12 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     else hipLaunchKernelGGL((k_conv_fwd_dma<0, BM_, BN_, NS_, MB_>), grid, block, 0, s, a, tiles_m, tiles_n);          \
   } while (0)
       // the default wide tile with the layers 2-4 operand sets compiled in (conv_epilogue_tile SPEC):
-      // forward (BN statistics only) and the stride-1 dgrads (conv2: BN1-backward, mask from a1;
+      // forward (BN statistics only; the evaluation's: nothing) and the stride-1 dgrads (conv2: BN1-backward, mask from a1;
       // conv1: skip gradient, previous BN2, mask from the block input; with a projection BN too it
       // spilled 22 VGPRs, so that one keeps the runtime flags)
       const int spec = (mode == 0 || mode == 4) ? conv_spec(a, mode) : -1;
       if (wide && var != 1 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (wide && var != 1 && mode == 0 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 4 && spec == 10) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 10>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 4 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide) {
@@ -1738,7 +1741,7 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
   const int tiles_m = (a.max_batch * rows + 127) / 128;
   const int tiles_n = (a.ncol + (wide ? 127 : 63)) / (wide ? 128 : 64);
   dim3 grid(tiles_m * tiles_n, parity ? 4 : 1, peers), block(256);
-#define CG_LAUNCH(M_, BN_, P_) hipLaunchKernelGGL((k_conv_gemm<M_, BN_, P_>), grid, block, 0, s, a, tiles_m, tiles_n)
+#define CG_LAUNCH(M_, BN_, P_, ...) hipLaunchKernelGGL((k_conv_gemm<M_, BN_, P_, ##__VA_ARGS__>), grid, block, 0, s, a, tiles_m, tiles_n)
   if (mode == 4) {
     if (wide) CG_LAUNCH(4, 128, false);
     else CG_LAUNCH(4, 64, false);
@@ -1749,7 +1752,15 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
     if (wide) CG_LAUNCH(0, 128, false);
     else CG_LAUNCH(0, 64, false);
   } else if (parity) {
-    if (wide) CG_LAUNCH(2, 128, false);
+    // stride-2 dgrads with their operand sets compiled in: the projection's (plain) and the block
+    // conv1's (skip gradient, previous BN2, mask from the block input); 1-4-tap K loops leave the
+    // epilogue the largest part of these kernels
+    const int spec = conv_spec(a, 2);
+    if (wide && spec == 0) CG_LAUNCH(2, 128, false, 0);
+    else if (wide && spec == 11) CG_LAUNCH(2, 128, false, 11);
+    else if (!wide && spec == 0) CG_LAUNCH(2, 64, false, 0);
+    else if (!wide && spec == 11) CG_LAUNCH(2, 64, false, 11);
+    else if (wide) CG_LAUNCH(2, 128, false);
     else CG_LAUNCH(2, 64, false);
   } else if (a.stride == 1) {  // MODE 3: MODE 1 specialised to stride 1 (no divisibility test, no division)
     if (wide) CG_LAUNCH(3, 128, false);
