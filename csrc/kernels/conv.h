@@ -57,6 +57,22 @@ struct ConvGemmArgs {
   // this [sc | sh] (2*ncol floats per peer) — the activation relu(BN(y0)) was never materialised
   // (its consumers read y0 through a BN prologue). Used when bnb_mask is null.
   const float* bnb_mask_ss; int64_t bnb_mask_ss_ps;
+  // fused BatchNorm finalize (optional, fin_cnt != nullptr; conv_fin_tail): the last workgroup of a
+  // peer to finish turns that peer's accumulator rows into the BN constants, in place of a
+  // k_bn_finalize (fin_ss set: `stats` rows, or the running statistics when fin_train is 0) or
+  // k_bn_bwd_finalize (fin_ss null: bnb_part0/1 -> fin_coef0/1 and dgamma/dbeta) launch.
+  // fin_cnt: conv_fin_words() arrival-counter ints per peer, 0 between launches (re-armed in-kernel)
+  int* fin_cnt;
+  const float* fin_gamma0; const float* fin_gamma1; const float* fin_beta;  // [peer * fin_param_ps + c]
+  int64_t fin_param_ps;
+  float* fin_rmean; float* fin_rvar; int64_t fin_run_ps;  // forward: running statistics
+  float* fin_ss; float* fin_ms;                            // forward: [sc | sh], [mean | inv] (2*ncol per peer)
+  float* fin_dgamma0; float* fin_dbeta0; float* fin_dgamma1; float* fin_dbeta1;  // dgrad: flat gradient
+  float* fin_coef0; float* fin_coef1;                      // dgrad: apply coefficients (3*ncol per peer)
+  int fin_C0, fin_C1;                                      // logical channels of BN 0 / 1
+  int fin_train;
+  float fin_eps, fin_momentum;
+  int fin_dbg;  // set by conv_gemm_launch from conv_set_fin_debug (timing probe only; 0 in use)
 };
 
 struct WgradArgs {
@@ -75,6 +91,8 @@ struct WgradArgs {
 
 extern "C" {
 int conv_gemm_launch(int mode, const ConvGemmArgs* a, int peers, void* stream);
+int conv_fin_words(void);
+int conv_set_fin_debug(int bits);
 int conv_set_dma(int on);
 int conv_set_dma_wgs(int n);
 int conv_set_wgrad_halo(int on);

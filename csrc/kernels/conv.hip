@@ -351,6 +351,186 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& a, const f32x4
   conv_epilogue_sums<MODE, BN, NT, SPEC>(a, lds, peer, n0, m0 >> 7, q);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused BatchNorm finalize (ConvGemmArgs::fin_cnt): the work of k_bn_finalize / k_bn_bwd_finalize
+// (cnn_ops.hip) done by the peer's last workgroup to finish, instead of a launch of its own after
+// every BN-producing conv (~40 launches of ~5 us plus their gaps per ResNet-18 step). The epilogue
+// sums are float atomics, which execute at the memory side and leave no L2 copy; every wave waits
+// for its own (vmcnt 0), the workgroup barrier joins them, one lane draws an arrival ticket from
+// the peer's counter (agent-scope atomic) and the workgroup with the last ticket reads the rows
+// back with sc1 loads and re-arms them with sc1 stores (conv_fin_gather): arrival-ticket hand-off,
+// MI355X_MICROARCH.md inter-workgroup visibility, valid-forms row 1. No workgroup waits for another.
+// ------------------------------------------------------------------------------------------------
+// red[j] = sum over the `rows` accumulator rows of base[r * E2 + j] (j < E2, E2 % 4 == 0), every
+// element re-armed to 0. The rows were written only by memory-side float atomics of this launch
+// (no L2 copy anywhere), so 16-byte sc1 loads (L1 bypassed, aux 16) read their final values, and
+// sc1 zero stores (write-through: the line leaves this XCD's L2 as well) re-arm them for the next
+// launch. Each thread sums its chunk column over a row subset in registers (all its loads in
+// flight), the subsets are added in a fixed order. Measured slower forms (profiles/r4u_bn_fin_tail):
+// reading the rows back by atomic exchange (+13-31 us per conv: one CU issuing 16 x 2 x Cp
+// returning atomics), LDS float atomicAdd of the loaded chunks (+12-45 us).
+__device__ __forceinline__ void conv_fin_gather(float* base, int rows, int E2, float* red) {
+  const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
+  const int Q = E2 >> 2;                  // 16-byte chunks per row
+  const int TPC = Q <= NT ? NT / Q : 1;   // threads per chunk column (each sums a row subset)
+  const __amdgpu_buffer_rsrc_t rs = conv_rsrc(base);
+  float* part = red + E2;                 // [TPC][E2] partial column sums, reduced in fixed order
+  constexpr int U = 16;
+  for (int q0 = 0; q0 < Q; q0 += (Q <= NT ? Q : NT)) {
+    const int q = q0 + (Q <= NT ? tid % Q : tid), rr = Q <= NT ? tid / Q : 0;
+    if (q < Q && rr < TPC) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = rr; r < rows; r += U * TPC) {
+        conv_u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int ri = r + u * TPC;
+          v[u] = (conv_u32x4)__builtin_amdgcn_raw_buffer_load_b128(rs, ri < rows ? (ri * Q + q) * 16 : CONV_OOB, 0, 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // out-of-range rows loaded zeros
+          acc[0] += __uint_as_float(v[u].x);
+          acc[1] += __uint_as_float(v[u].y);
+          acc[2] += __uint_as_float(v[u].z);
+          acc[3] += __uint_as_float(v[u].w);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part[rr * E2 + q * 4 + k] = acc[k];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < E2; j += NT) {
+    float t = 0.f;
+    for (int k = 0; k < TPC; ++k) t += part[k * E2 + j];
+    red[j] = t;
+  }
+  const conv_u32x4 z = {0u, 0u, 0u, 0u};
+  for (int e = tid; e < rows * Q; e += NT) __builtin_amdgcn_raw_buffer_store_b128(z, rs, e * 16, 0, 16);
+  __syncthreads();
+}
+
+// The per-channel operands are loaded before the gather (channels tid + k * blockDim.x, k < 4:
+// ncol <= 4 * blockDim.x, checked by conv_gemm_launch), so their latency overlaps it.
+constexpr int FIN_CPT = 4;
+__device__ __forceinline__ void conv_fin_fwd(const ConvGemmArgs& a, int peer, float* red) {
+  const int Cp = a.ncol, NT = (int)blockDim.x, tid = (int)threadIdx.x;
+  const bool train = a.fin_train != 0 && a.stats != nullptr;
+  const int n = (a.nbatch ? a.nbatch[peer] : a.max_batch) * a.out_h * a.out_w;
+  const float cnt = (float)max(1, n);
+  float* ssp = a.fin_ss + peer * 2 * Cp;
+  float* msp = a.fin_ms + peer * 2 * Cp;
+  float* rm = a.fin_rmean + peer * a.fin_run_ps;
+  float* rv = a.fin_rvar + peer * a.fin_run_ps;
+  float g[FIN_CPT], b[FIN_CPT], m0[FIN_CPT], v0[FIN_CPT];
+#pragma unroll
+  for (int k = 0; k < FIN_CPT; ++k) {
+    const int c = tid + k * NT;
+    const bool on = c < a.fin_C0;
+    g[k] = on ? a.fin_gamma0[peer * a.fin_param_ps + c] : 0.f;
+    b[k] = on ? a.fin_beta[peer * a.fin_param_ps + c] : 0.f;
+    m0[k] = on ? rm[c] : 0.f;
+    v0[k] = on ? rv[c] : 1.f;
+  }
+  if (train) conv_fin_gather(a.stats + peer * a.stats_ps, a.stats_rows > 1 ? a.stats_rows : 1, 2 * Cp, red);
+#pragma unroll
+  for (int k = 0; k < FIN_CPT; ++k) {
+    const int c = tid + k * NT;
+    if (c >= Cp) break;
+    if (c >= a.fin_C0) {
+      ssp[c] = 0.f; ssp[Cp + c] = 0.f; msp[c] = 0.f; msp[Cp + c] = 0.f;
+      continue;
+    }
+    float mean = m0[k], var = v0[k];
+    if (train) {
+      mean = red[c] / cnt;
+      var = fmaxf(red[Cp + c] / cnt - mean * mean, 0.f);
+      if (n > 0) {  // a peer without samples this step keeps its running statistics
+        const float unbiased = cnt > 1.f ? var * cnt / (cnt - 1.f) : var;
+        rm[c] = (1.f - a.fin_momentum) * m0[k] + a.fin_momentum * mean;
+        rv[c] = (1.f - a.fin_momentum) * v0[k] + a.fin_momentum * unbiased;
+      }
+    }
+    const float inv = rsqrtf(var + a.fin_eps);
+    ssp[c] = g[k] * inv;
+    ssp[Cp + c] = b[k] - mean * g[k] * inv;
+    msp[c] = mean;
+    msp[Cp + c] = inv;
+  }
+}
+
+__device__ __forceinline__ void conv_fin_bwd(const ConvGemmArgs& a, int peer, float* part, const float* ms, const float* gamma, float* dgamma,
+                                             float* dbeta, float* coef, int C, float* red) {
+  const int Cp = a.ncol, NT = (int)blockDim.x, tid = (int)threadIdx.x;
+  const float cnt = (float)max(1, (a.nbatch ? a.nbatch[peer] : a.max_batch) * a.out_h * a.out_w);
+  float* cp = coef + peer * 3 * Cp;
+  float k1[FIN_CPT], dg[FIN_CPT], db[FIN_CPT];
+#pragma unroll
+  for (int k = 0; k < FIN_CPT; ++k) {
+    const int c = tid + k * NT;
+    const bool on = c < C;
+    k1[k] = on ? gamma[peer * a.fin_param_ps + c] * ms[peer * 2 * Cp + Cp + c] : 0.f;
+    dg[k] = on ? dgamma[peer * a.fin_param_ps + c] : 0.f;
+    db[k] = on ? dbeta[peer * a.fin_param_ps + c] : 0.f;
+  }
+  conv_fin_gather(part + peer * a.bnb_part_ps, a.bnb_rows > 1 ? a.bnb_rows : 1, 2 * Cp, red);
+#pragma unroll
+  for (int k = 0; k < FIN_CPT; ++k) {
+    const int c = tid + k * NT;
+    if (c >= Cp) break;
+    if (c >= C) {
+      cp[c] = 0.f; cp[Cp + c] = 0.f; cp[2 * Cp + c] = 0.f;
+      continue;
+    }
+    const float sg = red[c], sgx = red[Cp + c];
+    dgamma[peer * a.fin_param_ps + c] = dg[k] + sgx;
+    dbeta[peer * a.fin_param_ps + c] = db[k] + sg;
+    cp[c] = k1[k];
+    cp[Cp + c] = sg / cnt;
+    cp[2 * Cp + c] = sgx / cnt;
+  }
+}
+
+// Arrival counters, per peer: one top word and FIN_SHARDS shard words, each on its own 128-byte
+// line. A workgroup draws its ticket from shard (block index % FIN_SHARDS), the last of a shard from
+// the top word. One counter per peer that every workgroup hit cost ~30 us per conv: returning
+// atomics on one line serialize at the memory side (~256 workgroups x 8 peers on one line,
+// profiles/r4u_bn_fin_tail); a shard sees ~1/8 of the arrivals, the top word at most 8.
+constexpr int FIN_LINE = 32, FIN_SHARDS = 8, FIN_WORDS = (FIN_SHARDS + 1) * FIN_LINE;
+
+// every workgroup calls this exactly once, as its last action (early exits included); flag: LDS the
+// workgroup no longer uses (one word + 2 * ncol floats from word 4)
+__device__ __forceinline__ void conv_fin_tail(const ConvGemmArgs& a, int peer, int* flag) {
+  if (a.fin_cnt == nullptr) return;
+  if (!(a.fin_dbg & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's epilogue atomics performed
+  __syncthreads();
+  if (a.fin_dbg & 2) return;
+  if (threadIdx.x == 0) {
+    int* cnt = a.fin_cnt + peer * FIN_WORDS;
+    const int nwg = (int)(gridDim.x * gridDim.y), b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int sh = b % FIN_SHARDS;
+    const int members = nwg / FIN_SHARDS + (sh < nwg % FIN_SHARDS ? 1 : 0);
+    int* sc = cnt + (1 + sh) * FIN_LINE;
+    bool last = false;
+    if (__hip_atomic_fetch_add(sc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(sc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == min(FIN_SHARDS, nwg) - 1;
+      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (*flag == 0 || (a.fin_dbg & 4)) return;
+  float* red = reinterpret_cast<float*>(flag) + 4;  // [2 * ncol] column sums
+  if (a.fin_ss != nullptr) {
+    conv_fin_fwd(a, peer, red);
+  } else {
+    if (a.bnb_part0 != nullptr) conv_fin_bwd(a, peer, a.bnb_part0, a.bnb_ms0, a.fin_gamma0, a.fin_dgamma0, a.fin_dbeta0, a.fin_coef0, a.fin_C0, red);
+    __syncthreads();  // red reused
+    if (a.bnb_part1 != nullptr) conv_fin_bwd(a, peer, a.bnb_part1, a.bnb_ms1, a.fin_gamma1, a.fin_dgamma1, a.fin_dbeta1, a.fin_coef1, a.fin_C1, red);
+  }
+}
+
 template <int MODE, int BN, bool PRO, int SPEC = -1>
 __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_m, int tiles_n) {
   // MODE 0 forward, MODE 1 dgrad (all taps; MODE 3 = MODE 1 at stride 1), MODE 2 strided dgrad by output parity class,
@@ -386,7 +566,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
-  if (m0 >= M) return;  // tile past this peer's batch
+  if (m0 >= M) {  // tile past this peer's batch
+    conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
+    return;
+  }
 
   const bf16* src = a.src + peer * a.src_ps;
   const bf16* wt = a.wt + peer * a.wt_ps;
@@ -599,6 +782,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmArgs a, int tiles_
 
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<MODE, BM, BN, 256, SPEC>(a, acc, lds, peer, m0, n0, M, hw, rw, ph, pw);
+  conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -703,7 +887,10 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
   const int tn = wgid % tiles_n, g0 = wgid / tiles_n;
   const int n0 = tn * BN;
   const int tiles_mp = (M + BM - 1) / BM;  // this peer's M tiles
-  if (g0 >= tiles_mp) return;  // uniform: no tile for this workgroup
+  if (g0 >= tiles_mp) {  // uniform: no tile for this workgroup
+    conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -902,6 +1089,7 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
     }
   }
   conv_epilogue_sums<EMODE, BN, NT, SPEC>(a, lds, peer, n0, MODE == 5 ? g0 * 4 + (int)blockIdx.y : g0, q);
+  conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
 }
 
 
@@ -958,7 +1146,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
   const int tiles_mp = (M + BM - 1) / BM;
   const int G = gridDim.x;
   const int g0 = xcd_remap(blockIdx.x, G);
-  if (g0 >= tiles_mp) return;
+  if (g0 >= tiles_mp) {
+    conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const __amdgpu_buffer_rsrc_t rs_src = conv_rsrc(a.src + peer * a.src_ps), rs_wt = conv_rsrc(a.wt + peer * a.wt_ps);
@@ -1082,6 +1273,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
       cur ^= 1;
     }
     conv_epilogue_sums<MODE, BN, NT, SPEC>(a, pat, peer, 0, g0, q);
+    conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
     return;
   }
   // MODE 0 prefetches the next tile's patch into registers under the MFMAs
@@ -1120,6 +1312,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
     __syncthreads();  // staging read: the next patch may be stored
   }
   conv_epilogue_sums<MODE, BN, NT, SPEC>(a, pat, peer, 0, g0, q);
+  conv_fin_tail(a, peer, reinterpret_cast<int*>(lds));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1645,8 +1838,18 @@ static int conv_spec(const ConvGemmArgs& a, int mode) {
   return (a.resid ? 1 : 0) | 2 | (a.bnb_part1 ? 4 : 0) | (a.bnb_mask ? 8 : (a.bnb_mask_ss ? 16 : 0));
 }
 
+static int g_fin_dbg = 0;
+extern "C" int conv_set_fin_debug(int bits) {
+  const int old = g_fin_dbg;
+  if (bits >= 0) g_fin_dbg = bits;
+  return old;
+}
+
 extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, void* stream) {
-  const ConvGemmArgs& a = *pa;
+  ConvGemmArgs a_ = *pa;
+  a_.fin_dbg = g_fin_dbg;
+  const ConvGemmArgs& a = a_;
+  if (a.fin_cnt != nullptr && a.ncol > FIN_CPT * 256) return 1;  // conv_fin_fwd / _bwd: channels per thread
   // mode 0 forward, 1 dgrad, 4 stride-1 dgrad as a forward conv over dY with k_conv_wt_flip weights
   // (the caller passes the forward-shaped arguments: src = dY, pad = R-1-pad, ncol = cin)
   // mode 5: stride-2 dgrad by parity class as forward convs over dY with conv_wt_flip_parity_launch's
@@ -1861,6 +2064,8 @@ extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) {
 }
 // rows of the BN-backward partial-sum buffers (MYFYP_BNB_ROWS, default 16; conv epilogues and
 // k_bn_bwd_reduce accumulate into them, k_bn_bwd_finalize sums and re-zeroes every row)
+extern "C" int conv_fin_words() { return FIN_WORDS; }  // ints per peer of a ConvGemmArgs::fin_cnt buffer
+
 extern "C" int conv_bnb_rows() {
   static int rows = -1;
   if (rows < 0) {

@@ -53,6 +53,11 @@ class ConvGemmArgs(ctypes.Structure):
         ("bnb_y1", c_void_p), ("bnb_y1_ps", c_int64), ("bnb_ms0", c_void_p), ("bnb_ms1", c_void_p),
         ("bnb_part0", c_void_p), ("bnb_part1", c_void_p), ("bnb_part_ps", c_int64), ("stats_rows", c_int),
         ("bnb_rows", c_int), ("bnb_mask_ss", c_void_p), ("bnb_mask_ss_ps", c_int64),
+        ("fin_cnt", c_void_p), ("fin_gamma0", c_void_p), ("fin_gamma1", c_void_p), ("fin_beta", c_void_p), ("fin_param_ps", c_int64),
+        ("fin_rmean", c_void_p), ("fin_rvar", c_void_p), ("fin_run_ps", c_int64), ("fin_ss", c_void_p), ("fin_ms", c_void_p),
+        ("fin_dgamma0", c_void_p), ("fin_dbeta0", c_void_p), ("fin_dgamma1", c_void_p), ("fin_dbeta1", c_void_p),
+        ("fin_coef0", c_void_p), ("fin_coef1", c_void_p), ("fin_C0", c_int), ("fin_C1", c_int), ("fin_train", c_int),
+        ("fin_eps", c_float), ("fin_momentum", c_float), ("fin_dbg", c_int),
     ]
 
 
@@ -112,6 +117,8 @@ _SIGS = {
     "cnn_bn_bwd_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "cnn_bn_bwd_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "cnn_bn_bwd_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "conv_fin_words": (c_int, []),
+    "conv_set_fin_debug": (c_int, [c_int]),
     "cnn_relu_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_colsum": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "cnn_maxpool2": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
@@ -242,6 +249,13 @@ class CNNGroup:
         # patch staging (one transform per staged pixel, not per tap) and the dgrad's ReLU mask taken
         # from y1 — a1 is never written (MYFYP_CNN_HALO_BN1=0: materialise it as before)
         self.halo_bn1 = os.environ.get("MYFYP_CNN_HALO_BN1", "1") != "0"
+        # BatchNorm finalize (batch statistics -> scale/shift, BN-backward sums -> apply coefficients)
+        # run by the last workgroup of the conv that produced the sums (conv.hip conv_fin_tail)
+        # instead of a k_bn_finalize / k_bn_bwd_finalize launch per BN. Opt-in (MYFYP_CNN_FUSE_FIN=1):
+        # measured neutral on ResNet-18 (2.536 vs 2.542 rounds/s, profiles/r4u_bn_fin_tail) — the
+        # ~40 launches and their gaps go, but the last workgroup's serial chain (store drain, arrival
+        # ticket, row gather, constants) lengthens every BN-producing conv by 2-12 us
+        self.fuse_fin = os.environ.get("MYFYP_CNN_FUSE_FIN", "0") == "1"
         # wgrad split-K target: workgroups per CU over all peers (more splits = more parallelism and
         # more fp32 atomics on the gradient)
         # stride-1 dgrad as a forward conv over dY with flipped weights (conv.hip MODE 4); 0 = MODE 3
@@ -543,13 +557,17 @@ class CNNGroup:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def conv(self, L: ConvL, src: torch.Tensor, out: torch.Tensor, mode: int = 0, bias: bool = False, relu: bool = False, resid=None, stats=None,
-             pro: Optional["BNL"] = None, bnb: Optional[tuple] = None, bnb_mask_bn: Optional["BNL"] = None) -> None:
+             pro: Optional["BNL"] = None, bnb: Optional[tuple] = None, bnb_mask_bn: Optional["BNL"] = None, fin: Optional["BNL"] = None,
+             train: bool = True, bnb_fin: bool = False) -> None:
         """``pro``: src holds that BatchNorm's input y; the conv reads relu(BN(y)) in its prologue.
         ``bnb`` (dgrad): ``(mask, [(bn, y), ...])`` — out is written as the ReLU-masked gradient g and
         the BN-backward sums of each listed BatchNorm (input y) accumulate in the epilogue; follow
         with ``bn_bwd(..., pre_reduced=True)``. ``bnb_mask_bn`` (with a None mask): the ReLU mask is
         relu(BN(y0)) > 0 of that BatchNorm, computed from y0 in the epilogue (the activation was
-        never materialised)."""
+        never materialised). ``fin`` (forward): that BatchNorm's finalize runs in the conv's last
+        workgroup (in place of ``bn_fin``; ``train`` False: from the running statistics).
+        ``bnb_fin`` (dgrad with ``bnb``): the listed BatchNorms' backward finalize runs there too
+        (then ``bn_bwd(..., pre_reduced=True, finalized=True)``)."""
         lib, P = _lib(), self.capacity
         shadow_f = self.shadow_off[L.name]
         a = ConvGemmArgs()
@@ -619,6 +637,28 @@ class CNNGroup:
                 bn1_, y1_ = rest[0]
                 a.bnb_y1, a.bnb_y1_ps, a.bnb_ms1 = y1_.data_ptr(), y1_.shape[1], self.ms(bn1_).data_ptr()
                 a.bnb_part1 = self.fbuf(f"bnsum_{bn1_.name}", nr * 2 * bn1_.Cp).data_ptr()
+            if bnb_fin:
+                gb, pb = self.grad.data_ptr(), self.params.data_ptr()
+                a.fin_cnt = self.ibuf(f"fincnt_b_{L.name}", lib.conv_fin_words()).data_ptr()
+                a.fin_param_ps = self.params.shape[1]
+                assert self.grad.shape[1] == self.params.shape[1]
+                for i, (bn_, _) in enumerate(targets):
+                    w_, b_ = self._off(bn_.module.weight), self._off(bn_.module.bias)
+                    setattr(a, f"fin_gamma{i}", pb + 4 * w_)
+                    setattr(a, f"fin_dgamma{i}", gb + 4 * w_)
+                    setattr(a, f"fin_dbeta{i}", gb + 4 * b_)
+                    setattr(a, f"fin_coef{i}", self.fbuf(f"bncoef_{bn_.name}", 3 * bn_.Cp).data_ptr())
+                    setattr(a, f"fin_C{i}", bn_.C)
+        if fin is not None:
+            assert mode == 0 and fin.Cp == a.ncol
+            base = self.params.data_ptr()
+            ro = self.n_params + self.bn_off[fin.name]
+            a.fin_cnt = self.ibuf(f"fincnt_f_{L.name}", lib.conv_fin_words()).data_ptr()
+            a.fin_gamma0, a.fin_beta = base + 4 * self._off(fin.module.weight), base + 4 * self._off(fin.module.bias)
+            a.fin_param_ps = a.fin_run_ps = self.params.shape[1]
+            a.fin_rmean, a.fin_rvar = base + 4 * ro, base + 4 * (ro + self.bn_total)
+            a.fin_ss, a.fin_ms = self.ss(fin).data_ptr(), self.ms(fin).data_ptr()
+            a.fin_C0, a.fin_train, a.fin_eps, a.fin_momentum = fin.C, int(train), fin.eps, fin.momentum
         _chk(lib.conv_gemm_launch(5 if par_dgrad else (4 if fwd_dgrad else mode), ctypes.byref(a), P, self._stream()), f"conv {L.name} mode {mode}")
 
     def _wgrad_split(self, L: ConvL) -> Tuple[int, int]:
@@ -660,6 +700,15 @@ class CNNGroup:
             base + 4 * self._off(g), base + 4 * self._off(b), self.params.shape[1], base + 4 * ro, base + 4 * (ro + self.bn_total), self.params.shape[1],
             bn.C, bn.Cp, bn.eps, bn.momentum, int(train), self.ss(bn).data_ptr(), self.ms(bn).data_ptr(), P, self._stream()), f"bn_fin {bn.name}")
 
+    def conv_bn(self, L: ConvL, src, out, bn: BNL, st, hw: int, train: bool, **kw) -> None:
+        """Forward conv producing BatchNorm ``bn``'s input, then that BN's finalize: in the conv's
+        last workgroup (``fuse_fin``) or as its own launch."""
+        if self.fuse_fin and self.device.type == "cuda":
+            self.conv(L, src, out, stats=st, fin=bn, train=train, **kw)
+        else:
+            self.conv(L, src, out, stats=st, **kw)
+            self.bn_fin(bn, st, st.shape[1] // (2 * L.cp_out) if st is not None else 0, hw, train)
+
     def _bn1_in_halo(self, c2: "ConvL") -> bool:
         """conv2 of this block takes BN1 + ReLU in its patch staging (k_conv_fwd_halo /
         k_conv_wgrad_halo shapes; the halo kernels must be on)."""
@@ -682,10 +731,12 @@ class CNNGroup:
                             y2.shape[1] if y2 is not None else 0, self.ss(bn2).data_ptr() if bn2 is not None else None, int(relu), self.nb.data_ptr(),
                             self.B * hw, hw, bn.Cp, out.data_ptr(), out.shape[1], P, self._stream()), f"bn_act {bn.name}")
 
-    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None, mask_from_y: bool = False, pre_reduced: bool = False) -> None:
+    def bn_bwd(self, bn: BNL, dz, mask, y, dy_out, hw, gout=None, mask_from_y: bool = False, pre_reduced: bool = False, finalized: bool = False) -> None:
         """``mask_from_y``: the ReLU after this BN was never materialised; its mask is y*sc + sh > 0.
         ``pre_reduced``: dz is already the masked gradient g and its sums were accumulated by the
-        producing dgrad's epilogue (``conv(..., bnb=...)``): only finalize + apply run."""
+        producing dgrad's epilogue (``conv(..., bnb=...)``): only finalize + apply run.
+        ``finalized``: that dgrad's last workgroup also ran the finalize (``conv(..., bnb_fin=True)``):
+        only the apply runs."""
         lib, P = _lib(), self.capacity
         mss = self.ss(bn).data_ptr() if mask_from_y else None
         nblk = max(1, min(128, (self.B * hw + 255) // 256))
@@ -698,10 +749,12 @@ class CNNGroup:
             _chk(lib.cnn_bn_bwd_reduce(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
                                        self.ms(bn).data_ptr(), self.nb.data_ptr(), hw, bn.Cp, part.data_ptr(), part.shape[1], nblk, _p(gout),
                                        gout.shape[1] if gout is not None else 0, P, self._stream(), mss), f"bn_bwd_reduce {bn.name}")
+        assert not finalized or pre_reduced
         gbase = self.grad.data_ptr()
-        _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nr, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
-                                     self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight), gbase + 4 * self._off(bn.module.bias),
-                                     bn.C, bn.Cp, coef.data_ptr(), P, self._stream()), f"bn_bwd_finalize {bn.name}")
+        if not finalized:
+            _chk(lib.cnn_bn_bwd_finalize(part.data_ptr(), part.shape[1], nr, self.nb.data_ptr(), hw, self.params.data_ptr() + 4 * self._off(bn.module.weight),
+                                         self.params.shape[1], self.ms(bn).data_ptr(), gbase + 4 * self._off(bn.module.weight),
+                                         gbase + 4 * self._off(bn.module.bias), bn.C, bn.Cp, coef.data_ptr(), P, self._stream()), f"bn_bwd_finalize {bn.name}")
         _chk(lib.cnn_bn_bwd_apply(dz.data_ptr(), dz.shape[1], _p(mask), mask.shape[1] if mask is not None else 0, y.data_ptr(), y.shape[1],
                                   self.ms(bn).data_ptr(), coef.data_ptr(), self.nb.data_ptr(), self.B * hw, hw, bn.Cp, dy_out.data_ptr(),
                                   dy_out.shape[1], P, self._stream(), mss), f"bn_bwd_apply {bn.name}")
@@ -733,8 +786,7 @@ class CNNGroup:
         hw = L.ho * L.wo
         y = self.act("y_stem", B * hw, L.cp_out)
         st = self.fbuf("st_stem", _lib().conv_gemm_stats_rows(B, L.ho, L.wo) * 2 * L.cp_out) if train else None
-        self.conv(L, x0, y, stats=st)
-        self.bn_fin(bn, st, _lib().conv_gemm_stats_rows(B, L.ho, L.wo), hw, train)
+        self.conv_bn(L, x0, y, bn, st, hw, train)
         a = self.act("a_stem", B * hw, L.cp_out)
         self.bn_act(bn, y, a, hw)
         for bi, (c1, bn1, c2, bn2, proj) in enumerate(self.blocks):
@@ -743,24 +795,21 @@ class CNNGroup:
             rows1 = _lib().conv_gemm_stats_rows(B, c1.ho, c1.wo)
             y1 = self.act(f"y1_{bi}", B * hw1, c1.cp_out)
             st1 = self.fbuf(f"st1_{bi}", rows1 * 2 * c1.cp_out) if train else None
-            self.conv(c1, a_in, y1, stats=st1)
-            self.bn_fin(bn1, st1, rows1, hw1, train)
+            self.conv_bn(c1, a_in, y1, bn1, st1, hw1, train)
             y2 = self.act(f"y2_{bi}", B * hw1, c2.cp_out)
             st2 = self.fbuf(f"st2_{bi}", rows1 * 2 * c2.cp_out) if train else None
             if self.fuse_bn1 or self._bn1_in_halo(c2):  # BN1-apply + ReLU in conv2's operand prologue (a1 never written)
-                self.conv(c2, y1, y2, stats=st2, pro=bn1)
+                self.conv_bn(c2, y1, y2, bn2, st2, hw1, train, pro=bn1)
             else:
                 a1 = self.act(f"a1_{bi}", B * hw1, c1.cp_out)
                 self.bn_act(bn1, y1, a1, hw1)
-                self.conv(c2, a1, y2, stats=st2)
-            self.bn_fin(bn2, st2, rows1, hw1, train)
+                self.conv_bn(c2, a1, y2, bn2, st2, hw1, train)
             a = self.act(f"a2_{bi}", B * hw1, c2.cp_out)
             if proj is not None:
                 cs, bns = proj
                 ys = self.act(f"ys_{bi}", B * hw1, cs.cp_out)
                 sts = self.fbuf(f"sts_{bi}", rows1 * 2 * cs.cp_out) if train else None
-                self.conv(cs, a_in, ys, stats=sts)
-                self.bn_fin(bns, sts, rows1, hw1, train)
+                self.conv_bn(cs, a_in, ys, bns, sts, hw1, train)
                 self.bn_act(bn2, y2, a, hw1, y2=ys, bn2=bns)
             else:
                 self.bn_act(bn2, y2, a, hw1, res=a_in)
@@ -786,6 +835,7 @@ class CNNGroup:
         _chk(lib.cnn_avgpool(1, dpooled.data_ptr(), dpooled.shape[1], self.nb.data_ptr(), B, self.final_hw, fc.cp_in, d.data_ptr(), d.shape[1],
                              self.capacity, self._stream()), "avgpool_bwd")
         fold = self.fold_bnb
+        ff = self.fuse_fin and self.device.type == "cuda"  # pre-reduced BN sums are finalized by their dgrad too
         pre = False  # d is already the masked gradient of this block's output, its BN sums accumulated
         for bi in range(len(self.blocks) - 1, -1, -1):
             c1, bn1, c2, bn2, proj = self.blocks[bi]
@@ -801,15 +851,15 @@ class CNNGroup:
             if proj is not None:
                 cs, bns = proj
                 ys = self.act(f"ys_{bi}", B * hw1, cs.cp_out)
-                self.bn_bwd(bn2, d, mask_out, y2, dy2, hw1, pre_reduced=pre)
+                self.bn_bwd(bn2, d, mask_out, y2, dy2, hw1, pre_reduced=pre, finalized=pre and ff)
                 dys = self.act(f"dys_{bi}", B * hw1, cs.cp_out)
-                self.bn_bwd(bns, d, mask_out, ys, dys, hw1, pre_reduced=pre)
+                self.bn_bwd(bns, d, mask_out, ys, dys, hw1, pre_reduced=pre, finalized=pre and ff)
                 dsc = self.act(f"dsc_{bi}", B * c1.h * c1.w, c1.cp_in)
                 self.conv(cs, dys, dsc, mode=1)
                 self.wgrad(cs, dys, a_in)
                 resid = dsc
             elif pre:
-                self.bn_bwd(bn2, d, None, y2, dy2, hw1, pre_reduced=True)
+                self.bn_bwd(bn2, d, None, y2, dy2, hw1, pre_reduced=True, finalized=ff)
                 resid = d  # already the masked gradient g
             else:
                 g = self.act(f"g_{bi}", B * hw1, c2.cp_out)
@@ -818,17 +868,17 @@ class CNNGroup:
             da1 = self.act(f"da1_{bi}", B * hw1, c1.cp_out)
             dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
             if halo1 and fold:  # a1 never written: mask from y1 in the dgrad epilogue, BN1 in the wgrad staging
-                self.conv(c2, dy2, da1, mode=1, bnb=(None, [(bn1, y1)]), bnb_mask_bn=bn1)
+                self.conv(c2, dy2, da1, mode=1, bnb=(None, [(bn1, y1)]), bnb_mask_bn=bn1, bnb_fin=ff)
                 self.wgrad(c2, dy2, y1, pro=bn1)
-                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True)
+                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True, finalized=ff)
             elif self.fuse_bn1 or halo1:
                 self.conv(c2, dy2, da1, mode=1)
                 self.wgrad(c2, dy2, y1, pro=bn1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, mask_from_y=True)
             elif fold:
-                self.conv(c2, dy2, da1, mode=1, bnb=(a1, [(bn1, y1)]))
+                self.conv(c2, dy2, da1, mode=1, bnb=(a1, [(bn1, y1)]), bnb_fin=ff)
                 self.wgrad(c2, dy2, a1)
-                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True)
+                self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True, finalized=ff)
             else:
                 self.conv(c2, dy2, da1, mode=1)
                 self.wgrad(c2, dy2, a1)
@@ -845,7 +895,7 @@ class CNNGroup:
                 else:
                     st = self.stem
                     bnb = (a_in, [(self.stem_bn, self.act("y_stem", B * st.ho * st.wo, st.cp_out))])
-            self.conv(c1, dy1, d_in, mode=1, resid=resid, bnb=bnb)
+            self.conv(c1, dy1, d_in, mode=1, resid=resid, bnb=bnb, bnb_fin=ff and bnb is not None)
             self.wgrad(c1, dy1, a_in)
             d = d_in
             pre = bnb is not None
@@ -853,7 +903,7 @@ class CNNGroup:
         hw = L.ho * L.wo
         dys = self.act("dy_stem", B * hw, L.cp_out)
         if pre:
-            self.bn_bwd(bn, d, None, self.act("y_stem", B * hw, L.cp_out), dys, hw, pre_reduced=True)
+            self.bn_bwd(bn, d, None, self.act("y_stem", B * hw, L.cp_out), dys, hw, pre_reduced=True, finalized=ff)
         else:
             self.bn_bwd(bn, d, self.act("a_stem", B * hw, L.cp_out), self.act("y_stem", B * hw, L.cp_out), dys, hw)
         self.wgrad(L, dys, self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c)))

@@ -210,7 +210,9 @@ def test_collective_two_processes_gloo(tmp_path):
         "--steps", "2", "--warmup", "1", "--n-train", "2000", "--n-test", "400", "--batch-size", "32",
     ]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
-    assert res.returncode == 0, res.stderr[-3000:]
+    if res.returncode != 0:  # the cause of a rank abort sits above torchrun's own failure report
+        cause = [l for l in res.stderr.splitlines() if any(k in l for k in ("Error", "terminate", "what()", "Traceback", "Fatal"))]
+        raise AssertionError("\n".join(cause[:40]) + "\n----\n" + res.stderr[-3000:])
     line = [l for l in res.stdout.splitlines() if l.startswith("{")][-1]
     import json
 
