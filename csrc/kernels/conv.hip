@@ -143,6 +143,13 @@ struct EpiSums {
 // scale / shift, 5 forward BN statistics; no bias, no ReLU, every column valid) — the runtime-flag epilogue keeps every
 // variant's registers and branches live in the persistent halo dgrad (11.7 VALU per MFMA); -1: flags
 // from the arguments.
+// EPI_PF: with a compile-time operand set that reads residual / mask / y operands (the dgrads), all of
+// this thread's operand chunks of the tile (every slab and pass) are loaded before the staging, in
+// one round trip — the pass loop used to issue them two rows at a time, exposing one HBM round trip
+// per two rows (four per 128 x 128 tile) while every wave of the workgroup waited in the epilogue.
+#ifndef EPI_PF
+#define EPI_PF 1
+#endif
 template <int MODE, int BM, int BN, int NT, int PARTS = 1, int SPEC = -1>
 __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], float* stg, int peer, int m0, int n0, int M,
                                                    int hw, int rw, int ph, int pw, EpiSums& q) {
@@ -212,6 +219,25 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
     const int hh = rem / rw, ww = rem - hh * rw;
     return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
   };
+  constexpr bool PF = EPI_PF && SP && (SPEC & 3) != 0;  // prefetch the operand chunks (see EPI_PF)
+  constexpr int NP = PF ? PARTS * PASSES : 1;
+  uint4 pr[NP], pm[NP], p0[NP], p1[NP];
+  if (PF) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const __amdgpu_buffer_rsrc_t rr_ = conv_rsrc(resid_on ? resid : a.out), rm_ = conv_rsrc(bmask_on ? bmask : a.out);
+    const __amdgpu_buffer_rsrc_t r0_ = conv_rsrc(bnb ? by0 : a.out), r1_ = conv_rsrc(bnb2 ? by1 : a.out);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int m = m0 + (k / PASSES) * SR + rr + (k % PASSES) * RP;
+      // rows past the batch (and a column chunk past ncol) load zeros through the buffer range check
+      const int off = (chok && m < M) ? (int)(((int64_t)out_row(m) * a.ncol + col0) * 2) : CONV_OOB;
+      pr[k] = resid_on ? conv_ld16(rr_, off) : z;
+      pm[k] = bmask_on ? conv_ld16(rm_, off) : z;
+      p0[k] = bnb ? conv_ld16(r0_, off) : z;
+      p1[k] = bnb2 ? conv_ld16(r1_, off) : z;
+    }
+  }
+#pragma unroll
   for (int part = 0; part < PARTS; ++part) {
   if (wr * 64 / SR == part) {  // this wave's rows are in the slab: stage them
 #pragma unroll
@@ -227,17 +253,24 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
   }
   __syncthreads();
   if (chok) {
-#pragma unroll 2
+#pragma unroll PF ? PASSES : 2
     for (int p = 0; p < PASSES; ++p) {
       const int row = rr + p * RP;  // row within the slab
       const int m = m0 + part * SR + row;
       if (m >= M) break;
       const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
       uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
-      if (resid_on) ur = *reinterpret_cast<const uint4*>(resid + o);
-      if (bmask_on) um = *reinterpret_cast<const uint4*>(bmask + o);
-      if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
-      if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
+      if (PF) {
+        ur = pr[PF ? part * PASSES + p : 0];
+        um = pm[PF ? part * PASSES + p : 0];
+        uy0 = p0[PF ? part * PASSES + p : 0];
+        uy1 = p1[PF ? part * PASSES + p : 0];
+      } else {
+        if (resid_on) ur = *reinterpret_cast<const uint4*>(resid + o);
+        if (bmask_on) um = *reinterpret_cast<const uint4*>(bmask + o);
+        if (bnb) uy0 = *reinterpret_cast<const uint4*>(by0 + o);
+        if (bnb2) uy1 = *reinterpret_cast<const uint4*>(by1 + o);
+      }
       const int sw = (((row >> 2) & 3) << 4) ^ ((row & 1) << 2);
       const float4 lo = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8) ^ sw));
       const float4 hi = *reinterpret_cast<const float4*>(cst + row * BN + ((ch * 8 + 4) ^ sw));
