@@ -143,6 +143,52 @@ struct EpiSums {
 // scale / shift, 5 forward BN statistics; no bias, no ReLU, every column valid) — the runtime-flag epilogue keeps every
 // variant's registers and branches live in the persistent halo dgrad (11.7 VALU per MFMA); -1: flags
 // from the arguments.
+// one tile's epilogue operand chunks (residual, ReLU mask, y0, y1), loaded ahead of the apply
+template <int NP>
+struct EpiPre {
+  uint4 r[NP], m[NP], y0[NP], y1[NP];
+};
+template <int BM, int BN, int NT, int PARTS>
+constexpr int epi_np() { return PARTS * ((BM / PARTS) / (NT / (BN / 8))); }
+
+// output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
+template <int MODE>
+__device__ __forceinline__ int conv_out_row(const ConvGemmArgs& a, int m, int hw, int rw, int ph, int pw) {
+  if (MODE != 2) return m;
+  const int img = m / hw, rem = m - img * hw;
+  const int hh = rem / rw, ww = rem - hh * rw;
+  return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
+}
+
+// the loads of conv_epilogue_tile's operand chunks for a compile-time operand set (SPEC >= 0), in the
+// order its passes consume them; rows past the batch (and a column chunk past ncol) load zeros
+// through the buffer range check
+template <int MODE, int BM, int BN, int NT, int PARTS, int SPEC>
+__device__ __forceinline__ void conv_epilogue_prefetch(const ConvGemmArgs& a, int peer, int m0, int n0, int M, int hw, int rw, int ph, int pw,
+                                                       EpiPre<epi_np<BM, BN, NT, PARTS>()>& pre) {
+  static_assert(SPEC >= 0, "compile-time operand sets only");
+  constexpr int CH = BN / 8, RP = NT / CH, SR = BM / PARTS, PASSES = SR / RP, NP = PARTS * PASSES;
+  constexpr bool resid_on = (SPEC & 1) != 0, bnb = MODE != 0 && (SPEC & 2) != 0;
+  constexpr bool bnb2 = bnb && (SPEC & 4) != 0, bmask_on = bnb && (SPEC & 8) != 0;
+  const int tid = threadIdx.x, ch = tid % CH, rr = tid / CH;
+  const int col0 = n0 + ch * 8;
+  const bool chok = col0 < a.ncol;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const __amdgpu_buffer_rsrc_t rr_ = conv_rsrc(resid_on ? a.resid + peer * a.resid_ps : a.out);
+  const __amdgpu_buffer_rsrc_t rm_ = conv_rsrc(bmask_on ? a.bnb_mask + peer * a.bnb_mask_ps : a.out);
+  const __amdgpu_buffer_rsrc_t r0_ = conv_rsrc(bnb ? a.bnb_y0 + peer * a.bnb_y0_ps : a.out);
+  const __amdgpu_buffer_rsrc_t r1_ = conv_rsrc(bnb2 ? a.bnb_y1 + peer * a.bnb_y1_ps : a.out);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int m = m0 + (k / PASSES) * SR + rr + (k % PASSES) * RP;
+    const int off = (chok && m < M) ? (int)(((int64_t)conv_out_row<MODE>(a, m, hw, rw, ph, pw) * a.ncol + col0) * 2) : CONV_OOB;
+    pre.r[k] = resid_on ? conv_ld16(rr_, off) : z;
+    pre.m[k] = bmask_on ? conv_ld16(rm_, off) : z;
+    pre.y0[k] = bnb ? conv_ld16(r0_, off) : z;
+    pre.y1[k] = bnb2 ? conv_ld16(r1_, off) : z;
+  }
+}
+
 // EPI_PF: with a compile-time operand set that reads residual / mask / y operands (the dgrads), all of
 // this thread's operand chunks of the tile (every slab and pass) are loaded before the staging, in
 // one round trip — the pass loop used to issue them two rows at a time, exposing one HBM round trip
@@ -150,9 +196,12 @@ struct EpiSums {
 #ifndef EPI_PF
 #define EPI_PF 1
 #endif
+// ext: the operand chunks already loaded by the caller (conv_epilogue_prefetch, issued before the
+// tile's MFMAs), or null
 template <int MODE, int BM, int BN, int NT, int PARTS = 1, int SPEC = -1>
 __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const f32x4 (&acc)[4][BN / 32], float* stg, int peer, int m0, int n0, int M,
-                                                   int hw, int rw, int ph, int pw, EpiSums& q) {
+                                                   int hw, int rw, int ph, int pw, EpiSums& q,
+                                                   const EpiPre<epi_np<BM, BN, NT, PARTS>()>* ext = nullptr) {
   constexpr bool SP = SPEC >= 0;
   constexpr int NF = BN / 32;
   constexpr int SR = BM / PARTS;  // staged rows per round (a multiple of the 64 rows of a wave)
@@ -212,31 +261,11 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       }
     }
   }
-  // output row of GEMM row m (MODE 2: back from the class sub-grid to the dX pixel)
-  auto out_row = [&](int m) -> int {
-    if (MODE != 2) return m;
-    const int img = m / hw, rem = m - img * hw;
-    const int hh = rem / rw, ww = rem - hh * rw;
-    return (img * a.out_h + 2 * hh + ph) * a.out_w + 2 * ww + pw;
-  };
+  auto out_row = [&](int m) -> int { return conv_out_row<MODE>(a, m, hw, rw, ph, pw); };
   constexpr bool PF = EPI_PF && SP && (SPEC & 3) != 0;  // prefetch the operand chunks (see EPI_PF)
-  constexpr int NP = PF ? PARTS * PASSES : 1;
-  uint4 pr[NP], pm[NP], p0[NP], p1[NP];
-  if (PF) {
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    const __amdgpu_buffer_rsrc_t rr_ = conv_rsrc(resid_on ? resid : a.out), rm_ = conv_rsrc(bmask_on ? bmask : a.out);
-    const __amdgpu_buffer_rsrc_t r0_ = conv_rsrc(bnb ? by0 : a.out), r1_ = conv_rsrc(bnb2 ? by1 : a.out);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int m = m0 + (k / PASSES) * SR + rr + (k % PASSES) * RP;
-      // rows past the batch (and a column chunk past ncol) load zeros through the buffer range check
-      const int off = (chok && m < M) ? (int)(((int64_t)out_row(m) * a.ncol + col0) * 2) : CONV_OOB;
-      pr[k] = resid_on ? conv_ld16(rr_, off) : z;
-      pm[k] = bmask_on ? conv_ld16(rm_, off) : z;
-      p0[k] = bnb ? conv_ld16(r0_, off) : z;
-      p1[k] = bnb2 ? conv_ld16(r1_, off) : z;
-    }
-  }
+  EpiPre<epi_np<BM, BN, NT, PARTS>()> own;
+  if (PF && ext == nullptr) conv_epilogue_prefetch<MODE, BM, BN, NT, PARTS, SP ? SPEC : 0>(a, peer, m0, n0, M, hw, rw, ph, pw, own);
+  const EpiPre<epi_np<BM, BN, NT, PARTS>()>& pre = ext != nullptr ? *ext : own;
 #pragma unroll
   for (int part = 0; part < PARTS; ++part) {
   if (wr * 64 / SR == part) {  // this wave's rows are in the slab: stage them
@@ -261,10 +290,10 @@ __device__ __forceinline__ void conv_epilogue_tile(const ConvGemmArgs& a, const 
       const int64_t o = (int64_t)out_row(m) * a.ncol + col0;
       uint4 ur = make_uint4(0, 0, 0, 0), um = ur, uy0 = ur, uy1 = ur;
       if (PF) {
-        ur = pr[PF ? part * PASSES + p : 0];
-        um = pm[PF ? part * PASSES + p : 0];
-        uy0 = p0[PF ? part * PASSES + p : 0];
-        uy1 = p1[PF ? part * PASSES + p : 0];
+        ur = pre.r[part * PASSES + p];
+        um = pre.m[part * PASSES + p];
+        uy0 = pre.y0[part * PASSES + p];
+        uy1 = pre.y1[part * PASSES + p];
       } else {
         if (resid_on) ur = *reinterpret_cast<const uint4*>(resid + o);
         if (bmask_on) um = *reinterpret_cast<const uint4*>(bmask + o);
@@ -1151,6 +1180,12 @@ __global__ __launch_bounds__(2 * BM, MINB) void k_conv_fwd_dma(ConvGemmArgs a, i
 #ifndef HALO_DMA4
 #define HALO_DMA4 1
 #endif
+// EPI_PF_HALO=1: the halo dgrads load their epilogue operands before the tile's MFMAs instead of at
+// the start of the epilogue. The kernels get faster (177 / 174 -> 168 / 163 us) but ResNet-18 does
+// not (2.594 / 2.585 vs 2.607 / 2.608 rounds/s, same box, profiles/r4x_halo_prefetch): off
+#ifndef EPI_PF_HALO
+#define EPI_PF_HALO 0
+#endif
 #ifndef HALO_SPEC  // the layer-1 dgrads with compile-time epilogue operand sets (conv_epilogue_tile SPEC)
 #define HALO_SPEC 1
 #endif
@@ -1269,6 +1304,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
       bf16* pc = pat + cur * PEP;
       wait_vmcnt<0>();
       __syncthreads();  // every wave's patch DMA landed (and the weights, the first time); the other buffer is free
+      // the dgrad epilogue's operand chunks of this tile, in flight under its MFMAs (issued before the
+      // next patch's DMA, so the epilogue's wait for them does not wait for that DMA)
+      EpiPre<epi_np<BM, BN, NT, 2>()> epre;
+      constexpr bool HPF = EPI_PF_HALO && EPI_PF && SPEC >= 0 && (SPEC & 3) != 0;
+      if (HPF) conv_epilogue_prefetch<MODE, BM, BN, NT, 2, HPF ? SPEC : 0>(a, peer, tm * BM, 0, M, HW, W, 0, 0, epre);
       if (tm + G < tiles_mp) dma_patch(tm + G, pat + (cur ^ 1) * PEP);  // lands under this tile's MFMAs + epilogue
       f32x4 acc[4][2];
 #pragma unroll
@@ -1302,7 +1342,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_fwd_halo(ConvGemmArgs a, int ti
         }
       }
       __syncthreads();  // patch reads done: the epilogue stages over it, two 128-row slabs
-      conv_epilogue_tile<MODE, BM, BN, NT, 2, SPEC>(a, acc, reinterpret_cast<float*>(pc), peer, tm * BM, 0, M, HW, W, 0, 0, q);
+      conv_epilogue_tile<MODE, BM, BN, NT, 2, SPEC>(a, acc, reinterpret_cast<float*>(pc), peer, tm * BM, 0, M, HW, W, 0, 0, q, HPF ? &epre : nullptr);
       cur ^= 1;
     }
     conv_epilogue_sums<MODE, BN, NT, SPEC>(a, pat, peer, 0, g0, q);
