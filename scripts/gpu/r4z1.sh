@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 final verification, part 1: the whole GPU test suite and smoke() on the committed tree
 set -o pipefail
-O=gpurun_out/r4z; mkdir -p $O
+O=${OUT:-gpurun_out/r4z}; mkdir -p $O
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 final verification, part 2: headline bench and BASELINE configs 3-5 on the committed tree
 set -o pipefail
-O=gpurun_out/r4z; mkdir -p $O
+O=${OUT:-gpurun_out/r4z}; mkdir -p $O
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 run() { local n=$1 s=$2; shift 2; timeout -k 10 $s "$@" > $O/$n.log 2>&1; local rc=$?; echo "== $n rc=$rc"; tail -1 $O/$n.log | cut -c1-400; case $rc in 0) ;; *) exit $rc;; esac; }
