@@ -1995,8 +1995,14 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
       // forward (BN statistics only; the evaluation's: nothing) and the stride-1 dgrads (conv2: BN1-backward, mask from a1;
       // conv1: skip gradient, previous BN2, mask from the block input; with a projection BN too it
       // spilled 22 VGPRs, so that one keeps the runtime flags)
-      const int spec = (mode == 0 || mode == 4) ? conv_spec(a, mode) : -1;
-      if (wide && var != 1 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
+      const int spec = conv_spec(a, mode);
+      // MODE 5 (stride-2 dgrad by parity class): the projection's plain dgrad and the block conv1's
+      // (skip gradient, previous BN2, mask from the block input), both tile widths
+      if (mode == 5 && wide && var != 1 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 128, 2, 2, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (mode == 5 && wide && var != 1 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 128, 2, 2, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (mode == 5 && !wide && var == 2 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 64, 2, 3, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (mode == 5 && !wide && var == 2 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 64, 2, 3, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (wide && var != 1 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 0 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 4 && spec == 10) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 10>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 4 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 11>), grid, block, 0, s, a, tiles_m, tiles_n);

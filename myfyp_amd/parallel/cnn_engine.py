@@ -577,7 +577,8 @@ class CNNGroup:
         # stride-2 dgrad by parity class, each class a forward conv over dY with its flipped taps
         # (conv.hip MODE 5, LDS-DMA kernel only). Opt-in (MYFYP_CNN_S2_FWD=1): measured neutral — the
         # classes' K loops are 1-4 taps long, and the flip costs more than the gather it saves
-        # (stride-2 dgrads 21.7 vs 20.3-22.1 ms per profiled run, profiles/r3z_conv_dma)
+        # (stride-2 dgrads 21.7 vs 20.3-22.1 ms per profiled run, profiles/r3z_conv_dma); with the
+        # compile-time epilogues on both paths still 0.9 % slower (profiles/r4y_s2_parity_spec)
         par_dgrad = mode == 1 and L.stride == 2 and L.colmap is None and self.dgrad_fwd and self.s2_fwd and lib.conv_set_dma(-1) != 0
         if par_dgrad:
             wt = self.shadow_t.data_ptr() + 2 * shadow_f
