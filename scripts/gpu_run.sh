@@ -164,7 +164,7 @@ for step in "$@"; do
     cnn_round_prof)  # kernel trace of full-size config-4 rounds (round boundary: evaluation, FedAvg, host gaps)
       run cnn_round_prof 400 rocprofv3 --kernel-trace -d "$O/cnn_round_prof" -o run -- python3 benchmarks/bench_cnn.py --model resnet18 --rounds 2 --warmup 1 ;;
     rehearsal)
-      for n in 2 4; do
+      for n in ${REHEARSAL_NS:-2 4}; do
         MYFYP_DIST_BACKEND=gloo run rehearsal_gloo_n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
           --master-addr 127.0.0.1 --master-port 2970$n bench.py --gpus $n --steps 10 --warmup 2
       done ;;
