@@ -2002,6 +2002,9 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
       else if (mode == 5 && wide && var != 1 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 128, 2, 2, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (mode == 5 && !wide && var == 2 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 64, 2, 3, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (mode == 5 && !wide && var == 2 && spec == 11) hipLaunchKernelGGL((k_conv_fwd_dma<5, 128, 64, 2, 3, 11>), grid, block, 0, s, a, tiles_m, tiles_n);
+      // the 64-column tile (the stem: K = 72, so the epilogue is most of the kernel) likewise
+      else if (!wide && var == 2 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 64, 2, 3, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
+      else if (!wide && var == 2 && mode == 0 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 64, 2, 3, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 0 && spec == 32) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 32>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 0 && spec == 0) hipLaunchKernelGGL((k_conv_fwd_dma<0, 128, 128, 2, 2, 0>), grid, block, 0, s, a, tiles_m, tiles_n);
       else if (wide && var != 1 && mode == 4 && spec == 10) hipLaunchKernelGGL((k_conv_fwd_dma<4, 128, 128, 2, 2, 10>), grid, block, 0, s, a, tiles_m, tiles_n);
