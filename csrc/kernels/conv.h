@@ -92,6 +92,7 @@ struct WgradArgs {
 extern "C" {
 int conv_gemm_launch(int mode, const ConvGemmArgs* a, int peers, void* stream);
 int conv_fin_words(void);
+int conv_args_abi(long long* out);
 int conv_set_fin_debug(int bits);
 int conv_set_dma(int on);
 int conv_set_dma_wgs(int n);

@@ -23,6 +23,8 @@
 //   maps it to torch order through LDS (a torch-order scatter here cost ~0.45 ms per layer).
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "conv.h"
 
 #include <cstdlib>
@@ -2146,7 +2148,16 @@ extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) {
 }
 // rows of the BN-backward partial-sum buffers (MYFYP_BNB_ROWS, default 16; conv epilogues and
 // k_bn_bwd_reduce accumulate into them, k_bn_bwd_finalize sums and re-zeroes every row)
-extern "C" int conv_fin_words() { return FIN_WORDS; }  // ints per peer of a ConvGemmArgs::fin_cnt buffer
+extern "C" int conv_fin_words() { return FIN_WORDS; }
+// layout of the argument structs the Python side mirrors with ctypes (checked when it loads the
+// library): size and offset of the last field of ConvGemmArgs, then of WgradArgs
+extern "C" int conv_args_abi(long long* out) {
+  out[0] = (long long)sizeof(ConvGemmArgs);
+  out[1] = (long long)offsetof(ConvGemmArgs, fin_dbg);
+  out[2] = (long long)sizeof(WgradArgs);
+  out[3] = (long long)offsetof(WgradArgs, pro_ss_ps);
+  return 4;
+}  // ints per peer of a ConvGemmArgs::fin_cnt buffer
 
 extern "C" int conv_bnb_rows() {
   static int rows = -1;

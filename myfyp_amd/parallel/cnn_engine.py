@@ -118,6 +118,7 @@ _SIGS = {
     "cnn_bn_bwd_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "cnn_bn_bwd_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "conv_fin_words": (c_int, []),
+    "conv_args_abi": (c_int, [c_void_p]),
     "conv_set_fin_debug": (c_int, [c_int]),
     "cnn_relu_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_colsum": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_int, c_void_p]),
@@ -143,6 +144,11 @@ def _lib():
             raise RuntimeError("Segment layout mismatch between Python and the native library")
         if lib.lenet_args_size() != ctypes.sizeof(LenetArgs):
             raise RuntimeError("LenetArgs layout mismatch between Python and the native library")
+        abi = (ctypes.c_longlong * 4)()
+        lib.conv_args_abi(abi)
+        want = (ctypes.sizeof(ConvGemmArgs), ConvGemmArgs.fin_dbg.offset, ctypes.sizeof(WgradArgs), WgradArgs.pro_ss_ps.offset)
+        if tuple(abi) != want:
+            raise RuntimeError(f"ConvGemmArgs / WgradArgs layout mismatch between Python and the native library: {tuple(abi)} vs {want}")
         lib._cnn_sigs = True
     return lib
 

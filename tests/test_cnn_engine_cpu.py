@@ -57,3 +57,21 @@ def test_handle_views_params_and_bn_buffers():
     np.testing.assert_array_equal(h.flat_params().shape, (g.n_params,))
     g.detach(h.slot)
     assert h.slot not in g.handles
+
+
+def test_native_struct_layouts_match_ctypes_mirrors():
+    """The kernel argument structs (ConvGemmArgs, WgradArgs, LenetArgs, Segment) have the same size and
+    field offsets in the native library as in their ctypes mirrors: _lib() checks them when it binds
+    the library (a mismatch would hand every conv kernel shifted arguments). The library loads
+    without a GPU."""
+    from myfyp_amd.ops import _native
+
+    try:
+        _native.load(required=True)
+    except Exception as e:  # not built in this checkout
+        pytest.skip(f"native library not built: {e}")
+    from myfyp_amd.parallel.cnn_engine import _lib
+
+    lib = _lib()
+    assert lib.conv_fin_words() > 0
+
