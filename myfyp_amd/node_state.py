@@ -85,7 +85,16 @@ class NodeState:
         self.votes_event.set()
         self.aggregated_model_event.set()
         self.notify_status()
+        init_lock = self.model_initialized_lock
         type(self).__init__(self, self.addr, self.simulation)
+        # a StartLearningStage still waiting for the initial model holds on to the OLD lock: release
+        # it so that stage wakes, sees the cleared round and ends the workflow (a stop that arrived
+        # before the initial model otherwise left it blocked for good)
+        if init_lock.locked():
+            try:
+                init_lock.release()
+            except RuntimeError:
+                pass
 
     def __str__(self) -> str:
         return (

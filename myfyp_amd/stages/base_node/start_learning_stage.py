@@ -29,6 +29,9 @@ class StartLearningStage(Stage):
         begin = time.time()
         logger.info(state.addr, "⏳ Waiting initialization.")
         state.model_initialized_lock.acquire()
+        if state.round is None:  # learning stopped while waiting for the initial model (NodeState.clear)
+            logger.info(state.addr, "Learning stopped before the model was initialized.")
+            return None
         communication_protocol.broadcast(communication_protocol.build_msg(ModelInitializedCommand.get_name()))
         logger.info(state.addr, "🗣️ Gossiping model initialization.")
         StartLearningStage._gossip_model(state, communication_protocol, learner)
