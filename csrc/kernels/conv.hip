@@ -2135,18 +2135,21 @@ extern "C" int conv_wt_flip_parity_launch(const void* wf, long long wf_ps, void*
 }
 
 // rows of the BN statistics buffer a conv epilogue writes: one (sum, sumsq) accumulator row
-// (MYFYP_BN_STAT_ROWS, default 16: the 64-channel forward convs were bound by 1024 workgroups per
-// peer adding into the same 128 addresses — 144 -> 122 us per conv with 16 rows, profiles/r3z_conv_dma)
+// (MYFYP_BN_STAT_ROWS). Round 3 set 16: the 64-channel forward convs were then bound by 1024
+// workgroups per peer adding into the same 128 addresses (144 -> 122 us per conv with 16 rows,
+// profiles/r3z_conv_dma). The persistent convs now add once per workgroup, and a sweep of the
+// row counts of both buffers on the round-4 tree put 4 ahead: ResNet-18 2.689 (4) / 2.681 (8) /
+// 2.675 (16) / 2.684 (2) / 2.683 (1) rounds/s, 3 alternations each (profiles/r4sw_bn_rows)
 extern "C" int conv_gemm_stats_rows(int max_batch, int out_h, int out_w) {
   static int rows = -1;
   if (rows < 0) {
     const char* e = getenv("MYFYP_BN_STAT_ROWS");
-    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 16;
+    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 4;
   }
   const int tiles = (max_batch * out_h * out_w + 127) / 128;
   return rows < tiles ? rows : (tiles > 0 ? tiles : 1);
 }
-// rows of the BN-backward partial-sum buffers (MYFYP_BNB_ROWS, default 16; conv epilogues and
+// rows of the BN-backward partial-sum buffers (MYFYP_BNB_ROWS, default 4 — see above; conv epilogues and
 // k_bn_bwd_reduce accumulate into them, k_bn_bwd_finalize sums and re-zeroes every row)
 extern "C" int conv_fin_words() { return FIN_WORDS; }
 // layout of the argument structs the Python side mirrors with ctypes (checked when it loads the
@@ -2163,7 +2166,7 @@ extern "C" int conv_bnb_rows() {
   static int rows = -1;
   if (rows < 0) {
     const char* e = getenv("MYFYP_BNB_ROWS");
-    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 16;
+    rows = e != nullptr && atoi(e) >= 1 ? atoi(e) : 4;
   }
   return rows;
 }
