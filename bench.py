@@ -62,11 +62,69 @@ def parse() -> argparse.Namespace:
                     help="one GPU: run FedAvg through a world-size-1 RCCL group (the multi-rank path: side-stream reduce -> RCCL all-reduce -> apply)")
     ap.add_argument("--no-failover", action="store_true", help="skip the per-round confirmation of the weight collectives (fault tolerance off)")
     ap.add_argument("--no-prewarm", action="store_true", help="do not prepare the fused engine at Node.start (round 0 captures the epoch graph)")
+    ap.add_argument("--launch", choices=["auto", "mesh", "ranks"], default="auto",
+                    help="mesh: ONE process drives the N GPUs (in-process RCCL mesh, ncclCommInitAll; under torchrun rank 0 "
+                         "drives them and the other ranks wait); ranks: one process per GPU (torchrun). auto = mesh")
+    ap.add_argument("--mesh-virtual", action="store_true",
+                    help="rehearsal: N mesh ranks on the visible device(s) with host-side collectives (n_gpus reports the physical count)")
     return ap.parse_args()
+
+
+def _env_world() -> tuple:
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+
+
+def plan_launch(args) -> str:
+    """Decide the process model BEFORE anything touches a GPU: "single" (one GPU), "mesh" (this
+    process drives --gpus devices), "park" (a torchrun rank other than 0 in mesh mode: it waits for
+    rank 0 and exits) or "ranks" (one process per GPU). Exits non-zero when the N GPUs asked for
+    cannot be used, so a run never reports fewer GPUs than requested."""
+    import torch
+
+    world, rank = _env_world()
+    if args.launch == "ranks":
+        if args.gpus != world:
+            raise SystemExit(f"bench: --launch ranks needs one process per GPU: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return "ranks" if world > 1 else "single"
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"bench: launched with {world} ranks but --gpus {args.gpus}")
+    if args.gpus <= 1:
+        return "single"
+    if world > 1 and args.launch == "auto" and torch.cuda.device_count() == 0:
+        return "ranks"  # CPU host under torchrun (gloo rehearsal): one process per rank
+    if world > 1 and rank != 0:
+        return "park"
+    have = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if args.gpus > have and not args.mesh_virtual:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {have} GPU(s) visible (use --mesh-virtual for a one-device rehearsal)")
+    return "mesh"
+
+
+def park(args) -> None:
+    """torchrun rank > 0 in mesh mode: rank 0 drives every GPU; wait for it on a CPU-only group."""
+    import datetime
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main() -> None:
     args = parse()
+    mode = plan_launch(args)
+    if mode == "park":
+        park(args)
+        return
+    world_env, _ = _env_world()
+    parked_group = mode == "mesh" and world_env > 1
+    if parked_group:  # rank 0 of a torchrun job in mesh mode: release the waiting ranks at the end
+        import datetime
+
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
     import numpy as np
     import torch
 
@@ -99,11 +157,20 @@ def main() -> None:
     Settings.COLLECTIVE_FAILOVER = not args.no_failover
     Settings.ENGINE_PREWARM = not args.no_prewarm
 
-    fed = Federation.init()
+    if mode == "mesh":
+        Settings.MESH_VIRTUAL = bool(args.mesh_virtual)
+        fed = Federation.init(devices=args.gpus)
+        if fed.mesh is None or fed.mesh_size != args.gpus:
+            raise SystemExit(f"bench: device mesh of {args.gpus} not formed (got {fed.mesh_size})")
+        mesh_devs = list(fed.devices)
+    else:
+        fed = Federation.init()
+        mesh_devs = [fed.device]
     world, rank = fed.world, fed.rank
-    if args.peers % world:
-        raise SystemExit(f"--peers {args.peers} must be divisible by the number of ranks {world}")
-    ppr = args.peers // world
+    n_units = fed.mesh_size if fed.mesh is not None else world
+    if args.peers % n_units:
+        raise SystemExit(f"--peers {args.peers} must be divisible by the number of GPUs {n_units}")
+    ppr = args.peers // world  # peers hosted by this process (all of them in mesh mode)
     data = synthetic_mnist(args.n_train, args.n_test, seed=2024, similarity=args.similarity, noise=args.noise)
     parts = data.generate_partitions(args.peers, RandomIIDPartitionStrategy)
     gids = [rank * ppr + j for j in range(ppr)]
@@ -126,7 +193,11 @@ def main() -> None:
     total_rounds = args.warmup + args.steps
     marks: dict = {}
     round_end: dict = {}
-    dev_sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    cuda_devs = sorted({d.index for d in mesh_devs if d.type == "cuda"})
+
+    def dev_sync() -> None:  # every device this process drives
+        for i in cuda_devs:
+            torch.cuda.synchronize(i)
 
     def hook(r: int, f) -> None:
         if r == args.warmup - 1 or (args.warmup == 0 and r == -1):
@@ -205,6 +276,12 @@ def main() -> None:
 
     rps = args.steps / elapsed if elapsed == elapsed and elapsed > 0 else 0.0
     coll = "none (one rank: local weighted-mean kernel)"
+    n_phys = len(cuda_devs) if cuda_devs else 0
+    if fed.mesh is not None:
+        coll = (f"in-process {fed.mesh.kind} mesh over {fed.mesh_size} devices (one process; per device reduce -> grouped all-reduce -> apply)"
+                + (" [virtual: members share one device]" if args.mesh_virtual else ""))
+        if fed.mesh.kind == "rccl":
+            coll = f"rccl mesh: ncclCommInitAll over {fed.mesh_size} GPUs in one process; per GPU reduce -> grouped ncclAllReduce -> apply"
     if fed.collective:
         import torch.distributed as dist
 
@@ -215,7 +292,7 @@ def main() -> None:
             "metric": METRIC,
             "value": round(rps, 3),
             "unit": "rounds/s",
-            "n_gpus": world,
+            "n_gpus": n_phys if fed.mesh is not None else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed / max(1, args.steps), 3),
@@ -229,9 +306,11 @@ def main() -> None:
                 "global_batch": args.batch_size * args.peers,
                 "local_batch": args.batch_size,
                 "seq_len": None,
-                "parallelism": f"fedavg-{args.peers}peers-dp{world}",
+                "parallelism": f"fedavg-{args.peers}peers-dp{n_units}" + ("-mesh" if fed.mesh is not None else ""),
                 "peers": args.peers,
-                "peers_per_gpu": ppr,
+                "peers_per_gpu": args.peers // n_units,
+                "launch": ("one process drives all GPUs (device mesh)" + (" ; torchrun ranks > 0 idle" if parked_group else "")) if fed.mesh is not None
+                else ("one process per GPU" if world > 1 else "single process, one GPU"),
                 "train_set_size": args.peers,
                 "epochs_per_round": args.epochs,
                 "optimizer": "adam lr=1e-3 (fresh per round)",
@@ -253,6 +332,11 @@ def main() -> None:
         }
         print(json.dumps(out), flush=True)
     fed.shutdown()
+    if parked_group:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,347 @@
+// In-process RCCL device mesh: one process drives G MI355X devices.
+//
+// The reference keeps every peer of a simulation in ONE process and moves models between them with
+// direct method calls (p2pfl/communication/protocols/memory/server_singleton.py:22-43,
+// memory_client.py:139). The MI355X equivalent keeps that process model: peers are placed
+// round-robin over the G devices, and the weights plane is a set of G RCCL communicators created
+// together by ncclCommInitAll. Every collective is issued from ONE host thread for all G devices
+// inside ncclGroupStart/End (the single-thread multi-device pattern RCCL requires), on each
+// device's compute stream, so the round's device work stays stream-ordered and the host never
+// waits:
+//
+//   rmesh_allreduce / rmesh_broadcast / rmesh_allgather / rmesh_p2p — grouped collectives over
+//   the mesh (p2p = the NeighborAvg topology exchange);
+//   rmesh_fedavg — the whole FedAvg of G stacked engine groups: per device the weighted partial
+//   sum of its rows (k_fedavg_reduce, weights as kernel arguments) → ONE grouped all-reduce of
+//   [Σ w x | Σ w] over xGMI → per device the apply kernel writing the mean into its live rows;
+//   rmesh_check / rmesh_abort / rmesh_shrink — failure handling: poll ncclCommGetAsyncError,
+//   ncclCommAbort every communicator (local: ends kernels stuck on a dead peer), and rebuild the
+//   mesh over the surviving devices with a fresh ncclCommInitAll.
+//
+// Every entry point returns 0 on success, non-zero on failure (message via rmesh_last_error()).
+// The current HIP device of the calling thread is restored on return.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../kernels/fl_ops.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Mesh {
+  std::vector<int> devs;          // HIP device ordinal per mesh rank
+  std::vector<ncclComm_t> comms;  // one communicator per device (rank i <-> devs[i])
+  bool aborted = false;
+};
+
+struct DeviceGuard {  // restores the caller's current device
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+bool nccl_ok(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess || r == ncclInProgress) return true;
+  g_err = std::string(what) + ": " + ncclGetErrorString(r);
+  return false;
+}
+
+bool hip_ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+bool dtype_of(int code, ncclDataType_t* t, size_t* size) {
+  switch (code) {
+    case 0: *t = ncclFloat32; *size = 4; return true;
+    case 1: *t = ncclBfloat16; *size = 2; return true;
+    case 2: *t = ncclFloat16; *size = 2; return true;
+    case 3: *t = ncclInt32; *size = 4; return true;
+    case 4: *t = ncclInt64; *size = 8; return true;
+    case 5: *t = ncclFloat64; *size = 8; return true;
+    case 6: *t = ncclUint8; *size = 1; return true;
+    default: g_err = "rmesh: unknown dtype code " + std::to_string(code); return false;
+  }
+}
+
+bool usable(Mesh* m) {
+  if (m == nullptr) {
+    g_err = "rmesh: null mesh";
+    return false;
+  }
+  if (m->aborted) {
+    g_err = "rmesh: mesh was aborted (rebuild it with rmesh_shrink)";
+    return false;
+  }
+  return true;
+}
+
+// Closes a ncclGroupStart opened by the caller whatever happened inside it (an unbalanced group
+// would poison every later RCCL call of this thread).
+bool group_end(bool ok) {
+  ncclResult_t r = ncclGroupEnd();
+  return nccl_ok(r, "ncclGroupEnd") && ok;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rmesh_last_error() { return g_err.c_str(); }
+
+int rmesh_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+// One communicator per device of devs[0..ndev) (a device may appear only once: RCCL refuses two
+// ranks on one device). Returns an opaque handle, or null (rmesh_last_error()).
+void* rmesh_create(int ndev, const int* devs) {
+  DeviceGuard g;
+  if (ndev < 1 || devs == nullptr) {
+    g_err = "rmesh_create: ndev must be >= 1";
+    return nullptr;
+  }
+  int count = 0;
+  if (!hip_ok(hipGetDeviceCount(&count), "hipGetDeviceCount")) return nullptr;
+  for (int i = 0; i < ndev; ++i) {
+    if (devs[i] < 0 || devs[i] >= count) {
+      g_err = "rmesh_create: device " + std::to_string(devs[i]) + " not visible (" + std::to_string(count) + " devices)";
+      return nullptr;
+    }
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) {
+        g_err = "rmesh_create: device " + std::to_string(devs[i]) + " listed twice";
+        return nullptr;
+      }
+  }
+  auto* m = new Mesh();
+  m->devs.assign(devs, devs + ndev);
+  m->comms.assign(ndev, nullptr);
+  if (!nccl_ok(ncclCommInitAll(m->comms.data(), ndev, m->devs.data()), "ncclCommInitAll")) {
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+int rmesh_size(void* h) { return h ? (int)static_cast<Mesh*>(h)->devs.size() : 0; }
+
+int rmesh_device(void* h, int rank) {
+  auto* m = static_cast<Mesh*>(h);
+  return (m && rank >= 0 && rank < (int)m->devs.size()) ? m->devs[rank] : -1;
+}
+
+// In-place all-reduce of bufs[i] (count elements on device devs[i]) on streams[i]. op: 0 sum,
+// 1 max, 2 min, 3 avg.
+int rmesh_allreduce(void* h, void** bufs, int64_t count, int dtype, int op, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  ncclDataType_t t;
+  size_t es;
+  if (!dtype_of(dtype, &t, &es)) return 2;
+  ncclRedOp_t rop = op == 1 ? ncclMax : op == 2 ? ncclMin : op == 3 ? ncclAvg : ncclSum;
+  DeviceGuard g;
+  bool ok = nccl_ok(ncclGroupStart(), "ncclGroupStart");
+  if (!ok) return 1;
+  for (size_t i = 0; i < m->devs.size() && ok; ++i)
+    ok = nccl_ok(ncclAllReduce(bufs[i], bufs[i], (size_t)count, t, rop, m->comms[i], (hipStream_t)streams[i]), "ncclAllReduce");
+  return group_end(ok) ? 0 : 1;
+}
+
+// bufs[root] is copied into every other device's buffer.
+int rmesh_broadcast(void* h, void** bufs, int64_t count, int dtype, int root, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  if (root < 0 || root >= (int)m->devs.size()) {
+    g_err = "rmesh_broadcast: root out of range";
+    return 2;
+  }
+  ncclDataType_t t;
+  size_t es;
+  if (!dtype_of(dtype, &t, &es)) return 2;
+  DeviceGuard g;
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (size_t i = 0; i < m->devs.size() && ok; ++i)
+    ok = nccl_ok(ncclBroadcast(bufs[i], bufs[i], (size_t)count, t, root, m->comms[i], (hipStream_t)streams[i]), "ncclBroadcast");
+  return group_end(ok) ? 0 : 1;
+}
+
+// recv[i] (G * count elements) <- concat over ranks of send[r] (count elements each).
+int rmesh_allgather(void* h, void** send, void** recv, int64_t count, int dtype, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  ncclDataType_t t;
+  size_t es;
+  if (!dtype_of(dtype, &t, &es)) return 2;
+  DeviceGuard g;
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (size_t i = 0; i < m->devs.size() && ok; ++i)
+    ok = nccl_ok(ncclAllGather(send[i], recv[i], (size_t)count, t, m->comms[i], (hipStream_t)streams[i]), "ncclAllGather");
+  return group_end(ok) ? 0 : 1;
+}
+
+// Grouped point-to-point exchange: op k is issued by mesh rank rank[k]; kind[k] 0 = send to
+// peer[k], 1 = receive from peer[k]; bufs[k] holds counts[k] elements on rank[k]'s device,
+// streams[k] is a stream of that device. All ops go in ONE group (no ordering deadlock).
+int rmesh_p2p(void* h, int nops, const int* kind, const int* rank, const int* peer, void** bufs, const int64_t* counts, int dtype, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  ncclDataType_t t;
+  size_t es;
+  if (!dtype_of(dtype, &t, &es)) return 2;
+  int G = (int)m->devs.size();
+  for (int k = 0; k < nops; ++k)
+    if (rank[k] < 0 || rank[k] >= G || peer[k] < 0 || peer[k] >= G || peer[k] == rank[k]) {
+      g_err = "rmesh_p2p: op " + std::to_string(k) + " has a bad rank/peer";
+      return 2;
+    }
+  DeviceGuard g;
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (int k = 0; k < nops && ok; ++k) {
+    ncclComm_t c = m->comms[rank[k]];
+    hipStream_t s = (hipStream_t)streams[k];
+    ok = kind[k] == 0 ? nccl_ok(ncclSend(bufs[k], (size_t)counts[k], t, peer[k], c, s), "ncclSend")
+                      : nccl_ok(ncclRecv(bufs[k], (size_t)counts[k], t, peer[k], c, s), "ncclRecv");
+  }
+  return group_end(ok) ? 0 : 1;
+}
+
+// FedAvg of G stacked engine groups (group i on mesh rank i): params[i] is a [P_i][ld] fp32 row
+// block, bufs[i] a scratch of n + 1 floats on that device, w[off_i .. off_i + P_i) the rows'
+// sample weights (0 = not a trainer) and mask[...] the rows that receive the mean (every live
+// local peer), with off_i = sum_{j<i} P_j. Per device: reduce (weights as kernel arguments) →
+// one grouped all-reduce of [Σ w x | Σ w] → apply. Three launches per device, host never waits.
+int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, const int64_t* ld, const float* w, const float* mask, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  const int G = (int)m->devs.size();
+  DeviceGuard g;
+  int off = 0;
+  for (int i = 0; i < G; ++i) {
+    if (P[i] < 0 || P[i] > FEDAVG_MAX_PEERS) {
+      g_err = "rmesh_fedavg: 0..64 rows per device";
+      return 2;
+    }
+    float* out = static_cast<float*>(bufs[i]);
+    hipStream_t s = (hipStream_t)streams[i];
+    if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+    if (P[i] == 0) {  // a device without live rows still takes part: it contributes zero
+      if (!hip_ok(hipMemsetAsync(out, 0, (size_t)(n + 1) * sizeof(float), s), "hipMemsetAsync")) return 1;
+    } else {
+      FedAvgWeights fw{};
+      double sum = 0.0;
+      for (int p = 0; p < P[i]; ++p) {
+        fw.w[p] = w[off + p];
+        sum += w[off + p];
+      }
+      fw.wsum = (float)sum;
+      fl_fedavg_reduce(out, out + n, static_cast<const float*>(params[i]), P[i], n, ld[i], fw, s);
+      if (!hip_ok(hipGetLastError(), "fl_fedavg_reduce")) return 1;
+    }
+    off += P[i];
+  }
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (int i = 0; i < G && ok; ++i)
+    ok = nccl_ok(ncclAllReduce(bufs[i], bufs[i], (size_t)(n + 1), ncclFloat32, ncclSum, m->comms[i], (hipStream_t)streams[i]), "ncclAllReduce");
+  if (!group_end(ok)) return 1;
+  off = 0;
+  for (int i = 0; i < G; ++i) {
+    if (P[i] > 0) {
+      unsigned long long bits = 0;
+      for (int p = 0; p < P[i]; ++p)
+        if (mask[off + p] != 0.f) bits |= 1ull << p;
+      if (bits) {
+        if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+        const float* out = static_cast<const float*>(bufs[i]);
+        fl_fedavg_apply(static_cast<float*>(params[i]), out, out + n, P[i], n, ld[i], bits, (hipStream_t)streams[i]);
+        if (!hip_ok(hipGetLastError(), "fl_fedavg_apply")) return 1;
+      }
+    }
+    off += P[i];
+  }
+  return 0;
+}
+
+// 0: every communicator healthy; otherwise the first asynchronous error (message set).
+int rmesh_check(void* h) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  for (size_t i = 0; i < m->comms.size(); ++i) {
+    ncclResult_t e = ncclSuccess;
+    if (!nccl_ok(ncclCommGetAsyncError(m->comms[i], &e), "ncclCommGetAsyncError")) return 1;
+    if (e != ncclSuccess && e != ncclInProgress) {
+      g_err = "rank " + std::to_string(i) + " (device " + std::to_string(m->devs[i]) + "): " + ncclGetErrorString(e);
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// Abort every communicator (local; never waits for a dead peer; ends kernels stuck in the mesh).
+int rmesh_abort(void* h) {
+  auto* m = static_cast<Mesh*>(h);
+  if (m == nullptr) return 1;
+  if (m->aborted) return 0;
+  DeviceGuard g;
+  int rc = 0;
+  for (size_t i = 0; i < m->comms.size(); ++i) {
+    if (m->comms[i] == nullptr) continue;
+    if (!nccl_ok(ncclCommAbort(m->comms[i]), "ncclCommAbort")) rc = 1;
+    m->comms[i] = nullptr;
+  }
+  m->aborted = true;
+  return rc;
+}
+
+// Rebuild the mesh over the listed surviving ranks (indices into the current device list): the
+// old communicators are aborted, a fresh ncclCommInitAll runs over the survivors' devices, and
+// the survivors are renumbered 0..nkeep-1 in the given order.
+int rmesh_shrink(void* h, const int* keep, int nkeep) {
+  auto* m = static_cast<Mesh*>(h);
+  if (m == nullptr || nkeep < 1) {
+    g_err = "rmesh_shrink: need a mesh and at least one survivor";
+    return 2;
+  }
+  std::vector<int> devs;
+  for (int k = 0; k < nkeep; ++k) {
+    if (keep[k] < 0 || keep[k] >= (int)m->devs.size()) {
+      g_err = "rmesh_shrink: survivor index out of range";
+      return 2;
+    }
+    devs.push_back(m->devs[keep[k]]);
+  }
+  if (!m->aborted && rmesh_abort(m) != 0) return 1;
+  DeviceGuard g;
+  std::vector<ncclComm_t> comms(devs.size(), nullptr);
+  if (!nccl_ok(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()), "ncclCommInitAll")) return 1;
+  m->devs = devs;
+  m->comms = comms;
+  m->aborted = false;
+  return 0;
+}
+
+void rmesh_destroy(void* h) {
+  auto* m = static_cast<Mesh*>(h);
+  if (m == nullptr) return;
+  DeviceGuard g;
+  if (!m->aborted)
+    for (auto c : m->comms)
+      if (c != nullptr) ncclCommDestroy(c);
+  delete m;
+}
+
+}  // extern "C"

@@ -48,6 +48,10 @@ class CollectiveCommunicationProtocol(InMemoryCommunicationProtocol):
     def build_client(self, addr: str, neighbors):
         return InMemoryClient(addr, neighbors)
 
+    def placement(self):
+        """(device, mesh rank) for this peer's learner when the process drives a device mesh."""
+        return Federation.get().placement()
+
     def bind_node(self, node) -> None:
         self.node = node
         Federation.get().register_local(node)

@@ -65,9 +65,13 @@ def classification_metrics(confusion: np.ndarray) -> Dict[str, float]:
 class TorchLearner(Learner):
     """Trains a ``TorchModel`` on the node's device."""
 
-    def __init__(self, model: TorchModel, data=None, self_addr: str = "unknown-node", aggregator=None, batch_size: Optional[int] = None, device: Optional[str] = None) -> None:
+    def __init__(self, model: TorchModel, data=None, self_addr: str = "unknown-node", aggregator=None, batch_size: Optional[int] = None, device: Optional[str] = None,
+                 mesh_rank: Optional[int] = None) -> None:
         super().__init__(model, data, self_addr, aggregator)
         self.device = torch.device(device or resolve_device())
+        # rank of this peer's device in the process's device mesh (parallel/device_mesh.py); None
+        # outside a mesh. Peers of one mesh rank share one stacked engine group.
+        self.mesh_rank = mesh_rank
         self.batch_size = int(batch_size or Settings.BATCH_SIZE)
         self._interrupt = threading.Event()
         self._data_cache: Dict[bool, Tuple[torch.Tensor, torch.Tensor]] = {}
@@ -109,10 +113,12 @@ class TorchLearner(Learner):
         from myfyp_amd.parallel.mlp_engine import MLPEngineHandle
 
         if MLPEngineHandle.supports(module, self.batch_size):
-            return MLPEngineHandle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
+            with torch.cuda.device(self.device):
+                return MLPEngineHandle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size, tag=self.mesh_rank)
         for handle in (CNNEngineHandle,):
             if handle.supports(module):
-                return handle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size)
+                with torch.cuda.device(self.device):
+                    return handle.attach(module, self.device, self._self_addr, learner=self, batch_size=self.batch_size, tag=self.mesh_rank)
         return None
 
     def flat_params(self) -> torch.Tensor:

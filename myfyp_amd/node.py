@@ -70,6 +70,19 @@ class Node:
         self.aggregator.set_node_name(self.addr)
         if learner is None:
             learner = LearnerFactory.create_learner(model)
+        # a process driving a device mesh places its peers round-robin over the devices
+        place = getattr(self._communication_protocol, "placement", None)
+        if place is not None and "device" not in (learner_kwargs or {}):
+            where = place()
+            if where is not None:
+                import inspect
+
+                params = inspect.signature(learner).parameters
+                learner_kwargs = dict(learner_kwargs or {})
+                if "device" in params:
+                    learner_kwargs["device"] = where[0]
+                if "mesh_rank" in params:
+                    learner_kwargs["mesh_rank"] = where[1]
         # plain learner, or (Settings.SIMULATION_POOL) one pinned to a device of the simulation pool
         self.learner: Learner = try_init_learner_with_ray(learner, model, data, self.addr, self.aggregator, **(learner_kwargs or {}))
         self.exp_name = exp_name

@@ -80,7 +80,9 @@ def build(verbose: bool = False, jobs: int = 8, variant: str = "") -> str:
     LIB_ = lib
     if not os.path.exists(LIB_) or os.path.getmtime(LIB_) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB_ + ".tmp"
-        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
+        # the in-process device mesh (csrc/runtime/rccl_mesh.hip) calls RCCL directly; at run time the
+        # soname librccl.so.1 resolves to the copy torch already loaded (one RCCL per process)
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed:\n{res.stdout}\n{res.stderr}")

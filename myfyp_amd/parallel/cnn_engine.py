@@ -215,12 +215,14 @@ class CNNGroup:
     _lock = threading.Lock()
 
     @classmethod
-    def get(cls, device: torch.device, module: torch.nn.Module, batch_size: int) -> "CNNGroup":
-        key = (str(device), arch_key(module), batch_size)
+    def get(cls, device: torch.device, module: torch.nn.Module, batch_size: int, tag=None) -> "CNNGroup":
+        """``tag``: the peer's device-mesh rank (a virtual mesh puts several ranks on one GPU)."""
+        key = (str(device), arch_key(module), batch_size, tag)
         with cls._lock:
             g = cls._groups.get(key)
             if g is None:
                 g = cls(device, module, batch_size)
+                g.mesh_rank = tag
                 cls._groups[key] = g
             return g
 
@@ -231,6 +233,7 @@ class CNNGroup:
 
     def __init__(self, device: torch.device, template: torch.nn.Module, batch_size: int, capacity: int = 8) -> None:
         self.device = device
+        self.mesh_rank = None
         self.B = batch_size
         self.arch = arch_of(template)
         self.lock = threading.RLock()
@@ -1223,12 +1226,12 @@ class CNNEngineHandle:
         return True
 
     @classmethod
-    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None) -> "CNNEngineHandle":
-        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner)
+    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None, tag=None) -> "CNNEngineHandle":
+        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner, tag)
 
-    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None) -> None:
+    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None, tag=None) -> None:
         self.addr, self.module, self.learner = addr, module, learner
-        self.group = CNNGroup.get(device, module, batch_size)
+        self.group = CNNGroup.get(device, module, batch_size, tag)
         self._data_id = id(learner.data) if learner is not None else None
         with self.group.lock:
             self.slot = self.group.attach(self)

@@ -1,0 +1,329 @@
+"""In-process device mesh: one process drives G devices; weights move over RCCL (xGMI).
+
+SURVEY §2.10 #2 / §7.3 / §7.4.2: the reference keeps all peers of a simulation in one process and
+moves models with direct calls (``p2pfl/communication/protocols/memory/server_singleton.py:22-43``,
+``test/node_test.py:79-132``). Here the peers of one process are placed round-robin over G MI355X
+devices; the co-located peers of each device form one stacked engine group, and the weights plane
+between devices is a set of G RCCL communicators created together (``ncclCommInitAll``) and driven
+from ONE host thread inside ``ncclGroupStart/End`` (``csrc/runtime/rccl_mesh.hip``).
+
+Two implementations of one interface:
+
+* :class:`RcclMesh` — the C++ wrapper (real devices, each listed once);
+* :class:`HostMesh` — the same collectives as torch ops over the member tensors, stream-ordered on
+  the current streams. It serves CPU hosts (tests of the multi-device logic with ``cpu`` members)
+  and *virtual* meshes whose members share one physical GPU (a one-GPU rehearsal of the N-device
+  path; RCCL refuses two ranks on one device).
+
+Every method takes one tensor per mesh rank (rank i's tensor lives on ``devices[i]``) and enqueues
+on each device's current stream: nothing here waits for the GPU.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+_DTYPE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.float64: 5, torch.uint8: 6}
+_OPS = {"sum": 0, "max": 1, "min": 2, "avg": 3}
+
+_SIGS = {
+    "rmesh_last_error": (ctypes.c_char_p, []),
+    "rmesh_version": (ctypes.c_int, []),
+    "rmesh_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_void_p]),
+    "rmesh_size": (ctypes.c_int, [ctypes.c_void_p]),
+    "rmesh_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "rmesh_allreduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "rmesh_broadcast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "rmesh_allgather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    "rmesh_p2p": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "rmesh_fedavg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "rmesh_check": (ctypes.c_int, [ctypes.c_void_p]),
+    "rmesh_abort": (ctypes.c_int, [ctypes.c_void_p]),
+    "rmesh_shrink": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "rmesh_destroy": (None, [ctypes.c_void_p]),
+}
+
+
+class MeshError(RuntimeError):
+    """A mesh collective failed (or the mesh was aborted)."""
+
+
+def _ptrs(vals: Sequence[int]) -> ctypes.Array:
+    return (ctypes.c_void_p * len(vals))(*vals)
+
+
+def _stream_ptr(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+
+
+class DeviceMesh:
+    """Common interface (see the module docstring)."""
+
+    kind = "abstract"
+
+    def __init__(self, devices: Sequence[torch.device]) -> None:
+        self.devices: List[torch.device] = [torch.device(d) for d in devices]
+        self.lock = threading.RLock()
+        self.calls = 0
+        self.shrinks = 0
+
+    @property
+    def size(self) -> int:
+        return len(self.devices)
+
+    def _check_members(self, ts: Sequence[torch.Tensor], what: str) -> None:
+        if len(ts) != self.size:
+            raise ValueError(f"{what}: {len(ts)} tensors for a mesh of {self.size}")
+        for t, d in zip(ts, self.devices):
+            if t.device != d and not (d.index is None and t.device.type == d.type):
+                raise ValueError(f"{what}: tensor on {t.device}, mesh rank on {d}")
+            if not t.is_contiguous():
+                raise ValueError(f"{what}: tensors must be contiguous")
+
+    # ------------------------------------------------------------------ interface
+    def all_reduce_(self, ts: Sequence[torch.Tensor], op: str = "sum") -> None:
+        raise NotImplementedError
+
+    def broadcast_(self, ts: Sequence[torch.Tensor], root: int) -> None:
+        raise NotImplementedError
+
+    def all_gather_(self, outs: Sequence[torch.Tensor], ins: Sequence[torch.Tensor]) -> None:
+        raise NotImplementedError
+
+    def p2p_(self, ops: Sequence[Tuple[str, int, int, torch.Tensor]]) -> None:
+        """``ops``: (``"send"`` | ``"recv"``, rank, peer, tensor); all in one group."""
+        raise NotImplementedError
+
+    def fedavg_stacked(self, params: Sequence[torch.Tensor], bufs: Sequence[torch.Tensor], P: Sequence[int], n: int,
+                       ld: Sequence[int], w: np.ndarray, mask: np.ndarray) -> None:
+        """FedAvg over the stacked groups (one per rank); see ``rmesh_fedavg``."""
+        raise NotImplementedError
+
+    def check(self) -> None:
+        pass
+
+    def abort(self) -> None:
+        pass
+
+    def shrink(self, keep: Sequence[int]) -> None:
+        """Rebuild over the surviving ranks ``keep`` (indices into ``devices``), renumbered in order."""
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class HostMesh(DeviceMesh):
+    """Torch-op implementation (CPU members, or virtual members on one GPU)."""
+
+    kind = "host"
+
+    def all_reduce_(self, ts, op: str = "sum") -> None:
+        self._check_members(ts, "all_reduce")
+        with self.lock:
+            self.calls += 1
+            acc = ts[0].detach().clone()
+            for t in ts[1:]:
+                x = t.to(acc.device)
+                if op in ("sum", "avg"):
+                    acc.add_(x)
+                elif op == "max":
+                    torch.maximum(acc, x, out=acc)
+                elif op == "min":
+                    torch.minimum(acc, x, out=acc)
+                else:
+                    raise ValueError(op)
+            if op == "avg":
+                acc.div_(len(ts))
+            for t in ts:
+                t.copy_(acc.to(t.device))
+
+    def broadcast_(self, ts, root: int) -> None:
+        self._check_members(ts, "broadcast")
+        with self.lock:
+            self.calls += 1
+            src = ts[root]
+            for i, t in enumerate(ts):
+                if i != root:
+                    t.copy_(src.to(t.device))
+
+    def all_gather_(self, outs, ins) -> None:
+        self._check_members(ins, "all_gather")
+        with self.lock:
+            self.calls += 1
+            cat = torch.cat([x.reshape(-1).to(ins[0].device) for x in ins])
+            for o in outs:
+                o.view(-1).copy_(cat.to(o.device))
+
+    def p2p_(self, ops) -> None:
+        with self.lock:
+            self.calls += 1
+            sends = {}
+            for kind, rank, peer, t in ops:
+                if kind == "send":
+                    sends.setdefault((rank, peer), []).append(t)
+            for kind, rank, peer, t in ops:
+                if kind == "recv":
+                    q = sends.get((peer, rank))
+                    if not q:
+                        raise MeshError(f"p2p: receive on rank {rank} from {peer} has no matching send")
+                    t.copy_(q.pop(0).to(t.device))
+
+    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask) -> None:
+        with self.lock:
+            self.calls += 1
+            off = 0
+            for i in range(self.size):
+                b = bufs[i]
+                if P[i] == 0:
+                    b.zero_()
+                else:
+                    rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])[:, :n]
+                    wt = torch.as_tensor(w[off : off + P[i]], dtype=torch.float32, device=rows.device)
+                    b[:n].copy_((wt[:, None] * rows).sum(0))
+                    b[n] = float(np.sum(w[off : off + P[i]], dtype=np.float64))
+                off += P[i]
+            self.all_reduce_(list(bufs))
+            off = 0
+            for i in range(self.size):
+                if P[i] > 0:
+                    b = bufs[i]
+                    mean = b[:n] / b[n].clamp_min(1e-30)
+                    rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])
+                    for p in range(P[i]):
+                        if mask[off + p] != 0:
+                            rows[p, :n].copy_(mean)
+                off += P[i]
+
+    def shrink(self, keep) -> None:
+        with self.lock:
+            self.devices = [self.devices[k] for k in keep]
+            self.shrinks += 1
+
+
+class RcclMesh(DeviceMesh):
+    """``csrc/runtime/rccl_mesh.hip`` through ctypes (GIL held: every call only enqueues)."""
+
+    kind = "rccl"
+
+    def __init__(self, devices: Sequence[torch.device]) -> None:
+        super().__init__(devices)
+        from myfyp_amd.ops import _native
+
+        _native.load(required=True)
+        lib = ctypes.PyDLL(_native.LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        self._lib = lib
+        idx = [d.index if d.index is not None else 0 for d in self.devices]
+        if len(set(idx)) != len(idx):
+            raise ValueError(f"RcclMesh: every device at most once (got {idx}); use HostMesh for virtual members")
+        arr = (ctypes.c_int * len(idx))(*idx)
+        self._h = lib.rmesh_create(len(idx), arr)
+        if not self._h:
+            raise MeshError(f"ncclCommInitAll over devices {idx} failed: {self._err()}")
+
+    def _err(self) -> str:
+        return self._lib.rmesh_last_error().decode()
+
+    def _rc(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise MeshError(f"{what}: {self._err()}")
+
+    def _streams(self) -> ctypes.Array:
+        return _ptrs([_stream_ptr(d) for d in self.devices])
+
+    @staticmethod
+    def _dtype(t: torch.Tensor) -> int:
+        code = _DTYPE.get(t.dtype)
+        if code is None:
+            raise TypeError(f"mesh collectives: unsupported dtype {t.dtype}")
+        return code
+
+    def all_reduce_(self, ts, op: str = "sum") -> None:
+        self._check_members(ts, "all_reduce")
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_allreduce(self._h, _ptrs([t.data_ptr() for t in ts]), ts[0].numel(), self._dtype(ts[0]), _OPS[op], self._streams()),
+                     "rmesh_allreduce")
+
+    def broadcast_(self, ts, root: int) -> None:
+        self._check_members(ts, "broadcast")
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_broadcast(self._h, _ptrs([t.data_ptr() for t in ts]), ts[0].numel(), self._dtype(ts[0]), int(root), self._streams()),
+                     "rmesh_broadcast")
+
+    def all_gather_(self, outs, ins) -> None:
+        self._check_members(ins, "all_gather")
+        self._check_members(outs, "all_gather")
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_allgather(self._h, _ptrs([t.data_ptr() for t in ins]), _ptrs([t.data_ptr() for t in outs]), ins[0].numel(),
+                                               self._dtype(ins[0]), self._streams()), "rmesh_allgather")
+
+    def p2p_(self, ops) -> None:
+        if not ops:
+            return
+        kinds = (ctypes.c_int * len(ops))(*[0 if k == "send" else 1 for k, _, _, _ in ops])
+        ranks = (ctypes.c_int * len(ops))(*[r for _, r, _, _ in ops])
+        peers = (ctypes.c_int * len(ops))(*[p for _, _, p, _ in ops])
+        counts = (ctypes.c_int64 * len(ops))(*[t.numel() for _, _, _, t in ops])
+        dt = self._dtype(ops[0][3])
+        if any(self._dtype(t) != dt for _, _, _, t in ops):
+            raise TypeError("p2p: one dtype per exchange")
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_p2p(self._h, len(ops), kinds, ranks, peers, _ptrs([t.data_ptr() for _, _, _, t in ops]), counts, dt,
+                                         _ptrs([_stream_ptr(self.devices[r]) for _, r, _, _ in ops])), "rmesh_p2p")
+
+    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask) -> None:
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
+        lda = (ctypes.c_int64 * self.size)(*[int(x) for x in ld])
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_fedavg(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in bufs]), Pa, int(n), lda,
+                                            w.ctypes.data, mask.ctypes.data, self._streams()), "rmesh_fedavg")
+
+    def check(self) -> None:
+        with self.lock:
+            self._rc(self._lib.rmesh_check(self._h), "rmesh_check")
+
+    def abort(self) -> None:
+        with self.lock:
+            self._rc(self._lib.rmesh_abort(self._h), "rmesh_abort")
+
+    def shrink(self, keep) -> None:
+        arr = (ctypes.c_int * len(keep))(*[int(k) for k in keep])
+        with self.lock:
+            self._rc(self._lib.rmesh_shrink(self._h, arr, len(keep)), "rmesh_shrink")
+            self.devices = [self.devices[k] for k in keep]
+            self.shrinks += 1
+
+    def close(self) -> None:
+        with self.lock:
+            if self._h:
+                self._lib.rmesh_destroy(self._h)
+                self._h = None
+
+
+def make_mesh(devices: Sequence[torch.device], backend: Optional[str] = None) -> DeviceMesh:
+    """``backend``: "rccl", "host" or None (RCCL when every member is a distinct GPU)."""
+    devs = [torch.device(d) for d in devices]
+    if backend is None:
+        distinct = len({(d.type, d.index) for d in devs}) == len(devs)
+        backend = "rccl" if all(d.type == "cuda" for d in devs) and distinct else "host"
+    if backend == "rccl":
+        return RcclMesh(devs)
+    if backend == "host":
+        return HostMesh(devs)
+    raise ValueError(f"unknown mesh backend {backend!r}")

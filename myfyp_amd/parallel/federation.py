@@ -29,6 +29,15 @@ the peers of all processes form one federation:
   gather) before anything is written, rebuild their groups over themselves and re-run the
   aggregation from the still-intact local rows (the reference's "aggregate whatever arrived",
   ``aggregator.py:191-208``, and drop-on-send-failure, ``grpc_client.py:176-186``);
+* **device mesh** (``Federation.init(devices=G)``, ``Settings.MESH_DEVICES``, ``bench.py --gpus G``)
+  — ONE process drives G GPUs, the reference's process model (all peers in one process,
+  ``p2pfl/communication/protocols/memory/server_singleton.py:22-43``): peers are placed
+  round-robin over the devices (:meth:`Federation.placement`), each device's peers form one stacked
+  engine group, and the weights plane between devices is an in-process RCCL mesh
+  (``ncclCommInitAll`` + grouped collectives from one thread, ``parallel/device_mesh.py`` /
+  ``csrc/runtime/rccl_mesh.hip``). Votes, membership and agreement are plain function calls: there
+  is no cross-process control plane. A device whose last peer stops leaves the mesh
+  (``ncclCommAbort`` + ``ncclCommInitAll`` over the survivors);
 * **forced collective** (``Settings.FORCE_COLLECTIVE`` / ``MYFYP_FORCE_COLLECTIVE=1``) — a
   single-process job still initialises the ``nccl`` (RCCL) process group at world size 1 and takes
   every multi-rank code path (bucketed side-stream FedAvg, broadcast, all-gather, group rebuild), so
@@ -305,15 +314,31 @@ class Federation:
         # fault injection (fault_injection.crash_in_collective): called right before a weight
         # collective is issued, with its kind
         self.pre_collective_hooks: List[Callable[[str], None]] = []
+        # in-process device mesh (parallel/device_mesh.py): the devices this process drives, the
+        # mesh ranks still taking part (original numbering) and the round-robin placement cursor
+        self.devices: List[torch.device] = [device]
+        self.mesh = None
+        self.mesh_members: List[int] = [0]
+        self._placed = 0
+        self._mesh_scratch: Dict[Tuple[int, int], torch.Tensor] = {}
 
     # ------------------------------------------------------------------ lifecycle
     @classmethod
-    def init(cls, backend: Optional[str] = None) -> "Federation":
-        """Initialise from ``torchrun`` env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    def init(cls, backend: Optional[str] = None, devices: Any = None, mesh_backend: Optional[str] = None) -> "Federation":
+        """Initialise from ``torchrun`` env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*), or — with
+        ``devices`` (a count or a list of device strings; default ``Settings.MESH_DEVICES`` /
+        ``MYFYP_MESH_DEVICES``) — as a single process driving a device mesh (env rank/world are then
+        ignored: the process is the whole federation)."""
         if cls._instance is not None:
             return cls._instance
         if Settings.GIL_SWITCH_INTERVAL:
             sys.setswitchinterval(float(Settings.GIL_SWITCH_INTERVAL))
+        if devices is None:
+            env = os.environ.get("MYFYP_MESH_DEVICES", "")
+            devices = int(env) if env.isdigit() else Settings.MESH_DEVICES
+        devs = mesh_devices(devices)
+        if devs is not None:
+            return cls._init_mesh(devs, mesh_backend or Settings.MESH_BACKEND)
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -365,6 +390,77 @@ class Federation:
         if store is not None and world > 1:
             inst.bus = StoreBus(store, rank, world, inst._deliver)
         return inst
+
+    @classmethod
+    def _init_mesh(cls, devs: List[torch.device], backend: Optional[str]) -> "Federation":
+        from myfyp_amd.parallel.device_mesh import make_mesh
+
+        if devs[0].type == "cuda":
+            torch.cuda.set_device(devs[0])
+        inst = cls._instance = cls(0, 1, 0, devs[0], None)
+        inst.devices = list(devs)
+        inst.mesh = make_mesh(devs, backend)
+        inst.mesh_members = list(range(len(devs)))
+        logger.info("rank0", f"device mesh over {[str(d) for d in devs]} ({inst.mesh.kind})")
+        return inst
+
+    @property
+    def mesh_size(self) -> int:
+        return len(self.mesh_members) if self.mesh is not None else 1
+
+    def placement(self) -> Optional[Tuple[str, int]]:
+        """Next peer's (device, mesh rank), round-robin over the mesh (None outside a mesh)."""
+        if self.mesh is None:
+            return None
+        with self._lock:
+            r = self.mesh_members[self._placed % len(self.mesh_members)]
+            self._placed += 1
+        return str(self.devices[r]), r
+
+    def mesh_position(self, mesh_rank: int) -> int:
+        """Index of an original mesh rank among the ranks still in the mesh."""
+        return self.mesh_members.index(mesh_rank)
+
+    def mesh_scratch(self, mesh_rank: int, numel: int) -> torch.Tensor:
+        """fp32 scratch on a mesh rank's device (a rank without live peers still joins a collective)."""
+        key = (mesh_rank, numel)
+        t = self._mesh_scratch.get(key)
+        if t is None:
+            t = self._mesh_scratch[key] = torch.zeros(numel, dtype=torch.float32, device=self.devices[mesh_rank])
+        return t
+
+    def mesh_leave(self, mesh_rank: int) -> None:
+        """A mesh rank's last peer stopped: rebuild the mesh over the other ranks (abort + init-all
+        over the survivors); it joins no further collective. The round driver calls this between
+        rounds, so no collective is in flight."""
+        if self.mesh is None or mesh_rank not in self.mesh_members or len(self.mesh_members) == 1:
+            return
+        keep = [i for i, r in enumerate(self.mesh_members) if r != mesh_rank]
+        t0 = time.perf_counter()
+        self.mesh.shrink(keep)
+        self.mesh_members = [self.mesh_members[i] for i in keep]
+        self.record("mesh_shrink", time.perf_counter() - t0)
+        logger.warning("rank0", f"mesh rank {mesh_rank} ({self.devices[mesh_rank]}) has no live peer: mesh rebuilt over {self.mesh_members}")
+
+    def mesh_ranks_alive(self) -> List[int]:
+        """Mesh ranks that still host a live local peer."""
+        alive = set()
+        for a in self.local_order:
+            node = self.local_nodes.get(a)
+            if node is None:
+                continue
+            r = getattr(node.learner, "mesh_rank", None)
+            alive.add(0 if r is None else r)
+        return [r for r in self.mesh_members if r in alive]
+
+    def mesh_sync(self) -> None:
+        """Drop mesh ranks without live peers (called between rounds)."""
+        if self.mesh is None:
+            return
+        alive = self.mesh_ranks_alive()
+        for r in [r for r in self.mesh_members if r not in alive]:
+            if len(self.mesh_members) > 1 and alive:
+                self.mesh_leave(r)
 
     @classmethod
     def get(cls) -> "Federation":
@@ -442,6 +538,12 @@ class Federation:
                 if self.shm is None and not self.departed and self.members == list(range(self.world)) and not self._aborted:
                     dist.barrier(group=self._pg)
                 dist.destroy_process_group()
+        if self.mesh is not None:
+            for d in self.devices:
+                if d.type == "cuda":
+                    torch.cuda.synchronize(d)
+            self.mesh.close()
+            self.mesh = None
         if self.shm is not None:
             self.shm.leave()
             synced = self.shm.wait_all_gone(float(Settings.COLLECTIVE_TIMEOUT), float(Settings.FAILURE_TIMEOUT))
@@ -769,6 +871,8 @@ class Federation:
         effect at exit). Nested sections reuse the outer agreement."""
         with self._section_lock:
             outer = self._frozen is not None
+            if not outer and self.mesh is not None:
+                self.mesh_sync()  # devices whose last peer stopped leave the mesh first
             if not outer:
                 # a confirmation that ended in an agreement gather already agreed on the members
                 # (every member took part in it): no second membership gather right after it
@@ -985,6 +1089,28 @@ class Federation:
 
     def record(self, name: str, seconds: float) -> None:
         self.stats.setdefault(name, []).append(seconds)
+
+
+def mesh_devices(spec: Any) -> Optional[List[torch.device]]:
+    """Device list of an in-process mesh from ``spec`` (count or list of device strings), or None
+    for no mesh (``spec`` None/0/1, or an empty list). A count larger than the visible GPUs raises, unless
+    ``Settings.MESH_VIRTUAL`` allows a virtual mesh (every member on cuda:0, HostMesh collectives:
+    a one-GPU rehearsal of the N-device path); on a CPU host the members are ``cpu``."""
+    if spec is None:
+        return None
+    if isinstance(spec, (list, tuple)):  # an explicit member list is always a mesh (even of one)
+        return [torch.device(d) for d in spec] or None
+    n = int(spec)
+    if n <= 1:
+        return None
+    if not torch.cuda.is_available():
+        return [torch.device("cpu")] * n
+    have = torch.cuda.device_count()
+    if n <= have:
+        return [torch.device("cuda", i) for i in range(n)]
+    if Settings.MESH_VIRTUAL:
+        return [torch.device("cuda", 0)] * n
+    raise RuntimeError(f"device mesh of {n} GPUs requested, {have} visible")
 
 
 def rccl_reserved_cus() -> int:

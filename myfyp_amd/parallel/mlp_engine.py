@@ -114,13 +114,16 @@ class MLPGroup:
     _lock = threading.Lock()
 
     @classmethod
-    def get(cls, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, precision: Optional[str] = None) -> "MLPGroup":
+    def get(cls, device: torch.device, dims: Tuple[int, int, int, int], batch_size: int, precision: Optional[str] = None, tag=None) -> "MLPGroup":
+        """``tag``: the peers' device-mesh rank (a virtual mesh puts several ranks on one GPU)."""
         precision = precision or Settings.MLP_PRECISION
-        key = (str(device), dims, batch_size, precision)
+        key = (str(device), dims, batch_size, precision, tag)
         with cls._lock:
             g = cls._groups.get(key)
             if g is None:
-                g = cls(device, dims, batch_size, precision=precision)
+                with torch.cuda.device(device):
+                    g = cls(device, dims, batch_size, precision=precision)
+                g.mesh_rank = tag
                 cls._groups[key] = g
             return g
 
@@ -136,6 +139,7 @@ class MLPGroup:
             raise ValueError(f"MLP precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
         self.device = device
+        self.mesh_rank = None
         self.dims = dims
         self.B = batch_size
         D0, D1, D2, D3 = dims
@@ -259,7 +263,7 @@ class MLPGroup:
 
     def uses_persistent(self) -> bool:
         """True if the next local epoch runs as the weight-stationary persistent kernel."""
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             return bool(_native.load(required=True).mlp_engine_uses_persistent(self._engine))
 
@@ -326,13 +330,18 @@ class MLPGroup:
         )
         _native.check(lib.mlp_engine_set_extras(self._engine, _p(anchor), _p(cg), _p(cl)), "set_extras")
 
+    def on_device(self):
+        """Make the group's GPU current for this thread (the native engine allocates and captures
+        on the current device; a process may drive several devices: parallel/device_mesh.py)."""
+        return torch.cuda.device(self.device)
+
     def prewarm(self, spec: dict) -> None:
         """One-time engine setup before the first fit (node start): bind the data, capture and
         upload the epoch graph for ``spec`` (no FedProx/SCAFFOLD extras: those re-capture on their
         first fit), allocate the evaluation side and load the code object. Runs no training work;
         a later change (another peer attaching, other optimizer settings) re-captures as before."""
         lib = _native.load(required=True)
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             self._set_optimizer(lib, spec, 0.0, None, None, None)
             _native.check(lib.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
@@ -341,7 +350,7 @@ class MLPGroup:
     # ------------------------------------------------------------------ batched fit
     def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             stream = torch.cuda.current_stream(self.device).cuda_stream
             specs = list(batch.values())
@@ -435,13 +444,13 @@ class MLPGroup:
 
     def f32_variant(self) -> int:
         """Gang layout the fp32 persistent epoch uses (1 owners + heads, 2 owners only)."""
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             return int(_native.load(required=True).mlp_engine_f32_variant(self._engine))
 
     def f32_ks(self) -> int:
         """Owner K split the fp32 persistent epoch uses (1 or 2)."""
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             return int(_native.load(required=True).mlp_engine_f32_ks(self._engine))
 
@@ -462,13 +471,13 @@ class MLPGroup:
     def debug_giveup(self, slot: Optional[int], at_end: bool = False) -> None:
         """Test hook: the peer in ``slot`` gives up on the first attempt of every fp32 epoch, at
         launch or (``at_end``) at the gang commit after its last step."""
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             _native.check(_native.load(required=True).mlp_engine_debug_giveup(self._engine, -1 if slot is None else int(slot), int(at_end)), "debug_giveup")
 
     def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
-        with self.lock:
+        with self.lock, self.on_device():
             self._ensure_engine()
             stream = torch.cuda.current_stream(self.device).cuda_stream
             active = np.zeros(self.capacity, dtype=np.int32)
@@ -561,13 +570,13 @@ class MLPEngineHandle:
         return bool(lib.mlp_shape_ok(*dims))
 
     @classmethod
-    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None) -> "MLPEngineHandle":
-        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner)
+    def attach(cls, module: torch.nn.Module, device: torch.device, addr: str, learner=None, batch_size: Optional[int] = None, tag=None) -> "MLPEngineHandle":
+        return cls(module, device, addr, int(batch_size or Settings.BATCH_SIZE), learner, tag)
 
-    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None) -> None:
+    def __init__(self, module: torch.nn.Module, device: torch.device, addr: str, batch_size: int, learner=None, tag=None) -> None:
         self.addr = addr
         self.module = module
-        self.group = MLPGroup.get(device, mlp_dims(module), batch_size)
+        self.group = MLPGroup.get(device, mlp_dims(module), batch_size, tag=tag)
         self.learner = learner
         self._data_id = id(learner.data) if learner is not None else None
         with self.group.lock:

@@ -30,6 +30,28 @@ def state_tensors(learner) -> List[torch.Tensor]:
     return out
 
 
+def on_device(dev: torch.device):
+    """Make ``dev`` the thread's current GPU (no-op for CPU members)."""
+    import contextlib
+
+    return torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
+
+
+def mesh_rank_of(learner) -> int:
+    r = getattr(learner, "mesh_rank", None)
+    return 0 if r is None else int(r)
+
+
+def _by_mesh_rank(fed: Federation, addrs, learners) -> Dict[int, List[Tuple[str, Any]]]:
+    out: Dict[int, List[Tuple[str, Any]]] = {r: [] for r in fed.mesh_members}
+    for a, lr in zip(addrs, learners):
+        r = mesh_rank_of(lr)
+        if r not in out:
+            raise RuntimeError(f"peer {a} sits on mesh rank {r}, which left the mesh")
+        out[r].append((a, lr))
+    return out
+
+
 def _stacked_group(learners) -> Optional[Any]:
     """Return the shared MLPGroup when every learner is a row of one stacked buffer."""
     groups = {id(getattr(lr, "_engine", None) and lr._engine.group) for lr in learners}
@@ -46,6 +68,9 @@ def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str)
     state tensors are packed into one flat buffer each, so ResNet-18's ~100 tensors cost one
     guarded broadcast and one agreement gather, not one per tensor: ADVICE r3)."""
     learners = {a: fed.local_nodes[a].learner for a in arrived if a in fed.local_nodes}
+    if fed.mesh is not None:
+        _mesh_initial_model(fed, learners, initiator)
+        return
 
     def run() -> None:
         # the initiator's rank, or (if it died) the lowest survivor: every survivor agrees on it
@@ -69,6 +94,38 @@ def sync_initial_model(fed: Federation, arrived: Dict[str, Any], initiator: str)
                     dst.copy_(s)
 
     fed.run_aggregation(run)
+
+
+def _mesh_initial_model(fed: Federation, learners: Dict[str, Any], initiator: str) -> None:
+    """Device mesh: pack the initiator's state tensors per dtype on its device, ONE RCCL broadcast
+    per dtype from its mesh rank, unpack into every peer of every device."""
+    ref_addr = initiator if initiator in learners else next(iter(learners))
+    root_r = mesh_rank_of(learners[ref_addr])
+    root = fed.mesh_position(root_r)
+    src = state_tensors(learners[ref_addr])
+    groups: Dict[Any, List[int]] = {}
+    for i, t in enumerate(src):
+        groups.setdefault(t.dtype, []).append(i)
+    per_rank: Dict[int, List[Any]] = {r: [None] * len(src) for r in fed.mesh_members}
+    for dt, idx in groups.items():
+        numel = sum(src[i].numel() for i in idx)
+        flats = []
+        for r in fed.mesh_members:
+            dev = fed.devices[r]
+            if r == root_r:
+                flats.append(torch.cat([src[i].detach().reshape(-1) for i in idx]).to(dev))
+            else:
+                flats.append(torch.empty(numel, dtype=dt, device=dev))
+        fed.mesh.broadcast_(flats, root)
+        for r, flat in zip(fed.mesh_members, flats):
+            for i, part in zip(idx, torch.split(flat, [src[i].numel() for i in idx])):
+                per_rank[r][i] = part.view_as(src[i])
+    with torch.no_grad():
+        for a, lr in learners.items():
+            r = mesh_rank_of(lr)
+            with on_device(fed.devices[r]):
+                for dst, s_ in zip(state_tensors(lr), per_rank[r]):
+                    dst.copy_(s_)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -259,6 +316,8 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
         learners = [fed.local_nodes[a].learner for a in addrs]
         weights = [float(arrived[a][0]) for a in addrs]
         contributors = [a for a, w in zip(addrs, weights) if w > 0]
+        if fed.mesh is not None:
+            return _mesh_mean(fed, addrs, learners, weights), contributors
         group = _stacked_group(learners)
         dev = learners[0].flat_params().device
         if group is not None and dev.type == "cuda":
@@ -293,6 +352,64 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
     total_w, contributors = fed.run_aggregation(run)
     fed.record("aggregate", time.perf_counter() - t0)
     return total_w, contributors
+
+
+def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
+    """FedAvg over a device mesh. Stacked engine groups (one per mesh rank): ONE native call —
+    per device reduce launch, one grouped RCCL all-reduce, per device apply launch
+    (``rmesh_fedavg``). Other learners: per device partial sums, one mesh all-reduce, unpack."""
+    wt_of = dict(zip(addrs, weights))
+    ranks = _by_mesh_rank(fed, addrs, learners)
+    groups = {r: {id(lr._engine.group): lr._engine.group for _, lr in v if getattr(lr, "_engine", None) is not None} for r, v in ranks.items()}
+    stacked = all(len(g) == 1 and len(groups[r]) == 1 for r, g in groups.items() if ranks[r]) and all(
+        getattr(lr, "_engine", None) is not None for v in ranks.values() for _, lr in v)
+    numels = {next(iter(g.values())).numel for g in groups.values() if g}
+    if stacked and len(numels) == 1 and all(next(iter(g.values())).params.is_cuda for g in groups.values() if g):
+        n = numels.pop()
+        params, bufs, P, ld, w, mask = [], [], [], [], [], []
+        for r in fed.mesh_members:
+            if ranks[r]:
+                g = next(iter(groups[r].values()))
+                wr = np.zeros(g.capacity, dtype=np.float32)
+                mr = np.zeros(g.capacity, dtype=np.float32)
+                for a, lr in ranks[r]:
+                    wr[lr._engine.slot] = wt_of[a]
+                    mr[lr._engine.slot] = 1.0
+                with on_device(g.device):
+                    bufs.append(g.fedavg_buffer())
+                params.append(g.params)
+                P.append(g.capacity)
+                ld.append(g.S)
+                w.append(wr)
+                mask.append(mr)
+            else:  # no live peer on this device (yet in the mesh): contributes zeros
+                scratch = fed.mesh_scratch(r, n + 1)
+                params.append(scratch)
+                bufs.append(scratch)
+                P.append(0)
+                ld.append(n)
+        fed.mesh.fedavg_stacked(params, bufs, P, n, ld, np.concatenate(w) if w else np.zeros(0, np.float32),
+                                np.concatenate(mask) if mask else np.zeros(0, np.float32))
+        return float(sum(weights))
+    ref = _pack(learners[0])
+    n = ref.numel()
+    accs = []
+    for r in fed.mesh_members:
+        dev = fed.devices[r]
+        with on_device(dev):
+            acc = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+            for a, lr in ranks[r]:
+                if wt_of[a] > 0:
+                    acc[:n].add_(_pack(lr), alpha=wt_of[a])
+            acc[n] = float(sum(wt_of[a] for a, _ in ranks[r]))
+        accs.append(acc)
+    fed.mesh.all_reduce_(accs)
+    for r, acc in zip(fed.mesh_members, accs):
+        with on_device(fed.devices[r]):
+            avg = acc[:n] / acc[n].clamp_min(1e-12)
+            for _, lr in ranks[r]:
+                _unpack_into(lr, avg)
+    return float(sum(weights))
 
 
 def _generic_mean(fed: Federation, addrs, learners, weights, final: bool, delayed: bool) -> float:
@@ -356,6 +473,10 @@ def _neighbors(fed: Federation, arrived: Dict[str, Any], aggregator, t0: float) 
         fed.record("aggregate", time.perf_counter() - t0)
         return []
     learners = [fed.local_nodes[a].learner for a in local]
+    if fed.mesh is not None and fed.mesh_size > 1:
+        _mesh_neighbors(fed, peers, index, w, local, learners)
+        fed.record("aggregate", time.perf_counter() - t0)
+        return local
     group = _stacked_group(learners)
     if fed.solo and group is not None and group.params.is_cuda and group.capacity <= 16 and group.S % 4 == 0:
         # every neighbour is a row of the same stacked engine buffer: the whole mixing step is one
@@ -411,6 +532,41 @@ def _neighbors(fed: Federation, arrived: Dict[str, Any], aggregator, t0: float) 
     return local
 
 
+def _mesh_neighbors(fed: Federation, peers, index, w, local, learners) -> None:
+    """Topology mixing over a device mesh: every row a peer needs from another device arrives by
+    ONE grouped RCCL send/recv exchange (``rmesh_p2p``); the mix runs on the receiving device."""
+    lr_of = dict(zip(local, learners))
+    rank = {a: mesh_rank_of(lr_of[a]) for a in local}
+    rows = {}
+    for a in local:
+        with on_device(fed.devices[rank[a]]):
+            rows[a] = _pack(lr_of[a])
+    # (source peer, destination mesh rank) pairs, in one deterministic order for both sides
+    need = sorted({(peers[j], rank[a]) for a in local for j in np.nonzero(w[index[a]])[0]
+                   if peers[j] in rank and rank[peers[j]] != rank[a]}, key=lambda x: (index[x[0]], x[1]))
+    got: Dict[Tuple[str, int], torch.Tensor] = {}
+    ops_ = []
+    for b, rd in need:
+        buf = torch.empty_like(rows[b], device=fed.devices[rd])
+        got[(b, rd)] = buf
+        ops_.append(("send", fed.mesh_position(rank[b]), fed.mesh_position(rd), rows[b]))
+        ops_.append(("recv", fed.mesh_position(rd), fed.mesh_position(rank[b]), buf))
+    if ops_:
+        fed.mesh.p2p_(ops_)
+    mixed = {}
+    for a in local:
+        i = index[a]
+        nz = [j for j in np.nonzero(w[i])[0] if peers[j] in rank]
+        ws = np.array([w[i, j] for j in nz], dtype=np.float64)
+        ws = ws / ws.sum()  # a dead neighbour's share folds back proportionally
+        srcs = [rows[peers[j]] if rank[peers[j]] == rank[a] else got[(peers[j], rank[a])] for j in nz]
+        with on_device(fed.devices[rank[a]]):
+            mixed[a] = ops.weighted_average([[t] for t in srcs], [float(x) for x in ws])[0]
+    for a in local:
+        with on_device(fed.devices[rank[a]]):
+            _unpack_into(lr_of[a], mixed[a])
+
+
 # aggregator kinds reduced on the device (no wire models, no host copies)
 DEVICE_KINDS = ("mean", "neighbor", "scaffold", "median")
 
@@ -437,7 +593,58 @@ def aggregate_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], a
     fed.record("aggregate", time.perf_counter() - t0)
 
 
+def _mesh_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> None:
+    """SCAFFOLD server step over a device mesh: per device the packed local reduction, ONE mesh
+    all-reduce, per device the apply (new model into its peers, its copy of the control variate)."""
+    addrs = [a for a in arrived if a in fed.local_nodes]
+    learners = [fed.local_nodes[a].learner for a in addrs]
+    ranks = _by_mesh_rank(fed, addrs, learners)
+    n = learners[0].flat_params().numel()
+    bufs, x_starts = [], {}
+    for r in fed.mesh_members:
+        dev = fed.devices[r]
+        dys, dcs, ws = [], [], []
+        with on_device(dev):
+            for a, lr in ranks[r]:
+                wt = float(arrived[a][0])
+                cb = _scaffold_cb(lr)
+                if wt > 0 and cb.delta_y is not None:
+                    dys.append(cb.delta_y)
+                    dcs.append(cb.delta_c)
+                    ws.append(wt)
+                    x_starts.setdefault(r, cb.x0)
+            buf = torch.zeros(2 * n + 2, dtype=torch.float32, device=dev)
+            if dys:
+                ops.scaffold_reduce(buf, dys, dcs, ws)
+        bufs.append(buf)
+    fed.mesh.all_reduce_(bufs)
+    cdev = fed.__dict__.setdefault("_mesh_c", {})
+    for r, buf in zip(fed.mesh_members, bufs):
+        if not ranks[r]:
+            continue
+        dev = fed.devices[r]
+        with on_device(dev):
+            x_start = x_starts.get(r)
+            if x_start is None:  # the round-start model: every peer starts the round from it
+                src = next((v for v in x_starts.values()), None)
+                x_start = src.to(dev) if src is not None else ranks[r][0][1].flat_params().detach().clone()
+            c_prev = cdev.get(r)
+            c_init = c_prev is None or c_prev.numel() != n
+            c_new = torch.empty(n, dtype=torch.float32, device=dev) if c_init else c_prev
+            flats = [lr.flat_params() for _, lr in ranks[r]]
+            with torch.no_grad():
+                ops.scaffold_apply(flats, x_start, buf, c_new, c_init, aggregator.global_lr)
+            cdev[r] = c_new
+            gc = ranks[r][0][1].split_flat(c_new)
+            for a, lr in ranks[r]:
+                fed.local_nodes[a].aggregator._c_dev = c_new
+                lr.get_model().add_info("scaffold", {"global_c": gc})
+                lr.update_callbacks_with_model_info()
+
+
 def _scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> None:
+    if fed.mesh is not None and fed.mesh_size > 1:
+        return _mesh_scaffold(fed, arrived, aggregator)
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     flats = [learners[a].flat_params() for a in addrs]
@@ -485,7 +692,42 @@ def aggregate_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> 
     fed.record("aggregate", time.perf_counter() - t0)
 
 
+def _mesh_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None:
+    """Coordinate median over a device mesh: every device packs its trainers' rows ([k_max, n],
+    zero-padded), ONE mesh all-gather, then per device one median launch into its peers."""
+    addrs = [a for a in arrived if a in fed.local_nodes]
+    learners = [fed.local_nodes[a].learner for a in addrs]
+    ranks = _by_mesh_rank(fed, addrs, learners)
+    trainers = {r: [(a, lr) for a, lr in v if float(arrived[a][0]) > 0] for r, v in ranks.items()}
+    counts = [len(trainers[r]) for r in fed.mesh_members]
+    if not sum(counts):
+        return
+    kmax = max(counts)
+    n = _pack(learners[0]).numel()
+    sends, recvs = [], []
+    for r in fed.mesh_members:
+        dev = fed.devices[r]
+        with on_device(dev):
+            s_ = torch.zeros(kmax, n, dtype=torch.float32, device=dev)
+            for i, (a, lr) in enumerate(trainers[r]):
+                s_[i].copy_(_pack(lr))
+            sends.append(s_)
+            recvs.append(torch.empty(len(counts) * kmax, n, dtype=torch.float32, device=dev))
+    fed.mesh.all_gather_(recvs, sends)
+    for r, recv in zip(fed.mesh_members, recvs):
+        if not ranks[r]:
+            continue
+        with on_device(fed.devices[r]):
+            rows = [recv[q * kmax + i] for q, c in enumerate(counts) for i in range(c)]
+            med = torch.empty(n, dtype=torch.float32, device=recv.device)
+            ops.median_into(rows, [med])
+            for _, lr in ranks[r]:
+                _unpack_into(lr, med)
+
+
 def _median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None:
+    if fed.mesh is not None and fed.mesh_size > 1:
+        return _mesh_median(fed, arrived)
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     trainers = [a for a in addrs if float(arrived[a][0]) > 0]

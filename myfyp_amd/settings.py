@@ -124,6 +124,14 @@ class Settings:
     # active (co-residency: every workgroup of a gang must be resident at once). None: derived from
     # the RCCL channel cap in force (see RCCL_MAX_CHANNELS)
     RCCL_RESERVED_CUS: Optional[int] = None
+    # in-process device mesh (parallel/device_mesh.py): ONE process drives this many GPUs, peers
+    # placed round-robin, weights over an in-process RCCL mesh (ncclCommInitAll). 1 = off; env
+    # MYFYP_MESH_DEVICES overrides. MESH_BACKEND: None (RCCL on distinct GPUs, else host torch ops),
+    # "rccl" or "host". MESH_VIRTUAL: a count above the visible GPUs puts every member on cuda:0
+    # (one-GPU rehearsal with host collectives) instead of raising.
+    MESH_DEVICES: int = 1
+    MESH_BACKEND: Optional[str] = None
+    MESH_VIRTUAL: bool = False
     # Node.start() prepares the fused engine (epoch-graph capture and upload, code-object load; no
     # training work) so round 0 does not pay it — like building a compiled model at load time
     ENGINE_PREWARM: bool = True
@@ -217,6 +225,9 @@ class Settings:
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
             "FUSED_ROUND": "FUSED_ROUND",
             "ROUND_DRIVER": "ROUND_DRIVER",
+            "MESH_DEVICES": "MESH_DEVICES",
+            "MESH_BACKEND": "MESH_BACKEND",
+            "MESH_VIRTUAL": "MESH_VIRTUAL",
         }
     )
 

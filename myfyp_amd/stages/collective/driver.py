@@ -134,12 +134,9 @@ class RoundDriver:
                     n[a] = lr.num_train_samples()
             out: Dict[str, Any] = {}
             if trainers:
-                group = cur[trainers[0]].kw["learner"]._engine.group
-                slot = {a: cur[a].kw["learner"]._engine.slot for a in trainers}
                 has_test = {a for a in trainers if (d := cur[a].kw["learner"].data) is not None and d.get_num_samples(train=False) > 0}
-                evs = group._run_eval_batch({slot[a]: () for a in trainers if a in has_test})
-                fits = group._run_fit_batch({slot[a]: reqs[a] for a in trainers})
-                out = {a: (evs.get(slot[a]), fits[slot[a]]) for a in trainers}
+                out = fused_round.run_groups(f, trainers, lambda a: cur[a].kw["learner"]._engine.slot, lambda a: cur[a].kw["learner"]._engine.group,
+                                             reqs, has_test)
             total = next(iter(states.values())).total_rounds
             aggregator = next(iter(cur.values())).kw["aggregator"]
             fused_round.aggregate(f, {a: (n.get(a, 0), None) for a in cur}, aggregator, final=total is None or round_ + 1 >= total)
@@ -200,14 +197,20 @@ class RoundDriver:
         set_gang_expectations(self.f, set(), None)
         self.f.confirm_collectives()  # the last round's all-reduce, before the final evaluation reads the rows
         pend = {}
-        first = next(iter(done.values())).kw["learner"]
-        group = first._engine.group
         slots = {a: m.kw["learner"]._engine.slot for a, m in done.items()}
         with_test = {a for a, m in done.items() if m.kw["learner"].data is not None and m.kw["learner"].data.get_num_samples(train=False) > 0}
-        evs = group._run_eval_batch({slots[a]: () for a in with_test}) if with_test else {}
+        evs = {}
+        by_group: Dict[int, Any] = {}
+        for a in with_test:
+            g = done[a].kw["learner"]._engine.group
+            by_group.setdefault(id(g), (g, []))[1].append(a)
+        for g, addrs in by_group.values():
+            res = g._run_eval_batch({slots[a]: () for a in addrs})
+            for a in addrs:
+                evs[slots[a], id(g)] = res[slots[a]]
         for a, m in done.items():
             if a in with_test:
-                pend[a] = m.kw["learner"]._evaluate_done(evs[slots[a]], logger.experiment_snapshot(a))
+                pend[a] = m.kw["learner"]._evaluate_done(evs[slots[a], id(m.kw["learner"]._engine.group)], logger.experiment_snapshot(a))
         for a, m in done.items():
             results = pend[a].result() if a in pend else {}
             logger.info(a, f"📈 Final evaluation: {results}")

@@ -34,7 +34,7 @@ def eligible(f, aggregator) -> bool:
     """Decided once per round by the vote leader, so every co-located peer takes the same path."""
     if not Settings.FUSED_ROUND or getattr(aggregator, "collective_kind", None) not in ("mean", "neighbor"):
         return False
-    groups = set()
+    groups: dict = {}
     for a in f.local_order:
         node = f.local_nodes.get(a)
         if node is None:
@@ -43,8 +43,28 @@ def eligible(f, aggregator) -> bool:
         eng = getattr(lr, "_engine", None)
         if eng is None or getattr(lr, "callbacks", None) or not hasattr(lr, "fit_request"):
             return False
-        groups.add(id(eng.group))
-    return len(groups) == 1
+        groups.setdefault(getattr(lr, "mesh_rank", None), set()).add(id(eng.group))
+    # one engine group, or (device mesh) one group per mesh rank
+    if f.mesh is None:
+        return len(groups) == 1 and all(len(v) == 1 for v in groups.values())
+    return bool(groups) and all(len(v) == 1 for v in groups.values())
+
+
+def run_groups(f, trainers, slot_of, group_of, reqs, with_test):
+    """Enqueue the evaluation and the local epoch(s) of every trainer, one engine group at a time
+    (one group per device of a mesh; each group's launches go to its own device's stream, so the
+    devices run concurrently while this thread moves on). Returns {addr: (eval, fit)}."""
+    by_group: dict = {}
+    for a in trainers:
+        g = group_of(a)
+        by_group.setdefault(id(g), (g, []))[1].append(a)
+    out = {}
+    for g, addrs in by_group.values():
+        evs = g._run_eval_batch({slot_of(a): () for a in addrs if a in with_test})
+        fits = g._run_fit_batch({slot_of(a): reqs[a] for a in addrs})
+        for a in addrs:
+            out[a] = (evs.get(slot_of(a)), fits[slot_of(a)])
+    return out
 
 
 def aggregate(f, arrived, aggregator, final: bool) -> None:
@@ -71,12 +91,8 @@ def join(state, learner, aggregator, trainer: bool) -> None:
         trainers = [a for a in addrs if arrived[a][0]]
         out = {}
         if trainers:
-            group = f.local_nodes[trainers[0]].learner._engine.group
-            slot = {a: f.local_nodes[a].learner._engine.slot for a in trainers}
-            evs = group._run_eval_batch({slot[a]: () for a in trainers if arrived[a][3]})
-            fits = group._run_fit_batch({slot[a]: arrived[a][2] for a in trainers})
-            for a in trainers:
-                out[a] = (evs.get(slot[a]), fits[slot[a]])
+            out = run_groups(f, trainers, lambda a: f.local_nodes[a].learner._engine.slot, lambda a: f.local_nodes[a].learner._engine.group,
+                             {a: arrived[a][2] for a in trainers}, {a for a in trainers if arrived[a][3]})
         aggregate(f, {a: (arrived[a][1], None) for a in addrs}, aggregator, final)
         for hook in list(f.round_hooks):
             hook(round_, f)
