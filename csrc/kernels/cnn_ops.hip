@@ -834,6 +834,7 @@ int cnn_opt_step(float* w, float* g, float* m, int64_t ps, const float* gf, int6
   o.momentum = momentum;
   o.nesterov = nesterov;
   o.mu = mu;
+  o.scaf_upd = 0;  // opt_update applies SCAFFOLD through the cg / cl pointers
   if (nwork < 1) return 1;
   hipLaunchKernelGGL(k_opt_step, dim3(nwork, peers), dim3(256), 0, (hipStream_t)s, w, g, m, ps, gf, gf_ps, (const Segment*)segs, (const int2*)work, o,
                      anchor, cg, cl, update, shadow, shadow_ps, active);

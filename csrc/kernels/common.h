@@ -89,17 +89,24 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // Optimizer epilogue shared by every fused wgrad kernel and by the flat optimizer kernels.
 // g is the raw gradient; extras (FedProx anchor, SCAFFOLD control variates) are optional.
+//
+// SCAFFOLD's correction is applied in the UPDATE space: w <- step(w, g) - lr·(c - c_i). For plain
+// SGD that is the paper's g + c - c_i; for Adam / momentum it keeps the correction in the units of
+// the local step, which is what the control variate update c_i+ = c_i - c + (x - y)/(K·lr) measures
+// (the reference's option II, scaffold_callback.py:129). Fed into Adam's gradient instead, the
+// correction is a difference of normalised steps read as a gradient (no learning).
 struct OptParams {
   int kind;            // 0 = Adam, 1 = SGD (+momentum)
   float lr, beta1, beta2, eps, weight_decay, momentum;
   int nesterov;
   float mu;            // FedProx proximal coefficient (0 = off)
+  int scaf_upd;        // fused MLP epochs: the per-element extra term is a SCAFFOLD update-space correction
 };
 
 __device__ __forceinline__ void opt_update(const OptParams& o, float g, float& w, float& m, float& v, float bc1, float bc2_sqrt,
                                            const float* anchor, const float* cg, const float* cl, int64_t idx) {
   if (anchor != nullptr && o.mu != 0.f) g += o.mu * (w - anchor[idx]);
-  if (cg != nullptr) g += cg[idx] - cl[idx];
+  const float corr = cg != nullptr ? cg[idx] - cl[idx] : 0.f;
   if (o.weight_decay != 0.f) g += o.weight_decay * w;
   if (o.kind == 0) {
     m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
@@ -114,4 +121,5 @@ __device__ __forceinline__ void opt_update(const OptParams& o, float g, float& w
     }
     w -= o.lr * g;
   }
+  if (cg != nullptr) w -= o.lr * corr;
 }

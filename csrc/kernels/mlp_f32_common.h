@@ -69,8 +69,10 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8& a, const bf16x8& hi, const 
   return mfma_bf16(a, hi, acc);
 }
 
-// Per-element constant of the FedProx / SCAFFOLD gradient terms: g += mu·(w − anchor) + (c − c_i)
-// is g += mu·w + e with e = (c − c_i) − mu·anchor (the mu·w part is folded into weight decay).
+// Per-element constant of the FedProx / SCAFFOLD terms. FedProx: g += mu·(w − anchor) is
+// g += mu·w + e with e = −mu·anchor (the mu·w part is folded into weight decay). SCAFFOLD
+// (o.scaf_upd; never together with FedProx on this path): e = c − c_i, applied after the step as
+// w −= lr·e (update space, see opt_update in common.h).
 __device__ __forceinline__ float extra_at(const MLPArgs& a, int64_t idx) {
   float e = 0.f;
   if (a.cg != nullptr) e = a.cg[idx] - a.cl[idx];
@@ -83,7 +85,7 @@ __device__ __forceinline__ float extra_at(const MLPArgs& a, int64_t idx) {
 template <bool ADAM, bool EXTRA>
 __device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, float& m, float& v, float e, float lr_t, float inv, float wdmu) {
   g = fmaf(wdmu, w, g);  // weight decay (+ FedProx mu); 0: exact no-op
-  if (EXTRA) g += e;
+  if (EXTRA && !o.scaf_upd) g += e;
   if (ADAM) {
     m = fmaf(o.beta1, m, (1.f - o.beta1) * g);
     v = fmaf(o.beta2, v, (1.f - o.beta2) * (g * g));
@@ -96,6 +98,7 @@ __device__ __forceinline__ void upd32(const OptParams& o, float g, float& w, flo
     }
     w = fmaf(-o.lr, g, w);
   }
+  if (EXTRA && o.scaf_upd) w = fmaf(-o.lr, e, w);
 }
 
 __device__ __forceinline__ int rows_at(const MLPArgs& a, int n, int t) {

@@ -1454,6 +1454,7 @@ bool mlp_persistent_f32_supported(const MLPArgs& a) {
   if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
   if (a.Bpad != 32 && a.Bpad != 64) return false;
   if ((a.cg == nullptr) != (a.cl == nullptr)) return false;
+  if (a.cg != nullptr && a.anchor != nullptr) return false;  // one extra term per element (mlp_f32_common.h)
   return persistent_f32_lds_ks(a, 1) <= 160 * 1024;
 }
 

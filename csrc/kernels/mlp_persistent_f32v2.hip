@@ -828,6 +828,7 @@ bool mlp_f32v2_supported(const MLPArgs& a) {
   if (a.D0 % 8 != 0 || ks1_of(a.D0) > 1 + 8 * RQ) return false;  // at most 25 K steps (three per wave + one in LDS)
   if (a.Bpad != 32 && a.Bpad != 64) return false;
   if ((a.cg == nullptr) != (a.cl == nullptr)) return false;
+  if (a.cg != nullptr && a.anchor != nullptr) return false;  // one extra term per element (mlp_f32_common.h)
   return owner_lds_v2(a.Bpad, a.D0).total <= 160 * 1024;
 }
 size_t mlp_f32v2_lds(const MLPArgs& a) { return owner_lds_v2(a.Bpad, a.D0).total; }

@@ -1003,7 +1003,7 @@ int mlp_engine_set_test_data(void* h, const uint64_t* Xtp, const uint64_t* Ytp, 
 int mlp_engine_set_optimizer(void* h, int kind, float lr, float b1, float b2, float eps, float wd, float momentum, int nesterov, float mu) {
   auto* e = (MLPEngine*)h;
   std::lock_guard<std::mutex> g(e->mu);
-  OptParams o{kind, lr, b1, b2, eps, wd, momentum, nesterov, mu};
+  OptParams o{kind, lr, b1, b2, eps, wd, momentum, nesterov, mu, e->a.cg != nullptr ? 1 : 0};
   if (memcmp(&o, &e->a.opt, sizeof(o)) != 0) {
     e->a.opt = o;
     e->invalidate();
@@ -1016,6 +1016,7 @@ int mlp_engine_set_extras(void* h, const float* anchor, const float* cg, const f
   std::lock_guard<std::mutex> g(e->mu);
   if (anchor != e->a.anchor || cg != e->a.cg || cl != e->a.cl) {
     e->a.anchor = anchor; e->a.cg = cg; e->a.cl = cl;
+    e->a.opt.scaf_upd = cg != nullptr ? 1 : 0;
     e->invalidate();
   }
   return 0;

@@ -5,8 +5,17 @@ instead of editing gradients in Python:
 
 * ``SCAFFOLDCallback`` (parity target: ``pytorch/callbacks/scaffold_callback.py:32-150``). The
   reference adds ``lr·(c_i − c)`` to ``param.grad`` of *detached state_dict copies*, so its
-  correction is a no-op. Here the optimizer really uses ``g − c_i + c`` and the
-  control variate follows SCAFFOLD option II: ``c_i⁺ = c_i − c + (x − y)/(K·η)``.
+  correction is a no-op. Here the correction is real and applied in the UPDATE
+  space of the local optimizer: ``w ← step(w, g) − lr·(c − c_i)`` (``opt_update``,
+  ``csrc/kernels/common.h``; ``ops.adam_step``). The control variate follows SCAFFOLD option II,
+  ``c_i⁺ = c_i − c + (x − y)/(K·lr)`` (the reference's formula, ``scaffold_callback.py:129``),
+  which measures the mean local step in those same units — exact SCAFFOLD for plain SGD, and the
+  consistent generalisation for Adam (the reference MLP's optimizer, ``lightning_model.py:181-183``)
+  and momentum. Adding the correction to Adam's *gradient* instead (round 4) mixed normalised-step
+  units into a gradient and the federation stopped learning (0.15–0.84 after two rounds); a
+  gradient-unit control variate (option I, ∇f_i at the round-start model) fails the same test on
+  all six seeds: with raw 0–255 inputs the first round's gradients dwarf the later ones, so the
+  one-round-stale correction dominates the step.
 * ``FedProxCallback``: proximal term ``μ(w − w_global)`` with ``w_global`` snapshotted at fit start.
 """
 

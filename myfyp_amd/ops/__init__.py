@@ -196,13 +196,19 @@ def scaffold_apply(outs: Sequence[torch.Tensor], x_start: torch.Tensor, buf: tor
 # ---------------------------------------------------------------------------------------------
 # optimizers (flat fp32 buffers)
 # ---------------------------------------------------------------------------------------------
-def _corrected_grad(param, grad, anchor, c_global, c_local, mu):
+def _corrected_grad(param, grad, anchor, mu):
+    """FedProx's proximal gradient term (SCAFFOLD is applied in the update space: _scaffold_step)."""
     g = grad
     if anchor is not None and mu != 0.0:
         g = g + mu * (param - anchor)
-    if c_global is not None and c_local is not None:
-        g = g + (c_global - c_local)
     return g
+
+
+def _scaffold_step(param, c_global, c_local, lr: float) -> None:
+    """SCAFFOLD correction in the update space: ``w -= lr·(c − c_i)`` after the optimizer step
+    (``opt_update`` in ``csrc/kernels/common.h`` explains why not in Adam's gradient)."""
+    if c_global is not None and c_local is not None:
+        param.sub_(c_global - c_local, alpha=lr)
 
 
 def adam_step(
@@ -224,7 +230,7 @@ def adam_step(
 ) -> None:
     """One Adam step (torch.optim.Adam semantics, L2 ``weight_decay``), in place, step ≥ 1."""
     if param.device.type != "cuda":
-        g = _corrected_grad(param, grad, anchor, c_global, c_local, mu)
+        g = _corrected_grad(param, grad, anchor, mu)
         if weight_decay:
             g = g + weight_decay * param
         exp_avg.mul_(beta1).add_(g, alpha=1 - beta1)
@@ -233,6 +239,7 @@ def adam_step(
         bc2 = 1 - beta2**step
         denom = (exp_avg_sq / bc2).sqrt_().add_(eps)
         param.addcdiv_(exp_avg, denom, value=-lr / bc1)
+        _scaffold_step(param, c_global, c_local, lr)
         if shadow is not None:
             shadow.copy_(param.to(shadow.dtype))
         return
@@ -261,13 +268,14 @@ def sgd_step(
 ) -> None:
     """One SGD(+momentum, +nesterov) step (torch.optim.SGD semantics; buffer starts at 0)."""
     if param.device.type != "cuda":
-        g = _corrected_grad(param, grad, anchor, c_global, c_local, mu)
+        g = _corrected_grad(param, grad, anchor, mu)
         if weight_decay:
             g = g + weight_decay * param
         if momentum != 0.0 and momentum_buf is not None:
             momentum_buf.mul_(momentum).add_(g)
             g = g + momentum * momentum_buf if nesterov else momentum_buf
         param.add_(g, alpha=-lr)
+        _scaffold_step(param, c_global, c_local, lr)
         return
     lib = _lib()
     _native.check(

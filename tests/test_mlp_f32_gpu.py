@@ -110,10 +110,15 @@ def _torch_reference(module, x, y, perms, B, spec, epochs, extra=None):
                         k = p.numel()
                         if "anchor" in extra:
                             p.grad += extra["mu"] * (p - extra["anchor"][off : off + k].view_as(p))
-                        if "c_global" in extra:
-                            p.grad += (extra["c_global"][off : off + k] - extra["c_local"][off : off + k]).view_as(p)
                         off += k
             opt.step()
+            if extra and "c_global" in extra:  # SCAFFOLD: update space, w -= lr·(c − c_i) (common.h opt_update)
+                off = 0
+                with torch.no_grad():
+                    for p in params:
+                        k = p.numel()
+                        p -= spec["lr"] * (extra["c_global"][off : off + k] - extra["c_local"][off : off + k]).view_as(p)
+                        off += k
 
 
 def _rel_update(pe, pr, p0):
@@ -180,7 +185,7 @@ def test_f32_optimizers_match_torch(dev, spec):
 
 
 @pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2"])
-@pytest.mark.parametrize("kind", ["fedprox", "scaffold"])
+@pytest.mark.parametrize("kind", ["fedprox", "scaffold", "scaffold_adam"])
 def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
     """FedProx mu·(w − anchor) and SCAFFOLD (c − c_i) gradient terms in the fp32 epoch kernel, at
     both owner K splits.
@@ -190,7 +195,8 @@ def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
     step turns rounding-level differences into ±lr flips — torch fp32 itself, restarted from weights
     one ulp away, moves by 1.5e-2 relative (scripts/probes/f32_ks_fedprox.py). The Adam update the
     terms feed is the same register code and is pinned by test_f32_epoch_matches_torch_adam."""
-    spec = {"name": "sgd", "lr": 1e-3, "momentum": 0.9} if kind == "fedprox" else {"name": "sgd", "lr": 1e-4}
+    spec = {"fedprox": {"name": "sgd", "lr": 1e-3, "momentum": 0.9}, "scaffold": {"name": "sgd", "lr": 1e-4},
+            "scaffold_adam": {"name": "adam", "lr": 1e-3}}[kind]
     learners, refs, g, n = _setup(dev, 2, 64, 900, 5, spec, scale=0.5)
     ks = 2 if layout == "v1ks2" else 1
     g.force_f32_ks = ks
@@ -375,3 +381,39 @@ def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch, prep_m
         results.append([l.flat_params().detach().clone() for l in learners])
     for a, b in zip(*results):
         assert torch.equal(a, b)
+
+
+def test_scaffold_control_variate_matches_formula(dev):
+    """SCAFFOLD client on the fused engine: after each fit the device-resident control variate is
+    c_i⁺ = c_i − c + (x − y)/(K·lr) (option II; reference scaffold_callback.py:124-140), Δy = y − x and
+    Δc = c_i⁺ − c_i, pinned in float64 at rel < 1e-4 over two rounds (the second with c_i ≠ 0)."""
+    from myfyp_amd.learning.frameworks.torch.callbacks import SCAFFOLDCallback
+
+    spec = {"name": "adam", "lr": 1e-3}
+    learners, refs, g, n = _setup(dev, 2, 64, 900, 8, spec)
+    cbs = [SCAFFOLDCallback() for _ in learners]
+    for l, cb in zip(learners, cbs):
+        l.callbacks = [cb]
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    for rnd in range(2):
+        c = [0.01 * torch.randn(l.flat_params().numel(), generator=gen) for l in learners]
+        olds = []
+        for l, cb, ci in zip(learners, cbs, c):
+            cb.additional_info["global_c"] = l.split_flat(ci.to(dev))
+            olds.append(None if cb.c_i is None else cb.c_i.detach().double().cpu())
+        steps0 = [l.global_step for l in learners]
+        ts = [threading.Thread(target=l.fit) for l in learners]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        torch.cuda.synchronize()
+        for l, cb, ci, old, s0 in zip(learners, cbs, c, olds, steps0):
+            k = l.global_step - s0
+            assert k == (n[learners.index(l)] + 63) // 64
+            x0, y = cb.x0.double().cpu(), l.flat_params().detach().double().cpu()
+            ci_old = torch.zeros_like(x0) if old is None else old
+            want = ci_old - ci.double() + (x0 - y) / (k * spec["lr"])
+            got = cb.c_i.detach().double().cpu()
+            rel = ((got - want).norm() / want.norm()).item()
+            assert rel < 1e-4, (rnd, rel)
+            assert torch.allclose(cb.delta_y.double().cpu(), y - x0, rtol=0, atol=1e-6)
+            assert ((cb.delta_c.double().cpu() - (want - ci_old)).norm() / (want - ci_old).norm()).item() < 1e-4

@@ -126,13 +126,16 @@ def test_gossip_convergence_with_non_trainers(seed):
             nd.stop()
 
 
-@pytest.mark.parametrize("aggregator", [FedAvg, FedMedian, lambda: Scaffold(global_lr=1.0), FedProx], ids=["fedavg", "fedmedian", "scaffold", "fedprox"])
-def test_collective_workflow_aggregators(data, aggregator):
+_AGGS = [(FedAvg, 7), (FedMedian, 7), (FedProx, 7)] + [(lambda: Scaffold(global_lr=1.0), s) for s in (7, 1, 2, 3, 4, 5)]
+
+
+@pytest.mark.parametrize("aggregator,seed", _AGGS, ids=["fedavg", "fedmedian", "fedprox"] + [f"scaffold-seed{s}" for s in (7, 1, 2, 3, 4, 5)])
+def test_collective_workflow_aggregators(data, aggregator, seed):
     Settings.BATCH_SIZE = 16
     Settings.TRAIN_SET_SIZE = 3
     from myfyp_amd.utils.seed import set_seed
 
-    set_seed(7)
+    set_seed(seed)
     Federation.reset()
     fed = Federation.init()
     n = 4
@@ -155,14 +158,9 @@ def test_collective_workflow_aggregators(data, aggregator):
         accs = [dict(logs[nd.addr]["test_metric"]) for nd in nodes]
         first = max(a[0] for a in accs if 0 in a)  # evaluations of the initial model (trainers)
         last = max(a[2] for a in accs)  # final evaluation (all peers)
-        # learns. SCAFFOLD's control-variate correction under Adam (the reference MLP's optimizer)
-        # has no such guarantee: after two rounds it lands anywhere in 0.15..0.84 depending on which
-        # 3 of 4 peers win the train-set vote (0.147 / 0.35 / 0.42 / 0.60 / 0.63 / 0.68 in 6 runs,
-        # 0.21..0.84 in 12 earlier ones), so for it the check is only that it does not diverge
-        if isinstance(nodes[0].aggregator, Scaffold):
-            assert last >= first - 0.02, (first, last)
-        else:
-            assert last > first + 0.1 and last > 0.5, (first, last)
+        # learns — SCAFFOLD included, over six seeds (its control variates are gradients at the
+        # round-start model under Adam, option I: callbacks.py)
+        assert last > first + 0.1 and last > 0.5, (first, last)
     finally:
         for nd in nodes:
             nd.stop()
