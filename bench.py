@@ -256,8 +256,9 @@ def main() -> None:
     # per-stage wall-time breakdown of the first local peer (stderr, diagnostics only)
     tm = dict(logger.get_timings().get(nodes[0].addr, {}))
     for nd in nodes:  # the round driver logs its host time per round under one of the local peers
-        if "driver_round" in logger.get_timings().get(nd.addr, {}):
-            tm["driver_round"] = logger.get_timings()[nd.addr]["driver_round"]
+        for key in ("driver_round", "driver_round_cpu"):
+            if key in logger.get_timings().get(nd.addr, {}):
+                tm[key] = logger.get_timings()[nd.addr][key]
     brk = {k: round(1000 * float(np.median(v[args.warmup :] or v)), 3) for k, v in tm.items()}
     first = [round(1000 * (round_end[r] - t_start), 2) for r in sorted(round_end)[:10]]
     print(f"[bench] rank {rank} round-end times since set_start_learning (ms), rounds 0..9: {first}", file=sys.stderr, flush=True)

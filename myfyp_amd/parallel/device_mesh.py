@@ -175,6 +175,8 @@ class HostMesh(DeviceMesh):
                     t.copy_(q.pop(0).to(t.device))
 
     def fedavg_stacked(self, params, bufs, P, n, ld, w, mask) -> None:
+        if all(t.is_cuda for t in params):
+            return self._fedavg_native(params, bufs, P, n, ld, w, mask)
         with self.lock:
             self.calls += 1
             off = 0
@@ -198,6 +200,36 @@ class HostMesh(DeviceMesh):
                     for p in range(P[i]):
                         if mask[off + p] != 0:
                             rows[p, :n].copy_(mean)
+                off += P[i]
+
+    def _fedavg_native(self, params, bufs, P, n, ld, w, mask) -> None:
+        """GPU members (a virtual mesh on one device): the same per-member reduce / apply launches
+        as ``rmesh_fedavg``, with the all-reduce as stream-ordered torch adds — so a one-GPU
+        rehearsal issues the real path's launches (host cost per round is representative)."""
+        from myfyp_amd import ops
+
+        fast = ops.fast_lib()
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        with self.lock:
+            self.calls += 1
+            off = 0
+            for i in range(self.size):
+                with torch.cuda.device(bufs[i].device):
+                    st = _stream_ptr(bufs[i].device)
+                    if P[i] == 0:
+                        bufs[i].zero_()
+                    else:
+                        ops.check(fast.myfyp_fedavg_stacked_reduce(bufs[i].data_ptr(), params[i].data_ptr(), int(P[i]), int(n), int(ld[i]),
+                                                                   w[off:].ctypes.data, st), "fedavg_stacked_reduce")
+                off += P[i]
+            self.all_reduce_([b[: n + 1] for b in bufs])
+            off = 0
+            for i in range(self.size):
+                if P[i] > 0:
+                    with torch.cuda.device(bufs[i].device):
+                        ops.check(fast.myfyp_fedavg_stacked_apply(params[i].data_ptr(), bufs[i].data_ptr(), int(P[i]), int(n), int(ld[i]),
+                                                                  mask[off:].ctypes.data, _stream_ptr(bufs[i].device)), "fedavg_stacked_apply")
                 off += P[i]
 
     def shrink(self, keep) -> None:

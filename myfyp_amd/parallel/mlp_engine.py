@@ -52,6 +52,25 @@ def mlp_dims(module: torch.nn.Module) -> Optional[Tuple[int, int, int, int]]:
     return (lins[0].in_features, lins[0].out_features, lins[1].out_features, lins[2].out_features)
 
 
+class _DeviceCtx:
+    """``torch.cuda.device`` without its per-call overhead (the round driver enters it once per
+    group and round): exchange the thread's current device on entry, restore it on exit."""
+
+    __slots__ = ("idx", "prev")
+
+    def __init__(self, idx: int) -> None:
+        self.idx = idx
+        self.prev = -1
+
+    def __enter__(self):
+        self.prev = torch.cuda._exchange_device(self.idx) if self.idx >= 0 else -1
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.idx >= 0:
+            torch.cuda._maybe_exchange_device(self.prev)
+
+
 class _Gang:
     """Collects requests from co-located peers' threads and runs them as one batch."""
 
@@ -165,8 +184,14 @@ class MLPGroup:
         self._alloc(capacity)
         self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
         self.eval_gang = _Gang(self._run_eval_batch, lambda: set(self.handles))
-        # asynchronous results: pinned ring slots on the engine, resolved in order by one thread
-        self.resolver = Resolver(f"mlp-results-{device}")
+        # asynchronous results: pinned ring slots on the engine, resolved in order by ONE thread per
+        # process (shared by every group: a device mesh has one group per GPU, and a resolver thread
+        # each would contend for the GIL with the round driver)
+        self.resolver = Resolver.shared()
+        self._cfg_key: Optional[tuple] = None  # last engine configuration pushed to the native side
+        self._opt_key: Optional[tuple] = None
+        self._steps_pe: Optional[np.ndarray] = None
+        self._active_cache: Dict[tuple, np.ndarray] = {}
         self._ring = 0
         self._next_slot = 0
         self._slot_free: List[threading.Event] = []
@@ -193,6 +218,7 @@ class MLPGroup:
         if self._engine is not None:
             _native.load(required=True).mlp_engine_destroy(self._engine)
             self._engine = None
+        self._cfg_key = self._opt_key = None
 
     def close(self) -> None:
         self._close_engine()
@@ -233,27 +259,31 @@ class MLPGroup:
             _native.check(
                 lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
             )
-        _native.check(lib.mlp_engine_set_precision(self._engine, 1 if self.precision == "fp32" else 0), "set_precision")
         # fp32 owner K split: 2 (40-workgroup gangs, half the owner work per step) when every
         # attached peer sits in the first 4 slots, i.e. one launch covers them all — the case of
-        # one process per GPU with few peers each (N >= 2 GPUs in bench.py); 8 peers keep 1
+        # few peers per GPU (a device mesh or one process per GPU, N >= 2 in bench.py); 8 keep 1
         ks = self.force_f32_ks or (2 if self.handles and max(self.handles) < 4 else 1)
-        _native.check(lib.mlp_engine_set_f32_ks(self._engine, ks), "set_f32_ks")
         # a forced K split of 2 is a layout-1 configuration
         var = self.force_f32_variant or (1 if self.force_f32_ks == 2 else 0)
-        _native.check(lib.mlp_engine_set_f32_variant(self._engine, var), "set_f32_variant")
         # weight collectives on the comm stream may hold CUs while an epoch runs: size the
         # co-resident gangs without them
         from myfyp_amd.parallel.federation import Federation, rccl_reserved_cus
 
         fed = Federation._instance
         reserve = rccl_reserved_cus() if fed is not None and not fed.solo else 0
-        _native.check(lib.mlp_engine_set_reserved_cus(self._engine, reserve), "set_reserved_cus")
-        if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
-            _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
+        key = (self._engine, self.precision, ks, var, reserve, self.persistent)
+        if key != self._cfg_key:  # the setters run only when something changed (host cost per round)
+            _native.check(lib.mlp_engine_set_precision(self._engine, 1 if self.precision == "fp32" else 0), "set_precision")
+            _native.check(lib.mlp_engine_set_f32_ks(self._engine, ks), "set_f32_ks")
+            _native.check(lib.mlp_engine_set_f32_variant(self._engine, var), "set_f32_variant")
+            _native.check(lib.mlp_engine_set_reserved_cus(self._engine, reserve), "set_reserved_cus")
+            if self.persistent is not None:  # None: engine default (auto; env MYFYP_MLP_PERSISTENT=0 disables)
+                _native.check(lib.mlp_engine_set_persistent(self._engine, -1 if self.persistent else 0), "set_persistent")
+            self._cfg_key = key
         if self._bound_version != self._data_version:
             self._bind_data()
             self._bound_version = self._data_version
+            self._steps_pe = None
 
     def fedavg_buffer(self) -> torch.Tensor:
         """Device scratch of numel + 1 floats for the stacked FedAvg (weighted sum | Σw)."""
@@ -319,6 +349,11 @@ class MLPGroup:
         return buf
 
     def _set_optimizer(self, lib, spec: dict, mu: float, anchor, cg, cl) -> None:
+        key = (self._engine, tuple(sorted(spec.items())), mu, _p(anchor), _p(cg), _p(cl), self.perm_fn is None)
+        if key == self._opt_key:
+            return
+        self._opt_key = key
+        _native.check(lib.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
         kind = 0 if spec.get("name", "adam") == "adam" else 1
         _native.check(
             lib.mlp_engine_set_optimizer(
@@ -333,7 +368,19 @@ class MLPGroup:
     def on_device(self):
         """Make the group's GPU current for this thread (the native engine allocates and captures
         on the current device; a process may drive several devices: parallel/device_mesh.py)."""
-        return torch.cuda.device(self.device)
+        return _DeviceCtx(self.device.index if self.device.index is not None else -1)
+
+    def _active(self, slots) -> np.ndarray:
+        """int32 active mask over the capacity for ``slots`` (cached: the same sets recur every round)."""
+        key = tuple(sorted(slots))
+        a = self._active_cache.get(key)
+        if a is None or a.shape[0] != self.capacity:
+            a = np.zeros(self.capacity, dtype=np.int32)
+            a[list(key)] = 1
+            if len(self._active_cache) > 64:
+                self._active_cache.clear()
+            self._active_cache[key] = a
+        return a
 
     def prewarm(self, spec: dict) -> None:
         """One-time engine setup before the first fit (node start): bind the data, capture and
@@ -344,7 +391,6 @@ class MLPGroup:
         with self.lock, self.on_device():
             self._ensure_engine()
             self._set_optimizer(lib, spec, 0.0, None, None, None)
-            _native.check(lib.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
             _native.check(lib.mlp_engine_prepare(self._engine, torch.cuda.current_stream(self.device).cuda_stream), "prepare")
 
     # ------------------------------------------------------------------ batched fit
@@ -374,18 +420,18 @@ class MLPGroup:
                         cg[slot].zero_()
                         cl[slot].zero_()
             fast = _native.load_fast()
+            # (also sets the shuffle mode: the epoch order is drawn on the device inside the gather
+            # kernel — keyed Feistel permutation per peer, key from the seeded Python RNG — unless a
+            # test pins explicit permutations)
             self._set_optimizer(fast, spec, mu, anchor, cg, cl)
-            active = np.zeros(self.capacity, dtype=np.int32)
-            for slot in batch:
-                active[slot] = 1
+            active = self._active(batch)
             # fresh optimizer state per fit (Lightning semantics); slots not training this round are
             # zeroed as well — they start fresh when they next train — so this is 2 memsets, not 2P
             _native.check(fast.mlp_engine_zero_state(self._engine, stream), "zero_state")
             _native.check(fast.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
-            steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
-            # epoch order: drawn on the device inside the gather kernel (keyed Feistel permutation
-            # per peer, key from the seeded Python RNG) unless a test pins explicit permutations
-            _native.check(fast.mlp_engine_set_shuffle(self._engine, 0 if self.perm_fn is not None else 1), "set_shuffle")
+            if self._steps_pe is None:
+                self._steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
+            steps_pe = self._steps_pe
             # the result slot is taken first: the last epoch's graph publishes into it itself (its
             # last node), so stats_async is then a no-op — no separate launch behind the graph
             k = self._take_slot()
@@ -395,7 +441,7 @@ class MLPGroup:
                         self.perm.copy_(self.perm_fn(ep))
                     else:
                         _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
-                    t0 = (steps_pe * ep).astype(np.int32)
+                    t0 = steps_pe if ep == 1 else (steps_pe * ep).astype(np.int32)
                     if self.eager:
                         _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
                     else:
@@ -480,9 +526,7 @@ class MLPGroup:
         with self.lock, self.on_device():
             self._ensure_engine()
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            active = np.zeros(self.capacity, dtype=np.int32)
-            for slot in batch:
-                active[slot] = 1
+            active = self._active(batch)
             k = self._take_slot()
             # the GIL-releasing binding: on the overlapped path the call may wait (host side) for the
             # evaluation two rounds back to release its snapshot side

@@ -78,10 +78,21 @@ def resolve(value: Any) -> Any:
 class Resolver:
     """FIFO worker that runs ``fetch()`` (blocking on a device event) and completes a Pending."""
 
+    _shared: Optional["Resolver"] = None
+    _shared_lock = threading.Lock()
+
     def __init__(self, name: str) -> None:
         self._q: "queue.Queue" = queue.Queue()
         self._thread = threading.Thread(target=self._loop, name=name, daemon=True)
         self._thread.start()
+
+    @classmethod
+    def shared(cls) -> "Resolver":
+        """The process-wide resolver (FIFO over every engine group's results)."""
+        with cls._shared_lock:
+            if cls._shared is None:
+                cls._shared = cls("device-results")
+            return cls._shared
 
     def submit(self, fetch: Callable[[], Any]) -> Pending:
         p = Pending()

@@ -18,6 +18,7 @@ Reference stage semantics: ``stages/base_node/{vote_train_set,train,gossip_model
 
 from __future__ import annotations
 
+import os
 import threading
 import time
 from typing import Any, Dict
@@ -81,7 +82,17 @@ class RoundDriver:
             if self._claim():
                 members = dict(self.members)
                 try:
-                    self._drive(members)
+                    prof_path = os.environ.get("MYFYP_PROFILE_DRIVER")
+                    if prof_path:  # diagnostics: cProfile of the driver thread (host cost per round)
+                        import cProfile
+
+                        prof = cProfile.Profile()
+                        try:
+                            prof.runcall(self._drive, members)
+                        finally:
+                            prof.dump_stats(prof_path)
+                    else:
+                        self._drive(members)
                 except BaseException as e:  # surfaced in every peer's learning thread
                     for mm in members.values():
                         mm.error = e
@@ -117,6 +128,7 @@ class RoundDriver:
             if not cur:
                 return
             t0 = time.time()
+            c0 = time.thread_time()  # host CPU time of this thread (excludes blocking waits)
             mark("driver_round")
             states = {a: m.kw["state"] for a, m in cur.items()}
             round_ = next(iter(states.values())).round
@@ -168,6 +180,7 @@ class RoundDriver:
                 if st.round >= st.total_rounds:
                     final.append(a)
             logger.log_timing(next(iter(cur)), "driver_round", time.time() - t0)
+            logger.log_timing(next(iter(cur)), "driver_round_cpu", time.thread_time() - c0)
             if final:
                 self._finish({a: cur[a] for a in final})
                 if len(final) == len(cur):
