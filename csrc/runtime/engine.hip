@@ -646,9 +646,16 @@ static bool gang_event_always() {
   }();
   return v != 0;
 }
-GangOrder& gang_order() {
-  static GangOrder g;
-  return g;
+// One order per DEVICE: persistent epochs only compete for the CUs of their own GPU. A device mesh
+// (one process driving several GPUs, csrc/runtime/rccl_mesh.hip) must not chain device d's epoch
+// behind device d-1's (that would serialise the GPUs), and an event may only be recorded on a stream
+// of the device it was created on.
+#define GANG_ORDER_MAX_DEVICES 64
+GangOrder& gang_order(hipStream_t s) {
+  static GangOrder g[GANG_ORDER_MAX_DEVICES];
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= GANG_ORDER_MAX_DEVICES) dev = 0;
+  return g[dev];
 }
 
 }  // namespace
@@ -1158,7 +1165,7 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
     CHECK_HIP(hipStreamWaitEvent(s, e->ev_gath[buf], 0));
   }
   if (e->graph_persistent) {
-    GangOrder& go = gang_order();
+    GangOrder& go = gang_order(s);
     std::lock_guard<std::mutex> og(go.mu);
     if (!go.ev) CHECK_HIP(hipEventCreateWithFlags(&go.ev, hipEventDisableTiming));
     if (gang_event_always()) {

@@ -52,6 +52,43 @@ def mlp_dims(module: torch.nn.Module) -> Optional[Tuple[int, int, int, int]]:
     return (lins[0].in_features, lins[0].out_features, lins[1].out_features, lins[2].out_features)
 
 
+class _CallTimer:
+    """Diagnostics (env ``MYFYP_TIME_CALLS=<path>``): host time between marks of the round's engine
+    calls, per label, summed over the run and written as JSON at exit."""
+
+    def __init__(self) -> None:
+        import os
+
+        self.path = os.environ.get("MYFYP_TIME_CALLS")
+        self.on = bool(self.path)
+        self.tot: Dict[str, list] = {}
+        self._t = threading.local()
+        if self.on:
+            import atexit
+
+            atexit.register(self.dump)
+
+    def mark(self, label: Optional[str]) -> None:
+        if not self.on:
+            return
+        now = time.perf_counter()
+        last = getattr(self._t, "t", None)
+        if label is not None and last is not None:
+            ent = self.tot.setdefault(label, [0, 0.0])
+            ent[0] += 1
+            ent[1] += now - last
+        self._t.t = now
+
+    def dump(self) -> None:
+        import json
+
+        with open(self.path, "w") as f:
+            json.dump({k: {"calls": n, "us_mean": round(1e6 * t / max(1, n), 2)} for k, (n, t) in sorted(self.tot.items())}, f, indent=1)
+
+
+_CALL_T = _CallTimer()
+
+
 class _DeviceCtx:
     """``torch.cuda.device`` without its per-call overhead (the round driver enters it once per
     group and round): exchange the thread's current device on entry, restore it on exit."""
@@ -396,6 +433,7 @@ class MLPGroup:
     # ------------------------------------------------------------------ batched fit
     def _run_fit_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
+        _CALL_T.mark(None)
         with self.lock, self.on_device():
             self._ensure_engine()
             stream = torch.cuda.current_stream(self.device).cuda_stream
@@ -425,16 +463,19 @@ class MLPGroup:
             # test pins explicit permutations)
             self._set_optimizer(fast, spec, mu, anchor, cg, cl)
             active = self._active(batch)
+            _CALL_T.mark("fit_prep")
             # fresh optimizer state per fit (Lightning semantics); slots not training this round are
             # zeroed as well — they start fresh when they next train — so this is 2 memsets, not 2P
             _native.check(fast.mlp_engine_zero_state(self._engine, stream), "zero_state")
             _native.check(fast.mlp_engine_begin(self._engine, active.ctypes.data, stream), "begin")
+            _CALL_T.mark("fit_zero_begin")
             if self._steps_pe is None:
                 self._steps_pe = np.array([(n + self.B - 1) // self.B for n in self.n_train], dtype=np.int32)
             steps_pe = self._steps_pe
             # the result slot is taken first: the last epoch's graph publishes into it itself (its
             # last node), so stats_async is then a no-op — no separate launch behind the graph
             k = self._take_slot()
+            _CALL_T.mark("fit_take_slot")
             try:
                 for ep in range(epochs):
                     if self.perm_fn is not None:
@@ -445,12 +486,16 @@ class MLPGroup:
                     if self.eager:
                         _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
                     else:
+                        _CALL_T.mark("fit_seed")
                         _native.check(fast.mlp_engine_run_epoch_pub(self._engine, t0.ctypes.data, k if ep == epochs - 1 else -1, stream), "run_epoch")
+                        _CALL_T.mark("fit_run_epoch")
                 _native.check(fast.mlp_engine_stats_async(self._engine, k, stream), "stats_async")
+                _CALL_T.mark("fit_stats_async")
             except BaseException:
                 self._slot_free[k].set()  # nothing will fetch this slot: give it back to the ring
                 raise
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=False))
+            _CALL_T.mark("fit_submit")
         out = {}
         for slot in batch:
             n = max(1, self.n_train[slot] * epochs)
@@ -523,15 +568,21 @@ class MLPGroup:
 
     def _run_eval_batch(self, batch: Dict[int, tuple]) -> Dict[int, tuple]:
         lib = _native.load(required=True)
+        _CALL_T.mark(None)
         with self.lock, self.on_device():
             self._ensure_engine()
             stream = torch.cuda.current_stream(self.device).cuda_stream
             active = self._active(batch)
             k = self._take_slot()
-            # the GIL-releasing binding: on the overlapped path the call may wait (host side) for the
-            # evaluation two rounds back to release its snapshot side
-            _native.check(lib.mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
+            # GIL kept (PyDLL): the call only enqueues, except that on the overlapped path it may poll
+            # (host side, bounded by GPU progress alone) for the evaluation two rounds back to release
+            # its snapshot side. Releasing the GIL here handed it to other threads for up to the
+            # switch interval per group and round (device mesh: 8 groups per round)
+            _CALL_T.mark("eval_prep")
+            _native.check(_native.load_fast().mlp_engine_eval_async(self._engine, active.ctypes.data, k, stream), "eval_async")
+            _CALL_T.mark("eval_async")
             raw = self.resolver.submit(lambda k=k: self._fetch(k, with_conf=True))
+            _CALL_T.mark("eval_submit")
         D3 = self.dims[3]
         return {slot: raw.map(lambda r, s=slot: (float(r[0][s]) / max(1, self.n_test[s]), r[2][s, :D3, :D3].copy())) for slot in batch}
 
