@@ -318,15 +318,19 @@ int shmc_barrier(void* handle, double timeout_s) {
 // This rank leaves: it never joins a later generation. 0 ok, 1 already gone. The kLeft bit tells
 // the others it left on purpose (after completing every collective it had joined), as opposed to
 // an eviction of an unresponsive rank (shmc_left_clean).
-int shmc_leave(void* handle) {
+// shmc_leave_ex(clean = 0): leave WITHOUT the kLeft bit — a rank that could not confirm every
+// collective it joined (timeout, error) must look like an eviction, so the survivors recover.
+int shmc_leave_ex(void* handle, int clean) {
   Handle* h = static_cast<Handle*>(handle);
   RankCtl* me = h->ctl(h->rank);
+  const uint64_t bits = kGone | (clean ? kLeft : 0);
   uint64_t s = me->status.load(std::memory_order_acquire);
   while (!(s & kGone)) {
-    if (me->status.compare_exchange_weak(s, kGone | kLeft | (s + 1), std::memory_order_acq_rel, std::memory_order_acquire)) return 0;
+    if (me->status.compare_exchange_weak(s, bits | ((s + 1) & kGenMask), std::memory_order_acq_rel, std::memory_order_acquire)) return 0;
   }
   return 1;
 }
+int shmc_leave(void* handle) { return shmc_leave_ex(handle, 1); }
 
 // Bitmask of the ranks that left on purpose (shmc_leave), not by eviction.
 uint64_t shmc_left_clean(void* handle) {

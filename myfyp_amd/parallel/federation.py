@@ -672,13 +672,17 @@ class Federation:
         ranks stop waiting for it at their next gather (shared-memory membership protocol)."""
         if self.departed or not self.collective:
             return
-        self.departed = True
-        if self._frozen is not None:
-            # inside a weights section this rank already agreed to take part: it completes the
-            # section's collectives and leaves at its exit (the others would wait for it otherwise)
-            self._depart_deferred = True
-        elif self.shm is not None:
-            self._leave_clean()
+        # under the section lock: a weights section that already gathered the membership (and so
+        # counts on this rank) must see the departure only at its exit (ADVICE r4: reading
+        # _frozen unlocked let a rank leave between the gather and the freeze)
+        with self._section_lock:
+            self.departed = True
+            if self._frozen is not None:
+                # inside a weights section this rank already agreed to take part: it completes the
+                # section's collectives and leaves at its exit (the others would wait for it otherwise)
+                self._depart_deferred = True
+            elif self.shm is not None:
+                self._leave_clean()
         logger.warning(f"rank{self.rank}", "last local peer stopped mid-experiment: rank departs the federation")
 
     def _leave_clean(self) -> None:
@@ -687,17 +691,29 @@ class Federation:
         after finishing them (``left_clean``) rather than one that failed inside them: no recovery,
         and the confirmed round result keeps the leaver's share."""
         deadline = time.perf_counter() + float(Settings.COLLECTIVE_TIMEOUT)
+        all_done = True
         for works, _, _, _ in self._pending:
             for w in works:
-                while w is not None and time.perf_counter() < deadline:
+                if w is None:
+                    continue
+                while True:
                     try:
                         if w.is_completed():
                             break
-                    except Exception:
+                    except Exception:  # a failed collective is not a completed one
+                        all_done = False
+                        break
+                    if time.perf_counter() >= deadline:
+                        all_done = False
                         break
                     time.sleep(0.0005)
         self._pending.clear()
-        self.shm.leave()
+        # kLeft ("left clean") only when every collective this rank joined was seen to complete;
+        # otherwise leave as an eviction, so the survivors recover instead of trusting its share
+        # (ADVICE r4)
+        if not all_done:
+            logger.warning(f"rank{self.rank}", "leaving with unconfirmed collectives: the others will treat this rank as failed")
+        self.shm.leave(clean=all_done)
 
     def _apply_members(self, ranks: List[int], force: bool = False) -> None:
         """Every survivor calls this with the same participant set at the same gather (``force``:
@@ -970,7 +986,11 @@ class Federation:
             if missing:
                 logger.info(f"rank{self.rank}", f"{what}: ranks {missing} left after completing it")
                 # the gather agreed the new member set (every member took part): adopt it, also
-                # for the frozen view of a deferred confirmation
+                # for the frozen view of a deferred confirmation. Collectives still pending on the
+                # old group are confirmed first: rebuilding aborts the old group, which would fail
+                # them and trigger the recovery a clean leave is meant to avoid
+                if self._pending and what != "deferred all_reduce":
+                    self._confirm_pending()
                 self._apply_members(ranks)
                 if self._frozen is not None:
                     self._frozen = (self._frozen[0], list(self.members))

@@ -54,6 +54,8 @@ def _load() -> Optional[ctypes.CDLL]:
     lib.shmc_allgather_m.argtypes = [vp, ctypes.c_char_p, u64, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), d, d]
     lib.shmc_leave.restype = i
     lib.shmc_leave.argtypes = [vp]
+    lib.shmc_leave_ex.restype = i
+    lib.shmc_leave_ex.argtypes = [vp, i]
     lib.shmc_heartbeat.restype = None
     lib.shmc_heartbeat.argtypes = [vp]
     lib.shmc_alive.restype = u64
@@ -155,9 +157,11 @@ class ShmCollective:
         base = ctypes.addressof(self._out)
         return ranks, {r: pickle.loads(ctypes.string_at(base + r * self.slot, int(self._lens[r]))) for r in ranks}
 
-    def leave(self) -> bool:
-        """Leave the job: later all-gathers of the other ranks no longer wait for this one."""
-        return self._lib.shmc_leave(self._h) == 0
+    def leave(self, clean: bool = True) -> bool:
+        """Leave the job: later all-gathers of the other ranks no longer wait for this one.
+        ``clean=False``: leave as if evicted (the others must not count on this rank having
+        completed the collectives it joined)."""
+        return self._lib.shmc_leave_ex(self._h, 1 if clean else 0) == 0
 
     def heartbeat(self) -> None:
         self._lib.shmc_heartbeat(self._h)

@@ -28,8 +28,13 @@ class StartLearningStage(Stage):
             logger.experiment_started(state.addr, state.experiment)
         begin = time.time()
         logger.info(state.addr, "⏳ Waiting initialization.")
-        state.model_initialized_lock.acquire()
-        if state.round is None:  # learning stopped while waiting for the initial model (NodeState.clear)
+        lock = state.model_initialized_lock
+        lock.acquire()
+        # learning stopped while waiting for the initial model (NodeState.clear released the lock
+        # it replaced). Test the lock's identity too: a new experiment may already have set a round
+        # on the cleared state before this thread ran, and this stale stage must not join it
+        # 
+        if state.round is None or state.model_initialized_lock is not lock:
             logger.info(state.addr, "Learning stopped before the model was initialized.")
             return None
         communication_protocol.broadcast(communication_protocol.build_msg(ModelInitializedCommand.get_name()))

@@ -1,16 +1,22 @@
-"""BASELINE config 5 in small: non-IID Dirichlet(0.5) partitions, ResNet-18, FedProx, on the fused
-HIP CNN engine (bf16 operands) against the torch autograd fp32 learner on the SAME partitions.
+"""BASELINE config 5 in small, on the GPU: non-IID Dirichlet(0.5) partitions, ResNet-18, FedProx,
+ONE PEER KILLED in round 1, eight rounds — the fused HIP CNN engine (bf16 operands) against the
+torch autograd fp32 learner (the oracle) on the SAME partitions and the same fault.
 
-Round 3 logged config 5 at chance for its 3 timed rounds; the round-4 bisect
-(``profiles/r4a_config5_bisect``) showed that the torch fp32 learner on identical partitions stays
-at chance for the same ~5 rounds before it climbs, and so does FedAvg on the same split without
-dropout: a slow start of this non-IID problem, not an engine defect. This test pins that the engine
-trains the same problem as torch: per-round mean training loss within the spread of two torch runs
-that differ only in their batch shuffle (the engine shuffles differently again), plus a margin for
-bf16. Reference semantics: the Dirichlet partitioner (/root/reference/p2pfl/learning/dataset/
-partition_strategies.py:161-430), FedAvg-style aggregation of what arrived (aggregator.py:191-208).
+What is pinned:
+
+* the survivors finish every round, agree (equal models), and their accuracy after the last round
+  is within a stated margin of the oracle's (the mean of two torch runs that differ only in their
+  batch shuffle): ``|acc_engine − acc_torch| ≤ max(2·spread, 0.08)`` (margin calibrated on the GPU,
+  ``profiles/r5_config5_test/README.md``);
+* per-round mean training loss within the torch shuffle spread plus a bf16 margin, and falling.
+
+Reference semantics: the Dirichlet partitioner (``/root/reference/p2pfl/learning/dataset/
+partition_strategies.py:161-430``); aggregating whatever arrived when a peer is gone
+(``/root/reference/p2pfl/learning/aggregators/aggregator.py:191-208``); the acceptance bar of
+``/root/reference/test/node_test.py:128-132``.
 """
 
+import os
 import sys
 import time
 
@@ -20,9 +26,12 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+PEERS, ROUNDS, KILLED = 4, 8, 3
 
-def _run(fused: bool, seed: int, rounds: int = 3, peers: int = 3):
+
+def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS):
     from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
+    from myfyp_amd.fault_injection import kill_at
     from myfyp_amd.learning.aggregators import FedProx
     from myfyp_amd.learning.dataset.partition_strategies import DirichletPartitionStrategy
     from myfyp_amd.learning.dataset.synthetic import synthetic_cifar10
@@ -34,7 +43,7 @@ def _run(fused: bool, seed: int, rounds: int = 3, peers: int = 3):
     from myfyp_amd.parallel.federation import Federation
     from myfyp_amd.settings import Settings
     from myfyp_amd.utils.seed import set_seed
-    from myfyp_amd.utils.utils import wait_to_finish
+    from myfyp_amd.utils.utils import check_equal_models, wait_to_finish
 
     saved = (Settings.USE_FUSED_KERNELS, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW)
     Settings.USE_FUSED_KERNELS = fused
@@ -45,7 +54,7 @@ def _run(fused: bool, seed: int, rounds: int = 3, peers: int = 3):
     CNNGroup.reset_all()
     Federation.reset()
     fed = Federation.init()
-    data = synthetic_cifar10(1024 * peers, 256 * peers, seed=7, similarity=0.85, noise=1.2, modes=4, label_noise=0.1)
+    data = synthetic_cifar10(1024 * peers, 256 * peers, seed=7, similarity=0.6, noise=1.0, modes=4, label_noise=0.05)
     parts = data.generate_partitions(peers, DirichletPartitionStrategy, alpha=0.5)
     exp = f"c5-{int(fused)}-{seed}-{time.time_ns()}"
     nodes = [
@@ -53,20 +62,24 @@ def _run(fused: bool, seed: int, rounds: int = 3, peers: int = 3):
              aggregator=FedProx(proximal_mu=0.01), exp_name=exp, learner_kwargs={"batch_size": 64})
         for g in range(peers)
     ]
+    live = [nd for g, nd in enumerate(nodes) if g != KILLED]
     try:
         for nd in nodes:
             nd.start()
         assert all((nd.learner._engine is not None) == fused for nd in nodes)
         fed.finalize()
+        kill_at(nodes[KILLED], "TrainStage", round=1)
         nodes[0].set_start_learning(rounds=rounds, epochs=1)
-        wait_to_finish(nodes, timeout=600)
+        wait_to_finish(live, timeout=900)
+        assert all(nd.learning_workflow.history.count("RoundFinishedStage") == rounds for nd in live)
+        check_equal_models(live, atol=1e-4 if fused else 1e-5)
         local = logger.get_local_logs()[exp]
         loss = []
         for r in range(rounds):
-            vals = [local[r][nd.addr]["train_loss"][-1][1] for nd in nodes if nd.addr in local.get(r, {}) and local[r][nd.addr].get("train_loss")]
+            vals = [local[r][nd.addr]["train_loss"][-1][1] for nd in live if nd.addr in local.get(r, {}) and local[r][nd.addr].get("train_loss")]
             loss.append(float(np.mean(vals)))
         logs = logger.get_global_logs()[exp]
-        acc = float(np.mean([dict(logs[nd.addr]["test_metric"])[rounds] for nd in nodes]))
+        acc = float(np.mean([dict(logs[nd.addr]["test_metric"])[rounds] for nd in live]))
         return loss, acc
     finally:
         for nd in nodes:
@@ -76,18 +89,21 @@ def _run(fused: bool, seed: int, rounds: int = 3, peers: int = 3):
         Settings.USE_FUSED_KERNELS, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW = saved
 
 
-def test_config5_engine_trains_like_torch_on_dirichlet_fedprox():
+def test_config5_engine_matches_torch_oracle_with_dropout():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     eng, acc_e = _run(True, 1)
     t1, acc_1 = _run(False, 1)
     t2, acc_2 = _run(False, 2)
-    print(f"[config5] engine loss {eng} acc {acc_e:.3f} | torch(1) {t1} acc {acc_1:.3f} | torch(2) {t2} acc {acc_2:.3f}", file=sys.stderr)
+    print(f"[config5] engine loss {np.round(eng, 4).tolist()} acc {acc_e:.4f} | torch(1) {np.round(t1, 4).tolist()} acc {acc_1:.4f} | "
+          f"torch(2) {np.round(t2, 4).tolist()} acc {acc_2:.4f}", file=sys.stderr)
+    acc_t, spread = 0.5 * (acc_1 + acc_2), abs(acc_1 - acc_2)
+    assert acc_t > 0.5, (acc_1, acc_2)  # the oracle learns this problem within the eight rounds
+    assert abs(acc_e - acc_t) <= max(2 * spread, 0.08), (acc_e, acc_1, acc_2)
     for r in range(len(eng)):
         ref = 0.5 * (t1[r] + t2[r])
-        spread = abs(t1[r] - t2[r])
         assert np.isfinite(eng[r]), eng
-        # shuffle spread of torch itself, plus 15 % of the loss for bf16 operands and the engine's
-        # own batch order
-        assert abs(eng[r] - ref) <= 2 * spread + 0.15 * ref, (r, eng, t1, t2)
+        # torch's own shuffle spread, plus 15 % of the loss for bf16 operands and the engine's own
+        # batch order
+        assert abs(eng[r] - ref) <= 2 * abs(t1[r] - t2[r]) + 0.15 * ref, (r, eng, t1, t2)
     assert eng[-1] < eng[0], eng  # the local objective goes down over the rounds

@@ -101,3 +101,44 @@ def test_clean_leave_with_a_deferred_all_reduce(tmp_path):
         assert o["result"] == [6.0] * 8, o
         assert o["members"] == [0, 1], o
         assert o["next"] == [3.0] * 4, o
+
+
+class _FakeShm:
+    def __init__(self):
+        self.clean = None
+
+    def leave(self, clean=True):
+        self.clean = clean
+        return True
+
+
+class _Work:
+    def __init__(self, mode):
+        self.mode = mode
+
+    def is_completed(self):
+        if self.mode == "raise":
+            raise RuntimeError("collective failed")
+        return self.mode == "done"
+
+
+@pytest.mark.parametrize("mode,clean", [("done", True), ("never", False), ("raise", False)])
+def test_leave_clean_only_after_confirmed_collectives(mode, clean):
+    """a departing rank sets the 'left clean' bit only when every collective it joined
+    was seen to complete; a pending work that never completes (or fails) makes it leave as an
+    eviction, so the survivors recover instead of trusting its share."""
+    import torch
+
+    from myfyp_amd.parallel.federation import Federation
+    from myfyp_amd.settings import Settings
+
+    f = Federation(0, 2, 0, torch.device("cpu"))
+    f.shm = _FakeShm()
+    f._pending = [([_Work(mode)], [0, 1], None, None)]
+    old = Settings.COLLECTIVE_TIMEOUT
+    Settings.COLLECTIVE_TIMEOUT = 0.05
+    try:
+        f._leave_clean()
+    finally:
+        Settings.COLLECTIVE_TIMEOUT = old
+    assert f.shm.clean is clean and not f._pending
