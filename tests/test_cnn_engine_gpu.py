@@ -592,6 +592,19 @@ def test_cnn_epoch_graph_captured_after_first_run(monkeypatch, late):
     assert np.isfinite(losses).all(), losses
 
 
+def _within_floor(floor, opt_in):
+    """Opt-in path vs default, per peer, against the default path's OWN run-to-run distance
+    measured in the same test (two default runs). ``scripts/probes/cnn_ab_noise.py`` on MI355X
+    (``profiles/r5_cnn_ab_noise/cnn_ab.log``): two default runs of one ResNet-18 epoch (batch 16,
+    SGD momentum) differ by cos 0.979-0.986 / rel 0.17-0.21 (fp32 atomic order in the BN
+    statistics and split-K sums flips bf16 roundings; the BatchNorms amplify them), and every
+    opt-in path lands at the same distance from the default (cos 0.976-0.984 / rel 0.18-0.22).
+    So the bound is that floor plus a small margin (rel x1.2 + 0.03, cos - 0.015) — no constant
+    fallback (round 4 allowed rel up to 0.25 whatever the floor)."""
+    for (c_n, r_n), (c_f, r_f) in zip(floor, opt_in):
+        assert c_f > c_n - 0.015 and r_f < 1.2 * r_n + 0.03, ((c_f, r_f), (c_n, r_n))
+
+
 def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     """BN1-apply + ReLU folded into conv2's forward / wgrad prologues, with the ReLU mask recomputed
     from y1 in the BN backward, against the path that materialises a1 (k_bn_act). The prologue
@@ -621,12 +634,7 @@ def test_resnet_bn1_prologue_fusion_matches_materialised_path(monkeypatch):
     def dist(xs, ys):
         return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
 
-    # the unfused path's repeats are nearly bit-identical since the patch-staged wgrad (no split-K
-    # atomics at these shapes), so the floor is also bounded by the measured bf16 chaos level
-    for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        # bounded by the run-to-run floor or, where that floor is ~0, by the measured bf16 chaos
-        # level (cos 0.977, rel 0.21) plus a ~20 % margin — no wider
-        assert c_f > min(c_n - 0.03, 0.965) and r_f < max(1.5 * r_n + 0.02, 0.25), ((c_f, r_f), (c_n, r_n))
+    _within_floor(dist(d_u2, d_u1), dist(d_f, d_u1))
     assert abs(l_f - l_u1) < 1e-2 * max(1.0, abs(l_u1)), (l_f, l_u1, l_u2)
 
 
@@ -671,8 +679,7 @@ def test_resnet_bn_finalize_in_conv_tail_matches_separate_launches(monkeypatch):
     def dist(xs, ys):
         return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
 
-    for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        assert c_f > min(c_n - 0.03, 0.965) and r_f < max(1.5 * r_n + 0.02, 0.25), ((c_f, r_f), (c_n, r_n))
+    _within_floor(dist(d_u2, d_u1), dist(d_f, d_u1))
 
 
 def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
@@ -703,10 +710,7 @@ def test_resnet_stride2_dgrad_as_parity_forward_matches_default(monkeypatch):
     def dist(xs, ys):
         return [(float(F.cosine_similarity(a, b, dim=0)), float((a - b).norm() / b.norm())) for a, b in zip(xs, ys)]
 
-    for (c_n, r_n), (c_f, r_f) in zip(dist(d_u2, d_u1), dist(d_f, d_u1)):
-        # bounded by the run-to-run floor or, where that floor is ~0, by the measured bf16 chaos
-        # level (cos 0.977, rel 0.21) plus a ~20 % margin — no wider
-        assert c_f > min(c_n - 0.03, 0.965) and r_f < max(1.5 * r_n + 0.02, 0.25), ((c_f, r_f), (c_n, r_n))
+    _within_floor(dist(d_u2, d_u1), dist(d_f, d_u1))
 
 
 @pytest.mark.parametrize("mode", [0, 4])
