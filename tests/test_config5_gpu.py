@@ -4,11 +4,19 @@ torch autograd fp32 learner (the oracle) on the SAME partitions and the same fau
 
 What is pinned:
 
-* the survivors finish every round, agree (equal models), and their accuracy after the last round
-  is within a stated margin of the oracle's (the mean of two torch runs that differ only in their
-  batch shuffle): ``|acc_engine − acc_torch| ≤ max(2·spread, 0.08)`` (margin calibrated on the GPU,
-  ``profiles/r5_config5_test/README.md``);
+* the survivors finish every round and agree on every floating tensor;
+* accuracy: the oracle (mean of two torch runs that differ only in their batch shuffle) and the
+  engine both end above 0.9 after ten rounds, within 0.08 of each other; over the rising part of
+  the curve (rounds 4-8) the engine's mean accuracy is within max(0.1, 2 × the oracle's seed spread)
+  of the oracle's;
 * per-round mean training loss within the torch shuffle spread plus a bf16 margin, and falling.
+
+Calibration (``scripts/probes/config5_calibrate.py``, ``profiles/r5_config5_test``): 2048 samples per
+peer, similarity 0.4, ten rounds — engine rounds-4-8 mean 0.806 / 0.851 (two seeds), torch 0.764 /
+0.795 / 0.826 (three seeds); final 0.991 / 0.998 vs 0.986 / 0.934 / 0.947. Smaller problems (1024
+per peer, eight rounds) swing between 0.16 and 0.54 final accuracy across torch seeds alone. These
+end-to-end bounds cannot see a 5 % update error (a 5 % learning-rate change moves the curves less
+than the seed spread); the kernel tests (``tests/test_cnn_engine_gpu.py``) pin the updates.
 
 Reference semantics: the Dirichlet partitioner (``/root/reference/p2pfl/learning/dataset/
 partition_strategies.py:161-430``); aggregating whatever arrived when a peer is gone
@@ -26,10 +34,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-PEERS, ROUNDS, KILLED = 4, 8, 3
+PEERS, ROUNDS, KILLED = 4, 10, 3
 
 
-def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS):
+def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS, n_per_peer: int = 2048, similarity: float = 0.4):
     from myfyp_amd.communication.protocols.collective.collective_protocol import CollectiveCommunicationProtocol
     from myfyp_amd.fault_injection import kill_at
     from myfyp_amd.learning.aggregators import FedProx
@@ -43,7 +51,7 @@ def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS):
     from myfyp_amd.parallel.federation import Federation
     from myfyp_amd.settings import Settings
     from myfyp_amd.utils.seed import set_seed
-    from myfyp_amd.utils.utils import check_equal_models, wait_to_finish
+    from myfyp_amd.utils.utils import wait_to_finish
 
     saved = (Settings.USE_FUSED_KERNELS, Settings.BATCH_SIZE, Settings.TRAIN_SET_SIZE, Settings.GANG_WINDOW)
     Settings.USE_FUSED_KERNELS = fused
@@ -54,7 +62,7 @@ def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS):
     CNNGroup.reset_all()
     Federation.reset()
     fed = Federation.init()
-    data = synthetic_cifar10(1024 * peers, 256 * peers, seed=7, similarity=0.6, noise=1.0, modes=4, label_noise=0.05)
+    data = synthetic_cifar10(n_per_peer * peers, 256 * peers, seed=7, similarity=similarity, noise=1.0, modes=4, label_noise=0.05)
     parts = data.generate_partitions(peers, DirichletPartitionStrategy, alpha=0.5)
     exp = f"c5-{int(fused)}-{seed}-{time.time_ns()}"
     nodes = [
@@ -72,15 +80,21 @@ def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS):
         nodes[0].set_start_learning(rounds=rounds, epochs=1)
         wait_to_finish(live, timeout=900)
         assert all(nd.learning_workflow.history.count("RoundFinishedStage") == rounds for nd in live)
-        check_equal_models(live, atol=1e-4 if fused else 1e-5)
+        # survivors agree on every floating tensor (BatchNorm's integer num_batches_tracked counts
+        # each peer's own local batches: the collective plane averages floating state only)
+        ref = [p for p in live[0].learner.get_model().get_parameters()]
+        for nd in live[1:]:
+            for a, b in zip(ref, nd.learner.get_model().get_parameters()):
+                if np.issubdtype(a.dtype, np.floating):
+                    assert np.allclose(a, b, atol=1e-4 if fused else 1e-5)
         local = logger.get_local_logs()[exp]
         loss = []
         for r in range(rounds):
             vals = [local[r][nd.addr]["train_loss"][-1][1] for nd in live if nd.addr in local.get(r, {}) and local[r][nd.addr].get("train_loss")]
             loss.append(float(np.mean(vals)))
         logs = logger.get_global_logs()[exp]
-        acc = float(np.mean([dict(logs[nd.addr]["test_metric"])[rounds] for nd in live]))
-        return loss, acc
+        curve = [float(np.mean([dict(logs[nd.addr]["test_metric"])[r] for nd in live if r in dict(logs[nd.addr]["test_metric"])])) for r in range(1, rounds + 1)]
+        return loss, curve
     finally:
         for nd in nodes:
             nd.stop()
@@ -95,11 +109,13 @@ def test_config5_engine_matches_torch_oracle_with_dropout():
     eng, acc_e = _run(True, 1)
     t1, acc_1 = _run(False, 1)
     t2, acc_2 = _run(False, 2)
-    print(f"[config5] engine loss {np.round(eng, 4).tolist()} acc {acc_e:.4f} | torch(1) {np.round(t1, 4).tolist()} acc {acc_1:.4f} | "
-          f"torch(2) {np.round(t2, 4).tolist()} acc {acc_2:.4f}", file=sys.stderr)
-    acc_t, spread = 0.5 * (acc_1 + acc_2), abs(acc_1 - acc_2)
-    assert acc_t > 0.5, (acc_1, acc_2)  # the oracle learns this problem within the eight rounds
-    assert abs(acc_e - acc_t) <= max(2 * spread, 0.08), (acc_e, acc_1, acc_2)
+    print(f"[config5] engine acc {np.round(acc_e, 3).tolist()} loss {np.round(eng, 3).tolist()} | torch(1) acc {np.round(acc_1, 3).tolist()} "
+          f"loss {np.round(t1, 3).tolist()} | torch(2) acc {np.round(acc_2, 3).tolist()} loss {np.round(t2, 3).tolist()}", file=sys.stderr)
+    final_t = 0.5 * (acc_1[-1] + acc_2[-1])
+    assert final_t > 0.9 and acc_e[-1] > 0.9, (acc_e[-1], acc_1[-1], acc_2[-1])
+    assert abs(acc_e[-1] - final_t) <= 0.08, (acc_e[-1], acc_1[-1], acc_2[-1])
+    mid_e, mid_1, mid_2 = (float(np.mean(c[3:8])) for c in (acc_e, acc_1, acc_2))
+    assert abs(mid_e - 0.5 * (mid_1 + mid_2)) <= max(0.1, 2 * abs(mid_1 - mid_2)), (mid_e, mid_1, mid_2)
     for r in range(len(eng)):
         ref = 0.5 * (t1[r] + t2[r])
         assert np.isfinite(eng[r]), eng
