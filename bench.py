@@ -70,61 +70,17 @@ def parse() -> argparse.Namespace:
     return ap.parse_args()
 
 
-def _env_world() -> tuple:
-    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
-
-
-def plan_launch(args) -> str:
-    """Decide the process model BEFORE anything touches a GPU: "single" (one GPU), "mesh" (this
-    process drives --gpus devices), "park" (a torchrun rank other than 0 in mesh mode: it waits for
-    rank 0 and exits) or "ranks" (one process per GPU). Exits non-zero when the N GPUs asked for
-    cannot be used, so a run never reports fewer GPUs than requested."""
-    import torch
-
-    world, rank = _env_world()
-    if args.launch == "ranks":
-        if args.gpus != world:
-            raise SystemExit(f"bench: --launch ranks needs one process per GPU: --gpus {args.gpus} but WORLD_SIZE={world}")
-        return "ranks" if world > 1 else "single"
-    if world > 1 and args.gpus != world:
-        raise SystemExit(f"bench: launched with {world} ranks but --gpus {args.gpus}")
-    if args.gpus <= 1:
-        return "single"
-    if world > 1 and args.launch == "auto" and torch.cuda.device_count() == 0:
-        return "ranks"  # CPU host under torchrun (gloo rehearsal): one process per rank
-    if world > 1 and rank != 0:
-        return "park"
-    have = torch.cuda.device_count()  # does not initialise the GPU on this image
-    if args.gpus > have and not args.mesh_virtual:
-        raise SystemExit(f"bench: --gpus {args.gpus} but {have} GPU(s) visible (use --mesh-virtual for a one-device rehearsal)")
-    return "mesh"
-
-
-def park(args) -> None:
-    """torchrun rank > 0 in mesh mode: rank 0 drives every GPU; wait for it on a CPU-only group."""
-    import datetime
-
-    import torch.distributed as dist
-
-    dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
 def main() -> None:
     args = parse()
-    mode = plan_launch(args)
+    from myfyp_amd.utils import launch
+
+    mode = launch.plan_launch(args.gpus, args.launch, args.mesh_virtual)
     if mode == "park":
-        park(args)
+        launch.park()
         return
-    world_env, _ = _env_world()
-    parked_group = mode == "mesh" and world_env > 1
+    parked_group = mode == "mesh" and launch.env_world()[0] > 1
     if parked_group:  # rank 0 of a torchrun job in mesh mode: release the waiting ranks at the end
-        import datetime
-
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
+        launch.cpu_group()
     import numpy as np
     import torch
 
@@ -334,10 +290,7 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     fed.shutdown()
     if parked_group:
-        import torch.distributed as dist
-
-        dist.barrier()
-        dist.destroy_process_group()
+        launch.release_parked()
 
 
 if __name__ == "__main__":

@@ -27,6 +27,9 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", choices=["lenet5", "resnet18"], default="resnet18")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (one process drives them: device mesh; see myfyp_amd/utils/launch.py)")
+    ap.add_argument("--launch", choices=["auto", "mesh", "ranks"], default="auto")
+    ap.add_argument("--mesh-virtual", action="store_true", help="rehearsal: --gpus mesh ranks on the visible device(s)")
     ap.add_argument("--peers", type=int, default=8)
     ap.add_argument("--batch-size", type=int, default=0, help="0 = 128 for resnet18, 64 for lenet5")
     ap.add_argument("--rounds", type=int, default=10)
@@ -98,6 +101,15 @@ def torch_step_ms(model_name: str, batch: int, iters: int = 20) -> float:
 
 def main() -> None:
     args = parse()
+    from myfyp_amd.utils import launch
+
+    mode = launch.plan_launch(args.gpus, args.launch, args.mesh_virtual)
+    if mode == "park":
+        launch.park()
+        return
+    parked_group = mode == "mesh" and launch.env_world()[0] > 1
+    if parked_group:
+        launch.cpu_group()
     import numpy as np
     import torch
 
@@ -130,7 +142,13 @@ def main() -> None:
     Settings.OVERLAP_COLLECTIVES = not args.no_overlap
     if args.bucket_mb > 0:
         Settings.BUCKET_BYTES = int(args.bucket_mb * (1 << 20))
-    fed = Federation.init()
+    if mode == "mesh":
+        Settings.MESH_VIRTUAL = bool(args.mesh_virtual)
+        fed = Federation.init(devices=args.gpus)
+        if fed.mesh is None or fed.mesh_size != args.gpus:
+            raise SystemExit(f"bench_cnn: device mesh of {args.gpus} not formed")
+    else:
+        fed = Federation.init()
     world, rank = fed.world, fed.rank
     ppr = args.peers // world
     data = synthetic_cifar10(args.n_train, args.n_test, seed=7, similarity=args.similarity, noise=args.noise, modes=args.modes, label_noise=args.label_noise)
@@ -154,7 +172,11 @@ def main() -> None:
         fault_injection.kill_at(nodes[-1], "TrainStage", round=min(1, args.warmup + args.rounds - 1))
     total = args.warmup + args.rounds
     marks, round_end = {}, {}
-    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    cuda_devs = sorted({d.index for d in fed.devices if d.type == "cuda"}) if torch.cuda.is_available() else []
+
+    def sync() -> None:  # every device this process drives
+        for i in cuda_devs:
+            torch.cuda.synchronize(i)
 
     def hook(r, f):
         if r == args.warmup - 1:
@@ -220,7 +242,9 @@ def main() -> None:
         n.stop()
     out = {
         "metric": f"rounds/sec, {args.model} {args.aggregator} {args.peers} peers",
-        "value": round(args.rounds / el, 4), "unit": "rounds/s", "n_gpus": world, "rounds": args.rounds, "warmup": args.warmup,
+        "value": round(args.rounds / el, 4), "unit": "rounds/s", "n_gpus": len(cuda_devs) if fed.mesh is not None else world,
+        "launch": "device mesh (one process)" if fed.mesh is not None else ("one process per GPU" if world > 1 else "single"),
+        "rounds": args.rounds, "warmup": args.warmup,
         "ms_per_round": round(1000 * el / args.rounds, 2),
         "train_images_per_s": round(args.n_train * args.rounds / el, 1),
         "engine": ("fused-hip" + ("-eager" if args.eager else "-hipgraph")) if fused else "autograd",
@@ -245,6 +269,8 @@ def main() -> None:
     if rank == 0:
         print(json.dumps(out), flush=True)
     fed.shutdown()
+    if parked_group:
+        launch.release_parked()
 
 
 if __name__ == "__main__":

@@ -568,6 +568,15 @@ class Federation:
         if inst is not None and inst.shm is not None:
             inst.shm.close()
             inst.shm = None
+        if inst is not None and inst.mesh is not None:
+            try:
+                for d in inst.devices:
+                    if d.type == "cuda":
+                        torch.cuda.synchronize(d)
+                inst.mesh.close()
+            except Exception as e:  # best effort (a test tearing down after a failure)
+                logger.debug("rank0", f"mesh close: {e}")
+            inst.mesh = None
         cls._instance = None
 
     def register_local(self, node) -> None:

@@ -219,7 +219,9 @@ def run_experiment(cfg: Any, verbose: bool = True) -> Dict[str, Any]:
     if collective:
         from myfyp_amd.parallel.federation import Federation
 
-        fed = Federation.init()
+        # `devices: N` (or network.devices): one process drives N GPUs (device mesh)
+        ndev = exp.get("devices", net.get("devices"))
+        fed = Federation.init(devices=int(ndev) if ndev else None)
     nodes: List[Any] = []
     by_index: Dict[int, Any] = {}
     start_round = 0

@@ -200,8 +200,12 @@ def test_gossip_peer_dropout(data):
 
 
 # ------------------------------------------------------------------------------------------ runner / CLI
-def test_yaml_runner(tmp_path):
+@pytest.mark.parametrize("devices", [None, 3], ids=["one-device", "mesh3"])
+def test_yaml_runner(tmp_path, devices):
+    """``devices: N`` runs the experiment on an N-device mesh in one process (CPU members here)."""
     import yaml
+
+    from myfyp_amd.parallel.federation import Federation
 
     cfg = {
         "experiment": {
@@ -214,9 +218,10 @@ def test_yaml_runner(tmp_path):
             "aggregator": {"package": "p2pfl.learning.aggregators.fedavg", "aggregator": "FedAvg"},
             "attack": {"node": 1, "kind": "gaussian_noise", "sigma": 0.05},
         },
-        "network": {"protocol": "collective", "nodes": 3},
+        "network": {"protocol": "collective", "nodes": 3, **({"devices": devices} if devices else {})},
         "settings": {"training": {"TRAIN_SET_SIZE": 3}},
     }
+    Federation.reset()
     p = tmp_path / "exp.yaml"
     p.write_text(yaml.safe_dump(cfg))
     from myfyp_amd.runner import run_experiment
