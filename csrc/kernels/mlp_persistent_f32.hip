@@ -132,8 +132,25 @@ __host__ __device__ constexpr int ng_of(int KS) { return NCG * KS; }         // 
 __host__ __device__ constexpr int roles_of(int KS) { return NCG * KS + NH; }  // workgroups per peer
 __host__ __device__ constexpr int ppl_of(int KS) { return KS == 1 ? 8 : 4; }  // peers per launch
 constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH, F_DONE = NCG * KSMAX + 2 * NH;
-constexpr int FPP = F_DONE + NCG * KSMAX + NH;  // flags per peer (laid out for KSMAX): + one commit flag per role
-static_assert(FPP == F32_FPP, "flag block layout shared with mlp_persistent_f32v2.hip");
+constexpr int FPP = F32_FPP;  // flag lines per peer (the block every layout shares)
+static_assert(F_DONE + NCG * KSMAX + NH <= F32_FPP, "layout-1 flags fit the shared block");
+// ---- gang layout 3 (row heads): the heads split the BATCH, not H2's columns. Head r owns batch rows
+// 16r..16r+15 and computes their whole forward tail: H2 rows (every column: no partial-logit
+// exchange between heads), logits, log-softmax + NLL, dlogits and dH2 rows. The owners own W2 (their
+// replica becomes the master: dW2 needs every batch row, which only they receive) and publish the
+// updated columns each step; the heads hold W3 / b2 / b3 replicas and keep them identical by summing
+// the heads' partial gradients in a fixed order. Per step the critical chain loses the head <-> head
+// hand-off and three quarters of the softmax; W2 / partial-gradient traffic runs beside the owners.
+constexpr int F3_DH2 = NCG * KSMAX;       // head r -> owners: dH2 rows 16r..16r+15 (BP / 16 heads)
+constexpr int F3_W2 = F3_DH2 + 4;         // owner cg (K part 0) -> heads: W2 columns 16cg.. after its update
+constexpr int F3_HP = F3_W2 + NCG;        // head r -> heads: partial dW3 / db2 / db3 over its rows
+constexpr int F3_DONE = F3_HP + 4;        // commit flags, one per role
+static_assert(F3_DONE + NCG * KSMAX + 4 <= F32_FPP, "layout-3 flags fit the shared block");
+__host__ __device__ constexpr int nhr_of(int BP) { return BP / 16; }  // row heads per peer
+__host__ __device__ constexpr int roles3_of(int KS, int BP) { return NCG * KS + nhr_of(BP); }
+constexpr int HPW = 16 * PD2 + PD2 + 16;  // floats of one head's partial gradients: dW3 [class][o2] | db2 | db3
+// exchange regions of layout 3, after layout 1's (dH2 uses layout 1's dh2x region, plain fp32)
+__host__ __device__ inline size_t v3_extra_floats(int P) { return (size_t)P * PD2 * PD1 + (size_t)P * 2 * 4 * HPW; }
 constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 799
 
 
@@ -207,17 +224,19 @@ __host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : 2; }
 // state. Each role publishes its commit flag and waits for all of them (bounded, like every other
 // hand-off); a gang that gave up anywhere stores nothing. Test hook: debug_giveup = p + 1 + 256
 // makes owner 0 of peer p give up right here on the first attempt.
-template <int KS>
+template <int KS, bool RH = false, int BP = 64>
 __device__ __forceinline__ bool gang_commit(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int role, int* sOk) {
   if (pb.fbase == 0 && role == 0 && a.debug_giveup == p + 1 + 256) {
     if (threadIdx.x == 0) __hip_atomic_store(pb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
   }
-  persist::publish(pb.flags, FPP, p, F_DONE + role, pb.fbase + DONE_MARK);
-  return persist::wg_wait(pb.flags, FPP, p, F_DONE, roles_of(KS), pb.fbase + DONE_MARK, pb.err, sOk);
+  constexpr int FD = RH ? F3_DONE : F_DONE;
+  constexpr int NR = RH ? roles3_of(KS, BP) : roles_of(KS);
+  persist::publish(pb.flags, FPP, p, FD + role, pb.fbase + DONE_MARK);
+  return persist::wg_wait(pb.flags, FPP, p, FD, NR, pb.fbase + DONE_MARK, pb.err, sOk);
 }
 
-template <int BP, bool ADAM, bool EXTRA, int KS>
+template <int BP, bool ADAM, bool EXTRA, int KS, bool RH>
 __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int g, char* smem, unsigned gen) {
   constexpr int MT = BP / 16;
   constexpr int RQ = rq_of(KS);
@@ -450,8 +469,9 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #endif
     if (g == 0) P32_STAMP(0, t, 2);
 
-    // the previous step's W2-replica update runs while the heads work on this step's H1
-    if (t > 0) w2_replica_update(t - 1, lr_prev, inv_prev);
+    // the previous step's W2-replica update runs while the heads work on this step's H1 (layout 3:
+    // W2 is updated in step t's C phase and published for the heads)
+    if (!RH && t > 0) w2_replica_update(t - 1, lr_prev, inv_prev);
     if (g == 0) P32_STAMP(0, t, 3);
 
     // next step's batch: pull this wave's columns into the XCD's L2 (staged after the dW1 MFMAs)
@@ -487,7 +507,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     // representative wait (one chunk per head: its first two columns of row 0), then the bulk load
     if (!persist::ll_wg_wait([&](int k) { return persist::ll_ld2(r_dh2, 16 * k * 8); }, NH, tag, pb.err, sOk)) return;
 #else
-    if (!persist::wg_wait(pb.flags, FPP, p, F_DH2, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+    if (!persist::wg_wait(pb.flags, FPP, p, RH ? F3_DH2 : F_DH2, RH ? nhr_of(BP) : NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
 #endif
     if (g == 0) P32_STAMP(0, t, 4);
     if (KS > 1) {
@@ -558,11 +578,34 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         acc = mfma_f32(av.z, w2c[2], acc);
         acc1[mt] = mfma_f32(av.w, w2c[3], acc);
       }
+      // layout 3: dW2[16w + 4h + i][16cg + c] over the batch (the same k-ordered chain as the
+      // deferred replica update), from the staged dH2 before the partials overwrite it
+      f32x4 dw2 = zero4();
+      if (RH) {
+        const float* h1p = sH1c;
+#pragma unroll
+        for (int kb = 0; kb < BP / 4; ++kb) dw2 = mfma_f32(sDH2[(4 * kb + h) * LDD + 16 * wave + c], h1p[(4 * kb + h) * 16 + c], dw2);
+      }
       lds_barrier();  // every wave has read its dH2 fragments before the partials overwrite them
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc1[mt];
+      if (RH) {
+        // W2(t + 1) = W2(t) updated with dW2(t); K part 0 publishes the columns for the heads' next
+        // H2 (write-through; the flag goes up after the drain below)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) upd32<ADAM, EXTRA>(o, dw2[i], w2c[i], m2c[i], v2c[i], e2c[i], lr_t, inv_bc2, wdmu);
+        if (kh == 0) {
+          float* w2x = pb.dh2x + (int64_t)a.P * 2 * BP * PD2 * 2 + (int64_t)p * PD2 * PD1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st_wt32(w2x + (16 * wave + 4 * h + i) * PD1 + NCG * cg + c, w2c[i]);
+        }
+      }
     }
-    lds_barrier();
+    if (RH && kh == 0) {
+      persist::publish(pb.flags, FPP, p, F3_W2 + cg, pb.fbase + (unsigned)(t + 2));  // (its barrier is C1's)
+    } else {
+      lds_barrier();
+    }
     if (tv < MT * 64) {  // tv: the step's laundered thread index (a hoisted offset would be spilled)
       const int mt = tv >> 6, hh = (tv & 63) >> 4, cc = tv & 15;
       f32x4 s = sRed[mt * 64 + (tv & 63)];
@@ -681,7 +724,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (g == 0) P32_STAMP(0, t, 6);
   }
 
-  if (!gang_commit<KS>(a, pb, p, g, sOk)) return;
+  if (!gang_commit<KS, RH, BP>(a, pb, p, g, sOk)) return;
   // ---- write the state back (fp32 master weights and moments; b1 from the bias slot). Every
   //      address is re-derived from laundered lane / row indices: the compiler would otherwise keep
   //      the prologue's 64-bit load addresses alive across the whole epoch (VGPR spills)
@@ -723,7 +766,16 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       }
     }
   }
-  if (pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
+  if (RH && kh == 0) {  // layout 3: the owners hold the master W2 columns
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = pS_w + a.off_w2 + (int64_t)(16 * wave + 4 * hw + i) * PD1 + NCG * cg + cw;
+      a.params[idx] = w2c[i];
+      a.m[idx] = m2c[i];
+      if (ADAM) a.v[idx] = v2c[i];
+    }
+  }
+  if (!RH && pb.w2chk != nullptr) {  // debug: the replica after the last step's update, for the bitwise check
     if (nsteps > 0) w2_replica_update(nsteps - 1, lr_t, inv_bc2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) pb.w2chk[(int64_t)p * PD2 * PD1 + (int64_t)(16 * wave + 4 * hw + i) * PD1 + NCG * cg + cw] = w2c[i];
@@ -1113,7 +1165,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     if (hd == 0) P32_STAMP(1, t, 8);
   }
 
-  if (!gang_commit<KS>(a, pb, p, ng_of(KS) + hd, sOk)) return;
+  if (!gang_commit<KS, false, BP>(a, pb, p, ng_of(KS) + hd, sOk)) return;
   // ---- write back W2 rows, b2, the W3 slice, b3 (head 0) and the epoch's loss / accuracy sums
 #pragma unroll
   for (int gg = 0; gg < 2; ++gg) {
@@ -1152,6 +1204,353 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
   }
 }
 
+// =============================================================================================
+// row-head workgroup (gang layout 3)
+// =============================================================================================
+constexpr int LDA3 = PD1 + 8;   // bf16 row stride of the head's split H1 rows (conflict-free 16-byte reads)
+constexpr int LDH23 = PD2 + 4;  // fp32 row stride of the head's H2 rows
+struct HeadRLds32 {
+  size_t a3, h2, red, dlog, w3s, b2s, b3s, ok, total;
+};
+__host__ __device__ inline HeadRLds32 headr_lds32() {
+  HeadRLds32 L;
+  size_t o = 0;
+  L.a3 = o;   o += al16((size_t)3 * 16 * LDA3 * 2);   // H1 rows as hi / mid / lo bf16 (exact split)
+  L.h2 = o;   o += al16((size_t)16 * LDH23 * 4);      // H2 rows
+  L.red = o;  o += al16((size_t)8 * 64 * 16);         // per-wave partial logits
+  L.dlog = o; o += al16((size_t)16 * LD16 * 4);       // dlogits rows
+  L.w3s = o;  o += al16((size_t)4 * 16 * LDH23 * 4);  // W3 replica: w, m, v, e planes [class][o2]
+  L.b2s = o;  o += al16((size_t)4 * PD2 * 4);         // b2 replica planes
+  L.b3s = o;  o += al16((size_t)4 * 16 * 4);          // b3 replica planes
+  L.ok = o;   o += 16;
+  L.total = o;
+  return L;
+}
+
+// Head r of layout 3: batch rows R0 = 16r .. 16r+15 of every step.
+//   H2 rows   = relu(H1 rows · W2ᵀ + b2): wave w computes the 16 columns 16w..16w+15 against W2 rows
+//               it loads itself (the owners' published columns, or the epoch's initial W2); both
+//               fp32 operands split exactly into bf16 hi / mid / lo, six bf16 MFMA terms per 32-wide
+//               K step (the three dropped cross terms are below 2^-32 of the product);
+//   logits    = per-wave partials over its 16 H2 columns (f32 MFMA), summed over the waves in order;
+//   softmax / NLL / dlogits of the 16 rows (one wave, DPP row reductions, as layout 1);
+//   dH2 rows  = dlogits · W3 ⊙ [H2 > 0] -> the owners (the step's only head -> owner hand-off);
+//   then, beside the owners' backward: partial dW3 / db2 / db3 over the 16 rows -> every head, summed
+//   over the heads in a fixed order, and the W3 / b2 / b3 replicas updated identically in all heads.
+template <int BP, bool ADAM, bool EXTRA, int KS>
+__device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int r, char* smem, unsigned gen) {
+  constexpr int NHR = nhr_of(BP);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, n = lane & 15;
+  const int D3 = a.D3;
+  const int R0 = 16 * r;
+  const HeadRLds32 L = headr_lds32();
+  bf16* sA = reinterpret_cast<bf16*>(smem + L.a3);
+  float* sH2 = reinterpret_cast<float*>(smem + L.h2);
+  f32x4* sRed = reinterpret_cast<f32x4*>(smem + L.red);
+  float* sDlog = reinterpret_cast<float*>(smem + L.dlog);
+  float* sW3 = reinterpret_cast<float*>(smem + L.w3s);  // plane q at q * 16 * LDH23
+  float* sB2 = reinterpret_cast<float*>(smem + L.b2s);  // plane q at q * PD2
+  float* sB3 = reinterpret_cast<float*>(smem + L.b3s);  // plane q at q * 16
+  int* sOk = reinterpret_cast<int*>(smem + L.ok);
+  constexpr int W3P = 16 * LDH23;
+
+  const OptParams& o = a.opt;
+  const int4 ctl = a.ctl[p];
+  const bool fresh = (ctl.x & 2) != 0;
+  const int nrows = ctl.y;
+  const int nsteps = (nrows + a.B - 1) / a.B;
+  const int64_t pS = (int64_t)p * a.S;
+  const float wdmu = o.weight_decay + (a.anchor != nullptr ? o.mu : 0.f);
+  float* const w2x = pb.dh2x + (int64_t)a.P * 2 * BP * PD2 * 2 + (int64_t)p * PD2 * PD1;
+  float* const hpx = pb.dh2x + (int64_t)a.P * 2 * BP * PD2 * 2 + (int64_t)a.P * PD2 * PD1 + (int64_t)p * 2 * 4 * HPW;
+
+  // ---- replicas of W3 [class][o2], b2, b3 (+ moments, extra term); classes >= D3 stay zero
+  for (int e = tid; e < 16 * PD2; e += NT) {
+    const int cls = e >> 7, o2 = e & (PD2 - 1);
+    float w = 0.f, m = 0.f, v = 0.f, x = 0.f;
+    if (cls < D3) {
+      const int64_t idx = pS + a.off_w3 + (int64_t)cls * PD2 + o2;
+      w = a.params[idx];
+      if (!fresh) {
+        m = a.m[idx];
+        if (ADAM) v = a.v[idx];
+      }
+      if (EXTRA) x = extra_at(a, idx);
+    }
+    const int off = cls * LDH23 + o2;
+    sW3[off] = w;
+    sW3[W3P + off] = m;
+    sW3[2 * W3P + off] = v;
+    sW3[3 * W3P + off] = x;
+  }
+  if (tid < PD2) {
+    const int64_t idx = pS + a.off_b2 + tid;
+    sB2[tid] = a.params[idx];
+    sB2[PD2 + tid] = fresh ? 0.f : a.m[idx];
+    sB2[2 * PD2 + tid] = (ADAM && !fresh) ? a.v[idx] : 0.f;
+    sB2[3 * PD2 + tid] = EXTRA ? extra_at(a, idx) : 0.f;
+  } else if (tid >= PD2 && tid < PD2 + 16) {
+    const int k = tid - PD2;
+    const int64_t idx = pS + a.off_b3 + k;
+    const bool kin = k < D3;
+    sB3[k] = kin ? a.params[idx] : 0.f;
+    sB3[16 + k] = (kin && !fresh) ? a.m[idx] : 0.f;
+    sB3[32 + k] = (kin && ADAM && !fresh) ? a.v[idx] : 0.f;
+    sB3[48 + k] = (kin && EXTRA) ? extra_at(a, idx) : 0.f;
+  }
+  __syncthreads();
+  float loss_acc = 0.f, correct_acc = 0.f;
+  const bool cin = n < D3;
+
+  persist::BiasCorr bc;
+  bc.init(o, ctl.z);
+  for (int t = 0; t < nsteps; ++t) {
+    int tv = tid;
+    asm volatile("" : "+v"(tv));
+    const int rows = rows_at(a, nrows, t);
+    float lr_t, inv_bc2;
+    bc.next(o, lr_t, inv_bc2);
+    const unsigned target = pb.fbase + (unsigned)(t + 1);
+    // labels of the softmax lanes' rows (wave 0: rows 4g + i), off the critical path
+    int yv[4] = {-1, -1, -1, -1};
+    if (wave == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = R0 + 4 * g + i;
+        if (b < rows) yv[i] = a.Yb[(int64_t)p * a.xb_rows + (int64_t)t * a.B + b];
+      }
+    }
+    // ---- W2 rows of this wave's H2 columns: W2[16w + n][32c + 8g .. +8], c < 8 (step 0: the
+    //      epoch's initial W2; later: the owners' columns updated with dW2(t - 1))
+    if (t > 0 && !persist::wg_wait(pb.flags, FPP, p, F3_W2, NCG, target, pb.err, sOk)) return;
+    float wb[8][8];
+    {
+      const float* src = t == 0 ? a.params + pS + a.off_w2 : w2x;
+      const __amdgpu_buffer_rsrc_t rw = rsrc_of(src, PD2 * PD1 * 4);
+      int lw = lane;
+      asm volatile("" : "+v"(lw));
+      const int rowoff = ((16 * wave + (lw & 15)) * PD1 + 8 * (lw >> 4)) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float4 lo = ld_sc1_16(rw, rowoff + 32 * c * 4), hi = ld_sc1_16(rw, rowoff + (32 * c + 4) * 4);
+        wb[c][0] = lo.x; wb[c][1] = lo.y; wb[c][2] = lo.z; wb[c][3] = lo.w;
+        wb[c][4] = hi.x; wb[c][5] = hi.y; wb[c][6] = hi.z; wb[c][7] = hi.w;
+      }
+    }
+    // ---- H1 rows R0.. from the owners (KS > 1: the K parts' partials summed in kh order, relu),
+    //      split exactly into three bf16 planes
+    if (r == 0) P32_STAMP(1, t, 0);
+    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, ng_of(KS), target, pb.err, sOk)) return;
+    if (r == 0) P32_STAMP(1, t, 1);
+    {
+      float4 u[KS][2];
+#pragma unroll
+      for (int k2 = 0; k2 < KS; ++k2) {
+        const __amdgpu_buffer_rsrc_t rh = rsrc_of(h1x_part(pb, p, k2, t, BP) + (int64_t)R0 * PD1, 16 * PD1 * 4);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) u[k2][k] = ld_sc1_16(rh, (tv + NT * k) * 16);  // 16 x 256 fp32 = 1024 chunks
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        float4 v = u[0][k];
+#pragma unroll
+        for (int k2 = 1; k2 < KS; ++k2) {
+          v.x += u[k2][k].x;
+          v.y += u[k2][k].y;
+          v.z += u[k2][k].z;
+          v.w += u[k2][k].w;
+        }
+        if (KS > 1) v = float4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        const float x[4] = {v.x, v.y, v.z, v.w};
+        bf16x4 xh, xm, xl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16 h0 = (bf16)x[i];
+          const float r1 = x[i] - (float)h0;
+          const bf16 m0 = (bf16)r1;
+          xh[i] = h0;
+          xm[i] = m0;
+          xl[i] = (bf16)(r1 - (float)m0);
+        }
+        const int e = tv + NT * k;
+        const int off = (e >> 6) * LDA3 + 4 * (e & 63);
+        *reinterpret_cast<bf16x4*>(sA + off) = xh;
+        *reinterpret_cast<bf16x4*>(sA + 16 * LDA3 + off) = xm;
+        *reinterpret_cast<bf16x4*>(sA + 32 * LDA3 + off) = xl;
+      }
+    }
+    lds_barrier();
+    if (r == 0) P32_STAMP(1, t, 2);
+    // ---- H2 rows, columns 16w .. 16w+15: C[row 4g + i][o2 = 16w + n]
+    float h2v[4];
+    {
+      f32x4 acc = zero4();
+      int la = lane;
+      asm volatile("" : "+v"(la));
+      const bf16* ap = sA + (la & 15) * LDA3 + 8 * (la >> 4);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bf16x8 ah = ld8(ap + 32 * c), am = ld8(ap + 16 * LDA3 + 32 * c), al = ld8(ap + 32 * LDA3 + 32 * c);
+        bf16x8 bh, bm, bl;
+        split3(wb[c], bh, bm, bl);
+        acc = mfma_bf16(al, bh, acc);  // smallest terms first
+        acc = mfma_bf16(ah, bl, acc);
+        acc = mfma_bf16(am, bm, acc);
+        acc = mfma_bf16(am, bh, acc);
+        acc = mfma_bf16(ah, bm, acc);
+        acc = mfma_bf16(ah, bh, acc);
+      }
+      const float bias = sB2[16 * wave + n];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = R0 + 4 * g + i;
+        h2v[i] = b < rows ? fmaxf(acc[i] + bias, 0.f) : 0.f;
+        sH2[(4 * g + i) * LDH23 + 16 * wave + n] = h2v[i];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's H2 columns, read back across its lanes
+    // ---- partial logits over this wave's 16 H2 columns: C[row 4g + i][class n]
+    {
+      f32x4 pl = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        pl = mfma_f32(sH2[n * LDH23 + 16 * wave + 4 * g + ks], sW3[n * LDH23 + 16 * wave + 4 * g + ks], pl);
+      sRed[wave * 64 + lane] = pl;
+    }
+    lds_barrier();
+    if (r == 0) P32_STAMP(1, t, 3);
+    // ---- logits (waves summed in order) + b3, log-softmax + NLL + argmax + dlogits (wave 0)
+    if (wave == 0) {
+      f32x4 ls = sRed[lane];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) ls += sRed[w * 64 + lane];
+      const float b3 = sB3[n];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int bl_ = 4 * g + i;
+        const bool rvalid = R0 + bl_ < rows;
+        const int y = yv[i];
+        const float logit = cin ? ls[i] + b3 : -INFINITY;
+        const float mx = row_max16(logit);
+        const float se = row_sum16(cin ? expf(logit - mx) : 0.f);
+        const float logp = logit - (mx + logf(se));
+        const int cand = row_min16((cin && logit == mx) ? n : 16);
+        if (rvalid && n == y) loss_acc -= logp;
+        if (rvalid && n == 0) correct_acc += (cand == y) ? 1.f : 0.f;
+        // dlogits: p_c / rows; the true class as −Σ_{c≠y} p_c / rows (no cancellation; layout 1)
+        const float pc = cin ? expf(logp) : 0.f;
+        const float others = row_sum16(n != y ? pc : 0.f);
+        sDlog[bl_ * LD16 + n] = (rvalid && cin) ? (n == y ? -others : pc) / (float)rows : 0.f;
+      }
+    }
+    lds_barrier();
+    if (r == 0) P32_STAMP(1, t, 4);
+    // ---- dH2 rows, columns 16w..16w+15 = dlogits · W3 ⊙ [H2 > 0] -> the owners
+    float dh2v[4];
+    {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma_f32(sDlog[n * LD16 + 4 * ks + g], sW3[(4 * ks + g) * LDH23 + 16 * wave + n], acc);
+      float* dst = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2 * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dh2v[i] = h2v[i] > 0.f ? acc[i] : 0.f;
+        st_wt32(dst + (R0 + 4 * g + i) * PD2 + 16 * wave + n, dh2v[i]);
+      }
+    }
+    persist::publish(pb.flags, FPP, p, F3_DH2 + r, target);
+    if (r == 0) P32_STAMP(1, t, 5);
+
+    // ---- off the critical path: partial gradients of W3 / b2 / b3 over these rows -> every head
+    float* hp_t = hpx + ((int64_t)(t & 1) * 4) * HPW;  // [head][HPW]
+    {
+      f32x4 acc = zero4();  // C[o2 = 16w + 4g + i][class n], k-ordered over the 16 rows
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) acc = mfma_f32(sH2[(4 * kb + g) * LDH23 + 16 * wave + n], sDlog[(4 * kb + g) * LD16 + n], acc);
+      float* hp = hp_t + r * HPW;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st_wt32(hp + n * PD2 + 16 * wave + 4 * g + i, acc[i]);
+      float sb = (dh2v[0] + dh2v[1]) + (dh2v[2] + dh2v[3]);  // db2: rows of this lane, then the 4 lane groups
+      sb += __shfl_xor(sb, 16);
+      sb += __shfl_xor(sb, 32);
+      if (g == 0) st_wt32(hp + 16 * PD2 + 16 * wave + n, sb);
+      if (wave == 0) {
+        float s3 = (sDlog[(4 * g) * LD16 + n] + sDlog[(4 * g + 1) * LD16 + n]) + (sDlog[(4 * g + 2) * LD16 + n] + sDlog[(4 * g + 3) * LD16 + n]);
+        s3 += __shfl_xor(s3, 16);
+        s3 += __shfl_xor(s3, 32);
+        if (g == 0) st_wt32(hp + 16 * PD2 + PD2 + n, s3);
+      }
+    }
+    persist::publish(pb.flags, FPP, p, F3_HP + r, target);
+    if (!persist::wg_wait(pb.flags, FPP, p, F3_HP, NHR, target, pb.err, sOk)) return;
+    {
+      // every head sums the heads' partials in head order (same bits everywhere) and updates its
+      // replicas with the same code
+      const __amdgpu_buffer_rsrc_t rp = rsrc_of(hp_t, 4 * HPW * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tv + NT * k;  // W3 entry [class e >> 7][o2 e & 127]
+        const int cls = e >> 7, o2 = e & (PD2 - 1);
+        float gs = 0.f;
+#pragma unroll
+        for (int q = 0; q < NHR; ++q) gs += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (q * HPW + e) * 4, 0, 16));
+        if (cls < D3) {
+          const int off = cls * LDH23 + o2;
+          upd32<ADAM, EXTRA>(o, gs, sW3[off], sW3[W3P + off], sW3[2 * W3P + off], sW3[3 * W3P + off], lr_t, inv_bc2, wdmu);
+        }
+      }
+      if (tv < PD2 + 16) {
+        const int e = 16 * PD2 + tv;
+        float gs = 0.f;
+#pragma unroll
+        for (int q = 0; q < NHR; ++q) gs += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (q * HPW + e) * 4, 0, 16));
+        if (tv < PD2) {
+          upd32<ADAM, EXTRA>(o, gs, sB2[tv], sB2[PD2 + tv], sB2[2 * PD2 + tv], sB2[3 * PD2 + tv], lr_t, inv_bc2, wdmu);
+        } else if (tv - PD2 < D3) {
+          const int k = tv - PD2;
+          upd32<ADAM, EXTRA>(o, gs, sB3[k], sB3[16 + k], sB3[32 + k], sB3[48 + k], lr_t, inv_bc2, wdmu);
+        }
+      }
+    }
+    __syncthreads();
+    if (r == 0) P32_STAMP(1, t, 6);
+  }
+
+  if (!gang_commit<KS, true, BP>(a, pb, p, ng_of(KS) + r, sOk)) return;
+  // ---- write back the W3 / b2 / b3 replicas (head 0) and every head's loss / accuracy sums
+  if (r == 0) {
+    for (int e = tid; e < D3 * PD2; e += NT) {
+      const int cls = e >> 7, o2 = e & (PD2 - 1);
+      const int64_t idx = pS + a.off_w3 + (int64_t)cls * PD2 + o2;
+      const int off = cls * LDH23 + o2;
+      a.params[idx] = sW3[off];
+      a.m[idx] = sW3[W3P + off];
+      if (ADAM) a.v[idx] = sW3[2 * W3P + off];
+    }
+    if (tid < PD2) {
+      const int64_t idx = pS + a.off_b2 + tid;
+      a.params[idx] = sB2[tid];
+      a.m[idx] = sB2[PD2 + tid];
+      if (ADAM) a.v[idx] = sB2[2 * PD2 + tid];
+    } else if (tid >= PD2 && tid < PD2 + D3) {
+      const int k = tid - PD2;
+      const int64_t idx = pS + a.off_b3 + k;
+      a.params[idx] = sB3[k];
+      a.m[idx] = sB3[16 + k];
+      if (ADAM) a.v[idx] = sB3[32 + k];
+    }
+  }
+  if (wave == 0) {
+    const float l = wave_sum(loss_acc), cr = wave_sum(correct_acc);
+    if (lane == 0) {
+      atomicAdd(&a.loss_acc[p], l);
+      atomicAdd(&a.correct_acc[p], (int)(cr + 0.5f));
+    }
+  }
+}
+
 // grid = ppl_of(KS) * roles_of(KS) blocks per group of peers: block b serves peer
 // p_base + b % ppl in role b / ppl, so a peer's workgroups share one XCD under round-robin dispatch
 // (speed only).
@@ -1164,7 +1563,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 // flags offset by RETRY_BASE (the aborted attempt's flag values are all smaller), and on success
 // sets err[p] = 2 ("recovered"). Gangs are independent: one peer's give-up never aborts another.
 
-template <int BP, bool ADAM, bool EXTRA, int KS>
+template <int BP, bool ADAM, bool EXTRA, int KS, bool RH = false>
 __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base, int attempt) {
   extern __shared__ __attribute__((aligned(16))) char smem_p32[];
   constexpr int PPL = ppl_of(KS);
@@ -1189,7 +1588,9 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
   }
   const unsigned gen = __hip_atomic_load(pb.gen + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (role < ng_of(KS))
-    owner32<BP, ADAM, EXTRA, KS>(a, pb, p, role, smem_p32, gen);
+    owner32<BP, ADAM, EXTRA, KS, RH>(a, pb, p, role, smem_p32, gen);
+  else if (RH)
+    headr32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32, gen);
   else
     head32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32, gen);
   if (role == 0) {
@@ -1363,18 +1764,21 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
 #endif
 int f32_ks_v1(const MLPArgs& a);
 
+bool v3_supported(const MLPArgs& a);
+
 int f32_variant(const MLPArgs& a) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("MYFYP_F32_VARIANT");
-    env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+    env = (e && (e[0] >= '1' && e[0] <= '3')) ? e[0] - '0' : 0;
   }
   int v = env;
-  if (!v && (a.f32_variant == 1 || a.f32_variant == 2)) v = a.f32_variant;
+  if (!v && (a.f32_variant >= 1 && a.f32_variant <= 3)) v = a.f32_variant;
   if (!v) {
     const bool adam_extra = a.opt.kind == 0 && (a.anchor != nullptr || a.cg != nullptr);
     v = (adam_extra && f32_ks_v1(a) == 1) ? 2 : F32_DEFAULT_VARIANT;
   }
+  if (v == 3 && !v3_supported(a)) v = 1;
   if (v == 2 && !mlp_f32v2_supported(a)) v = 1;
   return v;
 }
@@ -1390,45 +1794,58 @@ int f32_ks_wanted(const MLPArgs& a) {
   return a.P <= ppl_of(2) ? 2 : 1;
 }
 
-size_t persistent_f32_lds_ks(const MLPArgs& a, int KS) {
-  const size_t lo = owner_lds32(a.Bpad, a.D0, KS).total, lh = head_lds32(a.Bpad).total;
+size_t persistent_f32_lds_ks(const MLPArgs& a, int KS, bool rh = false) {
+  const size_t lo = owner_lds32(a.Bpad, a.D0, KS).total, lh = rh ? headr_lds32().total : head_lds32(a.Bpad).total;
   return lo > lh ? lo : lh;
 }
 
-template <int BP, bool ADAM, bool EXTRA, int KS>
-const void* f32_fn() {
-  return (const void*)mlp_persistent_f32_epoch<BP, ADAM, EXTRA, KS>;
+bool v3_supported(const MLPArgs& a) {
+  if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
+  if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
+  if (a.Bpad != 32 && a.Bpad != 64) return false;
+  if ((a.cg == nullptr) != (a.cl == nullptr)) return false;
+  if (a.cg != nullptr && a.anchor != nullptr) return false;
+  return persistent_f32_lds_ks(a, 1, true) <= 160 * 1024;
 }
-template <int BP, int KS>
+
+template <int BP, bool ADAM, bool EXTRA, int KS, bool RH = false>
+const void* f32_fn() {
+  return (const void*)mlp_persistent_f32_epoch<BP, ADAM, EXTRA, KS, RH>;
+}
+template <int BP, int KS, bool RH = false>
 hipError_t prepare_f32_bp(int lds) {
-  const void* fns[4] = {f32_fn<BP, true, false, KS>(), f32_fn<BP, true, true, KS>(), f32_fn<BP, false, false, KS>(), f32_fn<BP, false, true, KS>()};
+  const void* fns[4] = {f32_fn<BP, true, false, KS, RH>(), f32_fn<BP, true, true, KS, RH>(), f32_fn<BP, false, false, KS, RH>(),
+                        f32_fn<BP, false, true, KS, RH>()};
   for (const void* fn : fns) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
-template <int BP, int KS>
+template <int BP, int KS, bool RH = false>
 void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds, int attempt) {
-  const dim3 grid(ppl_of(KS) * roles_of(KS)), block(NT);
+  const dim3 grid(ppl_of(KS) * (RH ? roles3_of(KS, BP) : roles_of(KS))), block(NT);
   const bool adam = a.opt.kind == 0;
   const bool extra = a.anchor != nullptr || a.cg != nullptr;
-  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false, KS>), grid, block, lds, s, a, pb, p_base, attempt);
-  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true, KS>), grid, block, lds, s, a, pb, p_base, attempt);
-  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false, KS>), grid, block, lds, s, a, pb, p_base, attempt);
-  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true, KS>), grid, block, lds, s, a, pb, p_base, attempt);
+  if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false, KS, RH>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (adam) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, true, KS, RH>), grid, block, lds, s, a, pb, p_base, attempt);
+  else if (!extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, false, KS, RH>), grid, block, lds, s, a, pb, p_base, attempt);
+  else hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, false, true, KS, RH>), grid, block, lds, s, a, pb, p_base, attempt);
 }
 
 // Workgroups one launch of K split KS can have resident at once (occupancy calculator for the
 // instantiation: registers, LDS, 512 threads).
-int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS) {
+int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS, bool rh = false) {
   int per_cu = 0;
-  const size_t lds = persistent_f32_lds_ks(a, KS);
-  const void* fn = KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2>() : f32_fn<32, true, false, 2>())
-                           : (a.Bpad == 64 ? f32_fn<64, true, false, 1>() : f32_fn<32, true, false, 1>());
+  const size_t lds = persistent_f32_lds_ks(a, KS, rh);
+  const void* fn = rh ? (KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2, true>() : f32_fn<32, true, false, 2, true>())
+                                 : (a.Bpad == 64 ? f32_fn<64, true, false, 1, true>() : f32_fn<32, true, false, 1, true>()))
+                      : (KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2>() : f32_fn<32, true, false, 2>())
+                                 : (a.Bpad == 64 ? f32_fn<64, true, false, 1>() : f32_fn<32, true, false, 1>()));
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
   return per_cu * num_cus;
 }
+int roles_for(const MLPArgs& a, int KS) { return f32_variant(a) == 3 ? roles3_of(KS, a.Bpad) : roles_of(KS); }
 
 // The K split layout 1 uses: the wanted one if its launch is co-resident, else 1.
 int f32_ks_v1(const MLPArgs& a) {
@@ -1439,17 +1856,21 @@ int f32_ks_v1(const MLPArgs& a) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   }
   const int want = f32_ks_wanted(a);
-  if (want == 2 && ppl_of(2) * roles_of(2) > resident_capacity_ks(a, cus, 2)) return 1;
+  const bool rh = a.f32_variant == 3 && v3_supported(a);
+  if (want == 2 && ppl_of(2) * (rh ? roles3_of(2, a.Bpad) : roles_of(2)) > resident_capacity_ks(a, cus, 2, rh)) return 1;
   return want;
 }
 int f32_ks(const MLPArgs& a) { return f32_variant(a) == 2 ? 1 : f32_ks_v1(a); }
 
 }  // namespace
 
-size_t persistent_f32_lds(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_lds(a) : persistent_f32_lds_ks(a, f32_ks(a)); }
+size_t persistent_f32_lds(const MLPArgs& a) {
+  const int v = f32_variant(a);
+  return v == 2 ? mlp_f32v2_lds(a) : persistent_f32_lds_ks(a, f32_ks(a), v == 3);
+}
 
 bool mlp_persistent_f32_supported(const MLPArgs& a) {
-  if (f32_variant(a) == 2) return true;  // (layout 2's own shape check passed in f32_variant)
+  if (f32_variant(a) != 1) return true;  // (layout 2 / 3's own shape checks passed in f32_variant)
   if (a.D1 != PD1 || a.D2 != PD2 || a.D3 < 1 || a.D3 > 16) return false;
   if (a.D0 % 8 != 0 || ks1_of(a.D0) > KS1_MAX) return false;
   if (a.Bpad != 32 && a.Bpad != 64) return false;
@@ -1462,7 +1883,7 @@ size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
   // layout 1: H1 partials (fp32) + partial logits and dH2 as LL (value, tag) pairs; layout 2 carves
   // its own regions from the same allocation
-  const size_t v1 = (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * 2) * sizeof(float);
+  const size_t v1 = (mlp_persistent_f32_h1x_floats(P, Bpad) + (size_t)P * ((size_t)NH * Bpad * 16 + (size_t)2 * Bpad * PD2) * 2 + v3_extra_floats(P)) * sizeof(float);
   const size_t v2 = mlp_f32v2_bytes(P, Bpad);
   return v1 > v2 ? v1 : v2;
 }
@@ -1474,9 +1895,10 @@ int mlp_persistent_f32_x_direct(const MLPArgs& a) { return P32_XDIRECT && f32_va
 int mlp_persistent_f32_x_direct_build() { return P32_XDIRECT; }
 
 // Workgroups one epoch launch needs (its peers' gangs) and how many the device holds at once.
-int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_launch_wgs() : ppl_of(f32_ks(a)) * roles_of(f32_ks(a)); }
+int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_launch_wgs() : ppl_of(f32_ks(a)) * roles_for(a, f32_ks(a)); }
 int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
-  return f32_variant(a) == 2 ? mlp_f32v2_resident_capacity(a, num_cus) : resident_capacity_ks(a, num_cus, f32_ks(a));
+  const int v = f32_variant(a);
+  return v == 2 ? mlp_f32v2_resident_capacity(a, num_cus) : resident_capacity_ks(a, num_cus, f32_ks(a), v == 3);
 }
 int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
 
@@ -1487,6 +1909,12 @@ hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
     e = KS == 1 ? (a.Bpad == 64 ? prepare_f32_bp<64, 1>(lds) : prepare_f32_bp<32, 1>(lds))
                 : (a.Bpad == 64 ? prepare_f32_bp<64, 2>(lds) : prepare_f32_bp<32, 2>(lds));
     if (e != hipSuccess) return e;
+    if (v3_supported(a)) {
+      const int l3 = (int)persistent_f32_lds_ks(a, KS, true);
+      e = KS == 1 ? (a.Bpad == 64 ? prepare_f32_bp<64, 1, true>(l3) : prepare_f32_bp<32, 1, true>(l3))
+                  : (a.Bpad == 64 ? prepare_f32_bp<64, 2, true>(l3) : prepare_f32_bp<32, 2, true>(l3));
+      if (e != hipSuccess) return e;
+    }
   }
   if (mlp_f32v2_supported(a)) {
     e = mlp_f32v2_prepare(a);
@@ -1506,12 +1934,21 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
   }
   const int KS = f32_ks(a);
   const int ppl = ppl_of(KS);
-  const size_t lds = persistent_f32_lds_ks(a, KS);
+  const bool rh = f32_variant(a) == 3;
+  const size_t lds = persistent_f32_lds_ks(a, KS, rh);
   // groups of ppl peers: one launch each (a launch's gangs must all be co-resident), then the
   // recovery launches (attempt 1): a no-op exit for every gang that did not give up
   for (int attempt = 0; attempt < 2; ++attempt)
     for (int p0 = 0; p0 < a.P; p0 += ppl) {
-      if (KS == 2) {
+      if (rh) {
+        if (KS == 2) {
+          if (a.Bpad == 64) launch_f32_bp<64, 2, true>(a, pb, s, p0, lds, attempt);
+          else launch_f32_bp<32, 2, true>(a, pb, s, p0, lds, attempt);
+        } else {
+          if (a.Bpad == 64) launch_f32_bp<64, 1, true>(a, pb, s, p0, lds, attempt);
+          else launch_f32_bp<32, 1, true>(a, pb, s, p0, lds, attempt);
+        }
+      } else if (KS == 2) {
         if (a.Bpad == 64) launch_f32_bp<64, 2>(a, pb, s, p0, lds, attempt);
         else launch_f32_bp<32, 2>(a, pb, s, p0, lds, attempt);
       } else {

@@ -126,7 +126,13 @@ def _rel_update(pe, pr, p0):
     return ((d_e - d_r).norm() / (d_r.norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2"])
+def _layout(layout: str):
+    """(variant, owner K split) of a test layout id: v1ks1, v1ks2, v2, v3ks1, v3ks2."""
+    v = int(layout[1])
+    return v, (2 if layout.endswith("ks2") else 1)
+
+
+@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2", "v3ks1", "v3ks2"])
 @pytest.mark.parametrize("B", [64, 32])
 @pytest.mark.parametrize("epochs", [1, 2])
 def test_f32_epoch_matches_torch_adam(dev, B, epochs, layout):
@@ -136,10 +142,10 @@ def test_f32_epoch_matches_torch_adam(dev, B, epochs, layout):
     heads) at both owner K splits: 1 (24-workgroup gangs) and 2 (40-workgroup gangs)."""
     spec = {"name": "adam", "lr": 1e-3}
     learners, refs, g, n = _setup(dev, 2, B, 1400, 3, spec)
-    ks = 2 if layout == "v1ks2" else 1
+    var, ks = _layout(layout)
     g.force_f32_ks = ks
-    g.force_f32_variant = 2 if layout == "v2" else 1
-    assert g.f32_ks() == ks and g.f32_variant() == (2 if layout == "v2" else 1)
+    g.force_f32_variant = var
+    assert g.f32_ks() == ks and g.f32_variant() == var
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     for l in learners:
@@ -184,7 +190,7 @@ def test_f32_optimizers_match_torch(dev, spec):
                 assert rel < 1e-3, f"{spec} peer {i} {name}: relative update error {rel:.2e}"
 
 
-@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2"])
+@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2", "v3ks1", "v3ks2"])
 @pytest.mark.parametrize("kind", ["fedprox", "scaffold", "scaffold_adam"])
 def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
     """FedProx mu·(w − anchor) and SCAFFOLD (c − c_i) gradient terms in the fp32 epoch kernel, at
@@ -198,10 +204,10 @@ def test_f32_fedprox_scaffold_terms_match_torch(dev, kind, layout):
     spec = {"fedprox": {"name": "sgd", "lr": 1e-3, "momentum": 0.9}, "scaffold": {"name": "sgd", "lr": 1e-4},
             "scaffold_adam": {"name": "adam", "lr": 1e-3}}[kind]
     learners, refs, g, n = _setup(dev, 2, 64, 900, 5, spec, scale=0.5)
-    ks = 2 if layout == "v1ks2" else 1
+    var, ks = _layout(layout)
     g.force_f32_ks = ks
-    g.force_f32_variant = 2 if layout == "v2" else 1
-    assert g.f32_ks() == ks and g.f32_variant() == (2 if layout == "v2" else 1)
+    g.force_f32_variant = var
+    assert g.f32_ks() == ks and g.f32_variant() == var
     perms = _pin_perms(dev, g, learners, n)
     p0 = [[p.detach().clone() for p in l.model.get_model().parameters()] for l in learners]
     gen = torch.Generator(device="cpu").manual_seed(9)
@@ -306,7 +312,7 @@ def test_f32_partial_last_batch_and_bias(dev):
             assert rel < 1e-4, f"peer {i} {name}: relative update error {rel:.2e}"
 
 
-@pytest.mark.parametrize("layout", [2, 1])
+@pytest.mark.parametrize("layout", [2, 1, 3])
 @pytest.mark.parametrize("at_end", [False, True])
 def test_f32_giveup_recovered_by_retry_launch(dev, at_end, layout):
     """A gang that gives up (here: forced on its first attempt through the engine's test hook, as a
