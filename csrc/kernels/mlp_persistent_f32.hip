@@ -141,6 +141,12 @@ static_assert(F_DONE + NCG * KSMAX + NH <= F32_FPP, "layout-1 flags fit the shar
 // updated columns each step; the heads hold W3 / b2 / b3 replicas and keep them identical by summing
 // the heads' partial gradients in a fixed order. Per step the critical chain loses the head <-> head
 // hand-off and three quarters of the softmax; W2 / partial-gradient traffic runs beside the owners.
+// Measured (profiles/r5_layout3, phase stamps, 8 peers): correct (every fp32 test), but 16.9 us per
+// step against layout 1's 14.5: the heads' tail shrinks (H2 + logits + softmax 3.4 us vs 4.0), while
+// the owners' dH2 phase grows 1.5 -> 4.0 us (the dW2 update moved onto their critical path pushes
+// the bench instantiation to 8 spilled VGPRs), and the row heads' H2 is twice the work per head
+// (16 x 128 outputs instead of 64 x 16). Opt-in (MLPGroup.force_f32_variant = 3 /
+// MYFYP_F32_VARIANT=3); layout 1 stays the default.
 constexpr int F3_DH2 = NCG * KSMAX;       // head r -> owners: dH2 rows 16r..16r+15 (BP / 16 heads)
 constexpr int F3_W2 = F3_DH2 + 4;         // owner cg (K part 0) -> heads: W2 columns 16cg.. after its update
 constexpr int F3_HP = F3_W2 + NCG;        // head r -> heads: partial dW3 / db2 / db3 over its rows

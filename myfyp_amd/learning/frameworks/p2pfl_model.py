@@ -67,8 +67,13 @@ class P2PFLModel:
         num_samples: Optional[int] = None,
         contributors: Optional[List[str]] = None,
         additional_info: Optional[Dict[str, Any]] = None,
+        compression: Optional[Dict[str, Any]] = None,
     ) -> None:
+        from myfyp_amd.learning import compression as _comp
+
         self.model = model
+        # wire compression of this model's payloads (learning/compression.py; None = reference format)
+        self.compression = _comp.validate(compression)
         self.contributors: List[str] = list(contributors) if contributors is not None else []
         self.num_samples: int = num_samples if num_samples is not None else 0
         self.additional_info: Dict[str, Any] = additional_info if additional_info is not None else {}
@@ -81,14 +86,18 @@ class P2PFLModel:
     # ------------------------------------------------------------------ wire format
     @traced("encode")
     def encode_parameters(self, params: Optional[List[np.ndarray]] = None) -> bytes:
+        from myfyp_amd.learning import compression as _comp
+
         if params is None:
             params = self.get_parameters()
-        return pickle.dumps({"params": params, "additional_info": _to_host(self.additional_info)})
+        return _comp.encode(params, _to_host(self.additional_info), getattr(self, "compression", None))
 
     def decode_parameters(self, data: bytes) -> Tuple[List[np.ndarray], Dict[str, Any]]:
+        """Reference payloads and compressed ones (``learning/compression.py``) alike."""
+        from myfyp_amd.learning import compression as _comp
+
         try:
-            loaded = safe_loads(data)
-            return loaded["params"], loaded["additional_info"]
+            return _comp.decode(data, safe_loads)
         except Exception as e:
             raise DecodingParamsError("Error decoding parameters") from e
 

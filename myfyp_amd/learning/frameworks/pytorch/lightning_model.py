@@ -14,9 +14,11 @@ from myfyp_amd.models.mlp import MLP
 
 class LightningModel(TorchModel):
     """Reference-named :class:`TorchModel` (same constructor: model, params, num_samples,
-    contributors, additional_info)."""
+    contributors, additional_info, and the newer upstream's ``compression=`` dict — see
+    :mod:`myfyp_amd.learning.compression`)."""
 
     def build_copy(self, **kwargs) -> "LightningModel":
+        kwargs.setdefault("compression", self.compression)
         return LightningModel(None, _shapes=self.expected_shapes(), **kwargs)
 
 

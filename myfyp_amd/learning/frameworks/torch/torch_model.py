@@ -32,10 +32,11 @@ class TorchModel(P2PFLModel):
         contributors: Optional[List[str]] = None,
         additional_info: Optional[Dict[str, Any]] = None,
         _shapes: Optional[List[tuple]] = None,
+        compression: Optional[Dict[str, Any]] = None,
     ) -> None:
         self._params: Optional[List[np.ndarray]] = None
         self._shapes = _shapes
-        super().__init__(model, params, num_samples, contributors, additional_info)
+        super().__init__(model, params, num_samples, contributors, additional_info, compression=compression)
 
     # ------------------------------------------------------------------ params
     def _state_tensors(self) -> List[torch.Tensor]:
@@ -81,6 +82,7 @@ class TorchModel(P2PFLModel):
                 dst.copy_(src_t.to(dst.dtype), non_blocking=False)
 
     def build_copy(self, **kwargs) -> "TorchModel":
+        kwargs.setdefault("compression", self.compression)
         return TorchModel(None, _shapes=self.expected_shapes(), **kwargs)
 
     def get_framework(self) -> str:

@@ -22,7 +22,7 @@ One description drives every experiment the examples, the CLI and the FYP harnes
           params: {alpha: 0.5}
       model:
         name: MLP               # MLP | LeNet5 | ResNet18, or package + model_build_fn
-        params: {}
+        params: {}              # + compression: {ptq: {dtype: float16}, topk: {k: 0.1}, zlib: {level: 6}}
       aggregator:
         name: FedAvg            # FedAvg | FedMedian | Scaffold | FedProx | Krum | TrimmedMean
         params: {}
@@ -119,9 +119,10 @@ def build_model(spec: Optional[Dict[str, Any]], seed: Optional[int] = None, inde
         raise ValueError(f"unknown model {name!r}; choose from MLP, LeNet5, ResNet18")
     import myfyp_amd.models as zoo
 
+    compression = params.pop("compression", spec.get("compression"))
     if "seed" not in params and seed is not None:
         params["seed"] = seed + index
-    return TorchModel(getattr(zoo, cls_name)(**params))
+    return TorchModel(getattr(zoo, cls_name)(**params), compression=compression)
 
 
 def build_dataset(spec: Optional[Dict[str, Any]]):
