@@ -133,3 +133,15 @@ def test_compressed_peers_federate_over_memory_protocol():
         for nd in nodes:
             nd.stop()
         Settings.USE_FUSED_KERNELS = saved
+
+
+def test_newer_upstream_protobuff_import_paths():
+    """``exp_SAVE3.txt:9`` imports ``p2pfl.communication.protocols.protobuff.memory``."""
+    from myfyp_amd.communication.protocols.memory.memory_communication_protocol import InMemoryCommunicationProtocol
+    from myfyp_amd.communication.protocols.protobuff.grpc import GrpcCommunicationProtocol
+    from myfyp_amd.communication.protocols.protobuff.memory import MemoryCommunicationProtocol
+    from myfyp_amd.runner import resolve_protocol
+
+    assert MemoryCommunicationProtocol is InMemoryCommunicationProtocol
+    assert GrpcCommunicationProtocol.__name__ == "GrpcCommunicationProtocol"
+    assert resolve_protocol({"package": "p2pfl.communication.protocols.protobuff.memory", "protocol": "MemoryCommunicationProtocol"}) is InMemoryCommunicationProtocol
