@@ -842,3 +842,11 @@ int cnn_opt_step(float* w, float* g, float* m, int64_t ps, const float* gf, int6
 }
 int cnn_segment_size() { return (int)sizeof(Segment); }
 }
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_cnn_ops() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_input_prep)) == hipSuccess ? 0 : 1;
+}

@@ -2236,3 +2236,11 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
 #undef WG_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_conv() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_conv_wt_flip)) == hipSuccess ? 0 : 1;
+}

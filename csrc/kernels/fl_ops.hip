@@ -400,3 +400,11 @@ void fl_opt_step(float* param, const float* grad, float* m, float* v, bf16* shad
 void fl_scale_add_noise(float* t, int64_t n, float scale, float sigma, uint64_t seed, hipStream_t s) {
   hipLaunchKernelGGL(k_scale_add_noise, dim3(grid_for(n)), dim3(FL_BLOCK), 0, s, t, n, scale, sigma, seed);
 }
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_fl_ops() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_weighted_sum)) == hipSuccess ? 0 : 1;
+}

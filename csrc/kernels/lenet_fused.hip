@@ -792,3 +792,11 @@ int lenet_fused_step(const LenetArgs* a, int peers, int ipw, void* stream) {
 }
 
 }  // extern "C"
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_lenet() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_lenet_fc_grad<2>)) == hipSuccess ? 0 : 1;
+}

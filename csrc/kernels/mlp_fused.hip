@@ -801,3 +801,11 @@ void mlp_launch_sync_shadow(const MLPArgs& a, hipStream_t s) {
   const int64_t blocks = (a.numel + 255) / 256;
   hipLaunchKernelGGL(mlp_sync_shadow, dim3((unsigned)(blocks < 1024 ? blocks : 1024), a.P), dim3(256), 0, s, a);
 }
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_mlp_fused() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&mlp_wgrad_opt)) == hipSuccess ? 0 : 1;
+}

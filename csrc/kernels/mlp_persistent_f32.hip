@@ -1970,3 +1970,11 @@ void mlp_launch_eval_f32(const MLPArgs& a, int max_rows, hipStream_t s) {
   const dim3 grid((max_rows + EV_ROWS - 1) / EV_ROWS, a.P);
   hipLaunchKernelGGL(mlp_eval_f32, grid, dim3(NT), eval_lds32(a.D0), s, a);
 }
+
+// Resolve one kernel of this translation unit on the current device: loads the unit's code object
+// now (myfyp_warm_all, at engine prewarm) instead of at its first launch, which waited for the
+// kernels in flight (the first FedAvg launch blocked the host until the running epoch ended)
+extern "C" int myfyp_warm_mlp_f32() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&mlp_eval_f32)) == hipSuccess ? 0 : 1;
+}

@@ -615,9 +615,15 @@ struct MLPEngine {
       const char* e2 = getenv("MYFYP_GRAPH_EXECS");
       n_execs = (!prep_mode && e2 != nullptr && atoi(e2) == 1) ? 1 : 2;
     }
+    const auto c0 = std::chrono::steady_clock::now();
     if (capture_one(steps, 0, &graph)) return 1;
     if (prep_mode && capture_one(steps, 1, &graph_alt)) return 1;
+    const auto c1 = std::chrono::steady_clock::now();
     for (int i = 0; i < n_execs; ++i) CHECK_HIP(hipGraphInstantiate(&execs[i], (prep_mode && i == 1) ? graph_alt : graph, nullptr, nullptr, 0));
+    if (const char* tv = getenv("MYFYP_TIME_PREPARE"); tv != nullptr && atoi(tv) != 0)
+      fprintf(stderr, "[prepare] capture_one x%d %lld us, instantiate x%d %lld us\n", prep_mode ? 2 : 1,
+              (long long)std::chrono::duration_cast<std::chrono::microseconds>(c1 - c0).count(), n_execs,
+              (long long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - c1).count());
     exec = execs[0];
     graph_steps = steps;
     return 0;
@@ -1211,17 +1217,33 @@ int mlp_engine_prepare(void* h, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (e->max_steps <= 0) return 0;
   if (e->precision == 1 && !e->use_persistent()) return 0;  // run_epoch reports it
+  // MYFYP_TIME_PREPARE=1: host µs of each part on stderr (node-start breakdown, profiles/r5_start)
+  static const bool timed = [] {
+    const char* v = getenv("MYFYP_TIME_PREPARE");
+    return v != nullptr && atoi(v) != 0;
+  }();
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+  };
+  const auto t0 = now();
   if (!e->exec || e->graph_steps != e->max_steps) {
     if (e->capture(e->max_steps)) return 1;
   }
+  const auto t1 = now();
   for (int i = 0; i < e->n_execs; ++i)
     if (e->execs[i]) CHECK_HIP(hipGraphUpload(e->execs[i], s));
+  const auto t2 = now();
   if (e->use_persistent() && e->ensure_eval_side()) return 1;
+  const auto t3 = now();
   // code-object load: a publish of zero peers (its only store zeroes d_correct[0], which every fit
   // re-zeroes before accumulating; no ring slot is touched)
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, e->d_loss, e->d_correct, (const int*)nullptr, (const int*)nullptr, 0, e->d_loss,
                      e->d_correct, e->d_correct, (int*)nullptr, (unsigned*)nullptr, 0u);
   CHECK_HIP(hipGetLastError());
+  if (timed)
+    fprintf(stderr, "[prepare] capture %lld us, upload %lld us, eval side %lld us, publish launch %lld us\n", us(t0, t1), us(t1, t2), us(t2, t3),
+            us(t3, now()));
   return 0;
 }
 
@@ -1463,3 +1485,20 @@ int mlp_engine_eval(void* h, const int* active_host, float* loss_host, int* corr
 }
 
 }  // extern "C"
+
+// Load every kernel translation unit's code object on the current device (engine prewarm, once per
+// device): a unit's first launch otherwise loads it then, and that load waited for the kernels in
+// flight — the first FedAvg of a run blocked the host for the whole running epoch (1.7 ms,
+// profiles/r5_start). Returns the number of units that failed to resolve.
+extern "C" int myfyp_warm_fl_ops();
+extern "C" int myfyp_warm_cnn_ops();
+extern "C" int myfyp_warm_conv();
+extern "C" int myfyp_warm_lenet();
+extern "C" int myfyp_warm_mlp_fused();
+extern "C" int myfyp_warm_mlp_f32();
+extern "C" int myfyp_warm_all() {
+  hipFuncAttributes attr;
+  int bad = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_publish)) == hipSuccess ? 0 : 1;
+  bad += myfyp_warm_fl_ops() + myfyp_warm_cnn_ops() + myfyp_warm_conv() + myfyp_warm_lenet() + myfyp_warm_mlp_fused() + myfyp_warm_mlp_f32();
+  return bad;
+}

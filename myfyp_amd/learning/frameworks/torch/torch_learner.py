@@ -74,7 +74,7 @@ class TorchLearner(Learner):
         self.mesh_rank = mesh_rank
         self.batch_size = int(batch_size or Settings.BATCH_SIZE)
         self._interrupt = threading.Event()
-        self._data_cache: Dict[bool, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._data_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._data_key: Optional[int] = None
         self.global_step = 0
         self._engine = None  # fused grouped engine handle (set by _maybe_attach_engine)
@@ -166,16 +166,24 @@ class TorchLearner(Learner):
             self._engine.group.invalidate_data()
 
     # ------------------------------------------------------------------ data
-    def device_data(self, train: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    def device_data(self, train: bool = True, label_dtype: torch.dtype = torch.int64) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(images, labels) of the split on the learner's device, cached per split and label dtype.
+        Labels are converted on the host: the fused engines' int32 tables then cost no torch kernel
+        at node start (a torch kernel's first launch in a process loads its code object: tens of
+        ms on a fresh box, measured in ``profiles/r5_start``)."""
         key = id(self.data)
         if self._data_key != key:
             self._data_cache.clear()
             self._data_key = key
-        if train not in self._data_cache:
-            x = torch.from_numpy(np.ascontiguousarray(self.data.column("image", train)))
-            y = torch.from_numpy(np.ascontiguousarray(self.data.column("label", train)).astype(np.int64))
-            self._data_cache[train] = (x.to(self.device), y.to(self.device))
-        return self._data_cache[train]
+        ck = (train, label_dtype)
+        if ck not in self._data_cache:
+            xd = next((v[0] for k, v in self._data_cache.items() if k[0] == train), None)
+            if xd is None:
+                xd = torch.from_numpy(np.ascontiguousarray(self.data.column("image", train))).to(self.device)
+            ny = {torch.int64: np.int64, torch.int32: np.int32}[label_dtype]
+            y = torch.from_numpy(np.ascontiguousarray(self.data.column("label", train)).astype(ny))
+            self._data_cache[ck] = (xd, y.to(self.device))
+        return self._data_cache[ck]
 
     def num_train_samples(self) -> int:
         return self.data.get_num_samples(train=True)
@@ -227,7 +235,7 @@ class TorchLearner(Learner):
         if mean_loss is not None:
             snap, addr, gs = logger.experiment_snapshot(self._self_addr), self._self_addr, self.global_step
             if isinstance(mean_loss, Pending):  # fused engine: logged when the device result lands
-                mean_loss.add_done_callback(lambda v: logger.log_metric_at(addr, snap, "train_loss", float(v), step=gs))
+                mean_loss.map_off_thread(lambda v: logger.log_metric_at(addr, snap, "train_loss", float(v), step=gs))
             else:
                 logger.log_metric_at(addr, snap, "train_loss", float(mean_loss), step=gs)
         for cb in self.callbacks:
@@ -344,7 +352,7 @@ class TorchLearner(Learner):
                 logger.log_metric_at(addr, snap, k, v)
             return results
 
-        return raw.map(done)
+        return raw.map_off_thread(done)
 
     @traced("evaluate")
     def evaluate(self) -> Dict[str, float]:

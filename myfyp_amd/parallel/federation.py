@@ -58,6 +58,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 import torch
 
 from myfyp_amd.management.logger import logger
+from myfyp_amd.management.tracing import mark
 from myfyp_amd.settings import Settings
 from myfyp_amd.learning.frameworks.p2pfl_model import safe_loads
 from myfyp_amd.utils.lockcheck import make_lock
@@ -895,6 +896,7 @@ class Federation:
         take part always completes the collectives it agreed to (a concurrent ``depart()`` takes
         effect at exit). Nested sections reuse the outer agreement."""
         with self._section_lock:
+            mark("section:in")
             outer = self._frozen is not None
             if not outer and self.mesh is not None:
                 self.mesh_sync()  # devices whose last peer stopped leave the mesh first

@@ -426,6 +426,7 @@ class MLPGroup:
         a later change (another peer attaching, other optimizer settings) re-captures as before."""
         lib = _native.load(required=True)
         with self.lock, self.on_device():
+            _native.warm_device(torch.cuda.current_device())
             self._ensure_engine()
             self._set_optimizer(lib, spec, 0.0, None, None, None)
             _native.check(lib.mlp_engine_prepare(self._engine, torch.cuda.current_stream(self.device).cuda_stream), "prepare")
@@ -688,13 +689,13 @@ class MLPEngineHandle:
         if self.learner is None or self.learner.data is None:
             D0 = self.group.dims[0]
             return torch.zeros(0, D0, dtype=torch.uint8, device=self.group.device), torch.zeros(0, dtype=torch.int32, device=self.group.device)
-        x, y = self.learner.device_data(train)
+        x, y = self.learner.device_data(train, label_dtype=torch.int32)
         x = x.reshape(x.shape[0], -1)
         if x.dtype != torch.uint8:
             raise TypeError("fused MLP engine expects uint8 images")
         if not x.is_contiguous():
             x = x.contiguous()
-        return x, y.to(torch.int32)
+        return x, y
 
     def fit(self, learner, spec: dict, extra: dict) -> Tuple[int, float]:
         if self.learner is not learner or getattr(self, "_data_id", None) != id(learner.data):

@@ -69,6 +69,31 @@ class Pending:
         self.add_done_callback(lambda v: out.set_result(fn(v)))
         return out
 
+    def map_off_thread(self, fn: Callable[[Any], Any]) -> "Pending":
+        """Like :meth:`map`, but ``fn`` never runs on the calling thread: if the value is already
+        there, ``fn`` goes to the shared resolver thread (FIFO behind earlier results). For heavy
+        callbacks (metric logging) issued from the round driver: after a device synchronisation
+        every result of the queued rounds is already resolved, and running their logging inline
+        held the next launch back by 0.7 ms (``profiles/r5_start``)."""
+        with self._lock:
+            if not self._ev.is_set():
+                out = Pending()
+
+                def cb(v: Any) -> None:
+                    try:
+                        out.set_result(fn(v))
+                    except BaseException as e:  # surfaced to whoever waits on the Pending
+                        out.set_exception(e)
+
+                self._cbs.append(cb)
+                return out
+        if self._exc is not None:
+            out = Pending()
+            out.set_exception(self._exc)
+            return out
+        v = self._value
+        return Resolver.shared().submit(lambda: fn(v))
+
 
 def resolve(value: Any) -> Any:
     """Value of ``value`` (waiting if it is a :class:`Pending`)."""

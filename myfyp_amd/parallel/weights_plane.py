@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from myfyp_amd import ops
-from myfyp_amd.management.tracing import traced
+from myfyp_amd.management.tracing import mark, traced
 from myfyp_amd.parallel.federation import Federation
 
 
@@ -233,7 +233,9 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
         fed.defer_confirm(works, retry)
         return
     if fed.solo:  # nothing to all-reduce: weighted mean and write-back in one launch
+        mark("agg:launch")
         ops.check(fast.myfyp_fedavg_stacked_local(base, P, n, S, wp, mp, cur.cuda_stream), "fedavg_local")
+        mark("agg:launched")
         return
     if not Settings.OVERLAP_COLLECTIVES:
         buf = group.fedavg_buffer()
@@ -312,6 +314,7 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
     t0 = time.perf_counter()
 
     def run() -> Tuple[float, List[str]]:
+        mark("agg:run")
         addrs = [a for a in arrived if a in fed.local_nodes]  # a peer may die after arriving
         learners = [fed.local_nodes[a].learner for a in addrs]
         weights = [float(arrived[a][0]) for a in addrs]

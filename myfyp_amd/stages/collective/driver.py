@@ -145,15 +145,18 @@ class RoundDriver:
                     reqs[a] = lr.fit_request()
                     n[a] = lr.num_train_samples()
             out: Dict[str, Any] = {}
+            mark("driver:launch")
             if trainers:
                 has_test = {a for a in trainers if (d := cur[a].kw["learner"].data) is not None and d.get_num_samples(train=False) > 0}
                 out = fused_round.run_groups(f, trainers, lambda a: cur[a].kw["learner"]._engine.slot, lambda a: cur[a].kw["learner"]._engine.group,
                                              reqs, has_test)
+            mark("driver:aggregate")
             total = next(iter(states.values())).total_rounds
             aggregator = next(iter(cur.values())).kw["aggregator"]
             fused_round.aggregate(f, {a: (n.get(a, 0), None) for a in cur}, aggregator, final=total is None or round_ + 1 >= total)
             for hook in list(f.round_hooks):
                 hook(round_, f)
+            mark("driver:results")
             for a, m in cur.items():
                 lr = m.kw["learner"]
                 if a in out:
@@ -166,6 +169,7 @@ class RoundDriver:
                 model = lr.get_model()
                 model.set_contribution(train_set or [a], max(1, model.num_samples))
             # ---- GossipModelStage (no-op after the all-reduce) and RoundFinishedStage
+            mark("driver:finish")
             final = []
             for a, m in cur.items():
                 st = m.kw["state"]
@@ -189,6 +193,7 @@ class RoundDriver:
             cur = live()
             if not cur:
                 return
+            mark("driver:vote")
             votes = {}
             for a, m in cur.items():
                 history(m, "VoteTrainSetStage")

@@ -30,3 +30,14 @@ class StageFactory:
             raise Exception("Invalid stage name.")
         pkg = "base_node" if flavor == "gossip" else "collective"
         return getattr(importlib.import_module(f"myfyp_amd.stages.{pkg}.{mod}"), stage_name)
+
+    @staticmethod
+    def preload(flavor: str = "gossip") -> None:
+        """Import every stage module of ``flavor`` now (workflow construction), not on the first
+        transition: a first import inside a running experiment held the import lock for several ms
+        while all eight peer threads queued on it between StartLearning and the first vote
+        (``scripts/probes/start_sampler.py``, ``profiles/r5_start``)."""
+        for name in _STAGES:
+            StageFactory.get_stage(name, flavor)
+        if flavor != "gossip":
+            importlib.import_module("myfyp_amd.stages.collective.driver")

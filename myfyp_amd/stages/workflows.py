@@ -55,4 +55,5 @@ class LearningWorkflow(StageWokflow):
 
     def __init__(self, flavor: str = "gossip") -> None:
         self.flavor = flavor
+        StageFactory.preload(flavor)
         super().__init__(StageFactory.get_stage("StartLearningStage", flavor))

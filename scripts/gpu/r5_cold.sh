@@ -1,0 +1,7 @@
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 200 python scripts/probes/cold_probe.py > gpurun_out/cold_1.log 2>&1
+timeout -k 10 200 python scripts/probes/cold_probe.py > gpurun_out/cold_2.log 2>&1
+timeout -k 10 200 python scripts/probes/start_breakdown.py > gpurun_out/start_c.log 2>&1

@@ -1,0 +1,5 @@
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+MYFYP_ROCTX=1 timeout -k 10 240 rocprofv3 --kernel-trace --marker-trace --output-format csv -d gpurun_out/bench_trace -o run -- python bench.py --steps 20 --warmup 5 > gpurun_out/bench_trace.log 2>&1
