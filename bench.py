@@ -155,18 +155,35 @@ def main() -> None:
         for i in cuda_devs:
             torch.cuda.synchronize(i)
 
-    def hook(r: int, f) -> None:
-        if r == args.warmup - 1 or (args.warmup == 0 and r == -1):
+    def start_hook(r: int, f) -> None:
+        # the first timed round starts here: its train set is known, nothing of it is launched yet,
+        # and every warmup round has been launched (barrier + synchronize, then the clock starts)
+        if args.warmup > 0 and r == args.warmup:
             f.barrier()
             dev_sync()
             marks["t0"] = time.perf_counter()
+
+    def hook(r: int, f) -> None:
         round_end[r] = time.perf_counter()
-        if r == total_rounds - 1:
+        if r == total_rounds - 1:  # the last timed round's work is all enqueued
             dev_sync()
             f.barrier()
             marks["t1"] = time.perf_counter()
 
+    fed.round_start_hooks.append(start_hook)
     fed.round_hooks.append(hook)
+    import gc
+
+    gc_pauses: list = []  # diagnostics: interpreter garbage-collection pauses during the run
+    gc_t: dict = {}
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gc_t["t"] = time.perf_counter()
+        elif "t" in gc_t:
+            gc_pauses.append((info.get("generation", -1), 1000.0 * (time.perf_counter() - gc_t.pop("t"))))
+
+    gc.callbacks.append(on_gc)
     # evaluations resolve asynchronously: record when each round's accuracy actually landed on the host
     landed: dict = {}
     local_addrs = {n.addr for n in nodes}
@@ -223,6 +240,10 @@ def main() -> None:
         d = np.diff(ends) * 1000.0
         print(f"[bench] rank {rank} round-end interval ms: p10 {np.percentile(d, 10):.3f} p50 {np.percentile(d, 50):.3f} "
               f"p90 {np.percentile(d, 90):.3f} max {d.max():.3f}", file=sys.stderr, flush=True)
+    if gc_pauses:
+        worst = max(gc_pauses, key=lambda g: g[1])
+        print(f"[bench] rank {rank} gc pauses: {len(gc_pauses)}, total {sum(g[1] for g in gc_pauses):.2f} ms, max {worst[1]:.2f} ms (gen {worst[0]}), "
+              f"gen2: {sum(1 for g in gc_pauses if g[0] == 2)}", file=sys.stderr, flush=True)
     print(f"[bench] rank {rank} median ms per call: {json.dumps(brk)} fed: "
           f"{ {k: round(1000 * float(np.median(v)), 3) for k, v in fed.stats.items()} }", file=sys.stderr, flush=True)
     eng = getattr(nodes[0].learner, "_engine", None)

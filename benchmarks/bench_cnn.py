@@ -178,17 +178,20 @@ def main() -> None:
         for i in cuda_devs:
             torch.cuda.synchronize(i)
 
-    def hook(r, f):
-        if r == args.warmup - 1:
+    def start_hook(r, f):  # the first timed round's train set is known, nothing of it launched
+        if args.warmup > 0 and r == args.warmup:
             f.barrier()
             sync()
             marks["t0"] = time.perf_counter()
+
+    def hook(r, f):
         round_end[r] = time.perf_counter()
         if r == total - 1:
             sync()
             f.barrier()
             marks["t1"] = time.perf_counter()
 
+    fed.round_start_hooks.append(start_hook)
     fed.round_hooks.append(hook)
     landed: dict = {}  # round -> [(acc, host time the evaluation landed)]
     local_addrs = {n.addr for n in nodes}

@@ -287,6 +287,9 @@ class Federation:
         self.gang = LocalGang()
         self.finalized = threading.Event()
         self.round_hooks: List[Callable[[int, "Federation"], None]] = []
+        # called once per round and process when the round's train set is known, before its first
+        # launch (the vote's gang leader, or the round driver): (round, federation)
+        self.round_start_hooks: List[Callable[[int, "Federation"], None]] = []
         self.stats: Dict[str, List[float]] = {}
         self._lock = make_lock("Federation.state")
         self._cpu_pg = None

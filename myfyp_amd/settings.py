@@ -138,6 +138,9 @@ class Settings:
     # interpreter GIL switch interval (s) set by Federation.init: co-located peer threads hand the
     # GIL over often, and a thread returning from a device call waits up to this long for it
     GIL_SWITCH_INTERVAL: float | None = 2e-4
+    # objects alive when an experiment starts go to the collector's permanent generation for its
+    # duration (utils/gc_tuning.py): no full collection re-walks them mid-run
+    GC_FREEZE: bool = True
     # collective workflow: evaluate + fit + FedAvg of co-located fused-engine peers as ONE gang op
     FUSED_ROUND: bool = True
     # ... and the rounds of all co-located fused peers are driven by ONE host thread (driver.py)
@@ -223,6 +226,7 @@ class Settings:
             "RCCL_MAX_CHANNELS": "RCCL_MAX_CHANNELS",
             "ENGINE_PREWARM": "ENGINE_PREWARM",
             "GIL_SWITCH_INTERVAL": "GIL_SWITCH_INTERVAL",
+            "GC_FREEZE": "GC_FREEZE",
             "FUSED_ROUND": "FUSED_ROUND",
             "ROUND_DRIVER": "ROUND_DRIVER",
             "MESH_DEVICES": "MESH_DEVICES",

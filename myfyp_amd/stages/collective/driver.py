@@ -207,6 +207,8 @@ class RoundDriver:
                 train_set = tally_votes(allv)
             for a, m in cur.items():
                 m.kw["state"].train_set = list(train_set)
+            for hook in list(f.round_start_hooks):
+                hook(next(iter(cur.values())).kw["state"].round, f)
 
     def _finish(self, done: Dict[str, _Member]) -> None:
         """Last round's RoundFinishedStage tail: final evaluation, state reset, experiment end."""

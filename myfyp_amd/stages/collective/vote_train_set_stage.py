@@ -39,6 +39,8 @@ class VoteTrainSetStage(Stage):
             # ranks learn who is alive
             train_set = sorted(allv, key=lambda a: f.all_peers().index(a)) if everyone else tally_votes(allv)
             set_gang_expectations(f, set(train_set), set(train_set))
+            for hook in list(f.round_start_hooks):
+                hook(state.round, f)
             return train_set, fused_round.eligible(f, aggregator), driver.eligible(f, aggregator)
 
         train_set, state.fused_round, drive = f.gang_run(state.addr, votes, leader)
