@@ -227,7 +227,8 @@ struct MLPEngine {
   int n_execs = 2;
   unsigned long long launches = 0, launch_ns = 0, launch_max_ns = 0;
   int graph_steps = -1;
-  hipStream_t cap_stream = nullptr;
+  hipStream_t cap_stream = nullptr;  // capture stream when there is no prep stream to capture on
+  hipStream_t cs = nullptr;          // the stream the current capture runs on
   // engine-owned device buffers
   void* ws = nullptr;
   int* d_active = nullptr;
@@ -513,9 +514,31 @@ struct MLPEngine {
     graph_steps = -1;
   }
 
+  // Zeroed device buffer owned by the engine. Small ones (control words, accumulators, flags) are
+  // carved out of 2 MiB arena chunks that are allocated and zeroed once: an engine makes ~30 of
+  // them, and a hipMalloc + synchronous hipMemset each cost node start several ms
+  // (profiles/r5_start). 256-byte alignment (every consumer wants at most 16).
+  static constexpr size_t kArenaChunk = 2u << 20, kArenaMax = 256u << 10, kArenaAlign = 256;
+  char* arena = nullptr;
+  size_t arena_used = kArenaChunk;
   int alloc(void** p, size_t bytes) {
-    CHECK_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
-    CHECK_HIP(hipMemset(*p, 0, bytes < 16 ? 16 : bytes));
+    bytes = bytes < 16 ? 16 : bytes;
+    if (bytes <= kArenaMax) {
+      const size_t need = (bytes + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+      if (arena_used + need > kArenaChunk) {
+        void* c = nullptr;
+        CHECK_HIP(hipMalloc(&c, kArenaChunk));
+        CHECK_HIP(hipMemset(c, 0, kArenaChunk));
+        owned.push_back(c);
+        arena = (char*)c;
+        arena_used = 0;
+      }
+      *p = arena + arena_used;
+      arena_used += need;
+      return 0;
+    }
+    CHECK_HIP(hipMalloc(p, bytes));
+    CHECK_HIP(hipMemset(*p, 0, bytes));
     owned.push_back(*p);
     return 0;
   }
@@ -539,28 +562,28 @@ struct MLPEngine {
       a.Xb16 = xb16_buf[buf];
       a.Yb = yb_buf[buf];
     }
-    CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeRelaxed));
+    CHECK_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
     if (x_direct) {
       MLPArgs ga = a;
       set_flag_zeroing(ga);  // the index kernel zeroes the hand-off flags (no memset node)
-      mlp_launch_index_epoch(ga, cap_stream);
+      mlp_launch_index_epoch(ga, cs);
     } else if (!prep_mode) {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
       if (graph_persistent) set_flag_zeroing(ga);  // ... which also zeroes the hand-off flags (no memset node)
-      mlp_launch_gather_epoch(ga, cap_stream);
+      mlp_launch_gather_epoch(ga, cs);
     }
     int rc = 0;
     if (graph_persistent) {
-      rc = launch_epoch_kernel(cap_stream, false);
+      rc = launch_epoch_kernel(cs, false);
     } else {
-      for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cap_stream);
+      for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cs);
     }
     graph_has_pub = graph_publish() && !ring_events() && d_pub != nullptr;
-    if (graph_has_pub) hipLaunchKernelGGL(k_publish_dev, dim3(1), dim3(256), 0, cap_stream, d_loss, d_correct, pb.err, a.P, (const PubDst*)d_pub);
+    if (graph_has_pub) hipLaunchKernelGGL(k_publish_dev, dim3(1), dim3(256), 0, cs, d_loss, d_correct, pb.err, a.P, (const PubDst*)d_pub);
     a = saved;
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(cap_stream, &g);
+    const hipError_t e = hipStreamEndCapture(cs, &g);
     if (rc || e != hipSuccess) {
       if (g) hipGraphDestroy(g);
       if (!rc) g_last_error = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
@@ -590,9 +613,11 @@ struct MLPEngine {
   }
 
   int capture(int steps) {
+    const auto q0 = std::chrono::steady_clock::now();
     invalidate();
-    if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    const auto q1 = std::chrono::steady_clock::now();
     graph_persistent = use_persistent();
+    const auto q2 = std::chrono::steady_clock::now();
     x_direct = graph_persistent && precision == 1 && mlp_persistent_f32_x_direct(a);
     if (x_direct && (a.Xp16 == nullptr || a.xidx == nullptr)) {
       g_last_error = "fp32 direct-X epoch: no bf16 image table bound (mlp_engine_set_train_x16)";
@@ -615,7 +640,23 @@ struct MLPEngine {
       const char* e2 = getenv("MYFYP_GRAPH_EXECS");
       n_execs = (!prep_mode && e2 != nullptr && atoi(e2) == 1) ? 1 : 2;
     }
+    // capture on the prep stream when there is one (the engine's launches are serialised by its
+    // mutex, so nothing else enqueues there meanwhile): each stream beyond the first few costs a
+    // hardware queue, 5.5 ms to create (profiles/r5_start)
+    if (prep_mode) {
+      CHECK_HIP(hipStreamSynchronize(prep_stream));  // a re-capture: the previous graph's gather is done
+      cs = prep_stream;
+    } else {
+      if (!cap_stream) CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+      cs = cap_stream;
+    }
     const auto c0 = std::chrono::steady_clock::now();
+    if (const char* tv = getenv("MYFYP_TIME_PREPARE"); tv != nullptr && atoi(tv) != 0) {
+      auto d = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return (long long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+      };
+      fprintf(stderr, "[prepare] invalidate+stream %lld us, use_persistent %lld us, prep setup %lld us\n", d(q0, q1), d(q1, q2), d(q2, c0));
+    }
     if (capture_one(steps, 0, &graph)) return 1;
     if (prep_mode && capture_one(steps, 1, &graph_alt)) return 1;
     const auto c1 = std::chrono::steady_clock::now();
@@ -1496,9 +1537,12 @@ extern "C" int myfyp_warm_conv();
 extern "C" int myfyp_warm_lenet();
 extern "C" int myfyp_warm_mlp_fused();
 extern "C" int myfyp_warm_mlp_f32();
-extern "C" int myfyp_warm_all() {
+// families: bit 0 = the MLP engine's units, bit 1 = the CNN engine's (FedAvg kernels in both)
+extern "C" int myfyp_warm_all(int families) {
   hipFuncAttributes attr;
-  int bad = hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_publish)) == hipSuccess ? 0 : 1;
-  bad += myfyp_warm_fl_ops() + myfyp_warm_cnn_ops() + myfyp_warm_conv() + myfyp_warm_lenet() + myfyp_warm_mlp_fused() + myfyp_warm_mlp_f32();
+  int bad = myfyp_warm_fl_ops();
+  if (families & 1)
+    bad += (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_publish)) == hipSuccess ? 0 : 1) + myfyp_warm_mlp_fused() + myfyp_warm_mlp_f32();
+  if (families & 2) bad += myfyp_warm_cnn_ops() + myfyp_warm_conv() + myfyp_warm_lenet();
   return bad;
 }

@@ -99,7 +99,7 @@ _SIGNATURES = {
     "mlp_engine_f32_variant": (c_int, [c_void_p]),
     "mlp_engine_debug_giveup": (c_int, [c_void_p, c_int, c_int]),
     "mlp_engine_prepare": (c_int, [c_void_p, c_void_p]),
-    "myfyp_warm_all": (c_int, []),
+    "myfyp_warm_all": (c_int, [c_int]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
     "mlp_debug_persistent_f32_stamps": (c_int, [c_void_p]),  # likewise
 }
@@ -157,19 +157,20 @@ def load_fast() -> ctypes.PyDLL:
 _WARM: set = set()
 
 
-def warm_device(index: int) -> None:
-    """Load every kernel unit's code object on device ``index`` (the current device), once per
-    process and device: engine prewarm. A unit's first launch would otherwise load it then, waiting
-    for the kernels in flight (``myfyp_warm_all`` in engine.hip)."""
-    if index in _WARM:
+def warm_device(index: int, family: str = "mlp") -> None:
+    """Load the kernel units an engine ``family`` ("mlp" or "cnn") launches on device ``index`` (the
+    current device), once per process, device and family: engine prewarm. A unit's first launch
+    would otherwise load it then, waiting for the kernels in flight (``myfyp_warm_all``)."""
+    key = (index, family)
+    if key in _WARM:
         return
     lib = load(required=True)
     fn = getattr(lib, "myfyp_warm_all", None)
     if fn is not None:
-        bad = int(fn())
+        bad = int(fn(1 if family == "mlp" else 2))
         if bad:
             raise RuntimeError(f"native code objects: {bad} kernel unit(s) failed to load on device {index}")
-    _WARM.add(index)
+    _WARM.add(key)
 
 
 def available() -> bool:

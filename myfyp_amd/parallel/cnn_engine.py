@@ -238,7 +238,7 @@ class CNNGroup:
         self.arch = arch_of(template)
         if device.type == "cuda":  # code objects loaded now, not at a first launch behind running kernels
             with torch.cuda.device(device):
-                _native.warm_device(torch.cuda.current_device())
+                _native.warm_device(torch.cuda.current_device(), "cnn")
         self.lock = threading.RLock()
         self.resolver: Optional[Resolver] = None  # created on first use (device result copies)
         self.handles: Dict[int, "CNNEngineHandle"] = {}

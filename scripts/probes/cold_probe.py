@@ -41,4 +41,10 @@ x3 = step("h2d_pinned_47MB", lambda: hp.to("cuda", non_blocking=True))
 small = [np.ascontiguousarray(h[i * 7500:(i + 1) * 7500]) for i in range(8)]
 step("h2d_pageable_8x5.9MB", lambda: [torch.from_numpy(s).to("cuda") for s in small])
 step("first_kernel_fedavg", lambda: torch.zeros(8, 1024, device="cuda").sum(0))
+streams = []
+for i in range(5):
+    step(f"stream_create_{i}", lambda: streams.append(torch.cuda.Stream()))
+evs = []
+step("events_x8", lambda: [evs.append(torch.cuda.Event()) for _ in range(8)])
+step("warm_all", lambda: lib.myfyp_warm_all(3))
 print(json.dumps(out), flush=True)
