@@ -270,6 +270,7 @@ struct MLPEngine {
   // the previous evaluation cost the main stream a 6-7 us idle gap every round
   // (profiles/r4j_*/timeline.txt); evaluation r-2 ends about a round before the host gets here.
   hipStream_t eval_stream = nullptr;
+  bool eval_stream_owned = false;  // false: it is the prep stream
   hipEvent_t ev_snap = nullptr;
   struct EvalSide {
     float* params = nullptr;
@@ -343,7 +344,7 @@ struct MLPEngine {
     }
     if (xb16_buf[1]) hipFree(xb16_buf[1]);
     if (yb_buf[1]) hipFree(yb_buf[1]);
-    if (eval_stream) {
+    if (eval_stream && eval_stream_owned) {
       hipStreamSynchronize(eval_stream);
       hipStreamDestroy(eval_stream);
     }
@@ -463,7 +464,11 @@ struct MLPEngine {
   // evaluation resources for the overlapped path (allocated on first use)
   int ensure_eval_side() {
     if (!eval_stream) {
+      // a stream of its own: sharing the prep stream saved 5.5 ms of node start (one hardware
+      // queue fewer) but cost 15 % of the round rate (452-456 vs 527-539 rounds/s,
+      // profiles/r5_start): the evaluation's wait for the snapshot held the next-epoch gather
       CHECK_HIP(hipStreamCreateWithFlags(&eval_stream, hipStreamNonBlocking));
+      eval_stream_owned = true;
       CHECK_HIP(hipEventCreateWithFlags(&ev_snap, hipEventDisableTiming));
       for (auto& es : eside) {
         CHECK_HIP(hipEventCreateWithFlags(&es.done, hipEventDisableTiming));
