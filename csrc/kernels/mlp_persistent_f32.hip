@@ -48,18 +48,31 @@ void mlp_f32v2_launch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t
 
 // Optional phase timestamps (build with -DMLP_STAMPS): peer 0's owner 0 (role 0) and head 0 (role 1),
 // steps < 32, read with mlp_debug_persistent_f32_stamps (wall_clock64 ticks, 100 MHz).
+// Epoch-level stamps of peer 0's owner 0: [0] kernel entry, [1] first step start, [2] gang commit
+// passed, [3] write-back done (mlp_debug_persistent_f32_epoch_stamps).
 #ifdef MLP_STAMPS
-__device__ unsigned long long g_p32_stamps[2][32][10];
-#define P32_STAMP(role, t, i)                                                                   \
-  do {                                                                                          \
-    if (p == 0 && threadIdx.x == 0 && (t) < 32) g_p32_stamps[role][t][i] = wall_clock64(); \
+__device__ unsigned long long g_p32_stamps[2][128][10];
+__device__ unsigned long long g_p32_epoch[4];
+#define P32_STAMP(role, t, i)                                                                    \
+  do {                                                                                           \
+    if (p == 0 && threadIdx.x == 0 && (t) < 128) g_p32_stamps[role][t][i] = wall_clock64(); \
+  } while (0)
+#define P32_ESTAMP(i)                                        \
+  do {                                                       \
+    if (p == 0 && threadIdx.x == 0) g_p32_epoch[i] = wall_clock64(); \
   } while (0)
 extern "C" int mlp_debug_persistent_f32_stamps(void* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p32_stamps), sizeof(g_p32_stamps)) == hipSuccess ? 0 : 1;
 }
+extern "C" int mlp_debug_persistent_f32_epoch_stamps(void* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p32_epoch), sizeof(g_p32_epoch)) == hipSuccess ? 0 : 1;
+}
 #else
 #define P32_STAMP(role, t, i) \
   do {                        \
+  } while (0)
+#define P32_ESTAMP(i) \
+  do {                \
   } while (0)
 #endif
 
@@ -731,6 +744,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   }
 
   if (!gang_commit<KS, RH, BP>(a, pb, p, g, sOk)) return;
+  if (g == 0) P32_ESTAMP(2);
   // ---- write the state back (fp32 master weights and moments; b1 from the bias slot). Every
   //      address is re-derived from laundered lane / row indices: the compiler would otherwise keep
   //      the prologue's 64-bit load addresses alive across the whole epoch (VGPR spills)
@@ -1593,6 +1607,7 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     pb.fbase = 0;
   }
   const unsigned gen = __hip_atomic_load(pb.gen + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (role == 0 && !attempt) P32_ESTAMP(0);
   if (role < ng_of(KS))
     owner32<BP, ADAM, EXTRA, KS, RH>(a, pb, p, role, smem_p32, gen);
   else if (RH)
@@ -1601,6 +1616,7 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
     head32<BP, ADAM, EXTRA, KS>(a, pb, p, role - ng_of(KS), smem_p32, gen);
   if (role == 0) {
     __syncthreads();
+    if (!attempt) P32_ESTAMP(3);
     if (threadIdx.x == 0 && __hip_atomic_load(pb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       // owner 0 finished every step: the next launch tags its LL pairs with the next generation (a
       // gang that gave up keeps it; its retry differs by the attempt bit)
