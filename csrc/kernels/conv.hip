@@ -576,10 +576,17 @@ __device__ __forceinline__ void conv_fin_tail(const ConvGemmArgs& a, int peer, i
     const int members = nwg / FIN_SHARDS + (sh < nwg % FIN_SHARDS ? 1 : 0);
     int* sc = cnt + (1 + sh) * FIN_LINE;
     bool last = false;
-    if (__hip_atomic_fetch_add(sc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+    // release: this workgroup's epilogue sums (every wave drained, then the barrier above) are
+    // visible before its ticket; the shard's last arriver acquires its members' and releases them on
+    // with the top ticket; the last workgroup acquires everything before it gathers
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (__hip_atomic_fetch_add(sc, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
       __hip_atomic_store(sc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == min(FIN_SHARDS, nwg) - 1;
-      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == min(FIN_SHARDS, nwg) - 1;
+      if (last) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
     }
     *flag = last ? 1 : 0;
   }
