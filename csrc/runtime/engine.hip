@@ -227,6 +227,15 @@ struct MLPEngine {
   int n_execs = 2;
   unsigned long long launches = 0, launch_ns = 0, launch_max_ns = 0;
   int graph_steps = -1;
+  // gather ahead (prep mode): right after epoch r is launched, the gather of epoch r + 1 (seed given
+  // beforehand with mlp_engine_set_next_epoch_seed) is enqueued on the prep stream into the other
+  // batch buffer. In steady state the GPU does the same as before (the gather runs beside epoch r);
+  // the difference is that it is already enqueued when the host reaches epoch r + 1 — after a host
+  // synchronisation (the bench's clock start) or a late host, the gather is not exposed.
+  bool next_seed_valid = false;
+  unsigned long long next_seed = 0;
+  bool ahead_valid[2] = {false, false};
+  unsigned long long ahead_seed[2] = {0, 0};
   hipStream_t cap_stream = nullptr;  // capture stream when there is no prep stream to capture on
   hipStream_t cs = nullptr;          // the stream the current capture runs on
   // engine-owned device buffers
@@ -423,7 +432,10 @@ struct MLPEngine {
   }
   // Prep mode: the gather into batch buffer i on the prep stream, after the last epoch that read it;
   // it gets its own copy of the control words and the shuffle key (nothing on the main stream).
-  int prep_gather(int i, hipStream_t main) {
+  // ahead: the gather of the NEXT epoch (seed ``seed``), for every peer with data (the next round's
+  // active set is not known yet), ordered after the start of the epoch just launched (which reads
+  // the other buffer; the one that last read buffer i has then finished)
+  int prep_gather(int i, hipStream_t main, unsigned long long seed, bool ahead = false) {
     if (prep_level == 2 && start_rec) {
       CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_start, 0));
     } else if (done_rec[i]) {
@@ -434,8 +446,11 @@ struct MLPEngine {
     }
     CtlUpload u{};
     u.P = a.P;
-    u.seed = seed_host;
-    for (int p = 0; p < a.P; ++p) u.ctl[p] = ctl_host[p];
+    u.seed = seed;
+    for (int p = 0; p < a.P; ++p) {
+      u.ctl[p] = ctl_host[p];
+      if (ahead) u.ctl[p].x = ctl_host[p].y > 0 ? 1 : 0;
+    }
     hipLaunchKernelGGL(k_upload_ctl, dim3(1), dim3(256), 0, prep_stream, u, d_ctl_prep, d_active_prep, d_seed_prep, (PubDst*)nullptr);
     MLPArgs ga = a;
     ga.ctl = d_ctl_prep;
@@ -507,6 +522,7 @@ struct MLPEngine {
   }
 
   void invalidate() {
+    ahead_valid[0] = ahead_valid[1] = false;
     for (auto& x : execs) {
       if (x) hipGraphExecDestroy(x);
       x = nullptr;
@@ -1045,6 +1061,7 @@ int mlp_engine_x_direct(void* h) {
 int mlp_engine_set_counts(void* h, const int* n_host, const int* nt_host) {
   auto* e = (MLPEngine*)h;
   for (int p = 0; p < e->a.P; ++p) {
+    if (e->ctl_host[p].y != n_host[p]) e->ahead_valid[0] = e->ahead_valid[1] = false;
     e->ctl_host[p].y = n_host[p];
     e->ctl_host[p].w = nt_host[p];
   }
@@ -1133,6 +1150,15 @@ int mlp_engine_set_epoch_seed(void* h, unsigned long long seed) {
   return 0;
 }
 
+// Shuffle key of the epoch after the next one launched: that launch then enqueues its gather ahead
+// (prep mode; see MLPEngine::next_seed). The caller passes the same key to set_epoch_seed later.
+int mlp_engine_set_next_epoch_seed(void* h, unsigned long long seed) {
+  auto* e = (MLPEngine*)h;
+  e->next_seed = seed;
+  e->next_seed_valid = true;
+  return 0;
+}
+
 // Persistent-epoch mode: -1 auto (default; MYFYP_MLP_PERSISTENT=0 turns it off), 0 off.
 int mlp_engine_set_persistent(void* h, int mode) {
   auto* e = (MLPEngine*)h;
@@ -1213,7 +1239,9 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
   if (e->graph_persistent) e->pending_zero_acc = e->pending_fresh = false;
   const int buf = e->n_execs > 1 ? (int)(e->launches & 1) : 0;  // the executable launch_graph takes
   if (e->prep_mode) {
-    if (e->prep_gather(buf, s)) return 1;
+    const bool have = e->ahead_valid[buf] && e->ahead_seed[buf] == e->seed_host;
+    e->ahead_valid[buf] = false;
+    if (!have && e->prep_gather(buf, s, e->seed_host)) return 1;
     CHECK_HIP(hipStreamWaitEvent(s, e->ev_gath[buf], 0));
   }
   if (e->graph_persistent) {
@@ -1235,6 +1263,13 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
       CHECK_HIP(hipEventRecord(e->ev_done[buf], s));
       e->done_rec[buf] = true;
     }
+    if (e->prep_mode && e->prep_level == 2 && e->n_execs > 1 && e->next_seed_valid) {
+      const int nb = buf ^ 1;  // the buffer the next launch's executable reads
+      if (e->prep_gather(nb, s, e->next_seed, true)) return 1;
+      e->ahead_valid[nb] = true;
+      e->ahead_seed[nb] = e->next_seed;
+    }
+    e->next_seed_valid = false;
     if (gang_event_always()) {
       CHECK_HIP(hipEventRecord(go.ev, s));
       go.ev_ready = true;

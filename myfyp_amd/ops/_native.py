@@ -79,6 +79,7 @@ _SIGNATURES = {
     "mlp_engine_zero_state": (c_int, [c_void_p, c_void_p]),
     "mlp_engine_set_shuffle": (c_int, [c_void_p, c_int]),
     "mlp_engine_set_epoch_seed": (c_int, [c_void_p, ctypes.c_uint64]),
+    "mlp_engine_set_next_epoch_seed": (c_int, [c_void_p, ctypes.c_uint64]),
     "myfyp_fedavg_stacked_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_fedavg_stacked_apply": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_fedavg_stacked_local": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),

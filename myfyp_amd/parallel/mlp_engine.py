@@ -226,6 +226,7 @@ class MLPGroup:
         # each would contend for the GIL with the round driver)
         self.resolver = Resolver.shared()
         self._cfg_key: Optional[tuple] = None  # last engine configuration pushed to the native side
+        self._seed_ahead: Optional[int] = None  # shuffle key of the next epoch (its gather is already enqueued)
         self._opt_key: Optional[tuple] = None
         self._steps_pe: Optional[np.ndarray] = None
         self._active_cache: Dict[tuple, np.ndarray] = {}
@@ -481,8 +482,14 @@ class MLPGroup:
                 for ep in range(epochs):
                     if self.perm_fn is not None:
                         self.perm.copy_(self.perm_fn(ep))
+                        self._seed_ahead = None
                     else:
-                        _native.check(fast.mlp_engine_set_epoch_seed(self._engine, random.getrandbits(64)), "set_epoch_seed")
+                        # keys are drawn one epoch ahead: the engine enqueues the next epoch's gather
+                        # right after launching this one (same keys, same order as drawing each in turn)
+                        seed = self._seed_ahead if self._seed_ahead is not None else random.getrandbits(64)
+                        self._seed_ahead = random.getrandbits(64)
+                        _native.check(fast.mlp_engine_set_epoch_seed(self._engine, seed), "set_epoch_seed")
+                        _native.check(fast.mlp_engine_set_next_epoch_seed(self._engine, self._seed_ahead), "set_next_epoch_seed")
                     t0 = steps_pe if ep == 1 else (steps_pe * ep).astype(np.int32)
                     if self.eager:
                         _native.check(fast.mlp_engine_run_epoch_eager(self._engine, t0.ctypes.data, stream), "run_epoch")
