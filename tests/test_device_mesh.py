@@ -201,3 +201,22 @@ def test_bench_virtual_mesh_cpu():
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["n_gpus"] == 0 and out["config"]["peers_per_gpu"] == 2
     assert "mesh" in out["config"]["collective"]
+
+
+def test_bench_torchrun_mesh_parks_other_ranks_cpu():
+    """The driver's launch shape (``torch.distributed.run --nproc-per-node 2 bench.py --gpus 2``) with
+    ``--launch mesh --mesh-virtual`` on the CPU: rank 0 drives the two-member mesh, rank 1 parks on
+    the gloo barrier, both exit 0, and exactly one JSON line is printed."""
+    import json
+
+    from _ports import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+           str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch", "mesh", "--mesh-virtual", "--steps", "2", "--warmup", "1",
+           "--n-train", "2000", "--n-test", "400"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["config"]["peers_per_gpu"] == 4 and "mesh" in out["config"]["collective"]
