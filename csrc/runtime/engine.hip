@@ -236,6 +236,32 @@ struct MLPEngine {
   unsigned long long next_seed = 0;
   bool ahead_valid[2] = {false, false};
   unsigned long long ahead_seed[2] = {0, 0};
+  // The prep and evaluation streams are created on a helper thread started with the engine: each
+  // is a new hardware queue (5.5 ms to create, profiles/r5_start), and the data binding and code
+  // object loading of node start run meanwhile. take_stream joins it.
+  std::thread stream_maker;
+  bool making = false;
+  hipStream_t made[2] = {nullptr, nullptr};
+  void make_streams_async() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    making = true;
+    stream_maker = std::thread([this, dev] {
+      if (hipSetDevice(dev) != hipSuccess) return;
+      for (auto& st : made)
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+    });
+  }
+  hipStream_t take_stream(int i) {
+    if (making) {
+      stream_maker.join();
+      making = false;
+    }
+    hipStream_t st = made[i];
+    made[i] = nullptr;
+    if (st == nullptr && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+    return st;
+  }
   hipStream_t cap_stream = nullptr;  // capture stream when there is no prep stream to capture on
   hipStream_t cs = nullptr;          // the stream the current capture runs on
   // engine-owned device buffers
@@ -343,6 +369,9 @@ struct MLPEngine {
   }
 
   ~MLPEngine() {
+    if (making) stream_maker.join();
+    for (auto& st : made)
+      if (st) hipStreamDestroy(st);
     if (prep_stream) {
       hipStreamSynchronize(prep_stream);
       hipStreamDestroy(prep_stream);
@@ -482,7 +511,11 @@ struct MLPEngine {
       // a stream of its own: sharing the prep stream saved 5.5 ms of node start (one hardware
       // queue fewer) but cost 15 % of the round rate (452-456 vs 527-539 rounds/s,
       // profiles/r5_start): the evaluation's wait for the snapshot held the next-epoch gather
-      CHECK_HIP(hipStreamCreateWithFlags(&eval_stream, hipStreamNonBlocking));
+      eval_stream = take_stream(1);
+      if (eval_stream == nullptr) {
+        g_last_error = "evaluation stream creation failed";
+        return 1;
+      }
       eval_stream_owned = true;
       CHECK_HIP(hipEventCreateWithFlags(&ev_snap, hipEventDisableTiming));
       for (auto& es : eside) {
@@ -616,7 +649,11 @@ struct MLPEngine {
 
   int ensure_prep() {
     if (!prep_stream) {
-      CHECK_HIP(hipStreamCreateWithFlags(&prep_stream, hipStreamNonBlocking));
+      prep_stream = take_stream(0);
+      if (prep_stream == nullptr) {
+        g_last_error = "prep stream creation failed";
+        return 1;
+      }
       CHECK_HIP(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
       for (int i = 0; i < 2; ++i) {
         CHECK_HIP(hipEventCreateWithFlags(&ev_gath[i], hipEventDisableTiming));
@@ -915,6 +952,7 @@ void* mlp_engine_create(int P, int D0, int D1, int D2, int D3, int B) {
     return nullptr;
   }
   auto* e = new MLPEngine();
+  e->make_streams_async();
   MLPArgs& a = e->a;
   a.P = P;
   a.D0 = D0; a.D1 = D1; a.D2 = D2; a.D3 = D3;
