@@ -364,12 +364,13 @@ def test_f32_prewarm_is_transparent(dev):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("prep_mode", ["1", "2"])
-def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch, prep_mode):
+@pytest.mark.parametrize("prep_mode,epochs", [("1", 1), ("2", 1), ("2", 2)])
+def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch, prep_mode, epochs):
     """The epoch batch gather on its own stream into alternating batch buffers (mode 1: after the
     last epoch that read the buffer; mode 2: beside the previous epoch, on a capped grid-strided
-    grid) gives bit-identical training to the gather as the first node of the epoch graph: three
-    epochs (both buffers used, one reused) with the in-kernel shuffle of fixed keys."""
+    grid, and enqueued one epoch ahead — within a fit and across fits) gives bit-identical training
+    to the gather as the first node of the epoch graph: three fits (both buffers used, reused) with
+    the in-kernel shuffle of keys from one seeded stream."""
     import random
 
     from myfyp_amd.parallel.mlp_engine import MLPGroup
@@ -381,6 +382,8 @@ def test_f32_prep_stream_gather_matches_in_graph_gather(dev, monkeypatch, prep_m
         monkeypatch.setenv("MYFYP_PREP_GATHER", prep)
         MLPGroup.reset_all()
         learners, refs, g, n = _setup(dev, 3, 64, 1500, 7, spec)
+        for l in learners:
+            l.set_epochs(epochs)
         random.seed(4321)
         for _ in range(3):
             _fit_all(learners)
