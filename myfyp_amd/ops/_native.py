@@ -155,6 +155,15 @@ def load_fast() -> ctypes.PyDLL:
     return _FAST
 
 
+def debug_update_scale() -> float:
+    """Mutation-testing knob (``MYFYP_DEBUG_LR_SCALE``, default 1): the fused engines multiply their
+    learning rate by it, so every update they apply is off by that factor while the torch references
+    the tests compare against are not. Used once to show which tests catch a 5 % update error
+    (``profiles/r5_mutation``); never set in normal runs."""
+    v = os.environ.get("MYFYP_DEBUG_LR_SCALE")
+    return float(v) if v else 1.0
+
+
 _WARM: set = set()
 
 

@@ -1079,7 +1079,8 @@ class CNNGroup:
             spec, epochs = specs[0][0], max(r[1] for r in specs)
             extras_any = [r[2] for r in specs if r[2]]
             opt = {
-                "kind": 0 if spec.get("name", "sgd") == "adam" else 1, "lr": float(spec.get("lr", 0.01)), "momentum": float(spec.get("momentum", 0.0)),
+                "kind": 0 if spec.get("name", "sgd") == "adam" else 1, "lr": float(spec.get("lr", 0.01)) * _native.debug_update_scale(),
+                "momentum": float(spec.get("momentum", 0.0)),
                 "weight_decay": float(spec.get("weight_decay", 0.0)), "nesterov": int(bool(spec.get("nesterov", False))), "mu": 0.0,
             }
             if opt["kind"] == 0:

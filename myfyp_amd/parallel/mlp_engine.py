@@ -395,7 +395,7 @@ class MLPGroup:
         kind = 0 if spec.get("name", "adam") == "adam" else 1
         _native.check(
             lib.mlp_engine_set_optimizer(
-                self._engine, kind, float(spec.get("lr", 1e-3)), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
+                self._engine, kind, float(spec.get("lr", 1e-3)) * _native.debug_update_scale(), float(spec.get("beta1", 0.9)), float(spec.get("beta2", 0.999)),
                 float(spec.get("eps", 1e-8)), float(spec.get("weight_decay", 0.0)), float(spec.get("momentum", 0.0)),
                 int(bool(spec.get("nesterov", False))), mu,
             ),

@@ -350,6 +350,14 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
             # the engine rounds to bf16 at other points than autocast (operands per MFMA tile, fp32
             # epilogues), so its error is of the floor's size but not the same draw
             assert rel < max(0.05, 2.5 * rel16), (name, float(rel), float(cos), rel16)
+            if d_ref.numel() >= 256:
+                # the update's scale along torch's direction: rounding noise is unbiased, so this
+                # stays near 1 even where the deep-net floor is large; a wrong step size does not
+                # (a 5 % learning-rate error was caught here and by nothing else in this file,
+                # profiles/r5_mutation)
+                ratio = float(torch.dot(d_eng.double(), d_ref.double()) / torch.dot(d_ref.double(), d_ref.double()))
+                ratio16 = float(torch.dot(floors[i][name].double(), d_ref.double()) / torch.dot(d_ref.double(), d_ref.double()))
+                assert abs(ratio - 1.0) < max(0.02, 3.0 * abs(ratio16 - 1.0)), (name, ratio, ratio16)
         # BN running statistics follow torch
         for (name, b_ref) in ref.named_buffers():
             if "running" in name:
