@@ -14,51 +14,72 @@ import threading
 from typing import Any, Callable, List, Optional
 
 
-class Pending:
-    """A value produced later on the resolver thread (a tiny future)."""
+_STATE = threading.Lock()  # guards every Pending's state (held for a few instructions at a time)
 
-    __slots__ = ("_ev", "_value", "_exc", "_cbs", "_lock")
+
+class Pending:
+    """A value produced later on the resolver thread (a tiny future).
+
+    Cheap to create: the round driver makes a few dozen per round (one per peer and result, plus
+    ``map`` chains), so there is no per-instance lock or event. State changes happen under one
+    module-wide lock; a thread that blocks in :meth:`result` creates the event it waits on."""
+
+    __slots__ = ("_done", "_value", "_exc", "_cbs", "_ev")
 
     def __init__(self) -> None:
-        self._ev = threading.Event()
+        self._done = False
         self._value: Any = None
         self._exc: Optional[BaseException] = None
-        self._cbs: List[Callable[[Any], None]] = []
-        self._lock = threading.Lock()
+        self._cbs: Optional[List[Callable[[Any], None]]] = None
+        self._ev: Optional[threading.Event] = None
 
     @classmethod
     def completed(cls, value: Any) -> "Pending":
         p = cls()
-        p.set_result(value)
+        p._value = value
+        p._done = True
         return p
 
     def done(self) -> bool:
-        return self._ev.is_set()
+        return self._done
 
     def set_result(self, value: Any) -> None:
-        with self._lock:
+        with _STATE:
             self._value = value
-            self._ev.set()
-            cbs, self._cbs = self._cbs, []
-        for cb in cbs:
+            self._done = True
+            cbs, self._cbs = self._cbs, None
+            ev = self._ev
+        if ev is not None:
+            ev.set()
+        for cb in cbs or ():
             cb(value)
 
     def set_exception(self, exc: BaseException) -> None:
-        with self._lock:
+        with _STATE:
             self._exc = exc
-            self._ev.set()
-            self._cbs = []
+            self._done = True
+            self._cbs = None
+            ev = self._ev
+        if ev is not None:
+            ev.set()
 
     def result(self, timeout: Optional[float] = None) -> Any:
-        if not self._ev.wait(timeout):
-            raise TimeoutError("pending device result not ready")
+        if not self._done:
+            with _STATE:
+                if not self._done and self._ev is None:
+                    self._ev = threading.Event()
+                ev = self._ev
+            if ev is not None and not ev.wait(timeout):
+                raise TimeoutError("pending device result not ready")
         if self._exc is not None:
             raise self._exc
         return self._value
 
     def add_done_callback(self, fn: Callable[[Any], None]) -> None:
-        with self._lock:
-            if not self._ev.is_set():
+        with _STATE:
+            if not self._done:
+                if self._cbs is None:
+                    self._cbs = []
                 self._cbs.append(fn)
                 return
         if self._exc is None:
@@ -75,8 +96,8 @@ class Pending:
         callbacks (metric logging) issued from the round driver: after a device synchronisation
         every result of the queued rounds is already resolved, and running their logging inline
         held the next launch back by 0.7 ms (``profiles/r5_start``)."""
-        with self._lock:
-            if not self._ev.is_set():
+        with _STATE:
+            if not self._done:
                 out = Pending()
 
                 def cb(v: Any) -> None:
@@ -85,6 +106,8 @@ class Pending:
                     except BaseException as e:  # surfaced to whoever waits on the Pending
                         out.set_exception(e)
 
+                if self._cbs is None:
+                    self._cbs = []
                 self._cbs.append(cb)
                 return out
         if self._exc is not None:
