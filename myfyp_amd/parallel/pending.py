@@ -1,7 +1,7 @@
 """Deferred device results: the round's hot path never waits for the GPU.
 
 Fit statistics and evaluation results are copied device→pinned-host asynchronously; a
-:class:`Pending` stands for them until one :class:`Resolver` thread per engine group has waited on
+:class:`Pending` stands for them until the process's :class:`Resolver` thread (shared by every engine group and device) has waited on
 the copy's completion event (``hipEventSynchronize`` releases the GIL) and runs the callbacks
 (metric logging). Results resolve in submission (stream) order, so a blocking ``result()`` on a
 later item implies every earlier one is resolved too.
