@@ -145,3 +145,26 @@ def test_newer_upstream_protobuff_import_paths():
     assert MemoryCommunicationProtocol is InMemoryCommunicationProtocol
     assert GrpcCommunicationProtocol.__name__ == "GrpcCommunicationProtocol"
     assert resolve_protocol({"package": "p2pfl.communication.protocols.protobuff.memory", "protocol": "MemoryCommunicationProtocol"}) is InMemoryCommunicationProtocol
+
+
+def test_yaml_example_with_fyp_model_and_compression():
+    """``examples/configs/mnist_fyp_compressed_memory.yaml``: the FYP model builder with float16 +
+    zlib payloads over the in-memory gossip protocol finishes and learns."""
+    import os
+
+    from myfyp_amd.parallel.federation import Federation
+    from myfyp_amd.runner import run_experiment
+    from myfyp_amd.settings import Settings
+
+    saved = Settings.USE_FUSED_KERNELS
+    try:
+        Federation.reset()
+        cfg = os.path.join(os.path.dirname(__file__), "..", "myfyp_amd", "examples", "configs", "mnist_fyp_compressed_memory.yaml")
+        res = run_experiment(cfg, verbose=False)
+        for h in res["histories"].values():
+            assert h.count("RoundFinishedStage") == 3
+        accs = [m["test_metric"][-1][1] for m in res["global_logs"].values()]
+        assert min(accs) > 0.5, accs
+    finally:
+        Settings.USE_FUSED_KERNELS = saved
+        Federation.reset()
