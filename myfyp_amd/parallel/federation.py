@@ -403,7 +403,18 @@ class Federation:
             torch.cuda.set_device(devs[0])
         inst = cls._instance = cls(0, 1, 0, devs[0], None)
         inst.devices = list(devs)
-        inst.mesh = make_mesh(devs, backend)
+        try:
+            inst.mesh = make_mesh(devs, backend)
+        except Exception as e:  # noqa: BLE001 — RCCL init on this host failed
+            if backend is not None:
+                raise  # an explicitly requested backend must not be swapped silently
+            # the job still runs on every device, with the host mesh's device-to-device copies in
+            # place of RCCL; the choice is logged and reported (``mesh.kind`` = "host")
+            from myfyp_amd.parallel.device_mesh import HostMesh
+
+            logger.warning("rank0", f"RCCL device mesh over {[str(d) for d in devs]} failed ({e}); using the host mesh")
+            print(f"[federation] RCCL device mesh failed ({e}); falling back to the host mesh", file=sys.stderr, flush=True)
+            inst.mesh = HostMesh(devs)
         inst.mesh_members = list(range(len(devs)))
         logger.info("rank0", f"device mesh over {[str(d) for d in devs]} ({inst.mesh.kind})")
         return inst

@@ -220,3 +220,23 @@ def test_bench_torchrun_mesh_parks_other_ranks_cpu():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["config"]["peers_per_gpu"] == 4 and "mesh" in out["config"]["collective"]
+
+
+def test_mesh_falls_back_to_host_when_rccl_init_fails(monkeypatch):
+    """An RCCL mesh that cannot be created (auto backend) leaves a host mesh over the same devices,
+    reported as ``kind == "host"``; an explicitly requested backend still raises."""
+    from myfyp_amd.parallel import device_mesh
+
+    def broken(devs, backend=None):
+        raise MeshError("ncclCommInitAll failed (test)")
+
+    monkeypatch.setattr(device_mesh, "make_mesh", broken)
+    Federation.reset()
+    try:
+        fed = Federation._init_mesh([torch.device("cpu"), torch.device("cpu")], None)
+        assert fed.mesh.kind == "host" and fed.mesh_size == 2
+        Federation.reset()
+        with pytest.raises(MeshError):
+            Federation._init_mesh([torch.device("cpu"), torch.device("cpu")], "rccl")
+    finally:
+        Federation.reset()
