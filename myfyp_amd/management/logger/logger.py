@@ -210,9 +210,6 @@ class P2PFLogger:
             if node not in self._nodes:
                 raise Exception(f"Node {node} not registered.")
             self._nodes.pop(node)
-        from myfyp_amd.utils import gc_tuning
-
-        gc_tuning.experiment_finished(node)  # a node gone mid-experiment no longer holds the freeze
 
     def get_nodes(self) -> Dict[str, Dict[Any, Any]]:
         return self._nodes
@@ -232,19 +229,13 @@ class P2PFLogger:
             h(event, node, experiment)
 
     def experiment_started(self, node: str, experiment: Optional[Experiment]) -> None:
-        from myfyp_amd.utils import gc_tuning
-
         with self._nodes_lock:
             if node in self._nodes:
                 self._nodes[node]["Experiment"] = experiment
-        gc_tuning.experiment_started(node)
         self._fire("experiment_started", node, experiment)
 
     def experiment_finished(self, node: str) -> None:
-        from myfyp_amd.utils import gc_tuning
-
         self._fire("experiment_finished", node, self._nodes.get(node, {}).get("Experiment"))
-        gc_tuning.experiment_finished(node)
 
     def round_started(self, node: str, experiment: Optional[Experiment]) -> None:
         self._fire("round_started", node, experiment)

@@ -59,9 +59,12 @@ class NodeState:
         return self.experiment.exp_name if self.experiment is not None else None
 
     def set_experiment(self, exp_name: str, total_rounds: int, start_round: int = 0) -> None:
+        from myfyp_amd.utils import gc_tuning
+
         self.status = "Learning"
         self.experiment = Experiment(exp_name, total_rounds)
         self.experiment.round = start_round  # > 0 when resuming from a checkpoint
+        gc_tuning.experiment_started(self.addr)  # long-lived objects out of the collector's way
 
     def increase_round(self) -> None:
         if self.experiment is None:
@@ -81,6 +84,9 @@ class NodeState:
 
     def clear(self) -> None:
         """Reset the state (keeps the address, like the reference ``clear``)."""
+        from myfyp_amd.utils import gc_tuning
+
+        gc_tuning.experiment_finished(self.addr)
         # wake anybody blocked on the old primitives before replacing them
         self.votes_event.set()
         self.aggregated_model_event.set()

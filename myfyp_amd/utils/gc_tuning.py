@@ -5,7 +5,8 @@ for the whole run, yet every full (generation-2) collection walks it again: a si
 95 ms on the headline setup, 50 rounds' worth of device work (``bench.py`` prints the pauses).
 With ``Settings.GC_FREEZE`` the objects alive at the start move to the permanent generation
 (``gc.freeze``), so collections during the run only look at what the run itself allocates; the
-experiment's end unfreezes them again.
+experiment's end unfreezes them again. Driven by the node state's experiment lifecycle
+(``NodeState.set_experiment`` / ``clear``), per node: the freeze lasts while any local node runs.
 """
 
 from __future__ import annotations
