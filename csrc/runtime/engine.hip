@@ -608,34 +608,65 @@ struct MLPEngine {
     return 0;
   }
 
-  // One epoch graph: [gather (unless prep mode), epoch kernel + retry launch] or the step chain;
-  // buf selects the batch buffers the epoch reads in prep mode.
-  int capture_one(int steps, int buf, hipGraph_t* out) {
+  // One epoch: [gather (unless prep mode), epoch kernel + retry launch] or the step chain, then the
+  // fit's publish; buf selects the batch buffers the epoch reads in prep mode. Captured into the
+  // epoch graph, or enqueued directly (direct_epoch_launch()).
+  int enqueue_epoch(hipStream_t st, int steps, int buf) {
     const MLPArgs saved = a;
     if (prep_mode) {
       a.Xb16 = xb16_buf[buf];
       a.Yb = yb_buf[buf];
     }
-    CHECK_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
     if (x_direct) {
       MLPArgs ga = a;
       set_flag_zeroing(ga);  // the index kernel zeroes the hand-off flags (no memset node)
-      mlp_launch_index_epoch(ga, cs);
+      mlp_launch_index_epoch(ga, st);
     } else if (!prep_mode) {
       MLPArgs ga = a;  // the bf16 batch copy is only produced for the persistent kernel
       if (!graph_persistent) ga.Xb16 = nullptr;
       if (graph_persistent) set_flag_zeroing(ga);  // ... which also zeroes the hand-off flags (no memset node)
-      mlp_launch_gather_epoch(ga, cs);
+      mlp_launch_gather_epoch(ga, st);
     }
     int rc = 0;
     if (graph_persistent) {
-      rc = launch_epoch_kernel(cs, false);
+      rc = launch_epoch_kernel(st, false);
     } else {
-      for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, cs);
+      for (int s = 0; s < steps; ++s) mlp_launch_train_step(a, s, st);
     }
-    graph_has_pub = graph_publish() && !ring_events() && d_pub != nullptr;
-    if (graph_has_pub) hipLaunchKernelGGL(k_publish_dev, dim3(1), dim3(256), 0, cs, d_loss, d_correct, pb.err, a.P, (const PubDst*)d_pub);
+    if (graph_has_pub) hipLaunchKernelGGL(k_publish_dev, dim3(1), dim3(256), 0, st, d_loss, d_correct, pb.err, a.P, (const PubDst*)d_pub);
     a = saved;
+    return rc;
+  }
+
+  // MYFYP_EPOCH_GRAPH=0: the persistent epoch's launches (epoch, retry, publish) enqueued directly
+  // instead of as a graph launch. In isolation a graph launch costs the device ~6.5 us before its
+  // first kernel and ~2.7 us after its last, a plain kernel boundary ~1.3 us
+  // (scripts/probes/gap_probe.hip, profiles/r5_gap), but on the headline the two measured the same
+  // (534.4 / 534.7 direct vs 534.8 / 530.1 rounds/s, profiles/r5_bnd). Default: the graph.
+  bool direct_epoch_launch() const {
+    static const int v = [] {
+      const char* e = getenv("MYFYP_EPOCH_GRAPH");
+      return e != nullptr ? atoi(e) : 1;
+    }();
+    return v == 0 && graph_persistent;
+  }
+  int launch_epoch(hipStream_t s) {
+    if (!direct_epoch_launch()) return launch_graph(s);
+    const int buf = n_execs > 1 ? (int)(launches & 1) : 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (enqueue_epoch(s, graph_steps, buf)) return 1;
+    CHECK_HIP(hipGetLastError());
+    const unsigned long long ns = (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    ++launches;
+    launch_ns += ns;
+    if (ns > launch_max_ns) launch_max_ns = ns;
+    return 0;
+  }
+
+  int capture_one(int steps, int buf, hipGraph_t* out) {
+    graph_has_pub = graph_publish() && !ring_events() && d_pub != nullptr;
+    CHECK_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+    const int rc = enqueue_epoch(cs, steps, buf);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(cs, &g);
     if (rc || e != hipSuccess) {
@@ -1296,7 +1327,7 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
       CHECK_HIP(hipEventRecord(e->ev_start, s));
       e->start_rec = true;
     }
-    if (e->launch_graph(s)) return 1;
+    if (e->launch_epoch(s)) return 1;
     if (e->prep_mode && e->prep_level == 1) {  // (mode 2 orders its gathers by ev_start)
       CHECK_HIP(hipEventRecord(e->ev_done[buf], s));
       e->done_rec[buf] = true;
@@ -1315,7 +1346,7 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
     go.has_last = true;
     go.last = s;
   } else {
-    if (e->launch_graph(s)) return 1;
+    if (e->launch_epoch(s)) return 1;
   }
   if (pr != nullptr) {
     pr->stream = s;
