@@ -100,6 +100,8 @@ int conv_set_wgrad_halo(int on);
 int conv_set_fwd_halo(int on);  // layer-1 forward / stride-1 dgrad from one staged patch per tile (1, default)  // 64-channel 3x3 wgrads from one staged X patch (1, default) or the generic kernel  // persistent DMA conv: workgroups per launch (0 = auto)  // forward-shaped convs via the LDS-DMA kernel (1, default) or the register stage (0); -1 queries
 int conv_wgrad_launch(const WgradArgs* a, int peers, int splits, void* stream);
 int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int cout, int cin, int R, int S, int peers, void* stream);
+int conv_wt_flip_multi_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int n, const long long* offs, const int* dims, int peers,
+                              void* stream);
 int conv_wt_flip_parity_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int cout, int cin, int R, int S, int pad, int peers,
                                void* stream);
 }

@@ -2074,14 +2074,15 @@ extern "C" int conv_gemm_launch(int mode, const ConvGemmArgs* pa, int peers, voi
 // class order, class c = (ph, pw) as [ci][i'][j'][co] over its tR x tS taps r = r0 + 2 (tR-1-i'),
 // s = s0 + 2 (tS-1-j') (flipped, so the class runs as a forward conv over dY).
 // grid = (ceil(ci / 64) * ceil(co / 64), R * S, peers), block 256.
-__global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ wf, int64_t wf_ps, bf16* __restrict__ wt, int64_t wt_ps, int cout,
-                                                      int cin, int R, int S, int parity_pad) {
+// One 64 x 64 tile (index `tile`) of destination tap `tap` of one peer's weights.
+__device__ __forceinline__ void wt_flip_tile(const bf16* __restrict__ src, bf16* __restrict__ dst0, int cout, int cin, int R, int S, int parity_pad,
+                                             int tile, int tap) {
   // row pad 2: the transposed reads (column of 8 rows per 8-lane group, 8 groups) hit 32 distinct
   // banks; a +8 pad put the groups 32 banks apart (12.4 conflicts per LDS instruction, profiles/r3z_pmc)
-  __shared__ bf16 tile[64][64 + 2];
-  const int peer = blockIdx.z, tap = blockIdx.y;  // destination tap (all classes, in class order)
+  __shared__ bf16 tile_l[64][64 + 2];
+  auto& tl = tile_l;
   const int tci = (cin + 63) / 64;
-  const int ci0 = (blockIdx.x % tci) * 64, co0 = (blockIdx.x / tci) * 64;
+  const int ci0 = (tile % tci) * 64, co0 = (tile / tci) * 64;
   const int RS = R * S;
   int rs_src, taps, dtap, base_taps;  // source tap, taps of the destination block, tap within it, taps before it
   if (parity_pad < 0) {
@@ -2100,8 +2101,7 @@ __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ w
     dtap = t;
     base_taps = tap - t;
   }
-  const bf16* src = wf + peer * wf_ps;
-  bf16* dst = wt + peer * wt_ps + (int64_t)base_taps * cin * cout;
+  bf16* dst = dst0 + (int64_t)base_taps * cin * cout;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {  // 64 co rows x 8 chunks of 8 ci
     const int q = threadIdx.x + 256 * k, row = q >> 3, ch = q & 7;
@@ -2109,7 +2109,7 @@ __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ w
     bf8 v{};
     if (co < cout && ci < cin) v = *reinterpret_cast<const bf8*>(src + ((int64_t)co * RS + rs_src) * cin + ci);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) tile[row][ch * 8 + j] = v.v[j];
+    for (int j = 0; j < 8; ++j) tl[row][ch * 8 + j] = v.v[j];
   }
   __syncthreads();
 #pragma unroll
@@ -2119,9 +2119,33 @@ __global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ w
     if (ci >= cin || co >= cout) continue;
     bf8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v.v[j] = tile[ch * 8 + j][row];
+    for (int j = 0; j < 8; ++j) v.v[j] = tl[ch * 8 + j][row];
     *reinterpret_cast<bf8*>(dst + ((int64_t)ci * taps + dtap) * cout + co) = v;
   }
+}
+
+__global__ __launch_bounds__(256) void k_conv_wt_flip(const bf16* __restrict__ wf, int64_t wf_ps, bf16* __restrict__ wt, int64_t wt_ps, int cout,
+                                                      int cin, int R, int S, int parity_pad) {
+  const int peer = blockIdx.z;
+  wt_flip_tile(wf + peer * wf_ps, wt + peer * wt_ps, cout, cin, R, S, parity_pad, blockIdx.x, blockIdx.y);
+}
+
+// Every MODE-4 layer's flip of a backward pass in ONE launch (instead of one launch before each
+// layer's dgrad): block b of grid.x is tile (b - start[l]) / RS, tap (b - start[l]) % RS of layer l.
+#define WT_FLIP_MAX 32
+struct WtFlipBatch {
+  int n;
+  int start[WT_FLIP_MAX + 1];
+  int64_t off[WT_FLIP_MAX];  // element offset of the layer's weights in both the Wf and the Wt buffer
+  int cout[WT_FLIP_MAX], cin[WT_FLIP_MAX], R[WT_FLIP_MAX], S[WT_FLIP_MAX];
+};
+__global__ __launch_bounds__(256) void k_conv_wt_flip_multi(const bf16* __restrict__ wf, int64_t wf_ps, bf16* __restrict__ wt, int64_t wt_ps,
+                                                            WtFlipBatch fb) {
+  const int b = blockIdx.x, peer = blockIdx.y;
+  int l = 0;
+  while (l + 1 < fb.n && b >= fb.start[l + 1]) ++l;
+  const int local = b - fb.start[l], RS = fb.R[l] * fb.S[l];
+  wt_flip_tile(wf + peer * wf_ps + fb.off[l], wt + peer * wt_ps + fb.off[l], fb.cout[l], fb.cin[l], fb.R[l], fb.S[l], -1, local / RS, local % RS);
 }
 
 extern "C" int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int cout, int cin, int R, int S, int peers, void* stream) {
@@ -2129,6 +2153,29 @@ extern "C" int conv_wt_flip_launch(const void* wf, long long wf_ps, void* wt, lo
   const unsigned tiles = (unsigned)(((cin + 63) / 64) * ((cout + 63) / 64));
   hipLaunchKernelGGL(k_conv_wt_flip, dim3(tiles, (unsigned)(R * S), (unsigned)peers), dim3(256), 0, (hipStream_t)stream, (const bf16*)wf, (int64_t)wf_ps,
                      (bf16*)wt, (int64_t)wt_ps, cout, cin, R, S, -1);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+// n layers: offs[l] element offsets (same in wf and wt), dims[4 l ..] = cout, cin, R, S
+extern "C" int conv_wt_flip_multi_launch(const void* wf, long long wf_ps, void* wt, long long wt_ps, int n, const long long* offs, const int* dims,
+                                         int peers, void* stream) {
+  if (n < 1 || n > WT_FLIP_MAX || peers < 1) return 1;
+  WtFlipBatch fb{};
+  fb.n = n;
+  int blocks = 0;
+  for (int l = 0; l < n; ++l) {
+    const int cout = dims[4 * l], cin = dims[4 * l + 1], R = dims[4 * l + 2], S = dims[4 * l + 3];
+    if ((cout & 7) || (cin & 7) || R < 1 || S < 1) return 1;
+    fb.start[l] = blocks;
+    fb.off[l] = offs[l];
+    fb.cout[l] = cout;
+    fb.cin[l] = cin;
+    fb.R[l] = R;
+    fb.S[l] = S;
+    blocks += ((cin + 63) / 64) * ((cout + 63) / 64) * R * S;
+  }
+  fb.start[n] = blocks;
+  hipLaunchKernelGGL(k_conv_wt_flip_multi, dim3((unsigned)blocks, (unsigned)peers), dim3(256), 0, (hipStream_t)stream, (const bf16*)wf, (int64_t)wf_ps,
+                     (bf16*)wt, (int64_t)wt_ps, fb);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 // MODE 5's parity-class weights (stride-2 dgrad with padding `pad`)

@@ -110,6 +110,7 @@ _SIGS = {
     "conv_bnb_rows": (c_int, []),
     "conv_wgrad_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "conv_wt_flip_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "conv_wt_flip_multi_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "conv_wt_flip_parity_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
@@ -264,14 +265,22 @@ class CNNGroup:
         # BatchNorm finalize (batch statistics -> scale/shift, BN-backward sums -> apply coefficients)
         # run by the last workgroup of the conv that produced the sums (conv.hip conv_fin_tail)
         # instead of a k_bn_finalize / k_bn_bwd_finalize launch per BN. Opt-in (MYFYP_CNN_FUSE_FIN=1):
-        # measured neutral on ResNet-18 (2.536 vs 2.542 rounds/s, profiles/r4u_bn_fin_tail) — the
-        # ~40 launches and their gaps go, but the last workgroup's serial chain (store drain, arrival
-        # ticket, row gather, constants) lengthens every BN-producing conv by 2-12 us
+        # measured neutral on ResNet-18 in round 4 (2.536 vs 2.542 rounds/s, profiles/r4u_bn_fin_tail) —
+        # the ~40 launches and their gaps go, but the last workgroup's serial chain (store drain, arrival
+        # ticket, row gather, constants) lengthens every BN-producing conv by 2-12 us. With the
+        # device-scope release / acquire fences the arrival ticket needs (round 5) it is 17 % slower:
+        # 2.17-2.18 vs 2.62-2.64 rounds/s (profiles/r5_flip)
         self.fuse_fin = os.environ.get("MYFYP_CNN_FUSE_FIN", "0") == "1"
         # wgrad split-K target: workgroups per CU over all peers (more splits = more parallelism and
         # more fp32 atomics on the gradient)
         # stride-1 dgrad as a forward conv over dY with flipped weights (conv.hip MODE 4); 0 = MODE 3
         self.dgrad_fwd = os.environ.get("MYFYP_DGRAD_FWD", "1") != "0"
+        # ResNet backward: every MODE-4 layer's weight flip in one launch at the start of the pass
+        # (conv_wt_flip_multi_launch) instead of one before each dgrad (MYFYP_CNN_FLIP_BATCH=0):
+        # 13 launches fewer per step, round rate the same (2.632 vs 2.630 rounds/s, profiles/r5_flip)
+        self.flip_batch = os.environ.get("MYFYP_CNN_FLIP_BATCH", "1") != "0"
+        self._flipped: frozenset = frozenset()
+        self._flip_tables = None
         self.wgrad_tpc = int(os.environ.get("MYFYP_WGRAD_TPC", "2"))  # measured: 2 -> 75.6 ms wgrad, 4 -> 78.4, 8 -> 89.8 (scripts/probes/wgrad_tpc.sh)
         self.wgrad_tune = os.environ.get("MYFYP_WGRAD_TUNE", "1") != "0"  # per-layer split-K timed on the device (_tune_wgrad)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -602,8 +611,9 @@ class CNNGroup:
             a.ncol, a.ncol_valid = L.cp_in, L.cin
         elif fwd_dgrad:
             wt = self.shadow_t.data_ptr() + 2 * shadow_f
-            _chk(lib.conv_wt_flip_launch(self.shadow.data_ptr() + 2 * shadow_f, self.shadow.shape[1], wt, self.shadow_t.shape[1], L.cp_out, L.cp_in, L.R, L.S,
-                                         P, self._stream()), f"wt flip {L.name}")
+            if L.name not in self._flipped:
+                _chk(lib.conv_wt_flip_launch(self.shadow.data_ptr() + 2 * shadow_f, self.shadow.shape[1], wt, self.shadow_t.shape[1], L.cp_out, L.cp_in, L.R, L.S,
+                                             P, self._stream()), f"wt flip {L.name}")
             a.src, a.src_h, a.src_w, a.src_c = src.data_ptr(), L.ho, L.wo, L.cp_out
             a.out_h, a.out_w = L.h, L.w
             a.wt = wt
@@ -834,7 +844,30 @@ class CNNGroup:
         self._last_act = a
         return logits
 
+    def _flip_all(self, layers) -> None:
+        """One launch flipping the MODE-4 weights of every layer in ``layers`` (``conv`` then skips
+        their per-layer flips until the pass ends)."""
+        if self._flip_tables is None:
+            todo = [L for L in layers if L.stride == 1 and L.colmap is None]
+            offs = (ctypes.c_longlong * len(todo))(*[self.shadow_off[L.name] for L in todo])
+            dims = (c_int * (4 * len(todo)))(*[v for L in todo for v in (L.cp_out, L.cp_in, L.R, L.S)])
+            self._flip_tables = (frozenset(L.name for L in todo), len(todo), offs, dims)
+        names, n, offs, dims = self._flip_tables
+        if n:
+            _chk(_lib().conv_wt_flip_multi_launch(self.shadow.data_ptr(), self.shadow.shape[1], self.shadow_t.data_ptr(), self.shadow_t.shape[1], n, offs,
+                                                  dims, self.capacity, self._stream()), "wt flip (all layers)")
+        self._flipped = names
+
     def _backward_resnet(self, dlogits: torch.Tensor) -> None:
+        batched = self.flip_batch and self.dgrad_fwd and self.shadow_t is not None
+        if batched:
+            self._flip_all([self.fc] + [c for blk in self.blocks for c in (blk[0], blk[2])])
+        try:
+            self._backward_resnet_pass(dlogits)
+        finally:
+            self._flipped = frozenset()
+
+    def _backward_resnet_pass(self, dlogits: torch.Tensor) -> None:
         B, lib = self.B, _lib()
         fc = self.fc
         pooled = self.act("pooled", B, fc.cp_in)
