@@ -83,8 +83,6 @@ using persist::gu32;
 using persist::row_max16;
 using persist::row_min16;
 using persist::row_sum16;
-using persist::st_wt128;
-using persist::st_wt32;
 using namespace f32k;
 
 // A/B switches for timing builds (build variant "stamps+P32_BALANCE=0" etc.): the LDS-resident K
@@ -164,7 +162,10 @@ constexpr int F3_DH2 = NCG * KSMAX;       // head r -> owners: dH2 rows 16r..16r
 constexpr int F3_W2 = F3_DH2 + 4;         // owner cg (K part 0) -> heads: W2 columns 16cg.. after its update
 constexpr int F3_HP = F3_W2 + NCG;        // head r -> heads: partial dW3 / db2 / db3 over its rows
 constexpr int F3_DONE = F3_HP + 4;        // commit flags, one per role
-static_assert(F3_DONE + NCG * KSMAX + 4 <= F32_FPP, "layout-3 flags fit the shared block");
+static_assert(F3_DONE + NCG * KSMAX + 4 <= F32_FPP - 2, "layout-3 flags fit the shared block");
+// two flag lines (64 words) at the end of the block: the roles' XCC reports (persist::gang_same_xcd)
+constexpr int F_XCC = F32_FPP - 2;
+static_assert(F_DONE + NCG * KSMAX + NH <= F_XCC, "layout-1 flags leave the XCC lines free");
 __host__ __device__ constexpr int nhr_of(int BP) { return BP / 16; }  // row heads per peer
 __host__ __device__ constexpr int roles3_of(int KS, int BP) { return NCG * KS + nhr_of(BP); }
 constexpr int HPW = 16 * PD2 + PD2 + 16;  // floats of one head's partial gradients: dW3 [class][o2] | db2 | db3
@@ -478,7 +479,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #if P32_LL_H1
         persist::ll_st1(h1x_part(pb, p, kh, t, BP) + 2 * ((int64_t)b * PD1 + NCG * cg + cc), v, tag);
 #else
-        st_wt32(h1x_part(pb, p, kh, t, BP) + (int64_t)b * PD1 + NCG * cg + cc, v);
+        persist::pub32(pb.plain, h1x_part(pb, p, kh, t, BP) + (int64_t)b * PD1 + NCG * cg + cc, v);
 #endif
       }
     }
@@ -616,7 +617,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         if (kh == 0) {
           float* w2x = pb.dh2x + (int64_t)a.P * 2 * BP * PD2 * 2 + (int64_t)p * PD2 * PD1;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) st_wt32(w2x + (16 * wave + 4 * h + i) * PD1 + NCG * cg + c, w2c[i]);
+          for (int i = 0; i < 4; ++i) persist::pub32(pb.plain, w2x + (16 * wave + 4 * h + i) * PD1 + NCG * cg + c, w2c[i]);
         }
       }
     }
@@ -1031,7 +1032,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32, pl[0], pl[1], tag);
       persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32 + 16, pl[2], pl[3], tag);
 #else
-      st_wt128(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 4, (wave * 64 + lane) * 16, __builtin_bit_cast(u32x4, pl));
+      persist::pub128(pb.plain, pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 4, (wave * 64 + lane) * 16, __builtin_bit_cast(u32x4, pl));
 #endif
     }
     if (hd == 0) P32_STAMP(1, t, 3);
@@ -1137,7 +1138,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 #if P32_LL_DH2
         persist::ll_st1(dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
 #else
-        st_wt32(dst + b * PD2 + 16 * hd + c, v);
+        persist::pub32(pb.plain, dst + b * PD2 + 16 * hd + c, v);
 #endif
       }
     }
@@ -1477,7 +1478,7 @@ __device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         dh2v[i] = h2v[i] > 0.f ? acc[i] : 0.f;
-        st_wt32(dst + (R0 + 4 * g + i) * PD2 + 16 * wave + n, dh2v[i]);
+        persist::pub32(pb.plain, dst + (R0 + 4 * g + i) * PD2 + 16 * wave + n, dh2v[i]);
       }
     }
     persist::publish(pb.flags, FPP, p, F3_DH2 + r, target);
@@ -1491,16 +1492,16 @@ __device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       for (int kb = 0; kb < 4; ++kb) acc = mfma_f32(sH2[(4 * kb + g) * LDH23 + 16 * wave + n], sDlog[(4 * kb + g) * LD16 + n], acc);
       float* hp = hp_t + r * HPW;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st_wt32(hp + n * PD2 + 16 * wave + 4 * g + i, acc[i]);
+      for (int i = 0; i < 4; ++i) persist::pub32(pb.plain, hp + n * PD2 + 16 * wave + 4 * g + i, acc[i]);
       float sb = (dh2v[0] + dh2v[1]) + (dh2v[2] + dh2v[3]);  // db2: rows of this lane, then the 4 lane groups
       sb += __shfl_xor(sb, 16);
       sb += __shfl_xor(sb, 32);
-      if (g == 0) st_wt32(hp + 16 * PD2 + 16 * wave + n, sb);
+      if (g == 0) persist::pub32(pb.plain, hp + 16 * PD2 + 16 * wave + n, sb);
       if (wave == 0) {
         float s3 = (sDlog[(4 * g) * LD16 + n] + sDlog[(4 * g + 1) * LD16 + n]) + (sDlog[(4 * g + 2) * LD16 + n] + sDlog[(4 * g + 3) * LD16 + n]);
         s3 += __shfl_xor(s3, 16);
         s3 += __shfl_xor(s3, 32);
-        if (g == 0) st_wt32(hp + 16 * PD2 + PD2 + n, s3);
+        if (g == 0) persist::pub32(pb.plain, hp + 16 * PD2 + PD2 + n, s3);
       }
     }
     persist::publish(pb.flags, FPP, p, F3_HP + r, target);
@@ -1608,6 +1609,15 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
   }
   const unsigned gen = __hip_atomic_load(pb.gen + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (role == 0 && !attempt) P32_ESTAMP(0);
+  // hand-off payloads stay in the XCD's L2 when the whole gang runs on one XCD (KS = 1: blocks
+  // b = p mod 8 under round-robin dispatch): +4-7 % rounds/s (profiles/r5_plain). 100 us bound.
+  {
+    constexpr int NR = RH ? roles3_of(KS, BP) : roles_of(KS);
+    static_assert(NR <= 2 * persist::FLAG_LINE, "XCC report slots");
+    pb.plain = pb.plain_ok ? persist::gang_same_xcd(persist::flag_at(pb.flags, FPP, p, F_XCC), role, NR, pb.fbase ? 0x200u : 0x100u,
+                                                    reinterpret_cast<int*>(smem_p32), 10000ull)
+                           : 0;
+  }
   if (role < ng_of(KS))
     owner32<BP, ADAM, EXTRA, KS, RH>(a, pb, p, role, smem_p32, gen);
   else if (RH)
@@ -1945,7 +1955,19 @@ hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
   return hipFuncSetAttribute((const void*)mlp_eval_f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds32(a.D0));
 }
 
-hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags) {
+// MYFYP_F32_PLAIN_PUB=0: hand-off payloads always written through (A/B)
+static int f32_plain_env() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_F32_PLAIN_PUB");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb_in, hipStream_t s, bool zero_flags) {
+  MLPPersistF32Bufs pb = pb_in;
+  pb.plain_ok = f32_plain_env() != 0 ? 1 : 0;
+  pb.plain = 0;
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
     if (e != hipSuccess) return e;

@@ -34,6 +34,57 @@ __device__ __forceinline__ void st_wt128(float* base, int bytes, int off, u32x4_
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
+// Hand-off payload stores by gang placement: write-through (sc1) in general; plain when every
+// workgroup of the gang was seen on ONE XCD (the line then stays in that XCD's L2, which is where
+// the consumers' L1-bypassing loads look; sc1 stores drop it, and a same-XCD reader then reads at
+// the cross-XCD rate: MI355X_MICROARCH.md). Placement is checked at run time (gang_same_xcd), never
+// assumed: round-robin dispatch is observed behaviour, not a HIP guarantee.
+__device__ __forceinline__ void pub32(int plain, float* ptr, float v) {
+  if (plain)
+    *ptr = v;
+  else
+    __hip_atomic_store((gu32*)ptr, __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pub128(int plain, float* base, int bytes, int off, u32x4_t v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+  if (plain)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+
+// Gang placement check at kernel entry: role `role` of `nr` (nr <= 64) stores mark | its XCC id into
+// slots[role] (zeroed per launch; `mark` differs per attempt, 0x100 or 0x200), wave 0 polls all nr
+// slots (bounded by `ticks`), and the workgroup learns whether every role reported the same XCC.
+// Any timeout answers false (write-through stays, always correct). `word` is an LDS int.
+__device__ __forceinline__ int gang_same_xcd(unsigned* slots, int role, int nr, unsigned mark, int* word, unsigned long long ticks) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 0xFFu;
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(slots + role), mark | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    int same = 1;
+    unsigned v = mark | xcc;
+    for (;;) {
+      if (lane < nr) v = __hip_atomic_load((gu32*)(slots + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all((v & ~0xFFu) == mark)) break;
+      if (wall_clock64() - t0 > ticks) {
+        same = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (same) same = __all((v & 0xFFu) == xcc) ? 1 : 0;
+    if (lane == 0) *(volatile int*)word = same;
+  }
+  __syncthreads();
+  const int r = *(volatile int*)word;
+  __syncthreads();  // the word may be reused by the caller's LDS carving
+  return r;
+}
+
 __device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
   return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

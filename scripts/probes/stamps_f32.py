@@ -34,7 +34,7 @@ for it in range(2):
     [t.start() for t in ths]
     [t.join() for t in ths]
 torch.cuda.synchronize()
-st = np.zeros((2, 32, 10), dtype=np.uint64)
+st = np.zeros((2, 128, 10), dtype=np.uint64)  # g_p32_stamps[2][128][10]
 assert lib.mlp_debug_persistent_f32_stamps(st.ctypes.data) == 0
 st = st.astype(np.int64)
 print("owner: fwd+reduce | H1 publish | W2 replica | wait dH2 | dH2 load+C1+split | C2 (dW1+Adam+X) | step")
