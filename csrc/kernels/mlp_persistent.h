@@ -34,8 +34,9 @@ struct MLPPersistF32Bufs {
   int* err;         // give-up words: [0,64) per peer first attempt (1 gave up, 2 recovered), [64,128) retry
   unsigned fbase;   // hand-off flag base of the running attempt (set in the kernel)
   float* w2chk;     // debug: owners' W2 replica after the epoch [P][128][256], or null
-  int plain_ok;     // fp32 layouts 1 / 3: hand-off payloads may be stored plain when a gang sits on one XCD (set at launch)
-  int plain;        // ... and this gang does (set in the kernel)
+  int plain_ok;     // fp32 layouts 1 / 3: hand-offs may be stored plain when a gang sits on one XCD (set at launch;
+                    // 1 payloads and flags, 2 payloads only, 0 never)
+  int plain;        // plain_ok if this gang does, else 0 (set in the kernel)
 };
 
 bool mlp_persistent_f32_supported(const MLPArgs& a);

@@ -485,7 +485,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     }
     if (g == 0) P32_STAMP(0, t, 1);
 #if !P32_LL_H1
-    persist::publish(pb.flags, FPP, p, F_H1 + g, pb.fbase + (unsigned)(t + 1));
+    persist::publish_p(pb.flags, FPP, p, F_H1 + g, pb.fbase + (unsigned)(t + 1), pb.plain);
 #endif
     if (g == 0) P32_STAMP(0, t, 2);
 
@@ -622,7 +622,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       }
     }
     if (RH && kh == 0) {
-      persist::publish(pb.flags, FPP, p, F3_W2 + cg, pb.fbase + (unsigned)(t + 2));  // (its barrier is C1's)
+      persist::publish_p(pb.flags, FPP, p, F3_W2 + cg, pb.fbase + (unsigned)(t + 2), pb.plain);  // (its barrier is C1's)
     } else {
       lds_barrier();
     }
@@ -1037,7 +1037,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     }
     if (hd == 0) P32_STAMP(1, t, 3);
 #if !P32_LL_PL
-    persist::publish(pb.flags, FPP, p, F_PL + hd, pb.fbase + (unsigned)(t + 1));
+    persist::publish_p(pb.flags, FPP, p, F_PL + hd, pb.fbase + (unsigned)(t + 1), pb.plain);
     if (!persist::wg_wait(pb.flags, FPP, p, F_PL, NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
 #endif
     if (hd == 0) P32_STAMP(1, t, 4);
@@ -1145,7 +1145,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
 #if P32_LL_DH2
     lds_barrier();  // sDH2 for the off-path updates (the LL stores need no drain or flag)
 #else
-    persist::publish(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1));
+    persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain);
 #endif
     if (hd == 0) P32_STAMP(1, t, 7);
 
@@ -1481,7 +1481,7 @@ __device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         persist::pub32(pb.plain, dst + (R0 + 4 * g + i) * PD2 + 16 * wave + n, dh2v[i]);
       }
     }
-    persist::publish(pb.flags, FPP, p, F3_DH2 + r, target);
+    persist::publish_p(pb.flags, FPP, p, F3_DH2 + r, target, pb.plain);
     if (r == 0) P32_STAMP(1, t, 5);
 
     // ---- off the critical path: partial gradients of W3 / b2 / b3 over these rows -> every head
@@ -1504,7 +1504,7 @@ __device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         if (g == 0) persist::pub32(pb.plain, hp + 16 * PD2 + PD2 + n, s3);
       }
     }
-    persist::publish(pb.flags, FPP, p, F3_HP + r, target);
+    persist::publish_p(pb.flags, FPP, p, F3_HP + r, target, pb.plain);
     if (!persist::wg_wait(pb.flags, FPP, p, F3_HP, NHR, target, pb.err, sOk)) return;
     {
       // every head sums the heads' partials in head order (same bits everywhere) and updates its
@@ -1614,9 +1614,10 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
   {
     constexpr int NR = RH ? roles3_of(KS, BP) : roles_of(KS);
     static_assert(NR <= 2 * persist::FLAG_LINE, "XCC report slots");
-    pb.plain = pb.plain_ok ? persist::gang_same_xcd(persist::flag_at(pb.flags, FPP, p, F_XCC), role, NR, pb.fbase ? 0x200u : 0x100u,
-                                                    reinterpret_cast<int*>(smem_p32), 10000ull)
-                           : 0;
+    pb.plain = pb.plain_ok && persist::gang_same_xcd(persist::flag_at(pb.flags, FPP, p, F_XCC), role, NR, pb.fbase ? 0x200u : 0x100u,
+                                                     reinterpret_cast<int*>(smem_p32), 10000ull)
+                   ? pb.plain_ok
+                   : 0;
   }
   if (role < ng_of(KS))
     owner32<BP, ADAM, EXTRA, KS, RH>(a, pb, p, role, smem_p32, gen);
@@ -1955,7 +1956,8 @@ hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
   return hipFuncSetAttribute((const void*)mlp_eval_f32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds32(a.D0));
 }
 
-// MYFYP_F32_PLAIN_PUB=0: hand-off payloads always written through (A/B)
+// MYFYP_F32_PLAIN_PUB: 1 (default) payloads and flags plain for single-XCD gangs, 2 payloads only,
+// 0 everything written through (A/B)
 static int f32_plain_env() {
   static const int v = [] {
     const char* e = getenv("MYFYP_F32_PLAIN_PUB");
@@ -1966,7 +1968,7 @@ static int f32_plain_env() {
 
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb_in, hipStream_t s, bool zero_flags) {
   MLPPersistF32Bufs pb = pb_in;
-  pb.plain_ok = f32_plain_env() != 0 ? 1 : 0;
+  pb.plain_ok = f32_plain_env();
   pb.plain = 0;
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);

@@ -97,6 +97,22 @@ __device__ __forceinline__ void publish(unsigned* flags, int fpp, int p, int idx
   if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag_at(flags, fpp, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// publish() for a gang found on one XCD (plain != 0): the flag is stored without sc1 as well, so its
+// line stays in that XCD's L2, where the consumers' sc1 polls read it (a workgroup-scope atomic store
+// is a plain store the compiler keeps; the empty asm keeps it ahead of the caller's wait loop)
+__device__ __forceinline__ void publish_p(unsigned* flags, int fpp, int p, int idx, unsigned value, int plain) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (plain == 1) {  // (2: payloads plain, flags written through — A/B)
+      __hip_atomic_store((gu32*)flag_at(flags, fpp, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");
+    } else {
+      __hip_atomic_store((gu32*)flag_at(flags, fpp, p, idx), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Consumer side: wave 0 polls flags idx0..idx0+n-1 (one lane each, relaxed sc1 loads + s_sleep)
 // until all reach `target`, then the workgroup meets; every later load of the handed-off bytes is
 // an sc1 load. Bounded: gives up after `ticks` or when another workgroup gave up.
