@@ -1785,9 +1785,8 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
   }
 }
 
-// K split of a launch: MYFYP_F32_KS=1|2 (tests), else the engine's choice (2 when every active peer
-// sits in the first ppl_of(2) slots: one launch of 40-workgroup gangs does all the work), else 2
-// when P <= ppl_of(2). The occupancy check below may still veto 2.
+// K split of a launch: MYFYP_F32_KS=1|2 (tests), else the engine's choice, else 1. The occupancy
+// check below may still veto 2.
 // Gang layout: MYFYP_F32_VARIANT=1|2 (A/B runs), else the engine's choice (a.f32_variant), else
 // F32_DEFAULT_VARIANT, except for the Adam + FedProx/SCAFFOLD epoch at K split 1: layout 1's
 // instantiation spills VGPRs there (W1's register-resident Adam state plus the per-weight extra
@@ -1823,8 +1822,8 @@ int f32_ks_wanted(const MLPArgs& a) {
     env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }
   if (env) return env;
-  if (a.f32_ks == 1 || a.f32_ks == 2) return a.f32_ks;  // the engine's choice (active peers)
-  return a.P <= ppl_of(2) ? 2 : 1;
+  if (a.f32_ks == 1 || a.f32_ks == 2) return a.f32_ks;  // the engine's choice
+  return 1;  // single-XCD gangs (plain hand-offs) beat K split 2 at every peer count (profiles/r5_ksab)
 }
 
 size_t persistent_f32_lds_ks(const MLPArgs& a, int KS, bool rh = false) {

@@ -23,6 +23,7 @@ fresh optimizer state per ``fit`` (Lightning semantics).
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 import threading
 import time
@@ -297,10 +298,18 @@ class MLPGroup:
             _native.check(
                 lib.mlp_engine_bind_params(eng, _p(self.params), _p(self.shadow), _p(self.w2t), _p(self.m), _p(self.v), self.S), "bind_params"
             )
-        # fp32 owner K split: 2 (40-workgroup gangs, half the owner work per step) when every
-        # attached peer sits in the first 4 slots, i.e. one launch covers them all — the case of
-        # few peers per GPU (a device mesh or one process per GPU, N >= 2 in bench.py); 8 keep 1
-        ks = self.force_f32_ks or (2 if self.handles and max(self.handles) < 4 else 1)
+        # fp32 owner K split: 1 (24-workgroup gangs). Each gang then runs on ONE XCD and keeps its
+        # hand-offs in that XCD's L2 (csrc/kernels/persist_common.h gang_same_xcd), which beats
+        # K split 2's halved owner work on 40-workgroup gangs that must span two XCDs: 601-607 vs
+        # 570-578 rounds/s at 4 / 2 / 1 peers per GPU (profiles/r5_ksab). With the hand-offs forced
+        # write-through (MYFYP_F32_PLAIN_PUB=0) the old choice: 2 when every peer sits in the first
+        # 4 slots (one launch covers them all)
+        if self.force_f32_ks:
+            ks = self.force_f32_ks
+        elif os.environ.get("MYFYP_F32_PLAIN_PUB", "1") == "0":
+            ks = 2 if self.handles and max(self.handles) < 4 else 1
+        else:
+            ks = 1
         # a forced K split of 2 is a layout-1 configuration
         var = self.force_f32_variant or (1 if self.force_f32_ks == 2 else 0)
         # weight collectives on the comm stream may hold CUs while an epoch runs: size the
