@@ -477,7 +477,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         const float v = b < rows ? (KS == 1 ? fmaxf(s[i], 0.f) : s[i]) : 0.f;
         sH1c[b * 16 + cc] = v;
 #if P32_LL_H1
-        persist::ll_st1(h1x_part(pb, p, kh, t, BP) + 2 * ((int64_t)b * PD1 + NCG * cg + cc), v, tag);
+        persist::ll_st1p(pb.plain, h1x_part(pb, p, kh, t, BP) + 2 * ((int64_t)b * PD1 + NCG * cg + cc), v, tag);
 #else
         persist::pub32(pb.plain, h1x_part(pb, p, kh, t, BP) + (int64_t)b * PD1 + NCG * cg + cc, v);
 #endif
@@ -1029,8 +1029,8 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       // plx[p][hd][wave][lane] = 4 partial logits (rows 16·wave + 4h + i, class c) as two LL pair
       // chunks: the consuming lane of every head has the same (wave, h, c) and reads its four rows
 #if P32_LL_PL
-      persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32, pl[0], pl[1], tag);
-      persist::ll_st2(pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32 + 16, pl[2], pl[3], tag);
+      persist::ll_st2p(pb.plain, pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32, pl[0], pl[1], tag);
+      persist::ll_st2p(pb.plain, pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 8, (wave * 64 + lane) * 32 + 16, pl[2], pl[3], tag);
 #else
       persist::pub128(pb.plain, pb.plx + ((int64_t)p * NH + hd) * BP * 16 * 2, BP * 16 * 4, (wave * 64 + lane) * 16, __builtin_bit_cast(u32x4, pl));
 #endif
@@ -1136,7 +1136,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         const float v = sH2[b * LD16 + c] > 0.f ? acc[i] : 0.f;
         sDH2[b * LD16 + c] = v;
 #if P32_LL_DH2
-        persist::ll_st1(dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
+        persist::ll_st1p(pb.plain, dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
 #else
         persist::pub32(pb.plain, dst + b * PD2 + 16 * hd + c, v);
 #endif

@@ -54,8 +54,6 @@ using persist::al16;
 using persist::row_max16;
 using persist::row_min16;
 using persist::row_sum16;
-using persist::st_wt128;
-using persist::st_wt32;
 
 constexpr int NG = 16;  // owners per peer = the gang
 constexpr int PPL = 8;  // peers per launch (8 x 16 workgroups)
@@ -368,14 +366,14 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
         acc = mfma_f32(av.y, w2f[1], acc);
         acc = mfma_f32(av.z, w2f[2], acc);
         acc = mfma_f32(av.w, w2f[3], acc);
-        st_wt128(dst, BP * PD2 * 4, ((mt * 8 + wave) * 64 + lane) * 16, __builtin_bit_cast(u32x4, acc));
+        persist::pub128(pb.plain, dst, BP * PD2 * 4, ((mt * 8 + wave) * 64 + lane) * 16, __builtin_bit_cast(u32x4, acc));
       }
       if (tid < 32) {  // this owner's W3 columns (current weights) for every reducer's logits
         float* w3d = xbase + XL.w3s + (((int64_t)p * 2 + par) * NG + g) * 128;
-        st_wt128(w3d, 128 * 4, tid * 16, __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(sW3s + 4 * tid)));
+        persist::pub128(pb.plain, w3d, 128 * 4, tid * 16, __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(sW3s + 4 * tid)));
       }
     }
-    persist::publish(pb.flags, F32_FPP, p, F1 + g, target);
+    persist::publish_p(pb.flags, F32_FPP, p, F1 + g, target, pb.plain);
     V2_STAMP(t, 2);
 
     // next step's batch: pull this wave's columns into the XCD's L2 (staged during C2)
@@ -468,7 +466,7 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
         float acc = 0.f;
         for (int k = 0; k < D3; ++k) acc = fmaf(sDl[i * 16 + k], sW3[k * W3LD + o2], acc);
         const float hv = sH2r[i * PD2 + o2];
-        st_wt32(xbase + XL.dh2r + (rbase + R0 + i) * PD2 + o2, hv > 0.f ? acc : 0.f);
+        persist::pub32(pb.plain, xbase + XL.dh2r + (rbase + R0 + i) * PD2 + o2, hv > 0.f ? acc : 0.f);
       }
       // dW3ᵀ partial over the reducer rows: one MFMA per wave, A = dlogᵀ[class = c][row = h],
       // B = H2[row = h][o2 = 16w + c] -> C[class 4h + i][o2 16w + c], stored [o2][class]
@@ -476,15 +474,15 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
       const float av = h < RPO ? sDl[h * 16 + c] : 0.f;
       const float bv = h < RPO ? sH2r[h * PD2 + 16 * wave + c] : 0.f;
       const f32x4 pw = mfma_f32(av, bv, zero4());
-      st_wt128(dst, DW3P * 4, ((16 * wave + c) * 16 + 4 * h) * 4, __builtin_bit_cast(u32x4, pw));
+      persist::pub128(pb.plain, dst, DW3P * 4, ((16 * wave + c) * 16 + 4 * h) * 4, __builtin_bit_cast(u32x4, pw));
       if (tv < 16) {  // db3 partial: Σ over the reducer rows of dlogits
         float d = 0.f;
 #pragma unroll
         for (int r = 0; r < RPO; ++r) d += sDl[r * 16 + tv];
-        st_wt32(dst + PD2 * 16 + tv, d);
+        persist::pub32(pb.plain, dst + PD2 * 16 + tv, d);
       }
     }
-    persist::publish(pb.flags, F32_FPP, p, F2 + g, target);
+    persist::publish_p(pb.flags, F32_FPP, p, F2 + g, target, pb.plain);
     V2_STAMP(t, 4);
 
     // ================= C: backward of this slice
@@ -682,8 +680,8 @@ __device__ void owner_v2(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, i
   {
     const float l = wave_sum(loss_acc), cr = wave_sum(correct_acc);
     if (wave < (RPO < 2 ? 2 : RPO) && lane == 0) {  // waves >= RPO store zeros (whole float4 slots)
-      st_wt32(xbase + XL.lossp + ((int64_t)p * NG + g) * 8 + 2 * wave, l);
-      st_wt32(xbase + XL.lossp + ((int64_t)p * NG + g) * 8 + 2 * wave + 1, cr);
+      persist::pub32(pb.plain, xbase + XL.lossp + ((int64_t)p * NG + g) * 8 + 2 * wave, l);
+      persist::pub32(pb.plain, xbase + XL.lossp + ((int64_t)p * NG + g) * 8 + 2 * wave + 1, cr);
     }
   }
   if (!gang_commit_v2(a, pb, p, g, sOk)) return;
@@ -794,6 +792,13 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32v2_epoch(MLPArgs a, MLPP
     pb.err = err_first;
     pb.fbase = 0;
   }
+  // single-XCD gang (blocks b = p mod 8): hand-offs kept in that XCD's L2 (persist::gang_same_xcd,
+  // mlp_persistent_f32.hip); the last two lines of the shared flag block hold the XCC reports
+  static_assert(FDONE + NG <= F32_FPP - 2, "v2 flags leave the XCC lines free");
+  pb.plain = pb.plain_ok && persist::gang_same_xcd(persist::flag_at(pb.flags, F32_FPP, p, F32_FPP - 2), g, NG, pb.fbase ? 0x200u : 0x100u,
+                                                   reinterpret_cast<int*>(smem_v2), 10000ull)
+                 ? pb.plain_ok
+                 : 0;
   owner_v2<BP, ADAM, EXTRA>(a, pb, p, g, smem_v2);
   if (g == 0) {
     __syncthreads();

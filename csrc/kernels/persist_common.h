@@ -164,6 +164,23 @@ __device__ __forceinline__ void ll_st2(float* base, int bytes, int off, float v0
 __device__ __forceinline__ void ll_st1(float* pair, float v, unsigned tag) {
   st_wt(pair, ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, v));
 }
+// LL stores for a gang found on one XCD (plain: the pair stays in that XCD's L2; one 8- or 16-byte
+// store instruction each, as for the write-through form)
+__device__ __forceinline__ void ll_st1p(int plain, float* pair, float v, unsigned tag) {
+  const unsigned long long w = ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, v);
+  if (plain)
+    __hip_atomic_store((gu64*)pair, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    st_wt(pair, w);
+}
+__device__ __forceinline__ void ll_st2p(int plain, float* base, int bytes, int off, float v0, float v1, unsigned tag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+  const ll_u32x4 v = {__builtin_bit_cast(unsigned, v0), tag, __builtin_bit_cast(unsigned, v1), tag};
+  if (plain)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
 // 16-byte L1-bypassing load of two LL pairs
 __device__ __forceinline__ ll_u32x4 ll_ld2(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16); }
 __device__ __forceinline__ bool ll_ok2(const ll_u32x4& v, unsigned tag) { return v[1] == tag && v[3] == tag; }
