@@ -7,9 +7,11 @@ struct MLPPersistBufs {
   bf16* h1x;        // [P][Bpad][256]   owner g -> head: H1 columns 16g..16g+15
   bf16* w2x;        // [P][8][8][64][8]  owner g -> head: updated bf16 W2 in the head's B-fragment order
   bf16* dh2x;       // [P][Bpad][128]   head -> owners: dH2
-  unsigned* flags;  // [P][33][32] one 128-B line per flag (16 H1, 16 W2, 1 dH2); zeroed per launch
+  unsigned* flags;  // [P][35][32] one 128-B line per flag (16 H1, 16 W2, 1 dH2, 2 XCC reports); zeroed per launch
   size_t flag_bytes;
   int* err;         // sticky give-up word (bounded spins); zeroed per fit
+  int plain_ok;     // hand-offs may be stored plain when a gang sits on one XCD (set at launch)
+  int plain;        // ... and this gang does (set in the kernel)
 };
 
 // Shape / resource check for the persistent path (device-independent part).

@@ -65,7 +65,8 @@ constexpr int NT = 512;  // threads per workgroup (8 waves)
 constexpr int NG = 16;   // owners per peer (D1 / 16)
 constexpr int PD1 = 256, PD2 = 128;
 constexpr int ROLES = NG + 1;
-constexpr int FLAGS_PER_PEER = 2 * NG + 1;
+constexpr int FLAGS_PER_PEER = 2 * NG + 3;
+constexpr int F_XCC = 2 * NG + 1;  // two lines: the roles' XCC reports (persist::gang_same_xcd)
 constexpr int F_H1 = 0, F_W2 = NG, F_DH2 = 2 * NG;
 constexpr int KS1_MAX = 32;                              // D0 <= 1024
 constexpr int LD2 = PD2 + 8;                             // bf16 row stride of [*][128] LDS tiles
@@ -85,8 +86,16 @@ __device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-__device__ __forceinline__ void publish(unsigned* flags, int p, int idx, unsigned value) {
-  persist::publish(flags, FLAGS_PER_PEER, p, idx, value);
+__device__ __forceinline__ void publish(unsigned* flags, int p, int idx, unsigned value, int plain) {
+  persist::publish_p(flags, FLAGS_PER_PEER, p, idx, value, plain);
+}
+// 8-byte hand-off payload store: plain in a single-XCD gang (the line stays in that XCD's L2),
+// write-through otherwise (persist::pub32, mlp_persistent_f32.hip)
+__device__ __forceinline__ void pub64(int plain, void* ptr, unsigned long long v) {
+  if (plain)
+    __hip_atomic_store((persist::gu64*)ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    persist::st_wt(ptr, v);
 }
 __device__ __forceinline__ bool wg_wait(unsigned* flags, int p, int idx0, int n, unsigned target, int* err, int* sOk) {
   return persist::wg_wait(flags, FLAGS_PER_PEER, p, idx0, n, target, err, sOk);
@@ -273,7 +282,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     const int o2 = tv >> 2, part = tv & 3, half = part >> 1, sub = part & 1;
     const int lane_h = 2 * (g & 1) + half;
     const int64_t chunk = (((int64_t)p * 8 + (o2 >> 4)) * (PD1 / 32) + (g >> 1)) * 64 + lane_h * 16 + (o2 & 15);
-    st_wt(pb.w2x + chunk * 8 + 4 * sub, *reinterpret_cast<const unsigned long long*>(sW2g + o2 * 16 + 4 * part));
+    pub64(pb.plain, pb.w2x + chunk * 8 + 4 * sub, *reinterpret_cast<const unsigned long long*>(sW2g + o2 * 16 + 4 * part));
   };
   // ---- initial W2 publish (version 1)
   auto publish_w2 = [&](unsigned version) {
@@ -281,7 +290,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     for (int j = 0; j < 4; ++j) sW2g[(16 * wave + 4 * h + j) * 16 + c] = (bf16)w2[j];
     __syncthreads();
     w2_store(tid);
-    publish(pb.flags, p, F_W2 + g, version);
+    publish(pb.flags, p, F_W2 + g, version, pb.plain);
   };
   publish_w2(1u);
 
@@ -337,9 +346,9 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     lds_barrier();
     if (tid < BP * 4) {
       const int b = tv >> 2, part = tv & 3;
-      st_wt(pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + 4 * part, *reinterpret_cast<const unsigned long long*>(sH1 + b * 16 + 4 * part));
+      pub64(pb.plain, pb.h1x + ((int64_t)p * BP + b) * PD1 + NG * g + 4 * part, *reinterpret_cast<const unsigned long long*>(sH1 + b * 16 + 4 * part));
     }
-    publish(pb.flags, p, F_H1 + g, (unsigned)(t + 1));
+    publish(pb.flags, p, F_H1 + g, (unsigned)(t + 1), pb.plain);
     if (g == 0) PE_STAMP(0, t, 1);
 
     // next step's batch: pull this wave's columns into the XCD's L2 while the head works (the
@@ -461,7 +470,7 @@ __device__ void owner(const MLPArgs& a, const MLPPersistBufs& pb, int p, int g, 
     if (g == 0) PE_STAMP(0, t, 4);
     // updated W2 slice to the head (write-through) and the next batch into LDS; one drain + flag
     w2_store(tv);
-    publish(pb.flags, p, F_W2 + g, (unsigned)(t + 2));
+    publish(pb.flags, p, F_W2 + g, (unsigned)(t + 2), pb.plain);
     if (g == 0) PE_STAMP(0, t, 5);
   }
 
@@ -678,9 +687,9 @@ __device__ void head(const MLPArgs& a, const MLPPersistBufs& pb, int p, char* sm
     for (int k = 0; k < BP / 16; ++k) {  // row-wise 8-byte chunks: whole 256-byte rows per wave
       const int e = tv + NT * k;
       const int b = e >> 5, q = e & 31;
-      st_wt(pb.dh2x + ((int64_t)p * BP + b) * PD2 + 4 * q, *reinterpret_cast<const unsigned long long*>(sDH2 + b * LD2 + 4 * q));
+      pub64(pb.plain, pb.dh2x + ((int64_t)p * BP + b) * PD2 + 4 * q, *reinterpret_cast<const unsigned long long*>(sDH2 + b * LD2 + 4 * q));
     }
-    publish(pb.flags, p, F_DH2, (unsigned)(t + 1));
+    publish(pb.flags, p, F_DH2, (unsigned)(t + 1), pb.plain);
     PE_STAMP(1, t, 5);
 
     // ---- off the critical path: dW3 (waves 0..3), db2 (waves 4,5), db3 (wave 6)
@@ -760,6 +769,9 @@ __global__ __launch_bounds__(NT) void mlp_persistent_epoch(MLPArgs a, MLPPersist
   if (p >= a.P) return;
   const int4 ctl = a.ctl[p];
   if (!ctl.x || ctl.y <= 0) return;
+  // a peer's blocks share b & 7: one XCD under round-robin dispatch, checked here (speed only)
+  pb.plain = pb.plain_ok && persist::gang_same_xcd(persist::flag_at(pb.flags, FLAGS_PER_PEER, p, F_XCC), role, ROLES, 0x100u,
+                                                   reinterpret_cast<int*>(smem_pe), 10000ull);
   if (role < NG)
     owner<BP, ADAM>(a, pb, p, role, smem_pe);
   else
@@ -799,7 +811,14 @@ hipError_t mlp_persistent_prepare(const MLPArgs& a) {
   return a.Bpad == 64 ? prepare_one<64, false>(lds) : prepare_one<32, false>(lds);
 }
 
-hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb, hipStream_t s, bool zero_flags) {
+hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb_in, hipStream_t s, bool zero_flags) {
+  MLPPersistBufs pb = pb_in;
+  static const int plain_env = [] {  // MYFYP_F32_PLAIN_PUB=0: write-through hand-offs (A/B), as the fp32 kernel
+    const char* e = getenv("MYFYP_F32_PLAIN_PUB");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  pb.plain_ok = plain_env != 0 ? 1 : 0;
+  pb.plain = 0;
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);
     if (e != hipSuccess) return e;
