@@ -41,6 +41,7 @@ struct MLPPersistF32Bufs {
   int plain;        // plain_ok if this gang does, else 0 (set in the kernel)
 };
 
+int mlp_plain_pub_mode();  // single-XCD hand-off mode of the persistent kernels (MYFYP_F32_PLAIN_PUB / mlp_set_plain_pub)
 bool mlp_persistent_f32_supported(const MLPArgs& a);
 size_t mlp_persistent_f32_h1x_floats(int P, int Bpad);  // H1-partial exchange region at the start of the buffer
 size_t mlp_persistent_f32_bytes(int P, int Bpad);

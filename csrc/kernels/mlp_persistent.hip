@@ -813,11 +813,7 @@ hipError_t mlp_persistent_prepare(const MLPArgs& a) {
 
 hipError_t mlp_launch_persistent_epoch(const MLPArgs& a, const MLPPersistBufs& pb_in, hipStream_t s, bool zero_flags) {
   MLPPersistBufs pb = pb_in;
-  static const int plain_env = [] {  // MYFYP_F32_PLAIN_PUB=0: write-through hand-offs (A/B), as the fp32 kernel
-    const char* e = getenv("MYFYP_F32_PLAIN_PUB");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  pb.plain_ok = plain_env != 0 ? 1 : 0;
+  pb.plain_ok = mlp_plain_pub_mode() != 0 ? 1 : 0;  // as the fp32 kernels (MYFYP_F32_PLAIN_PUB)
   pb.plain = 0;
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);

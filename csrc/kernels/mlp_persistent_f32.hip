@@ -33,6 +33,8 @@
 // owners (8 × 4 KB, double-buffered by step parity because the owners re-read the previous step's
 // tile for their deferred W2-replica update) — the last two as LL (value, tag) pairs: no producer
 // drain, workgroup meet or flag store, the consumer's data load is its readiness check.
+#include <atomic>
+
 #include "mlp_persistent.h"
 #include "persist_common.h"
 #include "mlp_f32_common.h"
@@ -75,6 +77,10 @@ extern "C" int mlp_debug_persistent_f32_epoch_stamps(void* out) {
   do {                \
   } while (0)
 #endif
+
+// What each peer's gang decided in the last fp32 layout-1/3 epoch on this device (its pb.plain;
+// role 0 stores it after the placement check). Read with mlp_debug_plain_seen (tests).
+__device__ int g_plain_seen[64];
 
 namespace {
 
@@ -1618,6 +1624,7 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
                                                      reinterpret_cast<int*>(smem_p32), 10000ull)
                    ? pb.plain_ok
                    : 0;
+    if (role == 0 && threadIdx.x == 0 && p < 64) g_plain_seen[p] = pb.plain;
   }
   if (role < ng_of(KS))
     owner32<BP, ADAM, EXTRA, KS, RH>(a, pb, p, role, smem_p32, gen);
@@ -1956,18 +1963,25 @@ hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
 }
 
 // MYFYP_F32_PLAIN_PUB: 1 (default) payloads and flags plain for single-XCD gangs, 2 payloads only,
-// 0 everything written through (A/B)
-static int f32_plain_env() {
+// 0 everything written through (A/B); mlp_set_plain_pub overrides it (tests)
+static std::atomic<int> g_plain_override{-1};
+int mlp_plain_pub_mode() {
+  const int o = g_plain_override.load(std::memory_order_relaxed);
+  if (o >= 0) return o;
   static const int v = [] {
     const char* e = getenv("MYFYP_F32_PLAIN_PUB");
     return e != nullptr ? atoi(e) : 1;
   }();
   return v;
 }
+extern "C" int mlp_set_plain_pub(int mode) { return g_plain_override.exchange(mode < 0 ? -1 : mode); }
+extern "C" int mlp_debug_plain_seen(int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plain_seen), sizeof(g_plain_seen)) == hipSuccess ? 0 : 1;
+}
 
 hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb_in, hipStream_t s, bool zero_flags) {
   MLPPersistF32Bufs pb = pb_in;
-  pb.plain_ok = f32_plain_env();
+  pb.plain_ok = mlp_plain_pub_mode();
   pb.plain = 0;
   if (zero_flags) {
     hipError_t e = hipMemsetAsync(pb.flags, 0, pb.flag_bytes, s);

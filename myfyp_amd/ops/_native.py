@@ -101,6 +101,8 @@ _SIGNATURES = {
     "mlp_engine_debug_giveup": (c_int, [c_void_p, c_int, c_int]),
     "mlp_engine_prepare": (c_int, [c_void_p, c_void_p]),
     "myfyp_warm_all": (c_int, [c_int]),
+    "mlp_set_plain_pub": (c_int, [c_int]),  # single-XCD hand-off mode override (-1: MYFYP_F32_PLAIN_PUB)
+    "mlp_debug_plain_seen": (c_int, [c_void_p]),
     "mlp_debug_stamps": (c_int, [c_void_p]),  # only in the -DMLP_STAMPS diagnostics build
     "mlp_debug_persistent_f32_stamps": (c_int, [c_void_p]),  # likewise
 }

@@ -426,3 +426,35 @@ def test_scaffold_control_variate_matches_formula(dev):
             assert rel < 1e-4, (rnd, rel)
             assert torch.allclose(cb.delta_y.double().cpu(), y - x0, rtol=0, atol=1e-6)
             assert ((cb.delta_c.double().cpu() - (want - ci_old)).norm() / (want - ci_old).norm()).item() < 1e-4
+
+
+@pytest.mark.parametrize("peers", [2, 8])
+def test_f32_single_xcd_handoffs_bit_identical(dev, peers):
+    """Single-XCD gangs keep their hand-offs in L2 (plain stores, persist::gang_same_xcd): the same
+    fit with write-through hand-offs gives bit-identical parameters, and on MI355X every K-split-1
+    gang (blocks b = p mod 8) is found on one XCD, so the fast path is the one exercised."""
+    import ctypes
+
+    from myfyp_amd.ops import _native
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+
+    lib = _native.load(required=True)
+    spec = {"name": "adam", "lr": 1e-3}
+    out = {}
+    try:
+        for mode in (1, 0):
+            lib.mlp_set_plain_pub(mode)
+            MLPGroup.reset_all()
+            learners, refs, g, n = _setup(dev, peers, 64, 600 * peers, 11, spec)
+            assert g.f32_ks() == 1
+            _pin_perms(dev, g, learners, n)
+            _fit_all(learners)
+            seen = (ctypes.c_int * 64)()
+            assert lib.mlp_debug_plain_seen(seen) == 0
+            out[mode] = ([l.flat_params().detach().clone() for l in learners], list(seen)[:peers])
+    finally:
+        lib.mlp_set_plain_pub(-1)
+    assert out[0][1] == [0] * peers
+    assert out[1][1] == [1] * peers, f"gangs not all on one XCD: {out[1][1]}"
+    for a, b in zip(out[1][0], out[0][0]):
+        assert torch.equal(a, b)
