@@ -638,15 +638,16 @@ struct MLPEngine {
     return rc;
   }
 
-  // MYFYP_EPOCH_GRAPH=0: the persistent epoch's launches (epoch, retry, publish) enqueued directly
-  // instead of as a graph launch. In isolation a graph launch costs the device ~6.5 us before its
+  // The persistent epoch's launches (epoch, retry, publish) are enqueued directly instead of as a
+  // graph launch (MYFYP_EPOCH_GRAPH=1: the graph). A graph launch costs the device ~6.5 us before its
   // first kernel and ~2.7 us after its last, a plain kernel boundary ~1.3 us
-  // (scripts/probes/gap_probe.hip, profiles/r5_gap), but on the headline the two measured the same
-  // (534.4 / 534.7 direct vs 534.8 / 530.1 rounds/s, profiles/r5_bnd). Default: the graph.
+  // (scripts/probes/gap_probe.hip, profiles/r5_gap): +0.4 % rounds/s, 4 of 4 alternations
+  // (602.8 vs 600.6 mean, profiles/r5_direct); the host, rounds ahead, absorbs the two extra launch
+  // calls. The graphs are still captured (the step-chain path and MYFYP_EPOCH_GRAPH=1 use them).
   bool direct_epoch_launch() const {
     static const int v = [] {
       const char* e = getenv("MYFYP_EPOCH_GRAPH");
-      return e != nullptr ? atoi(e) : 1;
+      return e != nullptr ? atoi(e) : 0;
     }();
     return v == 0 && graph_persistent;
   }

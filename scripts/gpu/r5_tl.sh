@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: current headline round boundary (kernel-trace timeline of the main stream)
 set -o pipefail
-O=gpurun_out/r5_tl; mkdir -p $O
+O=gpurun_out/${TL_OUT:-r5_tl}; mkdir -p $O
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run -- python bench.py --steps 40 --warmup 5 > $O/tl.log 2>&1
