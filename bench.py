@@ -89,6 +89,7 @@ def main() -> None:
     from myfyp_amd.learning.dataset.synthetic import synthetic_mnist
     from myfyp_amd.learning.frameworks.torch import TorchModel
     from myfyp_amd.management.logger import logger
+    from myfyp_amd.management.tracing import mark
     from myfyp_amd.models import MLP
     from myfyp_amd.node import Node
     from myfyp_amd.parallel.federation import Federation
@@ -162,6 +163,7 @@ def main() -> None:
             f.barrier()
             dev_sync()
             marks["t0"] = time.perf_counter()
+            mark("bench:t0")  # roctx (MYFYP_ROCTX=1): the timed window's start on a kernel trace
 
     def hook(r: int, f) -> None:
         round_end[r] = time.perf_counter()
@@ -169,6 +171,7 @@ def main() -> None:
             dev_sync()
             f.barrier()
             marks["t1"] = time.perf_counter()
+            mark("bench:t1")
 
     fed.round_start_hooks.append(start_hook)
     fed.round_hooks.append(hook)

@@ -134,22 +134,23 @@ class RoundDriver:
             round_ = next(iter(states.values())).round
             train_set = list(next(iter(states.values())).train_set)
             trainers = [a for a in cur if a in train_set]
-            # ---- TrainStage / WaitAggregatedModelsStage: one fused round for every local peer
-            snaps, reqs, n = {}, {}, {}
-            for a, m in cur.items():
-                history(m, "TrainStage" if a in trainers else "WaitAggregatedModelsStage")
-                snaps[a] = logger.experiment_snapshot(a)
-                if a in trainers:
-                    m.kw["aggregator"].set_nodes_to_aggregate(train_set)
-                    lr = m.kw["learner"]
-                    reqs[a] = lr.fit_request()
-                    n[a] = lr.num_train_samples()
+            # ---- TrainStage / WaitAggregatedModelsStage: one fused round for every local peer. The
+            # launches go first, the per-peer bookkeeping after them: when the GPU is idle (the first
+            # round, or after a host synchronisation) it waits for nothing else
+            reqs = {a: cur[a].kw["learner"].fit_request() for a in trainers}
             out: Dict[str, Any] = {}
             mark("driver:launch")
             if trainers:
                 has_test = {a for a in trainers if (d := cur[a].kw["learner"].data) is not None and d.get_num_samples(train=False) > 0}
                 out = fused_round.run_groups(f, trainers, lambda a: cur[a].kw["learner"]._engine.slot, lambda a: cur[a].kw["learner"]._engine.group,
                                              reqs, has_test)
+            snaps, n = {}, {}
+            for a, m in cur.items():
+                history(m, "TrainStage" if a in trainers else "WaitAggregatedModelsStage")
+                snaps[a] = logger.experiment_snapshot(a)
+                if a in trainers:
+                    m.kw["aggregator"].set_nodes_to_aggregate(train_set)
+                    n[a] = m.kw["learner"].num_train_samples()
             mark("driver:aggregate")
             total = next(iter(states.values())).total_rounds
             aggregator = next(iter(cur.values())).kw["aggregator"]
