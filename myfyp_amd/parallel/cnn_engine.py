@@ -229,8 +229,16 @@ class CNNGroup:
 
     @classmethod
     def reset_all(cls) -> None:
+        """Forget every group, releasing their captured graphs now (after the devices drain), not
+        whenever the cyclic garbage collector reaches a dropped group: a torch CUDA graph destroyed
+        from inside a collection, at an arbitrary point of later work, aborted a GPU test run."""
         with cls._lock:
+            groups = list(cls._groups.values())
             cls._groups.clear()
+        for dev in {g.device for g in groups if g.device.type == "cuda"}:
+            torch.cuda.synchronize(dev)
+        for g in groups:
+            g.close()
 
     def __init__(self, device: torch.device, template: torch.nn.Module, batch_size: int, capacity: int = 8) -> None:
         self.device = device
