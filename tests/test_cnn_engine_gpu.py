@@ -339,6 +339,7 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
         x, y = lr_.device_data(True)
         _torch_step(ref, x[:batch], y[:batch], lr, momentum, wd)
         eng = dict(lr_.model.get_model().named_parameters())
+        num = num16 = den = 0.0  # the update scale over every layer with >= 256 elements
         for (name, p_ref), p0 in zip(ref.named_parameters(), before[i]):
             d_ref = (p_ref.detach() - p0).flatten()
             d_eng = (eng[name].detach() - p0).flatten()
@@ -354,10 +355,16 @@ def _run_one_step(model_fn, n_peers, batch, lr, momentum=0.0, wd=0.0):
                 # the update's scale along torch's direction: rounding noise is unbiased, so this
                 # stays near 1 even where the deep-net floor is large; a wrong step size does not
                 # (a 5 % learning-rate error was caught here and by nothing else in this file,
-                # profiles/r5_mutation)
-                ratio = float(torch.dot(d_eng.double(), d_ref.double()) / torch.dot(d_ref.double(), d_ref.double()))
-                ratio16 = float(torch.dot(floors[i][name].double(), d_ref.double()) / torch.dot(d_ref.double(), d_ref.double()))
-                assert abs(ratio - 1.0) < max(0.02, 3.0 * abs(ratio16 - 1.0)), (name, ratio, ratio16)
+                # profiles/r5_mutation). Per layer only a gross error (a small BN layer's ratio
+                # strays ~6 % from run to run: split-K atomics); the tight bound is on the sum
+                dr = torch.dot(d_ref.double(), d_ref.double())
+                de, d16 = torch.dot(d_eng.double(), d_ref.double()), torch.dot(floors[i][name].double(), d_ref.double())
+                ratio, ratio16 = float(de / dr), float(d16 / dr)
+                assert abs(ratio - 1.0) < max(0.1, 4.0 * abs(ratio16 - 1.0)), (name, ratio, ratio16)
+                num, num16, den = num + float(de), num16 + float(d16), den + float(dr)
+        if den > 0:
+            ratio, ratio16 = num / den, num16 / den
+            assert abs(ratio - 1.0) < max(0.02, 3.0 * abs(ratio16 - 1.0)), ("all layers", ratio, ratio16)
         # BN running statistics follow torch
         for (name, b_ref) in ref.named_buffers():
             if "running" in name:
