@@ -131,6 +131,9 @@ using namespace f32k;
 #ifndef P32_XDIRECT
 #define P32_XDIRECT 0
 #endif
+#ifndef P32_LDT_PAD
+#define P32_LDT_PAD 16
+#endif
 constexpr int SMR = (P32_SM8 && !P32_LL_PL) ? 2 : 4;  // softmax rows per lane
 #ifndef P32_LL_DH2
 #define P32_LL_DH2 0
@@ -200,7 +203,10 @@ __host__ __device__ inline int kh_of(int D0, int KS) { return (ks1_of(D0) + KS -
 __host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0, int KS) {
   OwnerLds32 L;
   L.ldx = kh_of(D0, KS) * 32 + 8;
-  L.ldt = Bpad + 8;
+  // dH1 split tiles: row stride Bpad + 16 bf16 (80 / 48 at Bpad 64 / 32) puts the 16 rows x 4 column
+  // chunks of C2's ds_read_b128 fragment reads on 16 distinct 4-bank slots in every lane group
+  // (MI355X_MICROARCH.md §LDS); Bpad + 8 left 2-way conflicts (P32_LDT_PAD=8: the old stride, A/B)
+  L.ldt = Bpad + P32_LDT_PAD;
   const int MT = Bpad / 16;
   const size_t red = (size_t)8 * MT * 64 * 16, dh2 = (size_t)Bpad * LDD * 4;
   size_t o = 0;
