@@ -134,6 +134,12 @@ using namespace f32k;
 #ifndef P32_LDT_PAD
 #define P32_LDT_PAD 16
 #endif
+// swizzled X tile (xsw; 0: row stride kh * 32 + 8, no swizzle). Measured (profiles/r5_xswz): LDS bank
+// conflicts per LDS instruction 2.89 -> 1.10, but 8.6 % more LDS instructions, 256 VGPRs, and the
+// epoch 2 % longer (581.5 / 585.8 / 589.7 vs 580.4 / 594.1 / 594.0 rounds/s): kept off
+#ifndef P32_XSWZ
+#define P32_XSWZ 0
+#endif
 constexpr int SMR = (P32_SM8 && !P32_LL_PL) ? 2 : 4;  // softmax rows per lane
 #ifndef P32_LL_DH2
 #define P32_LL_DH2 0
@@ -192,6 +198,26 @@ __device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, i
 }
 
 
+// X tile chunk swizzle: within each K step's 32 columns, 16-byte chunk c of row r is stored at chunk
+// c ^ ((r >> 2) & 3). Every access (staging stores, zero fill, forward reads, C2's transposed reads)
+// goes through it; combined with the row stride of owner_lds32 it leaves no LDS bank conflicts on
+// the forward's and C2's reads (r5: the transposed reads were 2-way conflicted).
+__device__ __forceinline__ int xsw(int r, int col) {
+  return P32_XSWZ ? (col & ~31) | ((((col >> 3) & 3) ^ ((r >> 2) & 3)) << 3) | (col & 7) : col;
+}
+// frag_b_tr_l on the swizzled X tile: the B fragment of K rows k0.. (a multiple of 16) and the 16
+// columns n0 = 32 s + 16 tt of K step s
+// (k0 a multiple of 16: row r0 = k0 + 8g + q has swizzle 2(g & 1), row r0 + 4 that one with bit 0 set)
+__device__ __forceinline__ bf16x8 frag_b_tr_x(const bf16* base, int ld, int k0, int s, int tt, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int cx = (2 * tt + (pp >> 1)) ^ (P32_XSWZ ? (g & 1) << 1 : 0);
+  const bf16* p0 = base + (k0 + 8 * g + q) * ld + 32 * s + (cx << 3) + 4 * (pp & 1);
+  const bf16* p1 = p0 + 4 * ld + (P32_XSWZ ? ((cx & 1) ? -8 : 8) : 0);
+  const mlp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p0));
+  const mlp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mlp_lds_s16x4*)(p1));
+  return __builtin_bit_cast(bf16x8, (mlp_s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 // ---- LDS carving (16-byte aligned offsets)
 struct OwnerLds32 {
   int ldx;  // bf16 row stride of the X tile
@@ -202,7 +228,10 @@ struct OwnerLds32 {
 __host__ __device__ inline int kh_of(int D0, int KS) { return (ks1_of(D0) + KS - 1) / KS; }
 __host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0, int KS) {
   OwnerLds32 L;
-  L.ldx = kh_of(D0, KS) * 32 + 8;
+  // X tile rows of kh K steps, padded so the row stride is 4 (mod 16) 16-byte chunks: with the chunk
+  // swizzle xsw() both the forward's ds_read_b64 A reads and C2's ds_read_b64_tr_b16 reads are
+  // conflict-free (MI355X_MICROARCH.md §LDS lane groups; no pad at D0 = 784, K split 1 or 2)
+  L.ldx = kh_of(D0, KS) * 32 + (P32_XSWZ ? 8 * ((4 - 4 * kh_of(D0, KS)) & 15) : 8);
   // dH1 split tiles: row stride Bpad + 16 bf16 (80 / 48 at Bpad 64 / 32) puts the 16 rows x 4 column
   // chunks of C2's ds_read_b128 fragment reads on 16 distinct 4-bank slots in every lane group
   // (MI355X_MICROARCH.md §LDS); Bpad + 8 left 2-way conflicts (P32_LDT_PAD=8: the old stride, A/B)
@@ -381,9 +410,9 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       if (s < KS1 && gcol < D0) {
         const bf16* src = xd ? (r < rows ? xp16 + (int64_t)xidx_p[t * a.B + r] * D0 + gcol : xp16)
                              : a.Xb16 + ((int64_t)p * a.xb_rows + (int64_t)t * a.B + r) * D0 + gcol;
-        *reinterpret_cast<uint4*>(sX + r * LDX + col) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4*>(sX + r * LDX + xsw(r, col)) = r < rows ? *reinterpret_cast<const uint4*>(src) : uint4{0u, 0u, 0u, 0u};
       } else if (s < KS1 && gcol == D0) {
-        *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows);
+        *reinterpret_cast<uint4*>(sX + r * LDX + xsw(r, col)) = bias_chunk(r < rows);
       }
     }
   };
@@ -392,7 +421,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (z0 < z1)
       for (int e = tid; e < BP * (z1 - z0); e += NT) {
         const int r = e / (z1 - z0), q = e % (z1 - z0);
-        sX[r * LDX + z0 + q] = (bf16)0.f;
+        sX[r * LDX + xsw(r, z0 + q)] = (bf16)0.f;
       }
   }
   if (nsteps > 0) xw_stage(0, lane);
@@ -438,8 +467,10 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       if (lds_step && mt != wave) continue;  // wave-uniform
-      const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * hq;
-      const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp), *reinterpret_cast<const bf16x4*>(xp + 16));
+      const int xs = P32_XSWZ ? cq >> 2 : 0;  // xsw of row 16mt + cq: swizzled chunks of columns 4hq.. and 16 + 4hq..
+      const bf16* xp = sX + (16 * mt + cq) * LDX + 32 * s + 4 * (hq & 1);
+      const bf16x8 af = cat8(*reinterpret_cast<const bf16x4*>(xp + (((hq >> 1) ^ xs) << 3)),
+                             *reinterpret_cast<const bf16x4*>(xp + (((2 + (hq >> 1)) ^ xs) << 3)));
       acc[mt] = mfma3(af, bh, bm, bl, acc[mt]);
     }
   };
@@ -712,7 +743,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
             f32x4 acc = zero4();  // C[k = 32s + 16tt + 4h + i][o1 = c]
 #pragma unroll
             for (int kb = 0; kb < BP / 32; ++kb)
-              acc = mfma3(frag_b_tr_l(sX, LDX, 32 * kb, 32 * s + 16 * tt, lq), ld8(dfrag + 32 * kb), ld8(dfrag + 16 * LDT + 32 * kb),
+              acc = mfma3(frag_b_tr_x(sX, LDX, 32 * kb, s, tt, lq), ld8(dfrag + 32 * kb), ld8(dfrag + 16 * LDT + 32 * kb),
                           ld8(dfrag + 32 * LDT + 32 * kb), acc);
             if (q < RQ) {
               const int qq = q < RQ ? q : 0;
@@ -744,9 +775,9 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
               const int r = idx >> 2, col = 32 * s + 8 * (idx & 3), gcol = C0 + col;
               if (!xmine) continue;
               if (gcol < D0)
-                *reinterpret_cast<uint4*>(sX + r * LDX + col) = xq[kk];
+                *reinterpret_cast<uint4*>(sX + r * LDX + xsw(r, col)) = xq[kk];
               else if (gcol == D0)
-                *reinterpret_cast<uint4*>(sX + r * LDX + col) = bias_chunk(r < rows_next);
+                *reinterpret_cast<uint4*>(sX + r * LDX + xsw(r, col)) = bias_chunk(r < rows_next);
             }
           }
         }
