@@ -1702,9 +1702,11 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
   const int p = blockIdx.y;
   const int4 ctl = a.ctl[p];
   if (!(ctl.x & 1)) return;
-  const int base = blockIdx.x * EV_ROWS;
+  // grid-stride over the peer's 64-row chunks (mlp_launch_eval_f32 caps the grid)
+  for (int chunk = blockIdx.x;; chunk += gridDim.x) {
+  const int base = chunk * EV_ROWS;
   const int rows = min(EV_ROWS, ctl.w - base);
-  if (rows <= 0) return;
+  if (rows <= 0) break;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, c = lane & 15;
@@ -1826,6 +1828,8 @@ __global__ __launch_bounds__(NT) void mlp_eval_f32(MLPArgs a) {
       atomicAdd(&a.loss_acc[p], loss_part);
       atomicAdd(&a.correct_acc[p], (int)(cp + 0.5f));
     }
+  }
+  __syncthreads();  // H2 (overlaying the X tile) read before the next chunk's X is staged
   }
 }
 
@@ -2055,9 +2059,23 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
   return hipGetLastError();
 }
 
+// The overlapped evaluation starts right before the epoch on the main stream is dispatched: a grid
+// of one workgroup per 64-row chunk (1256 at the headline) took every CU first, and the epoch's
+// gangs waited ~12 us for them to drain (profiles/r5_mlp_pmc/timeline_direct.txt). The grid is now
+// capped at MYFYP_EVAL_WGS workgroups over all peers (default 32: 4 per XCD under round-robin
+// dispatch, beside the 8 x 24 epoch workgroups), each looping over its peer's chunks.
+static int eval_wgs_cap() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_EVAL_WGS");
+    return e != nullptr ? atoi(e) : 32;
+  }();
+  return v;
+}
 void mlp_launch_eval_f32(const MLPArgs& a, int max_rows, hipStream_t s) {
   if (max_rows <= 0) return;
-  const dim3 grid((max_rows + EV_ROWS - 1) / EV_ROWS, a.P);
+  const int chunks = (max_rows + EV_ROWS - 1) / EV_ROWS, cap = eval_wgs_cap();
+  const int per_peer = cap > 0 ? (cap / a.P > 0 ? cap / a.P : 1) : chunks;
+  const dim3 grid(chunks < per_peer ? chunks : per_peer, a.P);
   hipLaunchKernelGGL(mlp_eval_f32, grid, dim3(NT), eval_lds32(a.D0), s, a);
 }
 
