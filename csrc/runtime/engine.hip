@@ -176,6 +176,14 @@ static bool graph_publish() {
   }();
   return v != 0;
 }
+// MYFYP_EVAL_GATHER_ORDER=0: the gather ahead always waits on an event recorded before the epoch (A/B)
+static bool eval_gather_order() {
+  static const int v = [] {
+    const char* e = getenv("MYFYP_EVAL_GATHER_ORDER");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
 static bool ring_events() {
   static const int v = [] {
     const char* e = getenv("MYFYP_RING_EVENTS");
@@ -307,6 +315,13 @@ struct MLPEngine {
   hipStream_t eval_stream = nullptr;
   bool eval_stream_owned = false;  // false: it is the prep stream
   hipEvent_t ev_snap = nullptr;
+  // The gather ahead is ordered after this round's overlapped evaluation (its done event is recorded
+  // on the evaluation stream anyway) when one was enqueued on the epoch's stream with no epoch
+  // launched since: no ordering event on the main stream, and the gather's workgroups start after
+  // the evaluation's instead of competing with the epoch's dispatch (profiles/r5_evalorder)
+  hipStream_t snap_rec_stream = nullptr;
+  unsigned long long snap_rec_launches = ~0ull;
+  hipEvent_t last_eval_done = nullptr;
   struct EvalSide {
     float* params = nullptr;
     bf16* shadow = nullptr;
@@ -464,8 +479,10 @@ struct MLPEngine {
   // ahead: the gather of the NEXT epoch (seed ``seed``), for every peer with data (the next round's
   // active set is not known yet), ordered after the start of the epoch just launched (which reads
   // the other buffer; the one that last read buffer i has then finished)
-  int prep_gather(int i, hipStream_t main, unsigned long long seed, bool ahead = false) {
-    if (prep_level == 2 && start_rec) {
+  int prep_gather(int i, hipStream_t main, unsigned long long seed, bool ahead = false, bool after_eval = false) {
+    if (after_eval) {  // this round's overlapped evaluation: it follows epoch r - 1, the last reader of buffer i
+      CHECK_HIP(hipStreamWaitEvent(prep_stream, last_eval_done, 0));
+    } else if (prep_level == 2 && start_rec) {
       CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_start, 0));
     } else if (done_rec[i]) {
       CHECK_HIP(hipStreamWaitEvent(prep_stream, ev_done[i], 0));
@@ -1324,9 +1341,15 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
       CHECK_HIP(hipEventRecord(go.ev, go.last));
       CHECK_HIP(hipStreamWaitEvent(s, go.ev, 0));
     }
+    const bool after_eval = e->prep_mode && e->prep_level == 2 && e->n_execs > 1 && e->next_seed_valid && e->last_eval_done != nullptr &&
+                            e->snap_rec_stream == s && e->snap_rec_launches == e->launches && eval_gather_order();
     if (e->prep_mode && e->prep_level == 2) {
-      CHECK_HIP(hipEventRecord(e->ev_start, s));
-      e->start_rec = true;
+      if (after_eval) {
+        e->start_rec = false;  // a later gather that is not ahead records its own ordering event
+      } else {
+        CHECK_HIP(hipEventRecord(e->ev_start, s));
+        e->start_rec = true;
+      }
     }
     if (e->launch_epoch(s)) return 1;
     if (e->prep_mode && e->prep_level == 1) {  // (mode 2 orders its gathers by ev_start)
@@ -1335,7 +1358,7 @@ static int run_epoch_impl(MLPEngine* e, const int* t0_host, int slot, hipStream_
     }
     if (e->prep_mode && e->prep_level == 2 && e->n_execs > 1 && e->next_seed_valid) {
       const int nb = buf ^ 1;  // the buffer the next launch's executable reads
-      if (e->prep_gather(nb, s, e->next_seed, true)) return 1;
+      if (e->prep_gather(nb, s, e->next_seed, true, after_eval)) return 1;
       e->ahead_valid[nb] = true;
       e->ahead_seed[nb] = e->next_seed;
     }
@@ -1519,6 +1542,9 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
     if (e->publish(xs, r, es.loss, es.correct, nullptr, es.conf)) return 1;
     CHECK_HIP(hipEventRecord(es.done, xs));
     es.rec = true;
+    e->snap_rec_stream = s;
+    e->snap_rec_launches = e->launches;
+    e->last_eval_done = es.done;
     return 0;
   }
   if (e->wait_evals(s)) return 1;
