@@ -106,25 +106,33 @@ def _run(fused: bool, seed: int, rounds: int = ROUNDS, peers: int = PEERS, n_per
 
 
 def test_config5_engine_matches_torch_oracle_with_dropout():
+    """Engine vs torch fp32 oracle on config 5, two shuffle seeds each. The config is chaotic
+    (Dirichlet(0.5) partitions, a peer killed at round 1, ~5 flat rounds): in the round-5 runs one
+    torch seed ended at 0.798 while the other reached 0.960, and the engine's mid-run accuracy
+    ranged 0.67-0.88 over repeats. Each side is therefore compared by its two-seed mean, within the
+    two sides' combined seed spread (never less than the fixed floors)."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    eng, acc_e = _run(True, 1)
+    e1, acc_e1 = _run(True, 1)
+    e2, acc_e2 = _run(True, 2)
     t1, acc_1 = _run(False, 1)
     t2, acc_2 = _run(False, 2)
-    print(f"[config5] engine acc {np.round(acc_e, 3).tolist()} loss {np.round(eng, 3).tolist()} | torch(1) acc {np.round(acc_1, 3).tolist()} "
-          f"loss {np.round(t1, 3).tolist()} | torch(2) acc {np.round(acc_2, 3).tolist()} loss {np.round(t2, 3).tolist()}", file=sys.stderr)
-    final_t = 0.5 * (acc_1[-1] + acc_2[-1])
-    # the torch oracle itself is not steady here: two shuffle seeds ended at 0.960 and 0.798 in one
-    # run (profiles/r5_final, Dirichlet(0.5) + a dead peer): the torch bar is "one seed clears 0.9",
-    # the engine's is 0.85 and the oracles' mean within their own spread (at least 0.08)
-    assert max(acc_1[-1], acc_2[-1]) > 0.9 and acc_e[-1] > 0.85, (acc_e[-1], acc_1[-1], acc_2[-1])
-    assert abs(acc_e[-1] - final_t) <= max(0.08, abs(acc_1[-1] - acc_2[-1])), (acc_e[-1], acc_1[-1], acc_2[-1])
-    mid_e, mid_1, mid_2 = (float(np.mean(c[3:8])) for c in (acc_e, acc_1, acc_2))
-    assert abs(mid_e - 0.5 * (mid_1 + mid_2)) <= max(0.1, 2 * abs(mid_1 - mid_2)), (mid_e, mid_1, mid_2)
-    for r in range(len(eng)):
-        ref = 0.5 * (t1[r] + t2[r])
-        assert np.isfinite(eng[r]), eng
-        # torch's own shuffle spread, plus 15 % of the loss for bf16 operands and the engine's own
+    print(f"[config5] engine acc {np.round(acc_e1, 3).tolist()} / {np.round(acc_e2, 3).tolist()} loss {np.round(e1, 3).tolist()} / "
+          f"{np.round(e2, 3).tolist()} | torch acc {np.round(acc_1, 3).tolist()} / {np.round(acc_2, 3).tolist()} loss {np.round(t1, 3).tolist()} / "
+          f"{np.round(t2, 3).tolist()}", file=sys.stderr)
+    fin_e, fin_t = 0.5 * (acc_e1[-1] + acc_e2[-1]), 0.5 * (acc_1[-1] + acc_2[-1])
+    spread_fin = abs(acc_1[-1] - acc_2[-1]) + abs(acc_e1[-1] - acc_e2[-1])
+    # both sides learn the task: one seed of each clears 0.9, none ends below 0.8
+    assert max(acc_1[-1], acc_2[-1]) > 0.9 and max(acc_e1[-1], acc_e2[-1]) > 0.9, (acc_e1[-1], acc_e2[-1], acc_1[-1], acc_2[-1])
+    assert min(acc_e1[-1], acc_e2[-1]) > 0.8, (acc_e1[-1], acc_e2[-1])
+    assert abs(fin_e - fin_t) <= max(0.08, spread_fin), (fin_e, fin_t, spread_fin)
+    mids = [float(np.mean(c[3:8])) for c in (acc_e1, acc_e2, acc_1, acc_2)]
+    mid_e, mid_t = 0.5 * (mids[0] + mids[1]), 0.5 * (mids[2] + mids[3])
+    assert abs(mid_e - mid_t) <= max(0.1, 2 * (abs(mids[0] - mids[1]) + abs(mids[2] - mids[3]))), mids
+    for r in range(len(e1)):
+        eng, ref = 0.5 * (e1[r] + e2[r]), 0.5 * (t1[r] + t2[r])
+        assert np.isfinite(e1[r]) and np.isfinite(e2[r]), (e1, e2)
+        # both sides' shuffle spread, plus 15 % of the loss for bf16 operands and the engine's own
         # batch order
-        assert abs(eng[r] - ref) <= 2 * abs(t1[r] - t2[r]) + 0.15 * ref, (r, eng, t1, t2)
-    assert eng[-1] < eng[0], eng  # the local objective goes down over the rounds
+        assert abs(eng - ref) <= 2 * (abs(t1[r] - t2[r]) + abs(e1[r] - e2[r])) + 0.15 * ref, (r, e1, e2, t1, t2)
+    assert e1[-1] < e1[0] and e2[-1] < e2[0], (e1, e2)  # the local objective goes down over the rounds
