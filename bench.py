@@ -63,11 +63,25 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-failover", action="store_true", help="skip the per-round confirmation of the weight collectives (fault tolerance off)")
     ap.add_argument("--no-prewarm", action="store_true", help="do not prepare the fused engine at Node.start (round 0 captures the epoch graph)")
     ap.add_argument("--launch", choices=["auto", "mesh", "ranks"], default="auto",
-                    help="mesh: ONE process drives the N GPUs (in-process RCCL mesh, ncclCommInitAll; under torchrun rank 0 "
-                         "drives them and the other ranks wait); ranks: one process per GPU (torchrun). auto = mesh")
+                    help="ranks: one process per GPU (torchrun, torch.distributed over RCCL); mesh: ONE process drives the N GPUs "
+                         "(in-process RCCL mesh, ncclCommInitAll; under torchrun rank 0 drives them and the other ranks wait). "
+                         "auto = ranks under torchrun, mesh for one process started with --gpus N")
     ap.add_argument("--mesh-virtual", action="store_true",
                     help="rehearsal: N mesh ranks on the visible device(s) with host-side collectives (n_gpus reports the physical count)")
     return ap.parse_args()
+
+
+def _engine_label(nodes, eager: bool) -> str:
+    """What actually launched the local epochs: the persistent epoch kernel is launched directly
+    (``MYFYP_EPOCH_GRAPH=0`` default since round 5); the step path replays a captured hipGraph."""
+    eng = getattr(nodes[0].learner, "_engine", None) if nodes else None
+    grp = getattr(eng, "group", None)
+    kind = getattr(grp, "epoch_launch_kind", None)
+    if callable(kind):
+        kind = kind()
+    if eager:
+        return "fused-hip-eager"
+    return f"fused-hip-{kind}" if kind else "fused-hip"
 
 
 def main() -> None:
@@ -117,8 +131,7 @@ def main() -> None:
     if mode == "mesh":
         Settings.MESH_VIRTUAL = bool(args.mesh_virtual)
         fed = Federation.init(devices=args.gpus)
-        if fed.mesh is None or fed.mesh_size != args.gpus:
-            raise SystemExit(f"bench: device mesh of {args.gpus} not formed (got {fed.mesh_size})")
+        launch.check_mesh(fed, args.gpus, bool(args.mesh_virtual), "bench")
         mesh_devs = list(fed.devices)
     else:
         fed = Federation.init()
@@ -297,7 +310,7 @@ def main() -> None:
                 "optimizer": "adam lr=1e-3 (fresh per round)",
                 "aggregator": "FedAvg (weighted all-reduce)",
                 "collective": coll,
-                "engine": "fused-hip" + ("-eager" if args.eager else "-hipgraph") if fused else "autograd",
+                "engine": _engine_label(nodes, args.eager) if fused else "autograd",
             },
             # headline time-to-target: Node.start() (incl. the engine prewarm) + set_start_learning
             # -> the evaluation that reaches the target (the prewarm moved setup out of

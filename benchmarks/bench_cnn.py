@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", choices=["lenet5", "resnet18"], default="resnet18")
-    ap.add_argument("--gpus", type=int, default=1, help="GPUs (one process drives them: device mesh; see myfyp_amd/utils/launch.py)")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (torchrun: one process per GPU; one process: device mesh; see myfyp_amd/utils/launch.py)")
     ap.add_argument("--launch", choices=["auto", "mesh", "ranks"], default="auto")
     ap.add_argument("--mesh-virtual", action="store_true", help="rehearsal: --gpus mesh ranks on the visible device(s)")
     ap.add_argument("--peers", type=int, default=8)
@@ -145,8 +145,7 @@ def main() -> None:
     if mode == "mesh":
         Settings.MESH_VIRTUAL = bool(args.mesh_virtual)
         fed = Federation.init(devices=args.gpus)
-        if fed.mesh is None or fed.mesh_size != args.gpus:
-            raise SystemExit(f"bench_cnn: device mesh of {args.gpus} not formed")
+        launch.check_mesh(fed, args.gpus, bool(args.mesh_virtual), "bench_cnn")
     else:
         fed = Federation.init()
     world, rank = fed.world, fed.rank

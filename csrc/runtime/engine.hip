@@ -1129,6 +1129,17 @@ int mlp_engine_set_train_data(void* h, const uint64_t* Xp, const uint64_t* Yp, c
 
 // Direct-X fp32 epochs: per-peer device pointers to exact-bf16 copies of the training images ([n_p][D0],
 // the caller keeps them alive and rebinds when the data changes). Re-captures.
+// Drain the prep stream (the next epoch's gather, enqueued ahead, reads the bound data tensors)
+// and forget the gathers ahead: called before the caller drops its references to the data it
+// bound, since the torch allocator does not know this stream.
+int mlp_engine_drain_prep(void* h) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (e->prep_stream) CHECK_HIP(hipStreamSynchronize(e->prep_stream));
+  e->ahead_valid[0] = e->ahead_valid[1] = false;
+  return 0;
+}
+
 int mlp_engine_set_train_x16(void* h, const uint64_t* Xp16) {
   auto* e = (MLPEngine*)h;
   std::lock_guard<std::mutex> g(e->mu);

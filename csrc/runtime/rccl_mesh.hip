@@ -16,7 +16,13 @@
 //   [Σ w x | Σ w] over xGMI → per device the apply kernel writing the mean into its live rows;
 //   rmesh_check / rmesh_abort / rmesh_shrink — failure handling: poll ncclCommGetAsyncError,
 //   ncclCommAbort every communicator (local: ends kernels stuck on a dead peer), and rebuild the
-//   mesh over the surviving devices with a fresh ncclCommInitAll.
+//   mesh over the surviving devices with a fresh ncclCommInitAll;
+//   rmesh_rebuild — the same rebuild for a HEALTHY mesh (a device whose last peer left): the
+//   caller has drained every device, so the communicators are destroyed, not aborted (an abort
+//   would end collectives still queued on a device);
+//   rmesh_debug_inject — fault hook: rmesh_check reports an asynchronous error on one rank.
+// The round-level policy around these (deadline per collective, retained partial sums, aggregate
+// what arrived) is parallel/mesh_guard.py.
 //
 // Every entry point returns 0 on success, non-zero on failure (message via rmesh_last_error()).
 // The current HIP device of the calling thread is restored on return.
@@ -37,6 +43,7 @@ struct Mesh {
   std::vector<int> devs;          // HIP device ordinal per mesh rank
   std::vector<ncclComm_t> comms;  // one communicator per device (rank i <-> devs[i])
   bool aborted = false;
+  int injected = -1;  // fault hook (rmesh_debug_inject): rmesh_check reports an error on this rank
 };
 
 struct DeviceGuard {  // restores the caller's current device
@@ -90,6 +97,8 @@ bool group_end(bool ok) {
   ncclResult_t r = ncclGroupEnd();
   return nccl_ok(r, "ncclGroupEnd") && ok;
 }
+
+int fedavg_apply_all(Mesh* m, void** params, void** res, const int* P, int64_t n, const int64_t* ld, const float* mask, void** streams);
 
 }  // namespace
 
@@ -224,7 +233,13 @@ int rmesh_p2p(void* h, int nops, const int* kind, const int* rank, const int* pe
 // sample weights (0 = not a trainer) and mask[...] the rows that receive the mean (every live
 // local peer), with off_i = sum_{j<i} P_j. Per device: reduce (weights as kernel arguments) →
 // one grouped all-reduce of [Σ w x | Σ w] → apply. Three launches per device, host never waits.
-int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, const int64_t* ld, const float* w, const float* mask, void** streams) {
+//
+// outs (nullable): out-of-place all-reduce into outs[i] (n + 1 floats), the apply reads outs. bufs
+// then keep each device's local partial sum after the call, so a failed or aborted all-reduce can
+// be re-run over the surviving devices from them (rmesh_fedavg_retry) without re-reading rows the
+// failed round's apply may already have overwritten.
+int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, const int64_t* ld, const float* w, const float* mask, void** streams,
+                 void** outs) {
   auto* m = static_cast<Mesh*>(h);
   if (!usable(m)) return 1;
   const int G = (int)m->devs.size();
@@ -256,9 +271,35 @@ int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, c
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
   bool ok = true;
   for (int i = 0; i < G && ok; ++i)
-    ok = nccl_ok(ncclAllReduce(bufs[i], bufs[i], (size_t)(n + 1), ncclFloat32, ncclSum, m->comms[i], (hipStream_t)streams[i]), "ncclAllReduce");
+    ok = nccl_ok(ncclAllReduce(bufs[i], outs ? outs[i] : bufs[i], (size_t)(n + 1), ncclFloat32, ncclSum, m->comms[i], (hipStream_t)streams[i]),
+                 "ncclAllReduce");
   if (!group_end(ok)) return 1;
-  off = 0;
+  return fedavg_apply_all(m, params, outs ? outs : bufs, P, n, ld, mask, streams);
+}
+
+// Second half of a FedAvg whose all-reduce failed: the retained partial sums bufs[i] (from
+// rmesh_fedavg with outs) are all-reduced again over the CURRENT (rebuilt) mesh into outs[i] and
+// applied to the rows in mask. Arrays are indexed by the current mesh ranks.
+int rmesh_fedavg_retry(void* h, void** params, void** bufs, void** outs, const int* P, int64_t n, const int64_t* ld, const float* mask, void** streams) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  const int G = (int)m->devs.size();
+  DeviceGuard g;
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (int i = 0; i < G && ok; ++i)
+    ok = nccl_ok(ncclAllReduce(bufs[i], outs[i], (size_t)(n + 1), ncclFloat32, ncclSum, m->comms[i], (hipStream_t)streams[i]), "ncclAllReduce");
+  if (!group_end(ok)) return 1;
+  return fedavg_apply_all(m, params, outs, P, n, ld, mask, streams);
+}
+
+}  // extern "C"
+
+namespace {
+// per device: the apply kernel over the rows in mask (the mean in res[i][0..n), Σw in res[i][n])
+int fedavg_apply_all(Mesh* m, void** params, void** res, const int* P, int64_t n, const int64_t* ld, const float* mask, void** streams) {
+  const int G = (int)m->devs.size();
+  int off = 0;
   for (int i = 0; i < G; ++i) {
     if (P[i] > 0) {
       unsigned long long bits = 0;
@@ -266,7 +307,7 @@ int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, c
         if (mask[off + p] != 0.f) bits |= 1ull << p;
       if (bits) {
         if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
-        const float* out = static_cast<const float*>(bufs[i]);
+        const float* out = static_cast<const float*>(res[i]);
         fl_fedavg_apply(static_cast<float*>(params[i]), out, out + n, P[i], n, ld[i], bits, (hipStream_t)streams[i]);
         if (!hip_ok(hipGetLastError(), "fl_fedavg_apply")) return 1;
       }
@@ -275,11 +316,18 @@ int rmesh_fedavg(void* h, void** params, void** bufs, const int* P, int64_t n, c
   }
   return 0;
 }
+}  // namespace
+
+extern "C" {
 
 // 0: every communicator healthy; otherwise the first asynchronous error (message set).
 int rmesh_check(void* h) {
   auto* m = static_cast<Mesh*>(h);
   if (!usable(m)) return 1;
+  if (m->injected >= 0 && m->injected < (int)m->devs.size()) {
+    g_err = "rank " + std::to_string(m->injected) + " (device " + std::to_string(m->devs[m->injected]) + "): injected asynchronous error (rmesh_debug_inject)";
+    return 1;
+  }
   for (size_t i = 0; i < m->comms.size(); ++i) {
     ncclResult_t e = ncclSuccess;
     if (!nccl_ok(ncclCommGetAsyncError(m->comms[i], &e), "ncclCommGetAsyncError")) return 1;
@@ -331,6 +379,52 @@ int rmesh_shrink(void* h, const int* keep, int nkeep) {
   m->devs = devs;
   m->comms = comms;
   m->aborted = false;
+  m->injected = -1;
+  return 0;
+}
+
+// Rebuild a healthy mesh over the listed ranks. The caller has drained every device of the mesh
+// (hipDeviceSynchronize / stream syncs), so no collective is queued: the communicators are
+// destroyed (a clean teardown) and a fresh ncclCommInitAll runs over the kept devices. An aborted
+// mesh takes rmesh_shrink's path.
+int rmesh_rebuild(void* h, const int* keep, int nkeep) {
+  auto* m = static_cast<Mesh*>(h);
+  if (m == nullptr || nkeep < 1) {
+    g_err = "rmesh_rebuild: need a mesh and at least one member";
+    return 2;
+  }
+  if (m->aborted) return rmesh_shrink(h, keep, nkeep);
+  std::vector<int> devs;
+  for (int k = 0; k < nkeep; ++k) {
+    if (keep[k] < 0 || keep[k] >= (int)m->devs.size()) {
+      g_err = "rmesh_rebuild: member index out of range";
+      return 2;
+    }
+    devs.push_back(m->devs[keep[k]]);
+  }
+  DeviceGuard g;
+  int rc = 0;
+  for (auto& c : m->comms) {
+    if (c != nullptr && !nccl_ok(ncclCommDestroy(c), "ncclCommDestroy")) rc = 1;
+    c = nullptr;
+  }
+  m->aborted = true;  // no usable communicator until the init below succeeds
+  if (rc != 0) return 1;
+  std::vector<ncclComm_t> comms(devs.size(), nullptr);
+  if (!nccl_ok(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()), "ncclCommInitAll")) return 1;
+  m->devs = devs;
+  m->comms = comms;
+  m->aborted = false;
+  m->injected = -1;
+  return 0;
+}
+
+// Fault hook for tests: rmesh_check reports an asynchronous error on mesh rank `rank` until the
+// mesh is rebuilt (-1 clears it).
+int rmesh_debug_inject(void* h, int rank) {
+  auto* m = static_cast<Mesh*>(h);
+  if (m == nullptr) return 1;
+  m->injected = rank;
   return 0;
 }
 

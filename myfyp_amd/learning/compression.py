@@ -87,10 +87,24 @@ def _encode_array(a: np.ndarray, c: Dict[str, Dict[str, Any]]) -> Any:
     return enc
 
 
-def _decode_array(enc: Any) -> np.ndarray:
+# Bounds on peer-supplied payloads: a compressed payload must not be able to make the
+# receiver allocate more than this (a zlib bomb, or a tiny top-k payload naming a huge shape). With
+# the receiving model's shapes known, the bound is the model's own size.
+MAX_DECODED_BYTES = 1 << 30
+MAX_ELEMENTS = 1 << 28
+
+
+def _decode_array(enc: Any, expect: Optional[tuple] = None, max_elems: int = MAX_ELEMENTS) -> np.ndarray:
     if "raw" in enc:
         return np.asarray(enc["raw"])
     shape = tuple(int(s) for s in enc["shape"])
+    if any(d < 0 for d in shape):
+        raise ValueError(f"compressed tensor: negative dimension in {shape}")
+    if expect is not None and tuple(expect) != shape:
+        raise ValueError(f"compressed tensor of shape {shape}, the model expects {tuple(expect)}")
+    n_elems = int(np.prod(shape, dtype=np.int64)) if shape else 1
+    if n_elems > max_elems:
+        raise ValueError(f"compressed tensor of {n_elems} elements exceeds the bound {max_elems}")
     if "q" in enc:
         qt = enc["qtype"]
         q = np.asarray(enc["q"])
@@ -102,11 +116,18 @@ def _decode_array(enc: Any) -> np.ndarray:
             vals = q.astype(np.float32) * np.float32(enc["scale"])
     else:
         vals = np.asarray(enc["v"], dtype=np.float32)
-    n = int(np.prod(shape)) if shape else 1
+    n = n_elems
     if "idx" in enc:
+        idx = np.asarray(enc["idx"])
+        if idx.ndim != 1 or not np.issubdtype(idx.dtype, np.integer) or idx.size != vals.size:
+            raise ValueError("compressed tensor: top-k indices must be a 1-D integer array, one per value")
+        if idx.size and (idx[0] < 0 or idx[-1] >= n or np.any(np.diff(idx) <= 0)):
+            raise ValueError("compressed tensor: top-k indices out of range or not strictly increasing")
         flat = np.zeros(n, dtype=np.float32)
-        flat[np.asarray(enc["idx"])] = vals
+        flat[idx] = vals
     else:
+        if vals.size != n:
+            raise ValueError(f"compressed tensor: {vals.size} values for shape {shape}")
         flat = vals
     return flat.reshape(shape).astype(np.dtype(enc["dtype"]))
 
@@ -125,12 +146,27 @@ def encode(params: List[np.ndarray], additional_info: Dict[str, Any], compressio
     return raw
 
 
-def decode(data: bytes, loads) -> Tuple[List[np.ndarray], Dict[str, Any]]:
+def decode(data: bytes, loads, expected_shapes: Optional[List[tuple]] = None) -> Tuple[List[np.ndarray], Dict[str, Any]]:
     """(params, additional_info) of a payload in the reference format or a compressed one; ``loads``
-    is the restricted unpickler."""
+    is the restricted unpickler. ``expected_shapes`` (the receiving model's) bounds what a
+    compressed payload may decode to: its inflated size, each tensor's shape, and the top-k
+    indices are checked before anything is allocated."""
+    max_bytes, max_elems = MAX_DECODED_BYTES, MAX_ELEMENTS
+    if expected_shapes:
+        model_elems = sum(int(np.prod(s, dtype=np.int64)) if len(s) else 1 for s in expected_shapes)
+        max_elems = max(1, model_elems)
+        # the pickled payload of an uncompressed fp32 model plus generous framing
+        max_bytes = min(MAX_DECODED_BYTES, 8 * model_elems + (16 << 20))
     if data[: len(MAGIC)] == MAGIC:
-        data = zlib.decompress(data[len(MAGIC):])
+        d = zlib.decompressobj()
+        out = d.decompress(data[len(MAGIC):], max_bytes)
+        if d.unconsumed_tail or not d.eof:
+            raise ValueError(f"compressed payload inflates past {max_bytes} bytes (or is truncated)")
+        data = out
     loaded = loads(data)
     if "compression" in loaded:
-        return [_decode_array(e) for e in loaded["params"]], loaded["additional_info"]
+        encs = loaded["params"]
+        if expected_shapes is not None and len(encs) != len(expected_shapes):
+            raise ValueError(f"compressed payload has {len(encs)} tensors, the model {len(expected_shapes)}")
+        return [_decode_array(e, None if expected_shapes is None else expected_shapes[i], max_elems) for i, e in enumerate(encs)], loaded["additional_info"]
     return loaded["params"], loaded["additional_info"]

@@ -97,7 +97,9 @@ class P2PFLModel:
         from myfyp_amd.learning import compression as _comp
 
         try:
-            return _comp.decode(data, safe_loads)
+            shapes_of = getattr(self, "expected_shapes", None)
+            shapes = shapes_of() if callable(shapes_of) else None
+            return _comp.decode(data, safe_loads, shapes)
         except Exception as e:
             raise DecodingParamsError("Error decoding parameters") from e
 

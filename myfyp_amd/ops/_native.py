@@ -66,6 +66,7 @@ _SIGNATURES = {
     "mlp_engine_run_epoch": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mlp_engine_run_epoch_pub": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "mlp_engine_set_train_x16": (c_int, [c_void_p, c_void_p]),
+    "mlp_engine_drain_prep": (c_int, [c_void_p]),
     "mlp_engine_x_direct": (c_int, [c_void_p]),
     "mlp_engine_x_direct_build": (c_int, []),
     "mlp_engine_run_epoch_eager": (c_int, [c_void_p, c_void_p, c_void_p]),

@@ -41,10 +41,15 @@ _SIGS = {
     "rmesh_broadcast": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "rmesh_allgather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     "rmesh_p2p": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
-    "rmesh_fedavg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "rmesh_fedavg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p]),
+    "rmesh_fedavg_retry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "rmesh_check": (ctypes.c_int, [ctypes.c_void_p]),
     "rmesh_abort": (ctypes.c_int, [ctypes.c_void_p]),
     "rmesh_shrink": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "rmesh_rebuild": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "rmesh_debug_inject": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "rmesh_destroy": (None, [ctypes.c_void_p]),
 }
 
@@ -59,6 +64,31 @@ def _ptrs(vals: Sequence[int]) -> ctypes.Array:
 
 def _stream_ptr(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+
+
+class Marker:
+    """Completion marker of a mesh member's queued work: an event recorded on the member device's
+    current stream (``cpu`` members complete synchronously)."""
+
+    def __init__(self, dev: torch.device) -> None:
+        self.ev = None
+        if dev.type == "cuda":
+            with torch.cuda.device(dev):
+                self.ev = torch.cuda.Event()
+                self.ev.record(torch.cuda.current_stream(dev))
+
+    def query(self) -> bool:
+        return True if self.ev is None else bool(self.ev.query())
+
+
+class _Stalled(Marker):
+    """A member that never completes (HostMesh fault hook)."""
+
+    def __init__(self) -> None:
+        self.ev = None
+
+    def query(self) -> bool:
+        return False
 
 
 class DeviceMesh:
@@ -100,9 +130,20 @@ class DeviceMesh:
         raise NotImplementedError
 
     def fedavg_stacked(self, params: Sequence[torch.Tensor], bufs: Sequence[torch.Tensor], P: Sequence[int], n: int,
-                       ld: Sequence[int], w: np.ndarray, mask: np.ndarray) -> None:
-        """FedAvg over the stacked groups (one per rank); see ``rmesh_fedavg``."""
+                       ld: Sequence[int], w: np.ndarray, mask: np.ndarray, outs: Optional[Sequence[torch.Tensor]] = None) -> None:
+        """FedAvg over the stacked groups (one per rank); see ``rmesh_fedavg``. With ``outs`` the
+        all-reduce is out of place and ``bufs`` keep each rank's local partial sum (the input of
+        :meth:`fedavg_retry`)."""
         raise NotImplementedError
+
+    def fedavg_retry(self, params, bufs, outs, P, n: int, ld, mask: np.ndarray) -> None:
+        """Re-run a FedAvg's all-reduce from the retained partial sums ``bufs`` over the CURRENT
+        members (after a shrink) into ``outs``, then apply to the masked rows."""
+        raise NotImplementedError
+
+    def marker(self, rank: int) -> Marker:
+        """Completion marker of everything queued so far on member ``rank``'s current stream."""
+        return Marker(self.devices[rank])
 
     def check(self) -> None:
         pass
@@ -111,7 +152,17 @@ class DeviceMesh:
         pass
 
     def shrink(self, keep: Sequence[int]) -> None:
-        """Rebuild over the surviving ranks ``keep`` (indices into ``devices``), renumbered in order."""
+        """Rebuild over the surviving ranks ``keep`` (indices into ``devices``), renumbered in order;
+        after a failure (the communicators are aborted, never waited for)."""
+        raise NotImplementedError
+
+    def rebuild(self, keep: Sequence[int]) -> None:
+        """Rebuild a HEALTHY mesh over ``keep`` (a device whose last peer left). The caller has
+        drained every member device; the communicators are destroyed, not aborted."""
+        self.shrink(keep)
+
+    def inject_error(self, rank: int) -> None:
+        """Fault hook: :meth:`check` reports an asynchronous error on ``rank`` until a rebuild."""
         raise NotImplementedError
 
     def close(self) -> None:
@@ -123,8 +174,37 @@ class HostMesh(DeviceMesh):
 
     kind = "host"
 
+    def __init__(self, devices: Sequence[torch.device]) -> None:
+        super().__init__(devices)
+        self._stalled: set = set()  # fault hook: members (by device position) that never complete
+        self._injected: Optional[int] = None
+        self.aborted = False
+
+    def stall(self, rank: int) -> None:
+        """Fault hook: member ``rank`` stops completing work (its markers and probes never fire),
+        like a device stuck in a kernel."""
+        self._stalled.add(int(rank))
+
+    def marker(self, rank: int) -> Marker:
+        if rank in self._stalled:
+            return _Stalled()
+        return super().marker(rank)
+
+    def inject_error(self, rank: int) -> None:
+        self._injected = int(rank)
+
+    def check(self) -> None:
+        if self.aborted:
+            raise MeshError("host mesh was aborted (rebuild it with shrink)")
+        if self._injected is not None:
+            raise MeshError(f"rank {self._injected}: injected asynchronous error")
+
+    def abort(self) -> None:
+        self.aborted = True
+
     def all_reduce_(self, ts, op: str = "sum") -> None:
         self._check_members(ts, "all_reduce")
+        self._live()
         with self.lock:
             self.calls += 1
             acc = ts[0].detach().clone()
@@ -145,6 +225,7 @@ class HostMesh(DeviceMesh):
 
     def broadcast_(self, ts, root: int) -> None:
         self._check_members(ts, "broadcast")
+        self._live()
         with self.lock:
             self.calls += 1
             src = ts[root]
@@ -154,6 +235,7 @@ class HostMesh(DeviceMesh):
 
     def all_gather_(self, outs, ins) -> None:
         self._check_members(ins, "all_gather")
+        self._live()
         with self.lock:
             self.calls += 1
             cat = torch.cat([x.reshape(-1).to(ins[0].device) for x in ins])
@@ -161,6 +243,7 @@ class HostMesh(DeviceMesh):
                 o.view(-1).copy_(cat.to(o.device))
 
     def p2p_(self, ops) -> None:
+        self._live()
         with self.lock:
             self.calls += 1
             sends = {}
@@ -174,9 +257,14 @@ class HostMesh(DeviceMesh):
                         raise MeshError(f"p2p: receive on rank {rank} from {peer} has no matching send")
                     t.copy_(q.pop(0).to(t.device))
 
-    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask) -> None:
+    def _live(self) -> None:
+        if self.aborted:
+            raise MeshError("host mesh was aborted (rebuild it with shrink)")
+
+    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask, outs=None) -> None:
+        self._live()
         if all(t.is_cuda for t in params):
-            return self._fedavg_native(params, bufs, P, n, ld, w, mask)
+            return self._fedavg_native(params, bufs, P, n, ld, w, mask, outs)
         with self.lock:
             self.calls += 1
             off = 0
@@ -190,19 +278,38 @@ class HostMesh(DeviceMesh):
                     b[:n].copy_((wt[:, None] * rows).sum(0))
                     b[n] = float(np.sum(w[off : off + P[i]], dtype=np.float64))
                 off += P[i]
-            self.all_reduce_(list(bufs))
-            off = 0
-            for i in range(self.size):
-                if P[i] > 0:
-                    b = bufs[i]
-                    mean = b[:n] / b[n].clamp_min(1e-30)
-                    rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])
-                    for p in range(P[i]):
-                        if mask[off + p] != 0:
-                            rows[p, :n].copy_(mean)
-                off += P[i]
+            self._reduce_apply(params, bufs, outs, P, n, ld, mask)
 
-    def _fedavg_native(self, params, bufs, P, n, ld, w, mask) -> None:
+    def _reduce_apply(self, params, bufs, outs, P, n, ld, mask) -> None:
+        if outs is None:
+            res = list(bufs)
+        else:
+            for o, b in zip(outs, bufs):
+                o[: n + 1].copy_(b[: n + 1])
+            res = list(outs)
+        self.all_reduce_([r[: n + 1] for r in res])
+        off = 0
+        for i in range(self.size):
+            if P[i] > 0:
+                b = res[i]
+                mean = b[:n] / b[n].clamp_min(1e-30)
+                rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])
+                for p in range(P[i]):
+                    if mask[off + p] != 0:
+                        rows[p, :n].copy_(mean)
+            off += P[i]
+
+    def fedavg_retry(self, params, bufs, outs, P, n, ld, mask) -> None:
+        self._live()
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        with self.lock:
+            self.calls += 1
+            if all(t.is_cuda for t in params):
+                self._native_reduce_apply(params, bufs, outs, P, n, ld, mask)
+            else:
+                self._reduce_apply(params, bufs, outs, P, n, ld, mask)
+
+    def _fedavg_native(self, params, bufs, P, n, ld, w, mask, outs=None) -> None:
         """GPU members (a virtual mesh on one device): the same per-member reduce / apply launches
         as ``rmesh_fedavg``, with the all-reduce as stream-ordered torch adds — so a one-GPU
         rehearsal issues the real path's launches (host cost per round is representative)."""
@@ -223,18 +330,34 @@ class HostMesh(DeviceMesh):
                         ops.check(fast.myfyp_fedavg_stacked_reduce(bufs[i].data_ptr(), params[i].data_ptr(), int(P[i]), int(n), int(ld[i]),
                                                                    w[off:].ctypes.data, st), "fedavg_stacked_reduce")
                 off += P[i]
-            self.all_reduce_([b[: n + 1] for b in bufs])
-            off = 0
-            for i in range(self.size):
-                if P[i] > 0:
-                    with torch.cuda.device(bufs[i].device):
-                        ops.check(fast.myfyp_fedavg_stacked_apply(params[i].data_ptr(), bufs[i].data_ptr(), int(P[i]), int(n), int(ld[i]),
-                                                                  mask[off:].ctypes.data, _stream_ptr(bufs[i].device)), "fedavg_stacked_apply")
-                off += P[i]
+            self._native_reduce_apply(params, bufs, outs, P, n, ld, mask)
+
+    def _native_reduce_apply(self, params, bufs, outs, P, n, ld, mask) -> None:
+        from myfyp_amd import ops
+
+        fast = ops.fast_lib()
+        if outs is None:
+            res = list(bufs)
+        else:
+            for o, b in zip(outs, bufs):
+                with torch.cuda.device(o.device):
+                    o[: n + 1].copy_(b[: n + 1])
+            res = list(outs)
+        self.all_reduce_([b[: n + 1] for b in res])
+        off = 0
+        for i in range(self.size):
+            if P[i] > 0:
+                with torch.cuda.device(res[i].device):
+                    ops.check(fast.myfyp_fedavg_stacked_apply(params[i].data_ptr(), res[i].data_ptr(), int(P[i]), int(n), int(ld[i]),
+                                                              mask[off:].ctypes.data, _stream_ptr(res[i].device)), "fedavg_stacked_apply")
+            off += P[i]
 
     def shrink(self, keep) -> None:
         with self.lock:
             self.devices = [self.devices[k] for k in keep]
+            self._stalled = {keep.index(r) for r in self._stalled if r in keep} if self._stalled else set()
+            self._injected = None
+            self.aborted = False
             self.shrinks += 1
 
 
@@ -316,7 +439,7 @@ class RcclMesh(DeviceMesh):
             self._rc(self._lib.rmesh_p2p(self._h, len(ops), kinds, ranks, peers, _ptrs([t.data_ptr() for _, _, _, t in ops]), counts, dt,
                                          _ptrs([_stream_ptr(self.devices[r]) for _, r, _, _ in ops])), "rmesh_p2p")
 
-    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask) -> None:
+    def fedavg_stacked(self, params, bufs, P, n, ld, w, mask, outs=None) -> None:
         w = np.ascontiguousarray(w, dtype=np.float32)
         mask = np.ascontiguousarray(mask, dtype=np.float32)
         Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
@@ -324,7 +447,22 @@ class RcclMesh(DeviceMesh):
         with self.lock:
             self.calls += 1
             self._rc(self._lib.rmesh_fedavg(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in bufs]), Pa, int(n), lda,
-                                            w.ctypes.data, mask.ctypes.data, self._streams()), "rmesh_fedavg")
+                                            w.ctypes.data, mask.ctypes.data, self._streams(),
+                                            None if outs is None else _ptrs([t.data_ptr() for t in outs])), "rmesh_fedavg")
+
+    def fedavg_retry(self, params, bufs, outs, P, n, ld, mask) -> None:
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
+        lda = (ctypes.c_int64 * self.size)(*[int(x) for x in ld])
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_fedavg_retry(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in bufs]),
+                                                  _ptrs([t.data_ptr() for t in outs]), Pa, int(n), lda, mask.ctypes.data, self._streams()),
+                     "rmesh_fedavg_retry")
+
+    def inject_error(self, rank: int) -> None:
+        with self.lock:
+            self._rc(self._lib.rmesh_debug_inject(self._h, int(rank)), "rmesh_debug_inject")
 
     def check(self) -> None:
         with self.lock:
@@ -338,6 +476,13 @@ class RcclMesh(DeviceMesh):
         arr = (ctypes.c_int * len(keep))(*[int(k) for k in keep])
         with self.lock:
             self._rc(self._lib.rmesh_shrink(self._h, arr, len(keep)), "rmesh_shrink")
+            self.devices = [self.devices[k] for k in keep]
+            self.shrinks += 1
+
+    def rebuild(self, keep) -> None:
+        arr = (ctypes.c_int * len(keep))(*[int(k) for k in keep])
+        with self.lock:
+            self._rc(self._lib.rmesh_rebuild(self._h, arr, len(keep)), "rmesh_rebuild")
             self.devices = [self.devices[k] for k in keep]
             self.shrinks += 1
 

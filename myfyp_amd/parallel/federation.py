@@ -322,6 +322,7 @@ class Federation:
         # mesh ranks still taking part (original numbering) and the round-robin placement cursor
         self.devices: List[torch.device] = [device]
         self.mesh = None
+        self.mesh_guard = None  # parallel/mesh_guard.py (mesh runs)
         self.mesh_members: List[int] = [0]
         self._placed = 0
         self._mesh_scratch: Dict[Tuple[int, int], torch.Tensor] = {}
@@ -403,19 +404,25 @@ class Federation:
             torch.cuda.set_device(devs[0])
         inst = cls._instance = cls(0, 1, 0, devs[0], None)
         inst.devices = list(devs)
+        physical = all(d.type == "cuda" for d in devs) and len({d.index for d in devs}) == len(devs)
         try:
             inst.mesh = make_mesh(devs, backend)
         except Exception as e:  # noqa: BLE001 — RCCL init on this host failed
-            if backend is not None:
-                raise  # an explicitly requested backend must not be swapped silently
-            # the job still runs on every device, with the host mesh's device-to-device copies in
-            # place of RCCL; the choice is logged and reported (``mesh.kind`` = "host")
+            if backend is not None or (physical and not Settings.MESH_HOST_FALLBACK):
+                # an explicitly requested backend, or distinct physical GPUs, must not be swapped
+                # silently for host copies (a "mesh" number that is not RCCL)
+                raise
+            # opt-in (MESH_HOST_FALLBACK): the job still runs on every device, with the host
+            # mesh's device-to-device copies in place of RCCL; reported as ``mesh.kind`` = "host"
             from myfyp_amd.parallel.device_mesh import HostMesh
 
             logger.warning("rank0", f"RCCL device mesh over {[str(d) for d in devs]} failed ({e}); using the host mesh")
             print(f"[federation] RCCL device mesh failed ({e}); falling back to the host mesh", file=sys.stderr, flush=True)
             inst.mesh = HostMesh(devs)
         inst.mesh_members = list(range(len(devs)))
+        from myfyp_amd.parallel.mesh_guard import MeshGuard
+
+        inst.mesh_guard = MeshGuard(inst)
         logger.info("rank0", f"device mesh over {[str(d) for d in devs]} ({inst.mesh.kind})")
         return inst
 
@@ -436,26 +443,69 @@ class Federation:
         """Index of an original mesh rank among the ranks still in the mesh."""
         return self.mesh_members.index(mesh_rank)
 
-    def mesh_scratch(self, mesh_rank: int, numel: int) -> torch.Tensor:
+    def mesh_scratch(self, mesh_rank: int, numel: int, tag: str = "") -> torch.Tensor:
         """fp32 scratch on a mesh rank's device (a rank without live peers still joins a collective)."""
-        key = (mesh_rank, numel)
+        key = (mesh_rank, numel, tag)
         t = self._mesh_scratch.get(key)
         if t is None:
             t = self._mesh_scratch[key] = torch.zeros(numel, dtype=torch.float32, device=self.devices[mesh_rank])
         return t
 
+    def mesh_track(self, kind: str, retry: Optional[Callable[[], None]] = None) -> None:
+        """Register the mesh collective just enqueued with the mesh guard (deadline, async-error
+        poll, retry from retained inputs: ``parallel/mesh_guard.py``)."""
+        g = self.mesh_guard
+        if g is not None:
+            g.track(kind, retry)
+
+    def mesh_confirm(self) -> bool:
+        """Confirm the pending mesh collectives (recovering from a failed one); True if a
+        recovery ran."""
+        g = self.mesh_guard
+        return g.confirm() if g is not None and self.mesh is not None else False
+
+    def mesh_drop_ranks(self, ranks: List[int]) -> None:
+        """Mesh ranks whose device stopped responding: their peers leave the experiment (they
+        are unregistered now, so the current aggregation runs over the others, and stopped in the
+        background: a stop may block on the lost device)."""
+        lost = []
+        with self._lock:
+            for a in list(self.local_order):
+                node = self.local_nodes.get(a)
+                if node is not None and getattr(node.learner, "mesh_rank", 0) in ranks:
+                    lost.append(node)
+        for node in lost:
+            logger.warning("rank0", f"peer {node.addr} sits on a lost device: it leaves the experiment")
+            self.unregister_local(node.addr)
+            threading.Thread(target=node.stop, name=f"stop-{node.addr}", daemon=True).start()
+
     def mesh_leave(self, mesh_rank: int) -> None:
-        """A mesh rank's last peer stopped: rebuild the mesh over the other ranks (abort + init-all
-        over the survivors); it joins no further collective. The round driver calls this between
-        rounds, so no collective is in flight."""
+        """A mesh rank's last peer stopped: rebuild the mesh over the other ranks; it joins no
+        further collective. The mesh is healthy, so the pending collectives are confirmed and
+        every member device is drained first (a collective or apply kernel of the previous round
+        may still be queued: ADVICE r5), then the communicators are destroyed, not aborted, and
+        a fresh init-all runs over the others."""
         if self.mesh is None or mesh_rank not in self.mesh_members or len(self.mesh_members) == 1:
             return
-        keep = [i for i, r in enumerate(self.mesh_members) if r != mesh_rank]
+        self.mesh_confirm()
+        if mesh_rank not in self.mesh_members or len(self.mesh_members) == 1:
+            return
         t0 = time.perf_counter()
-        self.mesh.shrink(keep)
-        self.mesh_members = [self.mesh_members[i] for i in keep]
+        self._mesh_rebuild([r for r in self.mesh_members if r != mesh_rank])
         self.record("mesh_shrink", time.perf_counter() - t0)
         logger.warning("rank0", f"mesh rank {mesh_rank} ({self.devices[mesh_rank]}) has no live peer: mesh rebuilt over {self.mesh_members}")
+
+    def _mesh_rebuild(self, ranks: List[int]) -> None:
+        """Rebuild the healthy mesh over the mesh ranks ``ranks``: pending collectives confirmed,
+        every member device drained, communicators destroyed, init-all over ``ranks``."""
+        self.mesh_confirm()
+        keep = [i for i, r in enumerate(self.mesh_members) if r in ranks]
+        for r in self.mesh_members:
+            d = self.devices[r]
+            if d.type == "cuda":
+                torch.cuda.synchronize(d)
+        self.mesh.rebuild(keep)
+        self.mesh_members = [self.mesh_members[i] for i in keep]
 
     def mesh_ranks_alive(self) -> List[int]:
         """Mesh ranks that still host a live local peer."""
@@ -554,7 +604,15 @@ class Federation:
                     dist.barrier(group=self._pg)
                 dist.destroy_process_group()
         if self.mesh is not None:
-            for d in self.devices:
+            try:
+                self.mesh_confirm()  # the last round's mesh collectives (a failure is recovered)
+                self.mesh.check()
+            except Exception as e:
+                logger.warning(f"rank{self.rank}", f"mesh collectives unconfirmed at shutdown: {e}")
+            if self.mesh_guard is not None:
+                self.mesh_guard.stop()
+            for r in self.mesh_members:
+                d = self.devices[r]
                 if d.type == "cuda":
                     torch.cuda.synchronize(d)
             self.mesh.close()
@@ -583,6 +641,8 @@ class Federation:
         if inst is not None and inst.shm is not None:
             inst.shm.close()
             inst.shm = None
+        if inst is not None and inst.mesh_guard is not None:
+            inst.mesh_guard.stop()
         if inst is not None and inst.mesh is not None:
             try:
                 for d in inst.devices:
@@ -913,7 +973,11 @@ class Federation:
             mark("section:in")
             outer = self._frozen is not None
             if not outer and self.mesh is not None:
-                self.mesh_sync()  # devices whose last peer stopped leave the mesh first
+                # the previous round's mesh collectives are confirmed (a failed one is recovered:
+                # abort, rebuild over the responsive devices, re-run from the retained partials),
+                # then devices whose last peer stopped leave the mesh
+                self.mesh_confirm()
+                self.mesh_sync()
             if not outer:
                 # a confirmation that ended in an agreement gather already agreed on the members
                 # (every member took part in it): no second membership gather right after it

@@ -32,6 +32,8 @@ from typing import Dict, List, Optional, Set, Tuple
 import numpy as np
 import torch
 
+from myfyp_amd.utils.seed import seed_generation
+
 from myfyp_amd.ops import _native
 from myfyp_amd.parallel.pending import Pending, Resolver
 from myfyp_amd.settings import Settings
@@ -228,6 +230,7 @@ class MLPGroup:
         self.resolver = Resolver.shared()
         self._cfg_key: Optional[tuple] = None  # last engine configuration pushed to the native side
         self._seed_ahead: Optional[int] = None  # shuffle key of the next epoch (its gather is already enqueued)
+        self._seed_gen = -1  # utils.seed.seed_generation() the key above was drawn under
         self._opt_key: Optional[tuple] = None
         self._steps_pe: Optional[np.ndarray] = None
         self._active_cache: Dict[tuple, np.ndarray] = {}
@@ -282,6 +285,7 @@ class MLPGroup:
     def invalidate_data(self) -> None:
         with self.lock:
             self._data_version += 1
+            self._seed_ahead = None  # the key drawn ahead belonged to the old data
 
     # ------------------------------------------------------------------ native engine
     def _ensure_engine(self) -> None:
@@ -349,6 +353,11 @@ class MLPGroup:
         lib = _native.load(required=True)
         cap, dev = self.capacity, self.device
         xs, ys, ns, xts, yts, nts = [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap, [0] * cap
+        if self._engine is not None and getattr(self, "_keep", None):
+            # a gather enqueued ahead on the engine's prep stream may still read the tensors bound
+            # so far (the torch allocator does not track that stream): drain it before dropping them
+            _native.check(lib.mlp_engine_drain_prep(self._engine), "drain_prep")
+        self._seed_ahead = None
         self._keep = []
         for slot, h in self.handles.items():
             (x, y), (xt, yt) = h.device_split(True), h.device_split(False)
@@ -494,7 +503,11 @@ class MLPGroup:
                         self._seed_ahead = None
                     else:
                         # keys are drawn one epoch ahead: the engine enqueues the next epoch's gather
-                        # right after launching this one (same keys, same order as drawing each in turn)
+                        # right after launching this one (same keys, same order as drawing each in
+                        # turn within one RNG stream; a set_seed() in between drops the key ahead)
+                        gen = seed_generation()
+                        if gen != self._seed_gen:
+                            self._seed_ahead, self._seed_gen = None, gen
                         seed = self._seed_ahead if self._seed_ahead is not None else random.getrandbits(64)
                         self._seed_ahead = random.getrandbits(64)
                         _native.check(fast.mlp_engine_set_epoch_seed(self._engine, seed), "set_epoch_seed")
@@ -549,6 +562,14 @@ class MLPGroup:
 
             logger.warning("mlp-engine", "persistent epoch: a gang gave up (workgroup not resident) and was re-run by the retry launch")
         return loss, correct, conf
+
+    def epoch_launch_kind(self) -> str:
+        """How a local epoch reaches the GPU: the persistent epoch kernel is launched directly
+        (engine.hip ``direct_epoch_launch``; ``MYFYP_EPOCH_GRAPH=1`` replays its captured graph
+        instead); the step path replays a captured hipGraph."""
+        if self.uses_persistent() and os.environ.get("MYFYP_EPOCH_GRAPH", "0") in ("", "0"):
+            return "persistent-direct"
+        return ("persistent-" if self.uses_persistent() else "steps-") + "hipgraph"
 
     def f32_variant(self) -> int:
         """Gang layout the fp32 persistent epoch uses (1 owners + heads, 2 owners only)."""

@@ -117,6 +117,7 @@ def _mesh_initial_model(fed: Federation, learners: Dict[str, Any], initiator: st
             else:
                 flats.append(torch.empty(numel, dtype=dt, device=dev))
         fed.mesh.broadcast_(flats, root)
+        fed.mesh_track("broadcast")
         for r, flat in zip(fed.mesh_members, flats):
             for i, part in zip(idx, torch.split(flat, [src[i].numel() for i in idx])):
                 per_rank[r][i] = part.view_as(src[i])
@@ -360,7 +361,14 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
 def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
     """FedAvg over a device mesh. Stacked engine groups (one per mesh rank): ONE native call —
     per device reduce launch, one grouped RCCL all-reduce, per device apply launch
-    (``rmesh_fedavg``). Other learners: per device partial sums, one mesh all-reduce, unpack."""
+    (``rmesh_fedavg``). Other learners: per device partial sums, one mesh all-reduce, unpack.
+
+    The all-reduce is out of place, so every device keeps its local partial sum [Σ w x | Σ w]. The
+    mesh guard (``parallel/mesh_guard.py``) confirms the collective at the next weights section;
+    if it failed (asynchronous RCCL error, or a device that never completed it within
+    ``COLLECTIVE_TIMEOUT``), the mesh is rebuilt over the responsive devices and ``retry`` re-runs
+    the all-reduce of the retained partial sums over them and re-applies: the survivors' average
+    of the round, i.e. the models that arrived (``aggregator.py:177-208``)."""
     wt_of = dict(zip(addrs, weights))
     ranks = _by_mesh_rank(fed, addrs, learners)
     groups = {r: {id(lr._engine.group): lr._engine.group for _, lr in v if getattr(lr, "_engine", None) is not None} for r, v in ranks.items()}
@@ -369,7 +377,7 @@ def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
     numels = {next(iter(g.values())).numel for g in groups.values() if g}
     if stacked and len(numels) == 1 and all(next(iter(g.values())).params.is_cuda for g in groups.values() if g):
         n = numels.pop()
-        params, bufs, P, ld, w, mask = [], [], [], [], [], []
+        per: Dict[int, tuple] = {}  # mesh rank -> (params, partial, result, P, ld, w, mask)
         for r in fed.mesh_members:
             if ranks[r]:
                 g = next(iter(groups[r].values()))
@@ -379,24 +387,30 @@ def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
                     wr[lr._engine.slot] = wt_of[a]
                     mr[lr._engine.slot] = 1.0
                 with on_device(g.device):
-                    bufs.append(g.fedavg_buffer())
-                params.append(g.params)
-                P.append(g.capacity)
-                ld.append(g.S)
-                w.append(wr)
-                mask.append(mr)
+                    out = getattr(g, "_mesh_out", None)
+                    if out is None or out.numel() != n + 1:
+                        out = g._mesh_out = torch.empty(n + 1, dtype=torch.float32, device=g.device)
+                    per[r] = (g.params, g.fedavg_buffer(), out, g.capacity, g.S, wr, mr)
             else:  # no live peer on this device (yet in the mesh): contributes zeros
                 scratch = fed.mesh_scratch(r, n + 1)
-                params.append(scratch)
-                bufs.append(scratch)
-                P.append(0)
-                ld.append(n)
-        fed.mesh.fedavg_stacked(params, bufs, P, n, ld, np.concatenate(w) if w else np.zeros(0, np.float32),
-                                np.concatenate(mask) if mask else np.zeros(0, np.float32))
+                per[r] = (scratch, scratch, fed.mesh_scratch(r, n + 1, "out"), 0, n, np.zeros(0, np.float32), np.zeros(0, np.float32))
+
+        def cols(k: int, rs) -> list:
+            return [per[r][k] for r in rs]
+
+        rs = list(fed.mesh_members)
+        fed.mesh.fedavg_stacked(cols(0, rs), cols(1, rs), cols(3, rs), n, cols(4, rs), np.concatenate(cols(5, rs)),
+                                np.concatenate(cols(6, rs)), outs=cols(2, rs))
+
+        def retry() -> None:  # over the current (rebuilt) mesh: the survivors' retained partials
+            live = [r for r in fed.mesh_members if r in per]
+            fed.mesh.fedavg_retry(cols(0, live), cols(1, live), cols(2, live), cols(3, live), n, cols(4, live), np.concatenate(cols(6, live)))
+
+        fed.mesh_track("fedavg", retry)
         return float(sum(weights))
     ref = _pack(learners[0])
     n = ref.numel()
-    accs = []
+    accs: Dict[int, torch.Tensor] = {}
     for r in fed.mesh_members:
         dev = fed.devices[r]
         with on_device(dev):
@@ -405,13 +419,24 @@ def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
                 if wt_of[a] > 0:
                     acc[:n].add_(_pack(lr), alpha=wt_of[a])
             acc[n] = float(sum(wt_of[a] for a, _ in ranks[r]))
-        accs.append(acc)
-    fed.mesh.all_reduce_(accs)
-    for r, acc in zip(fed.mesh_members, accs):
-        with on_device(fed.devices[r]):
-            avg = acc[:n] / acc[n].clamp_min(1e-12)
-            for _, lr in ranks[r]:
-                _unpack_into(lr, avg)
+        accs[r] = acc  # retained partial sum (the all-reduce below works on a copy)
+
+    def reduce_unpack() -> None:
+        live = [r for r in fed.mesh_members if r in accs]
+        outs = []
+        for r in live:
+            with on_device(fed.devices[r]):
+                outs.append(accs[r].clone())
+        fed.mesh.all_reduce_(outs)
+        for r, out in zip(live, outs):
+            with on_device(fed.devices[r]):
+                avg = out[:n] / out[n].clamp_min(1e-12)
+                for a, lr in ranks[r]:
+                    if a in fed.local_nodes:
+                        _unpack_into(lr, avg)
+
+    reduce_unpack()
+    fed.mesh_track("fedavg", reduce_unpack)
     return float(sum(weights))
 
 
@@ -556,6 +581,7 @@ def _mesh_neighbors(fed: Federation, peers, index, w, local, learners) -> None:
         ops_.append(("recv", fed.mesh_position(rd), fed.mesh_position(rank[b]), buf))
     if ops_:
         fed.mesh.p2p_(ops_)
+        fed.mesh_track("p2p")
     mixed = {}
     for a in local:
         i = index[a]
@@ -621,6 +647,7 @@ def _mesh_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggre
                 ops.scaffold_reduce(buf, dys, dcs, ws)
         bufs.append(buf)
     fed.mesh.all_reduce_(bufs)
+    fed.mesh_track("scaffold all_reduce")
     cdev = fed.__dict__.setdefault("_mesh_c", {})
     for r, buf in zip(fed.mesh_members, bufs):
         if not ranks[r]:
@@ -717,6 +744,7 @@ def _mesh_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None
             sends.append(s_)
             recvs.append(torch.empty(len(counts) * kmax, n, dtype=torch.float32, device=dev))
     fed.mesh.all_gather_(recvs, sends)
+    fed.mesh_track("median all_gather")
     for r, recv in zip(fed.mesh_members, recvs):
         if not ranks[r]:
             continue

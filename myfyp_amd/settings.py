@@ -132,6 +132,9 @@ class Settings:
     MESH_DEVICES: int = 1
     MESH_BACKEND: Optional[str] = None
     MESH_VIRTUAL: bool = False
+    # an RCCL mesh over distinct physical GPUs that fails to form raises; True swaps in the host
+    # mesh (device-to-device copies), reported as mesh.kind == "host" (benchmarks refuse it)
+    MESH_HOST_FALLBACK: bool = False
     # Node.start() prepares the fused engine (epoch-graph capture and upload, code-object load; no
     # training work) so round 0 does not pay it — like building a compiled model at load time
     ENGINE_PREWARM: bool = True
@@ -232,6 +235,7 @@ class Settings:
             "MESH_DEVICES": "MESH_DEVICES",
             "MESH_BACKEND": "MESH_BACKEND",
             "MESH_VIRTUAL": "MESH_VIRTUAL",
+            "MESH_HOST_FALLBACK": "MESH_HOST_FALLBACK",
         }
     )
 

@@ -168,3 +168,34 @@ def test_yaml_example_with_fyp_model_and_compression():
     finally:
         Settings.USE_FUSED_KERNELS = saved
         Federation.reset()
+
+
+def test_decode_refuses_bombs_and_bad_shapes():
+    """peer-supplied compressed payloads are bounded by the receiving model — a zlib
+    bomb, a tensor shape the model does not have, and out-of-range or unsorted top-k indices are
+    refused before anything large is allocated."""
+    import pickle
+    import zlib
+
+    from myfyp_amd.learning import compression as C
+    from myfyp_amd.learning.frameworks.p2pfl_model import safe_loads
+
+    shapes = [(4, 3), (3,)]
+    params = [np.arange(12, dtype=np.float32).reshape(4, 3), np.ones(3, np.float32)]
+    good = C.encode(params, {}, C.validate({"topk": {"k": 0.5}, "zlib": {}}))
+    out, _ = C.decode(good, safe_loads, shapes)
+    assert [o.shape for o in out] == shapes
+    bomb = C.MAGIC + zlib.compress(b"\0" * (64 << 20), 9)  # 64 MiB of zeros in ~64 KB
+    with pytest.raises(ValueError, match="inflates"):
+        C.decode(bomb, safe_loads, shapes)
+    huge = pickle.dumps({"params": [{"shape": np.array([1 << 20, 1 << 20]), "dtype": "float32", "idx": np.array([0]), "v": np.ones(1, np.float32)}],
+                         "additional_info": {}, "compression": ["topk"]})
+    with pytest.raises(ValueError):
+        C.decode(huge, safe_loads, [(4, 3)])
+    with pytest.raises(ValueError, match="exceeds"):
+        C.decode(huge, safe_loads)  # no model shapes: the global element bound still holds
+    for idx in (np.array([0, 12]), np.array([5, 2]), np.array([-1, 3])):
+        bad = pickle.dumps({"params": [{"shape": np.array([4, 3]), "dtype": "float32", "idx": idx, "v": np.ones(2, np.float32)}],
+                            "additional_info": {}, "compression": ["topk"]})
+        with pytest.raises(ValueError, match="indices"):
+            C.decode(bad, safe_loads, [(4, 3)])

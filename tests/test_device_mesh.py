@@ -240,3 +240,151 @@ def test_mesh_falls_back_to_host_when_rccl_init_fails(monkeypatch):
             Federation._init_mesh([torch.device("cpu"), torch.device("cpu")], "rccl")
     finally:
         Federation.reset()
+
+
+# ---------------------------------------------------------------------------------------------
+# mesh guard (parallel/mesh_guard.py): deadline, async-error poll, abort, rebuild, aggregate what
+# arrived (reference: aggregator.py:177-208, wait_agg_models_stage.py:40-67)
+# ---------------------------------------------------------------------------------------------
+@pytest.fixture
+def short_timeouts():
+    saved = (Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT, Settings.COLLECTIVE_FAILOVER)
+    Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT, Settings.COLLECTIVE_FAILOVER = 0.3, 0.2, True
+    yield
+    Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT, Settings.COLLECTIVE_FAILOVER = saved
+
+
+def _stacked_fedavg(fed, params, P, n, ld, w, mask):
+    """The stacked path of weights_plane._mesh_mean on explicit rows (out of place + guarded)."""
+    bufs = [torch.zeros(n + 1) for _ in P]
+    outs = [torch.zeros(n + 1) for _ in P]
+    offs = np.concatenate([[0], np.cumsum(P)])
+    fed.mesh.fedavg_stacked(params, bufs, P, n, ld, w, mask, outs=outs)
+
+    def retry():
+        live = list(fed.mesh_members)
+        fed.mesh.fedavg_retry([params[r] for r in live], [bufs[r] for r in live], [outs[r] for r in live], [P[r] for r in live], n,
+                              [ld[r] for r in live], np.concatenate([mask[offs[r] : offs[r + 1]] for r in live]))
+
+    fed.mesh_track("fedavg", retry)
+
+
+def _want(rows, w, members_rows):
+    sel = np.concatenate(members_rows)
+    return (w[sel, None] * rows[sel]).sum(0) / w[sel].sum()
+
+
+def test_mesh_guard_stalled_member_aggregates_survivors(short_timeouts):
+    """A mesh member that never completes the FedAvg: the deadline expires, the watchdog aborts the
+    mesh, the confirmation probes the devices, rebuilds over the two that answer, drops the third,
+    and re-runs the all-reduce from the survivors' retained partial sums: their rows end at the
+    survivors' weighted average (the models that arrived), not the three-member one."""
+    rng = np.random.default_rng(3)
+    Federation.reset()
+    try:
+        fed = Federation._init_mesh([torch.device("cpu")] * 3, "host")
+        n, ld, P = 9, 12, [2, 1, 2]
+        params = [torch.from_numpy(rng.standard_normal((p, ld)).astype(np.float32)) for p in P]
+        rows = np.concatenate([p.numpy()[:, :n] for p in params])
+        w = np.array([1.0, 2.0, 3.0, 4.0, 5.0], dtype=np.float32)
+        mask = np.ones(5, dtype=np.float32)
+        fed.mesh.stall(2)  # device 2 hangs: its completion markers and probes never fire
+        _stacked_fedavg(fed, params, P, n, [ld] * 3, w, mask)
+        time.sleep(0.5)  # past the deadline: the watchdog aborts the mesh
+        assert fed.mesh_guard.aborted and fed.mesh.aborted
+        assert fed.mesh_confirm() is True
+        assert fed.mesh_members == [0, 1] and fed.mesh_guard.lost == [2] and fed.mesh_guard.recoveries == 1
+        want = _want(rows, w, [np.arange(0, 2), np.arange(2, 3)])
+        got = np.concatenate([params[0].numpy()[:, :n], params[1].numpy()[:, :n]])
+        np.testing.assert_allclose(got, np.broadcast_to(want, got.shape), rtol=1e-5, atol=1e-6)
+        fed.mesh.check()  # healthy again
+        assert fed.mesh_confirm() is False  # the retry's own collective confirmed
+    finally:
+        Federation.reset()
+
+
+def test_mesh_guard_async_error_reinit_keeps_every_member(short_timeouts):
+    """An asynchronous error reported by the mesh (fault hook) on a collective that did complete:
+    abort, every device answers the probe, the mesh is re-initialised over all of them and the
+    FedAvg re-run from the retained partials gives exactly the undisturbed result."""
+    rng = np.random.default_rng(4)
+    Federation.reset()
+    try:
+        fed = Federation._init_mesh([torch.device("cpu")] * 2, "host")
+        n, ld, P = 7, 8, [2, 2]
+        params = [torch.from_numpy(rng.standard_normal((p, ld)).astype(np.float32)) for p in P]
+        ref = [p.clone() for p in params]
+        w = np.array([1.0, 0.0, 3.0, 2.0], dtype=np.float32)
+        mask = np.array([1, 1, 0, 1], dtype=np.float32)
+        _stacked_fedavg(fed, ref, P, n, [ld] * 2, w, mask)
+        assert fed.mesh_confirm() is False
+        _stacked_fedavg(fed, params, P, n, [ld] * 2, w, mask)
+        fed.mesh.inject_error(1)
+        assert fed.mesh_confirm() is True
+        assert fed.mesh_members == [0, 1] and fed.mesh_guard.lost == [] and fed.mesh.shrinks == 1
+        for a, b in zip(params, ref):
+            assert torch.equal(a, b)
+    finally:
+        Federation.reset()
+
+
+def test_mesh_workflow_survives_a_hung_device(data, short_timeouts):
+    """3 peers on a 3-device CPU mesh; device 2 hangs in round 1. Its peer leaves, the survivors
+    finish every round over the rebuilt two-device mesh and agree."""
+    from myfyp_amd.fault_injection import StageFault
+
+    Settings.BATCH_SIZE = 16
+    Settings.TRAIN_SET_SIZE = 3
+    Federation.reset()
+    fed = Federation.init(devices=3)
+    parts = data.generate_partitions(3, RandomIIDPartitionStrategy)
+    exp = f"meshhang-{time.time_ns()}"
+    nodes = [Node(TorchModel(MLP(seed=i)), parts[i], address=f"mh-{i}-{time.time_ns()}", protocol=CollectiveCommunicationProtocol, exp_name=exp)
+             for i in range(3)]
+    for nd in nodes:
+        nd.start()
+    try:
+        fed.finalize()
+        assert [nd.learner.mesh_rank for nd in nodes] == [0, 1, 2]
+        StageFault(nodes[2], "TrainStage", lambda n: fed.mesh.stall(2), round=1)
+        _run(nodes[:2], 4)
+        assert fed.mesh_members == [0, 1] and fed.mesh_guard.recoveries >= 1 and fed.mesh_guard.lost == [2]
+        assert nodes[2].addr not in fed.local_nodes
+        assert all(nd.learning_workflow.history.count("RoundFinishedStage") == 4 for nd in nodes[:2])
+        check_equal_models(nodes[:2], atol=1e-5)
+    finally:
+        for nd in nodes:
+            nd.stop()
+        Federation.reset()
+
+
+def test_bench_refuses_a_host_mesh_on_physical_gpus():
+    """``--gpus N`` over physical GPUs must run on the RCCL mesh: a host-copy mesh is refused (a
+    virtual rehearsal is not)."""
+    from types import SimpleNamespace
+
+    from myfyp_amd.utils import launch
+
+    fed = SimpleNamespace(mesh=SimpleNamespace(kind="host"), mesh_size=2)
+    with pytest.raises(SystemExit, match="RCCL"):
+        launch.check_mesh(fed, 2, virtual=False)
+    launch.check_mesh(fed, 2, virtual=True)
+    launch.check_mesh(SimpleNamespace(mesh=SimpleNamespace(kind="rccl"), mesh_size=2), 2, virtual=False)
+    with pytest.raises(SystemExit):
+        launch.check_mesh(SimpleNamespace(mesh=None, mesh_size=1), 2, virtual=False)
+
+
+def test_torchrun_defaults_to_one_process_per_gpu(monkeypatch):
+    """Under torchrun ``--launch auto`` is one process per GPU; one process started
+    with ``--gpus N`` drives a mesh."""
+    from myfyp_amd.utils import launch
+
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "2")
+    assert launch.plan_launch(4, "auto") == "ranks"
+    assert launch.plan_launch(4, "mesh", mesh_virtual=True) == "park"
+    monkeypatch.setenv("RANK", "0")
+    assert launch.plan_launch(4, "mesh", mesh_virtual=True) == "mesh"
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert launch.plan_launch(3, "auto", mesh_virtual=True) == "mesh"
+    assert launch.plan_launch(1, "auto") == "single"

@@ -109,7 +109,7 @@ def test_rccl_mesh_fedavg_bit_equal_to_local_kernel(P):
         m.close()
 
 
-def _mesh_run(devices, backend, n=4, rounds=3, virtual=False):
+def _mesh_run(devices, backend, n=4, rounds=3, virtual=False, aggregator=FedAvg):
     from myfyp_amd.utils.seed import set_seed
 
     Settings.BATCH_SIZE = 64
@@ -122,7 +122,7 @@ def _mesh_run(devices, backend, n=4, rounds=3, virtual=False):
     fed = Federation.init(devices=devices, mesh_backend=backend) if devices is not None else Federation.init()
     parts = synthetic_mnist(8000, 800, seed=5).generate_partitions(n, RandomIIDPartitionStrategy)
     exp = f"mg-{backend}-{time.time_ns()}"
-    nodes = [Node(TorchModel(MLP(seed=i)), parts[i], address=f"mg-{i}-{time.time_ns()}", aggregator=FedAvg(), protocol=CollectiveCommunicationProtocol,
+    nodes = [Node(TorchModel(MLP(seed=i)), parts[i], address=f"mg-{i}-{time.time_ns()}", aggregator=aggregator(), protocol=CollectiveCommunicationProtocol,
                   exp_name=exp) for i in range(n)]
     try:
         for nd in nodes:
@@ -154,6 +154,27 @@ def test_mesh_workflow_rccl_g1_matches_single_group():
     assert min(final) > 0.75, final
     _, _, solo_params, _, _ = _mesh_run(None, None)
     assert torch.equal(mesh_params, solo_params), (mesh_params - solo_params).abs().max()
+
+
+@pytest.mark.parametrize("agg", ["scaffold", "fedmedian", "fedprox"])
+def test_mesh_workflow_rccl_g1_aggregators_match_single_group(agg):
+    """the mesh variants of SCAFFOLD (``_mesh_scaffold``: packed reduction,
+    one RCCL all-reduce, apply), FedMedian (``_mesh_median``: RCCL all-gather + median kernel) and
+    FedProx (``rmesh_fedavg`` with the proximal term in the fused step) on the one-GPU RCCL mesh,
+    pinned to the same federation without a mesh: 4 fused peers, 3 rounds, the final parameters
+    equal to fp32 reduction-order tolerance, and every peer learns."""
+    from myfyp_amd.learning.aggregators import FedMedian, FedProx, Scaffold
+
+    make = {"scaffold": lambda: Scaffold(global_lr=1.0), "fedmedian": FedMedian, "fedprox": lambda: FedProx(proximal_mu=0.01)}[agg]
+    final, ngroups, mesh_params, calls, _ = _mesh_run(["cuda:0"], "rccl", aggregator=make)
+    assert ngroups == 1 and calls >= 3, calls
+    assert min(final) > 0.75, final
+    _, _, solo_params, _, _ = _mesh_run(None, None, aggregator=make)
+    d = (mesh_params - solo_params).abs()
+    scale = solo_params.abs().mean()
+    # the mesh and the single-group path reduce in different orders: fp32 ulps, amplified by Adam's
+    # sign-sensitivity on near-zero gradients over 3 local epochs (cf. test_device_mesh.py)
+    assert d.mean() < 1e-4 * max(1.0, float(scale)) and d.max() < 0.05, (float(d.mean()), float(d.max()))
 
 
 @pytest.mark.parametrize("g", [2, 4])
@@ -193,3 +214,119 @@ def test_bench_torchrun_mesh_virtual_gpu():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1 and out["config"]["peers_per_gpu"] == 4 and out["value"] > 50, out
+
+
+def _stacked_case(P: int, seed: int):
+    n = 235146
+    S = (n + 63) // 64 * 64
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    base = torch.randn(P, S, generator=g).to(DEV)
+    w = np.arange(1, P + 1, dtype=np.float32) * 11.0
+    mask = np.ones(P, dtype=np.float32)
+    ref = base.clone()
+    lib = _native.load(required=True)
+    _native.check(lib.myfyp_fedavg_stacked_local(ref.data_ptr(), P, n, S, w.ctypes.data, mask.ctypes.data, torch.cuda.current_stream(DEV).cuda_stream),
+                  "fedavg_local")
+    return n, S, base, w, mask, ref
+
+
+def _guarded_fedavg(fed, rows, P, n, S, w, mask):
+    buf = torch.empty(n + 1, dtype=torch.float32, device=DEV)
+    out = torch.empty(n + 1, dtype=torch.float32, device=DEV)
+    fed.mesh.fedavg_stacked([rows], [buf], [P], n, [S], w, mask, outs=[out])
+
+    def retry():
+        fed.mesh.fedavg_retry([rows], [buf], [out], [P], n, [S], mask)
+
+    fed.mesh_track("fedavg", retry)
+    return buf, out
+
+
+def test_rccl_mesh_async_error_recovers_bit_equal():
+    """An asynchronous RCCL error (fault hook: ``rmesh_check`` reports one) after a grouped FedAvg:
+    the round driver's confirmation aborts the mesh, probes the device, re-initialises RCCL and
+    re-runs the all-reduce from the retained partial sums; the rows end bit-equal to
+    ``k_fedavg_local`` over the same rows."""
+    saved = (Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT)
+    Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = 30.0, 10.0
+    Federation.reset()
+    try:
+        fed = Federation.init(devices=["cuda:0"], mesh_backend="rccl")
+        assert fed.mesh.kind == "rccl"
+        P = 8
+        n, S, base, w, mask, ref = _stacked_case(P, 5)
+        rows = base.clone()
+        _guarded_fedavg(fed, rows, P, n, S, w, mask)
+        fed.mesh.inject_error(0)
+        assert fed.mesh_confirm() is True
+        torch.cuda.synchronize()
+        assert fed.mesh_guard.recoveries == 1 and fed.mesh_members == [0] and fed.mesh.shrinks == 1
+        assert torch.equal(rows, ref), (rows - ref).abs().max()
+        fed.mesh.check()
+        # the rebuilt mesh keeps working, and a clean round confirms without a recovery
+        rows2 = base.clone()
+        _guarded_fedavg(fed, rows2, P, n, S, w, mask)
+        assert fed.mesh_confirm() is False
+        torch.cuda.synchronize()
+        assert torch.equal(rows2, ref)
+    finally:
+        Federation.reset()
+        Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = saved
+
+
+def test_rccl_mesh_rebuild_right_after_enqueued_fedavg():
+    """a healthy-mesh rebuild (a device's last peer left) issued right after a grouped
+    FedAvg was enqueued drains the devices first and destroys (not aborts) the communicators, so
+    the queued all-reduce and apply complete: the rows are exactly ``k_fedavg_local``'s."""
+    Federation.reset()
+    try:
+        fed = Federation.init(devices=["cuda:0"], mesh_backend="rccl")
+        P = 3
+        n, S, base, w, mask, ref = _stacked_case(P, 9)
+        rows = base.clone()
+        torch.cuda._sleep(50_000_000)  # keep the device busy so the FedAvg is still queued
+        _guarded_fedavg(fed, rows, P, n, S, w, mask)
+        fed._mesh_rebuild([0])
+        assert fed.mesh.shrinks == 1
+        torch.cuda.synchronize()
+        assert torch.equal(rows, ref), (rows - ref).abs().max()
+        fed.mesh.check()
+    finally:
+        Federation.reset()
+
+
+def test_mesh_workflow_rccl_g1_async_error_mid_experiment():
+    """4 fused peers on the one-GPU RCCL mesh; an asynchronous RCCL error is injected in round 1.
+    The next weights section recovers (abort, re-init, retained-partial re-run), every peer
+    finishes every round, and the models agree and learn."""
+    saved = (Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT)
+    Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = 30.0, 10.0
+    Settings.BATCH_SIZE = 64
+    Settings.TRAIN_SET_SIZE = 4
+    Settings.GANG_WINDOW = 5.0
+    MLPGroup.reset_all()
+    Federation.reset()
+    fed = Federation.init(devices=["cuda:0"], mesh_backend="rccl")
+    parts = synthetic_mnist(8000, 800, seed=5).generate_partitions(4, RandomIIDPartitionStrategy)
+    exp = f"mgerr-{time.time_ns()}"
+    nodes = [Node(TorchModel(MLP(seed=i)), parts[i], address=f"mge-{i}-{time.time_ns()}", aggregator=FedAvg(), protocol=CollectiveCommunicationProtocol,
+                  exp_name=exp) for i in range(4)]
+    try:
+        for nd in nodes:
+            nd.start()
+        fed.finalize()
+        # a round hook (the lock-step round driver stays in use): after round 1's FedAvg
+        fed.round_hooks.append(lambda r, f: f.mesh.inject_error(0) if r == 1 else None)
+        nodes[0].set_start_learning(rounds=4, epochs=1)
+        wait_to_finish(nodes, timeout=120)
+        assert fed.mesh_guard.recoveries == 1, fed.mesh_guard.recoveries
+        assert all(nd.learning_workflow.history.count("RoundFinishedStage") == 4 for nd in nodes)
+        check_equal_models(nodes, atol=1e-5)
+        logs = logger.get_global_logs()[exp]
+        assert min(dict(logs[nd.addr]["test_metric"])[4] for nd in nodes) > 0.75
+    finally:
+        for nd in nodes:
+            nd.stop()
+        Federation.reset()
+        MLPGroup.reset_all()
+        Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = saved

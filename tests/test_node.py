@@ -156,10 +156,11 @@ def test_collective_workflow_aggregators(data, aggregator, seed):
         check_equal_models(nodes, atol=1e-5)
         logs = logger.get_global_logs()[exp]
         accs = [dict(logs[nd.addr]["test_metric"]) for nd in nodes]
-        first = max(a[0] for a in accs if 0 in a)  # evaluations of the initial model (trainers)
-        last = max(a[2] for a in accs)  # final evaluation (all peers)
-        # learns — SCAFFOLD included, over six seeds (its control variates are gradients at the
-        # round-start model under Adam, option I: callbacks.py)
+        first = max(a[0] for a in accs if 0 in a)  # best evaluation of the initial model (trainers)
+        last = min(a[2] for a in accs)  # WORST final evaluation: every peer must clear the bar
+        # learns — SCAFFOLD included, over six seeds (correction applied in the update space after
+        # the optimizer step, option-II control variates: torch/callbacks.py; the gradient-space
+        # option-I correction diverged under the reference MLP's Adam)
         assert last > first + 0.1 and last > 0.5, (first, last)
     finally:
         for nd in nodes:
