@@ -18,7 +18,7 @@ __host__ __device__ inline int ks1_of(int D0) { return D0 / 32 + 1; }
 constexpr int LDD = PD2 + 4;   // fp32 row stride of the owner's dH2 tile [B][128]
 constexpr int LDH1 = PD1 + 4;  // fp32 row stride of the head's H1 tile [B][256]
 constexpr int LD16 = 20;       // fp32 row stride of [*][16] tiles
-constexpr int F32_FPP = 96;    // hand-off flag lines per peer (every gang layout shares the flag block)
+constexpr int F32_FPP = 304;   // hand-off flag lines per peer (every gang layout shares the flag block)
 constexpr unsigned DONE_MARK = 1u << 23;   // commit flag value (above every step's t + 1)
 constexpr unsigned RETRY_BASE = 1u << 24;  // hand-off flag base of the retry attempt
 constexpr int ERR_RETRY = 64;              // err layout: [0, 64) first attempt, [64, 128) retry, per peer

@@ -38,7 +38,8 @@ struct MLPPersistF32Bufs {
   float* w2chk;     // debug: owners' W2 replica after the epoch [P][128][256], or null
   int plain_ok;     // fp32 layouts 1 / 3: hand-offs may be stored plain when a gang sits on one XCD (set at launch;
                     // 1 payloads and flags, 2 payloads only, 0 never)
-  int plain;        // plain_ok if this gang does, else 0 (set in the kernel)
+  int plain;        // plain_ok if this gang does, else 0 (set in the kernel); cross-XCD K split: within a group
+  int plain_x;      // hand-offs between the groups of a gang (set in the kernel: plain, or 0 for a cross-XCD K split)
 };
 
 int mlp_plain_pub_mode();  // single-XCD hand-off mode of the persistent kernels (MYFYP_F32_PLAIN_PUB / mlp_set_plain_pub)

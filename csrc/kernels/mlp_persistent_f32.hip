@@ -149,17 +149,44 @@ constexpr int H1W = P32_LL_H1 ? 2 : 1;  // floats per H1 exchange element (value
 // C2 4.6 -> 6.6 us and 14 more VGPR spills)
 constexpr int NCG = 16;  // W1 column groups per peer (D1 / 16)
 constexpr int NH = 8;    // heads per peer (D2 / 16)
-constexpr int KSMAX = 2;
-// KS = K split of the owners: KS owners share a column group, each holding 1/KS of its K steps and
-// publishing a partial H1 slice (heads and the owner pair add the partials in kh order, so every
-// reader gets the same bits). KS = 1 when 8 peers share the GPU (8 x 24 workgroups); KS = 2 when at
-// most 4 do (4 x 40): the per-step owner work (forward, dW1, Adam, X staging) halves.
+constexpr int KSMAX = 8;
+constexpr int KSLAB = KSMAX + 1;  // H1 exchange slabs per peer: KSMAX K-part partials + the reduced slice
+// KS = K split of the owners: KS owners share a column group, each holding 1/KS of its K steps
+// (kpart_begin: as even as 25 K steps allow) and producing a partial H1 slice.
+//
+// Layout 1, KS > 1 — the cross-XCD K split ("XR", xr_of): the gang of ONE peer spans KS XCDs, so
+// that at 1 / 2 / 4 peers per GPU the XCDs an 8-peer GPU would give the other peers work on this
+// one's critical path (the 1 -> 8 curve was flat by construction). Block b runs on XCD
+// x = b mod 8 (round-robin dispatch, checked at run time); the peer's KS XCDs are x = KS·q + xx,
+// xx < KS. XCD xx holds column groups NCG/KS·xx .. + NCG/KS, each with ALL its KS K parts, and
+// XCD 0 also holds the 8 heads: 16 owners + 8 heads on XCD 0, 16 owners on the others. Per step:
+//   owners: partial H1 slice over their K steps -> K-part partials reduced among the KS owners of
+//     the column group INSIDE their XCD (plain stores, L2-resident), in kh order, relu (every owner
+//     of the group holds the same bits) -> K part 0 publishes the reduced slice to the heads
+//     (write-through: the heads sit on XCD 0);
+//   heads: exactly as at KS = 1 (head <-> head partial logits inside XCD 0: plain), dH2 written
+//     through to every XCD's owners.
+// So the step gains two write-through hand-offs and one XCD-local one, and loses KS-fold of the
+// owners' forward, dW1, Adam and next-batch staging (C2 was the step's largest segment).
+// Layout 3 (row heads) keeps the single-launch K split of round 4: KS = 2, 4 peers x 40
+// workgroups, the row heads add the partials.
 __host__ __device__ constexpr int ng_of(int KS) { return NCG * KS; }         // owners per peer
 __host__ __device__ constexpr int roles_of(int KS) { return NCG * KS + NH; }  // workgroups per peer
-__host__ __device__ constexpr int ppl_of(int KS) { return KS == 1 ? 8 : 4; }  // peers per launch
-constexpr int F_H1 = 0, F_PL = NCG * KSMAX, F_DH2 = NCG * KSMAX + NH, F_DONE = NCG * KSMAX + 2 * NH;
+__host__ __device__ constexpr bool xr_of(int KS, bool RH) { return KS > 1 && !RH; }
+__host__ __device__ constexpr int ppl_of(int KS, bool RH = false) { return RH ? (KS == 1 ? 8 : 4) : 8 / KS; }  // peers per launch
+// blocks of one launch: XR / KS = 1 layout 1 use 8 XCD columns x 24 (blocks of an XCD beyond its
+// roles exit at once); layout 3 one block per role
+__host__ __device__ constexpr int grid_of(int KS, bool RH, int nr) { return RH ? ppl_of(KS, true) * nr : 8 * (NCG + NH); }
+// first K step of K part kh (of KS) over ks1 K steps: balanced (25 = 4 + 3·7 at KS = 8)
+__host__ __device__ inline int kpart_begin(int ks1, int KS, int kh) { return (kh * ks1) / KS; }
+constexpr int F_H1 = 0;                       // NCG: reduced H1 slices (KS = 1: the owners' own); layout 3: partials (ng_of)
+constexpr int F_H1P = NCG;                    // NCG * KSMAX: XR K-part partials, index cg * KS + kh
+constexpr int F_PL = NCG + NCG * KSMAX, F_DH2 = F_PL + NH, F_DONE = F_DH2 + NH;
 constexpr int FPP = F32_FPP;  // flag lines per peer (the block every layout shares)
-static_assert(F_DONE + NCG * KSMAX + NH <= F32_FPP, "layout-1 flags fit the shared block");
+// XCC report slots (persist::gang_same_xcd / group_same_xcd): 5 lines = 160 slots, one per role
+constexpr int F_XCC = F32_FPP - 5;
+static_assert(F_DONE + NCG * KSMAX + NH <= F_XCC, "layout-1 flags fit the shared block");
+static_assert(roles_of(KSMAX) <= 5 * 32, "XCC report slots");
 // ---- gang layout 3 (row heads): the heads split the BATCH, not H2's columns. Head r owns batch rows
 // 16r..16r+15 and computes their whole forward tail: H2 rows (every column: no partial-logit
 // exchange between heads), logits, log-softmax + NLL, dlogits and dH2 rows. The owners own W2 (their
@@ -177,10 +204,7 @@ constexpr int F3_DH2 = NCG * KSMAX;       // head r -> owners: dH2 rows 16r..16r
 constexpr int F3_W2 = F3_DH2 + 4;         // owner cg (K part 0) -> heads: W2 columns 16cg.. after its update
 constexpr int F3_HP = F3_W2 + NCG;        // head r -> heads: partial dW3 / db2 / db3 over its rows
 constexpr int F3_DONE = F3_HP + 4;        // commit flags, one per role
-static_assert(F3_DONE + NCG * KSMAX + 4 <= F32_FPP - 2, "layout-3 flags fit the shared block");
-// two flag lines (64 words) at the end of the block: the roles' XCC reports (persist::gang_same_xcd)
-constexpr int F_XCC = F32_FPP - 2;
-static_assert(F_DONE + NCG * KSMAX + NH <= F_XCC, "layout-1 flags leave the XCC lines free");
+static_assert(F3_DONE + NCG * KSMAX + 4 <= F_XCC, "layout-3 flags fit the shared block");
 __host__ __device__ constexpr int nhr_of(int BP) { return BP / 16; }  // row heads per peer
 __host__ __device__ constexpr int roles3_of(int KS, int BP) { return NCG * KS + nhr_of(BP); }
 constexpr int HPW = 16 * PD2 + PD2 + 16;  // floats of one head's partial gradients: dW3 [class][o2] | db2 | db3
@@ -193,9 +217,16 @@ constexpr int KS1_MAX = 25;  // K steps of 32 over D0 + the bias column: D0 <= 7
 // owner reads the other K part's partial of step t at the start of its C phase, while that part may
 // already publish step t + 1's; it cannot reach step t + 2 before every owner has published t + 1
 // (the heads' dH2(t + 1) waits for all of them), so two buffers suffice.
+//
+// XR: slab KSMAX holds the reduced slices (K part 0 of each column group -> heads), also
+// double-buffered: K part 0 writes step t + 2's only after the heads' dH2(t + 1), i.e. after every
+// head has read step t's. An owner reads its siblings' partials of step t right after they appear;
+// a sibling cannot publish step t + 2's before this owner published t + 1's (the heads' dH2(t + 1)
+// needs this group's reduced slice of t + 1), which it does only after reading step t's.
 __device__ __forceinline__ float* h1x_part(const MLPPersistF32Bufs& pb, int p, int kh, int t, int BP) {
-  return pb.h1x + (((int64_t)p * KSMAX + kh) * 2 + (t & 1)) * BP * PD1 * H1W;
+  return pb.h1x + (((int64_t)p * KSLAB + kh) * 2 + (t & 1)) * BP * PD1 * H1W;
 }
+__device__ __forceinline__ float* h1x_red(const MLPPersistF32Bufs& pb, int p, int t, int BP) { return h1x_part(pb, p, KSMAX, t, BP); }
 
 
 // X tile chunk swizzle: within each K step's 32 columns, 16-byte chunk c of row r is stored at chunk
@@ -224,7 +255,7 @@ struct OwnerLds32 {
   int ldt;  // bf16 row stride of the transposed dH1 split tiles [3][16][B]
   size_t x, red, h1, dh1s, w1x, rows, ok, total;
 };
-// K steps of one owner: KH = ceil(KS1 / KS) (the last K-split owner may hold fewer)
+// K steps of one owner, at most: ceil(ks1 / KS) (kpart_begin splits them as evenly as possible)
 __host__ __device__ inline int kh_of(int D0, int KS) { return (ks1_of(D0) + KS - 1) / KS; }
 __host__ __device__ inline OwnerLds32 owner_lds32(int Bpad, int D0, int KS) {
   OwnerLds32 L;
@@ -277,7 +308,7 @@ __host__ __device__ inline HeadLds32 head_lds32(int Bpad) {
 // registers. KS = 1: K steps < 24 three per wave, and K step 24 (wave 0, D0 > 767) in LDS — four
 // register slots per wave would not fit beside the working set of two waves per SIMD. KS = 2: at
 // most 13 K steps per owner, two register slots per wave.
-__host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : 2; }
+__host__ __device__ constexpr int rq_of(int KS) { return KS == 1 ? 3 : KS == 2 ? 2 : 1; }  // KS 4 / 8: <= 7 / 4 K steps, one per wave
 
 // Gang commit: a role stores its state only after EVERY role of the gang finished every
 // step. Without it, heads that passed their last wait could write back while an owner still timed
@@ -307,9 +338,10 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   const int h = lane >> 4, c = lane & 15;
   const int cg = g % NCG, kh = g / NCG;  // column group, K part
   const int D0 = a.D0;
-  const int KH = kh_of(D0, KS);
-  const int s0 = kh * KH;  // first (global) K step of this owner; local K step j is global s0 + j
-  const int KS1 = (ks1_of(D0) - s0 < KH) ? ks1_of(D0) - s0 : KH;  // local K steps of this owner
+  constexpr bool XR = xr_of(KS, RH);  // cross-XCD K split (see the constants above)
+  static_assert(!(XR && P32_LL_H1), "the cross-XCD K split uses flag hand-offs for H1");
+  const int s0 = kpart_begin(ks1_of(D0), KS, kh);  // first (global) K step of this owner; local K step j is global s0 + j
+  const int KS1 = kpart_begin(ks1_of(D0), KS, kh + 1) - s0;  // local K steps of this owner (<= kh_of(D0, KS))
   const int C0 = 32 * s0;  // first global X column of the tile
   const OwnerLds32 L = owner_lds32(BP, D0, KS);
   const int LDX = L.ldx, LDT = L.ldt;
@@ -528,8 +560,37 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     }
     if (g == 0) P32_STAMP(0, t, 1);
 #if !P32_LL_H1
-    persist::publish_p(pb.flags, FPP, p, F_H1 + g, pb.fbase + (unsigned)(t + 1), pb.plain);
+    persist::publish_p(pb.flags, FPP, p, XR ? F_H1P + cg * KS + kh : F_H1 + g, pb.fbase + (unsigned)(t + 1), pb.plain);
 #endif
+    if (XR) {
+      // the column group's KS partials, all on this XCD (plain when the placement check passed):
+      // summed in kh order and relu'd by every owner of the group (same bits in each); K part 0
+      // hands the reduced slice to the heads, written through (they sit on the peer's first XCD)
+      if (!persist::wg_wait(pb.flags, FPP, p, F_H1P + cg * KS, KS, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+      if (tid < BP * 4) {
+        const int b = tid >> 2, c4 = 4 * (tid & 3);
+        float4 u[KS];
+#pragma unroll
+        for (int k2 = 0; k2 < KS; ++k2)
+          u[k2] = k2 == kh ? *reinterpret_cast<const float4*>(sH1c + b * 16 + c4)
+                           : ld_sc1_16(rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 4), (b * PD1 + NCG * cg + c4) * 4);
+        float4 sum = u[0];
+#pragma unroll
+        for (int k2 = 1; k2 < KS; ++k2) {
+          sum.x += u[k2].x;
+          sum.y += u[k2].y;
+          sum.z += u[k2].z;
+          sum.w += u[k2].w;
+        }
+        const float4 r = {fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f), fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)};
+        *reinterpret_cast<float4*>(sH1c + b * 16 + c4) = r;
+        if (kh == 0) persist::pub128(pb.plain_x, h1x_red(pb, p, t, BP), BP * PD1 * 4, (b * PD1 + NCG * cg + c4) * 4, __builtin_bit_cast(u32x4, r));
+      }
+      if (kh == 0)
+        persist::publish_p(pb.flags, FPP, p, F_H1 + cg, pb.fbase + (unsigned)(t + 1), pb.plain_x);
+      else
+        __syncthreads();  // the reduced slice is in sH1c for every wave
+    }
     if (g == 0) P32_STAMP(0, t, 2);
 
     // the previous step's W2-replica update runs while the heads work on this step's H1 (layout 3:
@@ -573,9 +634,9 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     if (!persist::wg_wait(pb.flags, FPP, p, RH ? F3_DH2 : F_DH2, RH ? nhr_of(BP) : NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
 #endif
     if (g == 0) P32_STAMP(0, t, 4);
-    if (KS > 1) {
-      // full H1 slice = the K parts' partials summed in kh order (the heads' order: same bits),
-      // relu; the other parts published theirs before the heads could produce this step's dH2
+    if (KS > 1 && !XR) {
+      // (layout 3) full H1 slice = the K parts' partials summed in kh order (the heads' order: same
+      // bits), relu; the other parts published theirs before the heads could produce this step's dH2
       if (tid < BP * 4) {
         const int b = tid >> 2, c4 = 4 * (tid & 3);
         float4 sum = {0.f, 0.f, 0.f, 0.f};
@@ -852,6 +913,8 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 template <int BP, bool ADAM, bool EXTRA, int KS>
 __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int hd, char* smem, unsigned gen) {
   constexpr int MT = BP / 16;
+  constexpr bool XR = xr_of(KS, false);
+  static_assert(!(XR && P32_LL_H1), "the cross-XCD K split uses flag hand-offs for H1");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, c = lane & 15;
@@ -995,14 +1058,16 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       }
     }
 #else
-    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, ng_of(KS), pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+    // XR: the owners reduced the K parts; the heads read one slice per column group, as at KS = 1
+    constexpr int KSR = XR ? 1 : KS;
+    if (!persist::wg_wait(pb.flags, FPP, p, F_H1, XR ? NCG : ng_of(KS), pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
     if (hd == 0) P32_STAMP(1, t, 1);
     {
       // every partial's loads issued before any is consumed (one L2 round trip, not KS)
-      float4 u[KS][BP / 8];
+      float4 u[KSR][BP / 8];
 #pragma unroll
-      for (int k2 = 0; k2 < KS; ++k2) {
-        const __amdgpu_buffer_rsrc_t r = rsrc_of(h1x_part(pb, p, k2, t, BP), BP * PD1 * 4);
+      for (int k2 = 0; k2 < KSR; ++k2) {
+        const __amdgpu_buffer_rsrc_t r = rsrc_of(XR ? h1x_red(pb, p, t, BP) : h1x_part(pb, p, k2, t, BP), BP * PD1 * 4);
 #pragma unroll
         for (int k = 0; k < BP / 8; ++k) u[k2][k] = ld_sc1_16(r, (tv + NT * k) * 16);  // BP x 256 fp32 = BP*64 chunks
       }
@@ -1010,13 +1075,13 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       for (int k = 0; k < BP / 8; ++k) {
         float4 v = u[0][k];
 #pragma unroll
-        for (int k2 = 1; k2 < KS; ++k2) {
+        for (int k2 = 1; k2 < KSR; ++k2) {
           v.x += u[k2][k].x;
           v.y += u[k2][k].y;
           v.z += u[k2][k].z;
           v.w += u[k2][k].w;
         }
-        if (KS > 1) v = float4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        if (KSR > 1) v = float4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
         const int e = tv + NT * k;
         *reinterpret_cast<float4*>(sH1 + (e >> 6) * LDH1 + 4 * (e & 63)) = v;
       }
@@ -1179,16 +1244,16 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         const float v = sH2[b * LD16 + c] > 0.f ? acc[i] : 0.f;
         sDH2[b * LD16 + c] = v;
 #if P32_LL_DH2
-        persist::ll_st1p(pb.plain, dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
+        persist::ll_st1p(pb.plain_x, dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
 #else
-        persist::pub32(pb.plain, dst + b * PD2 + 16 * hd + c, v);
+        persist::pub32(pb.plain_x, dst + b * PD2 + 16 * hd + c, v);  // (XR: to every XCD's owners)
 #endif
       }
     }
 #if P32_LL_DH2
     lds_barrier();  // sDH2 for the off-path updates (the LL stores need no drain or flag)
 #else
-    persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain);
+    persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain_x);
 #endif
     if (hd == 0) P32_STAMP(1, t, 7);
 
@@ -1630,10 +1695,26 @@ __device__ void headr32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
 template <int BP, bool ADAM, bool EXTRA, int KS, bool RH = false>
 __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPersistF32Bufs pb, int p_base, int attempt) {
   extern __shared__ __attribute__((aligned(16))) char smem_p32[];
-  constexpr int PPL = ppl_of(KS);
+  constexpr int PPL = ppl_of(KS, RH);
+  constexpr bool XR = xr_of(KS, RH);
   const int b = blockIdx.x;
-  const int p = p_base + b % PPL;
-  const int role = b / PPL;
+  int p, role;
+  if (!RH) {
+    // layout 1: block b runs on XCD x = b mod 8 (round-robin dispatch) as its i = b / 8-th block.
+    // The peer owns the KS XCDs x = KS·q + xx; on XCD xx: column groups (NCG / KS)·xx + i / KS,
+    // K part i mod KS (i < 16), and on xx = 0 the heads (i = 16..23). KS = 1: peer x, role i.
+    const int x = b & 7, i = b >> 3, xx = x % KS;
+    p = p_base + x / KS;
+    if (i < NCG)
+      role = (NCG / KS) * xx + i / KS + NCG * (i % KS);
+    else if (xx == 0)
+      role = ng_of(KS) + (i - NCG);
+    else
+      return;  // XCDs after a peer's first hold owners only
+  } else {
+    p = p_base + b % PPL;
+    role = b / PPL;
+  }
   if (p >= a.P) return;
   const int4 ctl = a.ctl[p];
   if (!(ctl.x & 1) || ctl.y <= 0) return;
@@ -1654,13 +1735,25 @@ __global__ __launch_bounds__(NT) void mlp_persistent_f32_epoch(MLPArgs a, MLPPer
   if (role == 0 && !attempt) P32_ESTAMP(0);
   // hand-off payloads stay in the XCD's L2 when the whole gang runs on one XCD (KS = 1: blocks
   // b = p mod 8 under round-robin dispatch): +4-7 % rounds/s (profiles/r5_plain). 100 us bound.
-  {
+  if constexpr (XR) {
+    // hand-offs inside a group (a column group's K parts; the heads) stay in the XCD's L2 when the
+    // group was seen on one XCD; everything between groups is written through (plain_x = 0)
+    const bool owner = role < ng_of(KS);
+    const int first = owner ? role % NCG : ng_of(KS), stride = owner ? NCG : 1, n = owner ? KS : NH;
+    pb.plain = pb.plain_ok && persist::group_same_xcd(persist::flag_at(pb.flags, FPP, p, F_XCC), role, first, stride, n, pb.fbase ? 0x200u : 0x100u,
+                                                      reinterpret_cast<int*>(smem_p32), 10000ull)
+                   ? pb.plain_ok
+                   : 0;
+    pb.plain_x = 0;
+    if (role == 0 && threadIdx.x == 0 && p < 64) g_plain_seen[p] = pb.plain;
+  } else {
     constexpr int NR = RH ? roles3_of(KS, BP) : roles_of(KS);
     static_assert(NR <= 2 * persist::FLAG_LINE, "XCC report slots");
     pb.plain = pb.plain_ok && persist::gang_same_xcd(persist::flag_at(pb.flags, FPP, p, F_XCC), role, NR, pb.fbase ? 0x200u : 0x100u,
                                                      reinterpret_cast<int*>(smem_p32), 10000ull)
                    ? pb.plain_ok
                    : 0;
+    pb.plain_x = pb.plain;
     if (role == 0 && threadIdx.x == 0 && p < 64) g_plain_seen[p] = pb.plain;
   }
   if (role < ng_of(KS))
@@ -1863,15 +1956,16 @@ int f32_variant(const MLPArgs& a) {
   return v;
 }
 
+bool ks_valid(int ks) { return ks == 1 || ks == 2 || ks == 4 || ks == 8; }
 int f32_ks_wanted(const MLPArgs& a) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("MYFYP_F32_KS");
-    env = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+    env = (e && ks_valid(atoi(e))) ? atoi(e) : 0;
   }
-  if (env) return env;
-  if (a.f32_ks == 1 || a.f32_ks == 2) return a.f32_ks;  // the engine's choice
-  return 1;  // single-XCD gangs (plain hand-offs) beat K split 2 at every peer count (profiles/r5_ksab)
+  int ks = env ? env : (ks_valid(a.f32_ks) ? a.f32_ks : 1);  // the engine's choice (by peers per launch)
+  if (ks > 2 && a.Bpad != 64) ks = 2;  // K splits 4 / 8 are instantiated for the 64-row batch tile only
+  return ks;
 }
 
 size_t persistent_f32_lds_ks(const MLPArgs& a, int KS, bool rh = false) {
@@ -1904,7 +1998,7 @@ hipError_t prepare_f32_bp(int lds) {
 }
 template <int BP, int KS, bool RH = false>
 void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, int p_base, size_t lds, int attempt) {
-  const dim3 grid(ppl_of(KS) * (RH ? roles3_of(KS, BP) : roles_of(KS))), block(NT);
+  const dim3 grid(grid_of(KS, RH, RH ? roles3_of(KS, BP) : roles_of(KS))), block(NT);
   const bool adam = a.opt.kind == 0;
   const bool extra = a.anchor != nullptr || a.cg != nullptr;
   if (adam && !extra) hipLaunchKernelGGL((mlp_persistent_f32_epoch<BP, true, false, KS, RH>), grid, block, lds, s, a, pb, p_base, attempt);
@@ -1918,16 +2012,21 @@ void launch_f32_bp(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s,
 int resident_capacity_ks(const MLPArgs& a, int num_cus, int KS, bool rh = false) {
   int per_cu = 0;
   const size_t lds = persistent_f32_lds_ks(a, KS, rh);
-  const void* fn = rh ? (KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2, true>() : f32_fn<32, true, false, 2, true>())
-                                 : (a.Bpad == 64 ? f32_fn<64, true, false, 1, true>() : f32_fn<32, true, false, 1, true>()))
-                      : (KS == 2 ? (a.Bpad == 64 ? f32_fn<64, true, false, 2>() : f32_fn<32, true, false, 2>())
-                                 : (a.Bpad == 64 ? f32_fn<64, true, false, 1>() : f32_fn<32, true, false, 1>()));
+  const bool b64 = a.Bpad == 64;
+  const void* fn = rh ? (KS == 2 ? (b64 ? f32_fn<64, true, false, 2, true>() : f32_fn<32, true, false, 2, true>())
+                                 : (b64 ? f32_fn<64, true, false, 1, true>() : f32_fn<32, true, false, 1, true>()))
+                      : (KS == 8 ? f32_fn<64, true, false, 8>()
+                         : KS == 4 ? f32_fn<64, true, false, 4>()
+                         : KS == 2 ? (b64 ? f32_fn<64, true, false, 2>() : f32_fn<32, true, false, 2>())
+                                   : (b64 ? f32_fn<64, true, false, 1>() : f32_fn<32, true, false, 1>()));
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
   return per_cu * num_cus;
 }
 int roles_for(const MLPArgs& a, int KS) { return f32_variant(a) == 3 ? roles3_of(KS, a.Bpad) : roles_of(KS); }
 
-// The K split layout 1 uses: the wanted one if its launch is co-resident, else 1.
+// The K split layout 1 / 3 uses: the wanted one if its launch is co-resident, else 1. Layout 3 keeps
+// K split <= 2. The cross-XCD K split (layout 1, KS > 1) needs 24 workgroups on a peer's first XCD
+// and 16 on the others: one workgroup per CU fits whenever the launch's 192 blocks do.
 int f32_ks_v1(const MLPArgs& a) {
   static int cus = 0;
   if (cus == 0) {
@@ -1935,9 +2034,15 @@ int f32_ks_v1(const MLPArgs& a) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   }
-  const int want = f32_ks_wanted(a);
+  int want = f32_ks_wanted(a);
   const bool rh = a.f32_variant == 3 && v3_supported(a);
-  if (want == 2 && ppl_of(2) * (rh ? roles3_of(2, a.Bpad) : roles_of(2)) > resident_capacity_ks(a, cus, 2, rh)) return 1;
+  if (rh && want > 2) want = 2;
+  // FedProx / SCAFFOLD terms (EXTRA) at K split 4 / 8: the instantiations with the extra term
+  // drift from torch even when the term is zero (mu = 0: 2 % on W1, scripts/probes/xr_extra_probe2.py,
+  // profiles/r6_xr), while the same launch without it is exact; K split 2 with the term is exact.
+  // Until that is understood, extra-term epochs use K split <= 2.
+  if ((a.anchor != nullptr || a.cg != nullptr) && want > 2) want = 2;
+  if (want > 1 && grid_of(want, rh, rh ? roles3_of(want, a.Bpad) : roles_of(want)) > resident_capacity_ks(a, cus, want, rh)) return 1;
   return want;
 }
 int f32_ks(const MLPArgs& a) { return f32_variant(a) == 2 ? 1 : f32_ks_v1(a); }
@@ -1959,7 +2064,7 @@ bool mlp_persistent_f32_supported(const MLPArgs& a) {
   return persistent_f32_lds_ks(a, 1) <= 160 * 1024;
 }
 
-size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSMAX * 2 * Bpad * PD1 * H1W; }
+size_t mlp_persistent_f32_h1x_floats(int P, int Bpad) { return (size_t)P * KSLAB * 2 * Bpad * PD1 * H1W; }
 size_t mlp_persistent_f32_bytes(int P, int Bpad) {
   // layout 1: H1 partials (fp32) + partial logits and dH2 as LL (value, tag) pairs; layout 2 carves
   // its own regions from the same allocation
@@ -1975,7 +2080,10 @@ int mlp_persistent_f32_x_direct(const MLPArgs& a) { return P32_XDIRECT && f32_va
 int mlp_persistent_f32_x_direct_build() { return P32_XDIRECT; }
 
 // Workgroups one epoch launch needs (its peers' gangs) and how many the device holds at once.
-int mlp_persistent_f32_launch_wgs(const MLPArgs& a) { return f32_variant(a) == 2 ? mlp_f32v2_launch_wgs() : ppl_of(f32_ks(a)) * roles_for(a, f32_ks(a)); }
+int mlp_persistent_f32_launch_wgs(const MLPArgs& a) {
+  const int v = f32_variant(a);
+  return v == 2 ? mlp_f32v2_launch_wgs() : grid_of(f32_ks(a), v == 3, roles_for(a, f32_ks(a)));
+}
 int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
   const int v = f32_variant(a);
   return v == 2 ? mlp_f32v2_resident_capacity(a, num_cus) : resident_capacity_ks(a, num_cus, f32_ks(a), v == 3);
@@ -1984,8 +2092,14 @@ int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
 
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
   hipError_t e;
-  for (int KS = 1; KS <= KSMAX; ++KS) {
+  for (int KS = 1; KS <= KSMAX; KS *= 2) {
     const int lds = (int)persistent_f32_lds_ks(a, KS);
+    if (KS > 2) {
+      if (a.Bpad != 64) continue;
+      e = KS == 4 ? prepare_f32_bp<64, 4>(lds) : prepare_f32_bp<64, 8>(lds);
+      if (e != hipSuccess) return e;
+      continue;
+    }
     e = KS == 1 ? (a.Bpad == 64 ? prepare_f32_bp<64, 1>(lds) : prepare_f32_bp<32, 1>(lds))
                 : (a.Bpad == 64 ? prepare_f32_bp<64, 2>(lds) : prepare_f32_bp<32, 2>(lds));
     if (e != hipSuccess) return e;
@@ -2033,8 +2147,8 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
     return hipGetLastError();
   }
   const int KS = f32_ks(a);
-  const int ppl = ppl_of(KS);
   const bool rh = f32_variant(a) == 3;
+  const int ppl = ppl_of(KS, rh);
   const size_t lds = persistent_f32_lds_ks(a, KS, rh);
   // groups of ppl peers: one launch each (a launch's gangs must all be co-resident), then the
   // recovery launches (attempt 1): a no-op exit for every gang that did not give up
@@ -2048,6 +2162,10 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
           if (a.Bpad == 64) launch_f32_bp<64, 1, true>(a, pb, s, p0, lds, attempt);
           else launch_f32_bp<32, 1, true>(a, pb, s, p0, lds, attempt);
         }
+      } else if (KS == 8) {
+        launch_f32_bp<64, 8>(a, pb, s, p0, lds, attempt);  // (f32_ks_wanted: Bpad 64 only)
+      } else if (KS == 4) {
+        launch_f32_bp<64, 4>(a, pb, s, p0, lds, attempt);
       } else if (KS == 2) {
         if (a.Bpad == 64) launch_f32_bp<64, 2>(a, pb, s, p0, lds, attempt);
         else launch_f32_bp<32, 2>(a, pb, s, p0, lds, attempt);

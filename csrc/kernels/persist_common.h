@@ -85,6 +85,38 @@ __device__ __forceinline__ int gang_same_xcd(unsigned* slots, int role, int nr, 
   return r;
 }
 
+// The same check for a GROUP of roles (first + k·stride, k < n <= 64) that hands off among itself:
+// role `role` reports into slots[role] and learns whether every member of its group reported its own
+// XCC. Members of different groups may sit on different XCDs (the cross-XCD K split).
+__device__ __forceinline__ int group_same_xcd(unsigned* slots, int role, int first, int stride, int n, unsigned mark, int* word,
+                                              unsigned long long ticks) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 0xFFu;
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(slots + role), mark | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    int same = 1;
+    unsigned v = mark | xcc;
+    for (;;) {
+      if (lane < n) v = __hip_atomic_load((gu32*)(slots + first + lane * stride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all((v & ~0xFFu) == mark)) break;
+      if (wall_clock64() - t0 > ticks) {
+        same = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (same) same = __all((v & 0xFFu) == xcc) ? 1 : 0;
+    if (lane == 0) *(volatile int*)word = same;
+  }
+  __syncthreads();
+  const int r = *(volatile int*)word;
+  __syncthreads();
+  return r;
+}
+
 __device__ __forceinline__ unsigned long long ld_wt(const void* ptr) {  // 8-byte L1-bypassing load
   return __hip_atomic_load((gu64*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -214,7 +214,7 @@ class MLPGroup:
         self.extras: Dict[str, torch.Tensor] = {}
         self.perm_fn = None  # test hook: callable(epoch) -> int32 [capacity, nmax] permutation
         self.eager = False  # debug/profiling A-B: launch steps without the hipGraph
-        self.force_f32_ks: Optional[int] = None  # test hook: fp32 owner K split (1 or 2)
+        self.force_f32_ks: Optional[int] = None  # test hook: fp32 owner K split (1, 2, 4, 8)
         # test / A-B hook: fp32 gang layout (1 owners + heads, 2 owners only; None = default)
         self.force_f32_variant: Optional[int] = None
         # weight-stationary persistent epoch kernel (csrc/kernels/mlp_persistent.hip): None = auto
@@ -308,14 +308,23 @@ class MLPGroup:
         # 570-578 rounds/s at 4 / 2 / 1 peers per GPU (profiles/r5_ksab). With the hand-offs forced
         # write-through (MYFYP_F32_PLAIN_PUB=0) the old choice: 2 when every peer sits in the first
         # 4 slots (one launch covers them all)
+        #
+        # Round 6: with at most 4 peers on the device, a peer's gang spans 8 / peers XCDs instead (the
+        # cross-XCD K split, csrc/kernels/mlp_persistent_f32.hip "XR"): the K parts of a column
+        # group reduce inside one XCD, and only the H1 and dH2 hand-offs cross XCDs. That puts the
+        # XCDs an 8-peer GPU gives to the other peers on this peer's critical path (N = 2 / 4 / 8
+        # GPUs hold 4 / 2 / 1 peers each). MYFYP_F32_XSPLIT=0 keeps K split 1.
         if self.force_f32_ks:
             ks = self.force_f32_ks
-        elif os.environ.get("MYFYP_F32_PLAIN_PUB", "1") == "0":
-            ks = 2 if self.handles and max(self.handles) < 4 else 1
+        elif os.environ.get("MYFYP_F32_XSPLIT", "1") != "0" and self.B == 64 and self.handles:
+            # measured (profiles/r6_xr): 1 peer K split 8 628.8 vs 612.2 rounds/s at K split 1, 2 peers
+            # K split 4 657.9 vs 622.7; 4 peers K split 2 612.8 vs 620.3 (loses: stays at 1)
+            used = max(self.handles) + 1  # peer slots one launch covers
+            ks = 8 if used <= 1 else 4 if used <= 2 else 1
         else:
             ks = 1
-        # a forced K split of 2 is a layout-1 configuration
-        var = self.force_f32_variant or (1 if self.force_f32_ks == 2 else 0)
+        # a forced K split > 1 is a layout-1 configuration
+        var = self.force_f32_variant or (1 if (self.force_f32_ks or 1) > 1 else 0)
         # weight collectives on the comm stream may hold CUs while an epoch runs: size the
         # co-resident gangs without them
         from myfyp_amd.parallel.federation import Federation, rccl_reserved_cus
@@ -578,7 +587,7 @@ class MLPGroup:
             return int(_native.load(required=True).mlp_engine_f32_variant(self._engine))
 
     def f32_ks(self) -> int:
-        """Owner K split the fp32 persistent epoch uses (1 or 2)."""
+        """Owner K split the fp32 persistent epoch uses (1, or 2 / 4 / 8: the cross-XCD K split)."""
         with self.lock, self.on_device():
             self._ensure_engine()
             return int(_native.load(required=True).mlp_engine_f32_ks(self._engine))

@@ -321,7 +321,11 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
         weights = [float(arrived[a][0]) for a in addrs]
         contributors = [a for a, w in zip(addrs, weights) if w > 0]
         if fed.mesh is not None:
-            return _mesh_mean(fed, addrs, learners, weights), contributors
+            mut = _MeshMutation(fed, addrs)
+            out = _mesh_mean(fed, addrs, learners, weights)
+            if mut.before:
+                mut.apply()
+            return out, contributors
         group = _stacked_group(learners)
         dev = learners[0].flat_params().device
         if group is not None and dev.type == "cuda":
@@ -468,6 +472,30 @@ def _generic_mean(fed: Federation, addrs, learners, weights, final: bool, delaye
     for lr in learners:
         _unpack_into(lr, avg)
     return total_w
+
+
+class _MeshMutation:
+    """Mutation-testing knob of the mesh aggregations (``MYFYP_DEBUG_MESH_SCALE``, default 1; never
+    set in normal runs): every peer's aggregation update is scaled, x <- x_before + s·(x_agg -
+    x_before), so the mesh result is off by (s - 1) of its update while the non-mesh path the GPU
+    tests compare against is not. Used once to show that the mesh aggregator tests catch a 5 %
+    update error (``profiles/r6_mutation``)."""
+
+    def __init__(self, fed: Federation, addrs) -> None:
+        import os
+
+        v = os.environ.get("MYFYP_DEBUG_MESH_SCALE")
+        self.scale = float(v) if v else 1.0
+        self.before = {}
+        if self.scale != 1.0:
+            for a in addrs:
+                if a in fed.local_nodes:
+                    lr = fed.local_nodes[a].learner
+                    self.before[a] = (lr, _pack(lr).clone())
+
+    def apply(self) -> None:
+        for lr, x0 in self.before.values():
+            _unpack_into(lr, x0 + self.scale * (_pack(lr) - x0))
 
 
 def _pack(learner) -> torch.Tensor:
@@ -673,8 +701,12 @@ def _mesh_scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggre
 
 
 def _scaffold(fed: Federation, arrived: Dict[str, Tuple[float, Any]], aggregator) -> None:
-    if fed.mesh is not None and fed.mesh_size > 1:
-        return _mesh_scaffold(fed, arrived, aggregator)
+    if fed.mesh is not None:  # (a one-device mesh too: its collectives still run through RCCL)
+        mut = _MeshMutation(fed, list(arrived))
+        _mesh_scaffold(fed, arrived, aggregator)
+        if mut.before:
+            mut.apply()
+        return
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     flats = [learners[a].flat_params() for a in addrs]
@@ -757,8 +789,12 @@ def _mesh_median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None
 
 
 def _median(fed: Federation, arrived: Dict[str, Tuple[float, Any]]) -> None:
-    if fed.mesh is not None and fed.mesh_size > 1:
-        return _mesh_median(fed, arrived)
+    if fed.mesh is not None:  # (a one-device mesh too: its collectives still run through RCCL)
+        mut = _MeshMutation(fed, list(arrived))
+        _mesh_median(fed, arrived)
+        if mut.before:
+            mut.apply()
+        return
     addrs = [a for a in arrived if a in fed.local_nodes]
     learners = {a: fed.local_nodes[a].learner for a in addrs}
     trainers = [a for a in addrs if float(arrived[a][0]) > 0]

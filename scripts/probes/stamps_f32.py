@@ -1,6 +1,8 @@
 """Phase timing of the fp32 persistent MLP epoch kernel (MYFYP_NATIVE_LIB=build/stamps/libmyfyp_hip.so).
 PEERS grouped peers (default 8), B = 64, two fits; per-step phase durations (us) of peer 0's owner 0
-and head 0, and the hand-off latencies between them."""
+and head 0, and the hand-off latencies between them. The owner K split follows the engine's choice
+(MYFYP_F32_KS forces one; at K split > 1 owner 0 is column group 0's K part 0, whose stamp 2 comes
+after the in-XCD reduction of the K parts and the reduced slice's publish)."""
 import ctypes
 import os
 import sys
@@ -29,6 +31,7 @@ parts = synthetic_mnist(60000, 10000, seed=1).generate_partitions(8, RandomIIDPa
 ls = [TorchLearner(TorchModel(MLP(seed=i)), parts[i], f"p{i}", batch_size=B, device="cuda") for i in range(P)]
 g = ls[0]._engine.group
 assert g.uses_persistent()
+print(f"peers {P}, owner K split {g.f32_ks()}, variant {g.f32_variant()}")
 for it in range(2):
     ths = [threading.Thread(target=l.fit) for l in ls]
     [t.start() for t in ths]

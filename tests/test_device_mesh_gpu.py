@@ -201,13 +201,15 @@ def test_bench_virtual_mesh_gpu():
 
 
 def test_bench_torchrun_mesh_virtual_gpu():
-    """The driver's multi-GPU launch shape on one GPU: ``torch.distributed.run --nproc-per-node 2
-    bench.py --gpus 2 --mesh-virtual``. Rank 0 drives the two-member mesh; rank 1 parks on the gloo
+    """The driver's multi-GPU launch shape on one GPU with the mesh asked for explicitly (torchrun's
+    default is one process per GPU): ``torch.distributed.run --nproc-per-node 2 bench.py --gpus 2
+    --launch mesh --mesh-virtual``. Rank 0 drives the two-member mesh; rank 1 parks on the gloo
     barrier and exits cleanly; exactly one JSON line comes out."""
     from _ports import free_port
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mesh-virtual", "--steps", "10", "--warmup", "3"]
+           "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch", "mesh", "--mesh-virtual", "--steps", "10", "--warmup",
+           "3"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=dict(os.environ))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

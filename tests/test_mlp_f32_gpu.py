@@ -127,19 +127,23 @@ def _rel_update(pe, pr, p0):
 
 
 def _layout(layout: str):
-    """(variant, owner K split) of a test layout id: v1ks1, v1ks2, v2, v3ks1, v3ks2."""
+    """(variant, owner K split) of a test layout id: v1ks1, v1ks2, v1ks4, v1ks8, v2, v3ks1, v3ks2."""
     v = int(layout[1])
-    return v, (2 if layout.endswith("ks2") else 1)
+    return v, (int(layout.split("ks")[1]) if "ks" in layout else 1)
 
 
-@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2", "v3ks1", "v3ks2"])
+@pytest.mark.parametrize("layout", ["v2", "v1ks1", "v1ks2", "v1ks4", "v1ks8", "v3ks1", "v3ks2"])
 @pytest.mark.parametrize("B", [64, 32])
 @pytest.mark.parametrize("epochs", [1, 2])
 def test_f32_epoch_matches_torch_adam(dev, B, epochs, layout):
     """Whole local epochs of the fp32 persistent kernel (2 peers, Adam 1e-3, raw 0..255 inputs)
     vs fp32 autograd + torch.optim.Adam on the same batches: relative update error < 1e-3. Every gang
-    layout: 2 (16 owners, two hand-offs per step: mlp_persistent_f32v2.hip), and layout 1 (owners +
-    heads) at both owner K splits: 1 (24-workgroup gangs) and 2 (40-workgroup gangs)."""
+    layout: 2 (16 owners, two hand-offs per step: mlp_persistent_f32v2.hip), layout 1 (owners +
+    heads) at owner K split 1 (24-workgroup gangs on one XCD) and at the cross-XCD K splits 2 / 4 / 8
+    (one peer's gang over 2 / 4 / 8 XCDs, K parts reduced inside each XCD: 4 / 2 / 1 peers per
+    launch, so 2 peers at K split 8 take two launches), and layout 3."""
+    if B != 64 and layout in ("v1ks4", "v1ks8"):
+        pytest.skip("K splits 4 / 8 are instantiated for the 64-row batch tile")
     spec = {"name": "adam", "lr": 1e-3}
     learners, refs, g, n = _setup(dev, 2, B, 1400, 3, spec)
     var, ks = _layout(layout)
@@ -428,11 +432,14 @@ def test_scaffold_control_variate_matches_formula(dev):
             assert ((cb.delta_c.double().cpu() - (want - ci_old)).norm() / (want - ci_old).norm()).item() < 1e-4
 
 
-@pytest.mark.parametrize("peers", [2, 8])
-def test_f32_single_xcd_handoffs_bit_identical(dev, peers):
+@pytest.mark.parametrize("peers,ks", [(2, 1), (8, 1), (1, 8), (2, 4), (4, 2)])
+def test_f32_single_xcd_handoffs_bit_identical(dev, peers, ks):
     """Single-XCD gangs keep their hand-offs in L2 (plain stores, persist::gang_same_xcd): the same
     fit with write-through hand-offs gives bit-identical parameters, and on MI355X every K-split-1
-    gang (blocks b = p mod 8) is found on one XCD, so the fast path is the one exercised."""
+    gang (blocks b = p mod 8) is found on one XCD, so the fast path is the one exercised. The
+    cross-XCD K split (ks > 1: one peer over ks XCDs) keeps the hand-offs INSIDE each group (a column
+    group's K parts; the heads) plain when the group is found on one XCD (persist::group_same_xcd),
+    and writes the H1 / dH2 hand-offs between XCDs through: bit-identical as well."""
     import ctypes
 
     from myfyp_amd.ops import _native
@@ -446,7 +453,9 @@ def test_f32_single_xcd_handoffs_bit_identical(dev, peers):
             lib.mlp_set_plain_pub(mode)
             MLPGroup.reset_all()
             learners, refs, g, n = _setup(dev, peers, 64, 600 * peers, 11, spec)
-            assert g.f32_ks() == 1
+            g.force_f32_ks = ks
+            g.force_f32_variant = 1
+            assert g.f32_ks() == ks
             _pin_perms(dev, g, learners, n)
             _fit_all(learners)
             seen = (ctypes.c_int * 64)()
