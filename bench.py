@@ -77,8 +77,13 @@ def _engine_label(nodes, eager: bool) -> str:
     eng = getattr(nodes[0].learner, "_engine", None) if nodes else None
     grp = getattr(eng, "group", None)
     kind = getattr(grp, "epoch_launch_kind", None)
-    if callable(kind):
-        kind = kind()
+    try:
+        kind = kind() if callable(kind) else kind
+        ks = grp.f32_ks() if getattr(grp, "precision", "") == "fp32" and grp.uses_persistent() else 1
+    except Exception:  # noqa: BLE001 — a label only
+        kind, ks = None, 1
+    if kind and ks > 1:
+        kind += f"-xcd-ksplit{ks}"
     if eager:
         return "fused-hip-eager"
     return f"fused-hip-{kind}" if kind else "fused-hip"
@@ -262,6 +267,7 @@ def main() -> None:
               f"gen2: {sum(1 for g in gc_pauses if g[0] == 2)}", file=sys.stderr, flush=True)
     print(f"[bench] rank {rank} median ms per call: {json.dumps(brk)} fed: "
           f"{ {k: round(1000 * float(np.median(v)), 3) for k, v in fed.stats.items()} }", file=sys.stderr, flush=True)
+    engine_label = _engine_label(nodes, args.eager) if fused else "autograd"  # (before the nodes stop)
     eng = getattr(nodes[0].learner, "_engine", None)
     if eng is not None and hasattr(eng.group, "graph_launch_stats"):
         print(f"[bench] rank {rank} epoch graph launches: {eng.group.graph_launch_stats()}", file=sys.stderr, flush=True)
@@ -310,7 +316,7 @@ def main() -> None:
                 "optimizer": "adam lr=1e-3 (fresh per round)",
                 "aggregator": "FedAvg (weighted all-reduce)",
                 "collective": coll,
-                "engine": _engine_label(nodes, args.eager) if fused else "autograd",
+                "engine": engine_label,
             },
             # headline time-to-target: Node.start() (incl. the engine prewarm) + set_start_learning
             # -> the evaluation that reaches the target (the prewarm moved setup out of

@@ -339,6 +339,10 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   const int cg = g % NCG, kh = g / NCG;  // column group, K part
   const int D0 = a.D0;
   constexpr bool XR = xr_of(KS, RH);  // cross-XCD K split (see the constants above)
+  // dH2 as LL (value, tag) pairs: opt-in (P32_LL_DH2). Measured across XCDs too (XR, one peer at
+  // K split 8, profiles/r6_xr/ll_dh2): the heads' publish 0.80 -> 0.32 us, the owners' load of the
+  // doubled payload 1.60 -> 2.10 us, the step 12.36 -> 12.52 us (627.8 vs 628.8 rounds/s): kept off
+  constexpr bool LLD = P32_LL_DH2;
   static_assert(!(XR && P32_LL_H1), "the cross-XCD K split uses flag hand-offs for H1");
   const int s0 = kpart_begin(ks1_of(D0), KS, kh);  // first (global) K step of this owner; local K step j is global s0 + j
   const int KS1 = kpart_begin(ks1_of(D0), KS, kh + 1) - s0;  // local K steps of this owner (<= kh_of(D0, KS))
@@ -463,7 +467,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
   auto w2_replica_update = [&](int tp, float lr_p, float inv_p) {
     // dH2(tp): LL pairs, verified at step tp; read through a buffer resource with 32-bit offsets from
     // a laundered lane (64-bit per-kb addresses hoisted out of the step loop would be spilled)
-    constexpr int DW = P32_LL_DH2 ? 2 : 1;  // floats per dH2 exchange element
+    constexpr int DW = LLD ? 2 : 1;  // floats per dH2 exchange element
     const __amdgpu_buffer_rsrc_t rd = rsrc_of(pb.dh2x + ((int64_t)p * 2 + (tp & 1)) * BP * PD2 * 2, BP * PD2 * 8);
     int lr = lane;
     asm volatile("" : "+v"(lr));
@@ -627,12 +631,12 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
     // ================= C: backward of this slice
     const float* dh2_t = pb.dh2x + ((int64_t)p * 2 + (t & 1)) * BP * PD2 * 2;
     const __amdgpu_buffer_rsrc_t r_dh2 = rsrc_of(dh2_t, BP * PD2 * 8);
-#if P32_LL_DH2
-    // representative wait (one chunk per head: its first two columns of row 0), then the bulk load
-    if (!persist::ll_wg_wait([&](int k) { return persist::ll_ld2(r_dh2, 16 * k * 8); }, NH, tag, pb.err, sOk)) return;
-#else
-    if (!persist::wg_wait(pb.flags, FPP, p, RH ? F3_DH2 : F_DH2, RH ? nhr_of(BP) : NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
-#endif
+    if constexpr (LLD) {
+      // representative wait (one chunk per head: its first two columns of row 0), then the bulk load
+      if (!persist::ll_wg_wait([&](int k) { return persist::ll_ld2(r_dh2, 16 * k * 8); }, NH, tag, pb.err, sOk)) return;
+    } else {
+      if (!persist::wg_wait(pb.flags, FPP, p, RH ? F3_DH2 : F_DH2, RH ? nhr_of(BP) : NH, pb.fbase + (unsigned)(t + 1), pb.err, sOk)) return;
+    }
     if (g == 0) P32_STAMP(0, t, 4);
     if (KS > 1 && !XR) {
       // (layout 3) full H1 slice = the K parts' partials summed in kh order (the heads' order: same
@@ -665,8 +669,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         *reinterpret_cast<float4*>(sH1c + b * 16 + c4) = float4{fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f), fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)};
       }
     }
-#if !P32_LL_DH2
-    {
+    if constexpr (!LLD) {
       float4 v[BP / 16];
 #pragma unroll
       for (int k = 0; k < BP / 16; ++k) v[k] = ld_sc1_16(r_dh2, (tv + NT * k) * 16);  // BP x 128 fp32 = BP*32 chunks
@@ -675,9 +678,7 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
         const int e = tv + NT * k;
         *reinterpret_cast<float4*>(sDH2 + (e >> 5) * LDD + 4 * (e & 31)) = v[k];
       }
-    }
-#else
-    {
+    } else {
       // BP x 128 LL pairs = BP*64 16-byte chunks (2 columns each), every tag verified
       persist::ll_u32x4 v[BP / 8];
       const bool ok = persist::ll_wait(v, [&](int k) { return persist::ll_ld2(r_dh2, (tv + NT * k) * 16); }, tag, pb.err);
@@ -688,7 +689,6 @@ __device__ void owner32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, in
       }
       if (!ok) sOk[1] = 0;
     }
-#endif
     lds_barrier();
     if (sOk[1] == 0) return;
     // C1: dH1 partials — wave w sums its 16 o2 rows (k order o2 = 16w + 4h + ks)
@@ -915,6 +915,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
   constexpr int MT = BP / 16;
   constexpr bool XR = xr_of(KS, false);
   static_assert(!(XR && P32_LL_H1), "the cross-XCD K split uses flag hand-offs for H1");
+  constexpr bool LLD = P32_LL_DH2;  // dH2 as LL pairs (owner32)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, c = lane & 15;
@@ -1243,18 +1244,16 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         const int b = 16 * wave + 4 * h + i;
         const float v = sH2[b * LD16 + c] > 0.f ? acc[i] : 0.f;
         sDH2[b * LD16 + c] = v;
-#if P32_LL_DH2
-        persist::ll_st1p(pb.plain_x, dst + 2 * (b * PD2 + 16 * hd + c), v, tag);
-#else
-        persist::pub32(pb.plain_x, dst + b * PD2 + 16 * hd + c, v);  // (XR: to every XCD's owners)
-#endif
+        if constexpr (LLD)
+          persist::ll_st1p(pb.plain_x, dst + 2 * (b * PD2 + 16 * hd + c), v, tag);  // (XR: written through to every XCD)
+        else
+          persist::pub32(pb.plain_x, dst + b * PD2 + 16 * hd + c, v);
       }
     }
-#if P32_LL_DH2
-    lds_barrier();  // sDH2 for the off-path updates (the LL stores need no drain or flag)
-#else
-    persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain_x);
-#endif
+    if constexpr (LLD)
+      lds_barrier();  // sDH2 for the off-path updates (the LL stores need no drain or flag)
+    else
+      persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain_x);
     if (hd == 0) P32_STAMP(1, t, 7);
 
     // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
