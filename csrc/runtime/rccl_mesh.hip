@@ -14,6 +14,9 @@
 //   rmesh_fedavg — the whole FedAvg of G stacked engine groups: per device the weighted partial
 //   sum of its rows (k_fedavg_reduce, weights as kernel arguments) → ONE grouped all-reduce of
 //   [Σ w x | Σ w] over xGMI → per device the apply kernel writing the mean into its live rows;
+//   rmesh_fedavg_bucketed — the same FedAvg bucketed and overlapped: per device the reduce and
+//   the per-bucket grouped all-reduces on a side (comm) stream, the compute stream waiting per
+//   bucket for its apply (or not at all: delayed averaging, landed by rmesh_delayed_land);
 //   rmesh_check / rmesh_abort / rmesh_shrink — failure handling: poll ncclCommGetAsyncError,
 //   ncclCommAbort every communicator (local: ends kernels stuck on a dead peer), and rebuild the
 //   mesh over the surviving devices with a fresh ncclCommInitAll;
@@ -30,6 +33,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -39,11 +43,18 @@ namespace {
 
 thread_local std::string g_err;
 
+struct DevEvents {  // reusable events of one device (bucketed FedAvg)
+  hipEvent_t ready = nullptr;       // compute stream -> comm stream: the rows are final
+  std::vector<hipEvent_t> bucket;   // comm stream -> compute stream: bucket k is all-reduced
+};
+
 struct Mesh {
   std::vector<int> devs;          // HIP device ordinal per mesh rank
   std::vector<ncclComm_t> comms;  // one communicator per device (rank i <-> devs[i])
   bool aborted = false;
   int injected = -1;  // fault hook (rmesh_debug_inject): rmesh_check reports an error on this rank
+  std::map<int, DevEvents> ev;  // by HIP device ordinal (survives a rebuild over fewer devices)
+  int last_nb = 0;              // buckets of the last bucketed FedAvg (its last event = "landed")
 };
 
 struct DeviceGuard {  // restores the caller's current device
@@ -99,6 +110,31 @@ bool group_end(bool ok) {
 }
 
 int fedavg_apply_all(Mesh* m, void** params, void** res, const int* P, int64_t n, const int64_t* ld, const float* mask, void** streams);
+
+// the current device's events, with at least nb bucket events (created on first use)
+DevEvents* events_for(Mesh* m, int dev, int nb) {
+  DevEvents& e = m->ev[dev];
+  if (e.ready == nullptr && !hip_ok(hipEventCreateWithFlags(&e.ready, hipEventDisableTiming), "hipEventCreate")) return nullptr;
+  while ((int)e.bucket.size() < nb) {
+    hipEvent_t x = nullptr;
+    if (!hip_ok(hipEventCreateWithFlags(&x, hipEventDisableTiming), "hipEventCreate")) return nullptr;
+    e.bucket.push_back(x);
+  }
+  return &e;
+}
+
+// [b0, b1) bucket bounds over n floats; every b0 a multiple of 4 (float4 kernels stay aligned)
+int64_t bucket_step(int64_t bucket) {
+  int64_t step = bucket / 4 * 4;
+  return step < 4 ? 4 : step;
+}
+
+unsigned long long mask_bits(const float* mask, int off, int P) {
+  unsigned long long bits = 0;
+  for (int p = 0; p < P; ++p)
+    if (mask[off + p] != 0.f) bits |= 1ull << p;
+  return bits;
+}
 
 }  // namespace
 
@@ -293,6 +329,156 @@ int rmesh_fedavg_retry(void* h, void** params, void** bufs, void** outs, const i
   return fedavg_apply_all(m, params, outs, P, n, ld, mask, streams);
 }
 
+// Bucketed, overlapped FedAvg: the weight exchange runs on a side stream of
+// every device. Buffers use the layout [Σw, pad x3 | Σ w x (n floats)] (n + 4 floats, the data
+// float4-aligned); keep[i] receives device i's local partial sums and is never overwritten by the
+// all-reduce (out of place into outs[i]), so a failed exchange can be re-run from it.
+//
+//   per device: event on the compute stream (the rows are final) -> the comm stream waits on it ->
+//   the weighted partial sums of every bucket on the comm stream;
+//   per bucket k: ONE grouped all-reduce over the mesh (bucket 0 also carries Σw), then an event
+//   per device on its comm stream;
+//   apply = 1: per device the compute stream waits on bucket k's event and applies bucket k, so
+//   bucket k's apply overlaps bucket k + 1's all-reduce and the compute stream never waits on the
+//   exchange as a whole; apply = 0 (delayed averaging): nothing is applied and the compute stream
+//   does not wait — the next local epoch runs beside the exchange (rmesh_delayed_land lands it).
+// Per device rows params[i] ([P_i][ld_i] fp32), weights w / mask as in rmesh_fedavg. A device with
+// P_i = 0 contributes zeros.
+int rmesh_fedavg_bucketed(void* h, void** params, void** keep, void** outs, const int* P, int64_t n, const int64_t* ld, const float* w,
+                          const float* mask, void** streams, void** comm_streams, int64_t bucket, int apply) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  const int G = (int)m->devs.size();
+  const int64_t step = bucket_step(bucket);
+  const int nb = n > 0 ? (int)((n + step - 1) / step) : 1;
+  DeviceGuard g;
+  int off = 0;
+  for (int i = 0; i < G; ++i) {
+    if (P[i] < 0 || P[i] > FEDAVG_MAX_PEERS) {
+      g_err = "rmesh_fedavg_bucketed: 0..64 rows per device";
+      return 2;
+    }
+    if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+    DevEvents* e = events_for(m, m->devs[i], nb);
+    if (e == nullptr) return 1;
+    hipStream_t cs = (hipStream_t)comm_streams[i];
+    if (!hip_ok(hipEventRecord(e->ready, (hipStream_t)streams[i]), "hipEventRecord") || !hip_ok(hipStreamWaitEvent(cs, e->ready, 0), "hipStreamWaitEvent"))
+      return 1;
+    float* kb = static_cast<float*>(keep[i]);
+    if (P[i] == 0) {
+      if (!hip_ok(hipMemsetAsync(kb, 0, (size_t)(n + 4) * sizeof(float), cs), "hipMemsetAsync")) return 1;
+    } else {
+      FedAvgWeights fw{};
+      double sum = 0.0;
+      for (int p = 0; p < P[i]; ++p) {
+        fw.w[p] = w[off + p];
+        sum += w[off + p];
+      }
+      fw.wsum = (float)sum;
+      const float* src = static_cast<const float*>(params[i]);
+      for (int k = 0; k < nb; ++k) {
+        const int64_t b0 = k * step, b1 = b0 + step < n ? b0 + step : n;
+        fl_fedavg_reduce(kb + 4 + b0, k == 0 ? kb : nullptr, src + b0, P[i], b1 - b0, ld[i], fw, cs);
+      }
+      if (!hip_ok(hipGetLastError(), "fl_fedavg_reduce")) return 1;
+    }
+    off += P[i];
+  }
+  for (int k = 0; k < nb; ++k) {
+    const int64_t b0 = k * step, b1 = b0 + step < n ? b0 + step : n;
+    const int64_t lo = k == 0 ? 0 : 4 + b0, hi = 4 + b1;
+    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+    bool ok = true;
+    for (int i = 0; i < G && ok; ++i)
+      ok = nccl_ok(ncclAllReduce(static_cast<float*>(keep[i]) + lo, static_cast<float*>(outs[i]) + lo, (size_t)(hi - lo), ncclFloat32, ncclSum, m->comms[i],
+                                 (hipStream_t)comm_streams[i]),
+                   "ncclAllReduce");
+    if (!group_end(ok)) return 1;
+    for (int i = 0; i < G; ++i) {
+      if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+      if (!hip_ok(hipEventRecord(m->ev[m->devs[i]].bucket[k], (hipStream_t)comm_streams[i]), "hipEventRecord")) return 1;
+    }
+  }
+  m->last_nb = nb;
+  if (!apply) return 0;
+  off = 0;
+  for (int i = 0; i < G; ++i) {
+    const unsigned long long bits = P[i] > 0 ? mask_bits(mask, off, P[i]) : 0ull;
+    off += P[i];
+    if (!bits) continue;
+    if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+    hipStream_t s = (hipStream_t)streams[i];
+    const float* ob = static_cast<const float*>(outs[i]);
+    float* dst = static_cast<float*>(params[i]);
+    for (int k = 0; k < nb; ++k) {
+      const int64_t b0 = k * step, b1 = b0 + step < n ? b0 + step : n;
+      if (!hip_ok(hipStreamWaitEvent(s, m->ev[m->devs[i]].bucket[k], 0), "hipStreamWaitEvent")) return 1;
+      fl_fedavg_apply(dst + b0, ob + 4 + b0, ob, P[i], b1 - b0, ld[i], bits, s);
+    }
+    if (!hip_ok(hipGetLastError(), "fl_fedavg_apply")) return 1;
+  }
+  return 0;
+}
+
+// Delayed averaging on the mesh: per device the compute stream waits on the last bucketed
+// exchange (if have_avg) and, for every masked row, lands it as x += avg / Σw - snap and takes the
+// new snapshot snap = x (one pass); without have_avg it only snapshots. snaps[i] is [P_i][ld_snap].
+int rmesh_delayed_land(void* h, void** params, void** snaps, void** outs, const int* P, int64_t n, const int64_t* ld, int64_t ld_snap, const float* mask,
+                       void** streams, int have_avg) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  const int G = (int)m->devs.size();
+  DeviceGuard g;
+  int off = 0;
+  for (int i = 0; i < G; ++i) {
+    const unsigned long long bits = P[i] > 0 ? mask_bits(mask, off, P[i]) : 0ull;
+    off += P[i];
+    if (!bits) continue;
+    if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+    hipStream_t s = (hipStream_t)streams[i];
+    const float* ob = static_cast<const float*>(outs[i]);
+    if (have_avg) {
+      auto it = m->ev.find(m->devs[i]);
+      if (it == m->ev.end() || m->last_nb < 1) {
+        g_err = "rmesh_delayed_land: no bucketed exchange pending on device " + std::to_string(m->devs[i]);
+        return 2;
+      }
+      if (!hip_ok(hipStreamWaitEvent(s, it->second.bucket[m->last_nb - 1], 0), "hipStreamWaitEvent")) return 1;
+    }
+    fl_fedavg_delayed_land(static_cast<float*>(params[i]), static_cast<float*>(snaps[i]), ld_snap, have_avg ? ob + 4 : nullptr, ob, P[i], n, ld[i], bits, s);
+    if (!hip_ok(hipGetLastError(), "fl_fedavg_delayed_land")) return 1;
+  }
+  return 0;
+}
+
+// Retry of a bucketed FedAvg after a failure: the retained partial sums keep[i] ([Σw, pad | data])
+// are all-reduced again over the CURRENT (rebuilt) mesh into outs[i] on the compute streams and,
+// if apply, applied to the masked rows. Arrays are indexed by the current mesh ranks.
+int rmesh_fedavg_bucketed_retry(void* h, void** params, void** keep, void** outs, const int* P, int64_t n, const int64_t* ld, const float* mask,
+                                void** streams, int apply) {
+  auto* m = static_cast<Mesh*>(h);
+  if (!usable(m)) return 1;
+  const int G = (int)m->devs.size();
+  DeviceGuard g;
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart")) return 1;
+  bool ok = true;
+  for (int i = 0; i < G && ok; ++i)
+    ok = nccl_ok(ncclAllReduce(keep[i], outs[i], (size_t)(n + 4), ncclFloat32, ncclSum, m->comms[i], (hipStream_t)streams[i]), "ncclAllReduce");
+  if (!group_end(ok)) return 1;
+  if (!apply) return 0;
+  int off = 0;
+  for (int i = 0; i < G; ++i) {
+    const unsigned long long bits = P[i] > 0 ? mask_bits(mask, off, P[i]) : 0ull;
+    off += P[i];
+    if (!bits) continue;
+    if (!hip_ok(hipSetDevice(m->devs[i]), "hipSetDevice")) return 1;
+    const float* ob = static_cast<const float*>(outs[i]);
+    fl_fedavg_apply(static_cast<float*>(params[i]), ob + 4, ob, P[i], n, ld[i], bits, (hipStream_t)streams[i]);
+    if (!hip_ok(hipGetLastError(), "fl_fedavg_apply")) return 1;
+  }
+  return 0;
+}
+
 }  // extern "C"
 
 namespace {
@@ -435,6 +621,11 @@ void rmesh_destroy(void* h) {
   if (!m->aborted)
     for (auto c : m->comms)
       if (c != nullptr) ncclCommDestroy(c);
+  for (auto& kv : m->ev) {
+    (void)hipSetDevice(kv.first);
+    if (kv.second.ready != nullptr) (void)hipEventDestroy(kv.second.ready);
+    for (auto e : kv.second.bucket) (void)hipEventDestroy(e);
+  }
   delete m;
 }
 

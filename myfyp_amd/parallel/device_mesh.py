@@ -45,6 +45,12 @@ _SIGS = {
                                     ctypes.c_void_p]),
     "rmesh_fedavg_retry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]),
+    "rmesh_fedavg_bucketed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
+    "rmesh_delayed_land": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "rmesh_fedavg_bucketed_retry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "rmesh_check": (ctypes.c_int, [ctypes.c_void_p]),
     "rmesh_abort": (ctypes.c_int, [ctypes.c_void_p]),
     "rmesh_shrink": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -58,6 +64,12 @@ class MeshError(RuntimeError):
     """A mesh collective failed (or the mesh was aborted)."""
 
 
+def _bucket_ranges(n: int, bucket: int) -> List[Tuple[int, int]]:
+    """[b0, b1) over n floats, every b0 a multiple of 4 (the native ``bucket_step``)."""
+    step = max(4, (int(bucket) // 4) * 4)
+    return [(b0, min(n, b0 + step)) for b0 in range(0, n, step)] or [(0, 0)]
+
+
 def _ptrs(vals: Sequence[int]) -> ctypes.Array:
     return (ctypes.c_void_p * len(vals))(*vals)
 
@@ -68,14 +80,14 @@ def _stream_ptr(dev: torch.device) -> int:
 
 class Marker:
     """Completion marker of a mesh member's queued work: an event recorded on the member device's
-    current stream (``cpu`` members complete synchronously)."""
+    current stream, or on ``stream`` (``cpu`` members complete synchronously)."""
 
-    def __init__(self, dev: torch.device) -> None:
+    def __init__(self, dev: torch.device, stream=None) -> None:
         self.ev = None
         if dev.type == "cuda":
             with torch.cuda.device(dev):
                 self.ev = torch.cuda.Event()
-                self.ev.record(torch.cuda.current_stream(dev))
+                self.ev.record(stream if stream is not None else torch.cuda.current_stream(dev))
 
     def query(self) -> bool:
         return True if self.ev is None else bool(self.ev.query())
@@ -141,9 +153,27 @@ class DeviceMesh:
         members (after a shrink) into ``outs``, then apply to the masked rows."""
         raise NotImplementedError
 
-    def marker(self, rank: int) -> Marker:
-        """Completion marker of everything queued so far on member ``rank``'s current stream."""
-        return Marker(self.devices[rank])
+    def fedavg_bucketed(self, params, keeps, outs, P, n: int, ld, w: np.ndarray, mask: np.ndarray, comm_streams, bucket: int, apply: bool = True) -> None:
+        """Bucketed, overlapped FedAvg (``rmesh_fedavg_bucketed``): per member the partial sums
+        [Σw, pad x3 | Σ w x] (n + 4 floats) into ``keeps`` and the per-bucket all-reduces into
+        ``outs``, on ``comm_streams``; with ``apply`` the member's compute stream waits per bucket
+        and applies it, without (delayed averaging) nothing waits: :meth:`delayed_land` lands it."""
+        raise NotImplementedError
+
+    def delayed_land(self, params, snaps, outs, P, n: int, ld, ld_snap: int, mask: np.ndarray, have_avg: bool) -> None:
+        """Per member, on the compute stream: (after the last bucketed exchange, if ``have_avg``)
+        masked rows x += avg / Σw - snap, then snap = x (``rmesh_delayed_land``)."""
+        raise NotImplementedError
+
+    def fedavg_bucketed_retry(self, params, keeps, outs, P, n: int, ld, mask: np.ndarray, apply: bool = True) -> None:
+        """Re-run a bucketed FedAvg's exchange from the retained ``keeps`` over the CURRENT members
+        (after a shrink), on the compute streams, then apply (if ``apply``)."""
+        raise NotImplementedError
+
+    def marker(self, rank: int, stream=None) -> Marker:
+        """Completion marker of everything queued so far on member ``rank``'s current stream (or
+        on ``stream``, e.g. its comm stream)."""
+        return Marker(self.devices[rank], stream)
 
     def check(self) -> None:
         pass
@@ -185,10 +215,10 @@ class HostMesh(DeviceMesh):
         like a device stuck in a kernel."""
         self._stalled.add(int(rank))
 
-    def marker(self, rank: int) -> Marker:
+    def marker(self, rank: int, stream=None) -> Marker:
         if rank in self._stalled:
             return _Stalled()
-        return super().marker(rank)
+        return super().marker(rank, stream)
 
     def inject_error(self, rank: int) -> None:
         self._injected = int(rank)
@@ -352,6 +382,162 @@ class HostMesh(DeviceMesh):
                                                               mask[off:].ctypes.data, _stream_ptr(res[i].device)), "fedavg_stacked_apply")
             off += P[i]
 
+    # ------------------------------------------------------------------ bucketed FedAvg
+    def fedavg_bucketed(self, params, keeps, outs, P, n, ld, w, mask, comm_streams, bucket, apply=True) -> None:
+        """Same launches as ``rmesh_fedavg_bucketed`` for GPU members (a virtual mesh: the
+        per-bucket all-reduce is a stream-ordered sum on member 0's comm stream); CPU members
+        compute the same result synchronously."""
+        self._live()
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        ranges = _bucket_ranges(n, bucket)
+        with self.lock:
+            self.calls += 1
+            if not all(t.is_cuda for t in params):
+                off = 0
+                for i in range(self.size):
+                    kb = keeps[i]
+                    kb.zero_()
+                    if P[i] > 0:
+                        rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])[:, :n]
+                        wt = torch.as_tensor(w[off : off + P[i]], dtype=torch.float32, device=rows.device)
+                        kb[4 : 4 + n].copy_((wt[:, None] * rows).sum(0))
+                        kb[0] = float(np.sum(w[off : off + P[i]], dtype=np.float64))
+                    off += P[i]
+                acc = keeps[0][: n + 4].clone()
+                for kb in keeps[1:]:
+                    acc.add_(kb[: n + 4].to(acc.device))
+                for o in outs:
+                    o[: n + 4].copy_(acc.to(o.device))
+                if apply:
+                    self._apply4(params, outs, P, n, ld, mask)
+                return
+            from myfyp_amd import ops
+
+            fast = ops.fast_lib()
+            off = 0
+            for i in range(self.size):
+                dev = keeps[i].device
+                cs = comm_streams[i]
+                with torch.cuda.device(dev):
+                    cs.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(cs):
+                        if P[i] == 0:
+                            keeps[i].zero_()
+                        else:
+                            kp, sp = keeps[i].data_ptr(), params[i].data_ptr()
+                            for k, (b0, b1) in enumerate(ranges):
+                                ops.check(fast.myfyp_fedavg_bucket_reduce(kp + 4 * (4 + b0), kp if k == 0 else None, sp + 4 * b0, int(P[i]), b1 - b0, int(ld[i]),
+                                                                          w[off:].ctypes.data, cs.cuda_stream), "fedavg_bucket_reduce")
+                off += P[i]
+            c0 = comm_streams[0]
+            self._bucket_events = []
+            for k, (b0, b1) in enumerate(ranges):
+                lo, hi = (0 if k == 0 else 4 + b0), 4 + b1
+                with torch.cuda.device(keeps[0].device):
+                    for cs in comm_streams[1:]:
+                        c0.wait_stream(cs)
+                    with torch.cuda.stream(c0):
+                        acc = keeps[0][lo:hi].clone()
+                        for kb in keeps[1:]:
+                            acc.add_(kb[lo:hi].to(acc.device))
+                        for o in outs:
+                            o[lo:hi].copy_(acc.to(o.device))
+                    ev = torch.cuda.Event()
+                    ev.record(c0)
+                self._bucket_events.append(ev)
+            for cs in comm_streams[1:]:
+                cs.wait_event(self._bucket_events[-1])
+            if not apply:
+                return
+            off = 0
+            for i in range(self.size):
+                if P[i] > 0 and np.any(mask[off : off + P[i]] != 0):
+                    dev = outs[i].device
+                    with torch.cuda.device(dev):
+                        cur = torch.cuda.current_stream(dev)
+                        op, dp = outs[i].data_ptr(), params[i].data_ptr()
+                        for k, (b0, b1) in enumerate(ranges):
+                            cur.wait_event(self._bucket_events[k])
+                            ops.check(fast.myfyp_fedavg_bucket_apply(dp + 4 * b0, op + 4 * (4 + b0), op, int(P[i]), b1 - b0, int(ld[i]),
+                                                                     mask[off:].ctypes.data, cur.cuda_stream), "fedavg_bucket_apply")
+                off += P[i]
+
+    def _apply4(self, params, outs, P, n, ld, mask) -> None:
+        off = 0
+        for i in range(self.size):
+            if P[i] > 0:
+                o = outs[i]
+                mean = o[4 : 4 + n] / o[0].clamp_min(1e-12)
+                rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])
+                for p in range(P[i]):
+                    if mask[off + p] != 0:
+                        rows[p, :n].copy_(mean)
+            off += P[i]
+
+    def delayed_land(self, params, snaps, outs, P, n, ld, ld_snap, mask, have_avg) -> None:
+        self._live()
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        with self.lock:
+            self.calls += 1
+            off = 0
+            for i in range(self.size):
+                if P[i] > 0 and np.any(mask[off : off + P[i]] != 0):
+                    dev = params[i].device
+                    if params[i].is_cuda:
+                        from myfyp_amd import ops
+
+                        with torch.cuda.device(dev):
+                            cur = torch.cuda.current_stream(dev)
+                            if have_avg:
+                                evs = getattr(self, "_bucket_events", None)
+                                if not evs:
+                                    raise MeshError("delayed_land: no bucketed exchange pending")
+                                cur.wait_event(evs[-1])
+                            o = outs[i]
+                            ops.check(ops.fast_lib().myfyp_fedavg_delayed_land(params[i].data_ptr(), snaps[i].data_ptr(), int(ld_snap),
+                                                                               o.data_ptr() + 16 if have_avg else None, o.data_ptr() if have_avg else None,
+                                                                               int(P[i]), int(n), int(ld[i]), mask[off:].ctypes.data, cur.cuda_stream),
+                                      "fedavg_delayed_land")
+                    else:
+                        rows = params[i].view(-1)[: P[i] * ld[i]].view(P[i], ld[i])
+                        sn = snaps[i].view(-1)[: P[i] * ld_snap].view(P[i], ld_snap)
+                        for p in range(P[i]):
+                            if mask[off + p] != 0:
+                                if have_avg:
+                                    rows[p, :n] += outs[i][4 : 4 + n] / outs[i][0].clamp_min(1e-12) - sn[p, :n]
+                                sn[p, :n].copy_(rows[p, :n])
+                off += P[i]
+
+    def fedavg_bucketed_retry(self, params, keeps, outs, P, n, ld, mask, apply=True) -> None:
+        self._live()
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        with self.lock:
+            self.calls += 1
+            for o, kb in zip(outs, keeps):
+                o[: n + 4].copy_(kb[: n + 4])
+            self.all_reduce_([o[: n + 4] for o in outs])
+            if not apply:
+                self._bucket_events = [] if not params or not params[0].is_cuda else [torch.cuda.Event()]
+                if self._bucket_events:
+                    with torch.cuda.device(params[0].device):
+                        self._bucket_events[0].record(torch.cuda.current_stream(params[0].device))
+                return
+            if all(t.is_cuda for t in params):
+                from myfyp_amd import ops
+
+                fast = ops.fast_lib()
+                off = 0
+                for i in range(self.size):
+                    if P[i] > 0:
+                        with torch.cuda.device(outs[i].device):
+                            op = outs[i].data_ptr()
+                            ops.check(fast.myfyp_fedavg_bucket_apply(params[i].data_ptr(), op + 16, op, int(P[i]), int(n), int(ld[i]), mask[off:].ctypes.data,
+                                                                     _stream_ptr(outs[i].device)), "fedavg_bucket_apply")
+                    off += P[i]
+            else:
+                self._apply4(params, outs, P, n, ld, mask)
+
     def shrink(self, keep) -> None:
         with self.lock:
             self.devices = [self.devices[k] for k in keep]
@@ -459,6 +645,37 @@ class RcclMesh(DeviceMesh):
             self._rc(self._lib.rmesh_fedavg_retry(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in bufs]),
                                                   _ptrs([t.data_ptr() for t in outs]), Pa, int(n), lda, mask.ctypes.data, self._streams()),
                      "rmesh_fedavg_retry")
+
+    def fedavg_bucketed(self, params, keeps, outs, P, n, ld, w, mask, comm_streams, bucket, apply=True) -> None:
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
+        lda = (ctypes.c_int64 * self.size)(*[int(x) for x in ld])
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_fedavg_bucketed(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in keeps]),
+                                                     _ptrs([t.data_ptr() for t in outs]), Pa, int(n), lda, w.ctypes.data, mask.ctypes.data, self._streams(),
+                                                     _ptrs([s.cuda_stream for s in comm_streams]), int(bucket), int(bool(apply))), "rmesh_fedavg_bucketed")
+
+    def delayed_land(self, params, snaps, outs, P, n, ld, ld_snap, mask, have_avg) -> None:
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
+        lda = (ctypes.c_int64 * self.size)(*[int(x) for x in ld])
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_delayed_land(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in snaps]),
+                                                  _ptrs([t.data_ptr() for t in outs]), Pa, int(n), lda, int(ld_snap), mask.ctypes.data, self._streams(),
+                                                  int(bool(have_avg))), "rmesh_delayed_land")
+
+    def fedavg_bucketed_retry(self, params, keeps, outs, P, n, ld, mask, apply=True) -> None:
+        mask = np.ascontiguousarray(mask, dtype=np.float32)
+        Pa = (ctypes.c_int * self.size)(*[int(p) for p in P])
+        lda = (ctypes.c_int64 * self.size)(*[int(x) for x in ld])
+        with self.lock:
+            self.calls += 1
+            self._rc(self._lib.rmesh_fedavg_bucketed_retry(self._h, _ptrs([t.data_ptr() for t in params]), _ptrs([t.data_ptr() for t in keeps]),
+                                                           _ptrs([t.data_ptr() for t in outs]), Pa, int(n), lda, mask.ctypes.data, self._streams(),
+                                                           int(bool(apply))), "rmesh_fedavg_bucketed_retry")
 
     def inject_error(self, rank: int) -> None:
         with self.lock:

@@ -451,12 +451,13 @@ class Federation:
             t = self._mesh_scratch[key] = torch.zeros(numel, dtype=torch.float32, device=self.devices[mesh_rank])
         return t
 
-    def mesh_track(self, kind: str, retry: Optional[Callable[[], None]] = None) -> None:
+    def mesh_track(self, kind: str, retry: Optional[Callable[[], None]] = None, streams=None) -> None:
         """Register the mesh collective just enqueued with the mesh guard (deadline, async-error
-        poll, retry from retained inputs: ``parallel/mesh_guard.py``)."""
+        poll, retry from retained inputs: ``parallel/mesh_guard.py``). ``streams`` (one per
+        member): where the collective ran, if not on the members' current streams."""
         g = self.mesh_guard
         if g is not None:
-            g.track(kind, retry)
+            g.track(kind, retry, streams)
 
     def mesh_confirm(self) -> bool:
         """Confirm the pending mesh collectives (recovering from a failed one); True if a

@@ -80,11 +80,12 @@ class MeshGuard:
     def _timeout(self) -> float:
         return float(Settings.COLLECTIVE_TIMEOUT)
 
-    def track(self, kind: str, retry: Optional[Callable[[], None]] = None) -> None:
-        """Register the collective just enqueued on every member's current stream."""
+    def track(self, kind: str, retry: Optional[Callable[[], None]] = None, streams=None) -> None:
+        """Register the collective just enqueued on every member's current stream (or on
+        ``streams[i]``: a delayed exchange that no compute stream waits on)."""
         if not Settings.COLLECTIVE_FAILOVER or self.mesh is None:
             return
-        markers = [self.mesh.marker(i) for i in range(self.mesh.size)]
+        markers = [self.mesh.marker(i, None if streams is None else streams[i]) for i in range(self.mesh.size)]
         with self.lock:
             self.pending.append(MeshOp(kind, self.fed.mesh_members, markers, retry, self._timeout()))
         self._ensure_thread()

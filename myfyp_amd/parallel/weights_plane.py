@@ -322,7 +322,7 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
         contributors = [a for a, w in zip(addrs, weights) if w > 0]
         if fed.mesh is not None:
             mut = _MeshMutation(fed, addrs)
-            out = _mesh_mean(fed, addrs, learners, weights)
+            out = _mesh_mean(fed, addrs, learners, weights, final)
             if mut.before:
                 mut.apply()
             return out, contributors
@@ -362,9 +362,13 @@ def aggregate_mean(fed: Federation, arrived: Dict[str, Tuple[float, Any]], final
     return total_w, contributors
 
 
-def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
-    """FedAvg over a device mesh. Stacked engine groups (one per mesh rank): ONE native call —
-    per device reduce launch, one grouped RCCL all-reduce, per device apply launch
+def _mesh_mean(fed: Federation, addrs, learners, weights, final: bool = True) -> float:
+    """FedAvg over a device mesh. Stacked engine groups (one per mesh rank): ONE native call.
+    With ``OVERLAP_COLLECTIVES`` (default) it is the bucketed exchange on each device's comm
+    stream (``rmesh_fedavg_bucketed``: reduce, per-bucket grouped all-reduce, the compute stream
+    waiting per bucket for its apply; ``DELAYED_AVERAGING`` runs it beside the next local epoch and
+    lands it a round later — see :func:`_mesh_mean_bucketed`); otherwise per device reduce launch,
+    one grouped RCCL all-reduce and per device apply launch on the compute streams
     (``rmesh_fedavg``). Other learners: per device partial sums, one mesh all-reduce, unpack.
 
     The all-reduce is out of place, so every device keeps its local partial sum [Σ w x | Σ w]. The
@@ -379,6 +383,10 @@ def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
     stacked = all(len(g) == 1 and len(groups[r]) == 1 for r, g in groups.items() if ranks[r]) and all(
         getattr(lr, "_engine", None) is not None for v in ranks.values() for _, lr in v)
     numels = {next(iter(g.values())).numel for g in groups.values() if g}
+    from myfyp_amd.settings import Settings
+
+    if stacked and len(numels) == 1 and (Settings.OVERLAP_COLLECTIVES or Settings.DELAYED_AVERAGING or getattr(fed, "_mesh_delayed", None)):
+        return _mesh_mean_bucketed(fed, ranks, groups, numels.pop(), wt_of, float(sum(weights)), bool(Settings.DELAYED_AVERAGING) and not final)
     if stacked and len(numels) == 1 and all(next(iter(g.values())).params.is_cuda for g in groups.values() if g):
         n = numels.pop()
         per: Dict[int, tuple] = {}  # mesh rank -> (params, partial, result, P, ld, w, mask)
@@ -442,6 +450,87 @@ def _mesh_mean(fed: Federation, addrs, learners, weights) -> float:
     reduce_unpack()
     fed.mesh_track("fedavg", reduce_unpack)
     return float(sum(weights))
+
+
+def _mesh_buf(g, name: str, numel: int) -> torch.Tensor:
+    """A zero-initialised fp32 buffer cached on an engine group (its device)."""
+    t = getattr(g, name, None)
+    if t is None or t.numel() != numel:
+        with on_device(g.params.device):
+            t = torch.zeros(numel, dtype=torch.float32, device=g.params.device)
+        setattr(g, name, t)
+    return t
+
+
+def _mesh_mean_bucketed(fed: Federation, ranks, groups, n: int, wt_of, total_w: float, delayed: bool) -> float:
+    """Bucketed, overlapped mesh FedAvg of stacked engine groups.
+
+    ``rmesh_fedavg_bucketed``: per device the weighted partial sums [Σw, pad | Σ w x] go to a
+    retained buffer (``keep``) on the device's comm stream, each bucket of ``BUCKET_BYTES`` is
+    all-reduced (grouped over the mesh) as soon as it is reduced, and the compute stream waits per
+    bucket for its apply — bucket k's apply overlaps bucket k + 1's all-reduce, and the next local
+    epoch is queued behind the applies without the host waiting.
+
+    Delayed averaging (``DELAYED_AVERAGING``, not on the last round; the ranks path's semantics,
+    ``_stacked_mean_cuda``): round r - 1's exchanged average is landed as x += avg - snap together
+    with the new snapshot (``rmesh_delayed_land``, one launch per device), then the snapshot rows
+    are exchanged on the comm streams with no apply and nothing waiting: the whole exchange runs
+    beside round r + 1's local epoch. The mesh guard watches the comm streams then.
+
+    Failure: the guard's ``retry`` re-runs the exchange from the retained ``keep`` buffers over the
+    rebuilt mesh (``rmesh_fedavg_bucketed_retry``) and re-applies — the survivors' average."""
+    from myfyp_amd.settings import Settings
+
+    bucket = max(4, int(Settings.BUCKET_BYTES) // 4)
+    per: Dict[int, tuple] = {}  # mesh rank -> (params, keep, out, P, ld, w, mask, snap)
+    for r in fed.mesh_members:
+        if ranks[r]:
+            g = next(iter(groups[r].values()))
+            wr = np.zeros(g.capacity, dtype=np.float32)
+            mr = np.zeros(g.capacity, dtype=np.float32)
+            for a, lr in ranks[r]:
+                wr[lr._engine.slot] = wt_of[a]
+                mr[lr._engine.slot] = 1.0
+            snap = _mesh_buf(g, "_mesh_snap", g.capacity * n) if (delayed or getattr(fed, "_mesh_delayed", None)) else None
+            per[r] = (g.params, _mesh_buf(g, "_mesh_keep4", n + 4), _mesh_buf(g, "_mesh_out4", n + 4), g.capacity, g.S, wr, mr, snap)
+        else:  # no live peer on this device (yet in the mesh): contributes zeros
+            scratch = fed.mesh_scratch(r, n + 4, "keep4")
+            per[r] = (scratch, scratch, fed.mesh_scratch(r, n + 4, "out4"), 0, n, np.zeros(0, np.float32), np.zeros(0, np.float32), scratch)
+
+    def cols(k: int, rs) -> list:
+        return [per[r][k] for r in rs]
+
+    rs = list(fed.mesh_members)
+    comm = [comm_stream(fed.devices[r]) if fed.devices[r].type == "cuda" else None for r in rs]
+    mask = np.concatenate(cols(6, rs))
+    if getattr(fed, "_mesh_delayed", None) is not None:  # land round r - 1's exchanged average
+        fed.mesh.delayed_land(cols(0, rs), cols(7, rs), cols(2, rs), cols(3, rs), n, cols(4, rs), n, mask, True)
+        fed._mesh_delayed = None
+        landed = True
+    else:
+        landed = False
+    if delayed:
+        if not landed:  # first delayed round: snapshot only
+            fed.mesh.delayed_land(cols(0, rs), cols(7, rs), cols(2, rs), cols(3, rs), n, cols(4, rs), n, mask, False)
+        fed.mesh.fedavg_bucketed(cols(7, rs), cols(1, rs), cols(2, rs), cols(3, rs), n, [n] * len(rs), np.concatenate(cols(5, rs)), mask, comm, bucket,
+                                 apply=False)
+        fed._mesh_delayed = True
+
+        def retry_delayed() -> None:  # survivors: the retained partial sums again, landed next round
+            live = [r for r in fed.mesh_members if r in per]
+            fed.mesh.fedavg_bucketed_retry(cols(7, live), cols(1, live), cols(2, live), cols(3, live), n, [n] * len(live), np.concatenate(cols(6, live)),
+                                           apply=False)
+
+        fed.mesh_track("fedavg (delayed)", retry_delayed, streams=comm)
+        return total_w
+    fed.mesh.fedavg_bucketed(cols(0, rs), cols(1, rs), cols(2, rs), cols(3, rs), n, cols(4, rs), np.concatenate(cols(5, rs)), mask, comm, bucket, apply=True)
+
+    def retry() -> None:  # over the current (rebuilt) mesh: the survivors' retained partials
+        live = [r for r in fed.mesh_members if r in per]
+        fed.mesh.fedavg_bucketed_retry(cols(0, live), cols(1, live), cols(2, live), cols(3, live), n, cols(4, live), np.concatenate(cols(6, live)))
+
+    fed.mesh_track("fedavg", retry)
+    return total_w
 
 
 def _generic_mean(fed: Federation, addrs, learners, weights, final: bool, delayed: bool) -> float:

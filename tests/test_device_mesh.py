@@ -388,3 +388,100 @@ def test_torchrun_defaults_to_one_process_per_gpu(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "1")
     assert launch.plan_launch(3, "auto", mesh_virtual=True) == "mesh"
     assert launch.plan_launch(1, "auto") == "single"
+
+
+# ---------------------------------------------------------------------------------------------
+# bucketed, overlapped mesh FedAvg (rmesh_fedavg_bucketed semantics)
+# ---------------------------------------------------------------------------------------------
+def _bucketed_case(seed: int, P=(3, 2), n=10, ld=12):
+    rng = np.random.default_rng(seed)
+    params = [torch.from_numpy(rng.standard_normal((p, ld)).astype(np.float32)) for p in P]
+    rows = np.concatenate([p.numpy()[:, :n] for p in params])
+    return list(P), n, ld, params, rows
+
+
+@pytest.mark.parametrize("bucket", [4, 8, 1 << 20])
+def test_host_mesh_bucketed_fedavg_matches_numpy(bucket):
+    """Partial sums [Σw, pad x3 | Σ w x] retained in ``keeps``, per-bucket all-reduce into ``outs``,
+    the mean applied to the masked rows; unmasked rows and padding untouched; every bucket size
+    (one float4 per bucket up to one bucket) gives the same rows."""
+    P, n, ld, params, rows = _bucketed_case(0)
+    m = _cpu_mesh(2)
+    w = np.array([1.0, 0.0, 3.0, 2.0, 4.0], dtype=np.float32)
+    mask = np.array([1, 1, 0, 1, 1], dtype=np.float32)
+    before = [p.clone() for p in params]
+    keeps = [torch.zeros(n + 4) for _ in P]
+    outs = [torch.zeros(n + 4) for _ in P]
+    m.fedavg_bucketed(params, keeps, outs, P, n, [ld, ld], w, mask, [None, None], bucket, apply=True)
+    want = (w[:, None] * rows).sum(0) / w.sum()
+    allrows, allbefore = torch.cat(params).numpy(), torch.cat(before).numpy()
+    fm = mask.astype(bool)
+    np.testing.assert_allclose(allrows[fm, :n], np.broadcast_to(want, (int(fm.sum()), n)), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(allrows[~fm], allbefore[~fm])
+    np.testing.assert_array_equal(allrows[:, n:], allbefore[:, n:])
+    # each member keeps its own partial sum (the retry input); outs hold the global one
+    np.testing.assert_allclose(keeps[0][4:].numpy(), (w[:3, None] * rows[:3]).sum(0), rtol=1e-6)
+    assert float(keeps[1][0]) == 6.0 and float(outs[0][0]) == float(outs[1][0]) == float(w.sum())
+
+
+def test_host_mesh_delayed_averaging_lands_a_round_later():
+    """Delayed averaging on the mesh: round r's snapshot is exchanged with no apply; at round r + 1
+    every masked row lands x += avg_r - snap_r (its local progress since the snapshot kept) and is
+    snapshotted again."""
+    P, n, ld, params, rows = _bucketed_case(1, P=(2, 2), n=6, ld=8)
+    m = _cpu_mesh(2)
+    w = np.array([1.0, 2.0, 3.0, 4.0], dtype=np.float32)
+    mask = np.ones(4, dtype=np.float32)
+    snaps = [torch.zeros(p * n) for p in P]
+    keeps = [torch.zeros(n + 4) for _ in P]
+    outs = [torch.zeros(n + 4) for _ in P]
+    m.delayed_land(params, snaps, outs, P, n, [ld, ld], n, mask, False)  # first round: snapshot only
+    m.fedavg_bucketed(snaps, keeps, outs, P, n, [n, n], w, mask, [None, None], 4, apply=False)
+    avg = (w[:, None] * rows).sum(0) / w.sum()
+    assert np.array_equal(torch.cat(params).numpy()[:, :n], rows)  # nothing applied yet
+    step = [torch.full_like(p, 0.25) for p in params]  # the next local epoch's progress
+    for p, d in zip(params, step):
+        p.add_(d)
+    m.delayed_land(params, snaps, outs, P, n, [ld, ld], n, mask, True)
+    got = torch.cat(params).numpy()[:, :n]
+    np.testing.assert_allclose(got, np.broadcast_to(avg + 0.25, got.shape), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(torch.cat([s.view(p, n) for s, p in zip(snaps, P)]).numpy(), got, rtol=0, atol=0)
+
+
+def _bucketed_guarded(fed, params, P, n, ld, w, mask, bucket=4):
+    keeps = [torch.zeros(n + 4) for _ in P]
+    outs = [torch.zeros(n + 4) for _ in P]
+    offs = np.concatenate([[0], np.cumsum(P)])
+    fed.mesh.fedavg_bucketed(params, keeps, outs, P, n, ld, w, mask, [None] * len(P), bucket, apply=True)
+
+    def retry():
+        live = list(fed.mesh_members)
+        fed.mesh.fedavg_bucketed_retry([params[r] for r in live], [keeps[r] for r in live], [outs[r] for r in live], [P[r] for r in live], n,
+                                       [ld[r] for r in live], np.concatenate([mask[offs[r] : offs[r + 1]] for r in live]))
+
+    fed.mesh_track("fedavg", retry)
+
+
+def test_mesh_guard_bucketed_stalled_member_aggregates_survivors(short_timeouts):
+    """The stalled-device recovery on the bucketed exchange: the survivors' retained [Σw | Σ w x]
+    are all-reduced again over the rebuilt mesh and applied — the average of what arrived."""
+    rng = np.random.default_rng(7)
+    Federation.reset()
+    try:
+        fed = Federation._init_mesh([torch.device("cpu")] * 3, "host")
+        n, ld, P = 9, 12, [2, 1, 2]
+        params = [torch.from_numpy(rng.standard_normal((p, ld)).astype(np.float32)) for p in P]
+        rows = np.concatenate([p.numpy()[:, :n] for p in params])
+        w = np.array([1.0, 2.0, 3.0, 4.0, 5.0], dtype=np.float32)
+        mask = np.ones(5, dtype=np.float32)
+        fed.mesh.stall(2)
+        _bucketed_guarded(fed, params, P, n, [ld] * 3, w, mask)
+        time.sleep(0.5)
+        assert fed.mesh_confirm() is True
+        assert fed.mesh_members == [0, 1] and fed.mesh_guard.lost == [2]
+        want = _want(rows, w, [np.arange(0, 2), np.arange(2, 3)])
+        got = np.concatenate([params[0].numpy()[:, :n], params[1].numpy()[:, :n]])
+        np.testing.assert_allclose(got, np.broadcast_to(want, got.shape), rtol=1e-5, atol=1e-6)
+        assert fed.mesh_confirm() is False
+    finally:
+        Federation.reset()

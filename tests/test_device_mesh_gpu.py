@@ -332,3 +332,130 @@ def test_mesh_workflow_rccl_g1_async_error_mid_experiment():
         Federation.reset()
         MLPGroup.reset_all()
         Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = saved
+
+
+# ---------------------------------------------------------------------------------------------
+# bucketed, overlapped mesh FedAvg (rmesh_fedavg_bucketed / rmesh_delayed_land)
+# ---------------------------------------------------------------------------------------------
+BUCKET = 60000  # floats: 4 buckets over the MLP's 235146 parameters
+
+
+@pytest.mark.parametrize("P", [1, 3, 8])
+def test_rccl_mesh_bucketed_fedavg_bit_equal_to_local_kernel(P):
+    """Reduce on the comm stream, per-bucket grouped all-reduce, per-bucket apply on the compute
+    stream behind a bucket event: the rows end exactly as ``k_fedavg_local`` writes them, with the
+    compute stream still busy when the call is enqueued (the comm stream must wait for it), and
+    again after an abort + re-init."""
+    from myfyp_amd.parallel.weights_plane import comm_stream
+
+    n, S, base, w, mask, ref = _stacked_case(P, 20 + P)
+    m = _mesh()
+    try:
+        for attempt in range(2):
+            got = base.clone()
+            keep = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+            out = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+            torch.cuda._sleep(20_000_000)  # the compute stream is busy: the reduce must wait for it
+            got.mul_(1.0)
+            m.fedavg_bucketed([got], [keep], [out], [P], n, [S], w, mask, [comm_stream(DEV)], BUCKET, apply=True)
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), f"attempt {attempt}: max diff {(got - ref).abs().max().item()}"
+            assert float(keep[0]) == float(np.sum(w, dtype=np.float64))
+            m.check()
+            if attempt == 0:
+                m.abort()
+                m.shrink([0])
+    finally:
+        m.close()
+
+
+def test_rccl_mesh_bucketed_async_error_recovers_bit_equal():
+    """The guard's recovery on the bucketed exchange: async error → abort → re-init → all-reduce of
+    the retained [Σw | Σ w x] → apply; the rows end exactly as ``k_fedavg_local`` writes them."""
+    from myfyp_amd.parallel.weights_plane import comm_stream
+
+    saved = (Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT)
+    Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = 30.0, 10.0
+    Federation.reset()
+    try:
+        fed = Federation.init(devices=["cuda:0"], mesh_backend="rccl")
+        P = 8
+        n, S, base, w, mask, ref = _stacked_case(P, 31)
+        rows = base.clone()
+        keep = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+        out = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+        fed.mesh.fedavg_bucketed([rows], [keep], [out], [P], n, [S], w, mask, [comm_stream(DEV)], BUCKET)
+        fed.mesh_track("fedavg", lambda: fed.mesh.fedavg_bucketed_retry([rows], [keep], [out], [P], n, [S], mask))
+        fed.mesh.inject_error(0)
+        assert fed.mesh_confirm() is True
+        torch.cuda.synchronize()
+        assert fed.mesh_guard.recoveries == 1 and fed.mesh_members == [0]
+        assert torch.equal(rows, ref), (rows - ref).abs().max()
+    finally:
+        Federation.reset()
+        Settings.COLLECTIVE_TIMEOUT, Settings.FAILURE_TIMEOUT = saved
+
+
+def test_rccl_mesh_delayed_averaging_lands_next_round():
+    """Delayed averaging on the RCCL mesh: snapshot, exchange on the comm stream with no apply
+    (the compute stream keeps training: a local step is added meanwhile), then the land launch
+    waits on the exchange and writes x + avg - snap, the snapshot following."""
+    from myfyp_amd.parallel.weights_plane import comm_stream
+
+    P = 4
+    n, S, base, w, mask, ref = _stacked_case(P, 41)  # ref: the weighted mean in every row
+    m = _mesh()
+    try:
+        rows = base.clone()
+        snap = torch.zeros(P * n, dtype=torch.float32, device=DEV)
+        keep = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+        out = torch.zeros(n + 4, dtype=torch.float32, device=DEV)
+        m.delayed_land([rows], [snap], [out], [P], n, [S], n, mask, False)
+        m.fedavg_bucketed([snap], [keep], [out], [P], n, [n], w, mask, [comm_stream(DEV)], BUCKET, apply=False)
+        rows[:, :n].add_(0.125)  # the next local epoch, beside the exchange
+        m.delayed_land([rows], [snap], [out], [P], n, [S], n, mask, True)
+        torch.cuda.synchronize()
+        want = ref[:, :n] + 0.125
+        assert torch.allclose(rows[:, :n], want, rtol=1e-5, atol=1e-5), (rows[:, :n] - want).abs().max()
+        assert torch.equal(snap.view(P, n), rows[:, :n])
+        assert torch.equal(rows[:, n:], base[:, n:])
+        m.check()
+    finally:
+        m.close()
+
+
+def test_virtual_mesh_bucketed_fedavg_matches_float64():
+    """Two virtual members on cuda:0 (HostMesh, GPU members): the bucketed exchange's launches with
+    a stream-ordered sum in place of RCCL give the float64 weighted mean of both members' rows."""
+    from myfyp_amd.parallel.device_mesh import HostMesh
+    from myfyp_amd.parallel.weights_plane import comm_stream
+
+    m = HostMesh([DEV, DEV])
+    n, S, b0, w0, mask0, _ = _stacked_case(3, 51)
+    _, _, b1, _, _, _ = _stacked_case(2, 52)
+    w = np.array([1.0, 2.0, 0.0, 4.0, 5.0], dtype=np.float32)
+    mask = np.ones(5, dtype=np.float32)
+    keeps = [torch.zeros(n + 4, device=DEV) for _ in range(2)]
+    outs = [torch.zeros(n + 4, device=DEV) for _ in range(2)]
+    r0, r1 = b0.clone(), b1.clone()
+    m.fedavg_bucketed([r0, r1], keeps, outs, [3, 2], n, [S, S], w, mask, [comm_stream(DEV)] * 2, BUCKET)
+    torch.cuda.synchronize()
+    allr = torch.cat([b0[:, :n], b1[:, :n]]).double()
+    want = (torch.from_numpy(w).double().to(DEV)[:, None] * allr).sum(0) / float(w.sum())
+    for r in (r0, r1):
+        assert torch.allclose(r[:, :n].double(), want.expand(r.shape[0], n), rtol=1e-5, atol=1e-5)
+
+
+def test_mesh_workflow_rccl_g1_delayed_averaging_learns():
+    """4 fused peers on the one-GPU RCCL mesh with DELAYED_AVERAGING: every round's exchange runs on
+    the comm stream beside the next local epoch and lands a round later (the last round aggregates
+    exactly); the models agree at the end and learn."""
+    saved = Settings.DELAYED_AVERAGING
+    Settings.DELAYED_AVERAGING = True
+    try:
+        final, ngroups, _, calls, hist = _mesh_run(["cuda:0"], "rccl", rounds=4)
+    finally:
+        Settings.DELAYED_AVERAGING = saved
+    assert ngroups == 1 and calls >= 4
+    assert min(final) > 0.75, final
+    assert all(h.count("RoundFinishedStage") == 4 for h in hist)
