@@ -319,7 +319,9 @@ class MLPGroup:
         elif os.environ.get("MYFYP_F32_XSPLIT", "1") != "0" and self.B == 64 and self.handles:
             # measured (profiles/r6_xr): 1 peer K split 8 628.8 vs 612.2 rounds/s at K split 1, 2 peers
             # K split 4 657.9 vs 622.7; 4 peers K split 2 612.8 vs 620.3 (loses: stays at 1)
-            used = max(self.handles) + 1  # peer slots one launch covers
+            # peer slots on this PHYSICAL device: a virtual mesh puts several groups on one GPU,
+            # whose launches then share its XCDs (one XCD per peer: K split 1)
+            used = self._device_peer_slots()
             ks = 8 if used <= 1 else 4 if used <= 2 else 1
         else:
             ks = 1
@@ -344,6 +346,19 @@ class MLPGroup:
             self._bind_data()
             self._bound_version = self._data_version
             self._steps_pe = None
+
+    def _device_peer_slots(self) -> int:
+        """Peer slots every MLP group on this group's physical device covers (its own launch's, plus
+        those of the other mesh ranks a virtual mesh placed on the same GPU)."""
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        used = max(self.handles) + 1 if self.handles else 0
+        with MLPGroup._lock:
+            others = [g for g in MLPGroup._groups.values() if g is not self and g.device.type == "cuda"
+                      and (g.device.index if g.device.index is not None else idx) == idx]
+        for g in others:
+            if g.handles:
+                used += max(g.handles) + 1
+        return max(1, used)
 
     def fedavg_buffer(self) -> torch.Tensor:
         """Device scratch of numel + 1 floats for the stacked FedAvg (weighted sum | Σw)."""
