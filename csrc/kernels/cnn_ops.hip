@@ -25,10 +25,19 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 // ------------------------------------------------------------------------------------------------
 // input: x_p[perm_p[offset + b]] (u8 HWC) -> bf16 [B][H][W][Cp] * scale ; labels -> int32; nb[p]
 // ------------------------------------------------------------------------------------------------
+// stop / fit_id (nullable): an interrupted fit (reference: a Lightning fit stopped mid-epoch,
+// lightning_learner.py:110-114). stop is host-pinned memory the host writes while the epoch runs;
+// a peer whose stop word equals its current fit id gets an empty batch from this step on, so every
+// later kernel of the step (optimizer included: it skips peers with nb = 0) leaves it alone.
 __global__ void k_input_prep(const uint8_t* const* xs, const int64_t* const* ys, const int* n_samples, const int* perm, int64_t perm_ps,
-                             int offset, int B, int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb) {
+                             int offset, int B, int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb,
+                             const int* stop, const int* fit_id) {
   const int peer = blockIdx.y;
-  const int n = n_samples[peer];
+  int n = n_samples[peer];
+  if (stop != nullptr) {
+    const int fid = fit_id[peer];
+    if (fid != 0 && __hip_atomic_load(stop + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == fid) n = 0;
+  }
   const int valid = max(0, min(B, n - offset));
   if (blockIdx.x == 0 && threadIdx.x == 0) nb[peer] = valid;
   const int64_t pix = (int64_t)B * H * W;
@@ -737,9 +746,10 @@ static inline int ew_row_blocks(int max_rows, int Cp) {
 
 extern "C" {
 int cnn_input_prep(const uint8_t* const* xs, const int64_t* const* ys, const int* n_samples, const int* perm, int64_t perm_ps, int offset, int B,
-                   int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb, int peers, void* s) {
+                   int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb, int peers, void* s, const int* stop,
+                   const int* fit_id) {
   hipLaunchKernelGGL(k_input_prep, dim3(ew_blocks((int64_t)B * H * W * (Cp / 8)), peers), dim3(256), 0, (hipStream_t)s, xs, ys, n_samples, perm,
-                     perm_ps, offset, B, H, W, C, Cp, scale, out, out_ps, labels, nb);
+                     perm_ps, offset, B, H, W, C, Cp, scale, out, out_ps, labels, nb, stop, fit_id);
   return ok();
 }
 int cnn_bn_finalize(const float* stats, int64_t stats_ps, int rows, const int* nb, int hw, const float* gamma, const float* beta, int64_t param_ps,

@@ -1717,7 +1717,12 @@ __device__ __forceinline__ bf16x8 frag_tr_rows(const bf16* base, int col0, int r
 
 // W: image width; HI: image height when a K step spans several whole images (H * W < 64: one
 // padded patch per image, NI images per step), 0 when it is 64 / W rows of one image
-template <int W, int HI, bool PRO>
+// PF: global loads in flight ahead of the K step being computed. PF = 1: the next K step's loads are
+// issued at the start of this one (one register stage). PF = 2: two register stages alternate, the
+// loads two K steps ahead — a K step's 36 MFMAs per wave (~1150 cycles per SIMD) are shorter than a
+// loaded HBM round trip, so at PF = 1 every K step waited for its own operands
+// (scripts/probes/wgrad_atomic_share.py, profiles/r6d_wgrad).
+template <int W, int HI, bool PRO, int PF = 1>
 __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int splits, int tiles_co, int tiles_ci) {
   constexpr int C = 64;
   constexpr int NI = HI ? 64 / (HI * W) : 1;    // images per K step
@@ -1747,11 +1752,14 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
   const int wco = wave & 1, wn = wave >> 1;
   const __amdgpu_buffer_rsrc_t rs_dy = conv_rsrc(a.dy + peer * a.dy_ps), rs_x = conv_rsrc(a.x + peer * a.x_ps);
 
-  uint4 rdy, rp[PPT];
+  struct Stage {  // one K step's operand chunks of this thread, in registers
+    uint4 dy, p[PPT];
+    unsigned pok;
+  };
+  Stage st0, st1;
   // PRO: x is a BatchNorm input y and the B operand is relu(y*sc + sh), applied once per staged X
   // pixel (as k_conv_fwd_halo); this thread's chunks are channels ci0 + 8 (tid & 7) .. +7
   float psc[8], psh[8];
-  unsigned pok = 0;
   if (PRO) {
     const float* pro = a.pro_ss + peer * a.pro_ss_ps;
 #pragma unroll
@@ -1760,11 +1768,12 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       psh[j] = pro[a.x_c + ci0 + (tid & 7) * 8 + j];
     }
   }
-  auto load = [&](int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows / images)
+  auto load = [&](Stage& S, int m0) {  // K step starting at pixel m0 (a multiple of 64: whole image rows / images)
     {
       const int row = tid >> 3, ch = tid & 7;
-      rdy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * a.dy_c + co0 + ch * 8) * 2 : CONV_OOB);
+      S.dy = conv_ld16(rs_dy, m0 + row < kend ? ((m0 + row) * a.dy_c + co0 + ch * 8) * 2 : CONV_OOB);
     }
+    S.pok = 0;
     const int img0 = m0 / HW, h0 = HI ? 0 : (m0 - img0 * HW) / W;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
@@ -1775,19 +1784,19 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
       const int h = h0 - 1 + pr, w = pc - 1, img = img0 + il;
       // images past the peer's batch (the last step of a multi-image K loop) load zeros
       const bool ok = e < PCH && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)W && img < nb;
-      rp[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * a.x_c + ci0 + ch * 8) * 2 : CONV_OOB);
-      if (PRO) pok = ok ? (pok | (1u << i)) : (pok & ~(1u << i));
+      S.p[i] = conv_ld16(rs_x, ok ? (((img * a.H + h) * W + w) * a.x_c + ci0 + ch * 8) * 2 : CONV_OOB);
+      if (PRO && ok) S.pok |= 1u << i;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Stage& S, int buf) {
     bf16* dys = lds + buf * STG;
     bf16* pat = dys + DYE;
-    *reinterpret_cast<uint4*>(dys + tr_off<64>(tid >> 3, (tid & 7) * 8)) = rdy;
+    *reinterpret_cast<uint4*>(dys + tr_off<64>(tid >> 3, (tid & 7) * 8)) = S.dy;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int e = tid + 512 * i;
-      uint4 v = rp[i];
-      if (PRO && ((pok >> i) & 1u)) v = bn_relu8(v, psc, psh);
+      uint4 v = S.p[i];
+      if (PRO && ((S.pok >> i) & 1u)) v = bn_relu8(v, psc, psh);
       if (e < PCH) *reinterpret_cast<uint4*>(pat + tr_off<64>(e >> 3, (e & 7) * 8)) = v;
     }
   };
@@ -1800,13 +1809,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
     for (int f = 0; f < 9; ++f) acc[i][f] = zero4();
 
   const int nk = (kend - kbeg + 63) / 64;
-  load(kbeg);
-  store(0);
-  __syncthreads();
-  int cur = 0;
   const int g = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load(kbeg + (kt + 1) * 64);
+  auto compute = [&](int cur) {
     const bf16* dys = lds + cur * STG;
     const bf16* pat = dys + DYE;
 #pragma unroll
@@ -1827,9 +1831,34 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_halo(WgradArgs a, int spl
         for (int i = 0; i < 2; ++i) acc[i][f] = mfma_bf16(af[i], b, acc[i][f]);
       }
     }
-    if (kt + 1 < nk) store(cur ^ 1);
+  };
+  load(st0, kbeg);
+  store(st0, 0);
+  if (PF == 1) {
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load(st0, kbeg + (kt + 1) * 64);
+      compute(cur);
+      if (kt + 1 < nk) store(st0, cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // buf[kt & 1] holds K step kt; the register stage of K step kt + 1 is in flight. Two register
+    // stages alternate (unrolled by two: register arrays need static indices)
+    if (nk > 1) load(st1, kbeg + 64);
+    __syncthreads();
+    auto step = [&](int kt, Stage& free_st, const Stage& next_st) {
+      if (kt + 2 < nk) load(free_st, kbeg + (kt + 2) * 64);  // free_st's K step kt is already in LDS
+      compute(kt & 1);
+      if (kt + 1 < nk) store(next_st, (kt + 1) & 1);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, st0, st1);
+      if (kt + 1 < nk) step(kt + 1, st1, st0);
+    }
   }
   // Wf-layout gradient [co][tap][ci]: block column n = tap * 64 + local ci
   float* grad = a.grad + peer * a.grad_ps;
@@ -1878,6 +1907,16 @@ static int g_wgrad_halo = [] {
 extern "C" int conv_set_wgrad_halo(int on) {
   const int old = g_wgrad_halo;
   if (on >= 0) g_wgrad_halo = on ? 1 : 0;
+  return old;
+}
+// halo wgrad prefetch depth (k_conv_wgrad_halo PF): MYFYP_WGRAD_PF=1|2, conv_set_wgrad_pf (tests / A-B)
+static int g_wgrad_halo_pf = [] {
+  const char* e = getenv("MYFYP_WGRAD_PF");
+  return (e != nullptr && atoi(e) == 2) ? 2 : 1;
+}();
+extern "C" int conv_set_wgrad_pf(int pf) {
+  const int old = g_wgrad_halo_pf;
+  if (pf == 1 || pf == 2) g_wgrad_halo_pf = pf;
   return old;
 }
 // widest channel count the halo wgrad takes (0 = any multiple of 64; MYFYP_WGRAD_HALO_MAXC, the A/B knob)
@@ -2244,10 +2283,15 @@ extern "C" int conv_wgrad_launch(const WgradArgs* pa, int peers, int splits, voi
       a.Ho == a.H && a.Wo == a.W && halo_shape && (g_wgrad_halo_max_c == 0 || (a.x_c <= g_wgrad_halo_max_c && a.dy_c <= g_wgrad_halo_max_c))) {
     const int tco = a.dy_c / 64, tci = a.x_c / 64;
     dim3 hg(splits * tco * tci, 1, peers), hb(512);
-#define WH_LAUNCH(W_, HI_)                                                                                          \
-  do {                                                                                                               \
-    if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, true>), hg, hb, 0, s, a, splits, tco, tci); \
-    else hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, false>), hg, hb, 0, s, a, splits, tco, tci);                  \
+#define WH_LAUNCH(W_, HI_)                                                                                                  \
+  do {                                                                                                                       \
+    if (g_wgrad_halo_pf == 2) {                                                                                              \
+      if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, true, 2>), hg, hb, 0, s, a, splits, tco, tci);  \
+      else hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, false, 2>), hg, hb, 0, s, a, splits, tco, tci);                    \
+    } else {                                                                                                                 \
+      if (a.pro_ss != nullptr) hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, true, 1>), hg, hb, 0, s, a, splits, tco, tci);  \
+      else hipLaunchKernelGGL((k_conv_wgrad_halo<W_, HI_, false, 1>), hg, hb, 0, s, a, splits, tco, tci);                    \
+    }                                                                                                                        \
   } while (0)
     if (a.W == 4) WH_LAUNCH(4, 4);  // 4 images per K step
     else if (a.W == 8) WH_LAUNCH(8, 0);

@@ -286,7 +286,13 @@ class TorchLearner(Learner):
         return steps, mean
 
     def interrupt_fit(self) -> None:
+        """Stop the running fit (reference ``lightning_learner.py:110-114``): the autograd loop
+        checks the flag every batch; a fused CNN fit already on the device stops at its next step
+        (``CNNEngineHandle.interrupt``). A fused MLP epoch (~1.5 ms on the device) runs to its end."""
         self._interrupt.set()
+        eng = self._engine
+        if eng is not None and hasattr(eng, "interrupt"):
+            eng.interrupt()
 
     # ------------------------------------------------------------------ evaluate
     @torch.no_grad()

@@ -105,6 +105,7 @@ _SIGS = {
     "conv_set_dma": (c_int, [c_int]),
     "conv_set_dma_wgs": (c_int, [c_int]),
     "conv_set_wgrad_halo": (c_int, [c_int]),
+    "conv_set_wgrad_pf": (c_int, [c_int]),
     "conv_set_fwd_halo": (c_int, [c_int]),
     "conv_gemm_stats_rows": (c_int, [c_int, c_int, c_int]),
     "conv_bnb_rows": (c_int, []),
@@ -112,7 +113,8 @@ _SIGS = {
     "conv_wt_flip_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "conv_wt_flip_multi_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "conv_wt_flip_parity_launch": (c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
-    "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+    "cnn_input_prep": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p,
+                               c_void_p, c_void_p]),
     "cnn_bn_finalize": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "cnn_bn_act": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_int, c_void_p]),
     "cnn_bn_bwd_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
@@ -296,6 +298,8 @@ class CNNGroup:
         self._data_version = 0
         self._bound_version = -1
         self.lenet_fused = False
+        self._fit_seq = 0  # fit ids (interrupt_fit): one per fused fit, 0 = none
+        self._slot_fit: Dict[int, int] = {}
         self._describe(template)
         self._alloc(capacity)
         self.fit_gang = _Gang(self._run_fit_batch, lambda: set(self.handles))
@@ -409,6 +413,12 @@ class CNNGroup:
         self.shadow = torch.zeros(capacity, self.shadow_numel, dtype=torch.bfloat16, device=dev)
         self.gradf = torch.zeros(capacity, self.shadow_numel, dtype=torch.float32, device=dev)
         self.shadow_t = torch.zeros_like(self.shadow) if self.dgrad_fwd else None  # MODE 4 weights (k_conv_wt_flip)
+        # interrupted fits: a stop word per slot in host-pinned memory (written by interrupt() while
+        # the epoch runs, read by every step's input kernel) and the device copy of each slot's
+        # current fit id (uploaded in stream order at the fit's start: a stale stop word never
+        # matches a later fit)
+        self._stop = torch.zeros(capacity, dtype=torch.int32, pin_memory=dev.type == "cuda")
+        self._fit_id = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.s2_fwd = os.environ.get("MYFYP_CNN_S2_FWD", "0") == "1"  # MODE 5 stride-2 dgrads (see conv())
         self.capacity = capacity
         for slot, h in self.handles.items():
@@ -808,7 +818,8 @@ class CNNGroup:
         perm = self.perm if train else None
         _chk(lib.cnn_input_prep(_p(t["xs"] if train else t["xts"]), _p(t["ys"] if train else t["yts"]), _p(t["n"] if train else t["nt"]), _p(perm),
                                 self.nmax if train else 0, offset, B, self.in_h, self.in_w, self.in_c, cp0, self.in_scale, x0.data_ptr(), x0.shape[1],
-                                self.labels.data_ptr(), self.nb.data_ptr(), P, self._stream()), "input_prep")
+                                self.labels.data_ptr(), self.nb.data_ptr(), P, self._stream(), _p(self._stop) if train else None,
+                                _p(self._fit_id) if train else None), "input_prep")
         return x0
 
     def _forward_resnet(self, x0: torch.Tensor, train: bool) -> torch.Tensor:
@@ -1146,6 +1157,10 @@ class CNNGroup:
             # inactive slots must not train: zero their sample count for this fit
             n_host = [self.n_train[s] if s in batch else 0 for s in range(self.capacity)]
             self._h2d(self.tab["n"], n_host)
+            self._fit_seq += 1
+            for slot in batch:
+                self._slot_fit[slot] = self._fit_seq
+            self._h2d(self._fit_id, [self._fit_seq if s in batch else 0 for s in range(self.capacity)])
             self.mom.zero_()
             self._shadow_sync()
             self.stat.zero_()
@@ -1168,6 +1183,16 @@ class CNNGroup:
             out[slot] = (int((self.n_train[slot] + self.B - 1) // self.B) * epochs,
                          raw.map(lambda r, s=slot, n=n: (float(r[0][s, 0]) / n, float(r[0][s, 1]) / n)))
         return out
+
+    def interrupt(self, slot: int) -> None:
+        """Stop ``slot``'s running fused fit at the next step (reference: a Lightning fit stopped
+        mid-epoch, ``lightning_learner.py:110-114``): its stop word takes the fit's id, and the
+        step's input kernel gives that peer an empty batch from then on (no forward, no gradient,
+        no optimizer update); the other peers of the gang train on. LeNet-5's one-kernel step and
+        a fit already finished are not affected."""
+        fid = self._slot_fit.get(slot)
+        if fid:
+            self._stop[slot] = fid
 
     def _h2d(self, dst: torch.Tensor, values) -> None:
         """Stream-ordered upload of a small host list (pinned staging; the caching host allocator
@@ -1316,6 +1341,10 @@ class CNNEngineHandle:
 
     def close(self) -> None:
         self.group.detach(self.slot)
+
+    def interrupt(self) -> None:
+        """Stop this peer's running fused fit at the next step (``CNNGroup.interrupt``)."""
+        self.group.interrupt(self.slot)
 
     def flat_params(self) -> torch.Tensor:
         return self.group.params[self.slot, : self.group.n_params]

@@ -863,3 +863,76 @@ def test_bn_prologue_in_patch_kernels_matches_materialised(h, n):
     (g_m, p_m), (g_y, p_y) = dgrad(True), dgrad(False)
     assert torch.equal(g_m, g_y)
     torch.testing.assert_close(p_y, p_m, rtol=1e-5, atol=1e-3)
+
+
+def test_resnet_fused_fit_interrupted_mid_epoch():
+    """``interrupt_fit`` on a fused CNN fit already on the device (reference: a Lightning fit stopped
+    mid-epoch, lightning_learner.py:110-114): the device is held busy so the epoch has not started
+    when peer 0 is interrupted; peer 0's parameters and BN running statistics stay exactly as they
+    were while peer 1 of the same gang trains on; the next fit (a new fit id) trains peer 0 again."""
+    import threading
+
+    from myfyp_amd.models import ResNet18
+
+    learners, _, _ = _make_learners(lambda i: ResNet18(seed=40 + i), 2, 64 * 6, 64, 64, 0.05, momentum=0.9)
+
+    def fit_all():
+        ths = [threading.Thread(target=lr_.fit) for lr_ in learners]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+
+    def state(i):
+        m = learners[i].model.get_model()
+        return [t.detach().clone() for t in list(m.parameters()) + [b for n, b in m.named_buffers() if "running" in n]]
+
+    fit_all()  # first fit: eager run + graph capture
+    torch.cuda.synchronize()
+    s0, s1 = state(0), state(1)
+    torch.cuda._sleep(200_000_000)  # the epoch queued behind this cannot start before the interrupt
+    fit_all()
+    learners[0].interrupt_fit()
+    torch.cuda.synchronize()
+    a0, a1 = state(0), state(1)
+    assert all(torch.equal(x, y) for x, y in zip(s0, a0)), "interrupted peer changed"
+    assert any(not torch.equal(x, y) for x, y in zip(s1, a1)), "the other peer did not train"
+    fit_all()  # a later fit is not affected by the stale stop word
+    torch.cuda.synchronize()
+    assert any(not torch.equal(x, y) for x, y in zip(a0, state(0))), "peer 0 did not train after the interrupted fit"
+
+
+@pytest.mark.parametrize("c,h,n,splits", [(64, 32, 2, 1), (64, 32, 3, 5), (128, 16, 3, 2), (256, 8, 5, 3), (512, 4, 16, 1), (64, 8, 3, 2)])
+def test_wgrad_halo_prefetch_depths_agree(c, h, n, splits):
+    """k_conv_wgrad_halo with two register stages in flight (PF 2, the default) against one (PF 1,
+    pinned to torch by test_conv_fwd_dgrad_wgrad_vs_torch's earlier rounds): K loops of 1, 2 and odd
+    step counts; equal up to the split-K atomics' order."""
+    from myfyp_amd.parallel.cnn_engine import WgradArgs, _lib
+
+    lib = _lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(c + h)
+    x = torch.randn(1, n * h * h * c, device=dev).to(torch.bfloat16)
+    dy = torch.randn(1, n * h * h * c, device=dev).to(torch.bfloat16)
+    M = n * h * h
+    k_per = max(64, ((M + splits - 1) // splits + 63) // 64 * 64)
+    sp = (M + k_per - 1) // k_per
+    grads = {}
+    old = lib.conv_set_wgrad_pf(1)
+    try:
+        for pf in (1, 2):
+            lib.conv_set_wgrad_pf(pf)
+            g = torch.zeros(1, c * 9 * c, device=dev)
+            a = WgradArgs()
+            a.dy, a.dy_ps, a.x, a.x_ps = dy.data_ptr(), dy.shape[1], x.data_ptr(), x.shape[1]
+            a.H, a.W, a.x_c, a.Ho, a.Wo, a.dy_c = h, h, c, h, h, c
+            a.R, a.S, a.stride, a.pad = 3, 3, 1, 1
+            a.grad, a.grad_ps, a.accumulate, a.k_per_split, a.max_batch = g.data_ptr(), g.shape[1], int(sp > 1), k_per, n
+            assert lib.conv_wgrad_launch(ctypes.byref(a), 1, sp, torch.cuda.current_stream().cuda_stream) == 0
+            torch.cuda.synchronize()
+            grads[pf] = g
+    finally:
+        lib.conv_set_wgrad_pf(old)
+    if sp == 1:
+        assert torch.equal(grads[1], grads[2])
+    else:
+        torch.testing.assert_close(grads[2], grads[1], rtol=1e-5, atol=1e-4 * float(grads[1].abs().max()))
+    assert float(grads[1].abs().max()) > 0
