@@ -1912,7 +1912,7 @@ extern "C" int conv_set_wgrad_halo(int on) {
 // halo wgrad prefetch depth (k_conv_wgrad_halo PF): MYFYP_WGRAD_PF=1|2, conv_set_wgrad_pf (tests / A-B)
 static int g_wgrad_halo_pf = [] {
   const char* e = getenv("MYFYP_WGRAD_PF");
-  return (e != nullptr && atoi(e) == 2) ? 2 : 1;
+  return (e != nullptr && atoi(e) == 1) ? 1 : 2;
 }();
 extern "C" int conv_set_wgrad_pf(int pf) {
   const int old = g_wgrad_halo_pf;

@@ -291,6 +291,13 @@ class CNNGroup:
         self.flip_batch = os.environ.get("MYFYP_CNN_FLIP_BATCH", "1") != "0"
         self._flipped: frozenset = frozenset()
         self._flip_tables = None
+        # ResNet backward: every weight gradient on a second stream (a branch of the captured step
+        # graph), forked after its dY is written and joined before the optimizer. The dgrad chain
+        # is the step's critical path; the weight gradients are leaves, so their workgroups fill
+        # the CUs the chain's kernels leave idle (partial waves, epilogues, split-K atomic tails)
+        # instead of running between them. MYFYP_CNN_WGRAD_STREAM=0: one stream
+        self.wgrad_stream = os.environ.get("MYFYP_CNN_WGRAD_STREAM", "0") != "0"
+        self._wg_side: Optional[torch.cuda.Stream] = None
         self.wgrad_tpc = int(os.environ.get("MYFYP_WGRAD_TPC", "2"))  # measured: 2 -> 75.6 ms wgrad, 4 -> 78.4, 8 -> 89.8 (scripts/probes/wgrad_tpc.sh)
         self.wgrad_tune = os.environ.get("MYFYP_WGRAD_TUNE", "1") != "0"  # per-layer split-K timed on the device (_tune_wgrad)
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -881,10 +888,30 @@ class CNNGroup:
         batched = self.flip_batch and self.dgrad_fwd and self.shadow_t is not None
         if batched:
             self._flip_all([self.fc] + [c for blk in self.blocks for c in (blk[0], blk[2])])
+        side = None
+        if self.wgrad_stream and self.device.type == "cuda":
+            if self._wg_side is None:
+                self._wg_side = torch.cuda.Stream(self.device)
+            side = self._wg_side
+        self._wg_branch = side
         try:
             self._backward_resnet_pass(dlogits)
         finally:
             self._flipped = frozenset()
+            self._wg_branch = None
+            if side is not None:  # join: the optimizer reads every weight gradient
+                torch.cuda.current_stream(self.device).wait_stream(side)
+
+    def _wgrad_b(self, L: ConvL, dy: torch.Tensor, x: torch.Tensor, pro: Optional["BNL"] = None) -> None:
+        """``wgrad`` on the backward's side stream when one is open (forked here: dY and x are final
+        on the current stream; nothing the branch reads is written again before the join)."""
+        side = getattr(self, "_wg_branch", None)
+        if side is None:
+            self.wgrad(L, dy, x, pro)
+            return
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self.wgrad(L, dy, x, pro)
 
     def _backward_resnet_pass(self, dlogits: torch.Tensor) -> None:
         B, lib = self.B, _lib()
@@ -892,7 +919,7 @@ class CNNGroup:
         pooled = self.act("pooled", B, fc.cp_in)
         dpooled = self.act("dpooled", B, fc.cp_in)
         self.conv(fc, dlogits, dpooled, mode=1)
-        self.wgrad(fc, dlogits, pooled)
+        self._wgrad_b(fc, dlogits, pooled)
         self.bias_grad(fc, dlogits, 1)
         last = self.blocks[-1][2]
         hw = last.ho * last.wo
@@ -921,7 +948,7 @@ class CNNGroup:
                 self.bn_bwd(bns, d, mask_out, ys, dys, hw1, pre_reduced=pre, finalized=pre and ff)
                 dsc = self.act(f"dsc_{bi}", B * c1.h * c1.w, c1.cp_in)
                 self.conv(cs, dys, dsc, mode=1)
-                self.wgrad(cs, dys, a_in)
+                self._wgrad_b(cs, dys, a_in)
                 resid = dsc
             elif pre:
                 self.bn_bwd(bn2, d, None, y2, dy2, hw1, pre_reduced=True, finalized=ff)
@@ -934,19 +961,19 @@ class CNNGroup:
             dy1 = self.act(f"dy1_{bi}", B * hw1, c1.cp_out)
             if halo1 and fold:  # a1 never written: mask from y1 in the dgrad epilogue, BN1 in the wgrad staging
                 self.conv(c2, dy2, da1, mode=1, bnb=(None, [(bn1, y1)]), bnb_mask_bn=bn1, bnb_fin=ff)
-                self.wgrad(c2, dy2, y1, pro=bn1)
+                self._wgrad_b(c2, dy2, y1, pro=bn1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True, finalized=ff)
             elif self.fuse_bn1 or halo1:
                 self.conv(c2, dy2, da1, mode=1)
-                self.wgrad(c2, dy2, y1, pro=bn1)
+                self._wgrad_b(c2, dy2, y1, pro=bn1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, mask_from_y=True)
             elif fold:
                 self.conv(c2, dy2, da1, mode=1, bnb=(a1, [(bn1, y1)]), bnb_fin=ff)
-                self.wgrad(c2, dy2, a1)
+                self._wgrad_b(c2, dy2, a1)
                 self.bn_bwd(bn1, da1, None, y1, dy1, hw1, pre_reduced=True, finalized=ff)
             else:
                 self.conv(c2, dy2, da1, mode=1)
-                self.wgrad(c2, dy2, a1)
+                self._wgrad_b(c2, dy2, a1)
                 self.bn_bwd(bn1, da1, a1, y1, dy1, hw1)
             bnb = None
             if fold:  # d_in is the gradient of the previous block's (or the stem's) ReLU(BN) output
@@ -961,7 +988,7 @@ class CNNGroup:
                     st = self.stem
                     bnb = (a_in, [(self.stem_bn, self.act("y_stem", B * st.ho * st.wo, st.cp_out))])
             self.conv(c1, dy1, d_in, mode=1, resid=resid, bnb=bnb, bnb_fin=ff and bnb is not None)
-            self.wgrad(c1, dy1, a_in)
+            self._wgrad_b(c1, dy1, a_in)
             d = d_in
             pre = bnb is not None
         L, bn = self.stem, self.stem_bn
@@ -971,7 +998,7 @@ class CNNGroup:
             self.bn_bwd(bn, d, None, self.act("y_stem", B * hw, L.cp_out), dys, hw, pre_reduced=True, finalized=ff)
         else:
             self.bn_bwd(bn, d, self.act("a_stem", B * hw, L.cp_out), self.act("y_stem", B * hw, L.cp_out), dys, hw)
-        self.wgrad(L, dys, self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c)))
+        self._wgrad_b(L, dys, self.act("x0", B * self.in_h * self.in_w, _cp(self.in_c)))
 
     def _forward_lenet(self, x0: torch.Tensor, train: bool) -> torch.Tensor:
         B, lib, P = self.B, _lib(), self.capacity
