@@ -33,13 +33,14 @@ __global__ void k_input_prep(const uint8_t* const* xs, const int64_t* const* ys,
                              int offset, int B, int H, int W, int C, int Cp, float scale, bf16* out, int64_t out_ps, int* labels, int* nb,
                              const int* stop, const int* fit_id) {
   const int peer = blockIdx.y;
-  int n = n_samples[peer];
-  if (stop != nullptr) {
-    const int fid = fit_id[peer];
-    if (fid != 0 && __hip_atomic_load(stop + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == fid) n = 0;
-  }
+  const int n = n_samples[peer];
   const int valid = max(0, min(B, n - offset));
-  if (blockIdx.x == 0 && threadIdx.x == 0) nb[peer] = valid;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // one host-memory read per peer and step: the batch this block stages below is then simply unused
+    const int fid = stop != nullptr ? fit_id[peer] : 0;
+    const bool stopped = fid != 0 && __hip_atomic_load(stop + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == fid;
+    nb[peer] = stopped ? 0 : valid;
+  }
   const int64_t pix = (int64_t)B * H * W;
   const int cpp = Cp / 8;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pix * cpp; i += (int64_t)gridDim.x * blockDim.x) {
