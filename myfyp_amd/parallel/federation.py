@@ -830,6 +830,12 @@ class Federation:
             t0 = time.perf_counter()
             ranks, _ = self.shm.allgather_members(None, float(Settings.FAILURE_TIMEOUT))
             self.record("cp_sync_members", time.perf_counter() - t0)
+            if ranks != self.members and self._pending:
+                # a collective left unconfirmed by the confirmation lag still runs on the old group:
+                # confirm it first (recovering if it failed), as when it was confirmed before this
+                # gather, then agree again — every survivor saw the same change and takes this path
+                self.confirm_collectives()
+                ranks, _ = self.shm.allgather_members(None, float(Settings.FAILURE_TIMEOUT))
             self._apply_members(ranks)
         return self.members
 
@@ -982,7 +988,7 @@ class Federation:
             if not outer:
                 # a confirmation that ended in an agreement gather already agreed on the members
                 # (every member took part in it): no second membership gather right after it
-                if not self.confirm_collectives():
+                if not self.confirm_collectives(force=False):
                     self.sync_members()
                 self._frozen = (self.departed, list(self.members))
             try:
@@ -1139,9 +1145,12 @@ class Federation:
         members = list(self._frozen[1]) if self._frozen is not None else list(self.members)
         self._pending.append((works, members, retry, self._pg))
 
-    def confirm_collectives(self) -> bool:
+    def confirm_collectives(self, force: bool = True) -> bool:
         """Confirm the deferred device collectives (every member completed them); on a failure
         the groups are rebuilt and the retained-input retry runs (synchronously confirmed).
+
+        ``force`` False (the weights-section entry, ``Settings.CONFIRM_LAG``): a newest collective
+        not yet complete on the device waits one more section; the others are confirmed.
 
         Called at the next weights-section entry: the round's all-reduce r is confirmed while the
         next local epoch r+1 — already queued behind it — runs, so confirming never idles the GPU
@@ -1152,15 +1161,41 @@ class Federation:
         from the same, correct, round-r model."""
         if not self._pending:
             return False
+        # lag (not forced): the newest collective, while still queued behind the running epoch, is
+        # left for the next section (or shutdown), so the round driver keeps launching ahead
+        # instead of waiting for the GPU to reach it; older ones are confirmed now. On a failure the
+        # oldest failed entry's retry re-runs the exchange from the partial sums retained last (the
+        # newest round's) over the survivors, and every newer entry is dropped with the group
+        keep_last = (not force and self._confirm_lag and not self._pending_complete(self._pending[-1]))
+        if keep_last and len(self._pending) == 1:
+            return False
         t0 = time.perf_counter()
         try:
-            self._confirm_pending()
+            self._confirm_pending(keep_last)
         finally:
             self.record("cp_confirm", time.perf_counter() - t0)
         return self._guarded() and not self._is_departed()
 
-    def _confirm_pending(self) -> None:
-        while self._pending:
+    @property
+    def _confirm_lag(self) -> bool:
+        return bool(Settings.CONFIRM_LAG) and os.environ.get("MYFYP_CONFIRM_LAG", "1") != "0"
+
+    @staticmethod
+    def _pending_complete(entry) -> bool:
+        """Non-blocking: every work of a deferred entry has completed on the device (a work that
+        raises counts as complete: confirming it surfaces the failure)."""
+        for w in entry[0]:
+            if w is None:
+                continue
+            try:
+                if not w.is_completed():
+                    return False
+            except Exception:  # noqa: BLE001 — an aborted communicator: confirm now
+                return True
+        return True
+
+    def _confirm_pending(self, keep_last: bool = False) -> None:
+        while len(self._pending) > (1 if keep_last else 0):
             works, members, retry, _ = self._pending.pop(0)
             with self._section_lock:
                 saved = self._frozen

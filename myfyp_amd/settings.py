@@ -114,6 +114,11 @@ class Settings:
     # failure-aware weight collectives (single-node shm control plane): liveness polled while
     # waiting, watchdog abort, agreement on every collective, re-run over the survivors
     COLLECTIVE_FAILOVER: bool = True
+    # deferred confirmation of the device weight collectives (parallel/federation.py
+    # confirm_collectives): the newest one, if not yet complete, waits one more weights section
+    # instead of blocking the round driver until the GPU reaches it (the host stays up to two rounds
+    # ahead; a failure is then recovered one round later). MYFYP_CONFIRM_LAG=0: block as before
+    CONFIRM_LAG: bool = True
     # Channels RCCL may use per collective. RCCL launches one workgroup per channel, so this is also
     # the number of CUs a concurrent RCCL kernel can hold. Federation.init exports it as RCCL's own
     # NCCL_MAX_NCHANNELS / NCCL_MAX_CTAS caps unless the environment already sets them; the cap
@@ -225,6 +230,7 @@ class Settings:
             "SHM_CONTROL_PLANE": "SHM_CONTROL_PLANE",
             "FORCE_COLLECTIVE": "FORCE_COLLECTIVE",
             "COLLECTIVE_FAILOVER": "COLLECTIVE_FAILOVER",
+            "CONFIRM_LAG": "CONFIRM_LAG",
             "RCCL_RESERVED_CUS": "RCCL_RESERVED_CUS",
             "RCCL_MAX_CHANNELS": "RCCL_MAX_CHANNELS",
             "ENGINE_PREWARM": "ENGINE_PREWARM",
