@@ -11,7 +11,8 @@ struct FedAvgWeights {
   float w[FEDAVG_MAX_PEERS];
   float wsum;
 };
-void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s);
+void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s,
+                      float* out2 = nullptr, float* wsum2 = nullptr);
 void fl_fedavg_apply(float* stacked, const float* out, const float* wsum_slot, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s);
 void fl_fedavg_delayed_land(float* stacked, float* snap, int64_t ld_snap, const float* avg, const float* wsum_slot, int P, int64_t n, int64_t ld,
                             unsigned long long mask, hipStream_t s);

@@ -83,11 +83,15 @@ __global__ __launch_bounds__(FL_BLOCK) void k_broadcast_rows(float* __restrict__
 //   apply:  stacked[p*ld + i] = out[i] / max(*wsum_slot, 1e-12) for rows with mask bit p set
 // A bucketed all-reduce calls them per bucket (sub-ranges of out / stacked, bucket 0 carries the
 // weight sum in a slot in front of the data, so bucket k's apply only waits for buckets 0 and k).
+// out2 / wsum2 (nullable): a second copy of the partial sums (the failover's retained input), written
+// by the same pass instead of a separate device copy behind it
 __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ out, float* __restrict__ wsum_slot, const float* __restrict__ stacked,
-                                                             int P, int64_t n, int64_t ld, FedAvgWeights w) {
+                                                             int P, int64_t n, int64_t ld, FedAvgWeights w, float* __restrict__ out2,
+                                                             float* __restrict__ wsum2) {
   const int64_t stride = (int64_t)gridDim.x * FL_BLOCK;
   const int64_t t0 = blockIdx.x * FL_BLOCK + threadIdx.x;
   if (t0 == 0 && wsum_slot != nullptr) *wsum_slot = w.wsum;
+  if (t0 == 0 && wsum2 != nullptr) *wsum2 = w.wsum;
   if ((ld % 4) == 0) {
     const int64_t n4 = n / 4;
     for (int64_t i = t0; i < n4; i += stride) {
@@ -99,12 +103,14 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ 
         acc.x += wp * v.x; acc.y += wp * v.y; acc.z += wp * v.z; acc.w += wp * v.w;
       }
       reinterpret_cast<float4*>(out)[i] = acc;
+      if (out2 != nullptr) reinterpret_cast<float4*>(out2)[i] = acc;
     }
     for (int64_t i = n4 * 4 + t0; i < n; i += stride) {
       float acc = 0.f;
       for (int p = 0; p < P; ++p)
         if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       out[i] = acc;
+      if (out2 != nullptr) out2[i] = acc;
     }
   } else {
     for (int64_t i = t0; i < n; i += stride) {
@@ -112,6 +118,7 @@ __global__ __launch_bounds__(FL_BLOCK) void k_fedavg_reduce(float* __restrict__ 
       for (int p = 0; p < P; ++p)
         if (w.w[p] != 0.f) acc += w.w[p] * stacked[p * ld + i];  // rows of weight 0 are never read (may be uninitialised)
       out[i] = acc;
+      if (out2 != nullptr) out2[i] = acc;
     }
   }
 }
@@ -178,8 +185,9 @@ void fl_fedavg_local(float* stacked, int P, int64_t n, int64_t ld, const FedAvgW
   hipLaunchKernelGGL(k_fedavg_local, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, stacked, P, n, ld, w, mask);
 }
 
-void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, wsum_slot, stacked, P, n, ld, w);
+void fl_fedavg_reduce(float* out, float* wsum_slot, const float* stacked, int P, int64_t n, int64_t ld, const FedAvgWeights& w, hipStream_t s,
+                      float* out2, float* wsum2) {
+  hipLaunchKernelGGL(k_fedavg_reduce, dim3(grid_for((n + 3) / 4)), dim3(FL_BLOCK), 0, s, out, wsum_slot, stacked, P, n, ld, w, out2, wsum2);
 }
 
 void fl_fedavg_apply(float* stacked, const float* out, const float* wsum_slot, int P, int64_t n, int64_t ld, unsigned long long mask, hipStream_t s) {

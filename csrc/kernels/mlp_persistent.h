@@ -57,6 +57,9 @@ int mlp_persistent_f32_x_direct(const MLPArgs& a);
 int mlp_persistent_f32_x_direct_build();  // the build's P32_XDIRECT  // gang layout: 1 owners + heads, 2 owners only          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
-hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true);
+// active (nullable, a.P host flags): launches (and retry launches) are enqueued only for the
+// groups of ppl peers with an active peer; null: every group (graph capture: any later active set)
+hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb, hipStream_t s, bool zero_flags = true,
+                                           const int* active = nullptr);
 // fp32 forward of every active peer's whole test split (loss sum, correct, confusion) in one launch
 void mlp_launch_eval_f32(const MLPArgs& a, int max_rows, hipStream_t s);

@@ -2133,7 +2133,7 @@ extern "C" int mlp_debug_plain_seen(int* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plain_seen), sizeof(g_plain_seen)) == hipSuccess ? 0 : 1;
 }
 
-hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb_in, hipStream_t s, bool zero_flags) {
+hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32Bufs& pb_in, hipStream_t s, bool zero_flags, const int* active) {
   MLPPersistF32Bufs pb = pb_in;
   pb.plain_ok = mlp_plain_pub_mode();
   pb.plain = 0;
@@ -2151,8 +2151,18 @@ hipError_t mlp_launch_persistent_f32_epoch(const MLPArgs& a, const MLPPersistF32
   const size_t lds = persistent_f32_lds_ks(a, KS, rh);
   // groups of ppl peers: one launch each (a launch's gangs must all be co-resident), then the
   // recovery launches (attempt 1): a no-op exit for every gang that did not give up
+  // (a group with no active peer is not launched: at one peer per device and K split 8 the other
+  // seven slots' launches and retries were 14 empty dispatches, ~80 us per round,
+  // profiles/r6k_forced_trace)
+  auto group_live = [&](int p0) {
+    if (active == nullptr) return true;
+    for (int p = p0; p < p0 + ppl && p < a.P; ++p)
+      if (active[p]) return true;
+    return false;
+  };
   for (int attempt = 0; attempt < 2; ++attempt)
     for (int p0 = 0; p0 < a.P; p0 += ppl) {
+      if (!group_live(p0)) continue;
       if (rh) {
         if (KS == 2) {
           if (a.Bpad == 64) launch_f32_bp<64, 2, true>(a, pb, s, p0, lds, attempt);

@@ -359,8 +359,12 @@ struct MLPEngine {
     return mlp_persistent_f32_launch_wgs(a) <= f32_cap;
   }
   int recoveries = 0;
+  // direct epoch launches: the active flags of this epoch (skip groups without an active peer);
+  // null while capturing the epoch graph (it must serve any later active set)
+  const int* launch_active = nullptr;
+  int launch_active_buf[MLP_CTL_MAX];
   int launch_epoch_kernel(hipStream_t s, bool zero_flags) {
-    const hipError_t le = precision == 1 ? mlp_launch_persistent_f32_epoch(a, pb32, s, zero_flags) : mlp_launch_persistent_epoch(a, pb, s, zero_flags);
+    const hipError_t le = precision == 1 ? mlp_launch_persistent_f32_epoch(a, pb32, s, zero_flags, launch_active) : mlp_launch_persistent_epoch(a, pb, s, zero_flags);
     if (le != hipSuccess) {
       g_last_error = std::string("persistent epoch launch: ") + hipGetErrorString(le);
       return 1;
@@ -672,7 +676,11 @@ struct MLPEngine {
     if (!direct_epoch_launch()) return launch_graph(s);
     const int buf = n_execs > 1 ? (int)(launches & 1) : 0;
     const auto t0 = std::chrono::steady_clock::now();
-    if (enqueue_epoch(s, graph_steps, buf)) return 1;
+    for (int p = 0; p < a.P && p < MLP_CTL_MAX; ++p) launch_active_buf[p] = ctl_host[p].x & 1;
+    launch_active = launch_active_buf;
+    const int rc_e = enqueue_epoch(s, graph_steps, buf);
+    launch_active = nullptr;
+    if (rc_e) return 1;
     CHECK_HIP(hipGetLastError());
     const unsigned long long ns = (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     ++launches;
@@ -858,6 +866,21 @@ int myfyp_fedavg_bucket_reduce(float* out, float* wsum_slot, const float* stacke
   }
   w.wsum = (float)sum;
   fl_fedavg_reduce(out, wsum_slot, stacked, P, n, ld, w, (hipStream_t)stream);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// the same, with a second copy of the partial sums (the failover's retained input) from the same pass
+int myfyp_fedavg_bucket_reduce2(float* out, float* wsum_slot, float* out2, float* wsum2, const float* stacked, int P, int64_t n, int64_t ld,
+                                const float* w_host, void* stream) {
+  if (!fedavg_rows_ok(P)) return 2;
+  FedAvgWeights w{};
+  double sum = 0.0;
+  for (int p = 0; p < P; ++p) {
+    w.w[p] = w_host[p];
+    sum += w_host[p];
+  }
+  w.wsum = (float)sum;
+  fl_fedavg_reduce(out, wsum_slot, stacked, P, n, ld, w, (hipStream_t)stream, out2, wsum2);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -86,6 +86,7 @@ _SIGNATURES = {
     "myfyp_fedavg_stacked_local": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "myfyp_fedavg_bucket_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_fedavg_bucket_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "myfyp_fedavg_bucket_reduce2": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_fedavg_delayed_land": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "myfyp_neighbor_mix_stacked": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "mlp_engine_uses_persistent": (c_int, [c_void_p]),

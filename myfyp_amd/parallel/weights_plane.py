@@ -183,10 +183,12 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
     """FedAvg of a stacked ``[capacity, S]`` group on the GPU, host never waits.
 
     * one rank: one ``k_fedavg_local`` launch (weighted mean written into every masked row);
-    * several ranks, ``OVERLAP_COLLECTIVES``: on the side stream, per bucket a reduce launch and an
-      async all-reduce (RCCL orders it after that launch), then per bucket wait + apply launch —
-      bucket k's all-reduce overlaps bucket k+1's reduce and bucket k-1's apply; the compute stream
-      waits on the side stream only at the point the next round touches the parameters;
+    * several ranks, ``OVERLAP_COLLECTIVES``: per bucket a reduce launch (which also writes the
+      failover's retained copy) and an async all-reduce on RCCL's stream, ordered after that launch,
+      then per bucket wait + apply launch — bucket k's all-reduce overlaps bucket k+1's reduce and
+      bucket k-1's apply. These run on the compute stream itself: the next epoch needs the average,
+      and a side stream only put two more cross-stream hops on the round's critical path
+      (``profiles/r6k_forced_trace``);
     * ``DELAYED_AVERAGING`` (opt-in, not on the last round): land the previous round's average as
       ``x += avg - snap`` and take the new snapshot (one launch), then reduce + all-reduce the
       snapshot on the side stream while the next round trains from the local weights.
@@ -252,7 +254,10 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
         keep = getattr(group, "_wp_keep_buf", None)
         if keep is None or keep.numel() != n + 4:
             keep = group._wp_keep_buf = torch.zeros(n + 4, dtype=torch.float32, device=dev)
-    works = _bucketed_reduce(fed, fast, comm_stream(dev), cur, base, S, n, P, wp, buf, apply=(base, S, mp), keep=keep)
+    # on the compute stream: the next epoch needs the average anyway, and the buckets still pipeline
+    # (bucket k's all-reduce runs on RCCL's stream while bucket k + 1 reduces); a side stream only
+    # added two cross-stream hops to the round's critical path (profiles/r6k_forced_trace)
+    works = _bucketed_reduce(fed, fast, cur, cur, base, S, n, P, wp, buf, apply=(base, S, mp), keep=keep)
     if keep is not None:
 
         def retry() -> None:  # survivors: all-reduce the retained local partials, apply again
@@ -274,19 +279,24 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
     the all-reduce works (confirmed later by the collective guard)."""
     from myfyp_amd.settings import Settings
 
-    cs.wait_stream(cur)  # the rows are final on the compute stream
+    same = cs.cuda_stream == cur.cuda_stream  # critical path: everything on the compute stream
+    if not same:
+        cs.wait_stream(cur)  # the rows are final on the compute stream
     bp = buf.data_ptr()
+    kp = keep.data_ptr() if keep is not None else None
     ranges = bucket_ranges(n, Settings.BUCKET_BYTES)
     works = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(cs)
     with torch.cuda.stream(cs):
         for k, (b0, b1) in enumerate(ranges):
-            ops.check(fast.myfyp_fedavg_bucket_reduce(bp + 4 * (4 + b0), bp if k == 0 else None, src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream),
-                      "fedavg_bucket_reduce")
+            if kp is None:
+                ops.check(fast.myfyp_fedavg_bucket_reduce(bp + 4 * (4 + b0), bp if k == 0 else None, src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream),
+                          "fedavg_bucket_reduce")
+            else:  # the retained copy from the same pass (no device copy behind it)
+                ops.check(fast.myfyp_fedavg_bucket_reduce2(bp + 4 * (4 + b0), bp if k == 0 else None, kp + 4 * (4 + b0), kp if k == 0 else None,
+                                                           src + 4 * b0, P, b1 - b0, ld, wp, cs.cuda_stream), "fedavg_bucket_reduce2")
             lo = 0 if k == 0 else 4 + b0
-            if keep is not None:
-                keep[lo : 4 + b1].copy_(buf[lo : 4 + b1])
             works.append(fed.all_reduce_async(buf[lo : 4 + b1]))
         for k, (b0, b1) in enumerate(ranges):
             if works[k] is not None:
@@ -296,11 +306,12 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
                 ops.check(fast.myfyp_fedavg_bucket_apply(dst + 4 * b0, bp + 4 * (4 + b0), bp, P, b1 - b0, dld, mp, cs.cuda_stream), "fedavg_bucket_apply")
     ev1.record(cs)
     fed.comm.device("fedavg_pipeline", 4 * (n + 1), ev0, ev1)  # resolved lazily by the node monitor
-    buf.record_stream(cs)
-    if keep is not None:
-        keep.record_stream(cs)
-    if apply is not None:
-        cur.wait_stream(cs)  # stream-level: the next kernel on the compute stream sees the average
+    if not same:
+        buf.record_stream(cs)
+        if keep is not None:
+            keep.record_stream(cs)
+        if apply is not None:
+            cur.wait_stream(cs)  # stream-level: the next kernel on the compute stream sees the average
     return works
 
 
