@@ -6,6 +6,7 @@ and run identically on every rank (same call order ⇒ matching RCCL collectives
 
 from __future__ import annotations
 
+import os
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -257,7 +258,8 @@ def _stacked_mean_cuda(fed: Federation, group, w: np.ndarray, mask: np.ndarray, 
     # on the compute stream: the next epoch needs the average anyway, and the buckets still pipeline
     # (bucket k's all-reduce runs on RCCL's stream while bucket k + 1 reduces); a side stream only
     # added two cross-stream hops to the round's critical path (profiles/r6k_forced_trace)
-    works = _bucketed_reduce(fed, fast, cur, cur, base, S, n, P, wp, buf, apply=(base, S, mp), keep=keep)
+    side = os.environ.get("MYFYP_FEDAVG_SIDE", "0") == "1"  # A/B: the side-stream pipeline of round 5
+    works = _bucketed_reduce(fed, fast, comm_stream(dev) if side else cur, cur, base, S, n, P, wp, buf, apply=(base, S, mp), keep=keep)
     if keep is not None:
 
         def retry() -> None:  # survivors: all-reduce the retained local partials, apply again
