@@ -87,12 +87,23 @@ class CommStats:
             self.us_last[kind] = us
             self.us_total[kind] = self.us_total.get(kind, 0.0) + us
 
+    # device-timed kinds record their event pair once every TIME_EVERY calls: two timing events per
+    # round sat on the critical-path FedAvg (~2.7 us each, profiles/r5_gap)
+    TIME_EVERY = 16
+
+    def timed(self, kind: str) -> bool:
+        with self._lock:
+            return self.calls.get(kind, 0) % self.TIME_EVERY == 0 or kind not in self.calls
+
     def host(self, kind: str, nbytes: int, seconds: float) -> None:
         with self._lock:
             self._add(kind, nbytes, seconds * 1e6)
 
     def device(self, kind: str, nbytes: int, ev0, ev1) -> None:
         with self._lock:
+            if ev1 is None:  # an untimed call (sampled timing): bytes and count only
+                self._add(kind, nbytes, None)
+                return
             self._pending.append((kind, int(nbytes), ev0, ev1))
             if len(self._pending) > 256:  # never resolved (no snapshot taken): keep bytes, drop timing
                 k, b, _, _ = self._pending.pop(0)

@@ -288,8 +288,10 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
     kp = keep.data_ptr() if keep is not None else None
     ranges = bucket_ranges(n, Settings.BUCKET_BYTES)
     works = []
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(cs)
+    timed = fed.comm.timed("fedavg_pipeline")
+    ev0, ev1 = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else (None, None)
+    if timed:
+        ev0.record(cs)
     with torch.cuda.stream(cs):
         for k, (b0, b1) in enumerate(ranges):
             if kp is None:
@@ -306,8 +308,9 @@ def _bucketed_reduce(fed: Federation, fast, cs, cur, src: int, ld: int, n: int, 
             if apply is not None:
                 dst, dld, mp = apply
                 ops.check(fast.myfyp_fedavg_bucket_apply(dst + 4 * b0, bp + 4 * (4 + b0), bp, P, b1 - b0, dld, mp, cs.cuda_stream), "fedavg_bucket_apply")
-    ev1.record(cs)
-    fed.comm.device("fedavg_pipeline", 4 * (n + 1), ev0, ev1)  # resolved lazily by the node monitor
+    if timed:
+        ev1.record(cs)
+    fed.comm.device("fedavg_pipeline", 4 * (n + 1), ev0, ev1)  # resolved lazily by the node monitor (sampled timing)
     if not same:
         buf.record_stream(cs)
         if keep is not None:
