@@ -508,11 +508,18 @@ struct MLPEngine {
     ga.Xb16 = xb16_buf[i];
     ga.Yb = yb_buf[i];
     ga.flags_zero = nullptr;
-    mlp_launch_gather_epoch(ga, prep_stream, prep_level == 2 ? prep_wgs : 0);
+    // debug (MYFYP_DEBUG_NO_GATHER=1, timing experiments only): once both batch buffers hold a real
+    // epoch, later epochs re-read them and no gather runs beside the epoch (prices its interference)
+    static const bool no_gather = [] {
+      const char* e = getenv("MYFYP_DEBUG_NO_GATHER");
+      return e != nullptr && atoi(e) != 0;
+    }();
+    if (!(no_gather && ++prep_gathers > 2)) mlp_launch_gather_epoch(ga, prep_stream, prep_level == 2 ? prep_wgs : 0);
     CHECK_HIP(hipGetLastError());
     CHECK_HIP(hipEventRecord(ev_gath[i], prep_stream));
     return 0;
   }
+  long long prep_gathers = 0;
 
   // publish into ring slot r; completion: the slot's sequence word (or its event, MYFYP_RING_EVENTS=1)
   int publish(hipStream_t s, ResultSlot& r, const float* loss, const int* correct, const int* err, const int* conf) {
@@ -1571,7 +1578,13 @@ int mlp_engine_eval_async(void* h, const int* active_host, int slot, void* strea
     CHECK_HIP(hipEventRecord(e->ev_snap, s));
     hipStream_t xs = e->eval_stream;
     CHECK_HIP(hipStreamWaitEvent(xs, e->ev_snap, 0));
-    e->launch_eval(ea, xs);
+    // debug (MYFYP_DEBUG_NO_EVAL=1, timing experiments only): no evaluation kernel beside the epoch
+    // (results read as zero loss / accuracy; prices the evaluation's interference)
+    static const bool no_eval = [] {
+      const char* v = getenv("MYFYP_DEBUG_NO_EVAL");
+      return v != nullptr && atoi(v) != 0;
+    }();
+    if (!no_eval) e->launch_eval(ea, xs);
     CHECK_HIP(hipGetLastError());
     if (e->publish(xs, r, es.loss, es.correct, nullptr, es.conf)) return 1;
     CHECK_HIP(hipEventRecord(es.done, xs));
