@@ -2040,7 +2040,11 @@ int f32_ks_v1(const MLPArgs& a) {
   // drift from torch even when the term is zero (mu = 0: 2 % on W1, scripts/probes/xr_extra_probe2.py,
   // profiles/r6_xr), while the same launch without it is exact; K split 2 with the term is exact.
   // Until that is understood, extra-term epochs use K split <= 2.
-  if ((a.anchor != nullptr || a.cg != nullptr) && want > 2) want = 2;
+  static const bool xr_extra = [] {  // debug: allow the extra-term instantiations at K split 4 / 8 (probes)
+    const char* e = getenv("MYFYP_F32_XR_EXTRA");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  if ((a.anchor != nullptr || a.cg != nullptr) && want > 2 && !xr_extra) want = 2;
   if (want > 1 && grid_of(want, rh, rh ? roles3_of(want, a.Bpad) : roles_of(want)) > resident_capacity_ks(a, cus, want, rh)) return 1;
   return want;
 }
