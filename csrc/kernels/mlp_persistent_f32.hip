@@ -122,6 +122,18 @@ using namespace f32k;
 #ifndef P32_SM8
 #define P32_SM8 1
 #endif
+// heads' softmax chain shortened (1): v_exp / v_log (__expf / __logf, within 2 ulp) instead of the
+// range-reduced library expf / logf, the class probability as e / Σe (no second exp), and the
+// argmax's DPP reduction (accuracy metric only) moved behind the dH2 publish; 0: library exp / log,
+// p = exp(logp), argmax inline
+#ifndef P32_FASTSM
+#define P32_FASTSM 1
+#endif
+// heads' H2 = H1 · W2ᵀ on the bf16 MFMA with both fp32 operands split exactly into three bf16
+// terms, six products kept (1), or on v_mfma_f32_16x16x4_f32 (0)
+#ifndef P32_H2BF
+#define P32_H2BF 0
+#endif
 // direct-X epochs (layout 1, opt-in build -DP32_XDIRECT=1): batch rows read from the static bf16 copy
 // of the peer's images through the epoch index (MLPArgs::Xp16 / xidx, written by mlp_index_epoch)
 // instead of a per-epoch gathered copy. Measured slower (profiles/r4p_direct_x): the round boundary
@@ -1016,6 +1028,11 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     constexpr int SMW = MT * (4 / SMR);  // softmax waves
     const int sm_mt = wave / (4 / SMR), sm_i0 = SMR * (wave % (4 / SMR));
     int yv[SMR];
+#if P32_FASTSM
+    int cand_v[SMR];
+#pragma unroll
+    for (int i = 0; i < SMR; ++i) cand_v[i] = 16;
+#endif
 #pragma unroll
     for (int i = 0; i < SMR; ++i) yv[i] = -1;
     if (wave < SMW) {
@@ -1098,6 +1115,34 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = zero4();
+#if P32_H2BF
+      // both fp32 operands split exactly into bf16 hi / mid / lo; six v_mfma_f32_16x16x32_bf16 terms
+      // replace eight f32 MFMAs per 32-wide K slice (the three dropped cross terms are below 2^-32
+      // of the product). K slot (h, j) of the bf16 fragment is o1 = 32w + 16(j / 4) + 4h + j % 4:
+      // exactly the eight W2 values this lane already holds (w2[j / 4][j % 4])
+      {
+        float wq[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wq[j] = w2[j >> 2][j & 3];
+        bf16x8 bh, bm, bl;
+        split3(wq, bh, bm, bl);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float* hp = sH1 + (16 * mt + c) * LDH1 + 32 * wave + 4 * h;
+          const float4 a0 = *reinterpret_cast<const float4*>(hp);
+          const float4 a1 = *reinterpret_cast<const float4*>(hp + 16);
+          const float aq[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          bf16x8 ah, am, al;
+          split3(aq, ah, am, al);
+          f32x4 t = mfma_bf16(al, bh, acc[mt]);  // smallest terms first
+          t = mfma_bf16(ah, bl, t);
+          t = mfma_bf16(am, bm, t);
+          t = mfma_bf16(am, bh, t);
+          t = mfma_bf16(ah, bm, t);
+          acc[mt] = mfma_bf16(ah, bh, t);
+        }
+      }
+#else
 #pragma unroll
       for (int gg = 0; gg < 2; ++gg) {
         const int g = 2 * wave + gg;
@@ -1110,6 +1155,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
           acc[mt] = mfma_f32(av.w, w2[gg][3], acc[mt]);
         }
       }
+#endif
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) sRed[(wave * MT + mt) * 64 + lane] = acc[mt];
     }
@@ -1216,6 +1262,14 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         const int y = yv[i];
         const float logit = cin ? lsum[i] + b3 : -INFINITY;
         const float mx = row_max16(logit);
+#if P32_FASTSM
+        const float ex = cin ? __expf(logit - mx) : 0.f;
+        const float se = row_sum16(ex);
+        const float logp = logit - (mx + __logf(se));
+        cand_v[i] = (cin && logit == mx) ? c : 16;  // argmax reduced behind the dH2 publish
+        if (rvalid && c == y) loss_acc -= logp;
+        const float pc = ex * __builtin_amdgcn_rcpf(se);
+#else
         const float se = row_sum16(cin ? expf(logit - mx) : 0.f);
         const float logp = logit - (mx + logf(se));
         const int cand = row_min16((cin && logit == mx) ? c : 16);
@@ -1226,6 +1280,7 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
         // reference's fp32 autograd produces through its log_softmax + cross_entropy pair
         // (lightning_model.py:178, :189): scripts/probes/f32_softmax_cancel.py.
         const float pc = cin ? expf(logp) : 0.f;
+#endif
         const float others = row_sum16(c != y ? pc : 0.f);
         sDlog[b * LD16 + c] = (rvalid && cin) ? (c == y ? -others : pc) / (float)rows : 0.f;
       }
@@ -1255,6 +1310,16 @@ __device__ void head32(const MLPArgs& a, const MLPPersistF32Bufs& pb, int p, int
     else
       persist::publish_p(pb.flags, FPP, p, F_DH2 + hd, pb.fbase + (unsigned)(t + 1), pb.plain_x);
     if (hd == 0) P32_STAMP(1, t, 7);
+#if P32_FASTSM
+    if (wave < SMW) {  // the deferred argmax (accuracy metric)
+#pragma unroll
+      for (int i = 0; i < SMR; ++i) {
+        const int b = 16 * sm_mt + 4 * h + sm_i0 + i;
+        const int cand = row_min16(cand_v[i]);
+        if (b < rows && c == 0) correct_acc += (cand == yv[i]) ? 1.f : 0.f;
+      }
+    }
+#endif
 
     // ---- off the critical path: W2 rows (every wave: its two o1 groups), W3 slice (wave 0),
     //      b2 (wave 1), b3 (wave 2, the same arithmetic in every head)
