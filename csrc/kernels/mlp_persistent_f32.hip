@@ -125,12 +125,15 @@ using namespace f32k;
 // heads' softmax chain shortened (1): v_exp / v_log (__expf / __logf, within 2 ulp) instead of the
 // range-reduced library expf / logf, the class probability as e / Σe (no second exp), and the
 // argmax's DPP reduction (accuracy metric only) moved behind the dH2 publish; 0: library exp / log,
-// p = exp(logp), argmax inline
+// p = exp(logp), argmax inline. Measured (profiles/r6t_fastsm): softmax 1.16 -> 0.92 us, 626.4 /
+// 627.4 / 628.0 vs 615.8 / 614.0 / 615.6 rounds/s
 #ifndef P32_FASTSM
 #define P32_FASTSM 1
 #endif
 // heads' H2 = H1 · W2ᵀ on the bf16 MFMA with both fp32 operands split exactly into three bf16
-// terms, six products kept (1), or on v_mfma_f32_16x16x4_f32 (0)
+// terms, six products kept (1), or on v_mfma_f32_16x16x4_f32 (0). Measured and not kept
+// (profiles/r6u_h2bf): the split of H1 per K slice costs more VALU than the MFMA time it saves,
+// H2 + partial logits 1.64 -> 1.96 us, 621.1 / 620.3 / 622.5 vs 626.8 / 626.3 / 629.5 rounds/s
 #ifndef P32_H2BF
 #define P32_H2BF 0
 #endif

@@ -18,6 +18,27 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr int FLAG_LINE = 32;                            // u32 per flag: one 128-byte line each
 constexpr unsigned long long SPIN_TICKS = 100000000ull;  // wall_clock64 runs at 100 MHz: 1 s
 
+// Poll loops: the hand-off's own load is the only memory round trip of an iteration. The gang's
+// error word (another L2 round trip) and the clock (s_memrealtime, a scalar-memory round trip)
+// are read on every PERSIST_POLL_EVERY-th iteration only: before, each iteration serialised three
+// round trips, so a flag that flipped was seen on average 1.5 of them late, on every hand-off of
+// every step. Timeouts and give-ups are still seen within PERSIST_POLL_EVERY iterations.
+// No s_sleep between polls (PERSIST_POLL_SLEEP 0): a polling wave has one load in flight at a time
+// either way. Measured on the 8-peer headline (profiles/r6v_poll, 3 runs each): every poll 627.0 /
+// 622.8 / 625.6 rounds/s, every 32nd + s_sleep 1 628.5 / 631.1 / 630.7, every 32nd without the
+// sleep 637.8 / 637.5 / 635.7
+#ifndef PERSIST_POLL_EVERY
+#define PERSIST_POLL_EVERY 32
+#endif
+#ifndef PERSIST_POLL_SLEEP
+#define PERSIST_POLL_SLEEP 0
+#endif
+static_assert((PERSIST_POLL_EVERY & (PERSIST_POLL_EVERY - 1)) == 0, "PERSIST_POLL_EVERY: a power of two");
+__device__ __forceinline__ bool poll_check(unsigned it) { return (it & (PERSIST_POLL_EVERY - 1)) == 0; }
+__device__ __forceinline__ void poll_sleep() {
+  if (PERSIST_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(PERSIST_POLL_SLEEP);
+}
+
 __device__ __forceinline__ unsigned* flag_at(unsigned* flags, int flags_per_peer, int p, int idx) {
   return flags + ((size_t)p * flags_per_peer + idx) * FLAG_LINE;
 }
@@ -155,19 +176,21 @@ __device__ __forceinline__ bool wg_wait(unsigned* flags, int fpp, int p, int idx
     const unsigned* f = flag_at(flags, fpp, p, idx0 + (lane < n ? lane : 0));
     const unsigned long long t0 = wall_clock64();
     int ok = 1;
-    for (;;) {
+    for (unsigned it = 1;; ++it) {
       const unsigned v = lane < n ? __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
       if (__all(v >= target)) break;
-      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
+      if (poll_check(it)) {
+        if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          ok = 0;
+          break;
+        }
+        if (wall_clock64() - t0 > ticks) {
+          if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
       }
-      if (wall_clock64() - t0 > ticks) {
-        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+      poll_sleep();
     }
     if (lane == 0) *sOk = ok;
   }
@@ -229,20 +252,22 @@ __device__ __forceinline__ bool ll_wait(ll_u32x4 (&v)[N], Load load, unsigned ta
 #pragma unroll
   for (int k = 0; k < N; ++k) v[k] = load(k);
   unsigned long long t0 = 0;
-  for (;;) {
+  for (unsigned it = 1;; ++it) {
     bool ready = true;
 #pragma unroll
     for (int k = 0; k < N; ++k) ready = ready && ll_ok2(v[k], tag);
     if (__all(ready)) return true;
-    if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
-    const unsigned long long now = wall_clock64();
-    if (t0 == 0) {
-      t0 = now;
-    } else if (now - t0 > ticks) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
+    if (it == 1 || poll_check(it)) {
+      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+      const unsigned long long now = wall_clock64();
+      if (t0 == 0) {
+        t0 = now;
+      } else if (now - t0 > ticks) {
+        if ((threadIdx.x & 63) == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
     }
-    __builtin_amdgcn_s_sleep(1);
+    poll_sleep();
 #pragma unroll
     for (int k = 0; k < N; ++k)
       if (!ll_ok2(v[k], tag)) v[k] = load(k);
@@ -260,19 +285,21 @@ __device__ __forceinline__ bool ll_wg_wait(Probe probe, int n, unsigned tag, int
     const int k = lane < n ? lane : 0;
     const unsigned long long t0 = wall_clock64();
     int ok = 1;
-    for (;;) {
+    for (unsigned it = 1;; ++it) {
       const bool ready = lane >= n || ll_ok2(probe(k), tag);
       if (__all(ready)) break;
-      if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
+      if (poll_check(it)) {
+        if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          ok = 0;
+          break;
+        }
+        if (wall_clock64() - t0 > ticks) {
+          if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
       }
-      if (wall_clock64() - t0 > ticks) {
-        if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+      poll_sleep();
     }
     if (lane == 0) *sOk = ok;
   }
