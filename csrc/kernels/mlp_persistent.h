@@ -56,6 +56,9 @@ int mlp_persistent_f32_variant(const MLPArgs& a);
 int mlp_persistent_f32_x_direct(const MLPArgs& a);
 int mlp_persistent_f32_x_direct_build();  // the build's P32_XDIRECT  // gang layout: 1 owners + heads, 2 owners only          // K split of the owners (1 or 2)             // workgroups (CUs) per peer
 int mlp_persistent_f32_flags_per_peer();   // u32 words per peer in the flag block
+// flag block layout: u32 per flag line, flag lines per peer, and how many of each peer's last lines
+// use every word (the gang placement slots); every other line's flag is its word 0
+void mlp_persistent_f32_flag_layout(int* line, int* lines_per_peer, int* full_lines);
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a);
 // active (nullable, a.P host flags): launches (and retry launches) are enqueued only for the
 // groups of ppl peers with an active peer; null: every group (graph capture: any later active set)

@@ -2160,6 +2160,11 @@ int mlp_persistent_f32_resident_capacity(const MLPArgs& a, int num_cus) {
   return v == 2 ? mlp_f32v2_resident_capacity(a, num_cus) : resident_capacity_ks(a, num_cus, f32_ks(a), v == 3);
 }
 int mlp_persistent_f32_flags_per_peer() { return FPP * persist::FLAG_LINE; }
+void mlp_persistent_f32_flag_layout(int* line, int* lines_per_peer, int* full_lines) {
+  *line = persist::FLAG_LINE;
+  *lines_per_peer = FPP;
+  *full_lines = FPP - F_XCC;  // the XCC report slots (persist::gang_same_xcd / group_same_xcd)
+}
 
 hipError_t mlp_persistent_f32_prepare(const MLPArgs& a) {
   hipError_t e;

@@ -55,6 +55,9 @@ struct CtlUpload {
   int* zero_conf;
   unsigned* zero_flags;  // the persistent epoch's hand-off flags (prep-stream gather mode)
   int n_flags;
+  // fp32 flag block: only word 0 of each flag line is a flag, except the last `flag_full` lines of
+  // every peer (the gang placement slots, every word used); 0 = zero all n_flags words
+  int flag_line, flag_lpp, flag_full;
   // where the epoch graph's last node publishes the fit's results (null loss: nowhere — an earlier
   // epoch of a multi-epoch fit, or stats published by a separate launch)
   struct PubDst {
@@ -79,8 +82,22 @@ __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long 
     for (int q = p; q < u.P * 256; q += blockDim.x) u.zero_conf[q] = 0;
   if (u.zero_err)
     for (int q = p; q < MLP_ERR_WORDS; q += blockDim.x) u.zero_err[q] = 0;
-  if (u.zero_flags)
-    for (int q = p; q < u.n_flags; q += blockDim.x) u.zero_flags[q] = 0u;
+  if (u.zero_flags) {
+    if (u.flag_line > 0) {
+      // one store per flag line (was every word of every line: 8 peers x 304 lines x 32 words,
+      // ~12 us of one workgroup between two epochs, profiles/r6w_bnd), whole lines for the slots
+      const int lines = u.n_flags / u.flag_line;
+      for (int q = p; q < lines; q += blockDim.x) u.zero_flags[(int64_t)q * u.flag_line] = 0u;
+      const int per_peer = u.flag_full * u.flag_line / 4;  // 16-byte chunks of one peer's slot lines
+      for (int q = p; q < (lines / u.flag_lpp) * per_peer; q += blockDim.x) {
+        const int pp = q / per_peer, k = q - pp * per_peer;
+        uint4* base = reinterpret_cast<uint4*>(u.zero_flags + ((int64_t)pp * u.flag_lpp + u.flag_lpp - u.flag_full) * u.flag_line);
+        base[k] = uint4{0u, 0u, 0u, 0u};
+      }
+    } else {
+      for (int q = p; q < u.n_flags; q += blockDim.x) u.zero_flags[q] = 0u;
+    }
+  }
   if (p == 0) *seed = u.seed;
 }
 
@@ -460,7 +477,12 @@ struct MLPEngine {
   int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false, bool zero_flags = false, const PubDst* pub = nullptr) {
     CtlUpload u{};
     if (pub) u.pub = *pub;  // else null: the graph's publish node does nothing
-    if (zero_flags) flag_words(&u.zero_flags, &u.n_flags);
+    if (zero_flags) {
+      flag_words(&u.zero_flags, &u.n_flags);
+#ifndef ENGINE_FLAGS_DENSE  // (A/B build: -DENGINE_FLAGS_DENSE zeroes every word, as before)
+      if (precision == 1) mlp_persistent_f32_flag_layout(&u.flag_line, &u.flag_lpp, &u.flag_full);
+#endif
+    }
     u.P = a.P;
     u.with_active = active_host != nullptr;
     u.seed = seed_host;
