@@ -169,8 +169,34 @@ __device__ __forceinline__ void publish_p(unsigned* flags, int fpp, int p, int i
 // Consumer side: wave 0 polls flags idx0..idx0+n-1 (one lane each, relaxed sc1 loads + s_sleep)
 // until all reach `target`, then the workgroup meets; every later load of the handed-off bytes is
 // an sc1 load. Bounded: gives up after `ticks` or when another workgroup gave up.
+//
+// PERSIST_WAVE_POLL (A/B build): every wave polls the flags itself and goes on to its payload loads
+// when it sees them, without the workgroup meet (flags are monotone within a launch: a wave that
+// saw them set cannot disagree with another; a wave that times out or sees the error word returns
+// false and the caller's wave leaves the kernel, which a later barrier of the others tolerates).
 __device__ __forceinline__ bool wg_wait(unsigned* flags, int fpp, int p, int idx0, int n, unsigned target, int* err, int* sOk,
                                         unsigned long long ticks = SPIN_TICKS) {
+#ifdef PERSIST_WAVE_POLL
+  {
+    const int lane = threadIdx.x & 63;
+    const unsigned* f = flag_at(flags, fpp, p, idx0 + (lane < n ? lane : 0));
+    const unsigned long long t0 = wall_clock64();
+    for (unsigned it = 1;; ++it) {
+      const unsigned v = lane < n ? __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__all(v >= target)) break;
+      if (poll_check(it)) {
+        if (__hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+        if (wall_clock64() - t0 > ticks) {
+          if (lane == 0) __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return false;
+        }
+      }
+      poll_sleep();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return true;
+  }
+#endif
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const unsigned* f = flag_at(flags, fpp, p, idx0 + (lane < n ? lane : 0));
