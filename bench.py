@@ -153,10 +153,19 @@ def main() -> None:
         Node(TorchModel(MLP(seed=100 + g)), parts[g], address=f"peer-{g}", protocol=CollectiveCommunicationProtocol, learner_kwargs={"batch_size": args.batch_size})
         for g in gids
     ]
+    prof_start = os.environ.get("MYFYP_PROFILE_START")  # diagnostics: cProfile of the node starts
+    if prof_start:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t_ns = time.perf_counter()
     for n in nodes:
         n.start()  # Settings.ENGINE_PREWARM: the fused engine captures its epoch graph here
     node_start_s = time.perf_counter() - t_ns
+    if prof_start:
+        prof.disable()
+        prof.dump_stats(prof_start)
     fed.finalize()
     if args.eager:
         for n in nodes:
