@@ -174,6 +174,8 @@ __device__ __forceinline__ void publish_p(unsigned* flags, int fpp, int p, int i
 // when it sees them, without the workgroup meet (flags are monotone within a launch: a wave that
 // saw them set cannot disagree with another; a wave that times out or sees the error word returns
 // false and the caller's wave leaves the kernel, which a later barrier of the others tolerates).
+// Measured within noise of the meet (profiles/r6z_wavepoll: 641.7 / 616.9 / 637.3 vs 641.1 / 610.3 /
+// 639.8 rounds/s): off.
 __device__ __forceinline__ bool wg_wait(unsigned* flags, int fpp, int p, int idx0, int n, unsigned target, int* err, int* sOk,
                                         unsigned long long ticks = SPIN_TICKS) {
 #ifdef PERSIST_WAVE_POLL
