@@ -87,7 +87,9 @@ __global__ void k_upload_ctl(CtlUpload u, int4* ctl, int* active, unsigned long 
       // one store per flag line (was every word of every line: 8 peers x 304 lines x 32 words,
       // ~12 us of one workgroup between two epochs, profiles/r6w_bnd), whole lines for the slots
       const int lines = u.n_flags / u.flag_line;
+#ifndef ENGINE_FLAGS_BROKEN_TEST  // (negative control of test_f32_flag_block_sparse_zeroing only)
       for (int q = p; q < lines; q += blockDim.x) u.zero_flags[(int64_t)q * u.flag_line] = 0u;
+#endif
       const int per_peer = u.flag_full * u.flag_line / 4;  // 16-byte chunks of one peer's slot lines
       for (int q = p; q < (lines / u.flag_lpp) * per_peer; q += blockDim.x) {
         const int pp = q / per_peer, k = q - pp * per_peer;
@@ -474,6 +476,8 @@ struct MLPEngine {
       *n = (int)(pb.flag_bytes / sizeof(unsigned));
     }
   }
+  bool debug_poison_flags = false;  // test hook: every word of the flag block set to ~0 before its zeroing
+  int poisoned = 0;                 // uploads that poisoned the block (the hook reports it)
   int upload(hipStream_t s, const int* active_host, bool zero_fit = false, bool fresh = false, bool zero_flags = false, const PubDst* pub = nullptr) {
     CtlUpload u{};
     if (pub) u.pub = *pub;  // else null: the graph's publish node does nothing
@@ -482,6 +486,12 @@ struct MLPEngine {
 #ifndef ENGINE_FLAGS_DENSE  // (A/B build: -DENGINE_FLAGS_DENSE zeroes every word, as before)
       if (precision == 1) mlp_persistent_f32_flag_layout(&u.flag_line, &u.flag_lpp, &u.flag_full);
 #endif
+      // (the words the sparse zeroing skips must never be read: a stale ~0 there would release a
+      // consumer before its hand-off is written; tests/test_mlp_f32_gpu.py poisons them)
+      if (debug_poison_flags) {
+        CHECK_HIP(hipMemsetAsync(u.zero_flags, 0xFF, (size_t)u.n_flags * sizeof(unsigned), s));
+        ++poisoned;
+      }
     }
     u.P = a.P;
     u.with_active = active_host != nullptr;
@@ -1715,6 +1725,15 @@ int mlp_engine_debug_giveup(void* h, int peer, int at_end) {
   e->a.debug_giveup = peer < 0 ? 0 : peer + 1 + (at_end ? 256 : 0);
   e->invalidate();
   return 0;
+}
+
+// Test hook: fill the whole hand-off flag block with ~0 before each epoch's (sparse) flag zeroing
+// (on = 1 / 0; -1 leaves the setting). Returns how many uploads have poisoned it so far.
+int mlp_engine_debug_poison_flags(void* h, int on) {
+  auto* e = (MLPEngine*)h;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (on >= 0) e->debug_poison_flags = on != 0;
+  return e->poisoned;
 }
 
 int mlp_engine_ring_size() { return MLP_RING; }

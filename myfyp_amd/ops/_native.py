@@ -101,6 +101,7 @@ _SIGNATURES = {
     "mlp_engine_set_f32_variant": (c_int, [c_void_p, c_int]),
     "mlp_engine_f32_variant": (c_int, [c_void_p]),
     "mlp_engine_debug_giveup": (c_int, [c_void_p, c_int, c_int]),
+    "mlp_engine_debug_poison_flags": (c_int, [c_void_p, c_int]),
     "mlp_engine_prepare": (c_int, [c_void_p, c_void_p]),
     "myfyp_warm_all": (c_int, [c_int]),
     "mlp_set_plain_pub": (c_int, [c_int]),  # single-XCD hand-off mode override (-1: MYFYP_F32_PLAIN_PUB)

@@ -7,6 +7,7 @@ identical batches: relative update error < 1e-3 over whole epochs (the bf16 engi
 """
 
 import copy
+import random
 import threading
 
 import numpy as np
@@ -466,4 +467,39 @@ def test_f32_single_xcd_handoffs_bit_identical(dev, peers, ks):
     assert out[0][1] == [0] * peers
     assert out[1][1] == [1] * peers, f"gangs not all on one XCD: {out[1][1]}"
     for a, b in zip(out[1][0], out[0][0]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("peers,ks", [(8, 1), (1, 8)])
+def test_f32_flag_block_sparse_zeroing(dev, peers, ks):
+    """Between epochs only word 0 of each hand-off flag line, plus the gang-placement slot lines, is
+    zeroed (engine.hip k_upload_ctl, profiles/r6x_flags). With every word of the block set to ~0
+    before each epoch's zeroing, a flag read anywhere else would release its consumer before the
+    hand-off is written: the same fits must still give bit-identical parameters."""
+    from myfyp_amd.ops import _native
+    from myfyp_amd.parallel.mlp_engine import MLPGroup
+
+    lib = _native.load(required=True)
+    spec = {"name": "adam", "lr": 1e-3}
+    out = {}
+    for poison in (0, 1):
+        MLPGroup.reset_all()
+        learners, refs, g, n = _setup(dev, peers, 64, 600 * peers, 13, spec)
+        g.force_f32_ks = ks
+        g.force_f32_variant = 1
+        assert g.f32_ks() == ks
+        # the device-side epoch shuffle (pinned permutations would leave the prep-stream gather
+        # mode, whose control upload is where the sparse zeroing runs), keyed from the same seed
+        random.seed(1234)
+        with g.lock:
+            g._ensure_engine()
+            lib.mlp_engine_debug_poison_flags(g._engine, poison)
+        for l in learners:
+            l.set_epochs(2)
+        _fit_all(learners)
+        with g.lock:
+            done = lib.mlp_engine_debug_poison_flags(g._engine, 0)
+        assert (done > 0) == bool(poison), done  # the sparse zeroing ran after the poison
+        out[poison] = [l.flat_params().detach().clone() for l in learners]
+    for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
